@@ -1,0 +1,105 @@
+// Communicator interface: one implementation over RCCL (GPU tensors, xGMI) and
+// one over TCP (CPU tensors, the no-GPU plumbing and test path).
+//
+// Parity: the reference reaches collectives through ProcessGroupGloo
+// (main.py:50, main.py:65, main.py:90-91). Here the
+// process-group object in Python owns one Communicator per device type.
+#pragma once
+
+#include <ATen/ATen.h>
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../store/tcp_store.h"
+
+namespace dcp {
+
+enum class ReduceOp : int { SUM = 0, AVG = 1, PRODUCT = 2, MIN = 3, MAX = 4 };
+
+// Handle of an in-flight collective.
+class Work {
+ public:
+  virtual ~Work() = default;
+  // True once the collective finished (device-side for RCCL).
+  virtual bool is_completed() = 0;
+  // Make the caller's current stream wait for completion (GPU: no host block;
+  // host backend: blocks the calling thread). Raises on communicator failure.
+  virtual void wait() = 0;
+  // Block the calling host thread until completion.
+  virtual void synchronize() = 0;
+  // Elapsed device time in ms between issue and completion, or -1 if unknown.
+  virtual double elapsed_ms() { return -1.0; }
+  std::vector<at::Tensor> outputs;
+};
+
+using WorkPtr = std::shared_ptr<Work>;
+
+class Communicator {
+ public:
+  Communicator(std::shared_ptr<TCPStore> store, std::string prefix, int rank, int size)
+      : store_(std::move(store)), prefix_(std::move(prefix)), rank_(rank), size_(size) {}
+  virtual ~Communicator() = default;
+
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  virtual std::string backend() const = 0;
+
+  virtual WorkPtr all_reduce(at::Tensor& t, ReduceOp op) = 0;
+  virtual WorkPtr broadcast(at::Tensor& t, int root) = 0;
+  // out: contiguous [size * in.numel()] (any shape with that numel).
+  virtual WorkPtr all_gather(at::Tensor& out, const at::Tensor& in) = 0;
+  // in: contiguous [size * out.numel()].
+  virtual WorkPtr reduce_scatter(at::Tensor& out, const at::Tensor& in, ReduceOp op) = 0;
+  // Equal splits: in/out contiguous with numel divisible by size.
+  virtual WorkPtr all_to_all(at::Tensor& out, const at::Tensor& in) = 0;
+  virtual WorkPtr send(const at::Tensor& t, int dst) = 0;
+  virtual WorkPtr recv(at::Tensor& t, int src) = 0;
+  virtual WorkPtr barrier() = 0;
+  // Tear down without waiting for peers (failure path).
+  virtual void abort() {}
+  // Non-empty once the communicator hit an unrecoverable error.
+  virtual std::string error() { return {}; }
+
+  // Debug collective fingerprinting: when enabled every
+  // collective first checks through the store that all ranks issue the same
+  // (op, dtype, numel, root) at the same sequence number, turning a would-be
+  // RCCL hang into an error that names the diverging rank.
+  void set_debug_fingerprint(bool on) { fingerprint_ = on; }
+  bool debug_fingerprint() const { return fingerprint_; }
+
+  // Counters for observability.
+  int64_t ops_issued() const { return ops_.load(); }
+  int64_t bytes_issued() const { return bytes_.load(); }
+
+ protected:
+  void account(const char* op, const at::Tensor& t, int64_t extra = 0);
+  void check_fingerprint(const char* op, const at::Tensor& t, int64_t extra);
+
+  std::shared_ptr<TCPStore> store_;
+  std::string prefix_;
+  int rank_;
+  int size_;
+  bool fingerprint_ = false;
+  int64_t seq_ = 0;
+  std::atomic<int64_t> ops_{0};
+  std::atomic<int64_t> bytes_{0};
+};
+
+// Host (CPU) communicator: full TCP mesh, ring algorithms, one worker thread so
+// collectives run asynchronously to the caller (the Reducer overlaps them with
+// backward exactly as on GPU).
+std::shared_ptr<Communicator> make_host_communicator(std::shared_ptr<TCPStore> store, const std::string& prefix,
+                                                     int rank, int size, int64_t timeout_ms);
+
+// RCCL communicator on `device`, comm stream from the torch pool.
+std::shared_ptr<Communicator> make_rccl_communicator(std::shared_ptr<TCPStore> store, const std::string& prefix,
+                                                     int rank, int size, int device, int64_t timeout_ms);
+
+bool rccl_available();
+std::string rccl_version();
+
+}  // namespace dcp

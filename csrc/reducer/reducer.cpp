@@ -1,0 +1,416 @@
+#include "reducer.h"
+
+#include <torch/csrc/autograd/engine.h>
+#include <torch/csrc/autograd/utils/lambda_post_hook.h>
+#include <torch/csrc/autograd/variable.h>
+
+#include <algorithm>
+#include <map>
+#include <unordered_set>
+
+#include "../common.h"
+#include "../ops.h"
+
+namespace dcp {
+
+// ------------------------------------------------------------ planner ----
+std::vector<std::vector<int64_t>> compute_bucket_assignment(const std::vector<int64_t>& sizes_bytes,
+                                                            const std::vector<int64_t>& keys,
+                                                            const std::vector<int64_t>& limits,
+                                                            const std::vector<int64_t>& order) {
+  DCP_CHECK(sizes_bytes.size() == keys.size(), "planner: sizes/keys length mismatch");
+  DCP_CHECK(!limits.empty(), "planner: empty limit list");
+  struct Acc {
+    std::vector<int64_t> idx;
+    int64_t size = 0;
+  };
+  std::map<int64_t, Acc> open;
+  std::map<int64_t, size_t> limit_it;
+  std::vector<std::vector<int64_t>> result;
+  const size_t n = order.empty() ? sizes_bytes.size() : order.size();
+  for (size_t k = 0; k < n; ++k) {
+    const int64_t i = order.empty() ? static_cast<int64_t>(k) : order[k];
+    DCP_CHECK(i >= 0 && i < static_cast<int64_t>(sizes_bytes.size()), "planner: bad index ", i);
+    const int64_t key = keys[i];
+    Acc& b = open[key];
+    b.idx.push_back(i);
+    b.size += sizes_bytes[i];
+    size_t& li = limit_it[key];  // value-initialised to 0 on first use
+    if (b.size >= limits[li]) {
+      result.push_back(std::move(b.idx));
+      b = Acc();
+      if (li + 1 < limits.size()) ++li;
+    }
+  }
+  for (auto& kv : open)
+    if (!kv.second.idx.empty()) result.push_back(std::move(kv.second.idx));
+  if (order.empty()) {
+    std::sort(result.begin(), result.end(), [](const std::vector<int64_t>& a, const std::vector<int64_t>& b) {
+      return *std::min_element(a.begin(), a.end()) < *std::min_element(b.begin(), b.end());
+    });
+  }
+  return result;
+}
+
+namespace {
+
+int64_t bucket_key(const at::Tensor& t) {
+  return (static_cast<int64_t>(t.scalar_type()) << 32) | (static_cast<int64_t>(t.device().type()) << 16) |
+         static_cast<int64_t>(t.device().index() + 1);
+}
+
+bool same_layout(const at::Tensor& a, const at::Tensor& b) {
+  return a.sizes() == b.sizes() && (a.strides() == b.strides() || (a.is_contiguous() && b.is_contiguous()));
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ reducer ----
+Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t>> buckets,
+                 std::shared_ptr<Communicator> comm, ReducerOptions opts)
+    : params_(std::move(params)), comm_(std::move(comm)), opts_(opts) {
+  for (auto& p : params_) {
+    DCP_CHECK(p.requires_grad(), "Reducer: every parameter must require grad");
+    DCP_CHECK(p.is_non_overlapping_and_dense(), "Reducer: parameters must be dense");
+  }
+  ready_.assign(params_.size(), 0);
+  unused_.assign(params_.size(), 0);
+  build_buckets(buckets);
+}
+
+Reducer::~Reducer() {
+  for (size_t i = 0; i < grad_accs_.size() && i < hook_handles_.size(); ++i)
+    grad_accs_[i]->del_post_hook(hook_handles_[i]);
+}
+
+void Reducer::build_buckets(const std::vector<std::vector<int64_t>>& assignment) {
+  std::vector<char> seen(params_.size(), 0);
+  std::vector<Bucket> out;
+  out.reserve(assignment.size());
+  where_.assign(params_.size(), {-1, -1});
+  for (size_t bi = 0; bi < assignment.size(); ++bi) {
+    const auto& idx = assignment[bi];
+    DCP_CHECK(!idx.empty(), "Reducer: empty bucket");
+    Bucket b;
+    b.params = idx;
+    const at::Tensor& p0 = params_[idx[0]];
+    int64_t total = 0;
+    for (int64_t i : idx) {
+      DCP_CHECK(i >= 0 && i < static_cast<int64_t>(params_.size()) && !seen[i], "Reducer: bad bucket index ", i);
+      seen[i] = 1;
+      DCP_CHECK(params_[i].scalar_type() == p0.scalar_type() && params_[i].device() == p0.device(),
+                "Reducer: a bucket must be single dtype/device");
+      b.offsets.push_back(total);
+      total += params_[i].numel();
+    }
+    b.flat = at::zeros({total}, p0.options().requires_grad(false));
+    if (opts_.comm_dtype != at::ScalarType::Undefined && opts_.comm_dtype != p0.scalar_type())
+      b.wire = at::empty({total}, b.flat.options().dtype(opts_.comm_dtype));
+    else
+      b.wire = b.flat;
+    for (size_t s = 0; s < idx.size(); ++s) {
+      const at::Tensor& p = params_[idx[s]];
+      b.views.push_back(b.flat.as_strided(p.sizes(), p.strides(), b.offsets[s]));
+      where_[idx[s]] = {static_cast<int64_t>(bi), static_cast<int64_t>(s)};
+    }
+    b.pending_grads.resize(idx.size());
+    b.pending = static_cast<int>(idx.size());
+    b.stats.bytes = total * p0.element_size();
+    b.stats.num_params = static_cast<int64_t>(idx.size());
+    out.push_back(std::move(b));
+  }
+  for (size_t i = 0; i < params_.size(); ++i) DCP_CHECK(seen[i], "Reducer: parameter ", i, " not in any bucket");
+  buckets_ = std::move(out);
+  next_bucket_ = 0;
+}
+
+void Reducer::register_hooks() {
+  std::weak_ptr<Reducer> weak = shared_from_this();
+  for (size_t i = 0; i < params_.size(); ++i) {
+    auto acc = torch::autograd::impl::grad_accumulator(params_[i]);
+    DCP_CHECK(acc, "Reducer: parameter ", i, " has no grad accumulator (not a leaf?)");
+    const int64_t idx = static_cast<int64_t>(i);
+    auto handle = acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
+        [weak, idx](const torch::autograd::variable_list& outputs, const torch::autograd::variable_list&) {
+          if (auto self = weak.lock()) self->autograd_hook(idx);
+          return outputs;
+        }));
+    grad_accs_.push_back(std::move(acc));
+    hook_handles_.push_back(handle);
+  }
+}
+
+void Reducer::set_expect_backward(bool v) {
+  std::lock_guard<std::mutex> g(mu_);
+  expect_hooks_ = v;
+}
+
+void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs, bool require_sync) {
+  std::lock_guard<std::mutex> g(mu_);
+  DCP_CHECK(!finalize_queued_, "Reducer: forward called while a backward reduction is still in progress");
+  expect_hooks_ = require_sync;
+  if (!require_sync) return;
+  unused_list_.clear();
+  std::fill(unused_.begin(), unused_.end(), 0);
+  if (opts_.find_unused_parameters) find_unused(outputs);
+}
+
+void Reducer::find_unused(const std::vector<at::Tensor>& outputs) {
+  // Traverse the autograd graph from the outputs; parameters whose
+  // AccumulateGrad node is unreachable get no gradient this iteration.
+  std::unordered_set<torch::autograd::Node*> seen;
+  std::vector<torch::autograd::Node*> stack;
+  for (auto& o : outputs) {
+    if (!o.defined() || !o.requires_grad()) continue;
+    auto fn = o.grad_fn();
+    if (fn) {
+      if (seen.insert(fn.get()).second) stack.push_back(fn.get());
+    } else {
+      auto acc = torch::autograd::impl::try_get_grad_accumulator(o);
+      if (acc) seen.insert(acc.get());
+    }
+  }
+  while (!stack.empty()) {
+    auto* n = stack.back();
+    stack.pop_back();
+    for (const auto& e : n->next_edges()) {
+      auto* nx = e.function.get();
+      if (nx && seen.insert(nx).second) stack.push_back(nx);
+    }
+  }
+  for (size_t i = 0; i < params_.size(); ++i) {
+    if (!seen.count(grad_accs_[i].get())) {
+      unused_[i] = 1;
+      unused_list_.push_back(static_cast<int64_t>(i));
+    }
+  }
+}
+
+void Reducer::autograd_hook(int64_t index) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!expect_hooks_) return;
+  if (!finalize_queued_) {
+    finalize_queued_ = true;
+    backward_t0_ms_ = static_cast<double>(now_ms());
+    std::weak_ptr<Reducer> weak = shared_from_this();
+    torch::autograd::Engine::get_default_engine().queue_callback([weak] {
+      if (auto self = weak.lock()) self->finalize();
+    });
+  }
+  if (opts_.find_unused_parameters && !marked_unused_) {
+    marked_unused_ = true;
+    for (int64_t u : unused_list_) mark_ready(u, /*unused=*/true);
+  }
+  mark_ready(index, /*unused=*/false);
+  launch_ready_buckets();
+}
+
+void Reducer::mark_ready(int64_t i, bool unused) {
+  DCP_CHECK(!ready_[i], "Reducer: parameter ", i,
+            " was marked ready twice in one backward (reentrant backward / shared parameters across "
+            "checkpointed regions are not supported; or find_unused_parameters misclassified it)");
+  ready_[i] = 1;
+  if (record_order_) ready_order_.push_back(i);
+  auto [bi, s] = where_[i];
+  Bucket& b = buckets_[bi];
+  const at::Tensor& view = b.views[s];
+  const at::Tensor& grad = params_[i].grad();
+  if (unused || !grad.defined()) {
+    b.pending_grads[s] = at::Tensor();
+    view.zero_();
+  } else if (grad.data_ptr() == view.data_ptr() && same_layout(grad, view)) {
+    b.pending_grads[s] = at::Tensor();  // accumulated in place (gradient_as_bucket_view)
+  } else {
+    b.pending_grads[s] = grad;
+  }
+  --b.pending;
+}
+
+void Reducer::launch_ready_buckets() {
+  while (next_bucket_ < buckets_.size() && buckets_[next_bucket_].pending == 0) {
+    launch(buckets_[next_bucket_]);
+    ++next_bucket_;
+  }
+}
+
+void Reducer::launch(Bucket& b) {
+  // Pack: one multi-tensor launch for every gradient not already in place.
+  const bool compressed = !b.wire.is_same(b.flat);
+  std::vector<at::Tensor> src, dst;
+  for (size_t s = 0; s < b.params.size(); ++s) {
+    at::Tensor& g = b.pending_grads[s];
+    at::Tensor target = compressed
+        ? b.wire.as_strided(b.views[s].sizes(), b.views[s].strides(), b.offsets[s])
+        : b.views[s];
+    const at::Tensor& from = g.defined() ? g : b.views[s];
+    if (!g.defined() && !compressed) continue;  // already in the bucket
+    if (same_layout(from, target) && from.is_non_overlapping_and_dense() &&
+        (from.is_cuda() || from.device().is_cpu())) {
+      src.push_back(from);
+      dst.push_back(target);
+    } else {
+      target.copy_(from);
+    }
+  }
+  if (!src.empty()) {
+    // mt_copy needs a single src dtype per call; grads match the bucket dtype
+    // except under autocast-free mixed setups, which we copy per tensor.
+    bool uniform = true;
+    for (auto& t : src) uniform = uniform && t.scalar_type() == src[0].scalar_type();
+    if (uniform) {
+      ops::mt_copy(src, dst, 1.0);
+    } else {
+      for (size_t k = 0; k < src.size(); ++k) dst[k].copy_(src[k]);
+    }
+  }
+  for (auto& g : b.pending_grads) g = at::Tensor();
+  b.stats.ready_ms = static_cast<double>(now_ms()) - backward_t0_ms_;
+  if (comm_hook_) {
+    b.work = comm_hook_(b.wire);
+  } else {
+    b.work = comm_->all_reduce(b.wire, opts_.average ? ReduceOp::AVG : ReduceOp::SUM);
+  }
+  b.launched = true;
+}
+
+void Reducer::finalize() {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!finalize_queued_) return;
+  // Every bucket must have been launched: an unready parameter means the
+  // model produced no gradient for it and find_unused_parameters was off.
+  std::vector<int64_t> missing;
+  for (auto& b : buckets_)
+    if (!b.launched)
+      for (size_t s = 0; s < b.params.size(); ++s)
+        if (!ready_[b.params[s]]) missing.push_back(b.params[s]);
+  if (!missing.empty()) {
+    // reset so the next iteration can proceed after the user fixes things
+    finalize_queued_ = false;
+    expect_hooks_ = false;
+    std::string ids;
+    for (size_t k = 0; k < missing.size() && k < 16; ++k) ids += (k ? ", " : "") + std::to_string(missing[k]);
+    throw Error(str_cat("Reducer: expected to have finished reduction but parameters [", ids,
+                        "] received no gradient. Pass find_unused_parameters=True to DistributedDataParallel "
+                        "if parts of the model do not take part in the loss."));
+  }
+
+  std::vector<char> global_used;
+  if (opts_.find_unused_parameters) {
+    at::Tensor used = at::empty({static_cast<int64_t>(params_.size())}, at::kInt);
+    for (size_t i = 0; i < params_.size(); ++i) used[i] = unused_[i] ? 0 : 1;
+    at::Tensor dev_used = used.to(params_[0].device());
+    comm_->all_reduce(dev_used, ReduceOp::MAX)->wait();
+    at::Tensor h = dev_used.cpu();
+    global_used.resize(params_.size());
+    for (size_t i = 0; i < params_.size(); ++i) global_used[i] = h[i].item<int>() != 0;
+  }
+
+  for (auto& b : buckets_) {
+    b.work->wait();
+    b.stats.comm_ms = b.work->elapsed_ms();
+    if (!b.wire.is_same(b.flat)) ops::mt_copy({b.wire}, {b.flat}, 1.0);
+    std::vector<at::Tensor> src, dst;
+    for (size_t s = 0; s < b.params.size(); ++s) {
+      const int64_t i = b.params[s];
+      at::Tensor& grad = params_[i].mutable_grad();
+      const bool used = global_used.empty() || global_used[i];
+      if (!grad.defined()) {
+        if (used) grad = opts_.gradient_as_bucket_view ? b.views[s] : b.views[s].clone();
+        continue;
+      }
+      if (opts_.gradient_as_bucket_view) {
+        if (grad.data_ptr() != b.views[s].data_ptr()) grad = b.views[s];
+      } else if (same_layout(grad, b.views[s])) {
+        src.push_back(b.views[s]);
+        dst.push_back(grad);
+      } else {
+        grad.copy_(b.views[s]);
+      }
+    }
+    if (!src.empty()) ops::mt_copy(src, dst, 1.0);
+    b.work.reset();
+    b.launched = false;
+    b.pending = static_cast<int>(b.params.size());
+  }
+  std::fill(ready_.begin(), ready_.end(), 0);
+  next_bucket_ = 0;
+  finalize_queued_ = false;
+  marked_unused_ = false;
+  expect_hooks_ = false;
+  ++iterations_;
+  if (record_order_) {
+    record_order_ = false;
+    if (opts_.rebuild_buckets) rebuild_from_ready_order();
+  }
+}
+
+void Reducer::rebuild_from_ready_order() {
+  // Complete the observed order with parameters that produced no gradient.
+  std::vector<int64_t> order = ready_order_;
+  std::vector<char> in(params_.size(), 0);
+  for (int64_t i : order) in[i] = 1;
+  for (int64_t i = static_cast<int64_t>(params_.size()) - 1; i >= 0; --i)
+    if (!in[i]) order.push_back(i);
+  // Adopt rank 0's order everywhere: different orders would mismatch the
+  // collective sequence across ranks and hang RCCL.
+  at::Tensor t = at::from_blob(order.data(), {static_cast<int64_t>(order.size())}, at::kLong).clone();
+  at::Tensor dev = t.to(params_[0].device());
+  auto w = comm_->broadcast(dev, 0);
+  w->wait();
+  w->synchronize();
+  at::Tensor back = dev.cpu();
+  for (size_t k = 0; k < order.size(); ++k) order[k] = back[k].item<int64_t>();
+
+  std::vector<int64_t> sizes, keys;
+  for (auto& p : params_) {
+    sizes.push_back(p.numel() * p.element_size());
+    keys.push_back(bucket_key(p));
+  }
+  auto assignment = compute_bucket_assignment(sizes, keys, {opts_.first_bucket_bytes, opts_.bucket_bytes_cap}, order);
+  if (assignment == bucket_indices()) return;
+  // Keep current gradients (bucket views in gradient_as_bucket_view mode).
+  std::vector<at::Tensor> old_grads(params_.size());
+  for (size_t i = 0; i < params_.size(); ++i) old_grads[i] = params_[i].grad();
+  build_buckets(assignment);
+  if (opts_.gradient_as_bucket_view) {
+    for (size_t i = 0; i < params_.size(); ++i) {
+      if (!old_grads[i].defined()) continue;
+      auto [bi, s] = where_[i];
+      buckets_[bi].views[s].copy_(old_grads[i]);
+      params_[i].mutable_grad() = buckets_[bi].views[s];
+    }
+  }
+  ++rebuilds_;
+}
+
+void Reducer::wait_all() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& b : buckets_)
+    if (b.work) b.work->synchronize();
+}
+
+std::vector<std::vector<int64_t>> Reducer::bucket_indices() const {
+  std::vector<std::vector<int64_t>> r;
+  for (auto& b : buckets_) r.push_back(b.params);
+  return r;
+}
+
+std::vector<int64_t> Reducer::bucket_sizes_bytes() const {
+  std::vector<int64_t> r;
+  for (auto& b : buckets_) r.push_back(b.stats.bytes);
+  return r;
+}
+
+std::vector<BucketStats> Reducer::bucket_stats() const {
+  std::vector<BucketStats> r;
+  for (auto& b : buckets_) r.push_back(b.stats);
+  return r;
+}
+
+std::vector<at::Tensor> Reducer::bucket_buffers() const {
+  std::vector<at::Tensor> r;
+  for (auto& b : buckets_) r.push_back(b.flat);
+  return r;
+}
+
+}  // namespace dcp

@@ -1,0 +1,141 @@
+// Gradient Reducer: bucketing, autograd-hook driven launch of bucket
+// all-reduces overlapped with backward, finalize, ready-order rebuild.
+//
+// Parity: torch's C++ Reducer that the reference gets from
+// DistributedDataParallel(model, device_ids=[rank]) (main.py:122, SURVEY §2b
+// F6/F7, §3.3). The semantics kept: per-parameter post-accumulate hooks, in-
+// order bucket launch while backward continues, finalize at the end of
+// backward, gradients averaged over the world, `no_sync`, find_unused_
+// parameters, gradient_as_bucket_view, bucket rebuild from the observed
+// gradient-ready order (rank 0's order adopted everywhere).
+//
+// MI355X design: one flat buffer per bucket; pack/unpack are ONE multi-tensor
+// HIP launch per bucket (csrc/kernels/multi_tensor.hip) instead of a copy per
+// parameter; averaging is folded into RCCL (ncclAvg) so there is no separate
+// scale pass; optional bf16 wire compression packs fp32 grads straight into a
+// bf16 comm buffer in the same launch.
+#pragma once
+
+#include <ATen/ATen.h>
+#include <torch/csrc/autograd/function.h>
+
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../comm/communicator.h"
+
+namespace dcp {
+
+// torch-compatible bucket planner (semantics of
+// torch.distributed._compute_bucket_assignment_by_size): greedy packing per
+// (dtype, device) key under the limit list; `order` empty = natural order and
+// buckets sorted by min index, else tensors visited in `order` and buckets kept
+// in that order.
+std::vector<std::vector<int64_t>> compute_bucket_assignment(const std::vector<int64_t>& sizes_bytes,
+                                                            const std::vector<int64_t>& keys,
+                                                            const std::vector<int64_t>& limits,
+                                                            const std::vector<int64_t>& order);
+
+struct ReducerOptions {
+  bool gradient_as_bucket_view = false;
+  bool find_unused_parameters = false;
+  bool rebuild_buckets = true;
+  int64_t first_bucket_bytes = 1 << 20;
+  int64_t bucket_bytes_cap = 25 << 20;
+  // at::ScalarType of the wire buffer; Undefined = same as the gradient.
+  at::ScalarType comm_dtype = at::ScalarType::Undefined;
+  // false -> SUM instead of AVG (for custom hooks that pre-scale).
+  bool average = true;
+};
+
+struct BucketStats {
+  int64_t bytes = 0;
+  int64_t num_params = 0;
+  double ready_ms = 0;   // host time since backward start when the bucket became ready
+  double comm_ms = -1;   // device time of its collective (when timing enabled)
+};
+
+class Reducer : public std::enable_shared_from_this<Reducer> {
+ public:
+  using CommHook = std::function<WorkPtr(at::Tensor& bucket)>;
+
+  Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t>> buckets,
+          std::shared_ptr<Communicator> comm, ReducerOptions opts);
+  ~Reducer();
+
+  // Must be called once after construction (hooks capture a weak_ptr).
+  void register_hooks();
+
+  // Called from DDP forward: expect hooks in the next backward iff require_sync.
+  void prepare_for_backward(const std::vector<at::Tensor>& outputs, bool require_sync);
+  // Called when a forward ran without a following backward being expected.
+  void set_expect_backward(bool v);
+
+  // Custom comm hook (runs on the autograd thread with the bucket buffer).
+  void set_comm_hook(CommHook hook) { comm_hook_ = std::move(hook); }
+
+  std::vector<std::vector<int64_t>> bucket_indices() const;
+  std::vector<int64_t> bucket_sizes_bytes() const;
+  std::vector<BucketStats> bucket_stats() const;
+  std::vector<int64_t> ready_order() const { return ready_order_; }
+  int64_t num_iterations() const { return iterations_; }
+  int64_t num_rebuilds() const { return rebuilds_; }
+  bool has_rebuilt() const { return rebuilds_ > 0; }
+  // Bucket buffers (tests / optimizers that work on flat buffers).
+  std::vector<at::Tensor> bucket_buffers() const;
+  // Wait for in-flight reductions (used by no_sync exit / destructor paths).
+  void wait_all();
+
+ private:
+  struct Bucket {
+    std::vector<int64_t> params;
+    std::vector<int64_t> offsets;
+    at::Tensor flat;                  // gradient dtype
+    at::Tensor wire;                  // == flat, or compressed copy
+    std::vector<at::Tensor> views;    // as_strided views matching param layouts
+    std::vector<at::Tensor> pending_grads;  // copy mode: grads to pack at launch
+    int pending = 0;
+    bool launched = false;
+    WorkPtr work;
+    BucketStats stats;
+  };
+
+  void build_buckets(const std::vector<std::vector<int64_t>>& assignment);
+  void autograd_hook(int64_t index);
+  void mark_ready(int64_t index, bool unused);
+  void launch_ready_buckets();
+  void launch(Bucket& b);
+  void finalize();
+  void rebuild_from_ready_order();
+  void find_unused(const std::vector<at::Tensor>& outputs);
+
+  std::vector<at::Tensor> params_;
+  std::shared_ptr<Communicator> comm_;
+  ReducerOptions opts_;
+  CommHook comm_hook_;
+
+  std::vector<Bucket> buckets_;
+  std::vector<std::pair<int64_t, int64_t>> where_;  // param -> (bucket, slot)
+  std::vector<std::shared_ptr<torch::autograd::Node>> grad_accs_;
+  std::vector<uintptr_t> hook_handles_;
+
+  std::mutex mu_;
+  bool expect_hooks_ = false;
+  bool require_sync_ = true;
+  bool finalize_queued_ = false;
+  bool marked_unused_ = false;
+  size_t next_bucket_ = 0;
+  std::vector<char> ready_;
+  std::vector<char> unused_;
+  std::vector<int64_t> unused_list_;
+  std::vector<int64_t> ready_order_;
+  bool record_order_ = true;
+  int64_t iterations_ = 0;
+  int64_t rebuilds_ = 0;
+  double backward_t0_ms_ = 0;
+  at::Tensor local_used_;  // find_unused: per-param used flags (int32, on device)
+};
+
+}  // namespace dcp

@@ -1,0 +1,180 @@
+"""Native build driver: compiles csrc/ into the in-tree extension ``_C``.
+
+No hipify, no CUDA: ``.hip`` sources go through ``hipcc --offload-arch=gfx950``,
+``.cpp`` sources (torch/pybind glue, store, communicators, reducer) through the
+host C++ compiler with the same flags torch's ROCm extensions use, and the
+objects are linked against torch's bundled ``libamdhip64`` / ``librccl`` so a
+single HIP runtime and a single RCCL live in the process.
+
+The resulting ``distributed_compute_pytorch_amd/_C*.so`` is git-ignored but
+travels to the GPU box with the repo snapshot.
+
+Usage: ``python -m distributed_compute_pytorch_amd._build [-j N] [--force]``.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO = PKG_DIR.parent
+CSRC = REPO / "csrc"
+BUILD = REPO / "build" / "native"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+EXT_NAME = "_C"
+
+
+def _torch_paths():
+    import torch
+
+    root = Path(torch.__file__).resolve().parent
+    return root / "include", root / "lib"
+
+
+def ext_path() -> Path:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return PKG_DIR / f"{EXT_NAME}{suffix}"
+
+
+def _flags():
+    inc, _ = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    defs = [
+        "-D__HIP_PLATFORM_AMD__=1",
+        "-DUSE_ROCM=1",
+        "-DHIPBLAS_V2",
+        f"-DTORCH_EXTENSION_NAME={EXT_NAME}",
+        "-DTORCH_API_INCLUDE_EXTENSION_H",
+        "-D_GLIBCXX_USE_CXX11_ABI=1",
+    ]
+    incs = [
+        f"-I{CSRC}",
+        f"-I{inc}",
+        f"-I{inc / 'torch' / 'csrc' / 'api' / 'include'}",
+        f"-I{py_inc}",
+        f"-I{ROCM / 'include'}",
+    ]
+    common = ["-O3", "-fPIC", "-std=c++17", "-Wno-unused-parameter", "-Wno-deprecated-declarations"]
+    cxx = ["g++"] + common + defs + incs + ["-fvisibility=hidden"]
+    hip = (
+        [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+        + common
+        + defs
+        + incs
+        + [
+            "-D__HIP_NO_HALF_OPERATORS__=1",
+            "-D__HIP_NO_HALF_CONVERSIONS__=1",
+            "-fno-gpu-rdc",
+        ]
+    )
+    return cxx, hip
+
+
+def _link_cmd(objs, out):
+    _, lib = _torch_paths()
+    return (
+        ["g++", "-shared", "-o", str(out)]
+        + [str(o) for o in objs]
+        + [
+            f"-L{lib}",
+            "-ltorch",
+            "-ltorch_cpu",
+            "-ltorch_python",
+            "-lc10",
+            "-lc10_hip",
+            "-ltorch_hip",
+            f"{lib / 'libamdhip64.so'}",
+            f"{lib / 'librccl.so'}",
+            f"-Wl,-rpath,{lib}",
+            "-Wl,--no-as-needed",
+        ]
+    )
+
+
+def _sources():
+    srcs = sorted(CSRC.rglob("*.cpp")) + sorted(CSRC.rglob("*.hip"))
+    return srcs
+
+
+def _header_digest():
+    h = hashlib.sha1()
+    for p in sorted(list(CSRC.rglob("*.h")) + list(CSRC.rglob("*.cuh")) + list(CSRC.rglob("*.inc"))):
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def _obj_for(src: Path, cmd, hdr):
+    rel = src.relative_to(CSRC)
+    key = hashlib.sha1((" ".join(cmd) + hdr).encode() + src.read_bytes()).hexdigest()[:16]
+    return BUILD / (str(rel).replace("/", "__") + f".{key}.o")
+
+
+def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -> Path:
+    """Compile every native source for gfx950 and link ``_C``. Returns the .so path."""
+    BUILD.mkdir(parents=True, exist_ok=True)
+    cxx, hip = _flags()
+    hdr = _header_digest()
+    tasks = []
+    objs = []
+    for src in _sources():
+        cmd = hip if src.suffix == ".hip" else cxx
+        obj = _obj_for(src, cmd, hdr)
+        objs.append(obj)
+        if force or not obj.exists():
+            tasks.append((src, cmd, obj))
+
+    def compile_one(t):
+        src, cmd, obj = t
+        full = cmd + (["-x", "hip"] if src.suffix == ".hip" else []) + ["-c", str(src), "-o", str(obj) + ".tmp"]
+        if verbose:
+            print(" ".join(full), flush=True)
+        r = subprocess.run(full, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+        os.replace(str(obj) + ".tmp", obj)
+        return src
+
+    if tasks:
+        n = jobs or min(8, os.cpu_count() or 4)
+        with ThreadPoolExecutor(max_workers=n) as ex:
+            for src in ex.map(compile_one, tasks):
+                print(f"[dcp build] compiled {src.relative_to(REPO)}", flush=True)
+    out = ext_path()
+    newest_obj = max(o.stat().st_mtime for o in objs)
+    if force or tasks or not out.exists() or out.stat().st_mtime < newest_obj:
+        tmp = out.with_suffix(".tmp.so")
+        r = subprocess.run(_link_cmd(objs, tmp), capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, out)
+        print(f"[dcp build] linked {out.relative_to(REPO)}", flush=True)
+    # drop stale objects
+    keep = {o.name for o in objs}
+    for o in BUILD.glob("*.o"):
+        if o.name not in keep:
+            o.unlink()
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--clean", action="store_true")
+    a = ap.parse_args(argv)
+    if a.clean:
+        shutil.rmtree(BUILD, ignore_errors=True)
+    build(a.jobs, a.force, a.verbose)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

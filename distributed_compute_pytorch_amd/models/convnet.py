@@ -1,0 +1,43 @@
+"""The reference model: MNIST ConvNet (main.py:20-45).
+
+conv(1→32,k3) → ReLU → conv(32→64,k3) → ReLU → maxpool2 → Dropout2d(0.25)
+→ flatten(9216) → fc(9216→128) → BatchNorm1d(128) → ReLU → dropout(0.5)
+→ fc(128→10) → log_softmax.  1,200,138 parameters, 3 BN buffers.
+
+Parameter registration order and names match the reference exactly
+(conv1, conv2, dropout1, dropout2, fc1, fc2, batchnorm), so state_dict keys —
+``module.conv1.weight`` … ``module.batchnorm.num_batches_tracked`` under DDP —
+are identical. The reference applies ``Dropout2d`` to the 2-D
+fc1 activation, which acts element-wise; ``nn.Dropout`` is
+used for ``dropout2`` so behaviour is the same without the 2.x warning.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+
+class ConvNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 32, 3, 1)
+        self.conv2 = nn.Conv2d(32, 64, 3, 1)
+        self.dropout1 = nn.Dropout2d(0.25)
+        self.dropout2 = nn.Dropout(0.5)
+        self.fc1 = nn.Linear(9216, 128)
+        self.fc2 = nn.Linear(128, 10)
+        self.batchnorm = nn.BatchNorm1d(128)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = F.relu(self.conv1(x))
+        x = F.relu(self.conv2(x))
+        x = F.max_pool2d(x, 2)
+        x = self.dropout1(x)
+        x = torch.flatten(x, 1)
+        x = self.fc1(x)
+        x = self.batchnorm(x)
+        x = F.relu(x)
+        x = self.dropout2(x)
+        x = self.fc2(x)
+        return F.log_softmax(x, dim=1)

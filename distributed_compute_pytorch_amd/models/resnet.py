@@ -1,0 +1,110 @@
+"""ResNet-50 (v1.5: stride on the 3×3 conv) — BASELINE configs #2 and #4.
+
+Architecture and init follow the standard ImageNet ResNet-50 (25,557,032
+parameters; kaiming-normal fan_out convs, BN γ=1/β=0, optional zero-init of
+the last BN γ in each residual branch). Written from scratch (torchvision is
+not available here).
+
+MI355X layout: the model is meant to run channels_last (NHWC) in bf16
+autocast — MIOpen's NHWC implicit-GEMM convolutions feed the MFMA cores
+without layout transposes. ``fused_bn=True`` replaces every BN(+ReLU)(+residual
+add) with the hand-written HIP kernels of :mod:`..ops.batchnorm` (one read +
+one write per activation in the forward, statistics fused).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Type
+
+import torch
+from torch import nn
+
+from ..ops.batchnorm import BatchNormAct2d
+
+
+def conv3x3(cin, cout, stride=1):
+    return nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+
+
+def conv1x1(cin, cout, stride=1):
+    return nn.Conv2d(cin, cout, 1, stride, 0, bias=False)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None,
+                 fused_bn: bool = False):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = conv1x1(cin, width)
+        self.bn1 = BatchNormAct2d(width, act=True, fused=fused_bn)
+        self.conv2 = conv3x3(width, width, stride)
+        self.bn2 = BatchNormAct2d(width, act=True, fused=fused_bn)
+        self.conv3 = conv1x1(width, cout)
+        # BN3 + residual add + ReLU are one fused op
+        self.bn3 = BatchNormAct2d(cout, act=True, residual=True, fused=fused_bn)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), identity)
+
+
+def _downsample(cin, cout, stride, fused_bn):
+    # nn.Sequential keeps torchvision's state_dict keys (downsample.0 / downsample.1)
+    return nn.Sequential(conv1x1(cin, cout, stride), BatchNormAct2d(cout, act=False, fused=fused_bn))
+
+
+class ResNet(nn.Module):
+    def __init__(self, block: Type[Bottleneck], layers: List[int], num_classes: int = 1000,
+                 zero_init_residual: bool = False, fused_bn: bool = False):
+        super().__init__()
+        self.inplanes = 64
+        self.fused_bn = fused_bn
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = BatchNormAct2d(64, act=True, fused=fused_bn)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, BatchNormAct2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+
+    def _make_layer(self, block, width, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != width * block.expansion:
+            downsample = _downsample(self.inplanes, width * block.expansion, stride, self.fused_bn)
+        layers = [block(self.inplanes, width, stride, downsample, self.fused_bn)]
+        self.inplanes = width * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, width, fused_bn=self.fused_bn))
+        return nn.Sequential(*layers)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(self.avgpool(x), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, **kw)
+
+
+def resnet18_like(num_classes: int = 10, **kw) -> ResNet:
+    """Tiny bottleneck ResNet for tests (same code path, few layers)."""
+    return ResNet(Bottleneck, [1, 1, 1, 1], num_classes, **kw)

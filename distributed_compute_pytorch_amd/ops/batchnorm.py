@@ -1,0 +1,66 @@
+"""BatchNorm2d (+ReLU) (+residual add) for NHWC activations.
+
+``BatchNormAct2d`` is an ``nn.BatchNorm2d`` subclass (identical parameters,
+buffers and state_dict keys) whose forward optionally adds a residual and
+applies ReLU. With ``fused=True`` on a GPU it runs the hand-written gfx950
+kernels of ``csrc/kernels/batchnorm.hip`` through :class:`_BNActFn`; otherwise
+it is the plain ATen composition (reference path, and the numerics oracle).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+from .._ext import C as _C
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1, act: bool = True,
+                 residual: bool = False, fused: bool = False):
+        super().__init__(num_features, eps=eps, momentum=momentum)
+        self.act = act
+        self.residual = residual
+        self.fused = fused
+
+    def _use_fused(self, x: torch.Tensor) -> bool:
+        return self.fused and x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if self._use_fused(x):
+            return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.num_batches_tracked,
+                          self.training, self.momentum, self.eps, residual if self.residual else None, self.act)
+        y = super().forward(x)
+        if self.residual and residual is not None:
+            y = y + residual
+        if self.act:
+            y = F.relu(y, inplace=True)
+        return y
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act):
+        y, mean, invstd = _C.bn_act_fwd(x, weight, bias, running_mean, running_var, residual, training,
+                                        float(momentum), float(eps), bool(act))
+        ctx.save_for_backward(x, weight, bias, mean, invstd, y)
+        ctx.has_res = residual is not None
+        ctx.act = act
+        ctx.training = training
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, bias, mean, invstd, y = ctx.saved_tensors
+        gx, gw, gb, gres = _C.bn_act_bwd(gy.contiguous(memory_format=torch.channels_last), x, weight, bias, mean,
+                                         invstd, y, ctx.act, ctx.has_res, ctx.training)
+        return gx, gw, gb, None, None, None, None, None, (gres if ctx.has_res else None), None
+
+
+def bn_act(x, weight, bias, running_mean, running_var, num_batches_tracked, training, momentum, eps, residual,
+           act):
+    if training and num_batches_tracked is not None:
+        num_batches_tracked.add_(1)
+    return _BNActFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act)

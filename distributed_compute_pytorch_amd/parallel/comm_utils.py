@@ -1,0 +1,137 @@
+"""Coalesced broadcast / parameter verification helpers.
+
+Parity: torch's ``_broadcast_coalesced`` (comm.cpp) and
+``_verify_param_shape_across_processes`` that DDP runs at construction and,
+for buffers, every training forward.
+Flatten/unflatten is one multi-tensor HIP launch per dtype group
+(``_C.mt_copy``), the broadcast one RCCL call per group.
+"""
+from __future__ import annotations
+
+import hashlib
+from collections import OrderedDict
+from typing import Dict, List, Sequence
+
+import torch
+
+from .._ext import C as _C
+
+_MT_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
+
+
+def is_dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense (any dim permutation), like ATen's check."""
+    if t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)):
+        return True
+    expected = 1
+    for size, stride in sorted(zip(t.shape, t.stride()), key=lambda a: a[1]):
+        if size == 1:
+            continue
+        if stride != expected:
+            return False
+        expected *= size
+    return True
+
+
+def _group_by_dtype(tensors: Sequence[torch.Tensor]):
+    groups: "OrderedDict[tuple, List[int]]" = OrderedDict()
+    for i, t in enumerate(tensors):
+        groups.setdefault((t.dtype, t.device), []).append(i)
+    return groups
+
+
+def _flat_views(flat: torch.Tensor, tensors: Sequence[torch.Tensor]):
+    views, off = [], 0
+    for t in tensors:
+        n = t.numel()
+        views.append(flat.as_strided(t.shape, t.stride(), off) if is_dense(t)
+                     else flat[off:off + n].view(t.shape))
+        off += n
+    return views
+
+
+def pack(tensors: Sequence[torch.Tensor], flat: torch.Tensor):
+    dense = all(is_dense(t) for t in tensors)
+    views = _flat_views(flat, tensors)
+    if dense and flat.dtype in _MT_DTYPES and all(t.dtype == flat.dtype for t in tensors):
+        _C.mt_copy(list(tensors), views, 1.0)
+    else:
+        for v, t in zip(views, tensors):
+            v.copy_(t)
+
+
+def unpack(flat: torch.Tensor, tensors: Sequence[torch.Tensor]):
+    dense = all(is_dense(t) for t in tensors)
+    views = _flat_views(flat, tensors)
+    if dense and flat.dtype in _MT_DTYPES and all(t.dtype == flat.dtype for t in tensors):
+        _C.mt_copy(views, list(tensors), 1.0)
+    else:
+        for v, t in zip(views, tensors):
+            t.copy_(v)
+
+
+class CoalescedBroadcaster:
+    """Broadcast a fixed list of tensors from ``src`` with one collective per
+    (dtype, device) group; flat buffers are allocated once and reused (the
+    per-forward buffer broadcast is latency-bound)."""
+
+    def __init__(self, tensors: Sequence[torch.Tensor], cap_bytes: int = 250 << 20):
+        self.tensors = list(tensors)
+        self.cap = cap_bytes
+        self.plan = []  # list of (indices, flat)
+        for (dtype, device), idx in _group_by_dtype(self.tensors).items():
+            chunk, size = [], 0
+            for i in idx:
+                nb = self.tensors[i].numel() * self.tensors[i].element_size()
+                if chunk and size + nb > self.cap:
+                    self.plan.append(self._mk(chunk, dtype, device))
+                    chunk, size = [], 0
+                chunk.append(i)
+                size += nb
+            if chunk:
+                self.plan.append(self._mk(chunk, dtype, device))
+
+    def _mk(self, idx, dtype, device):
+        n = sum(self.tensors[i].numel() for i in idx)
+        return idx, torch.empty(n, dtype=dtype, device=device)
+
+    @torch.no_grad()
+    def __call__(self, pg, src: int = 0):
+        works = []
+        for idx, flat in self.plan:
+            ts = [self.tensors[i] for i in idx]
+            if pg.rank() == src:
+                pack(ts, flat)
+            works.append((pg.comm_for(flat).broadcast(flat, src), idx, flat))
+        for w, idx, flat in works:
+            w.wait()
+            if pg.rank() != src:
+                unpack(flat, [self.tensors[i] for i in idx])
+
+
+def broadcast_coalesced(pg, tensors: Sequence[torch.Tensor], src: int = 0, cap_bytes: int = 250 << 20):
+    if pg.size() == 1 or not tensors:
+        return
+    CoalescedBroadcaster(tensors, cap_bytes)(pg, src)
+
+
+def verify_params_across_processes(pg, params: Sequence[torch.Tensor]):
+    """All ranks must hold the same parameter list (count, shapes, dtypes):
+    otherwise the bucket collectives would mismatch and hang."""
+    if pg.size() == 1:
+        return
+    desc = ";".join(f"{tuple(p.shape)}:{p.dtype}:{tuple(p.stride())}" for p in params)
+    digest = hashlib.sha1(desc.encode()).hexdigest()
+    key = f"{pg.prefix}/ddp/verify/{_verify_seq.setdefault(pg.prefix, 0)}"
+    _verify_seq[pg.prefix] += 1
+    pg.store.set(f"{key}/{pg.rank()}", f"{len(params)}|{digest}".encode())
+    mine = f"{len(params)}|{digest}"
+    for r in range(pg.size()):
+        other = pg.store.get(f"{key}/{r}").decode()
+        if other != mine:
+            raise RuntimeError(
+                f"DDP: rank {pg.rank()} has parameters [{mine}] but rank {r} has [{other}]; every rank must "
+                "construct the same model")
+
+
+_verify_seq: Dict[str, int] = {}
