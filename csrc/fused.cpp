@@ -1,9 +1,124 @@
 #include "fused.h"
 
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include "common.h"
+#include "kernels/bn_kernels.h"
+
 namespace dcp {
 namespace fused {
 
-void bind(pybind11::module& m) { (void)m; }
+namespace {
+
+hipStream_t stream_of(const at::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+int bn_dtype(const at::Tensor& x) {
+  if (x.scalar_type() == at::kBFloat16) return kern::BN_BF16;
+  if (x.scalar_type() == at::kFloat) return kern::BN_F32;
+  throw Error(str_cat("fused BN: unsupported activation dtype ", c10::toString(x.scalar_type())));
+}
+
+void check_nhwc(const at::Tensor& x, const char* what) {
+  DCP_CHECK(x.is_cuda(), what, ": device tensor required");
+  DCP_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), what,
+            ": expected a channels_last 4-D tensor");
+  DCP_CHECK(x.size(1) % 8 == 0, what, ": channel count must be a multiple of 8");
+  DCP_CHECK(x.numel() / 8 < (int64_t(1) << 32), what, ": tensor too large");
+}
+
+const float* opt_ptr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+
+}  // namespace
+
+// Returns (y, mean, invstd). Training: batch statistics (+ running-stat update).
+// Eval: running statistics.
+std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
+                                   const c10::optional<at::Tensor>& bias,
+                                   const c10::optional<at::Tensor>& running_mean,
+                                   const c10::optional<at::Tensor>& running_var,
+                                   const c10::optional<at::Tensor>& residual, bool training, double momentum,
+                                   double eps, bool act) {
+  check_nhwc(x, "bn_act_fwd");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  at::Tensor res;
+  if (residual.has_value() && residual->defined()) {
+    res = residual->contiguous(at::MemoryFormat::ChannelsLast);
+    DCP_CHECK(res.sizes() == x.sizes() && res.scalar_type() == x.scalar_type(), "bn_act_fwd: residual mismatch");
+  }
+  at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
+  at::Tensor b = bias.has_value() && bias->defined() ? bias->to(at::kFloat).contiguous() : at::Tensor();
+  at::Tensor mean = at::empty({C}, fopt);
+  at::Tensor invstd = at::empty({C}, fopt);
+  at::Tensor scale = at::empty({C}, fopt);
+  at::Tensor shift = at::empty({C}, fopt);
+  auto s = stream_of(x);
+  if (training) {
+    const int nblk = kern::bn_partial_blocks(M, static_cast<int>(C));
+    at::Tensor part = at::empty({nblk * 2 * C}, fopt);
+    float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
+    float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
+    kern::bn_forward_train(bn_dtype(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, y.data_ptr(), M,
+                           static_cast<int>(C), w.defined() ? w.data_ptr<float>() : nullptr,
+                           b.defined() ? b.data_ptr<float>() : nullptr, rm, rv, static_cast<float>(momentum),
+                           static_cast<float>(eps), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                           scale.data_ptr<float>(), shift.data_ptr<float>(), part.data_ptr<float>(), act, s);
+  } else {
+    DCP_CHECK(running_mean.has_value() && running_var.has_value(), "bn_act_fwd: eval mode needs running stats");
+    mean.copy_(*running_mean);
+    invstd.copy_(at::rsqrt(*running_var + eps));
+    at::Tensor g = w.defined() ? w : at::ones({C}, fopt);
+    at::Tensor bb = b.defined() ? b : at::zeros({C}, fopt);
+    scale.copy_(g * invstd);
+    shift.copy_(bb - mean * scale);
+    kern::bn_apply(bn_dtype(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, y.data_ptr(), M,
+                   static_cast<int>(C), scale.data_ptr<float>(), shift.data_ptr<float>(), act, s);
+  }
+  return {y, mean, invstd};
+}
+
+// Returns (dx, dweight, dbias, dresidual).
+std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const at::Tensor& x, const c10::optional<at::Tensor>& weight,
+                                   const c10::optional<at::Tensor>& bias, const at::Tensor& mean,
+                                   const at::Tensor& invstd, const at::Tensor& y, bool act, bool has_res,
+                                   bool training) {
+  check_nhwc(x, "bn_act_bwd");
+  c10::hip::HIPGuard guard(x.device().index());
+  at::Tensor g = gy.contiguous(at::MemoryFormat::ChannelsLast);
+  if (g.scalar_type() != x.scalar_type()) g = g.to(x.scalar_type());
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  at::Tensor gres = has_res ? at::empty_like(x, at::MemoryFormat::ChannelsLast) : at::Tensor();
+  const bool has_w = weight.has_value() && weight->defined();
+  at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
+  at::Tensor dw = at::empty({C}, fopt);
+  at::Tensor db = at::empty({C}, fopt);
+  at::Tensor k = at::empty({3 * C}, fopt);
+  const int nblk = kern::bn_partial_blocks(M, static_cast<int>(C));
+  at::Tensor part = at::empty({nblk * 2 * C}, fopt);
+  kern::bn_backward(bn_dtype(x), g.data_ptr(), y.data_ptr(), x.data_ptr(), M, static_cast<int>(C),
+                    has_w ? w.data_ptr<float>() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(), act,
+                    has_res, has_res ? gres.data_ptr() : nullptr, dx.data_ptr(), dw.data_ptr<float>(),
+                    db.data_ptr<float>(), k.data_ptr<float>(), k.data_ptr<float>() + C, k.data_ptr<float>() + 2 * C,
+                    part.data_ptr<float>(), training, stream_of(x));
+  at::Tensor dweight = has_w ? dw.to(weight->scalar_type()) : at::Tensor();
+  const bool has_b = bias.has_value() && bias->defined();
+  at::Tensor dbias = has_b ? db.to(bias->scalar_type()) : at::Tensor();
+  return {dx, dweight, dbias, gres};
+}
+
+void bind(pybind11::module& m) {
+  m.def("bn_act_fwd", &bn_act_fwd, "fused NHWC BatchNorm(+residual)(+ReLU) forward");
+  m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward");
+}
 
 }  // namespace fused
 }  // namespace dcp

@@ -1,0 +1,69 @@
+"""Fused NHWC BatchNorm(+residual)(+ReLU) kernels vs the fp32 ATen composition."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, w, b, rm, rv, res, act, training, momentum=0.1, eps=1e-5):
+    y = F.batch_norm(x, rm, rv, w, b, training, momentum, eps)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if act else y
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 9), (2, 2048, 3, 3), (16, 24, 5, 5), (3, 4096, 2, 2)])
+@pytest.mark.parametrize("act,residual", [(True, False), (True, True), (False, False)])
+@pytest.mark.parametrize("training", [True, False])
+def test_bn_act_fwd_bwd(cuda, dtype, shape, act, residual, training):
+    from distributed_compute_pytorch_amd.ops.batchnorm import bn_act
+
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    x = (torch.randn(shape, device=cuda) * 2 + 0.5).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(shape, device=cuda).contiguous(memory_format=torch.channels_last) if residual else None
+    w = torch.rand(C, device=cuda) + 0.5
+    b = torch.randn(C, device=cuda)
+    rm0, rv0 = torch.randn(C, device=cuda) * 0.1, torch.rand(C, device=cuda) + 0.5
+    gy = torch.randn(shape, device=cuda).contiguous(memory_format=torch.channels_last)
+
+    # fp32 reference on the same (dtype-rounded) inputs
+    xr = x.to(dtype).float().requires_grad_()
+    rr = r.to(dtype).float().requires_grad_() if residual else None
+    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
+    rm_r, rv_r = rm0.clone(), rv0.clone()
+    yr = _ref(xr, wr, br, rm_r, rv_r, rr, act, training)
+    yr.backward(gy.to(dtype).float())
+
+    xo = x.to(dtype).detach().clone().contiguous(memory_format=torch.channels_last).requires_grad_()
+    ro = r.to(dtype).detach().clone().contiguous(memory_format=torch.channels_last).requires_grad_() if residual else None
+    wo, bo = w.clone().requires_grad_(), b.clone().requires_grad_()
+    rm_o, rv_o = rm0.clone(), rv0.clone()
+    nbt = torch.zeros((), dtype=torch.long, device=cuda)
+    yo = bn_act(xo, wo, bo, rm_o, rv_o, nbt, training, 0.1, 1e-5, ro, act)
+    yo.backward(gy.to(dtype))
+
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(yo.float(), yr, **tol)
+    torch.testing.assert_close(xo.grad.float(), xr.grad, **tol)
+    torch.testing.assert_close(wo.grad, wr.grad, rtol=1e-3 if dtype == torch.float32 else 2e-2,
+                               atol=1e-3 * (N * H * W) ** 0.5 if dtype == torch.float32 else 0.5)
+    torch.testing.assert_close(bo.grad, br.grad, rtol=1e-3, atol=1e-2 if dtype == torch.float32 else 0.5)
+    if residual:
+        torch.testing.assert_close(ro.grad.float(), rr.grad, **tol)
+    torch.testing.assert_close(rm_o, rm_r, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rv_o, rv_r, rtol=1e-3, atol=1e-3)
+
+
+def test_bn_module_state_dict_compat(cuda):
+    from distributed_compute_pytorch_amd.ops import BatchNormAct2d
+
+    m = BatchNormAct2d(64, fused=True).to(cuda)
+    ref = torch.nn.BatchNorm2d(64).to(cuda)
+    assert m.state_dict().keys() == ref.state_dict().keys()
+    x = torch.randn(4, 64, 8, 8, device=cuda).contiguous(memory_format=torch.channels_last)
+    m.train()
+    m(x)
+    assert int(m.num_batches_tracked) == 1

@@ -60,24 +60,36 @@ def test_ddp_matches_local_training(pg, cuda, grad_as_view):
     assert set(ddp.state_dict().keys()) == {"module." + k for k in ref.state_dict().keys()}
 
 
-def test_resnet50_bf16_step(pg, cuda):
+def test_resnet50_bf16_step_matches_stock(pg, cuda):
+    """Our DDP + fused SGD + fused BN vs plain torch (no DDP, torch SGD, ATen BN)
+    on the same init and batch: losses must track within bf16 noise."""
     import distributed_compute_pytorch_amd as dcp
     from distributed_compute_pytorch_amd.models import resnet50
 
-    model = resnet50().to(cuda).to(memory_format=torch.channels_last)
-    ddp = dcp.parallel.DistributedDataParallel(model, device_ids=[0])
-    opt = dcp.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9)
-    x = torch.randn(8, 3, 224, 224, device=cuda).contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (8,), device=cuda)
-    losses = []
-    for _ in range(3):
-        opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = F.cross_entropy(ddp(x), y)
-        loss.backward()
-        opt.step()
-        losses.append(loss.item())
-    assert all(torch.isfinite(torch.tensor(losses)))
-    assert losses[-1] < losses[0]
+    torch.manual_seed(0)
+    ref = resnet50(num_classes=100).to(cuda).to(memory_format=torch.channels_last)
+    model = resnet50(num_classes=100, fused_bn=True).to(cuda).to(memory_format=torch.channels_last)
+    model.load_state_dict(ref.state_dict())
+    ddp = dcp.parallel.DistributedDataParallel(model, device_ids=[0], gradient_as_bucket_view=True)
+    o_ref = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9)
+    opt = dcp.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(16, 3, 128, 128, generator=g).to(cuda).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 100, (16,), generator=g).to(cuda)
+    l_ref, l_ours = [], []
+    for _ in range(4):
+        for m, o, acc in ((ref, o_ref, l_ref), (ddp, opt, l_ours)):
+            o.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            o.step()
+            acc.append(loss.item())
+    assert all(torch.isfinite(torch.tensor(l_ours)))
+    assert l_ours[-1] < l_ours[0]
+    for a, b in zip(l_ref, l_ours):
+        assert abs(a - b) < 0.05 * max(1.0, abs(a)), (l_ref, l_ours)
+    for (n, p), q in zip(ref.named_parameters(), model.parameters()):
+        torch.testing.assert_close(q.float(), p.float(), rtol=0.1, atol=2e-2, msg=n)
     info = ddp.ddp_logging_data()
     assert info["rebuilds"] == 1 and sum(info["bucket_sizes"]) == sum(p.numel() * 4 for p in model.parameters())
