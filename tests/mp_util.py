@@ -1,0 +1,21 @@
+"""Helpers for multi-process CPU tests (host backend, 127.0.0.1 rendezvous)."""
+import os
+
+from distributed_compute_pytorch_amd.distributed.launch import free_port, spawn
+
+
+def _entry(rank, fn, world, port, backend, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import distributed_compute_pytorch_amd as dcp
+
+    if backend is not None:
+        dcp.distributed.init_process_group(backend)
+    try:
+        fn(rank, world, *args)
+    finally:
+        if backend is not None:
+            dcp.distributed.destroy_process_group()
+
+
+def run_world(fn, world=2, *args, backend="gloo", timeout=180):
+    spawn(_entry, (fn, world, free_port(), backend, args), nprocs=world, timeout=timeout)

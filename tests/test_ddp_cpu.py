@@ -1,0 +1,226 @@
+"""DDP parity oracle on CPU: our DDP (host backend) vs stock torch DDP (gloo),
+world_size 2, same model / seeds / data (SURVEY §4.2 'Integration parity oracle')."""
+import copy
+import datetime
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from mp_util import run_world
+
+
+def _init_torch_pg(rank, world):
+    import torch.distributed as tdist
+
+    port = int(os.environ["MASTER_PORT"]) + 1
+    tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                             timeout=datetime.timedelta(seconds=60))
+    return tdist
+
+
+def _step(model, opt, x, y, seed):
+    opt.zero_grad()
+    with torch.random.fork_rng():
+        torch.manual_seed(seed)
+        loss = F.nll_loss(model(x), y)
+    loss.backward()
+    opt.step()
+    return loss.detach()
+
+
+def _parity(rank, world, kwargs, steps, accumulate):
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.models import ConvNet
+
+    tdist = _init_torch_pg(rank, world)
+    torch.manual_seed(0)
+    m_ours = ConvNet()
+    m_ref = copy.deepcopy(m_ours)
+    ours = dcp.parallel.DistributedDataParallel(m_ours, **kwargs)
+    ref_kw = {k: v for k, v in kwargs.items() if k in ("gradient_as_bucket_view", "bucket_cap_mb",
+                                                         "find_unused_parameters", "broadcast_buffers")}
+    ref = nn.parallel.DistributedDataParallel(m_ref, **ref_kw)
+    o1 = dcp.optim.Adadelta(ours.parameters(), lr=1e-3)
+    o2 = torch.optim.Adadelta(ref.parameters(), lr=1e-3)
+    s1 = dcp.optim.StepLR(o1, step_size=1, gamma=0.7)
+    s2 = torch.optim.lr_scheduler.StepLR(o2, step_size=1, gamma=0.7)
+    g = torch.Generator().manual_seed(100 + rank)
+    for it in range(steps):
+        xs = [torch.randn(16, 1, 28, 28, generator=g) for _ in range(accumulate)]
+        ys = [torch.randint(0, 10, (16,), generator=g) for _ in range(accumulate)]
+        losses = []
+        for model, opt in ((ours, o1), (ref, o2)):
+            opt.zero_grad()
+            for k in range(accumulate):
+                ctx = model.no_sync() if k < accumulate - 1 else _null()
+                with ctx:
+                    with torch.random.fork_rng():
+                        torch.manual_seed(1000 * it + k)
+                        loss = F.nll_loss(model(xs[k]), ys[k])
+                    loss.backward()
+            opt.step()
+            losses.append(loss.detach())
+        torch.testing.assert_close(losses[0], losses[1], rtol=1e-5, atol=1e-6)
+        s1.step()
+        s2.step()
+    for (n, p), q in zip(m_ref.named_parameters(), m_ours.parameters()):
+        torch.testing.assert_close(q, p, rtol=2e-5, atol=1e-6, msg=n)
+    for (n, b), c in zip(m_ref.named_buffers(), m_ours.buffers()):
+        torch.testing.assert_close(c, b, rtol=2e-5, atol=1e-6, msg=n)
+    assert list(ours.state_dict().keys()) == list(ref.state_dict().keys())
+    assert o1.state_dict()["param_groups"][0]["lr"] == pytest.approx(o2.state_dict()["param_groups"][0]["lr"])
+    assert list(o1.state_dict()["state"][0].keys()) == list(o2.state_dict()["state"][0].keys())
+    # all ranks hold identical replicas
+    flat = torch.cat([p.detach().reshape(-1) for p in m_ours.parameters()])
+    other = flat.clone()
+    dcp.distributed.broadcast(other, 0)
+    torch.testing.assert_close(flat, other)
+    tdist.destroy_process_group()
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+@pytest.mark.parametrize("kwargs", [{}, {"gradient_as_bucket_view": True}, {"bucket_cap_mb": 0.05},
+                                    {"broadcast_buffers": False}])
+def test_ddp_matches_torch_ddp(kwargs):
+    run_world(_parity, 2, kwargs, 3, 1)
+
+
+def test_ddp_no_sync_accumulation_matches_torch():
+    run_world(_parity, 2, {}, 2, 3)
+
+
+def _bucket_rebuild(rank, world):
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.models import ConvNet
+
+    torch.manual_seed(0)
+    m = dcp.parallel.DistributedDataParallel(ConvNet())
+    x = torch.randn(4, 1, 28, 28)
+    for _ in range(2):
+        F.nll_loss(m(x), torch.zeros(4, dtype=torch.long)).backward()
+    info = m.ddp_logging_data()
+    # torch rebuilds into 4,725,288 B + 75,264 B
+    assert info["bucket_sizes"] == [4725288, 75264], info
+    assert info["rebuilds"] == 1
+
+
+def test_bucket_rebuild_matches_reference_sizes():
+    run_world(_bucket_rebuild, 2)
+
+
+class _Branchy(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = nn.Linear(8, 8)
+        self.b = nn.Linear(8, 8)
+        self.head = nn.Linear(8, 2)
+
+    def forward(self, x, use_b):
+        h = self.a(x)
+        if use_b:
+            h = self.b(h)
+        return self.head(h)
+
+
+def _unused(rank, world):
+    import distributed_compute_pytorch_amd as dcp
+
+    torch.manual_seed(0)
+    m = _Branchy()
+    ref = copy.deepcopy(m)
+    ddp = dcp.parallel.DistributedDataParallel(m, find_unused_parameters=True)
+    x = torch.randn(4, 8) + rank
+    # rank 0 uses branch b, rank 1 does not: b's grad must still be averaged
+    ddp(x, use_b=(rank == 0)).sum().backward()
+    grads = {n: p.grad.clone() if p.grad is not None else None for n, p in m.named_parameters()}
+    # expected: average of per-rank local grads (zeros for unused)
+    outs = []
+    for r in range(world):
+        rr = copy.deepcopy(ref)
+        rr(torch.randn(4, 8) * 0 + x - rank + r, use_b=(r == 0)).sum().backward()
+        outs.append({n: (p.grad if p.grad is not None else torch.zeros_like(p)) for n, p in rr.named_parameters()})
+    for n in grads:
+        exp = sum(o[n] for o in outs) / world
+        torch.testing.assert_close(grads[n], exp, rtol=1e-5, atol=1e-6, msg=n)
+
+
+def test_find_unused_parameters():
+    run_world(_unused, 2)
+
+
+def _unused_error(rank, world):
+    import distributed_compute_pytorch_amd as dcp
+
+    m = _Branchy()
+    ddp = dcp.parallel.DistributedDataParallel(m)
+    with pytest.raises(RuntimeError, match="find_unused_parameters"):
+        ddp(torch.randn(2, 8), use_b=False).sum().backward()
+
+
+def test_unused_without_flag_raises():
+    run_world(_unused_error, 2)
+
+
+def _compress(rank, world):
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.parallel import comm_hooks
+
+    torch.manual_seed(0)
+    base = nn.Sequential(nn.Linear(32, 64), nn.ReLU(), nn.Linear(64, 4))
+    a, b, c = copy.deepcopy(base), copy.deepcopy(base), copy.deepcopy(base)
+    da = dcp.parallel.DistributedDataParallel(a)
+    db = dcp.parallel.DistributedDataParallel(b, comm_dtype=torch.bfloat16)
+    dc = dcp.parallel.DistributedDataParallel(c)
+    dc.register_comm_hook(None, comm_hooks.allreduce_hook)
+    x = torch.randn(8, 32) * (rank + 1)
+    for d in (da, db, dc):
+        d(x).pow(2).sum().backward()
+    for pa, pb, pc in zip(a.parameters(), b.parameters(), c.parameters()):
+        torch.testing.assert_close(pc.grad, pa.grad)
+        torch.testing.assert_close(pb.grad, pa.grad, rtol=2e-2, atol=2e-2)
+
+
+def test_bf16_wire_compression_and_comm_hook():
+    run_world(_compress, 2)
+
+
+def _ckpt(rank, world, path):
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.models import ConvNet
+
+    torch.manual_seed(0)
+    m = dcp.parallel.DistributedDataParallel(ConvNet())
+    opt = dcp.optim.Adadelta(m.parameters(), lr=1e-3)
+    sch = dcp.optim.StepLR(opt, 1, 0.7)
+    F.nll_loss(m(torch.randn(4, 1, 28, 28)), torch.zeros(4, dtype=torch.long)).backward()
+    opt.step()
+    sch.step()
+    dcp.utils.save_checkpoint(path, m, opt, sch, epoch=3, step=7)
+    dcp.utils.save_model(m, path + ".model")
+    m2 = dcp.parallel.DistributedDataParallel(ConvNet())
+    opt2 = dcp.optim.Adadelta(m2.parameters(), lr=1e-3)
+    sch2 = dcp.optim.StepLR(opt2, 1, 0.7)
+    meta = dcp.utils.load_checkpoint(path, m2, opt2, sch2)
+    assert meta["epoch"] == 3 and meta["step"] == 7
+    for p, q in zip(m.parameters(), m2.parameters()):
+        torch.testing.assert_close(p, q)
+    assert opt2.param_groups[0]["lr"] == pytest.approx(0.7e-3)
+    sd = torch.load(path + ".model", weights_only=True)
+    assert next(iter(sd)).startswith("module.")
+    from distributed_compute_pytorch_amd.models import ConvNet as CN
+    plain = CN()
+    plain.load_state_dict({k[len("module."):]: v for k, v in sd.items()})
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    run_world(_ckpt, 2, str(tmp_path / "ck.pt"))
