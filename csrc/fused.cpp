@@ -5,6 +5,7 @@
 
 #include "common.h"
 #include "kernels/bn_kernels.h"
+#include "kernels/ln_kernels.h"
 
 namespace dcp {
 namespace fused {
@@ -115,7 +116,95 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const at::Tensor& x, co
   return {dx, dweight, dbias, gres};
 }
 
+// ------------------------------------------------------------ LayerNorm ---
+int ln_dtype(const at::Tensor& x) {
+  if (x.scalar_type() == at::kBFloat16) return kern::LN_BF16;
+  if (x.scalar_type() == at::kFloat) return kern::LN_F32;
+  throw Error(str_cat("fused LayerNorm: unsupported dtype ", c10::toString(x.scalar_type())));
+}
+
+bool layer_norm_supported(int64_t D) { return kern::ln_supported(static_cast<int>(D)); }
+
+// x: [..., D] contiguous. Returns (y, mean, rstd) with mean/rstd [rows] fp32.
+std::vector<at::Tensor> layer_norm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
+                                       const c10::optional<at::Tensor>& bias, double eps) {
+  DCP_CHECK(x.is_cuda() && x.is_contiguous(), "layer_norm_fwd: contiguous device tensor required");
+  const int64_t D = x.size(-1);
+  DCP_CHECK(kern::ln_supported(static_cast<int>(D)), "layer_norm_fwd: D must be a multiple of 8 and <= 4096");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t rows = x.numel() / D;
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor y = at::empty_like(x);
+  at::Tensor mean = at::empty({rows}, fopt), rstd = at::empty({rows}, fopt);
+  at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
+  at::Tensor b = bias.has_value() && bias->defined() ? bias->to(at::kFloat).contiguous() : at::Tensor();
+  kern::ln_forward(ln_dtype(x), x.data_ptr(), w.defined() ? w.data_ptr<float>() : nullptr,
+                   b.defined() ? b.data_ptr<float>() : nullptr, y.data_ptr(), mean.data_ptr<float>(),
+                   rstd.data_ptr<float>(), rows, static_cast<int>(D), static_cast<float>(eps), stream_of(x));
+  return {y, mean, rstd};
+}
+
+// Returns (dx, dweight, dbias).
+std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& weight,
+                                       const c10::optional<at::Tensor>& bias, const at::Tensor& mean,
+                                       const at::Tensor& rstd) {
+  c10::hip::HIPGuard guard(x.device().index());
+  at::Tensor g = dy.contiguous();
+  if (g.scalar_type() != x.scalar_type()) g = g.to(x.scalar_type());
+  const int64_t D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dw = at::empty({D}, fopt), db = at::empty({D}, fopt);
+  at::Tensor part = at::empty({static_cast<int64_t>(kern::ln_bwd_blocks(rows)) * 2 * D}, fopt);
+  const bool has_w = weight.has_value() && weight->defined();
+  at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
+  kern::ln_backward(ln_dtype(x), g.data_ptr(), x.data_ptr(), has_w ? w.data_ptr<float>() : nullptr,
+                    mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(),
+                    db.data_ptr<float>(), part.data_ptr<float>(), rows, static_cast<int>(D), stream_of(x));
+  const bool has_b = bias.has_value() && bias->defined();
+  return {dx, has_w ? dw.to(weight->scalar_type()) : at::Tensor(), has_b ? db.to(bias->scalar_type()) : at::Tensor()};
+}
+
+// ------------------------------------------------------- cross-entropy ---
+// logits [rows, V] (row stride may exceed V), target [rows] int64.
+std::vector<at::Tensor> cross_entropy_fwd(const at::Tensor& logits, const at::Tensor& target, int64_t ignore_index,
+                                          double label_smoothing) {
+  DCP_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "cross_entropy_fwd: [rows, V] row-major");
+  DCP_CHECK(target.scalar_type() == at::kLong, "cross_entropy_fwd: int64 targets");
+  c10::hip::HIPGuard guard(logits.device().index());
+  const int64_t rows = logits.size(0);
+  at::Tensor tg = target.contiguous();
+  auto fopt = logits.options().dtype(at::kFloat);
+  at::Tensor loss = at::empty({rows}, fopt), lse = at::empty({rows}, fopt);
+  kern::xent_forward(ln_dtype(logits), logits.data_ptr(), logits.stride(0), tg.data_ptr<int64_t>(), rows,
+                     static_cast<int>(logits.size(1)), ignore_index, static_cast<float>(label_smoothing),
+                     loss.data_ptr<float>(), lse.data_ptr<float>(), stream_of(logits));
+  return {loss, lse};
+}
+
+// dloss: [rows] fp32 or a 1-element fp32 tensor broadcast to every row.
+at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& target, const at::Tensor& lse,
+                             const at::Tensor& dloss, int64_t ignore_index, double label_smoothing) {
+  c10::hip::HIPGuard guard(logits.device().index());
+  const int64_t rows = logits.size(0);
+  at::Tensor tg = target.contiguous();
+  at::Tensor dl = dloss.to(at::kFloat).contiguous();
+  const int stride = dl.numel() == 1 ? 0 : 1;
+  DCP_CHECK(stride == 0 || dl.numel() == rows, "cross_entropy_bwd: dloss must be [rows] or scalar");
+  at::Tensor d = at::empty({rows, logits.size(1)}, logits.options());
+  kern::xent_backward(ln_dtype(logits), logits.data_ptr(), logits.stride(0), tg.data_ptr<int64_t>(),
+                      lse.data_ptr<float>(), dl.data_ptr<float>(), stride, rows, static_cast<int>(logits.size(1)),
+                      ignore_index, static_cast<float>(label_smoothing), d.data_ptr(), d.stride(0), stream_of(logits));
+  return d;
+}
+
 void bind(pybind11::module& m) {
+  m.def("layer_norm_supported", &layer_norm_supported);
+  m.def("layer_norm_fwd", &layer_norm_fwd);
+  m.def("layer_norm_bwd", &layer_norm_bwd);
+  m.def("cross_entropy_fwd", &cross_entropy_fwd);
+  m.def("cross_entropy_bwd", &cross_entropy_bwd);
   m.def("bn_act_fwd", &bn_act_fwd, "fused NHWC BatchNorm(+residual)(+ReLU) forward");
   m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward");
 }

@@ -1,0 +1,293 @@
+// LayerNorm forward/backward for [rows, D] (bf16 / fp32 activations, fp32
+// affine). One wave64 per row, row held in registers (D/512 16-B vectors per
+// lane for bf16), exact two-pass mean/variance from registers — each element
+// is read once from HBM in the forward. Backward: one read of (dy, x) per row
+// for dx, plus per-workgroup partial column sums of dgamma/dbeta (slabs, no
+// float atomics) reduced by a second small kernel.
+//
+// Parity: replaces ATen's layer_norm kernels on the BERT-base / GPT-2-small
+// hot path (SURVEY §2f "LayerNorm fwd/bwd", BASELINE config #3/#5).
+#include <hip/hip_runtime.h>
+
+#include "ln_kernels.h"
+
+namespace dcp {
+namespace kern {
+namespace {
+
+constexpr int kWaves = 4;  // rows per workgroup
+constexpr int kT = 64 * kWaves;
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+template <int D>
+struct L8;
+
+template <>
+struct L8<LN_BF16> {
+  __device__ static void ld(const void* p, int64_t i, float (&o)[8]) {
+    const uint4 v = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + i);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[2 * k] = __uint_as_float(w[k] << 16);
+      o[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  __device__ static void st(void* p, int64_t i, const float (&o)[8]) {
+    uint4 v;
+    v.x = f2bf(o[0]) | (static_cast<uint32_t>(f2bf(o[1])) << 16);
+    v.y = f2bf(o[2]) | (static_cast<uint32_t>(f2bf(o[3])) << 16);
+    v.z = f2bf(o[4]) | (static_cast<uint32_t>(f2bf(o[5])) << 16);
+    v.w = f2bf(o[6]) | (static_cast<uint32_t>(f2bf(o[7])) << 16);
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + i) = v;
+  }
+};
+
+template <>
+struct L8<LN_F32> {
+  __device__ static void ld(const void* p, int64_t i, float (&o)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+    const float4 b = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+    o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+  __device__ static void st(void* p, int64_t i, const float (&o)[8]) {
+    *reinterpret_cast<float4*>(static_cast<float*>(p) + i) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(static_cast<float*>(p) + i + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  }
+};
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// VPL = 16-B vectors per lane (D <= VPL*512).
+template <int DT, int VPL>
+__global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, const float* __restrict__ w,
+                                                    const float* __restrict__ b, void* __restrict__ y,
+                                                    float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                    int64_t rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = D >> 3;
+  const int64_t base = row * D;
+  float v[VPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int vi = lane + j * 64;
+    if (vi < nv) {
+      L8<DT>::ld(x, base + vi * 8, v[j]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[j][k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[j][k] = 0.f;
+    }
+  }
+  const float mean = wsum(s) / static_cast<float>(D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    if (lane + j * 64 < nv) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = v[j][k] - mean;
+        q = fmaf(d, d, q);
+      }
+    }
+  }
+  const float rstd = rsqrtf(wsum(q) / static_cast<float>(D) + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int vi = lane + j * 64;
+    if (vi < nv) {
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = vi * 8 + k;
+        const float xn = (v[j][k] - mean) * rstd;
+        o[k] = w ? fmaf(xn, w[c], b ? b[c] : 0.f) : xn;
+      }
+      L8<DT>::st(y, base + vi * 8, o);
+    }
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
+// partial[blk][0][D] += dy * xhat (dgamma), partial[blk][1][D] += dy (dbeta)
+template <int DT, int VPL>
+__global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy, const void* __restrict__ x,
+                                                    const float* __restrict__ w, const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd, void* __restrict__ dx,
+                                                    float* __restrict__ part, int64_t rows, int D,
+                                                    int rows_per_blk) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // [kWaves][2][D]
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nv = D >> 3;
+  float accg[VPL][8], accb[VPL][8];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) accg[j][k] = accb[j][k] = 0.f;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_blk;
+  const int64_t r1 = min(rows, r0 + rows_per_blk);
+  for (int64_t row = r0 + wid; row < r1; row += kWaves) {
+    const int64_t base = row * D;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[VPL][8], g[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int vi = lane + j * 64;
+      if (vi < nv) {
+        float dv[8];
+        L8<DT>::ld(dy, base + vi * 8, dv);
+        L8<DT>::ld(x, base + vi * 8, xh[j]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int c = vi * 8 + k;
+          xh[j][k] = (xh[j][k] - mu) * rs;
+          accg[j][k] = fmaf(dv[k], xh[j][k], accg[j][k]);
+          accb[j][k] += dv[k];
+          g[j][k] = w ? dv[k] * w[c] : dv[k];
+          s1 += g[j][k];
+          s2 = fmaf(g[j][k], xh[j][k], s2);
+        }
+      }
+    }
+    const float m1 = wsum(s1) / static_cast<float>(D);
+    const float m2 = wsum(s2) / static_cast<float>(D);
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int vi = lane + j * 64;
+      if (vi < nv) {
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = rs * (g[j][k] - m1 - xh[j][k] * m2);
+        L8<DT>::st(dx, base + vi * 8, o);
+      }
+    }
+  }
+  // reduce the 4 waves' column partials through LDS, one slab per workgroup
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int vi = lane + j * 64;
+    if (vi < nv) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        smem[(wid * 2 + 0) * D + vi * 8 + k] = accg[j][k];
+        smem[(wid * 2 + 1) * D + vi * 8 + k] = accb[j][k];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += kT) {
+    const int which = c / D, col = c % D;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < kWaves; ++q) s += smem[(q * 2 + which) * D + col];
+    part[(static_cast<int64_t>(blockIdx.x) * 2 + which) * D + col] = s;
+  }
+}
+
+__global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int D, float* __restrict__ dw,
+                                       float* __restrict__ db) {
+  constexpr int tpc = 16;
+  const int c = blockIdx.x * (256 / tpc) + threadIdx.x / tpc;
+  const int j = threadIdx.x % tpc;
+  float sg = 0.f, sb = 0.f;
+  if (c < D) {
+    for (int b = j; b < nblk; b += tpc) {
+      sg += part[(static_cast<int64_t>(b) * 2 + 0) * D + c];
+      sb += part[(static_cast<int64_t>(b) * 2 + 1) * D + c];
+    }
+  }
+#pragma unroll
+  for (int off = tpc / 2; off > 0; off >>= 1) {
+    sg += __shfl_xor(sg, off, 64);
+    sb += __shfl_xor(sb, off, 64);
+  }
+  if (c < D && j == 0) {
+    if (dw) dw[c] = sg;
+    if (db) db[c] = sb;
+  }
+}
+
+template <int DT>
+void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w, const float* b, void* y, float* mean,
+                  float* rstd, int64_t rows, int D, float eps) {
+  switch (vpl) {
+    case 1: hipLaunchKernelGGL((ln_fwd_kernel<DT, 1>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps); break;
+    case 2: hipLaunchKernelGGL((ln_fwd_kernel<DT, 2>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps); break;
+    case 4: hipLaunchKernelGGL((ln_fwd_kernel<DT, 4>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps); break;
+    default: hipLaunchKernelGGL((ln_fwd_kernel<DT, 8>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps);
+  }
+}
+
+template <int DT>
+void bwd_dispatch(int vpl, dim3 g, size_t sm, hipStream_t s, const void* dy, const void* x, const float* w,
+                  const float* mean, const float* rstd, void* dx, float* part, int64_t rows, int D, int rpb) {
+#define DCP_LNB(V) \
+  hipLaunchKernelGGL((ln_bwd_kernel<DT, V>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb)
+  switch (vpl) {
+    case 1: DCP_LNB(1); break;
+    case 2: DCP_LNB(2); break;
+    case 4: DCP_LNB(4); break;
+    default: DCP_LNB(8);
+  }
+#undef DCP_LNB
+}
+
+inline int vpl_for(int D) {
+  const int nv = D / 8;
+  const int v = (nv + 63) / 64;
+  return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : 8;
+}
+
+}  // namespace
+
+bool ln_supported(int D) { return D % 8 == 0 && D <= 4096; }
+
+int ln_bwd_blocks(int64_t rows) {
+  int64_t nb = (rows + 15) / 16;  // >= 16 rows (4 per wave) per workgroup
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  return static_cast<int>(nb);
+}
+
+void ln_forward(int dtype, const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                int64_t rows, int D, float eps, hipStream_t s) {
+  const dim3 g(static_cast<unsigned>((rows + kWaves - 1) / kWaves));
+  const int vpl = vpl_for(D);
+  if (dtype == LN_BF16) fwd_dispatch<LN_BF16>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
+  else fwd_dispatch<LN_F32>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
+}
+
+void ln_backward(int dtype, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
+                 void* dx, float* dw, float* db, float* part, int64_t rows, int D, hipStream_t s) {
+  const int nblk = ln_bwd_blocks(rows);
+  const int rpb = static_cast<int>((rows + nblk - 1) / nblk);
+  const size_t sm = sizeof(float) * kWaves * 2 * D;
+  const int vpl = vpl_for(D);
+  if (dtype == LN_BF16) bwd_dispatch<LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
+  else bwd_dispatch<LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, part, nblk, D, dw, db);
+}
+
+}  // namespace kern
+}  // namespace dcp

@@ -1,0 +1,33 @@
+// Launch API of the LayerNorm kernels (layernorm.hip) and the fused
+// softmax-cross-entropy kernels (xent.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dcp {
+namespace kern {
+
+enum LnDType : int { LN_F32 = 0, LN_BF16 = 1 };
+
+bool ln_supported(int D);
+int ln_bwd_blocks(int64_t rows);
+void ln_forward(int dtype, const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                int64_t rows, int D, float eps, hipStream_t s);
+// part: workspace [ln_bwd_blocks(rows) * 2 * D] fp32
+void ln_backward(int dtype, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
+                 void* dx, float* dw, float* db, float* part, int64_t rows, int D, hipStream_t s);
+
+// Cross-entropy over [rows, V] logits (bf16/fp32, row stride ld elements).
+// Forward: loss[row] = lse - logit[target] (0 for ignore_index), lse saved.
+void xent_forward(int dtype, const void* logits, int64_t ld, const int64_t* target, int64_t rows, int V,
+                  int64_t ignore_index, float label_smoothing, float* loss, float* lse, hipStream_t s);
+// Backward: dlogits = (softmax - onehot(smoothed)) * dloss[row * dloss_stride]
+// (dloss_stride 0 = one device scalar for every row, e.g. grad/count for 'mean').
+void xent_backward(int dtype, const void* logits, int64_t ld, const int64_t* target, const float* lse,
+                   const float* dloss, int dloss_stride, int64_t rows, int V, int64_t ignore_index,
+                   float label_smoothing, void* dlogits, int64_t ld_out, hipStream_t s);
+
+}  // namespace kern
+}  // namespace dcp

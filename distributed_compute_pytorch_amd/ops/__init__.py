@@ -1,4 +1,6 @@
 """Hand-written gfx950 ops exposed as torch modules / autograd functions."""
 from .batchnorm import BatchNormAct2d, bn_act
+from .layernorm import FusedLayerNorm, fused_layer_norm
+from .cross_entropy import fused_cross_entropy
 
-__all__ = ["BatchNormAct2d", "bn_act"]
+__all__ = ["BatchNormAct2d", "bn_act", "FusedLayerNorm", "fused_layer_norm", "fused_cross_entropy"]

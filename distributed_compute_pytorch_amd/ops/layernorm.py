@@ -1,0 +1,45 @@
+"""Fused LayerNorm (gfx950 HIP kernels, csrc/kernels/layernorm.hip).
+
+``FusedLayerNorm`` is an ``nn.LayerNorm`` subclass (same parameters /
+state_dict keys). On a GPU with a supported shape (last dim a multiple of 8,
+≤ 4096, contiguous) it runs the hand-written kernels; under bf16 autocast the
+activation stays bf16 (statistics and affine in fp32 registers) instead of
+autocast's fp32 upcast of layer_norm. Elsewhere it is ``F.layer_norm``.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+from .._ext import C as _C
+
+
+class _LNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        y, mean, rstd = _C.layer_norm_fwd(x, weight, bias, eps)
+        ctx.save_for_backward(x, weight, bias, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        dx, dw, db = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd)
+        return dx, dw, db, None
+
+
+def fused_layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
+    D = x.shape[-1]
+    if x.is_cuda and len(normalized_shape) == 1 and _C.layer_norm_supported(D) and x.dtype in (torch.float32,
+                                                                                             torch.bfloat16):
+        if torch.is_autocast_enabled() and x.dtype == torch.float32:
+            x = x.to(torch.get_autocast_dtype("cuda"))
+        with torch.autocast("cuda", enabled=False):
+            return _LNFn.apply(x.contiguous(), weight, bias, eps)
+    return F.layer_norm(x, normalized_shape, weight, bias, eps)
+
+
+class FusedLayerNorm(nn.LayerNorm):
+    def forward(self, x):
+        return fused_layer_norm(x, self.normalized_shape, self.weight, self.bias, self.eps)

@@ -70,6 +70,7 @@ def test_resnet50_bf16_step_matches_stock(pg, cuda):
     ref = resnet50(num_classes=100).to(cuda).to(memory_format=torch.channels_last)
     model = resnet50(num_classes=100, fused_bn=True).to(cuda).to(memory_format=torch.channels_last)
     model.load_state_dict(ref.state_dict())
+    init = {n: p.detach().clone() for n, p in ref.named_parameters()}
     ddp = dcp.parallel.DistributedDataParallel(model, device_ids=[0], gradient_as_bucket_view=True)
     o_ref = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9)
     opt = dcp.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9)
@@ -89,7 +90,11 @@ def test_resnet50_bf16_step_matches_stock(pg, cuda):
     assert l_ours[-1] < l_ours[0]
     for a, b in zip(l_ref, l_ours):
         assert abs(a - b) < 0.05 * max(1.0, abs(a)), (l_ref, l_ours)
-    for (n, p), q in zip(ref.named_parameters(), model.parameters()):
-        torch.testing.assert_close(q.float(), p.float(), rtol=0.1, atol=2e-2, msg=n)
+    # compare the parameter UPDATES (bf16 grads differ in rounding between the
+    # two BN implementations, so compare relative update error, not raw values)
+    for (n, p), q, p0 in zip(ref.named_parameters(), model.parameters(), init.values()):
+        du_ref, du_ours = (p.detach() - p0).float(), (q.detach() - p0).float()
+        rel = (du_ours - du_ref).norm() / du_ref.norm().clamp_min(1e-12)
+        assert rel < 0.25, (n, float(rel))
     info = ddp.ddp_logging_data()
     assert info["rebuilds"] == 1 and sum(info["bucket_sizes"]) == sum(p.numel() * 4 for p in model.parameters())
