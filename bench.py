@@ -6,14 +6,16 @@ MI355X; scaling efficiency" on "ResNet-50 DDP bf16 ... synthetic ImageNet
 224×224 batches". One process per GPU (torch.distributed.run or our
 launcher), RCCL over xGMI, weak scaling (fixed per-GPU batch).
 
-A step = zero_grad + forward (bf16 autocast, channels_last) + cross-entropy +
-backward (bucketed RCCL all-reduce overlapped) + fused SGD-momentum update.
-Synthetic data / random-init weights of the full ResNet-50 (25.6 M params).
+A step = zero_grad + forward (bf16 autocast, channels_last) + loss + backward
+(bucketed RCCL all-reduce overlapped with backward) + fused optimizer update.
+Synthetic data / random-init weights of the full-size model.
 
-    python bench.py                       # 1 GPU, defaults
+    python bench.py                                   # ResNet-50, 1 GPU
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
-        --master-port 29500 bench.py --gpus 8 --steps 30 --warmup 10
-    python bench.py --impl torch          # stock torch DDP + torch.optim.SGD baseline
+        --master-port 29500 bench.py --gpus 8
+    python bench.py --impl torch                      # stock torch DDP + torch.optim baseline
+    python bench.py --model gpt2                      # GPT-2-small + grad accumulation (config #5)
+    python bench.py --model bert                      # BERT-base pre-training (config #3)
 """
 from __future__ import annotations
 
@@ -24,9 +26,14 @@ import sys
 import time
 
 import torch
-import torch.nn.functional as F
 
-BASELINE_METRIC = "samples/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency"
+METRICS = {
+    "resnet50": "samples/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency",
+    "bert": "samples/sec (whole node) BERT-base DDP bf16",
+    "gpt2": "samples/sec (whole node) GPT-2-small DDP + grad accumulation bf16",
+    "convnet": "samples/sec (whole node) reference ConvNet DDP",
+    "mlp": "samples/sec (whole node) 2-layer MLP DDP",
+}
 
 
 def log(*a):
@@ -38,10 +45,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--model", default="resnet50", choices=sorted(METRICS))
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU (micro-)batch")
+    ap.add_argument("--seq-len", type=int, default=None)
+    ap.add_argument("--accum", type=int, default=None, help="gradient-accumulation micro-steps")
     ap.add_argument("--impl", choices=["ours", "torch"], default="ours")
-    ap.add_argument("--fused-bn", type=int, default=1)
+    ap.add_argument("--fused", "--fused-bn", dest="fused", type=int, default=1)
     ap.add_argument("--channels-last", type=int, default=1)
     ap.add_argument("--bucket-cap-mb", type=float, default=None)
     ap.add_argument("--first-bucket-mb", type=float, default=None)
@@ -71,15 +80,15 @@ def main():
         os.environ["WORLD_SIZE"] = "1"
 
     import distributed_compute_pytorch_amd as dcp
-    from distributed_compute_pytorch_amd.models import resnet50
+    from distributed_compute_pytorch_amd import workloads
 
-    fused_bn = bool(a.fused_bn) and a.impl == "ours"
+    ours = a.impl == "ours"
+    fused = bool(a.fused) and ours
     torch.manual_seed(0)
-    model = resnet50(fused_bn=fused_bn).to(dev)
-    if a.channels_last:
-        model = model.to(memory_format=torch.channels_last)
+    wl = workloads.build(a.model, dev, batch=a.batch, fused=fused, seq_len=a.seq_len, accum=a.accum,
+                         channels_last=bool(a.channels_last))
 
-    if a.impl == "ours":
+    if ours:
         dcp.distributed.init_process_group("rccl", device_id=local)
         kw = {}
         if a.bucket_cap_mb is not None:
@@ -88,10 +97,10 @@ def main():
             kw["first_bucket_mb"] = a.first_bucket_mb
         if a.comm_dtype == "bf16":
             kw["comm_dtype"] = torch.bfloat16
-        ddp = dcp.parallel.DistributedDataParallel(model, device_ids=[local], gradient_as_bucket_view=bool(
-            a.grad_as_view), **kw)
-        opt = dcp.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-        barrier = lambda: dcp.distributed.barrier()  # noqa: E731
+        ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[local],
+                                                   gradient_as_bucket_view=bool(a.grad_as_view), **kw)
+        opt = wl.make_optimizer(ddp.parameters())
+        barrier = dcp.distributed.barrier
 
         def max_over_ranks(x):
             t = torch.tensor([x], device=dev)
@@ -104,28 +113,19 @@ def main():
         kw = {}
         if a.bucket_cap_mb is not None:
             kw["bucket_cap_mb"] = a.bucket_cap_mb
-        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], **kw)
-        opt = torch.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-        barrier = lambda: tdist.barrier()  # noqa: E731
+        ddp = torch.nn.parallel.DistributedDataParallel(wl.model, device_ids=[local], **kw)
+        ours_opt = wl.make_optimizer([torch.nn.Parameter(torch.zeros(1, device=dev))])
+        cls = getattr(torch.optim, type(ours_opt).__name__)
+        opt = cls(ddp.parameters(), **{k: v for k, v in ours_opt.defaults.items()
+                                       if k not in ("decoupled_weight_decay",)})
+        barrier = tdist.barrier
 
         def max_over_ranks(x):
             t = torch.tensor([x], device=dev)
             tdist.all_reduce(t, tdist.ReduceOp.MAX)
             return float(t.item())
 
-    data = dcp.utils.SyntheticBatches(a.batch, (3, 224, 224), 1000, dev, channels_last=bool(a.channels_last),
-                                      pool=2)
-
-    def step():
-        x, y = next(data)
-        opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = ddp(x)
-            loss = F.cross_entropy(out, y)
-        loss.backward()
-        opt.step()
-        return loss
-
+    step = workloads.make_step(wl, ddp, opt)
     t_w = time.time()
     for i in range(a.warmup):
         loss = step()
@@ -141,13 +141,30 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed)
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     ms = elapsed / a.steps * 1000.0
-    total = a.batch * world * a.steps / elapsed
+    samples_per_step = wl.per_gpu_batch * wl.accum * world
+    total = samples_per_step * a.steps / elapsed
     if rank == 0:
+        cfg = {
+            "model": a.model,
+            "global_batch": samples_per_step,
+            "per_gpu_batch": wl.per_gpu_batch,
+            "grad_accum": wl.accum,
+            "seq_len": wl.seq_len,
+            "parallelism": f"dp{world}",
+            "impl": a.impl,
+            "fused_kernels": fused,
+            "optimizer": type(opt).__name__,
+            "comm_dtype": a.comm_dtype,
+        }
+        if a.model == "resnet50":
+            cfg.update(image_size=224, channels_last=bool(a.channels_last))
+        if ours:
+            info = ddp.ddp_logging_data()
+            cfg["buckets_mb"] = [round(b / 2**20, 2) for b in info["bucket_sizes"]]
         rec = {
-            "metric": BASELINE_METRIC,
+            "metric": METRICS[a.model],
             "value": round(total, 2),
             "unit": "samples/s",
             "n_gpus": world,
@@ -157,31 +174,18 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (on-device random 224x224 images, random labels); random-init weights",
-            "config": {
-                "model": "resnet50",
-                "global_batch": a.batch * world,
-                "per_gpu_batch": a.batch,
-                "seq_len": None,
-                "image_size": 224,
-                "parallelism": f"dp{world}",
-                "impl": a.impl,
-                "fused_bn": fused_bn,
-                "channels_last": bool(a.channels_last),
-                "optimizer": "SGD(momentum=0.9, wd=1e-4)",
-                "comm_dtype": a.comm_dtype,
-            },
+            "dtype": "bf16" if wl.amp else "fp32",
+            "data": "synthetic (on-device random inputs/labels); random-init weights",
+            "config": cfg,
         }
-        if a.impl == "ours":
-            info = ddp.ddp_logging_data()
-            rec["config"]["buckets_mb"] = [round(b / 2**20, 2) for b in info["bucket_sizes"]]
+        if wl.seq_len:
+            rec["tokens_per_s"] = round(total * wl.seq_len, 1)
         line = json.dumps(rec)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    if a.impl == "ours":
+    if ours:
         dcp.distributed.destroy_process_group()
     else:
         import torch.distributed as tdist

@@ -389,3 +389,7 @@ def all_gather_object(object_list, obj, group=None):
     pg.store.set(f"{base}/{pg.rank()}", pickle.dumps(obj))
     for r in range(pg.size()):
         object_list[r] = pickle.loads(pg.store.get(f"{base}/{r}"))
+
+
+from . import launch  # noqa: E402,F401  (spawn / launch_env / free_port)
+from .launch import spawn  # noqa: E402,F401

@@ -1,0 +1,146 @@
+"""BERT-base (110 M) pre-training model — BASELINE config #3.
+
+12 layers, hidden 768, 12 heads, FFN 3072, max 512 positions, vocab 30522,
+GELU(erf), post-LN; heads: masked-LM (transform + tied decoder) and
+next-sentence prediction. Random init (std 0.02).
+
+MI355X path: every LayerNorm is the hand-written kernel; the MLM head runs
+only on the masked positions (gathered first: ~15 % of tokens), and its
+vocab cross-entropy is the fused kernel on bf16 logits; attention is
+``scaled_dot_product_attention``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+from ..ops.cross_entropy import fused_cross_entropy
+from ..ops.layernorm import FusedLayerNorm
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_position: int = 512
+    type_vocab: int = 2
+    dropout: float = 0.1
+    eps: float = 1e-12
+    fused: bool = True
+
+
+def _ln(cfg, d):
+    return FusedLayerNorm(d, eps=cfg.eps) if cfg.fused else nn.LayerNorm(d, eps=cfg.eps)
+
+
+class BertSelfAttention(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.heads = cfg.heads
+        self.query = nn.Linear(cfg.hidden, cfg.hidden)
+        self.key = nn.Linear(cfg.hidden, cfg.hidden)
+        self.value = nn.Linear(cfg.hidden, cfg.hidden)
+        self.dropout = cfg.dropout
+
+    def forward(self, x, mask):
+        B, T, C = x.shape
+        h = self.heads
+
+        def split(t):
+            return t.view(B, T, h, C // h).transpose(1, 2)
+
+        y = F.scaled_dot_product_attention(split(self.query(x)), split(self.key(x)), split(self.value(x)),
+                                           attn_mask=mask, dropout_p=self.dropout if self.training else 0.0)
+        return y.transpose(1, 2).reshape(B, T, C)
+
+
+class BertLayer(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.attention = BertSelfAttention(cfg)
+        self.attn_out = nn.Linear(cfg.hidden, cfg.hidden)
+        self.attn_ln = _ln(cfg, cfg.hidden)
+        self.intermediate = nn.Linear(cfg.hidden, cfg.intermediate)
+        self.output = nn.Linear(cfg.intermediate, cfg.hidden)
+        self.out_ln = _ln(cfg, cfg.hidden)
+        self.drop = nn.Dropout(cfg.dropout)
+
+    def forward(self, x, mask):
+        x = self.attn_ln(x + self.drop(self.attn_out(self.attention(x, mask))))
+        return self.out_ln(x + self.drop(self.output(F.gelu(self.intermediate(x)))))
+
+
+class BertForPreTraining(nn.Module):
+    def __init__(self, cfg: BertConfig = BertConfig()):
+        super().__init__()
+        self.cfg = cfg
+        self.word_embeddings = nn.Embedding(cfg.vocab_size, cfg.hidden)
+        self.position_embeddings = nn.Embedding(cfg.max_position, cfg.hidden)
+        self.token_type_embeddings = nn.Embedding(cfg.type_vocab, cfg.hidden)
+        self.emb_ln = _ln(cfg, cfg.hidden)
+        self.emb_drop = nn.Dropout(cfg.dropout)
+        self.layers = nn.ModuleList([BertLayer(cfg) for _ in range(cfg.layers)])
+        self.pooler = nn.Linear(cfg.hidden, cfg.hidden)
+        self.mlm_transform = nn.Linear(cfg.hidden, cfg.hidden)
+        self.mlm_ln = _ln(cfg, cfg.hidden)
+        self.mlm_bias = nn.Parameter(torch.zeros(cfg.vocab_size))
+        self.nsp = nn.Linear(cfg.hidden, 2)
+        self.apply(self._init)
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, (nn.Linear, nn.Embedding)):
+            nn.init.normal_(m.weight, 0.0, 0.02)
+        if isinstance(m, nn.Linear) and m.bias is not None:
+            nn.init.zeros_(m.bias)
+
+    def forward(self, input_ids, token_type_ids=None, attention_mask=None, mlm_labels=None, nsp_labels=None,
+                mlm_positions=None):
+        """``mlm_labels``: either [B, T] with -100 for unmasked tokens, or — with
+        ``mlm_positions`` [B, P] (fixed predictions per sequence, no host sync) —
+        the [B, P] label ids of those positions."""
+        B, T = input_ids.shape
+        pos = torch.arange(T, device=input_ids.device)
+        if token_type_ids is None:
+            token_type_ids = torch.zeros_like(input_ids)
+        x = self.word_embeddings(input_ids) + self.position_embeddings(pos) + self.token_type_embeddings(
+            token_type_ids)
+        x = self.emb_drop(self.emb_ln(x))
+        mask = None
+        if attention_mask is not None:
+            mask = attention_mask[:, None, None, :].to(torch.bool)
+        for layer in self.layers:
+            x = layer(x, mask)
+        pooled = torch.tanh(self.pooler(x[:, 0]))
+        nsp_logits = self.nsp(pooled)
+        if mlm_labels is None:
+            return x, nsp_logits
+        # MLM head on masked positions only
+        if mlm_positions is not None:
+            sel = (mlm_positions + torch.arange(B, device=x.device)[:, None] * T).reshape(-1)
+            tgt = mlm_labels.reshape(-1)
+        else:
+            flat_labels = mlm_labels.reshape(-1)
+            sel = (flat_labels != -100).nonzero(as_tuple=True)[0]  # host sync: prefer mlm_positions
+            tgt = flat_labels.index_select(0, sel)
+        h = x.reshape(B * T, -1).index_select(0, sel)
+        h = self.mlm_ln(F.gelu(self.mlm_transform(h)))
+        logits = F.linear(h, self.word_embeddings.weight, self.mlm_bias)
+        if self.cfg.fused:
+            mlm = fused_cross_entropy(logits, tgt)
+        else:
+            mlm = F.cross_entropy(logits.float(), tgt)
+        loss = mlm
+        if nsp_labels is not None:
+            loss = loss + F.cross_entropy(nsp_logits.float(), nsp_labels)
+        return loss
+
+
+def bert_base(**kw) -> BertForPreTraining:
+    return BertForPreTraining(BertConfig(**kw))

@@ -1,0 +1,127 @@
+"""GPT-2 small (124 M) — BASELINE config #5 (DDP + gradient accumulation + bf16 AMP).
+
+12 layers, d_model 768, 12 heads, context 1024, vocab 50257, GELU(tanh), pre-LN,
+tied LM head. Random init (std 0.02, residual projections scaled by
+1/sqrt(2·n_layer)). Parameter names follow the common GPT-2 layout
+(wte, wpe, h.N.ln_1, h.N.attn.c_attn, ...).
+
+MI355X path: LayerNorm = hand-written kernel (bf16 activations, fp32 stats),
+attention = ``scaled_dot_product_attention`` (flash kernels of PyTorch-ROCm),
+loss = fused vocab cross-entropy straight from bf16 logits.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+from ..ops.cross_entropy import fused_cross_entropy
+from ..ops.layernorm import FusedLayerNorm
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    n_embd: int = 768
+    n_layer: int = 12
+    n_head: int = 12
+    dropout: float = 0.1
+    fused: bool = True
+
+
+class CausalSelfAttention(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.n_head = cfg.n_head
+        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+        self.dropout = cfg.dropout
+        self.resid_drop = nn.Dropout(cfg.dropout)
+
+    def forward(self, x):
+        B, T, C = x.shape
+        q, k, v = self.c_attn(x).split(C, dim=2)
+        h = self.n_head
+        q = q.view(B, T, h, C // h).transpose(1, 2)
+        k = k.view(B, T, h, C // h).transpose(1, 2)
+        v = v.view(B, T, h, C // h).transpose(1, 2)
+        y = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0, is_causal=True)
+        y = y.transpose(1, 2).contiguous().view(B, T, C)
+        return self.resid_drop(self.c_proj(y))
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+        self.drop = nn.Dropout(cfg.dropout)
+
+    def forward(self, x):
+        return self.drop(self.c_proj(F.gelu(self.c_fc(x), approximate="tanh")))
+
+
+def _ln(cfg, d):
+    return FusedLayerNorm(d) if cfg.fused else nn.LayerNorm(d)
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.ln_1 = _ln(cfg, cfg.n_embd)
+        self.attn = CausalSelfAttention(cfg)
+        self.ln_2 = _ln(cfg, cfg.n_embd)
+        self.mlp = MLP(cfg)
+
+    def forward(self, x):
+        x = x + self.attn(self.ln_1(x))
+        return x + self.mlp(self.ln_2(x))
+
+
+class GPT2(nn.Module):
+    def __init__(self, cfg: GPT2Config = GPT2Config()):
+        super().__init__()
+        self.cfg = cfg
+        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+        self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
+        self.drop = nn.Dropout(cfg.dropout)
+        self.h = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
+        self.ln_f = _ln(cfg, cfg.n_embd)
+        self.apply(self._init)
+        for n, p in self.named_parameters():
+            if n.endswith("c_proj.weight"):
+                nn.init.normal_(p, 0.0, 0.02 / math.sqrt(2 * cfg.n_layer))
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, 0.0, 0.02)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, 0.0, 0.02)
+
+    def forward(self, idx, targets=None):
+        B, T = idx.shape
+        pos = torch.arange(T, device=idx.device)
+        x = self.drop(self.wte(idx) + self.wpe(pos))
+        for blk in self.h:
+            x = blk(x)
+        x = self.ln_f(x)
+        logits = F.linear(x, self.wte.weight)  # tied head
+        if targets is None:
+            return logits
+        flat = logits.view(B * T, -1)
+        if self.cfg.fused:
+            loss = fused_cross_entropy(flat, targets.reshape(-1))
+        else:
+            loss = F.cross_entropy(flat.float(), targets.reshape(-1))
+        return loss
+
+
+def gpt2_small(**kw) -> GPT2:
+    return GPT2(GPT2Config(**kw))
