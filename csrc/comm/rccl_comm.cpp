@@ -135,6 +135,7 @@ class RcclCommunicator : public Communicator {
     check_tensor(t);
     account("all_reduce", t, static_cast<int>(op));
     return launch({t}, [&](hipStream_t s) {
+      if (size_ == 1) return;  // identity for every op on one rank (in place)
       NCCL_OK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
                             to_nccl(op, t.scalar_type()), comm_, s));
     });
@@ -144,6 +145,7 @@ class RcclCommunicator : public Communicator {
     check_tensor(t);
     account("broadcast", t, root);
     return launch({t}, [&](hipStream_t s) {
+      if (size_ == 1) return;
       NCCL_OK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, s));
     });
   }

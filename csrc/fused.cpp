@@ -24,7 +24,7 @@ void check_nhwc(const at::Tensor& x, const char* what) {
   DCP_CHECK(x.is_cuda(), what, ": device tensor required");
   DCP_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), what,
             ": expected a channels_last 4-D tensor");
-  DCP_CHECK(x.size(1) % 8 == 0, what, ": channel count must be a multiple of 8");
+  DCP_CHECK(kern::bn_supported(static_cast<int>(x.size(1))), what, ": unsupported channel count ", x.size(1));
   DCP_CHECK(x.numel() / 8 < (int64_t(1) << 32), what, ": tensor too large");
 }
 
@@ -57,27 +57,24 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
   at::Tensor b = bias.has_value() && bias->defined() ? bias->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor mean = at::empty({C}, fopt);
   at::Tensor invstd = at::empty({C}, fopt);
-  at::Tensor scale = at::empty({C}, fopt);
-  at::Tensor shift = at::empty({C}, fopt);
   auto s = stream_of(x);
   if (training) {
-    const int nblk = kern::bn_partial_blocks(M, static_cast<int>(C));
-    at::Tensor part = at::empty({nblk * 2 * C}, fopt);
+    at::Tensor acc = at::empty({2 * C}, fopt);
     float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
     float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
     kern::bn_forward_train(bn_dtype(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, y.data_ptr(), M,
                            static_cast<int>(C), w.defined() ? w.data_ptr<float>() : nullptr,
                            b.defined() ? b.data_ptr<float>() : nullptr, rm, rv, static_cast<float>(momentum),
                            static_cast<float>(eps), mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                           scale.data_ptr<float>(), shift.data_ptr<float>(), part.data_ptr<float>(), act, s);
+                           acc.data_ptr<float>(), act, s);
   } else {
     DCP_CHECK(running_mean.has_value() && running_var.has_value(), "bn_act_fwd: eval mode needs running stats");
     mean.copy_(*running_mean);
     invstd.copy_(at::rsqrt(*running_var + eps));
     at::Tensor g = w.defined() ? w : at::ones({C}, fopt);
     at::Tensor bb = b.defined() ? b : at::zeros({C}, fopt);
-    scale.copy_(g * invstd);
-    shift.copy_(bb - mean * scale);
+    at::Tensor scale = g * invstd;
+    at::Tensor shift = bb - mean * scale;
     kern::bn_apply(bn_dtype(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, y.data_ptr(), M,
                    static_cast<int>(C), scale.data_ptr<float>(), shift.data_ptr<float>(), act, s);
   }
@@ -102,14 +99,11 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const at::Tensor& x, co
   at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor dw = at::empty({C}, fopt);
   at::Tensor db = at::empty({C}, fopt);
-  at::Tensor k = at::empty({3 * C}, fopt);
-  const int nblk = kern::bn_partial_blocks(M, static_cast<int>(C));
-  at::Tensor part = at::empty({nblk * 2 * C}, fopt);
+  at::Tensor acc = at::empty({2 * C}, fopt);
   kern::bn_backward(bn_dtype(x), g.data_ptr(), y.data_ptr(), x.data_ptr(), M, static_cast<int>(C),
                     has_w ? w.data_ptr<float>() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(), act,
                     has_res, has_res ? gres.data_ptr() : nullptr, dx.data_ptr(), dw.data_ptr<float>(),
-                    db.data_ptr<float>(), k.data_ptr<float>(), k.data_ptr<float>() + C, k.data_ptr<float>() + 2 * C,
-                    part.data_ptr<float>(), training, stream_of(x));
+                    db.data_ptr<float>(), acc.data_ptr<float>(), training, stream_of(x));
   at::Tensor dweight = has_w ? dw.to(weight->scalar_type()) : at::Tensor();
   const bool has_b = bias.has_value() && bias->defined();
   at::Tensor dbias = has_b ? db.to(bias->scalar_type()) : at::Tensor();
@@ -200,6 +194,7 @@ at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& target,
 }
 
 void bind(pybind11::module& m) {
+  m.def("bn_supported", [](int64_t C) { return kern::bn_supported(static_cast<int>(C)); });
   m.def("layer_norm_supported", &layer_norm_supported);
   m.def("layer_norm_fwd", &layer_norm_fwd);
   m.def("layer_norm_bwd", &layer_norm_bwd);

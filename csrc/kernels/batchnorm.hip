@@ -16,8 +16,10 @@
 //                       apply pass (write dx).
 // vs the ATen composition BN → add → ReLU this removes the separate add and
 // ReLU passes (3-4 full activation round trips per bottleneck BN) and 2-4
-// launches per layer. Partial-sum slabs, not float atomics (guide G12), so
-// results are bitwise reproducible.
+// launches per layer. Per-workgroup column sums are combined with fp32
+// atomics into a [2][C] accumulator (2C adds per workgroup), and the apply
+// kernels derive the per-channel coefficients in their prologue, so there is
+// no separate finalize launch.
 //
 // Parity: replaces cuDNN/MIOpen batch-norm + ATen relu/add kernels of the
 // ResNet-50 configs (SURVEY §2f P1 "BN2d fwd/bwd + ReLU fused").
@@ -96,17 +98,17 @@ __device__ __forceinline__ Geo geo(int C) {
   return g;
 }
 
-// Reduce acc[2][8] across the `rpi` row groups of the workgroup and write the
-// partial slab part[blk][0/1][C].
-__device__ __forceinline__ void block_reduce_store(float (&a)[kV], float (&b)[kV], const Geo& g, int chunk0,
-                                                   int C, float* part, int64_t blk, int nblk, float* smem) {
+// Reduce a[8], b[8] across the `rpi` row groups of the workgroup through LDS
+// and add the block's column sums into acc[0][C] / acc[1][C] with fp32
+// atomics (2C atomic adds per workgroup: a few hundred KB per launch, far
+// below the ≈1.3 TB/s atomic rate, and it removes the partial-slab finalize).
+__device__ __forceinline__ void block_reduce_atomic(float (&a)[kV], float (&b)[kV], const Geo& g, int chunk0, int C,
+                                                    float* acc, float* smem) {
   const int t = threadIdx.x;
-  const int lane_c = t % g.tpr;   // channel vector within chunk
-  const int grp = t / g.tpr;      // row group
-  const bool active = grp < g.rpi;
-  // smem layout: [2][rpi][tpr*8]
+  const int lane_c = t % g.tpr;
+  const int grp = t / g.tpr;
   const int W = g.tpr * kV;
-  if (active) {
+  if (grp < g.rpi) {
 #pragma unroll
     for (int k = 0; k < kV; ++k) {
       smem[(0 * g.rpi + grp) * W + lane_c * kV + k] = a[k];
@@ -114,26 +116,23 @@ __device__ __forceinline__ void block_reduce_store(float (&a)[kV], float (&b)[kV
     }
   }
   __syncthreads();
-  // each thread finalises some of the 2*W column sums
   for (int col = t; col < 2 * W; col += kT) {
     const int which = col / W;
     const int cc = col % W;
     float s = 0.f;
     for (int r = 0; r < g.rpi; ++r) s += smem[(which * g.rpi + r) * W + cc];
     const int c = chunk0 * kV + cc;
-    if (c < C) part[(static_cast<int64_t>(blk) * 2 + which) * C + c] = s;
+    if (c < C) atomicAdd(acc + which * C + c, s);
   }
-  __syncthreads();
-  (void)nblk;
 }
 
 // ------------------------------------------------------------- stats ----
+// acc[0][c] += Σ (x - x[row0][c]), acc[1][c] += Σ (x - x[row0][c])²
 template <int D>
 __global__ void __launch_bounds__(kT) bn_stats_kernel(const void* __restrict__ x, int64_t M, int C,
-                                                      int64_t rows_per_blk, float* __restrict__ part) {
+                                                      int64_t rows_per_blk, float* __restrict__ acc) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const Geo g = geo(C);
-  const int nchunks = (g.cv + g.tpr - 1) / g.tpr;
   const int chunk = blockIdx.y;
   const int lane_c = threadIdx.x % g.tpr;
   const int grp = threadIdx.x / g.tpr;
@@ -144,9 +143,22 @@ __global__ void __launch_bounds__(kT) bn_stats_kernel(const void* __restrict__ x
   float s[kV], q[kV], sh[kV];
 #pragma unroll
   for (int k = 0; k < kV; ++k) s[k] = q[k] = 0.f;
-  if (cv_ok) V8<D>::ld(x, static_cast<int64_t>(cvec) * kV, sh);  // shift = row 0
   if (cv_ok) {
-    for (int64_t r = r0 + grp; r < r1; r += g.rpi) {
+    V8<D>::ld(x, static_cast<int64_t>(cvec) * kV, sh);  // shift = row 0
+    int64_t r = r0 + grp;
+    // two rows in flight per iteration
+    for (; r + g.rpi < r1; r += 2 * g.rpi) {
+      float v[kV], w[kV];
+      V8<D>::ld(x, r * C + cvec * kV, v);
+      V8<D>::ld(x, (r + g.rpi) * C + cvec * kV, w);
+#pragma unroll
+      for (int k = 0; k < kV; ++k) {
+        const float d = v[k] - sh[k], e = w[k] - sh[k];
+        s[k] += d + e;
+        q[k] = fmaf(d, d, fmaf(e, e, q[k]));
+      }
+    }
+    if (r < r1) {
       float v[kV];
       V8<D>::ld(x, r * C + cvec * kV, v);
 #pragma unroll
@@ -157,83 +169,74 @@ __global__ void __launch_bounds__(kT) bn_stats_kernel(const void* __restrict__ x
       }
     }
   }
-  (void)nchunks;
-  // partial slab index includes the chunk dimension through the channel offset
-  block_reduce_store(s, q, g, chunk * g.tpr, C, part, blockIdx.x, gridDim.x, smem);
+  block_reduce_atomic(s, q, g, chunk * g.tpr, C, acc, smem);
 }
 
-// one thread per channel: fold partials -> mean/invstd/scale/shift, running stats
+// Per-channel statistics from the accumulators (used by every apply thread
+// for its own 8 channels, and by the first thread group to publish
+// mean/invstd and update the running statistics).
 template <int D>
-__global__ void bn_stats_finalize_kernel(const float* __restrict__ part, int nblk, const void* __restrict__ x,
-                                         int64_t M, int C, const float* __restrict__ gamma,
-                                         const float* __restrict__ beta, float* __restrict__ mean_out,
-                                         float* __restrict__ invstd_out, float* __restrict__ scale,
-                                         float* __restrict__ shift, float* running_mean, float* running_var,
-                                         float momentum, float eps) {
-  // block = 256 threads = 4 waves handling 64 channels? -> simple: blockDim.x threads cooperate on
-  // `cpb` channels with `tpc` threads each.
-  constexpr int tpc = 16;
-  const int cpb = kT / tpc;
-  const int c = blockIdx.x * cpb + threadIdx.x / tpc;
-  const int j = threadIdx.x % tpc;
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int b = j; b < nblk; b += tpc) {
-      s += part[(static_cast<int64_t>(b) * 2 + 0) * C + c];
-      q += part[(static_cast<int64_t>(b) * 2 + 1) * C + c];
-    }
-  }
-#pragma unroll
-  for (int off = tpc / 2; off > 0; off >>= 1) {
-    s += __shfl_xor(s, off, 64);
-    q += __shfl_xor(q, off, 64);
-  }
-  if (c < C && j == 0) {
-    const float sh = D == BN_BF16 ? bf2f(static_cast<const uint16_t*>(x)[c]) : static_cast<const float*>(x)[c];
-    const double dm = s / static_cast<double>(M);
-    double var = q / static_cast<double>(M) - dm * dm;
-    if (var < 0) var = 0;
-    const float mean = sh + static_cast<float>(dm);
-    const float inv = rsqrtf(static_cast<float>(var) + eps);
-    mean_out[c] = mean;
-    invstd_out[c] = inv;
-    const float gm = gamma ? gamma[c] : 1.f;
-    const float bt = beta ? beta[c] : 0.f;
-    scale[c] = gm * inv;
-    shift[c] = bt - mean * gm * inv;
-    if (running_mean) {
-      const float unb = M > 1 ? static_cast<float>(var * static_cast<double>(M) / static_cast<double>(M - 1))
-                              : static_cast<float>(var);
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
-    }
-  }
+__device__ __forceinline__ void stats_for(const float* acc, const void* x, int64_t M, int C, int c, float eps,
+                                          float* mean, float* var, float* invstd) {
+  const float sh = D == BN_BF16 ? bf2f(static_cast<const uint16_t*>(x)[c]) : static_cast<const float*>(x)[c];
+  const float dm = acc[c] / static_cast<float>(M);
+  float v = acc[C + c] / static_cast<float>(M) - dm * dm;
+  v = v < 0.f ? 0.f : v;
+  *mean = sh + dm;
+  *var = v;
+  *invstd = rsqrtf(v + eps);
 }
 
 // ------------------------------------------------------------- apply ----
-template <int D, bool RES, bool ACT>
+// y = act(x*scale[c] + shift[c] (+ res)). TRAIN: scale/shift derived in the
+// prologue from acc (batch stats); else from the given scale/shift arrays.
+// Thread → channel mapping is constant across the grid-stride loop when
+// (grid*256) % (C/8) == 0 (always true for power-of-two C ≤ 2048), so each
+// thread keeps its 8 scale/shift values in registers.
+template <int D, bool RES, bool ACT, bool TRAIN>
 __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ res,
-                                                      const float* __restrict__ scale, const float* __restrict__ shift,
-                                                      void* __restrict__ y, int64_t nvec, int C) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sc = smem;
-  float* sf = smem + C;
-  for (int c = threadIdx.x; c < C; c += kT) {
-    sc[c] = scale[c];
-    sf[c] = shift[c];
-  }
-  __syncthreads();
+                                                      const float* __restrict__ acc, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, const float* __restrict__ scale_in,
+                                                      const float* __restrict__ shift_in, void* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                                      float* running_mean, float* running_var, float momentum,
+                                                      float eps, int64_t M, int64_t nvec, int C) {
   const int cv = C / kV;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * kT) {
-    const int c0 = static_cast<int>(static_cast<uint32_t>(v) % static_cast<uint32_t>(cv)) * kV;
+  const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
+  const int c0 = static_cast<int>(tid % cv) * kV;
+  float sc[kV], sf[kV];
+#pragma unroll
+  for (int k = 0; k < kV; ++k) {
+    const int c = c0 + k;
+    if (TRAIN) {
+      float mean, var, inv;
+      stats_for<D>(acc, x, M, C, c, eps, &mean, &var, &inv);
+      const float gm = gamma ? gamma[c] : 1.f;
+      sc[k] = gm * inv;
+      sf[k] = (beta ? beta[c] : 0.f) - mean * sc[k];
+      if (tid < cv) {  // one writer per channel
+        mean_out[c] = mean;
+        invstd_out[c] = inv;
+        if (running_mean) {
+          const float unb = M > 1 ? var * (static_cast<float>(M) / static_cast<float>(M - 1)) : var;
+          running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+          running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+        }
+      }
+    } else {
+      sc[k] = scale_in[c];
+      sf[k] = shift_in[c];
+    }
+  }
+  for (int64_t v = tid; v < nvec; v += stride) {
     float a[kV];
     V8<D>::ld(x, v * kV, a);
     float r[kV];
     if (RES) V8<D>::ld(res, v * kV, r);
 #pragma unroll
     for (int k = 0; k < kV; ++k) {
-      float o = fmaf(a[k], sc[c0 + k], sf[c0 + k]);
+      float o = fmaf(a[k], sc[k], sf[k]);
       if (RES) o += r[k];
       if (ACT) o = fmaxf(o, 0.f);
       a[k] = o;
@@ -243,13 +246,13 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
 }
 
 // -------------------------------------------------------- bwd reduce ----
-// g = gy * (y > 0) (ACT) ; sums: dbeta = Σ g, dgamma_raw = Σ g*(x-mean)
+// g = gy * (y > 0) (ACT); acc[0][c] += Σ g, acc[1][c] += Σ g*(x-mean)
 // STORE_G: write g (the gradient of the residual branch) as a side output.
 template <int D, bool ACT, bool STORE_G>
 __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restrict__ gy, const void* __restrict__ y,
                                                            const void* __restrict__ x, const float* __restrict__ mean,
                                                            int64_t M, int C, int64_t rows_per_blk,
-                                                           float* __restrict__ part, void* __restrict__ gout) {
+                                                           float* __restrict__ acc, void* __restrict__ gout) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const Geo g = geo(C);
   const int chunk = blockIdx.y;
@@ -284,70 +287,41 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
       }
     }
   }
-  block_reduce_store(sb, sg, g, chunk * g.tpr, C, part, blockIdx.x, gridDim.x, smem);
-}
-
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int64_t M, int C,
-                                       const float* __restrict__ gamma, const float* __restrict__ invstd,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k1,
-                                       float* __restrict__ k2, float* __restrict__ k3, bool training) {
-  constexpr int tpc = 16;
-  const int cpb = kT / tpc;
-  const int c = blockIdx.x * cpb + threadIdx.x / tpc;
-  const int j = threadIdx.x % tpc;
-  double sb = 0.0, sg = 0.0;
-  if (c < C) {
-    for (int b = j; b < nblk; b += tpc) {
-      sb += part[(static_cast<int64_t>(b) * 2 + 0) * C + c];
-      sg += part[(static_cast<int64_t>(b) * 2 + 1) * C + c];
-    }
-  }
-#pragma unroll
-  for (int off = tpc / 2; off > 0; off >>= 1) {
-    sb += __shfl_xor(sb, off, 64);
-    sg += __shfl_xor(sg, off, 64);
-  }
-  if (c < C && j == 0) {
-    const float inv = invstd[c];
-    const float gm = gamma ? gamma[c] : 1.f;
-    const float db = static_cast<float>(sb);
-    const float dg = static_cast<float>(sg) * inv;  // Σ g * xhat
-    if (dgamma) dgamma[c] = dg;
-    if (dbeta) dbeta[c] = db;
-    k1[c] = gm * inv;
-    if (training) {
-      k2[c] = db / static_cast<float>(M);
-      k3[c] = dg / static_cast<float>(M) * inv;
-    } else {
-      k2[c] = 0.f;
-      k3[c] = 0.f;
-    }
-  }
+  block_reduce_atomic(sb, sg, g, chunk * g.tpr, C, acc, smem);
 }
 
 // dx = k1 * (g - k2 - (x - mean) * k3); g from gout (FROM_G) or gy*(y>0).
+// k1 = gamma*invstd, k2 = Σg/M, k3 = Σg(x-mean)/M * invstd² (training) —
+// derived per thread in the prologue from acc; the first thread group writes
+// dgamma = Σg(x-mean)*invstd and dbeta = Σg.
 template <int D, bool ACT, bool FROM_G>
 __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict__ gsrc, const void* __restrict__ y,
                                                           const void* __restrict__ x, const float* __restrict__ mean,
-                                                          const float* __restrict__ k1, const float* __restrict__ k2,
-                                                          const float* __restrict__ k3, void* __restrict__ dx,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ gamma, const float* __restrict__ acc,
+                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                          bool training, void* __restrict__ dx, int64_t M,
                                                           int64_t nvec, int C) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* s1 = smem;
-  float* s2 = smem + C;
-  float* s3 = smem + 2 * C;
-  float* sm = smem + 3 * C;
-  for (int c = threadIdx.x; c < C; c += kT) {
-    s1[c] = k1[c];
-    s2[c] = k2[c];
-    s3[c] = k3[c];
-    sm[c] = mean[c];
-  }
-  __syncthreads();
   const int cv = C / kV;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * kT) {
-    const int c0 = static_cast<int>(static_cast<uint32_t>(v) % static_cast<uint32_t>(cv)) * kV;
+  const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
+  const int c0 = static_cast<int>(tid % cv) * kV;
+  float k1[kV], k2[kV], k3[kV], mu[kV];
+#pragma unroll
+  for (int k = 0; k < kV; ++k) {
+    const int c = c0 + k;
+    const float inv = invstd[c];
+    const float sb = acc[c], sg = acc[C + c];
+    mu[k] = mean[c];
+    k1[k] = (gamma ? gamma[c] : 1.f) * inv;
+    k2[k] = training ? sb / static_cast<float>(M) : 0.f;
+    k3[k] = training ? sg / static_cast<float>(M) * inv * inv : 0.f;
+    if (tid < cv) {
+      if (dgamma) dgamma[c] = sg * inv;
+      if (dbeta) dbeta[c] = sb;
+    }
+  }
+  for (int64_t v = tid; v < nvec; v += stride) {
     float gv[kV], xv[kV];
     V8<D>::ld(gsrc, v * kV, gv);
     if (ACT && !FROM_G) {
@@ -358,23 +332,19 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict
     }
     V8<D>::ld(x, v * kV, xv);
 #pragma unroll
-    for (int k = 0; k < kV; ++k) {
-      const int c = c0 + k;
-      gv[k] = s1[c] * (gv[k] - s2[c] - (xv[k] - sm[c]) * s3[c]);
-    }
+    for (int k = 0; k < kV; ++k) gv[k] = k1[k] * (gv[k] - k2[k] - (xv[k] - mu[k]) * k3[k]);
     V8<D>::st(dx, v * kV, gv);
   }
 }
 
-// grid for the reduction kernels
+// grid for the reduction kernels: ~2 workgroups per CU in total
 inline void red_geometry(int64_t M, int C, int* nblk, int64_t* rows_per_blk, int* nchunks) {
   const int cv = C / kV;
   const int tpr = cv < kT ? cv : kT;
   const int rpi = kT / tpr;
   *nchunks = (cv + tpr - 1) / tpr;
-  // aim for >= 16 row iterations per thread and <= ~2048 workgroups total
-  int64_t want = (M + static_cast<int64_t>(rpi) * 16 - 1) / (static_cast<int64_t>(rpi) * 16);
-  const int64_t cap = 2048 / *nchunks;
+  int64_t want = (M + static_cast<int64_t>(rpi) * 8 - 1) / (static_cast<int64_t>(rpi) * 8);  // >= 8 rows/thread
+  const int64_t cap = 512 / *nchunks > 0 ? 512 / *nchunks : 1;
   if (want > cap) want = cap;
   if (want < 1) want = 1;
   int64_t rpb = (M + want - 1) / want;
@@ -383,10 +353,15 @@ inline void red_geometry(int64_t M, int C, int* nblk, int64_t* rows_per_blk, int
   *nblk = static_cast<int>((M + rpb - 1) / rpb);
 }
 
-inline int apply_grid(int64_t nvec) {
-  int64_t g = (nvec + kT * 4 - 1) / (kT * 4);
-  if (g > 4096) g = 4096;
+// apply grid: multiple of nothing special (cv | 256 keeps thread→channel fixed),
+// ≤ 1024 workgroups (4 per CU) so the per-thread prologue stays cheap
+inline int apply_grid(int64_t nvec, int cv) {
+  int64_t g = (nvec + kT * 2 - 1) / (kT * 2);
+  if (g > 1024) g = 1024;
   if (g < 1) g = 1;
+  // the prologue/channel mapping needs (g*256) % cv == 0
+  if ((g * kT) % cv != 0) g = ((g * kT + cv - 1) / cv * cv + kT - 1) / kT;
+  while ((g * kT) % cv != 0) ++g;
   return static_cast<int>(g);
 }
 
@@ -399,42 +374,47 @@ inline size_t red_smem(int C) {
 
 }  // namespace
 
-int bn_partial_blocks(int64_t M, int C) {
-  int nblk, nchunks;
-  int64_t rpb;
-  red_geometry(M, C, &nblk, &rpb, &nchunks);
-  return nblk;
-}
+bool bn_supported(int C) { return C % kV == 0 && (C / kV <= kT ? (kT % (C / kV) == 0) : ((C / kV) % kT == 0)); }
 
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
-                      float* mean, float* invstd, float* scale, float* shift, float* part, bool act,
-                      hipStream_t s) {
+                      float* mean, float* invstd, float* acc, bool act, hipStream_t s) {
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
+  (void)hipMemsetAsync(acc, 0, sizeof(float) * 2 * C, s);
   const size_t sm = red_smem(C);
   if (dtype == BN_BF16)
-    hipLaunchKernelGGL(bn_stats_kernel<BN_BF16>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, part);
+    hipLaunchKernelGGL(bn_stats_kernel<BN_BF16>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
   else
-    hipLaunchKernelGGL(bn_stats_kernel<BN_F32>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, part);
-  const int fin_blocks = (C + 15) / 16;
-  if (dtype == BN_BF16)
-    hipLaunchKernelGGL(bn_stats_finalize_kernel<BN_BF16>, dim3(fin_blocks), dim3(kT), 0, s, part, nblk, x, M, C,
-                       gamma, beta, mean, invstd, scale, shift, running_mean, running_var, momentum, eps);
-  else
-    hipLaunchKernelGGL(bn_stats_finalize_kernel<BN_F32>, dim3(fin_blocks), dim3(kT), 0, s, part, nblk, x, M, C,
-                       gamma, beta, mean, invstd, scale, shift, running_mean, running_var, momentum, eps);
-  bn_apply(dtype, x, res, y, M, C, scale, shift, act, s);
+    hipLaunchKernelGGL(bn_stats_kernel<BN_F32>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
+  const int64_t nvec = M * C / kV;
+  const int grid = apply_grid(nvec, C / kV);
+#define DCP_BN_APPLY(D, R, A)                                                                                     \
+  hipLaunchKernelGGL((bn_apply_kernel<D, R, A, true>), dim3(grid), dim3(kT), 0, s, x, res, acc, gamma, beta,      \
+                     nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M, nvec, C)
+  const bool r = res != nullptr;
+  if (dtype == BN_BF16) {
+    if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
+    else if (r) DCP_BN_APPLY(BN_BF16, true, false);
+    else if (act) DCP_BN_APPLY(BN_BF16, false, true);
+    else DCP_BN_APPLY(BN_BF16, false, false);
+  } else {
+    if (r && act) DCP_BN_APPLY(BN_F32, true, true);
+    else if (r) DCP_BN_APPLY(BN_F32, true, false);
+    else if (act) DCP_BN_APPLY(BN_F32, false, true);
+    else DCP_BN_APPLY(BN_F32, false, false);
+  }
+#undef DCP_BN_APPLY
 }
 
 void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
               const float* shift, bool act, hipStream_t s) {
   const int64_t nvec = M * C / kV;
-  const int grid = apply_grid(nvec);
-  const size_t sm = sizeof(float) * 2 * C;
-#define DCP_BN_APPLY(D, R, A) \
-  hipLaunchKernelGGL((bn_apply_kernel<D, R, A>), dim3(grid), dim3(kT), sm, s, x, res, scale, shift, y, nvec, C)
+  const int grid = apply_grid(nvec, C / kV);
+#define DCP_BN_APPLY(D, R, A)                                                                                  \
+  hipLaunchKernelGGL((bn_apply_kernel<D, R, A, false>), dim3(grid), dim3(kT), 0, s, x, res, nullptr, nullptr, \
+                     nullptr, scale, shift, y, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, M, nvec, C)
   const bool r = res != nullptr;
   if (dtype == BN_BF16) {
     if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
@@ -452,15 +432,15 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 
 void bn_backward(int dtype, const void* gy, const void* y, const void* x, int64_t M, int C, const float* gamma,
                  const float* mean, const float* invstd, bool act, bool store_g, void* gout, void* dx,
-                 float* dgamma, float* dbeta, float* k1, float* k2, float* k3, float* part, bool training,
-                 hipStream_t s) {
+                 float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s) {
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
+  (void)hipMemsetAsync(acc, 0, sizeof(float) * 2 * C, s);
   const size_t sm = red_smem(C);
 #define DCP_BN_RED(D, A, G)                                                                                 \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G>), dim3(nblk, nchunks), dim3(kT), sm, s, gy, y, x, mean, M, C, \
-                     rpb, part, gout)
+                     rpb, acc, gout)
   if (dtype == BN_BF16) {
     if (act && store_g) DCP_BN_RED(BN_BF16, true, true);
     else if (act) DCP_BN_RED(BN_BF16, true, false);
@@ -473,16 +453,13 @@ void bn_backward(int dtype, const void* gy, const void* y, const void* x, int64_
     else DCP_BN_RED(BN_F32, false, false);
   }
 #undef DCP_BN_RED
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kT), 0, s, part, nblk, M, C, gamma, invstd,
-                     dgamma, dbeta, k1, k2, k3, training);
   const int64_t nvec = M * C / kV;
-  const int grid = apply_grid(nvec);
-  const size_t sm2 = sizeof(float) * 4 * C;
+  const int grid = apply_grid(nvec, C / kV);
   // g source: the stored masked gradient when available, else recompute the mask
   const void* gsrc = store_g ? gout : gy;
-#define DCP_BN_BAPPLY(D, A, F)                                                                                    \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F>), dim3(grid), dim3(kT), sm2, s, gsrc, y, x, mean, k1, k2, k3, \
-                     dx, nvec, C)
+#define DCP_BN_BAPPLY(D, A, F)                                                                                   \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F>), dim3(grid), dim3(kT), 0, s, gsrc, y, x, mean, invstd, gamma, \
+                     acc, dgamma, dbeta, training, dx, M, nvec, C)
   if (dtype == BN_BF16) {
     if (store_g) DCP_BN_BAPPLY(BN_BF16, false, true);
     else if (act) DCP_BN_BAPPLY(BN_BF16, true, false);

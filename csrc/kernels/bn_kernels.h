@@ -10,25 +10,25 @@ namespace kern {
 
 enum BnDType : int { BN_F32 = 0, BN_BF16 = 1 };
 
-// Number of partial-sum workgroups (rows of the [nblk][2][C] fp32 workspace).
-int bn_partial_blocks(int64_t M, int C);
+// Channel counts the kernels handle (C % 8 == 0 and C/8 divides / is a
+// multiple of 256, e.g. every power of two ≥ 8).
+bool bn_supported(int C);
 
 // Training forward: batch statistics, running-stat update, y = act(bn(x) [+ res]).
-// mean/invstd/scale/shift: [C] fp32 outputs. part: workspace [nblk*2*C] fp32.
+// mean/invstd: [C] fp32 outputs. acc: workspace [2*C] fp32 (zeroed here).
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
-                      float* mean, float* invstd, float* scale, float* shift, float* part, bool act, hipStream_t s);
+                      float* mean, float* invstd, float* acc, bool act, hipStream_t s);
 
 // y = act(x * scale[c] + shift[c] [+ res])
 void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
               const float* shift, bool act, hipStream_t s);
 
 // Backward. g = gy * (y > 0) if act else gy; store_g writes g to gout (the
-// residual-branch gradient). dx = k1*(g - k2 - (x-mean)*k3).
+// residual-branch gradient). acc: workspace [2*C] fp32 (zeroed here).
 void bn_backward(int dtype, const void* gy, const void* y, const void* x, int64_t M, int C, const float* gamma,
                  const float* mean, const float* invstd, bool act, bool store_g, void* gout, void* dx,
-                 float* dgamma, float* dbeta, float* k1, float* k2, float* k3, float* part, bool training,
-                 hipStream_t s);
+                 float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s);
 
 }  // namespace kern
 }  // namespace dcp

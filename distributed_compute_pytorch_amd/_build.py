@@ -101,7 +101,8 @@ def _link_cmd(objs, out):
 
 def _sources():
     srcs = sorted(CSRC.rglob("*.cpp")) + sorted(CSRC.rglob("*.hip"))
-    return srcs
+    # standalone sanitizer / self-test programs are not part of the extension
+    return [s for s in srcs if "selftest" not in s.parts]
 
 
 def _header_digest():

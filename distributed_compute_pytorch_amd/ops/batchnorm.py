@@ -26,7 +26,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.fused = fused
 
     def _use_fused(self, x: torch.Tensor) -> bool:
-        return self.fused and x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+        return (self.fused and x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
+                and x.is_contiguous(memory_format=torch.channels_last) and _C.bn_supported(x.shape[1]))
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         if self._use_fused(x):

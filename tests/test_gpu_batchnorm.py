@@ -14,7 +14,7 @@ def _ref(x, w, b, rm, rv, res, act, training, momentum=0.1, eps=1e-5):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 9), (2, 2048, 3, 3), (16, 24, 5, 5), (3, 4096, 2, 2)])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 9), (2, 2048, 3, 3), (16, 32, 5, 5), (3, 4096, 2, 2)])
 @pytest.mark.parametrize("act,residual", [(True, False), (True, True), (False, False)])
 @pytest.mark.parametrize("training", [True, False])
 def test_bn_act_fwd_bwd(cuda, dtype, shape, act, residual, training):
@@ -67,3 +67,12 @@ def test_bn_module_state_dict_compat(cuda):
     m.train()
     m(x)
     assert int(m.num_batches_tracked) == 1
+
+
+def test_bn_module_falls_back_for_odd_channels(cuda):
+    from distributed_compute_pytorch_amd.ops import BatchNormAct2d
+
+    m = BatchNormAct2d(24, fused=True).to(cuda)
+    x = torch.randn(4, 24, 8, 8, device=cuda).contiguous(memory_format=torch.channels_last)
+    ref = F.relu(F.batch_norm(x, None, None, m.weight, m.bias, True))
+    torch.testing.assert_close(m(x), ref, rtol=1e-4, atol=1e-4)
