@@ -67,6 +67,13 @@ ncclRedOp_t to_nccl(ReduceOp op, at::ScalarType st) {
 
 class RcclCommunicator;
 
+// DCP_COMM_STREAM_PRIORITY=high puts collectives on a high-priority queue
+// (default: normal priority, same as the compute stream).
+bool comm_stream_high_priority() {
+  const char* v = std::getenv("DCP_COMM_STREAM_PRIORITY");
+  return v && std::string(v) == "high";
+}
+
 class RcclWork : public Work {
  public:
   RcclWork(RcclCommunicator* comm, hipStream_t stream, int device, int64_t timeout_ms, bool timing);
@@ -94,7 +101,7 @@ class RcclCommunicator : public Communicator {
       : Communicator(std::move(store), prefix, rank, size),
         device_(device),
         timeout_ms_(timeout_ms),
-        stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, static_cast<c10::DeviceIndex>(device))) {
+        stream_(c10::hip::getStreamFromPool(comm_stream_high_priority(), static_cast<c10::DeviceIndex>(device))) {
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
     ncclUniqueId id;
     const std::string key = prefix_ + "/rccl/uid";
@@ -109,6 +116,8 @@ class RcclCommunicator : public Communicator {
     NCCL_OK(ncclCommInitRank(&comm_, size_, id, rank_));
     const char* t = std::getenv("DCP_COMM_TIMING");
     timing_ = t && std::string(t) == "1";
+    const char* h = std::getenv("DCP_SINGLE_RANK_HOP");
+    single_rank_hop_ = h && std::string(h) == "1";
     watchdog_ = std::thread([this] { watchdog(); });
   }
 
@@ -248,6 +257,15 @@ class RcclCommunicator : public Communicator {
     raise_if_error();
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
     hipStream_t caller = c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(device_)).stream();
+    if (size_ == 1 && !single_rank_hop_) {
+      // One rank: every collective is an identity (or a local copy issued by
+      // `issue` on the caller's stream) — no comm-stream round trip.
+      auto work = std::make_shared<RcclWork>(this, caller, device_, timeout_ms_, false);
+      issue(caller);
+      HIP_OK(hipEventRecord(work->end_, caller));
+      work->outputs = std::move(ts);
+      return work;
+    }
     hipStream_t comm = stream_.stream();
     auto work = std::make_shared<RcclWork>(this, comm, device_, timeout_ms_, timing_);
     // comm stream waits for everything the caller queued so far (producers of ts)
@@ -314,6 +332,7 @@ class RcclCommunicator : public Communicator {
   c10::hip::HIPStream stream_;
   ncclComm_t comm_ = nullptr;
   bool timing_ = false;
+  bool single_rank_hop_ = false;
   std::atomic<bool> aborted_{false};
   std::mutex mu_;
   std::condition_variable cv_;

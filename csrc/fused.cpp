@@ -6,6 +6,7 @@
 #include "common.h"
 #include "kernels/bn_kernels.h"
 #include "kernels/ln_kernels.h"
+#include "kernels/dropout_kernels.h"
 
 namespace dcp {
 namespace fused {
@@ -120,19 +121,23 @@ int ln_dtype(const at::Tensor& x) {
 bool layer_norm_supported(int64_t D) { return kern::ln_supported(static_cast<int>(D)); }
 
 // x: [..., D] contiguous. Returns (y, mean, rstd) with mean/rstd [rows] fp32.
+// out_dtype: y's dtype (default x's; fp32 x -> bf16 y for autocast).
 std::vector<at::Tensor> layer_norm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
-                                       const c10::optional<at::Tensor>& bias, double eps) {
+                                       const c10::optional<at::Tensor>& bias, double eps,
+                                       c10::optional<at::ScalarType> out_dtype) {
   DCP_CHECK(x.is_cuda() && x.is_contiguous(), "layer_norm_fwd: contiguous device tensor required");
   const int64_t D = x.size(-1);
   DCP_CHECK(kern::ln_supported(static_cast<int>(D)), "layer_norm_fwd: D must be a multiple of 8 and <= 4096");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t rows = x.numel() / D;
   auto fopt = x.options().dtype(at::kFloat);
-  at::Tensor y = at::empty_like(x);
+  at::Tensor y = at::empty_like(x, x.options().dtype(out_dtype.has_value() ? *out_dtype : x.scalar_type()));
+  DCP_CHECK(!(x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kFloat),
+            "layer_norm_fwd: bf16 input with fp32 output is not supported");
   at::Tensor mean = at::empty({rows}, fopt), rstd = at::empty({rows}, fopt);
   at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor b = bias.has_value() && bias->defined() ? bias->to(at::kFloat).contiguous() : at::Tensor();
-  kern::ln_forward(ln_dtype(x), x.data_ptr(), w.defined() ? w.data_ptr<float>() : nullptr,
+  kern::ln_forward(ln_dtype(x), ln_dtype(y), x.data_ptr(), w.defined() ? w.data_ptr<float>() : nullptr,
                    b.defined() ? b.data_ptr<float>() : nullptr, y.data_ptr(), mean.data_ptr<float>(),
                    rstd.data_ptr<float>(), rows, static_cast<int>(D), static_cast<float>(eps), stream_of(x));
   return {y, mean, rstd};
@@ -144,7 +149,9 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
                                        const at::Tensor& rstd) {
   c10::hip::HIPGuard guard(x.device().index());
   at::Tensor g = dy.contiguous();
-  if (g.scalar_type() != x.scalar_type()) g = g.to(x.scalar_type());
+  // dy arrives in y's dtype (bf16 when the forward wrote bf16 from fp32 x)
+  if (!(x.scalar_type() == at::kFloat && g.scalar_type() == at::kBFloat16) && g.scalar_type() != x.scalar_type())
+    g = g.to(x.scalar_type());
   const int64_t D = x.size(-1);
   const int64_t rows = x.numel() / D;
   auto fopt = x.options().dtype(at::kFloat);
@@ -153,7 +160,7 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
   at::Tensor part = at::empty({static_cast<int64_t>(kern::ln_bwd_blocks(rows)) * 2 * D}, fopt);
   const bool has_w = weight.has_value() && weight->defined();
   at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
-  kern::ln_backward(ln_dtype(x), g.data_ptr(), x.data_ptr(), has_w ? w.data_ptr<float>() : nullptr,
+  kern::ln_backward(ln_dtype(x), ln_dtype(g), g.data_ptr(), x.data_ptr(), has_w ? w.data_ptr<float>() : nullptr,
                     mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(),
                     db.data_ptr<float>(), part.data_ptr<float>(), rows, static_cast<int>(D), stream_of(x));
   const bool has_b = bias.has_value() && bias->defined();
@@ -193,10 +200,52 @@ at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& target,
   return d;
 }
 
+// -------------------------------------------------------------- dropout ---
+int dr_dtype(const at::Tensor& x) {
+  if (x.scalar_type() == at::kBFloat16) return kern::DR_BF16;
+  if (x.scalar_type() == at::kFloat) return kern::DR_F32;
+  throw Error(str_cat("fused dropout: unsupported dtype ", c10::toString(x.scalar_type())));
+}
+
+// y = residual + dropout(x) (residual optional; y takes the residual's dtype,
+// e.g. bf16 branch + fp32 residual stream -> fp32). seed/offset fully
+// determine the mask. out_dtype (when no residual) selects y's dtype.
+at::Tensor dropout_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual, double p, int64_t seed,
+                       int64_t offset, c10::optional<at::ScalarType> out_dtype) {
+  DCP_CHECK(x.is_cuda() && x.is_contiguous(), "dropout_fwd: contiguous device tensor required");
+  c10::hip::HIPGuard guard(x.device().index());
+  at::Tensor res;
+  at::ScalarType yt = out_dtype.has_value() ? *out_dtype : x.scalar_type();
+  if (residual.has_value() && residual->defined()) {
+    res = residual->contiguous();
+    DCP_CHECK(res.sizes() == x.sizes(), "dropout_fwd: residual shape mismatch");
+    yt = res.scalar_type();
+  }
+  at::Tensor y = at::empty_like(x, x.options().dtype(yt));
+  kern::dropout(dr_dtype(x), dr_dtype(y), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, y.data_ptr(),
+                x.numel(), static_cast<float>(p), static_cast<uint64_t>(seed), static_cast<uint64_t>(offset),
+                stream_of(x));
+  return y;
+}
+
+at::Tensor feature_dropout_fwd(const at::Tensor& x, double p, int64_t seed, int64_t offset) {
+  DCP_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() >= 2, "feature_dropout: contiguous [N, C, ...] tensor");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t rows = x.size(0) * x.size(1);
+  at::Tensor y = at::empty_like(x);
+  kern::feature_dropout(dr_dtype(x), x.data_ptr(), y.data_ptr(), rows, rows ? x.numel() / rows : 0,
+                        static_cast<float>(p), static_cast<uint64_t>(seed), static_cast<uint64_t>(offset), stream_of(x));
+  return y;
+}
+
 void bind(pybind11::module& m) {
+  m.def("dropout_fwd", &dropout_fwd, pybind11::arg("x"), pybind11::arg("residual"), pybind11::arg("p"),
+        pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("out_dtype") = pybind11::none());
+  m.def("feature_dropout_fwd", &feature_dropout_fwd);
   m.def("bn_supported", [](int64_t C) { return kern::bn_supported(static_cast<int>(C)); });
   m.def("layer_norm_supported", &layer_norm_supported);
-  m.def("layer_norm_fwd", &layer_norm_fwd);
+  m.def("layer_norm_fwd", &layer_norm_fwd, pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
+        pybind11::arg("eps"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("layer_norm_bwd", &layer_norm_bwd);
   m.def("cross_entropy_fwd", &cross_entropy_fwd);
   m.def("cross_entropy_bwd", &cross_entropy_bwd);

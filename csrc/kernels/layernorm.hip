@@ -69,8 +69,10 @@ __device__ __forceinline__ float wsum(float v) {
   return v;
 }
 
-// VPL = 16-B vectors per lane (D <= VPL*512).
-template <int DT, int VPL>
+// VPL = 16-B vectors per lane (D <= VPL*512). XD: dtype of x (and dx), YD:
+// dtype of y (and dy) — x fp32 / y bf16 is the autocast residual-stream case:
+// the LayerNorm output feeds a bf16 GEMM directly, no separate cast pass.
+template <int XD, int YD, int VPL>
 __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, const float* __restrict__ w,
                                                     const float* __restrict__ b, void* __restrict__ y,
                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -86,7 +88,7 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, 
   for (int j = 0; j < VPL; ++j) {
     const int vi = lane + j * 64;
     if (vi < nv) {
-      L8<DT>::ld(x, base + vi * 8, v[j]);
+      L8<XD>::ld(x, base + vi * 8, v[j]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s += v[j][k];
     } else {
@@ -122,14 +124,14 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, 
         const float xn = (v[j][k] - mean) * rstd;
         o[k] = w ? fmaf(xn, w[c], b ? b[c] : 0.f) : xn;
       }
-      L8<DT>::st(y, base + vi * 8, o);
+      L8<YD>::st(y, base + vi * 8, o);
     }
   }
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 // partial[blk][0][D] += dy * xhat (dgamma), partial[blk][1][D] += dy (dbeta)
-template <int DT, int VPL>
+template <int XD, int YD, int VPL>
 __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy, const void* __restrict__ x,
                                                     const float* __restrict__ w, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, void* __restrict__ dx,
@@ -156,8 +158,8 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
       const int vi = lane + j * 64;
       if (vi < nv) {
         float dv[8];
-        L8<DT>::ld(dy, base + vi * 8, dv);
-        L8<DT>::ld(x, base + vi * 8, xh[j]);
+        L8<YD>::ld(dy, base + vi * 8, dv);
+        L8<XD>::ld(x, base + vi * 8, xh[j]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const int c = vi * 8 + k;
@@ -179,7 +181,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
         float o[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = rs * (g[j][k] - m1 - xh[j][k] * m2);
-        L8<DT>::st(dx, base + vi * 8, o);
+        L8<XD>::st(dx, base + vi * 8, o);
       }
     }
   }
@@ -228,22 +230,25 @@ __global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
   }
 }
 
-template <int DT>
+template <int XD, int YD>
 void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w, const float* b, void* y, float* mean,
                   float* rstd, int64_t rows, int D, float eps) {
+#define DCP_LNF(V) \
+  hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps)
   switch (vpl) {
-    case 1: hipLaunchKernelGGL((ln_fwd_kernel<DT, 1>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps); break;
-    case 2: hipLaunchKernelGGL((ln_fwd_kernel<DT, 2>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps); break;
-    case 4: hipLaunchKernelGGL((ln_fwd_kernel<DT, 4>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps); break;
-    default: hipLaunchKernelGGL((ln_fwd_kernel<DT, 8>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps);
+    case 1: DCP_LNF(1); break;
+    case 2: DCP_LNF(2); break;
+    case 4: DCP_LNF(4); break;
+    default: DCP_LNF(8);
   }
+#undef DCP_LNF
 }
 
-template <int DT>
+template <int XD, int YD>
 void bwd_dispatch(int vpl, dim3 g, size_t sm, hipStream_t s, const void* dy, const void* x, const float* w,
                   const float* mean, const float* rstd, void* dx, float* part, int64_t rows, int D, int rpb) {
 #define DCP_LNB(V) \
-  hipLaunchKernelGGL((ln_bwd_kernel<DT, V>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb)
+  hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb)
   switch (vpl) {
     case 1: DCP_LNB(1); break;
     case 2: DCP_LNB(2); break;
@@ -270,22 +275,27 @@ int ln_bwd_blocks(int64_t rows) {
   return static_cast<int>(nb);
 }
 
-void ln_forward(int dtype, const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
-                int64_t rows, int D, float eps, hipStream_t s) {
+void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const float* b, void* y, float* mean,
+                float* rstd, int64_t rows, int D, float eps, hipStream_t s) {
   const dim3 g(static_cast<unsigned>((rows + kWaves - 1) / kWaves));
   const int vpl = vpl_for(D);
-  if (dtype == LN_BF16) fwd_dispatch<LN_BF16>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
-  else fwd_dispatch<LN_F32>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
+  if (xdtype == LN_BF16) fwd_dispatch<LN_BF16, LN_BF16>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
+  else if (ydtype == LN_BF16) fwd_dispatch<LN_F32, LN_BF16>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
+  else fwd_dispatch<LN_F32, LN_F32>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
 }
 
-void ln_backward(int dtype, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
-                 void* dx, float* dw, float* db, float* part, int64_t rows, int D, hipStream_t s) {
+void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
+                 const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, hipStream_t s) {
   const int nblk = ln_bwd_blocks(rows);
   const int rpb = static_cast<int>((rows + nblk - 1) / nblk);
   const size_t sm = sizeof(float) * kWaves * 2 * D;
   const int vpl = vpl_for(D);
-  if (dtype == LN_BF16) bwd_dispatch<LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
-  else bwd_dispatch<LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
+  if (xdtype == LN_BF16)
+    bwd_dispatch<LN_BF16, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
+  else if (ydtype == LN_BF16)
+    bwd_dispatch<LN_F32, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
+  else
+    bwd_dispatch<LN_F32, LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, part, nblk, D, dw, db);
 }
 

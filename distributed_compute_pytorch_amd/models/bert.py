@@ -18,7 +18,12 @@ from torch import nn
 from torch.nn import functional as F
 
 from ..ops.cross_entropy import fused_cross_entropy
+from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
+
+
+def _plain_dropout_add(x, residual, p, training):
+    return residual + F.dropout(x, p, training)
 
 
 @dataclass
@@ -69,11 +74,12 @@ class BertLayer(nn.Module):
         self.intermediate = nn.Linear(cfg.hidden, cfg.intermediate)
         self.output = nn.Linear(cfg.intermediate, cfg.hidden)
         self.out_ln = _ln(cfg, cfg.hidden)
-        self.drop = nn.Dropout(cfg.dropout)
+        self.p = cfg.dropout
+        self._dadd = dropout_add if cfg.fused else _plain_dropout_add
 
     def forward(self, x, mask):
-        x = self.attn_ln(x + self.drop(self.attn_out(self.attention(x, mask))))
-        return self.out_ln(x + self.drop(self.output(F.gelu(self.intermediate(x)))))
+        x = self.attn_ln(self._dadd(self.attn_out(self.attention(x, mask)), x, self.p, self.training))
+        return self.out_ln(self._dadd(self.output(F.gelu(self.intermediate(x))), x, self.p, self.training))
 
 
 class BertForPreTraining(nn.Module):

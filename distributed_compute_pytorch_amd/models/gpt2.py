@@ -19,7 +19,12 @@ from torch import nn
 from torch.nn import functional as F
 
 from ..ops.cross_entropy import fused_cross_entropy
+from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
+
+
+def _plain_dropout_add(x, residual, p, training):
+    return residual + F.dropout(x, p, training)
 
 
 @dataclass
@@ -40,7 +45,6 @@ class CausalSelfAttention(nn.Module):
         self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
         self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
         self.dropout = cfg.dropout
-        self.resid_drop = nn.Dropout(cfg.dropout)
 
     def forward(self, x):
         B, T, C = x.shape
@@ -51,7 +55,7 @@ class CausalSelfAttention(nn.Module):
         v = v.view(B, T, h, C // h).transpose(1, 2)
         y = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0, is_causal=True)
         y = y.transpose(1, 2).contiguous().view(B, T, C)
-        return self.resid_drop(self.c_proj(y))
+        return self.c_proj(y)  # residual dropout is fused with the add in Block
 
 
 class MLP(nn.Module):
@@ -59,10 +63,9 @@ class MLP(nn.Module):
         super().__init__()
         self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
         self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
-        self.drop = nn.Dropout(cfg.dropout)
 
     def forward(self, x):
-        return self.drop(self.c_proj(F.gelu(self.c_fc(x), approximate="tanh")))
+        return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
 
 
 def _ln(cfg, d):
@@ -76,10 +79,12 @@ class Block(nn.Module):
         self.attn = CausalSelfAttention(cfg)
         self.ln_2 = _ln(cfg, cfg.n_embd)
         self.mlp = MLP(cfg)
+        self.p = cfg.dropout
+        self._dadd = dropout_add if cfg.fused else _plain_dropout_add
 
     def forward(self, x):
-        x = x + self.attn(self.ln_1(x))
-        return x + self.mlp(self.ln_2(x))
+        x = self._dadd(self.attn(self.ln_1(x)), x, self.p, self.training)
+        return self._dadd(self.mlp(self.ln_2(x)), x, self.p, self.training)
 
 
 class GPT2(nn.Module):

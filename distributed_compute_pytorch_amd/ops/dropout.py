@@ -1,0 +1,83 @@
+"""Counter-based Philox dropout (csrc/kernels/dropout.hip).
+
+The mask is a function of (seed, offset, element index): nothing is stored,
+the backward regenerates it. Seeds come from torch's CPU generator, so
+``torch.manual_seed`` makes runs reproducible (the reference
+seeds every rank identically). ``dropout_add(x, residual, p)`` fuses the
+transformer residual add.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+from .._ext import C as _C
+
+_OK = (torch.float32, torch.bfloat16)
+
+
+def _seed():
+    return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+
+
+class _DropFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, p, seed):
+        ctx.p, ctx.seed, ctx.has_res, ctx.xdtype = p, seed, residual is not None, x.dtype
+        return _C.dropout_fwd(x, residual, p, seed, 0)
+
+    @staticmethod
+    def backward(ctx, gy):
+        gx = _C.dropout_fwd(gy.contiguous(), None, ctx.p, ctx.seed, 0, ctx.xdtype)
+        return gx, (gy if ctx.has_res else None), None, None
+
+
+class _FeatDropFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        ctx.p, ctx.seed = p, seed
+        return _C.feature_dropout_fwd(x, p, seed, 0)
+
+    @staticmethod
+    def backward(ctx, gy):
+        return _C.feature_dropout_fwd(gy.contiguous(), ctx.p, ctx.seed, 0), None, None
+
+
+def _usable(x):
+    return x.is_cuda and x.dtype in _OK and x.is_contiguous()
+
+
+def fused_dropout(x, p: float = 0.5, training: bool = True):
+    if not training or p == 0.0:
+        return x
+    if _usable(x):
+        return _DropFn.apply(x, None, float(p), _seed())
+    return F.dropout(x, p, training)
+
+
+def dropout_add(x, residual, p: float = 0.1, training: bool = True):
+    """residual + dropout(x) in one pass."""
+    if not training or p == 0.0:
+        return residual + x
+    if _usable(x) and residual.shape == x.shape and residual.dtype in _OK:
+        return _DropFn.apply(x, residual.contiguous(), float(p), _seed())
+    return residual + F.dropout(x, p, training)
+
+
+def fused_feature_dropout(x, p: float = 0.5, training: bool = True):
+    if not training or p == 0.0:
+        return x
+    if _usable(x) and x.dim() >= 3:
+        return _FeatDropFn.apply(x, float(p), _seed())
+    return F.dropout2d(x, p, training)
+
+
+class FusedDropout(nn.Dropout):
+    def forward(self, x):
+        return fused_dropout(x, self.p, self.training)
+
+
+class FusedDropout2d(nn.Dropout2d):
+    def forward(self, x):
+        return fused_feature_dropout(x, self.p, self.training)

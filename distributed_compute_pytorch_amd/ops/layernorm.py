@@ -17,8 +17,8 @@ from .._ext import C as _C
 
 class _LNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
-        y, mean, rstd = _C.layer_norm_fwd(x, weight, bias, eps)
+    def forward(ctx, x, weight, bias, eps, out_dtype):
+        y, mean, rstd = _C.layer_norm_fwd(x, weight, bias, eps, out_dtype)
         ctx.save_for_backward(x, weight, bias, mean, rstd)
         return y
 
@@ -26,17 +26,19 @@ class _LNFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight, bias, mean, rstd = ctx.saved_tensors
         dx, dw, db = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def fused_layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
     D = x.shape[-1]
     if x.is_cuda and len(normalized_shape) == 1 and _C.layer_norm_supported(D) and x.dtype in (torch.float32,
                                                                                              torch.bfloat16):
+        out_dtype = None
         if torch.is_autocast_enabled() and x.dtype == torch.float32:
-            x = x.to(torch.get_autocast_dtype("cuda"))
+            # fp32 residual stream in, bf16 out: the cast is fused into the kernel
+            out_dtype = torch.get_autocast_dtype("cuda")
         with torch.autocast("cuda", enabled=False):
-            return _LNFn.apply(x.contiguous(), weight, bias, eps)
+            return _LNFn.apply(x.contiguous(), weight, bias, eps, out_dtype)
     return F.layer_norm(x, normalized_shape, weight, bias, eps)
 
 

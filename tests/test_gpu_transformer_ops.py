@@ -67,3 +67,73 @@ def test_cross_entropy_unaligned_rows(cuda):
     sl = logits[1:]  # storage offset 50257 elements: misaligned start
     torch.testing.assert_close(fused_cross_entropy(sl, target[1:]), F.cross_entropy(sl.float(), target[1:]),
                                rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n", [1, 7, 4096, 1000003])
+def test_dropout_statistics_and_backward(cuda, dtype, n):
+    from distributed_compute_pytorch_amd.ops import dropout_add, fused_dropout
+
+    torch.manual_seed(0)
+    x = torch.randn(n, device=cuda, dtype=dtype).requires_grad_()
+    y = fused_dropout(x, 0.3)
+    kept = (y != 0)
+    if n > 1000:
+        assert abs(kept.float().mean().item() - 0.7) < 0.02
+    torch.testing.assert_close(y[kept].float(), (x[kept] / 0.7).float(), rtol=1e-2, atol=1e-2)
+    y.backward(torch.ones_like(y))
+    # gradient mask == forward mask (regenerated from the same counter)
+    assert torch.equal(x.grad != 0, kept)
+    r = torch.randn(n, device=cuda, dtype=dtype)
+    torch.manual_seed(5)
+    z = dropout_add(x.detach(), r, 0.3)
+    torch.manual_seed(5)
+    z2 = fused_dropout(x.detach(), 0.3) + r
+    torch.testing.assert_close(z.float(), z2.float(), rtol=1e-2, atol=1e-2)
+
+
+def test_feature_dropout(cuda):
+    from distributed_compute_pytorch_amd.ops import fused_feature_dropout
+
+    x = torch.randn(64, 32, 6, 6, device=cuda, requires_grad=True)
+    y = fused_feature_dropout(x, 0.25)
+    per_ch = (y.detach() != 0).reshape(64, 32, -1)
+    assert torch.all(per_ch.all(-1) | (~per_ch).all(-1))  # whole channels kept or dropped
+    frac = per_ch.all(-1).float().mean().item()
+    assert abs(frac - 0.75) < 0.06
+    y.sum().backward()
+    torch.testing.assert_close((x.grad != 0), (y.detach() != 0))
+
+
+def test_layer_norm_autocast_fp32_in_bf16_out(cuda):
+    from distributed_compute_pytorch_amd.ops import FusedLayerNorm
+
+    torch.manual_seed(0)
+    m = FusedLayerNorm(768).to(cuda)
+    ref = torch.nn.LayerNorm(768).to(cuda)
+    x = torch.randn(4, 64, 768, device=cuda, requires_grad=True)
+    xr = x.detach().clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+        yr = ref(xr)
+    assert y.dtype == torch.bfloat16 and x.dtype == torch.float32
+    torch.testing.assert_close(y.float(), yr.float(), rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.to(y.dtype))
+    yr.backward(g)
+    assert x.grad.dtype == torch.float32
+    torch.testing.assert_close(x.grad, xr.grad, rtol=3e-2, atol=3e-2)
+
+
+def test_dropout_add_mixed_dtypes(cuda):
+    from distributed_compute_pytorch_amd.ops import dropout_add
+
+    x = torch.randn(1 << 16, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(1 << 16, device=cuda, dtype=torch.float32, requires_grad=True)
+    y = dropout_add(x, r, 0.2)
+    assert y.dtype == torch.float32
+    y.backward(torch.ones_like(y))
+    assert x.grad.dtype == torch.bfloat16 and r.grad.dtype == torch.float32
+    kept = (y.detach() - r.detach()) != 0
+    assert torch.equal(x.grad != 0, kept)
+    torch.testing.assert_close(r.grad, torch.ones_like(r))

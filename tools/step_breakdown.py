@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--fused", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--profile", type=int, default=1)
+    ap.add_argument("--fused-model", type=int, default=0, help="use fused kernels even with torch DDP")
+    ap.add_argument("--tag", default="")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(29000 + os.getpid() % 1000))
@@ -33,7 +35,8 @@ def main():
 
     ours_ddp = a.variant in ("ours", "ours_ddp_torch_opt", "ours_nodpp_none")
     ours_opt = a.variant in ("ours", "torch_ddp_ours_opt")
-    wl = workloads.build(a.model, dev, batch=a.batch, fused=bool(a.fused) and ours_ddp)
+    fused = bool(a.fused) and (ours_ddp or a.fused_model)
+    wl = workloads.build(a.model, dev, batch=a.batch, fused=fused)
     if a.variant == "noddp_ours_opt":
         ddp = wl.model
         opt = wl.make_optimizer(ddp.parameters())
@@ -75,7 +78,7 @@ def main():
         torch.cuda.synchronize(); ph["bwd"] += time.perf_counter() - t; t = time.perf_counter()
         opt.step()
         torch.cuda.synchronize(); ph["opt"] += time.perf_counter() - t
-    res = {"variant": a.variant, "model": a.model, "free_running_ms": round(t_total * 1e3, 2),
+    res = {"variant": a.variant, "tag": a.tag, "fused": fused, "model": a.model, "free_running_ms": round(t_total * 1e3, 2),
            "host_issue_ms": round(t_host * 1e3, 2)}
     res.update({k + "_ms": round(v / a.steps * 1e3, 2) for k, v in ph.items()})
     print(json.dumps(res), flush=True)
