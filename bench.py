@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--grad-as-view", type=int, default=1)
     ap.add_argument("--benchmark-cudnn", type=int, default=1)
+    ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a HIP graph")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -125,7 +126,7 @@ def main():
             tdist.all_reduce(t, tdist.ReduceOp.MAX)
             return float(t.item())
 
-    step = workloads.make_step(wl, ddp, opt)
+    step = workloads.make_step(wl, ddp, opt, graph=bool(a.graph))
     t_w = time.time()
     for i in range(a.warmup):
         loss = step()
@@ -157,6 +158,7 @@ def main():
             "fused_kernels": fused,
             "optimizer": type(opt).__name__,
             "comm_dtype": a.comm_dtype,
+            "hip_graph": bool(a.graph),
         }
         if a.model == "resnet50":
             cfg.update(image_size=224, channels_last=bool(a.channels_last))

@@ -279,7 +279,9 @@ class RcclCommunicator : public Communicator {
     issue(comm);
     HIP_OK(hipEventRecord(work->end_, comm));
     work->outputs = std::move(ts);
-    {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(comm, &cap);
+    if (cap == hipStreamCaptureStatusNone) {  // captured events are not queryable: no deadline tracking
       std::lock_guard<std::mutex> g(mu_);
       inflight_.push_back(work);
     }

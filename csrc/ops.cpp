@@ -33,11 +33,29 @@ struct TableEntry {
   at::Tensor dev;
   int n;
   int64_t nchunks;
+  at::Tensor host;          // pinned source of the upload
+  bool persistent = false;  // uploaded inside a HIP-graph capture: the
+                            // captured memcpy node re-reads `host` on every
+                            // replay, so neither may ever be freed
 };
 
 std::mutex g_cache_mu;
 std::list<TableEntry> g_cache;  // MRU at front
 constexpr size_t kCacheCap = 32;
+// Evicted pinned upload buffers wait here until the copy that read them has
+// finished (raw hipMemcpyAsync: the torch host allocator does not track it).
+std::vector<std::pair<hipEvent_t, at::Tensor>> g_graveyard;
+
+void reap_graveyard() {
+  for (auto it = g_graveyard.begin(); it != g_graveyard.end();) {
+    if (hipEventQuery(it->first) == hipSuccess) {
+      (void)hipEventDestroy(it->first);
+      it = g_graveyard.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
 
 // lists[d][i]: tensor i of list d. All lists must have the same length; rows
 // (same i) must have identical numel. Empty tensors are skipped.
@@ -73,9 +91,35 @@ TableEntry get_table(const std::vector<const TensorList*>& lists) {
   at::Tensor host = at::empty({static_cast<int64_t>(words.size())},
                               at::TensorOptions().dtype(at::kLong).pinned_memory(true));
   std::memcpy(host.data_ptr(), words.data(), words.size() * sizeof(int64_t));
-  at::Tensor d = host.to(dev, /*non_blocking=*/true);
-  g_cache.push_front(TableEntry{std::move(words), d, n, chunks});
-  if (g_cache.size() > kCacheCap) g_cache.pop_back();
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const hipStream_t st = c10::hip::getCurrentHIPStream(dev.index()).stream();
+  (void)hipStreamIsCapturing(st, &cap);
+  const bool capturing = cap == hipStreamCaptureStatusActive;
+  at::Tensor d = at::empty({static_cast<int64_t>(words.size())}, at::TensorOptions().dtype(at::kLong).device(dev));
+  DCP_CHECK(hipMemcpyAsync(d.data_ptr(), host.data_ptr(), words.size() * sizeof(int64_t), hipMemcpyHostToDevice,
+                           st) == hipSuccess,
+            "table upload failed");
+  TableEntry e{std::move(words), d, n, chunks, host, capturing};
+  g_cache.push_front(std::move(e));
+  // evict the least recently used non-persistent entry (never while capturing:
+  // the deferred-free event would itself be captured)
+  if (!capturing) {
+    reap_graveyard();
+    if (g_cache.size() > kCacheCap) {
+      for (auto it = std::prev(g_cache.end());; --it) {
+        if (!it->persistent) {
+          hipEvent_t ev;
+          if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
+              hipEventRecord(ev, st) == hipSuccess) {
+            g_graveyard.emplace_back(ev, it->host);
+          }
+          g_cache.erase(it);
+          break;
+        }
+        if (it == g_cache.begin()) break;
+      }
+    }
+  }
   return g_cache.front();
 }
 

@@ -117,15 +117,18 @@ def build(name: str, device, batch: Optional[int] = None, fused: bool = True, se
     raise ValueError(f"unknown workload {name!r}")
 
 
-def make_step(wl: Workload, ddp, opt, device_type: str = "cuda"):
+def make_step(wl: Workload, ddp, opt, device_type: str = "cuda", graph: bool = False):
     """One optimizer step = ``accum`` micro-batches (all but the last under
-    ``no_sync``), bf16 autocast when ``wl.amp``."""
+    ``no_sync``), bf16 autocast when ``wl.amp``. ``graph=True`` captures the
+    whole step (fwd + bwd + reduction + optimizer) into one HIP graph and
+    replays it (see :mod:`.utils.graphs`)."""
 
-    def step():
+    def run(*flat):
         opt.zero_grad(set_to_none=True)
         loss = None
+        n = len(flat) // wl.accum
         for k in range(wl.accum):
-            batch = next(wl.data)
+            batch = flat[k * n:(k + 1) * n]
             ctx = ddp.no_sync() if (k < wl.accum - 1 and hasattr(ddp, "no_sync")) else _Null()
             with ctx:
                 with torch.autocast(device_type, dtype=torch.bfloat16, enabled=wl.amp):
@@ -136,7 +139,19 @@ def make_step(wl: Workload, ddp, opt, device_type: str = "cuda"):
         opt.step()
         return loss
 
-    return step
+    def next_flat():
+        out = []
+        for _ in range(wl.accum):
+            out.extend(next(wl.data))
+        return out
+
+    if not graph:
+        return lambda: run(*next_flat())
+    from .utils.graphs import CapturedStep
+
+    static = [t.clone() for t in next_flat()]
+    captured = CapturedStep(run, static)
+    return lambda: captured(*next_flat())
 
 
 class _Null:

@@ -60,12 +60,9 @@ def test_ddp_matches_local_training(pg, cuda, grad_as_view):
     assert set(ddp.state_dict().keys()) == {"module." + k for k in ref.state_dict().keys()}
 
 
-@pytest.mark.parametrize("amp", [False, True])
-def test_resnet_step_matches_stock(pg, cuda, amp):
-    """Our DDP + fused SGD + fused BN vs plain torch (no DDP, torch SGD, ATen BN)
-    on the same init and batch. fp32: parameter updates agree tightly; bf16:
-    losses track (bf16 rounding makes early-layer updates diverge in either
-    implementation, so only the loss trajectory is compared)."""
+def test_resnet_grads_match_stock_fp32(pg, cuda):
+    """One fp32 step: every parameter gradient through our DDP + fused BN
+    equals the stock ATen model's (relative error < 1e-3)."""
     import distributed_compute_pytorch_amd as dcp
     from distributed_compute_pytorch_amd.models import resnet50
 
@@ -73,7 +70,31 @@ def test_resnet_step_matches_stock(pg, cuda, amp):
     ref = resnet50(num_classes=100).to(cuda).to(memory_format=torch.channels_last)
     model = resnet50(num_classes=100, fused_bn=True).to(cuda).to(memory_format=torch.channels_last)
     model.load_state_dict(ref.state_dict())
-    init = {n: p.detach().clone() for n, p in ref.named_parameters()}
+    ddp = dcp.parallel.DistributedDataParallel(model, device_ids=[0], gradient_as_bucket_view=True)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(16, 3, 96, 96, generator=g).to(cuda).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 100, (16,), generator=g).to(cuda)
+    l1 = F.cross_entropy(ref(x), y)
+    l1.backward()
+    l2 = F.cross_entropy(ddp(x), y)
+    l2.backward()
+    torch.testing.assert_close(l2, l1, rtol=1e-5, atol=1e-5)
+    for (n, p), q in zip(ref.named_parameters(), model.parameters()):
+        rel = (q.grad - p.grad).norm() / p.grad.norm().clamp_min(1e-12)
+        assert rel < 1e-3, (n, float(rel))
+    for (n, b), c in zip(ref.named_buffers(), model.buffers()):
+        torch.testing.assert_close(c.float(), b.float(), rtol=1e-4, atol=1e-5, msg=n)
+
+
+def test_resnet_bf16_loss_tracks_stock(pg, cuda):
+    """bf16 autocast, 3 SGD steps: loss trajectories agree within bf16 noise."""
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.models import resnet50
+
+    torch.manual_seed(0)
+    ref = resnet50(num_classes=100).to(cuda).to(memory_format=torch.channels_last)
+    model = resnet50(num_classes=100, fused_bn=True).to(cuda).to(memory_format=torch.channels_last)
+    model.load_state_dict(ref.state_dict())
     ddp = dcp.parallel.DistributedDataParallel(model, device_ids=[0], gradient_as_bucket_view=True)
     o_ref = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9)
     opt = dcp.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9)
@@ -84,18 +105,14 @@ def test_resnet_step_matches_stock(pg, cuda, amp):
     for _ in range(3):
         for m, o, acc in ((ref, o_ref, l_ref), (ddp, opt, l_ours)):
             o.zero_grad()
-            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
                 loss = F.cross_entropy(m(x), y)
             loss.backward()
             o.step()
             acc.append(loss.item())
     assert all(torch.isfinite(torch.tensor(l_ours)))
+    assert l_ours[-1] < l_ours[0]
     for a, b in zip(l_ref, l_ours):
-        assert abs(a - b) < (0.05 if amp else 1e-3) * max(1.0, abs(a)), (l_ref, l_ours)
-    if not amp:
-        for (n, p), q, p0 in zip(ref.named_parameters(), model.parameters(), init.values()):
-            du_ref, du_ours = (p.detach() - p0), (q.detach() - p0)
-            rel = (du_ours - du_ref).norm() / du_ref.norm().clamp_min(1e-12)
-            assert rel < 2e-2, (n, float(rel))
+        assert abs(a - b) < 0.08 * max(1.0, abs(a)), (l_ref, l_ours)
     info = ddp.ddp_logging_data()
     assert info["rebuilds"] == 1 and sum(info["bucket_sizes"]) == sum(p.numel() * 4 for p in model.parameters())

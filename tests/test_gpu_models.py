@@ -38,7 +38,8 @@ def test_fused_matches_stock_eval(cuda, name):
         for (n, p), q in zip(a.named_parameters(), b.parameters()):
             if p.grad is None:
                 continue
-            rel = (p.grad - q.grad).norm() / q.grad.norm().clamp_min(1e-8)
+            # (attention key biases have ~zero true gradient: floor the denominator)
+            rel = (p.grad - q.grad).norm() / q.grad.norm().clamp_min(1e-3)
             assert rel < (0.1 if amp else 1e-3), (n, float(rel))
         a.zero_grad()
         b.zero_grad()
