@@ -7,6 +7,7 @@
 #include "kernels/bn_kernels.h"
 #include "kernels/ln_kernels.h"
 #include "kernels/dropout_kernels.h"
+#include "kernels/pool_kernels.h"
 
 namespace dcp {
 namespace fused {
@@ -238,7 +239,55 @@ at::Tensor feature_dropout_fwd(const at::Tensor& x, double p, int64_t seed, int6
   return y;
 }
 
+// -------------------------------------------------------------- maxpool ---
+kern::PoolGeom pool_geom(const at::Tensor& x, int64_t k, int64_t s, int64_t p) {
+  kern::PoolGeom g;
+  g.N = static_cast<int>(x.size(0));
+  g.C = static_cast<int>(x.size(1));
+  g.H = static_cast<int>(x.size(2));
+  g.W = static_cast<int>(x.size(3));
+  g.K = static_cast<int>(k);
+  g.S = static_cast<int>(s);
+  g.P = static_cast<int>(p);
+  g.OH = (g.H + 2 * g.P - g.K) / g.S + 1;
+  g.OW = (g.W + 2 * g.P - g.K) / g.S + 1;
+  return g;
+}
+
+bool maxpool_supported(const at::Tensor& x, int64_t k, int64_t p) {
+  return x.is_cuda() && x.dim() == 4 && x.size(1) % 8 == 0 && k * k <= 255 && 2 * p <= k &&
+         (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) &&
+         x.is_contiguous(at::MemoryFormat::ChannelsLast);
+}
+
+// Returns (y [NHWC], idx uint8 window offsets).
+std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p) {
+  DCP_CHECK(maxpool_supported(x, k, p), "maxpool2d_fwd: needs channels_last bf16/fp32, C % 8 == 0");
+  c10::hip::HIPGuard guard(x.device().index());
+  auto g = pool_geom(x, k, s, p);
+  at::Tensor y = at::empty({g.N, g.C, g.OH, g.OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor idx = at::empty({static_cast<int64_t>(g.N) * g.OH * g.OW * g.C}, x.options().dtype(at::kByte));
+  kern::maxpool2d_forward(x.scalar_type() == at::kBFloat16 ? kern::POOL_BF16 : kern::POOL_F32, x.data_ptr(),
+                          y.data_ptr(), idx.data_ptr<uint8_t>(), g, stream_of(x));
+  return {y, idx};
+}
+
+at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& idx, const at::Tensor& x, int64_t k, int64_t s,
+                         int64_t p) {
+  c10::hip::HIPGuard guard(x.device().index());
+  auto g = pool_geom(x, k, s, p);
+  at::Tensor go = gy.contiguous(at::MemoryFormat::ChannelsLast);
+  if (go.scalar_type() != x.scalar_type()) go = go.to(x.scalar_type());
+  at::Tensor gx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  kern::maxpool2d_backward(x.scalar_type() == at::kBFloat16 ? kern::POOL_BF16 : kern::POOL_F32, go.data_ptr(),
+                           idx.data_ptr<uint8_t>(), gx.data_ptr(), g, stream_of(x));
+  return gx;
+}
+
 void bind(pybind11::module& m) {
+  m.def("maxpool_supported", &maxpool_supported);
+  m.def("maxpool2d_fwd", &maxpool2d_fwd);
+  m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("dropout_fwd", &dropout_fwd, pybind11::arg("x"), pybind11::arg("residual"), pybind11::arg("p"),
         pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("feature_dropout_fwd", &feature_dropout_fwd);

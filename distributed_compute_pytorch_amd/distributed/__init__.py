@@ -196,6 +196,29 @@ def _parse_init(init_method: str, rank: int, world_size: int):
     raise ValueError(f"unsupported init_method {init_method!r}")
 
 
+def _bootstrap_from_agent_store(addr: str, port: int, rank: int, world_size: int, timeout_ms: int):
+    """Under torchrun / torch.distributed.run the elastic agent already hosts a
+    (torch) TCPStore on MASTER_ADDR:MASTER_PORT. Rank 0 starts our C++ store on
+    an ephemeral port and publishes it through the agent's store; the other
+    ranks read it and connect. (Same-protocol reuse is impossible: the agent
+    store speaks torch's wire format.)"""
+    import datetime
+
+    import torch.distributed as tdist
+
+    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    key = f"dcp/store_addr/{attempt}"
+    agent = tdist.TCPStore(addr, port, world_size, False, timeout=datetime.timedelta(milliseconds=timeout_ms))
+    if rank == 0:
+        ours = _C.TCPStore(addr, 0, world_size, True, timeout_ms, False)
+        agent.set(key, f"{ours.local_ip()}:{ours.port}")
+    else:
+        host, p = agent.get(key).decode().rsplit(":", 1)
+        ours = _C.TCPStore(host, int(p), world_size, False, timeout_ms, False)
+    ours.barrier("init")
+    return ours
+
+
 def init_process_group(backend: Optional[str] = None, init_method: Optional[str] = None,
                        timeout: Optional[_dt.timedelta] = None, world_size: int = -1, rank: int = -1,
                        store=None, group_name: str = "", pg_options=None, device_id=None) -> None:
@@ -208,7 +231,11 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
     timeout_ms = int((timeout or _DEFAULT_TIMEOUT).total_seconds() * 1000)
     if store is None:
         addr, port, rank, world_size = _parse_init(init_method, rank, world_size)
-        store = _C.TCPStore(addr, port, world_size, rank == 0, timeout_ms, True)
+        if (init_method in (None, "env://") and
+                os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() in ("true", "1")):
+            store = _bootstrap_from_agent_store(addr, port, rank, world_size, timeout_ms)
+        else:
+            store = _C.TCPStore(addr, port, world_size, rank == 0, timeout_ms, True)
     else:
         if rank < 0 or world_size < 0:
             raise ValueError("explicit store needs rank and world_size")

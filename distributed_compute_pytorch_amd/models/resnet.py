@@ -19,6 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.pool import FusedMaxPool2d
 
 
 def conv3x3(cin, cout, stride=1):
@@ -66,7 +67,7 @@ class ResNet(nn.Module):
         self.fused_bn = fused_bn
         self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
         self.bn1 = BatchNormAct2d(64, act=True, fused=fused_bn)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.maxpool = (FusedMaxPool2d if fused_bn else nn.MaxPool2d)(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)

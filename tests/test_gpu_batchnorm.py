@@ -76,3 +76,23 @@ def test_bn_module_falls_back_for_odd_channels(cuda):
     x = torch.randn(4, 24, 8, 8, device=cuda).contiguous(memory_format=torch.channels_last)
     ref = F.relu(F.batch_norm(x, None, None, m.weight, m.bias, True))
     torch.testing.assert_close(m(x), ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 16, 9, 7), 3, 2, 1),
+                                         ((2, 8, 8, 8), 2, 2, 0), ((1, 32, 5, 5), 3, 1, 1)])
+def test_maxpool_nhwc(cuda, dtype, shape, k, s, p):
+    from distributed_compute_pytorch_amd.ops import fused_max_pool2d
+
+    torch.manual_seed(0)
+    x = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    xr = x.detach().float().requires_grad_()
+    xo = x.detach().clone().requires_grad_()
+    yr = F.max_pool2d(xr, k, s, p)
+    yo = fused_max_pool2d(xo, k, s, p)
+    torch.testing.assert_close(yo.float(), yr, rtol=0, atol=0)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    yo.backward(g.to(dtype))
+    tol = dict(rtol=1e-6, atol=1e-6) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(xo.grad.float(), xr.grad, **tol)

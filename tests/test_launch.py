@@ -1,5 +1,6 @@
 """Launcher semantics: error propagation and fault injection."""
 import os
+import subprocess
 import sys
 import textwrap
 import time
@@ -67,3 +68,38 @@ def test_launch_env_fault_injection(tmp_path):
     code = launch_env([sys.executable, str(script)], 3, timeout=120)
     assert code != 0
     assert time.time() - t0 < 60
+
+
+def test_torchrun_agent_store_compat(tmp_path):
+    """Under torch.distributed.run the elastic agent already listens on
+    MASTER_PORT (TORCHELASTIC_USE_AGENT_STORE=True): our store must bootstrap
+    through it instead of binding the same port (this is how the driver
+    launches the multi-GPU bench)."""
+    from distributed_compute_pytorch_amd.distributed.launch import free_port
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "job.py"
+    script.write_text(textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {repo!r})
+        import torch, torch.nn.functional as F
+        import distributed_compute_pytorch_amd as dcp
+        from distributed_compute_pytorch_amd.models import ConvNet
+        dcp.distributed.init_process_group("gloo")
+        r, w = dcp.distributed.get_rank(), dcp.distributed.get_world_size()
+        torch.manual_seed(0)
+        m = dcp.parallel.DistributedDataParallel(ConvNet())
+        F.nll_loss(m(torch.randn(4, 1, 28, 28) + r), torch.zeros(4, dtype=torch.long)).backward()
+        g = m.module.fc1.weight.grad.clone()
+        ref = g.clone(); dcp.distributed.broadcast(ref, 0)
+        assert torch.allclose(g, ref), "replicas diverged"
+        t = torch.tensor([float(r)]); dcp.distributed.all_reduce(t)
+        assert t.item() == sum(range(w))
+        dcp.distributed.destroy_process_group()
+        print("OK", r)
+    """))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "3",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(script)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.count("OK") == 3
