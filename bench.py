@@ -89,6 +89,13 @@ def main():
     wl = workloads.build(a.model, dev, batch=a.batch, fused=fused, seq_len=a.seq_len, accum=a.accum,
                          channels_last=bool(a.channels_last))
 
+    import contextlib
+
+    from distributed_compute_pytorch_amd.utils.graphs import capture_stream
+
+    # graph capture: build DDP / optimizer under the capture stream (AccumulateGrad
+    # nodes are bound to the stream current at their creation)
+    stream_ctx = torch.cuda.stream(capture_stream()) if a.graph else contextlib.nullcontext()
     if ours:
         dcp.distributed.init_process_group("rccl", device_id=local)
         kw = {}
@@ -98,9 +105,10 @@ def main():
             kw["first_bucket_mb"] = a.first_bucket_mb
         if a.comm_dtype == "bf16":
             kw["comm_dtype"] = torch.bfloat16
-        ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[local],
-                                                   gradient_as_bucket_view=bool(a.grad_as_view), **kw)
-        opt = wl.make_optimizer(ddp.parameters())
+        with stream_ctx:
+            ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[local],
+                                                       gradient_as_bucket_view=bool(a.grad_as_view), **kw)
+            opt = wl.make_optimizer(ddp.parameters())
         barrier = dcp.distributed.barrier
 
         def max_over_ranks(x):
@@ -114,7 +122,8 @@ def main():
         kw = {}
         if a.bucket_cap_mb is not None:
             kw["bucket_cap_mb"] = a.bucket_cap_mb
-        ddp = torch.nn.parallel.DistributedDataParallel(wl.model, device_ids=[local], **kw)
+        with stream_ctx:
+            ddp = torch.nn.parallel.DistributedDataParallel(wl.model, device_ids=[local], **kw)
         ours_opt = wl.make_optimizer([torch.nn.Parameter(torch.zeros(1, device=dev))])
         cls = getattr(torch.optim, type(ours_opt).__name__)
         opt = cls(ddp.parameters(), **{k: v for k, v in ours_opt.defaults.items()

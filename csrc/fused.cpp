@@ -3,11 +3,15 @@
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include <map>
+#include <mutex>
+
 #include "common.h"
 #include "kernels/bn_kernels.h"
 #include "kernels/ln_kernels.h"
 #include "kernels/dropout_kernels.h"
 #include "kernels/pool_kernels.h"
+#include "kernels/metrics_kernels.h"
 
 namespace dcp {
 namespace fused {
@@ -32,6 +36,43 @@ void check_nhwc(const at::Tensor& x, const char* what) {
 
 const float* opt_ptr(const c10::optional<at::Tensor>& t) {
   return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+
+// Zeroed fp32 accumulators for the BN column sums. Eager mode: bump-allocated
+// from a per-(device, stream) arena that is re-zeroed by ONE memset when it
+// wraps (stream order puts that memset after every earlier consumer), instead
+// of one fill launch per BatchNorm call. Under HIP-graph capture each call gets
+// its own allocation + captured memset node (replays must re-zero).
+struct ZeroArena {
+  at::Tensor buf;
+  int64_t used = 0;
+};
+std::mutex g_arena_mu;
+std::map<std::pair<int, hipStream_t>, ZeroArena> g_arenas;
+constexpr int64_t kArenaFloats = int64_t(4) << 20;  // 16 MiB
+
+at::Tensor zeroed_floats(int64_t n, const at::Tensor& like, hipStream_t st) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(st, &cap);
+  const int64_t need = (n + 63) / 64 * 64;
+  if (cap != hipStreamCaptureStatusNone || need > kArenaFloats / 4) {
+    at::Tensor t = at::empty({need}, like.options().dtype(at::kFloat));
+    DCP_CHECK(hipMemsetAsync(t.data_ptr(), 0, sizeof(float) * need, st) == hipSuccess, "memset failed");
+    return t.narrow(0, 0, n);
+  }
+  std::lock_guard<std::mutex> g(g_arena_mu);
+  ZeroArena& a = g_arenas[{static_cast<int>(like.get_device()), st}];
+  if (!a.buf.defined()) {
+    a.buf = at::empty({kArenaFloats}, like.options().dtype(at::kFloat));
+    DCP_CHECK(hipMemsetAsync(a.buf.data_ptr(), 0, sizeof(float) * kArenaFloats, st) == hipSuccess, "memset failed");
+  }
+  if (a.used + need > kArenaFloats) {
+    DCP_CHECK(hipMemsetAsync(a.buf.data_ptr(), 0, sizeof(float) * kArenaFloats, st) == hipSuccess, "memset failed");
+    a.used = 0;
+  }
+  at::Tensor t = a.buf.narrow(0, a.used, n);
+  a.used += need;
+  return t;
 }
 
 }  // namespace
@@ -61,7 +102,7 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
   at::Tensor invstd = at::empty({C}, fopt);
   auto s = stream_of(x);
   if (training) {
-    at::Tensor acc = at::empty({2 * C}, fopt);
+    at::Tensor acc = zeroed_floats(2 * C, x, s);
     float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
     float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
     kern::bn_forward_train(bn_dtype(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, y.data_ptr(), M,
@@ -101,7 +142,7 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const at::Tensor& x, co
   at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor dw = at::empty({C}, fopt);
   at::Tensor db = at::empty({C}, fopt);
-  at::Tensor acc = at::empty({2 * C}, fopt);
+  at::Tensor acc = zeroed_floats(2 * C, x, stream_of(x));
   kern::bn_backward(bn_dtype(x), g.data_ptr(), y.data_ptr(), x.data_ptr(), M, static_cast<int>(C),
                     has_w ? w.data_ptr<float>() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(), act,
                     has_res, has_res ? gres.data_ptr() : nullptr, dx.data_ptr(), dw.data_ptr<float>(),
@@ -284,7 +325,34 @@ at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& idx, const at::
   return gx;
 }
 
+// -------------------------------------------------------------- metrics ---
+// acc: fp64 [3] on the scores' device: [Σ loss, #correct, #count] += batch.
+void eval_metrics_(at::Tensor& acc, const at::Tensor& scores, const at::Tensor& target, bool log_probs,
+                   int64_t ignore_index) {
+  DCP_CHECK(acc.scalar_type() == at::kDouble && acc.numel() == 3, "eval_metrics_: acc must be fp64 [3]");
+  DCP_CHECK(scores.dim() == 2 && target.dim() == 1 && target.size(0) == scores.size(0), "eval_metrics_: shapes");
+  if (!scores.is_cuda()) {
+    auto s = scores.to(at::kFloat);
+    auto valid = target.ne(ignore_index);
+    auto t = target.clamp_min(0);
+    auto lp = log_probs ? s : at::log_softmax(s, 1);
+    auto picked = lp.gather(1, t.unsqueeze(1)).squeeze(1);
+    acc[0] += (-picked * valid).sum().item<double>();
+    acc[1] += (s.argmax(1).eq(target) & valid).sum().item<double>();
+    acc[2] += valid.sum().item<double>();
+    return;
+  }
+  c10::hip::HIPGuard guard(scores.device().index());
+  at::Tensor sc = scores.contiguous();
+  if (sc.scalar_type() != at::kFloat && sc.scalar_type() != at::kBFloat16) sc = sc.to(at::kFloat);
+  at::Tensor tg = target.contiguous();
+  kern::eval_metrics(sc.scalar_type() == at::kBFloat16 ? kern::MET_BF16 : kern::MET_F32, sc.data_ptr(),
+                     tg.data_ptr<int64_t>(), sc.size(0), static_cast<int>(sc.size(1)), log_probs, ignore_index,
+                     acc.data_ptr<double>(), stream_of(sc));
+}
+
 void bind(pybind11::module& m) {
+  m.def("eval_metrics_", &eval_metrics_);
   m.def("maxpool_supported", &maxpool_supported);
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);

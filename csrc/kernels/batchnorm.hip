@@ -90,10 +90,14 @@ struct Geo {
   int cv;    // channel vectors total = C/8
 };
 
+// ≤ 32 threads per row: a wide-C layer is split into channel chunks (grid.y)
+// so the grid fills the chip with few row slabs (few atomics).
+constexpr int kMaxTpr = 32;
+
 __device__ __forceinline__ Geo geo(int C) {
   Geo g;
   g.cv = C / kV;
-  g.tpr = g.cv < kT ? g.cv : kT;
+  g.tpr = g.cv < kMaxTpr ? g.cv : kMaxTpr;
   g.rpi = kT / g.tpr;
   return g;
 }
@@ -268,10 +272,12 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
   if (cv_ok) {
 #pragma unroll
     for (int k = 0; k < kV; ++k) mu[k] = mean[cvec * kV + k];
+#pragma unroll 2
     for (int64_t r = r0 + grp; r < r1; r += g.rpi) {
       const int64_t off = r * C + cvec * kV;
       float gv[kV], xv[kV];
       V8<D>::ld(gy, off, gv);
+      V8<D>::ld(x, off, xv);
       if (ACT) {
         float yv[kV];
         V8<D>::ld(y, off, yv);
@@ -279,7 +285,6 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
         for (int k = 0; k < kV; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
       }
       if (STORE_G) V8<D>::st(gout, off, gv);
-      V8<D>::ld(x, off, xv);
 #pragma unroll
       for (int k = 0; k < kV; ++k) {
         sb[k] += gv[k];
@@ -337,14 +342,18 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict
   }
 }
 
-// grid for the reduction kernels: ~2 workgroups per CU in total
+// grid for the reduction kernels: ~2048 workgroups over (row slabs × channel
+// chunks), ≥ 4 row iterations per thread, ≤ ~256K column atomics per launch.
 inline void red_geometry(int64_t M, int C, int* nblk, int64_t* rows_per_blk, int* nchunks) {
   const int cv = C / kV;
-  const int tpr = cv < kT ? cv : kT;
+  const int tpr = cv < kMaxTpr ? cv : kMaxTpr;
   const int rpi = kT / tpr;
   *nchunks = (cv + tpr - 1) / tpr;
-  int64_t want = (M + static_cast<int64_t>(rpi) * 8 - 1) / (static_cast<int64_t>(rpi) * 8);  // >= 8 rows/thread
-  const int64_t cap = 512 / *nchunks > 0 ? 512 / *nchunks : 1;
+  int64_t want = (M + static_cast<int64_t>(rpi) * 4 - 1) / (static_cast<int64_t>(rpi) * 4);
+  int64_t cap = 2048 / *nchunks;
+  const int64_t atomic_cap = (int64_t(128) << 10) / C;
+  if (cap > atomic_cap) cap = atomic_cap;
+  if (cap < 1) cap = 1;
   if (want > cap) want = cap;
   if (want < 1) want = 1;
   int64_t rpb = (M + want - 1) / want;
@@ -367,14 +376,21 @@ inline int apply_grid(int64_t nvec, int cv) {
 
 inline size_t red_smem(int C) {
   const int cv = C / kV;
-  const int tpr = cv < kT ? cv : kT;
+  const int tpr = cv < kMaxTpr ? cv : kMaxTpr;
   const int rpi = kT / tpr;
   return sizeof(float) * 2 * rpi * tpr * kV;
 }
 
 }  // namespace
 
-bool bn_supported(int C) { return C % kV == 0 && (C / kV <= kT ? (kT % (C / kV) == 0) : ((C / kV) % kT == 0)); }
+bool bn_supported(int C) {
+  // reductions: C/8 ≤ 32 must divide 256, else be a multiple of 32; apply: C/8 must divide 256 or be a multiple
+  const int cv = C / kV;
+  if (C % kV != 0) return false;
+  const bool red_ok = cv <= kMaxTpr ? (kT % cv == 0) : (cv % kMaxTpr == 0);
+  const bool app_ok = cv <= kT ? (kT % cv == 0) : (cv % kT == 0);
+  return red_ok && app_ok;
+}
 
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
@@ -382,7 +398,6 @@ void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
-  (void)hipMemsetAsync(acc, 0, sizeof(float) * 2 * C, s);
   const size_t sm = red_smem(C);
   if (dtype == BN_BF16)
     hipLaunchKernelGGL(bn_stats_kernel<BN_BF16>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
@@ -436,7 +451,6 @@ void bn_backward(int dtype, const void* gy, const void* y, const void* x, int64_
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
-  (void)hipMemsetAsync(acc, 0, sizeof(float) * 2 * C, s);
   const size_t sm = red_smem(C);
 #define DCP_BN_RED(D, A, G)                                                                                 \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G>), dim3(nblk, nchunks), dim3(kT), sm, s, gy, y, x, mean, M, C, \

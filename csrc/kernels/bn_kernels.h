@@ -15,7 +15,7 @@ enum BnDType : int { BN_F32 = 0, BN_BF16 = 1 };
 bool bn_supported(int C);
 
 // Training forward: batch statistics, running-stat update, y = act(bn(x) [+ res]).
-// mean/invstd: [C] fp32 outputs. acc: workspace [2*C] fp32 (zeroed here).
+// mean/invstd: [C] fp32 outputs. acc: ZEROED workspace [2*C] fp32.
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
                       float* mean, float* invstd, float* acc, bool act, hipStream_t s);
@@ -25,7 +25,7 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
               const float* shift, bool act, hipStream_t s);
 
 // Backward. g = gy * (y > 0) if act else gy; store_g writes g to gout (the
-// residual-branch gradient). acc: workspace [2*C] fp32 (zeroed here).
+// residual-branch gradient). acc: ZEROED workspace [2*C] fp32.
 void bn_backward(int dtype, const void* gy, const void* y, const void* x, int64_t M, int C, const float* gamma,
                  const float* mean, const float* invstd, bool act, bool store_g, void* gout, void* dx,
                  float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s);

@@ -17,6 +17,8 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace dcp {
@@ -152,6 +154,28 @@ __global__ void __launch_bounds__(kThreads) mt_copy_kernel(Tab tab, int64_t nchu
     }
     for (int64_t i = i0 + threadIdx.x; i < len; i += kThreads)
       Acc<DD>::st(dst, base + i, scale * Acc<SD>::ld(src, base + i));
+  });
+}
+
+// Bit-exact copy (same dtype, scale 1): moves 16-B vectors when aligned.
+// ES = element size in bytes (2 or 4); 8-byte types are passed as 4-byte
+// views by the host. Used for bucket pack/unpack and coalesced broadcasts of
+// any dtype (int64 buffers included) without a float round trip.
+template <int ES>
+__global__ void __launch_bounds__(kThreads) mt_rawcopy_kernel(Tab tab, int64_t nchunks) {
+  using W = typename std::conditional<ES == 2, uint16_t, uint32_t>::type;
+  constexpr int per16 = 16 / ES;
+  for_each_chunk(tab, nchunks, [&](int t, int64_t base, int64_t len) {
+    const W* src = static_cast<const W*>(tab.ptr(0, t)) + base;
+    W* dst = static_cast<W*>(tab.ptr(1, t)) + base;
+    int64_t i0 = 0;
+    if (aligned(src, 16) && aligned(dst, 16)) {
+      const int64_t nv = len / per16;
+      for (int64_t v = threadIdx.x; v < nv; v += kThreads)
+        reinterpret_cast<uint4*>(dst)[v] = reinterpret_cast<const uint4*>(src)[v];
+      i0 = nv * per16;
+    }
+    for (int64_t i = i0 + threadIdx.x; i < len; i += kThreads) dst[i] = src[i];
   });
 }
 
@@ -434,6 +458,13 @@ inline Tab tab_of(TableView t) { return Tab{t.base, t.n}; }
 
 void mt_copy(TableView t, int64_t nchunks, DType src, DType dst, float scale, hipStream_t s) {
   if (nchunks <= 0) return;
+  if (src == dst && scale == 1.0f) {
+    if (src == F32)
+      hipLaunchKernelGGL((mt_rawcopy_kernel<4>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks);
+    else
+      hipLaunchKernelGGL((mt_rawcopy_kernel<2>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks);
+    return;
+  }
   DCP_DISPATCH_DTYPE(src, SD, DCP_DISPATCH_DTYPE(dst, DD,
       hipLaunchKernelGGL((mt_copy_kernel<SD, DD>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks, scale)));
 }

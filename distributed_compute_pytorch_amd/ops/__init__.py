@@ -2,8 +2,9 @@
 from .batchnorm import BatchNormAct2d, bn_act
 from .layernorm import FusedLayerNorm, fused_layer_norm
 from .cross_entropy import fused_cross_entropy
+from .metrics import EvalMetrics
 from .pool import FusedMaxPool2d, fused_max_pool2d
 from .dropout import FusedDropout, FusedDropout2d, dropout_add, fused_dropout, fused_feature_dropout
 
 __all__ = ["BatchNormAct2d", "bn_act", "FusedLayerNorm", "fused_layer_norm", "fused_cross_entropy", "FusedDropout",
-           "FusedDropout2d", "dropout_add", "fused_dropout", "fused_feature_dropout", "FusedMaxPool2d", "fused_max_pool2d"]
+           "FusedDropout2d", "dropout_add", "fused_dropout", "fused_feature_dropout", "FusedMaxPool2d", "fused_max_pool2d", "EvalMetrics"]

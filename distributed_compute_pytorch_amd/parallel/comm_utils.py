@@ -50,24 +50,46 @@ def _flat_views(flat: torch.Tensor, tensors: Sequence[torch.Tensor]):
     return views
 
 
+_WORD_VIEW = {torch.int64: torch.float32, torch.float64: torch.float32, torch.int32: torch.float32,
+              torch.int16: torch.bfloat16}
+
+
+def _as_words(ts: Sequence[torch.Tensor]):
+    """Bit-preserving float32/bf16 views of 2/4/8-byte tensors (for the raw
+    multi-tensor copy): one launch moves every buffer regardless of dtype."""
+    out = []
+    for t in ts:
+        wd = _WORD_VIEW.get(t.dtype, t.dtype)
+        if wd is t.dtype:
+            out.append(t)
+        elif t.is_contiguous():
+            out.append(t.reshape(-1).view(wd))
+        else:
+            return None
+    return out
+
+
+def _copy_list(src: Sequence[torch.Tensor], dst: Sequence[torch.Tensor]):
+    if src and src[0].is_cuda and all(is_dense(t) for t in list(src) + list(dst)) \
+            and all(s.dtype == d.dtype for s, d in zip(src, dst)):
+        ws, wd = _as_words(src), _as_words(dst)
+        if ws is not None and wd is not None and all(t.dtype in _MT_DTYPES for t in ws):
+            _C.mt_copy(ws, wd, 1.0)  # same dtype, scale 1 -> bit-exact raw copy kernel
+            return
+    if src and not src[0].is_cuda and all(s.dtype == d.dtype for s, d in zip(src, dst)) and \
+            all(t.dtype in _MT_DTYPES for t in src) and all(is_dense(t) for t in list(src) + list(dst)):
+        _C.mt_copy(list(src), list(dst), 1.0)
+        return
+    for s, d in zip(src, dst):
+        d.copy_(s)
+
+
 def pack(tensors: Sequence[torch.Tensor], flat: torch.Tensor):
-    dense = all(is_dense(t) for t in tensors)
-    views = _flat_views(flat, tensors)
-    if dense and flat.dtype in _MT_DTYPES and all(t.dtype == flat.dtype for t in tensors):
-        _C.mt_copy(list(tensors), views, 1.0)
-    else:
-        for v, t in zip(views, tensors):
-            v.copy_(t)
+    _copy_list(list(tensors), _flat_views(flat, tensors))
 
 
 def unpack(flat: torch.Tensor, tensors: Sequence[torch.Tensor]):
-    dense = all(is_dense(t) for t in tensors)
-    views = _flat_views(flat, tensors)
-    if dense and flat.dtype in _MT_DTYPES and all(t.dtype == flat.dtype for t in tensors):
-        _C.mt_copy(views, list(tensors), 1.0)
-    else:
-        for v, t in zip(views, tensors):
-            t.copy_(v)
+    _copy_list(_flat_views(flat, tensors), list(tensors))
 
 
 class CoalescedBroadcaster:

@@ -15,11 +15,18 @@ Everything the step touches is capture-safe by construction:
 * the fused optimizers read hyper-parameters at capture time — changing the
   LR after capture requires re-capturing (``CapturedStep.recapture``).
 
-Usage::
+The autograd engine binds every parameter's AccumulateGrad node to the stream
+that was current when the node was created, and the Reducer keeps those nodes
+alive; so construct the DDP model (and run warmup / capture) under ONE side
+stream — :func:`capture_stream` returns it::
 
-    step = CapturedStep(step_fn, static_batch)      # step_fn(batch) -> loss
+    s = capture_stream()
+    with torch.cuda.stream(s):
+        ddp = DistributedDataParallel(model, ...)
+        opt = SGD(ddp.parameters(), ...)
+    step = CapturedStep(step_fn, static_batch, stream=s)   # step_fn(batch) -> loss
     for batch in loader:
-        loss = step(batch)                          # copies into static buffers, replays
+        loss = step(batch)                                 # copies into static buffers, replays
 """
 from __future__ import annotations
 
@@ -28,19 +35,31 @@ from typing import Callable, Sequence
 import torch
 
 
+_STREAMS = {}
+
+
+def capture_stream(device=None) -> torch.cuda.Stream:
+    """The per-device side stream used for DDP construction, warmup and capture."""
+    dev = torch.cuda.current_device() if device is None else device
+    if dev not in _STREAMS:
+        _STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return _STREAMS[dev]
+
+
 class CapturedStep:
     def __init__(self, step_fn: Callable, static_inputs: Sequence[torch.Tensor], warmup: int = 3,
-                 pool=None):
+                 pool=None, stream: torch.cuda.Stream = None):
         self.step_fn = step_fn
         self.static_inputs = list(static_inputs)
         self.warmup = warmup
         self.pool = pool
+        self.stream = stream or capture_stream()
         self.graph = None
         self.static_out = None
         self._capture()
 
     def _capture(self):
-        s = torch.cuda.Stream()
+        s = self.stream
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(self.warmup):
@@ -48,7 +67,7 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool):
+        with torch.cuda.graph(g, pool=self.pool, stream=s):
             self.static_out = self.step_fn(*self.static_inputs)
         self.graph = g
 

@@ -147,10 +147,10 @@ def make_step(wl: Workload, ddp, opt, device_type: str = "cuda", graph: bool = F
 
     if not graph:
         return lambda: run(*next_flat())
-    from .utils.graphs import CapturedStep
+    from .utils.graphs import CapturedStep, capture_stream
 
     static = [t.clone() for t in next_flat()]
-    captured = CapturedStep(run, static)
+    captured = CapturedStep(run, static, stream=capture_stream())
     return lambda: captured(*next_flat())
 
 

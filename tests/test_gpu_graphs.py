@@ -13,7 +13,7 @@ def test_captured_step_matches_eager(cuda):
     import distributed_compute_pytorch_amd as dcp
     from distributed_compute_pytorch_amd.distributed.launch import free_port
     from distributed_compute_pytorch_amd.models import resnet18_like
-    from distributed_compute_pytorch_amd.utils.graphs import CapturedStep
+    from distributed_compute_pytorch_amd.utils.graphs import CapturedStep, capture_stream
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
     dcp.distributed.init_process_group("rccl", device_id=0)
@@ -22,7 +22,9 @@ def test_captured_step_matches_eager(cuda):
         base = resnet18_like(num_classes=10, fused_bn=True).to(cuda).to(memory_format=torch.channels_last)
         m_eager, m_graph = copy.deepcopy(base), copy.deepcopy(base)
         d_e = dcp.parallel.DistributedDataParallel(m_eager, device_ids=[0], gradient_as_bucket_view=True)
-        d_g = dcp.parallel.DistributedDataParallel(m_graph, device_ids=[0], gradient_as_bucket_view=True)
+        s = capture_stream()
+        with torch.cuda.stream(s):
+            d_g = dcp.parallel.DistributedDataParallel(m_graph, device_ids=[0], gradient_as_bucket_view=True)
         o_e = dcp.optim.SGD(d_e.parameters(), lr=0.05, momentum=0.9)
         o_g = dcp.optim.SGD(d_g.parameters(), lr=0.05, momentum=0.9)
         g = torch.Generator(device="cpu").manual_seed(1)
@@ -43,7 +45,7 @@ def test_captured_step_matches_eager(cuda):
         # the capture helper runs 3 warmup steps on the first batch
         for _ in range(3):
             run_e(*batches[0])
-        cap = CapturedStep(run_g, [t.clone() for t in batches[0]], warmup=3)  # capture does not execute
+        cap = CapturedStep(run_g, [t.clone() for t in batches[0]], warmup=3, stream=s)  # capture does not execute
         le, lg = [], []
         for b in batches[1:]:
             le.append(run_e(*b).item())

@@ -137,3 +137,30 @@ def test_dropout_add_mixed_dtypes(cuda):
     kept = (y.detach() - r.detach()) != 0
     assert torch.equal(x.grad != 0, kept)
     torch.testing.assert_close(r.grad, torch.ones_like(r))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("log_probs", [True, False])
+def test_eval_metrics(cuda, dtype, log_probs):
+    from distributed_compute_pytorch_amd.ops import EvalMetrics
+
+    torch.manual_seed(0)
+    m = EvalMetrics(cuda, log_probs=log_probs)
+    tot_loss, tot_corr, tot_n = 0.0, 0, 0
+    for _ in range(3):
+        s = torch.randn(777, 1000, device=cuda)
+        if log_probs:
+            s = torch.log_softmax(s, 1)
+        y = torch.randint(0, 1000, (777,), device=cuda)
+        y[:5] = -100
+        s = s.to(dtype)
+        m.update(s, y)
+        sf = s.float()
+        lp = sf if log_probs else torch.log_softmax(sf, 1)
+        tot_loss += F.nll_loss(lp, y, ignore_index=-100, reduction="sum").item()
+        tot_corr += (sf.argmax(1).eq(y) & y.ne(-100)).sum().item()
+        tot_n += y.ne(-100).sum().item()
+    avg, acc, n = m.compute(all_reduce=False)
+    assert n == tot_n
+    assert abs(avg - tot_loss / tot_n) < 1e-3 * max(1, abs(avg))
+    assert abs(acc - tot_corr / tot_n) < 1e-9
