@@ -125,7 +125,10 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
 }
 
 // Returns (dx, dweight, dbias, dresidual).
-std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const at::Tensor& x, const c10::optional<at::Tensor>& weight,
+// gy2: optional second output gradient (dual-output BN: the output feeds two
+// consumers); summed inside the reduction kernel when has_res.
+std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const c10::optional<at::Tensor>& gy2_opt,
+                                   const at::Tensor& x, const c10::optional<at::Tensor>& weight,
                                    const c10::optional<at::Tensor>& bias, const at::Tensor& mean,
                                    const at::Tensor& invstd, const at::Tensor& y, bool act, bool has_res,
                                    bool training) {
@@ -133,6 +136,15 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const at::Tensor& x, co
   c10::hip::HIPGuard guard(x.device().index());
   at::Tensor g = gy.contiguous(at::MemoryFormat::ChannelsLast);
   if (g.scalar_type() != x.scalar_type()) g = g.to(x.scalar_type());
+  at::Tensor g2;
+  if (gy2_opt.has_value() && gy2_opt->defined()) {
+    g2 = gy2_opt->contiguous(at::MemoryFormat::ChannelsLast);
+    if (g2.scalar_type() != x.scalar_type()) g2 = g2.to(x.scalar_type());
+    if (!has_res) {  // kernel sums only on the store_g path
+      g = g + g2;
+      g2 = at::Tensor();
+    }
+  }
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
   auto fopt = x.options().dtype(at::kFloat);
@@ -143,7 +155,8 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const at::Tensor& x, co
   at::Tensor dw = at::empty({C}, fopt);
   at::Tensor db = at::empty({C}, fopt);
   at::Tensor acc = zeroed_floats(2 * C, x, stream_of(x));
-  kern::bn_backward(bn_dtype(x), g.data_ptr(), y.data_ptr(), x.data_ptr(), M, static_cast<int>(C),
+  kern::bn_backward(bn_dtype(x), g.data_ptr(), g2.defined() ? g2.data_ptr() : nullptr, y.data_ptr(), x.data_ptr(),
+                    M, static_cast<int>(C),
                     has_w ? w.data_ptr<float>() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(), act,
                     has_res, has_res ? gres.data_ptr() : nullptr, dx.data_ptr(), dw.data_ptr<float>(),
                     db.data_ptr<float>(), acc.data_ptr<float>(), training, stream_of(x));

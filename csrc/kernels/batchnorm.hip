@@ -252,8 +252,13 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
 // -------------------------------------------------------- bwd reduce ----
 // g = gy * (y > 0) (ACT); acc[0][c] += Σ g, acc[1][c] += Σ g*(x-mean)
 // STORE_G: write g (the gradient of the residual branch) as a side output.
-template <int D, bool ACT, bool STORE_G>
-__global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restrict__ gy, const void* __restrict__ y,
+// GY2: a second output gradient summed on the fly (the BN output feeds two
+// consumers — next block's conv and its residual add — and the dual-output
+// autograd Function hands both gradients here instead of autograd adding
+// them with a separate elementwise pass).
+template <int D, bool ACT, bool STORE_G, bool GY2>
+__global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restrict__ gy, const void* __restrict__ gy2,
+                                                           const void* __restrict__ y,
                                                            const void* __restrict__ x, const float* __restrict__ mean,
                                                            int64_t M, int C, int64_t rows_per_blk,
                                                            float* __restrict__ acc, void* __restrict__ gout) {
@@ -277,6 +282,12 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
       const int64_t off = r * C + cvec * kV;
       float gv[kV], xv[kV];
       V8<D>::ld(gy, off, gv);
+      if (GY2) {
+        float g2[kV];
+        V8<D>::ld(gy2, off, g2);
+#pragma unroll
+        for (int k = 0; k < kV; ++k) gv[k] += g2[k];
+      }
       V8<D>::ld(x, off, xv);
       if (ACT) {
         float yv[kV];
@@ -445,17 +456,30 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 #undef DCP_BN_APPLY
 }
 
-void bn_backward(int dtype, const void* gy, const void* y, const void* x, int64_t M, int C, const float* gamma,
-                 const float* mean, const float* invstd, bool act, bool store_g, void* gout, void* dx,
-                 float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s) {
+void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, const void* x, int64_t M, int C,
+                 const float* gamma, const float* mean, const float* invstd, bool act, bool store_g, void* gout,
+                 void* dx, float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s) {
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
   const size_t sm = red_smem(C);
-#define DCP_BN_RED(D, A, G)                                                                                 \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G>), dim3(nblk, nchunks), dim3(kT), sm, s, gy, y, x, mean, M, C, \
-                     rpb, acc, gout)
-  if (dtype == BN_BF16) {
+#define DCP_BN_RED(D, A, G)                                                                                  \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G, false>), dim3(nblk, nchunks), dim3(kT), sm, s, gy, nullptr, y, \
+                     x, mean, M, C, rpb, acc, gout)
+  // the second gradient is only supported with store_g (the host sums otherwise)
+  if (gy2 != nullptr) {
+    if (dtype == BN_BF16) {
+      if (act) hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, true, true, true>), dim3(nblk, nchunks), dim3(kT), sm, s,
+                                  gy, gy2, y, x, mean, M, C, rpb, acc, gout);
+      else hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, false, true, true>), dim3(nblk, nchunks), dim3(kT), sm, s,
+                              gy, gy2, y, x, mean, M, C, rpb, acc, gout);
+    } else {
+      if (act) hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, true, true, true>), dim3(nblk, nchunks), dim3(kT), sm, s,
+                                  gy, gy2, y, x, mean, M, C, rpb, acc, gout);
+      else hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, false, true, true>), dim3(nblk, nchunks), dim3(kT), sm, s,
+                              gy, gy2, y, x, mean, M, C, rpb, acc, gout);
+    }
+  } else if (dtype == BN_BF16) {
     if (act && store_g) DCP_BN_RED(BN_BF16, true, true);
     else if (act) DCP_BN_RED(BN_BF16, true, false);
     else if (store_g) DCP_BN_RED(BN_BF16, false, true);

@@ -26,9 +26,10 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 
 // Backward. g = gy * (y > 0) if act else gy; store_g writes g to gout (the
 // residual-branch gradient). acc: ZEROED workspace [2*C] fp32.
-void bn_backward(int dtype, const void* gy, const void* y, const void* x, int64_t M, int C, const float* gamma,
-                 const float* mean, const float* invstd, bool act, bool store_g, void* gout, void* dx,
-                 float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s);
+// gy2 (optional, requires store_g): second output gradient, summed with gy.
+void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, const void* x, int64_t M, int C,
+                 const float* gamma, const float* mean, const float* invstd, bool act, bool store_g, void* gout,
+                 void* dx, float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s);
 
 }  // namespace kern
 }  // namespace dcp

@@ -47,11 +47,31 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
+    def forward(self, x: torch.Tensor, identity: Optional[torch.Tensor] = None, dual: bool = False):
+        """``identity``: alias of ``x`` produced by the previous block's
+        dual-output BN (its gradient is summed inside that BN's backward)."""
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        elif identity is None:
+            identity = x
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), identity)
+        return self.bn3(self.conv3(out), identity, dual=dual)
+
+
+class BottleneckStage(nn.Sequential):
+    """nn.Sequential of bottlenecks (same state_dict keys) that threads the
+    dual-output BN alias from each block into the next block's residual."""
+
+    def forward(self, x):
+        blocks = list(self)
+        ident = None
+        for i, blk in enumerate(blocks):
+            nxt = blocks[i + 1] if i + 1 < len(blocks) else None
+            dual = nxt is not None and nxt.downsample is None
+            out = blk(x, ident, dual=dual)
+            x, ident = (out if dual else (out, None))
+        return x
 
 
 def _downsample(cin, cout, stride, fused_bn):
@@ -93,7 +113,7 @@ class ResNet(nn.Module):
         self.inplanes = width * block.expansion
         for _ in range(1, blocks):
             layers.append(block(self.inplanes, width, fused_bn=self.fused_bn))
-        return nn.Sequential(*layers)
+        return BottleneckStage(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.maxpool(self.bn1(self.conv1(x)))

@@ -29,39 +29,49 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return (self.fused and x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
                 and x.is_contiguous(memory_format=torch.channels_last) and _C.bn_supported(x.shape[1]))
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, dual: bool = False):
+        """``dual=True`` returns (y, y_alias): two autograd outputs over the same
+        data for two consumers (next conv + next residual add); their gradients
+        are summed inside this op's backward kernel instead of by a separate
+        autograd add."""
         if self._use_fused(x):
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.num_batches_tracked,
-                          self.training, self.momentum, self.eps, residual if self.residual else None, self.act)
+                          self.training, self.momentum, self.eps, residual if self.residual else None, self.act,
+                          dual)
         y = super().forward(x)
         if self.residual and residual is not None:
             y = y + residual
         if self.act:
             y = F.relu(y, inplace=True)
-        return y
+        return (y, y) if dual else y
 
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act):
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual):
         y, mean, invstd = _C.bn_act_fwd(x, weight, bias, running_mean, running_var, residual, training,
                                         float(momentum), float(eps), bool(act))
         ctx.save_for_backward(x, weight, bias, mean, invstd, y)
         ctx.has_res = residual is not None
         ctx.act = act
         ctx.training = training
+        ctx.dual = dual
+        if dual:
+            return y, y.view_as(y)
         return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, gy2=None):
         x, weight, bias, mean, invstd, y = ctx.saved_tensors
-        gx, gw, gb, gres = _C.bn_act_bwd(gy.contiguous(memory_format=torch.channels_last), x, weight, bias, mean,
-                                         invstd, y, ctx.act, ctx.has_res, ctx.training)
-        return gx, gw, gb, None, None, None, None, None, (gres if ctx.has_res else None), None
+        if gy is None:
+            gy, gy2 = gy2, None
+        gx, gw, gb, gres = _C.bn_act_bwd(gy, gy2, x, weight, bias, mean, invstd, y, ctx.act, ctx.has_res,
+                                         ctx.training)
+        return gx, gw, gb, None, None, None, None, None, (gres if ctx.has_res else None), None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, num_batches_tracked, training, momentum, eps, residual,
-           act):
+           act, dual: bool = False):
     if training and num_batches_tracked is not None:
         num_batches_tracked.add_(1)
-    return _BNActFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act)
+    return _BNActFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual)

@@ -94,5 +94,45 @@ def test_maxpool_nhwc(cuda, dtype, shape, k, s, p):
     g = torch.randn_like(yr)
     yr.backward(g)
     yo.backward(g.to(dtype))
-    tol = dict(rtol=1e-6, atol=1e-6) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
-    torch.testing.assert_close(xo.grad.float(), xr.grad, **tol)
+    if dtype == torch.float32:
+        torch.testing.assert_close(xo.grad.float(), xr.grad, rtol=1e-6, atol=1e-6)
+    else:
+        # bf16 inputs tie inside windows; ATen and we may route a tied gradient
+        # to different (equally valid) positions: require near-total agreement
+        # and identical per-sample gradient mass
+        same = torch.isclose(xo.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+        assert same.float().mean().item() > 0.999
+        torch.testing.assert_close(xo.grad.float().sum((1, 2, 3)), xr.grad.sum((1, 2, 3)), rtol=1e-2, atol=1e-1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_dual_output_sums_gradients(cuda, dtype):
+    """dual=True: two consumers' gradients are summed inside the BN backward."""
+    from distributed_compute_pytorch_amd.ops.batchnorm import bn_act
+
+    torch.manual_seed(0)
+    shape = (8, 256, 7, 7)
+    x = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    w, b = torch.rand(256, device=cuda) + 0.5, torch.randn(256, device=cuda)
+    g1 = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    g2 = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+
+    def run(dual):
+        xx = x.detach().clone().requires_grad_()
+        rr = r.detach().clone().requires_grad_()
+        ww, bb = w.clone().requires_grad_(), b.clone().requires_grad_()
+        nbt = torch.zeros((), dtype=torch.long, device=cuda)
+        out = bn_act(xx, ww, bb, torch.zeros(256, device=cuda), torch.ones(256, device=cuda), nbt, True, 0.1, 1e-5,
+                     rr, True, dual)
+        if dual:
+            y, ya = out
+            torch.autograd.backward([y, ya], [g1, g2])
+        else:
+            out.backward((g1.float() + g2.float()).to(dtype))
+        return xx.grad, rr.grad, ww.grad, bb.grad
+
+    a, bq = run(True), run(False)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=5e-2)
+    for u, v in zip(a, bq):
+        torch.testing.assert_close(u.float(), v.float(), **tol)
