@@ -36,6 +36,22 @@ METRICS = {
 }
 
 
+def _vs_baseline(model, wl, world, total):
+    """value / (stock PyTorch DDP per-GPU throughput measured on MI355X x N):
+    profiles/stock_baselines.json (BASELINE.md "Measured on MI355X"). None when
+    the config differs from the measured one."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "stock_baselines.json")
+    try:
+        with open(path) as f:
+            ref = json.load(f).get(model)
+    except (OSError, ValueError):
+        return None
+    if not ref or ref.get("per_gpu_batch") != wl.per_gpu_batch or ref.get("grad_accum", 1) != wl.accum \
+            or ref.get("seq_len") != wl.seq_len:
+        return None
+    return round(total / (ref["samples_per_s_per_gpu"] * world), 4)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -191,6 +207,7 @@ def main():
         }
         if wl.seq_len:
             rec["tokens_per_s"] = round(total * wl.seq_len, 1)
+        rec["vs_baseline"] = _vs_baseline(a.model, wl, world, total)
         line = json.dumps(rec)
         print(line, flush=True)
         if a.json_out:

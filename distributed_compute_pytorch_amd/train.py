@@ -1,0 +1,172 @@
+"""General trainer CLI: the reference's proc()/train()/test() loop (main.py:55-134)
+on this framework, for every model family, with structured metrics,
+checkpoint/resume and optional HIP-graph capture.
+
+    python -m distributed_compute_pytorch_amd.train --model convnet --gpus 2 --epochs 1
+    python -m distributed_compute_pytorch_amd.distributed.run --nproc-per-node 8 \
+        -m distributed_compute_pytorch_amd.train --model resnet50 --dtype bf16 --steps-per-epoch 100
+
+Launched without RANK in the environment it spawns ``--gpus`` ranks itself
+(like the reference's mp.spawn, main.py:150); under a launcher it runs as the
+given rank.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+from torch.utils.data import DataLoader
+
+from . import distributed as dist
+from .config import TrainConfig, parse_config
+
+
+def _device(cfg: TrainConfig, local_rank: int):
+    if not cfg.no_cuda and torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+        return torch.device("cuda", local_rank)
+    return torch.device("cpu")
+
+
+def _mnist_loaders(cfg, rank, world):
+    from .utils.data import DistributedSampler, MNISTIdx, SyntheticDataset
+
+    try:
+        if cfg.synthetic:
+            raise FileNotFoundError
+        tr, te = MNISTIdx(cfg.data_dir, True), MNISTIdx(cfg.data_dir, False)
+    except FileNotFoundError:
+        tr, te = SyntheticDataset(60000, seed=cfg.seed), SyntheticDataset(10000, seed=cfg.seed + 1)
+    s_tr = DistributedSampler(tr, world, rank, seed=cfg.seed)
+    s_te = DistributedSampler(te, world, rank, shuffle=False)
+    pin = not cfg.no_cuda and torch.cuda.is_available()
+    return (DataLoader(tr, batch_size=cfg.batch_size, sampler=s_tr, pin_memory=pin), s_tr,
+            DataLoader(te, batch_size=cfg.batch_size, sampler=s_te, pin_memory=pin))
+
+
+def run_rank(cfg: TrainConfig, rank: int, world: int, local_rank: int):
+    from . import ops
+    from . import workloads
+    from .parallel import DistributedDataParallel
+    from .utils import JsonLogger, load_checkpoint, save_checkpoint, save_model
+
+    device = _device(cfg, local_rank)
+    backend = cfg.backend if cfg.backend != "auto" else ("rccl" if device.type == "cuda" else "host")
+    if not dist.is_initialized():
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                device_id=local_rank if device.type == "cuda" else None)
+    torch.manual_seed(cfg.seed)
+    log = JsonLogger(rank, cfg.metrics_file, stream=sys.stdout)
+    mnist = cfg.model in ("convnet", "mlp")
+    wl = workloads.build(cfg.model, device, batch=cfg.batch_size, fused=device.type == "cuda",
+                         accum=cfg.grad_accum, channels_last=device.type == "cuda")
+    if mnist:
+        wl.amp = cfg.dtype == "bf16"
+    kw = {}
+    if cfg.bucket_cap_mb:
+        kw["bucket_cap_mb"] = cfg.bucket_cap_mb
+    if cfg.first_bucket_mb:
+        kw["first_bucket_mb"] = cfg.first_bucket_mb
+    if cfg.comm_dtype == "bf16":
+        kw["comm_dtype"] = torch.bfloat16
+    model = DistributedDataParallel(wl.model, device_ids=[local_rank] if device.type == "cuda" else None,
+                                    broadcast_buffers=cfg.broadcast_buffers,
+                                    find_unused_parameters=cfg.find_unused_parameters,
+                                    gradient_as_bucket_view=cfg.gradient_as_bucket_view, **kw)
+    opt = wl.make_optimizer(model.parameters())
+    for g in opt.param_groups:
+        g["lr"] = cfg.lr if mnist else g["lr"]
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=cfg.gamma)
+    start_epoch = 0
+    if cfg.resume and os.path.exists(cfg.resume):
+        meta = load_checkpoint(cfg.resume, model, opt, sched, map_location=device)
+        start_epoch = meta["epoch"] + 1
+        log.log(event="resumed", epoch=meta["epoch"])
+    log.log(event="config", rank0_device=str(device), world_size=world, config=cfg.to_json())
+
+    if mnist:
+        train_loader, train_sampler, test_loader = _mnist_loaders(cfg, rank, world)
+    for epoch in range(start_epoch, cfg.epochs):
+        model.train()
+        t0 = time.time()
+        seen = 0
+        if mnist:
+            train_sampler.set_epoch(epoch)
+            batches = iter(train_loader)
+            nsteps = len(train_loader) if not cfg.steps_per_epoch else min(cfg.steps_per_epoch, len(train_loader))
+        else:
+            batches = wl.data
+            nsteps = cfg.steps_per_epoch or 100
+        for b in range(nsteps):
+            opt.zero_grad(set_to_none=True)
+            for k in range(wl.accum):
+                bt = tuple(t.to(device, non_blocking=True) for t in next(batches))
+                ctx = model.no_sync() if k < wl.accum - 1 else _Null()
+                with ctx, torch.autocast(device.type, dtype=torch.bfloat16, enabled=wl.amp):
+                    loss = wl.loss_fn(model, bt) / wl.accum
+                loss.backward()
+                seen += bt[0].shape[0]
+            if cfg.clip_grad_norm > 0:
+                from .optim import clip_grad_norm_
+                clip_grad_norm_(model.parameters(), cfg.clip_grad_norm)
+            opt.step()
+            if b % cfg.log_every == 0:
+                t = loss.detach().float().clone() * wl.accum
+                dist.all_reduce(t, dist.ReduceOp.AVG if t.is_cuda else dist.ReduceOp.SUM)
+                if not t.is_cuda:
+                    t /= world
+                log.log(event="train", epoch=epoch, step=b, steps=nsteps, loss=round(t.item(), 6),
+                        lr=opt.param_groups[0]["lr"])
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.time() - t0
+        log.log(event="epoch", epoch=epoch, seconds=round(dt, 3),
+                samples_per_s=round(seen * world / max(dt, 1e-9), 1))
+        if mnist:
+            model.eval()
+            m = ops.EvalMetrics(device, log_probs=True)
+            with torch.no_grad():
+                for img, label in test_loader:
+                    m.update(model(img.to(device)), label.to(device))
+            avg, acc, n = m.compute()
+            log.log(event="eval", epoch=epoch, avg_loss=round(avg, 6), accuracy=round(acc, 6), samples=n)
+        sched.step()
+        if cfg.checkpoint:
+            save_checkpoint(cfg.checkpoint, model, opt, sched, epoch=epoch)
+    if cfg.save_model:
+        save_model(model, cfg.save_model)
+    dist.destroy_process_group()
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _spawn_entry(rank, cfg, world, port):
+    os.environ.update(MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=str(port))
+    run_rank(cfg, rank, world, rank)
+
+
+def main(argv=None):
+    cfg = parse_config(argv)
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        run_rank(cfg, int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]),
+                 int(os.environ.get("LOCAL_RANK", os.environ["RANK"])))
+        return
+    world = cfg.gpus
+    if not cfg.no_cuda and torch.cuda.is_available() and world > torch.cuda.device_count():
+        raise SystemExit(f"--gpus {world} but only {torch.cuda.device_count()} GPUs are visible")
+    from .distributed.launch import free_port, spawn
+
+    spawn(_spawn_entry, (cfg, world, int(os.environ.get("MASTER_PORT", free_port()))), nprocs=world)
+
+
+if __name__ == "__main__":
+    main()
