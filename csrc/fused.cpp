@@ -266,7 +266,8 @@ int dr_dtype(const at::Tensor& x) {
 // e.g. bf16 branch + fp32 residual stream -> fp32). seed/offset fully
 // determine the mask. out_dtype (when no residual) selects y's dtype.
 at::Tensor dropout_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual, double p, int64_t seed,
-                       int64_t offset, c10::optional<at::ScalarType> out_dtype) {
+                       int64_t offset, c10::optional<at::ScalarType> out_dtype,
+                       const c10::optional<at::Tensor>& offset_dev) {
   DCP_CHECK(x.is_cuda() && x.is_contiguous(), "dropout_fwd: contiguous device tensor required");
   c10::hip::HIPGuard guard(x.device().index());
   at::Tensor res;
@@ -279,17 +280,21 @@ at::Tensor dropout_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& res
   at::Tensor y = at::empty_like(x, x.options().dtype(yt));
   kern::dropout(dr_dtype(x), dr_dtype(y), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, y.data_ptr(),
                 x.numel(), static_cast<float>(p), static_cast<uint64_t>(seed), static_cast<uint64_t>(offset),
+                offset_dev.has_value() && offset_dev->defined() ? offset_dev->data_ptr<int64_t>() : nullptr,
                 stream_of(x));
   return y;
 }
 
-at::Tensor feature_dropout_fwd(const at::Tensor& x, double p, int64_t seed, int64_t offset) {
+at::Tensor feature_dropout_fwd(const at::Tensor& x, double p, int64_t seed, int64_t offset,
+                               const c10::optional<at::Tensor>& offset_dev) {
   DCP_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() >= 2, "feature_dropout: contiguous [N, C, ...] tensor");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t rows = x.size(0) * x.size(1);
   at::Tensor y = at::empty_like(x);
   kern::feature_dropout(dr_dtype(x), x.data_ptr(), y.data_ptr(), rows, rows ? x.numel() / rows : 0,
-                        static_cast<float>(p), static_cast<uint64_t>(seed), static_cast<uint64_t>(offset), stream_of(x));
+                        static_cast<float>(p), static_cast<uint64_t>(seed), static_cast<uint64_t>(offset),
+                        offset_dev.has_value() && offset_dev->defined() ? offset_dev->data_ptr<int64_t>() : nullptr,
+                        stream_of(x));
   return y;
 }
 
@@ -370,8 +375,10 @@ void bind(pybind11::module& m) {
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("dropout_fwd", &dropout_fwd, pybind11::arg("x"), pybind11::arg("residual"), pybind11::arg("p"),
-        pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("out_dtype") = pybind11::none());
-  m.def("feature_dropout_fwd", &feature_dropout_fwd);
+        pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("out_dtype") = pybind11::none(),
+        pybind11::arg("offset_dev") = pybind11::none());
+  m.def("feature_dropout_fwd", &feature_dropout_fwd, pybind11::arg("x"), pybind11::arg("p"), pybind11::arg("seed"),
+        pybind11::arg("offset"), pybind11::arg("offset_dev") = pybind11::none());
   m.def("bn_supported", [](int64_t C) { return kern::bn_supported(static_cast<int>(C)); });
   m.def("layer_norm_supported", &layer_norm_supported);
   m.def("layer_norm_fwd", &layer_norm_fwd, pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),

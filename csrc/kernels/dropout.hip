@@ -97,7 +97,10 @@ __device__ __forceinline__ bool al(const void* p, int a) { return (reinterpret_c
 template <int XD, int RD, bool RES>
 __global__ void __launch_bounds__(kT) dropout_kernel(const void* __restrict__ x, const void* __restrict__ res,
                                                      void* __restrict__ y, int64_t n, uint32_t thr, float scale,
-                                                     uint64_t seed, uint64_t offset) {
+                                                     uint64_t seed, uint64_t offset, const int64_t* offset_dev) {
+  // device-side Philox offset (graph-capture safe: a replay reads the value
+  // advanced by the previous replay, so every replay draws fresh masks)
+  if (offset_dev) offset += static_cast<uint64_t>(*offset_dev);
   using AX = E4<XD>;
   using AR = E4<RD>;
   const int64_t n4 = n >> 2;
@@ -140,7 +143,8 @@ __global__ void __launch_bounds__(kT) dropout_kernel(const void* __restrict__ x,
 template <int D>
 __global__ void __launch_bounds__(kT) feature_dropout_kernel(const void* __restrict__ x, void* __restrict__ y,
                                                              int64_t rows, int64_t inner, uint32_t thr, float scale,
-                                                             uint64_t seed, uint64_t offset) {
+                                                             uint64_t seed, uint64_t offset, const int64_t* offset_dev) {
+  if (offset_dev) offset += static_cast<uint64_t>(*offset_dev);
   using A = E4<D>;
   for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
     const U4 r = philox(seed, offset + static_cast<uint64_t>(row >> 2));
@@ -166,13 +170,14 @@ uint32_t dropout_threshold(float p) {
 }
 
 void dropout(int xdtype, int ydtype, const void* x, const void* res, void* y, int64_t n, float p, uint64_t seed,
-             uint64_t offset, hipStream_t s) {
+             uint64_t offset, const int64_t* offset_dev, hipStream_t s) {
   if (n <= 0) return;
   const uint32_t thr = dropout_threshold(p);
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   const dim3 g = grid_for((n + 3) / 4);
 #define DCP_DR(XD, RD, R) \
-  hipLaunchKernelGGL((dropout_kernel<XD, RD, R>), g, dim3(kT), 0, s, x, res, y, n, thr, scale, seed, offset)
+  hipLaunchKernelGGL((dropout_kernel<XD, RD, R>), g, dim3(kT), 0, s, x, res, y, n, thr, scale, seed, offset, \
+                     offset_dev)
   if (xdtype == DR_BF16 && ydtype == DR_BF16) {
     if (res) DCP_DR(DR_BF16, DR_BF16, true); else DCP_DR(DR_BF16, DR_BF16, false);
   } else if (xdtype == DR_BF16 && ydtype == DR_F32) {
@@ -186,15 +191,17 @@ void dropout(int xdtype, int ydtype, const void* x, const void* res, void* y, in
 }
 
 void feature_dropout(int dtype, const void* x, void* y, int64_t rows, int64_t inner, float p, uint64_t seed,
-                     uint64_t offset, hipStream_t s) {
+                     uint64_t offset, const int64_t* offset_dev, hipStream_t s) {
   if (rows <= 0) return;
   const uint32_t thr = dropout_threshold(p);
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   const dim3 g(static_cast<unsigned>(rows < 65535 ? rows : 65535));
   if (dtype == DR_BF16)
-    hipLaunchKernelGGL(feature_dropout_kernel<DR_BF16>, g, dim3(kT), 0, s, x, y, rows, inner, thr, scale, seed, offset);
+    hipLaunchKernelGGL(feature_dropout_kernel<DR_BF16>, g, dim3(kT), 0, s, x, y, rows, inner, thr, scale, seed, offset,
+                       offset_dev);
   else
-    hipLaunchKernelGGL(feature_dropout_kernel<DR_F32>, g, dim3(kT), 0, s, x, y, rows, inner, thr, scale, seed, offset);
+    hipLaunchKernelGGL(feature_dropout_kernel<DR_F32>, g, dim3(kT), 0, s, x, y, rows, inner, thr, scale, seed, offset,
+                       offset_dev);
 }
 
 }  // namespace kern

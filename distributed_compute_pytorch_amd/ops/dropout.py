@@ -1,10 +1,12 @@
 """Counter-based Philox dropout (csrc/kernels/dropout.hip).
 
 The mask is a function of (seed, offset, element index): nothing is stored,
-the backward regenerates it. Seeds come from torch's CPU generator, so
-``torch.manual_seed`` makes runs reproducible (the reference
-seeds every rank identically). ``dropout_add(x, residual, p)`` fuses the
-transformer residual add.
+the backward regenerates it. The seed is drawn from torch's CPU generator
+(``torch.manual_seed`` makes runs reproducible; SURVEY App. A14: the reference
+seeds every rank identically). The Philox offset lives in a device tensor that
+every call advances with a tiny kernel, so HIP-graph replays draw fresh masks
+(a host-side counter would be frozen into the captured graph).
+``dropout_add(x, residual, p)`` fuses the transformer residual add.
 """
 from __future__ import annotations
 
@@ -17,31 +19,61 @@ from .._ext import C as _C
 _OK = (torch.float32, torch.bfloat16)
 
 
+_RNG = {}
+
+
+def _rng(device):
+    """(seed, device offset tensor) for `device`; re-seeded when torch's
+    initial seed changes (torch.manual_seed)."""
+    key = (device.type, device.index)
+    cur = torch.initial_seed()
+    st = _RNG.get(key)
+    if st is None or st[2] != cur:
+        seed = int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+        st = (seed, torch.zeros(1, dtype=torch.int64, device=device), cur)
+        _RNG[key] = st
+    return st[0], st[1]
+
+
+def _take_offset(device, n):
+    """Snapshot the device offset for this call and advance it by n/4 Philox counters."""
+    seed, base = _rng(device)
+    used = base.clone()
+    base.add_((n + 3) // 4)
+    return seed, used
+
+
 def _seed():
     return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
 
 
 class _DropFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, p, seed):
+    def forward(ctx, x, residual, p, rng):
+        seed, off = rng
         ctx.p, ctx.seed, ctx.has_res, ctx.xdtype = p, seed, residual is not None, x.dtype
-        return _C.dropout_fwd(x, residual, p, seed, 0)
+        ctx.save_for_backward(off)
+        return _C.dropout_fwd(x, residual, p, seed, 0, None, off)
 
     @staticmethod
     def backward(ctx, gy):
-        gx = _C.dropout_fwd(gy.contiguous(), None, ctx.p, ctx.seed, 0, ctx.xdtype)
+        (off,) = ctx.saved_tensors
+        gx = _C.dropout_fwd(gy.contiguous(), None, ctx.p, ctx.seed, 0, ctx.xdtype, off)
         return gx, (gy if ctx.has_res else None), None, None
 
 
 class _FeatDropFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p, seed):
+    def forward(ctx, x, p, rng):
+        seed, off = rng
         ctx.p, ctx.seed = p, seed
-        return _C.feature_dropout_fwd(x, p, seed, 0)
+        ctx.save_for_backward(off)
+        return _C.feature_dropout_fwd(x, p, seed, 0, off)
 
     @staticmethod
     def backward(ctx, gy):
-        return _C.feature_dropout_fwd(gy.contiguous(), ctx.p, ctx.seed, 0), None, None
+        (off,) = ctx.saved_tensors
+        return _C.feature_dropout_fwd(gy.contiguous(), ctx.p, ctx.seed, 0, off), None, None
 
 
 def _usable(x):
@@ -52,7 +84,7 @@ def fused_dropout(x, p: float = 0.5, training: bool = True):
     if not training or p == 0.0:
         return x
     if _usable(x):
-        return _DropFn.apply(x, None, float(p), _seed())
+        return _DropFn.apply(x, None, float(p), _take_offset(x.device, x.numel()))
     return F.dropout(x, p, training)
 
 
@@ -61,7 +93,7 @@ def dropout_add(x, residual, p: float = 0.1, training: bool = True):
     if not training or p == 0.0:
         return residual + x
     if _usable(x) and residual.shape == x.shape and residual.dtype in _OK:
-        return _DropFn.apply(x, residual.contiguous(), float(p), _seed())
+        return _DropFn.apply(x, residual.contiguous(), float(p), _take_offset(x.device, x.numel()))
     return residual + F.dropout(x, p, training)
 
 
@@ -69,7 +101,7 @@ def fused_feature_dropout(x, p: float = 0.5, training: bool = True):
     if not training or p == 0.0:
         return x
     if _usable(x) and x.dim() >= 3:
-        return _FeatDropFn.apply(x, float(p), _seed())
+        return _FeatDropFn.apply(x, float(p), _take_offset(x.device, x.shape[0] * x.shape[1] * 4))
     return F.dropout2d(x, p, training)
 
 
