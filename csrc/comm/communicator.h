@@ -61,6 +61,8 @@ class Communicator {
   virtual WorkPtr barrier() = 0;
   // Tear down without waiting for peers (failure path).
   virtual void abort() {}
+  // raw handle of the device stream collectives run on (0 = none / host)
+  virtual int64_t stream_handle() const { return 0; }
   // Non-empty once the communicator hit an unrecoverable error.
   virtual std::string error() { return {}; }
 

@@ -138,6 +138,7 @@ class RcclCommunicator : public Communicator {
     }
   }
 
+  int64_t stream_handle() const override { return reinterpret_cast<int64_t>(stream_.stream()); }
   std::string backend() const override { return "rccl"; }
 
   WorkPtr all_reduce(at::Tensor& t, ReduceOp op) override {

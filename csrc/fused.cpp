@@ -28,10 +28,15 @@ int bn_dtype(const at::Tensor& x) {
 
 void check_nhwc(const at::Tensor& x, const char* what) {
   DCP_CHECK(x.is_cuda(), what, ": device tensor required");
-  DCP_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), what,
-            ": expected a channels_last 4-D tensor");
+  DCP_CHECK((x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)) || (x.dim() == 2 && x.is_contiguous()),
+            what, ": expected a channels_last 4-D or contiguous [N, C] tensor");
   DCP_CHECK(kern::bn_supported(static_cast<int>(x.size(1))), what, ": unsupported channel count ", x.size(1));
   DCP_CHECK(x.numel() / 8 < (int64_t(1) << 32), what, ": tensor too large");
+}
+
+// [N, C] row-major is NHWC with H = W = 1: both layouts are "channels innermost".
+at::MemoryFormat cl_fmt(const at::Tensor& x) {
+  return x.dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous;
 }
 
 const float* opt_ptr(const c10::optional<at::Tensor>& t) {
@@ -90,10 +95,10 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
   auto fopt = x.options().dtype(at::kFloat);
-  at::Tensor y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  at::Tensor y = at::empty_like(x, cl_fmt(x));
   at::Tensor res;
   if (residual.has_value() && residual->defined()) {
-    res = residual->contiguous(at::MemoryFormat::ChannelsLast);
+    res = residual->contiguous(cl_fmt(x));
     DCP_CHECK(res.sizes() == x.sizes() && res.scalar_type() == x.scalar_type(), "bn_act_fwd: residual mismatch");
   }
   at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
@@ -134,11 +139,11 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const c10::optional<at:
                                    bool training) {
   check_nhwc(x, "bn_act_bwd");
   c10::hip::HIPGuard guard(x.device().index());
-  at::Tensor g = gy.contiguous(at::MemoryFormat::ChannelsLast);
+  at::Tensor g = gy.contiguous(cl_fmt(x));
   if (g.scalar_type() != x.scalar_type()) g = g.to(x.scalar_type());
   at::Tensor g2;
   if (gy2_opt.has_value() && gy2_opt->defined()) {
-    g2 = gy2_opt->contiguous(at::MemoryFormat::ChannelsLast);
+    g2 = gy2_opt->contiguous(cl_fmt(x));
     if (g2.scalar_type() != x.scalar_type()) g2 = g2.to(x.scalar_type());
     if (!has_res) {  // kernel sums only on the store_g path
       g = g + g2;
@@ -148,8 +153,8 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const c10::optional<at:
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
   auto fopt = x.options().dtype(at::kFloat);
-  at::Tensor dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
-  at::Tensor gres = has_res ? at::empty_like(x, at::MemoryFormat::ChannelsLast) : at::Tensor();
+  at::Tensor dx = at::empty_like(x, cl_fmt(x));
+  at::Tensor gres = has_res ? at::empty_like(x, cl_fmt(x)) : at::Tensor();
   const bool has_w = weight.has_value() && weight->defined();
   at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor dw = at::empty({C}, fopt);
@@ -255,6 +260,28 @@ at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& target,
   return d;
 }
 
+// ---------------------------------------------------------- log-softmax ---
+at::Tensor log_softmax_fwd(const at::Tensor& x, c10::optional<at::ScalarType> out_dtype) {
+  DCP_CHECK(x.is_cuda() && x.dim() >= 1, "log_softmax_fwd: device tensor required");
+  c10::hip::HIPGuard guard(x.device().index());
+  at::Tensor xc = x.contiguous();
+  const int64_t D = x.size(-1);
+  at::Tensor y = at::empty_like(xc, xc.options().dtype(out_dtype.has_value() ? *out_dtype : x.scalar_type()));
+  kern::log_softmax_forward(ln_dtype(xc), xc.data_ptr(), ln_dtype(y), y.data_ptr(), D ? xc.numel() / D : 0,
+                            static_cast<int>(D), stream_of(x));
+  return y;
+}
+
+at::Tensor log_softmax_bwd(const at::Tensor& gy, const at::Tensor& y, at::ScalarType x_dtype) {
+  c10::hip::HIPGuard guard(y.device().index());
+  at::Tensor g = gy.to(y.scalar_type()).contiguous();
+  const int64_t D = y.size(-1);
+  at::Tensor gx = at::empty_like(y, y.options().dtype(x_dtype));
+  kern::log_softmax_backward(ln_dtype(y), g.data_ptr(), y.data_ptr(), ln_dtype(gx), gx.data_ptr(),
+                             D ? y.numel() / D : 0, static_cast<int>(D), stream_of(y));
+  return gx;
+}
+
 // -------------------------------------------------------------- dropout ---
 int dr_dtype(const at::Tensor& x) {
   if (x.scalar_type() == at::kBFloat16) return kern::DR_BF16;
@@ -319,27 +346,46 @@ bool maxpool_supported(const at::Tensor& x, int64_t k, int64_t p) {
          x.is_contiguous(at::MemoryFormat::ChannelsLast);
 }
 
-// Returns (y [NHWC], idx uint8 window offsets).
-std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p) {
+kern::PoolEpi pool_epi(bool relu, double drop_p, int64_t seed, const c10::optional<at::Tensor>& offset_dev) {
+  kern::PoolEpi e;
+  e.relu = relu ? 1 : 0;
+  if (drop_p > 0.0) {
+    DCP_CHECK(drop_p < 1.0, "fused pool: dropout p must be < 1");
+    e.thr = kern::dropout_threshold(static_cast<float>(drop_p));
+    e.scale = static_cast<float>(1.0 / (1.0 - drop_p));
+    e.seed = static_cast<uint64_t>(seed);
+    if (offset_dev.has_value() && offset_dev->defined()) e.offset_dev = offset_dev->data_ptr<int64_t>();
+  }
+  return e;
+}
+
+// Returns (y [NHWC], idx uint8 window offsets). Optional fused epilogue:
+// y = Dropout2d_p(relu(maxpool(x))) (see pool.hip).
+std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p, bool relu, double drop_p,
+                                      int64_t seed, const c10::optional<at::Tensor>& offset_dev) {
   DCP_CHECK(maxpool_supported(x, k, p), "maxpool2d_fwd: needs channels_last bf16/fp32, C % 8 == 0");
   c10::hip::HIPGuard guard(x.device().index());
   auto g = pool_geom(x, k, s, p);
   at::Tensor y = at::empty({g.N, g.C, g.OH, g.OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor idx = at::empty({static_cast<int64_t>(g.N) * g.OH * g.OW * g.C}, x.options().dtype(at::kByte));
   kern::maxpool2d_forward(x.scalar_type() == at::kBFloat16 ? kern::POOL_BF16 : kern::POOL_F32, x.data_ptr(),
-                          y.data_ptr(), idx.data_ptr<uint8_t>(), g, stream_of(x));
+                          y.data_ptr(), idx.data_ptr<uint8_t>(), g, pool_epi(relu, drop_p, seed, offset_dev),
+                          stream_of(x));
   return {y, idx};
 }
 
-at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& idx, const at::Tensor& x, int64_t k, int64_t s,
-                         int64_t p) {
-  c10::hip::HIPGuard guard(x.device().index());
-  auto g = pool_geom(x, k, s, p);
+// gx: [in_shape] channels_last, gy's dtype.
+at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& idx, at::IntArrayRef in_shape, int64_t k, int64_t s,
+                         int64_t p, double drop_p, int64_t seed, const c10::optional<at::Tensor>& offset_dev) {
+  DCP_CHECK(in_shape.size() == 4, "maxpool2d_bwd: 4-D input shape expected");
+  c10::hip::HIPGuard guard(gy.device().index());
+  at::Tensor gx = at::empty(in_shape, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto g = pool_geom(gx, k, s, p);
   at::Tensor go = gy.contiguous(at::MemoryFormat::ChannelsLast);
-  if (go.scalar_type() != x.scalar_type()) go = go.to(x.scalar_type());
-  at::Tensor gx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
-  kern::maxpool2d_backward(x.scalar_type() == at::kBFloat16 ? kern::POOL_BF16 : kern::POOL_F32, go.data_ptr(),
-                           idx.data_ptr<uint8_t>(), gx.data_ptr(), g, stream_of(x));
+  DCP_CHECK(go.size(2) == g.OH && go.size(3) == g.OW && idx.numel() == go.numel(), "maxpool2d_bwd: shape mismatch");
+  kern::maxpool2d_backward(gy.scalar_type() == at::kBFloat16 ? kern::POOL_BF16 : kern::POOL_F32, go.data_ptr(),
+                           idx.data_ptr<uint8_t>(), gx.data_ptr(), g, pool_epi(false, drop_p, seed, offset_dev),
+                           stream_of(gy));
   return gx;
 }
 
@@ -369,11 +415,34 @@ void eval_metrics_(at::Tensor& acc, const at::Tensor& scores, const at::Tensor& 
                      acc.data_ptr<double>(), stream_of(sc));
 }
 
+// Ends a stream capture left open by a failed torch.cuda.graph block (a
+// capture invalidated mid-way can leave the stream, and the streams forked
+// into it, in capture mode, poisoning every later launch on the device).
+bool abort_capture(int64_t stream_ptr) {
+  auto s = reinterpret_cast<hipStream_t>(stream_ptr);
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (st == hipStreamCaptureStatusNone) return false;
+  hipGraph_t g = nullptr;
+  (void)hipStreamEndCapture(s, &g);
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  return true;
+}
+
 void bind(pybind11::module& m) {
+  m.def("abort_capture", &abort_capture, "end a dangling stream capture; true if one was open");
   m.def("eval_metrics_", &eval_metrics_);
   m.def("maxpool_supported", &maxpool_supported);
-  m.def("maxpool2d_fwd", &maxpool2d_fwd);
-  m.def("maxpool2d_bwd", &maxpool2d_bwd);
+  m.def("maxpool2d_fwd", &maxpool2d_fwd, pybind11::arg("x"), pybind11::arg("k"), pybind11::arg("s"),
+        pybind11::arg("p"), pybind11::arg("relu") = false, pybind11::arg("drop_p") = 0.0,
+        pybind11::arg("seed") = 0, pybind11::arg("offset_dev") = pybind11::none());
+  m.def("maxpool2d_bwd", &maxpool2d_bwd, pybind11::arg("gy"), pybind11::arg("idx"), pybind11::arg("in_shape"),
+        pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("drop_p") = 0.0,
+        pybind11::arg("seed") = 0, pybind11::arg("offset_dev") = pybind11::none());
   m.def("dropout_fwd", &dropout_fwd, pybind11::arg("x"), pybind11::arg("residual"), pybind11::arg("p"),
         pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("out_dtype") = pybind11::none(),
         pybind11::arg("offset_dev") = pybind11::none());
@@ -385,6 +454,8 @@ void bind(pybind11::module& m) {
         pybind11::arg("eps"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("layer_norm_bwd", &layer_norm_bwd);
   m.def("cross_entropy_fwd", &cross_entropy_fwd);
+  m.def("log_softmax_fwd", &log_softmax_fwd, pybind11::arg("x"), pybind11::arg("out_dtype") = pybind11::none());
+  m.def("log_softmax_bwd", &log_softmax_bwd);
   m.def("cross_entropy_bwd", &cross_entropy_bwd);
   m.def("bn_act_fwd", &bn_act_fwd, "fused NHWC BatchNorm(+residual)(+ReLU) forward");
   m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward");

@@ -30,5 +30,12 @@ void xent_backward(int dtype, const void* logits, int64_t ld, const int64_t* tar
                    const float* dloss, int dloss_stride, int64_t rows, int V, int64_t ignore_index,
                    float label_smoothing, void* dlogits, int64_t ld_out, hipStream_t s);
 
+// Row log-softmax over contiguous [rows, D] (any D; tuned for small class
+// counts). y may be a wider dtype than x (bf16 logits -> fp32 log-probs).
+void log_softmax_forward(int xdtype, const void* x, int ydtype, void* y, int64_t rows, int D, hipStream_t s);
+// gx = gy - exp(y) * rowsum(gy); gy has y's dtype, gx has x's.
+void log_softmax_backward(int ydtype, const void* gy, const void* y, int xdtype, void* gx, int64_t rows, int D,
+                          hipStream_t s);
+
 }  // namespace kern
 }  // namespace dcp

@@ -8,9 +8,17 @@
 // the gradients whose arg-max offset points at it. No zero-fill pass, no
 // atomics, every input-gradient element written exactly once.
 //
-// Parity: SURVEY §2f K5/K20 (max_pool2d_with_indices fwd/bwd, P1).
+// Optional fused epilogue (reference ConvNet: relu → maxpool → Dropout2d,
+// main.py:33-36): ReLU commutes with max, so relu(max) is applied to the 4×
+// smaller pooled tensor, and the per-(n, c) dropout scale is regenerated from
+// Philox in both directions — one kernel each way replaces ReLU, pool,
+// bernoulli, div and mul (and their backward counterparts).
+//
+// Parity: SURVEY §2f K4-K6 / K19-K21 (relu, max_pool2d_with_indices,
+// feature_dropout fwd/bwd; P1 "pool bwd fused with the ReLU bwd").
 #include <hip/hip_runtime.h>
 
+#include "philox.h"
 #include "pool_kernels.h"
 
 namespace dcp {
@@ -62,9 +70,22 @@ struct P8<POOL_F32> {
   }
 };
 
+// dropout scales of channels c0..c0+7 of sample n (c0 % 8 == 0)
+__device__ __forceinline__ void drop_scales(const PoolEpi& e, uint64_t off, int n, int C, int c0, float (&m)[8]) {
+  const int64_t row = static_cast<int64_t>(n) * C + c0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const U4 r = philox(e.seed, off + static_cast<uint64_t>((row + 4 * h) >> 2));
+    const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m[4 * h + k] = keep(rr[k], e.thr) ? e.scale : 0.f;
+  }
+}
+
 template <int D>
 __global__ void __launch_bounds__(kT) maxpool_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
-                                                         uint8_t* __restrict__ idx, PoolGeom g) {
+                                                         uint8_t* __restrict__ idx, PoolGeom g, PoolEpi e) {
+  const uint64_t doff = e.offset + (e.offset_dev ? static_cast<uint64_t>(*e.offset_dev) : 0);
   const int cv = g.C / 8;
   const int64_t total = static_cast<int64_t>(g.N) * g.OH * g.OW * cv;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x; t < total;
@@ -101,6 +122,20 @@ __global__ void __launch_bounds__(kT) maxpool_fwd_kernel(const void* __restrict_
         }
       }
     }
+    if (e.relu) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (!(m[k] > 0.f)) {  // ReLU (NaN stays NaN like ATen's relu)
+          if (m[k] == m[k]) m[k] = 0.f;
+          a[k] = 255;
+        }
+    }
+    if (e.thr) {
+      float sc[8];
+      drop_scales(e, doff, n, g.C, c8 * 8, sc);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m[k] *= sc[k];
+    }
     P8<D>::st(y, t * 8, m);
     uint2 packed;
     packed.x = a[0] | (a[1] << 8) | (a[2] << 16) | (static_cast<uint32_t>(a[3]) << 24);
@@ -111,7 +146,8 @@ __global__ void __launch_bounds__(kT) maxpool_fwd_kernel(const void* __restrict_
 
 template <int D>
 __global__ void __launch_bounds__(kT) maxpool_bwd_kernel(const void* __restrict__ gy, const uint8_t* __restrict__ idx,
-                                                         void* __restrict__ gx, PoolGeom g) {
+                                                         void* __restrict__ gx, PoolGeom g, PoolEpi e) {
+  const uint64_t doff = e.offset + (e.offset_dev ? static_cast<uint64_t>(*e.offset_dev) : 0);
   const int cv = g.C / 8;
   const int64_t total = static_cast<int64_t>(g.N) * g.H * g.W * cv;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x; t < total;
@@ -147,6 +183,12 @@ __global__ void __launch_bounds__(kT) maxpool_bwd_kernel(const void* __restrict_
         }
       }
     }
+    if (e.thr) {
+      float sc[8];
+      drop_scales(e, doff, n, g.C, c8 * 8, sc);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] *= sc[k];
+    }
     P8<D>::st(gx, t * 8, acc);
   }
 }
@@ -160,16 +202,20 @@ inline dim3 grid_for(int64_t work) {
 
 }  // namespace
 
-void maxpool2d_forward(int dtype, const void* x, void* y, uint8_t* idx, const PoolGeom& g, hipStream_t s) {
+void maxpool2d_forward(int dtype, const void* x, void* y, uint8_t* idx, const PoolGeom& g, const PoolEpi& e,
+                       hipStream_t s) {
   const dim3 grid = grid_for(static_cast<int64_t>(g.N) * g.OH * g.OW * (g.C / 8));
-  if (dtype == POOL_BF16) hipLaunchKernelGGL(maxpool_fwd_kernel<POOL_BF16>, grid, dim3(kT), 0, s, x, y, idx, g);
-  else hipLaunchKernelGGL(maxpool_fwd_kernel<POOL_F32>, grid, dim3(kT), 0, s, x, y, idx, g);
+  if (dtype == POOL_BF16) hipLaunchKernelGGL(maxpool_fwd_kernel<POOL_BF16>, grid, dim3(kT), 0, s, x, y, idx, g, e);
+  else hipLaunchKernelGGL(maxpool_fwd_kernel<POOL_F32>, grid, dim3(kT), 0, s, x, y, idx, g, e);
 }
 
-void maxpool2d_backward(int dtype, const void* gy, const uint8_t* idx, void* gx, const PoolGeom& g, hipStream_t s) {
+void maxpool2d_backward(int dtype, const void* gy, const uint8_t* idx, void* gx, const PoolGeom& g,
+                        const PoolEpi& e, hipStream_t s) {
   const dim3 grid = grid_for(static_cast<int64_t>(g.N) * g.H * g.W * (g.C / 8));
-  if (dtype == POOL_BF16) hipLaunchKernelGGL(maxpool_bwd_kernel<POOL_BF16>, grid, dim3(kT), 0, s, gy, idx, gx, g);
-  else hipLaunchKernelGGL(maxpool_bwd_kernel<POOL_F32>, grid, dim3(kT), 0, s, gy, idx, gx, g);
+  if (dtype == POOL_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<POOL_BF16>, grid, dim3(kT), 0, s, gy, idx, gx, g, e);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<POOL_F32>, grid, dim3(kT), 0, s, gy, idx, gx, g, e);
 }
 
 }  // namespace kern

@@ -184,6 +184,79 @@ __global__ void __launch_bounds__(kT) xent_bwd_kernel(const void* __restrict__ l
   for (int j = tail0 + threadIdx.x; j < V; j += kT) st1(j, grad(j, ldx(row, j, DT)));
 }
 
+
+// ---- row log-softmax (classifier heads: ConvNet [B, 10]) ----
+// One wave64 per row, rows grid-strided over 4-wave workgroups. Lanes stride
+// the row (D is small: the head's class count), wave-shuffle max and sum-exp.
+__device__ __forceinline__ void stx(void* p, int64_t i, int dt, float v) {
+  if (dt == LN_BF16) static_cast<uint16_t*>(p)[i] = f2bf(v);
+  else static_cast<float*>(p)[i] = v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(kT) log_softmax_fwd_kernel(const void* __restrict__ x, int xdt,
+                                                             void* __restrict__ y, int ydt, int64_t rows, int D) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * (kT / 64) + (threadIdx.x >> 6); r < rows;
+       r += static_cast<int64_t>(gridDim.x) * (kT / 64)) {
+    const int64_t base = r * D;
+    float m = -INFINITY;
+    for (int j = lane; j < D; j += 64) m = fmaxf(m, ldx(x, base + j, xdt));
+    m = wave_max(m);
+    float se = 0.f;
+    for (int j = lane; j < D; j += 64) se += __expf(ldx(x, base + j, xdt) - m);
+    const float l = m + __logf(wave_sum(se));
+    for (int j = lane; j < D; j += 64) stx(y, base + j, ydt, ldx(x, base + j, xdt) - l);
+  }
+}
+
+// gx = gy - softmax * sum(gy), softmax = exp(y)
+__global__ void __launch_bounds__(kT) log_softmax_bwd_kernel(const void* __restrict__ gy, const void* __restrict__ y,
+                                                             int ydt, void* __restrict__ gx, int xdt, int64_t rows,
+                                                             int D) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * (kT / 64) + (threadIdx.x >> 6); r < rows;
+       r += static_cast<int64_t>(gridDim.x) * (kT / 64)) {
+    const int64_t base = r * D;
+    float sg = 0.f;
+    for (int j = lane; j < D; j += 64) sg += ldx(gy, base + j, ydt);
+    sg = wave_sum(sg);
+    for (int j = lane; j < D; j += 64)
+      stx(gx, base + j, xdt, ldx(gy, base + j, ydt) - __expf(ldx(y, base + j, ydt)) * sg);
+  }
+}
+
+}  // namespace
+
+void log_softmax_forward(int xdtype, const void* x, int ydtype, void* y, int64_t rows, int D, hipStream_t s) {
+  if (rows <= 0) return;
+  int64_t g = (rows + kT / 64 - 1) / (kT / 64);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(log_softmax_fwd_kernel, dim3(static_cast<unsigned>(g)), dim3(kT), 0, s, x, xdtype, y, ydtype,
+                     rows, D);
+}
+
+void log_softmax_backward(int ydtype, const void* gy, const void* y, int xdtype, void* gx, int64_t rows, int D,
+                          hipStream_t s) {
+  if (rows <= 0) return;
+  int64_t g = (rows + kT / 64 - 1) / (kT / 64);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(log_softmax_bwd_kernel, dim3(static_cast<unsigned>(g)), dim3(kT), 0, s, gy, y, ydtype, gx,
+                     xdtype, rows, D);
+}
+
+namespace {
 }  // namespace
 
 void xent_forward(int dtype, const void* logits, int64_t ld, const int64_t* target, int64_t rows, int V,

@@ -155,6 +155,15 @@ class GroupMember:
 _state = {"default": None, "groups": [], "group_count": 0}
 
 
+def _comm_stream_handles() -> List[int]:
+    """Raw HIP stream handles of every live RCCL communicator (graph-capture recovery)."""
+    out = []
+    for pg in [_state["default"], *_state["groups"]]:
+        if pg is not None and pg._rccl is not None:
+            out.append(int(pg._rccl.stream_handle))
+    return out
+
+
 def is_available() -> bool:
     return True
 

@@ -10,6 +10,11 @@ Parameter registration order and names match the reference exactly
 are identical. The reference applies ``Dropout2d`` to the 2-D
 fc1 activation, which acts element-wise; ``nn.Dropout`` is
 used for ``dropout2`` so behaviour is the same without the 2.x warning.
+
+``fused=True`` (GPU) runs the MI355X path with identical parameters and
+state_dict: conv2 → [ReLU + max-pool + Dropout2d] as one NHWC kernel each
+way, fc1 → [BatchNorm1d + ReLU] on the fused BN kernels, Philox dropout, and a
+wave-per-row log-softmax.
 """
 from __future__ import annotations
 
@@ -17,19 +22,24 @@ import torch
 from torch import nn
 from torch.nn import functional as F
 
+from ..ops.batchnorm import BatchNormAct1d
+
 
 class ConvNet(nn.Module):
-    def __init__(self):
+    def __init__(self, fused: bool = False):
         super().__init__()
+        self.fused = fused
         self.conv1 = nn.Conv2d(1, 32, 3, 1)
         self.conv2 = nn.Conv2d(32, 64, 3, 1)
         self.dropout1 = nn.Dropout2d(0.25)
         self.dropout2 = nn.Dropout(0.5)
         self.fc1 = nn.Linear(9216, 128)
         self.fc2 = nn.Linear(128, 10)
-        self.batchnorm = nn.BatchNorm1d(128)
+        self.batchnorm = BatchNormAct1d(128, act=fused, fused=fused)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.fused and x.is_cuda:
+            return self._forward_fused(x)
         x = F.relu(self.conv1(x))
         x = F.relu(self.conv2(x))
         x = F.max_pool2d(x, 2)
@@ -41,3 +51,14 @@ class ConvNet(nn.Module):
         x = self.dropout2(x)
         x = self.fc2(x)
         return F.log_softmax(x, dim=1)
+
+    def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
+        from ..ops import fused_dropout, fused_log_softmax, relu_max_pool2d_dropout
+
+        x = F.relu(self.conv1(x))
+        x = self.conv2(x).contiguous(memory_format=torch.channels_last)
+        x = relu_max_pool2d_dropout(x, 2, 2, 0, self.dropout1.p, self.training)
+        x = torch.flatten(x, 1)
+        x = self.batchnorm(self.fc1(x))  # BN1d + ReLU
+        x = fused_dropout(x, self.dropout2.p, self.training)
+        return fused_log_softmax(self.fc2(x), 1)

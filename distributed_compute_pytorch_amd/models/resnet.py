@@ -63,12 +63,14 @@ class BottleneckStage(nn.Sequential):
     """nn.Sequential of bottlenecks (same state_dict keys) that threads the
     dual-output BN alias from each block into the next block's residual."""
 
+    use_dual = True
+
     def forward(self, x):
         blocks = list(self)
         ident = None
         for i, blk in enumerate(blocks):
             nxt = blocks[i + 1] if i + 1 < len(blocks) else None
-            dual = nxt is not None and nxt.downsample is None
+            dual = self.use_dual and nxt is not None and nxt.downsample is None
             out = blk(x, ident, dual=dual)
             x, ident = (out if dual else (out, None))
         return x
@@ -81,13 +83,16 @@ def _downsample(cin, cout, stride, fused_bn):
 
 class ResNet(nn.Module):
     def __init__(self, block: Type[Bottleneck], layers: List[int], num_classes: int = 1000,
-                 zero_init_residual: bool = False, fused_bn: bool = False):
+                 zero_init_residual: bool = False, fused_bn: bool = False, fused_pool: Optional[bool] = None,
+                 dual_bn: bool = True):
         super().__init__()
         self.inplanes = 64
         self.fused_bn = fused_bn
+        self.dual_bn = dual_bn
+        fused_pool = fused_bn if fused_pool is None else fused_pool
         self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
         self.bn1 = BatchNormAct2d(64, act=True, fused=fused_bn)
-        self.maxpool = (FusedMaxPool2d if fused_bn else nn.MaxPool2d)(kernel_size=3, stride=2, padding=1)
+        self.maxpool = (FusedMaxPool2d if fused_pool else nn.MaxPool2d)(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
@@ -113,7 +118,9 @@ class ResNet(nn.Module):
         self.inplanes = width * block.expansion
         for _ in range(1, blocks):
             layers.append(block(self.inplanes, width, fused_bn=self.fused_bn))
-        return BottleneckStage(*layers)
+        stage = BottleneckStage(*layers)
+        stage.use_dual = self.dual_bn
+        return stage
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.maxpool(self.bn1(self.conv1(x)))

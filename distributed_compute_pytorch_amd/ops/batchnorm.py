@@ -75,3 +75,24 @@ def bn_act(x, weight, bias, running_mean, running_var, num_batches_tracked, trai
     if training and num_batches_tracked is not None:
         num_batches_tracked.add_(1)
     return _BNActFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual)
+
+
+class BatchNormAct1d(nn.BatchNorm1d):
+    """``nn.BatchNorm1d`` over [N, C] (+ReLU) on the same fused kernels: a
+    row-major [N, C] tensor is NHWC with H = W = 1 (reference ConvNet's
+    fc1 → BatchNorm1d(128) → ReLU, main.py:39-41)."""
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1, act: bool = True,
+                 fused: bool = False):
+        super().__init__(num_features, eps=eps, momentum=momentum)
+        self.act = act
+        self.fused = fused
+
+    def forward(self, x: torch.Tensor):
+        if (self.fused and x.is_cuda and x.dim() == 2 and x.dtype in (torch.bfloat16, torch.float32)
+                and x.is_contiguous() and _C.bn_supported(x.shape[1])
+                and (self.training or self.track_running_stats)):
+            return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.num_batches_tracked,
+                          self.training, self.momentum, self.eps, None, self.act)
+        y = super().forward(x)
+        return F.relu(y) if self.act else y

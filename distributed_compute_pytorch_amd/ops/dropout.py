@@ -101,7 +101,7 @@ def fused_feature_dropout(x, p: float = 0.5, training: bool = True):
     if not training or p == 0.0:
         return x
     if _usable(x) and x.dim() >= 3:
-        return _FeatDropFn.apply(x, float(p), _take_offset(x.device, x.shape[0] * x.shape[1] * 4))
+        return _FeatDropFn.apply(x, float(p), _take_offset(x.device, x.shape[0] * x.shape[1]))
     return F.dropout2d(x, p, training)
 
 

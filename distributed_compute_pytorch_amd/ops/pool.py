@@ -1,4 +1,6 @@
-"""NHWC max-pool with uint8 arg-max and gather backward (csrc/kernels/pool.hip)."""
+"""NHWC max-pool with uint8 arg-max and gather backward (csrc/kernels/pool.hip),
+optionally fused with ReLU and channel dropout (the reference ConvNet's
+relu → max_pool2d → Dropout2d, main.py:33-36)."""
 from __future__ import annotations
 
 import torch
@@ -10,26 +12,40 @@ from .._ext import C as _C
 
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p):
-        y, idx = _C.maxpool2d_fwd(x, k, s, p)
-        ctx.save_for_backward(idx)
-        ctx.geom = (k, s, p)
-        ctx.shape, ctx.dtype, ctx.device = x.shape, x.dtype, x.device
+    def forward(ctx, x, k, s, p, relu, drop_p, rng):
+        seed, off = rng if rng is not None else (0, None)
+        y, idx = _C.maxpool2d_fwd(x, k, s, p, relu, drop_p, seed, off)
+        ctx.save_for_backward(idx, off if off is not None else idx.new_empty(0))
+        ctx.geom = (k, s, p, drop_p, seed)
+        ctx.shape = tuple(x.shape)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        (idx,) = ctx.saved_tensors
-        k, s, p = ctx.geom
-        like = torch.empty(ctx.shape, dtype=ctx.dtype, device=ctx.device).contiguous(
-            memory_format=torch.channels_last)
-        return _C.maxpool2d_bwd(gy, idx, like, k, s, p), None, None, None
+        idx, off = ctx.saved_tensors
+        k, s, p, drop_p, seed = ctx.geom
+        gx = _C.maxpool2d_bwd(gy, idx, list(ctx.shape), k, s, p, drop_p, seed, off if off.numel() else None)
+        return gx, None, None, None, None, None, None
 
 
 def fused_max_pool2d(x, kernel_size: int = 3, stride: int = 2, padding: int = 0):
     if _C.maxpool_supported(x, kernel_size, padding):
-        return _MaxPoolFn.apply(x, kernel_size, stride, padding)
+        return _MaxPoolFn.apply(x, kernel_size, stride, padding, False, 0.0, None)
     return F.max_pool2d(x, kernel_size, stride, padding)
+
+
+def relu_max_pool2d_dropout(x, kernel_size: int = 2, stride: int = None, padding: int = 0, p: float = 0.0,
+                            training: bool = True):
+    """Dropout2d_p(max_pool2d(relu(x))) in one kernel each way (NHWC bf16/fp32, C % 8 == 0);
+    falls back to the ATen composition otherwise."""
+    stride = kernel_size if stride is None else stride
+    drop = p if training else 0.0
+    if _C.maxpool_supported(x, kernel_size, padding):
+        from .dropout import _take_offset
+
+        rng = _take_offset(x.device, x.shape[0] * x.shape[1]) if drop > 0 else None
+        return _MaxPoolFn.apply(x, kernel_size, stride, padding, True, float(drop), rng)
+    return F.dropout2d(F.max_pool2d(F.relu(x), kernel_size, stride, padding), drop, training)
 
 
 class FusedMaxPool2d(nn.MaxPool2d):

@@ -46,6 +46,16 @@ def capture_stream(device=None) -> torch.cuda.Stream:
     return _STREAMS[dev]
 
 
+def _comm_streams():
+    """Raw handles of the communicator streams forked into a capture."""
+    try:
+        from ..distributed import _comm_stream_handles
+
+        return _comm_stream_handles()
+    except Exception:
+        return []
+
+
 class CapturedStep:
     def __init__(self, step_fn: Callable, static_inputs: Sequence[torch.Tensor], warmup: int = 3,
                  pool=None, stream: torch.cuda.Stream = None):
@@ -67,8 +77,18 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool, stream=s):
-            self.static_out = self.step_fn(*self.static_inputs)
+        # thread_local: the communicator watchdog thread polls events while we
+        # capture; in the default global mode that would invalidate the capture
+        try:
+            with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
+                self.static_out = self.step_fn(*self.static_inputs)
+        except Exception:
+            from .._ext import C as _C
+
+            _C.abort_capture(s.cuda_stream)
+            for extra in _comm_streams():
+                _C.abort_capture(extra)
+            raise
         self.graph = g
 
     def recapture(self):

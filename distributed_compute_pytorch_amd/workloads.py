@@ -104,7 +104,7 @@ def build(name: str, device, batch: Optional[int] = None, fused: bool = True, se
                                                 nsp_labels=bt[4]), b, T, accum=accum or 1)
     if name == "convnet":
         b = batch or 128
-        m = models.ConvNet().to(device)
+        m = models.ConvNet(fused=fused and device.type == "cuda").to(device)
         data = SyntheticBatches(b, (1, 28, 28), 10, device, pool=4)
         return Workload(name, m, data, lambda params: dopt.Adadelta(params, lr=1e-3),
                         lambda model, bt: F.nll_loss(model(bt[0]), bt[1]), b, None, amp=False)

@@ -102,7 +102,11 @@ def test_maxpool_nhwc(cuda, dtype, shape, k, s, p):
         # and identical per-sample gradient mass
         same = torch.isclose(xo.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
         assert same.float().mean().item() > 0.999
-        torch.testing.assert_close(xo.grad.float().sum((1, 2, 3)), xr.grad.sum((1, 2, 3)), rtol=1e-2, atol=1e-1)
+        # per-sample gradient mass: exact up to bf16 rounding of ~numel(y)
+        # accumulated values (random-walk error ~ 2^-9 * sqrt(n))
+        n_out = yr[0].numel()
+        torch.testing.assert_close(xo.grad.float().sum((1, 2, 3)), xr.grad.sum((1, 2, 3)), rtol=0,
+                                   atol=0.01 * n_out ** 0.5)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -133,6 +137,11 @@ def test_bn_dual_output_sums_gradients(cuda, dtype):
         return xx.grad, rr.grad, ww.grad, bb.grad
 
     a, bq = run(True), run(False)
-    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=5e-2)
     for u, v in zip(a, bq):
-        torch.testing.assert_close(u.float(), v.float(), **tol)
+        if dtype == torch.float32:
+            torch.testing.assert_close(u.float(), v.float(), rtol=1e-4, atol=1e-4)
+        else:
+            # dual sums g1 + g2 in fp32 inside the kernel; the reference path
+            # rounds the sum to bf16 first — compare in norm
+            rel = float((u.float() - v.float()).norm() / v.float().norm())
+            assert rel < 2e-2, rel

@@ -1,0 +1,146 @@
+"""Fused ConvNet path (reference model, main.py:20-45): BN1d+ReLU, fused
+relu+maxpool+Dropout2d, log-softmax — each against the fp32 ATen composition."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn1d_relu_matches_aten(cuda, dtype):
+    from distributed_compute_pytorch_amd.ops import BatchNormAct1d
+
+    torch.manual_seed(0)
+    ref = torch.nn.BatchNorm1d(128).to(cuda)
+    ours = BatchNormAct1d(128, act=True, fused=True).to(cuda)
+    with torch.no_grad():
+        ref.weight.uniform_(0.5, 1.5)
+        ref.bias.normal_()
+    ours.load_state_dict(ref.state_dict())
+    x = torch.randn(128, 128, device=cuda) * 3 + 1
+    xr = x.clone().requires_grad_()
+    xo = x.to(dtype).requires_grad_()
+    yr = F.relu(ref(xr))
+    yo = ours(xo)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    yo.backward(g.to(dtype))
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(yo.float(), yr, **tol)
+    torch.testing.assert_close(ours.running_mean, ref.running_mean, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(ours.running_var, ref.running_var, rtol=1e-3, atol=1e-3)
+    assert int(ours.num_batches_tracked) == int(ref.num_batches_tracked) == 1
+    rel = lambda a, b: float((a.float() - b).norm() / b.norm())
+    lim = 1e-4 if dtype == torch.float32 else 2e-2
+    assert rel(xo.grad, xr.grad) < lim
+    assert rel(ours.weight.grad, ref.weight.grad) < lim
+    assert rel(ours.bias.grad, ref.bias.grad) < lim
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(128, 10), (64, 1000), (7, 3)])
+def test_log_softmax_matches_aten(cuda, dtype, shape):
+    from distributed_compute_pytorch_amd.ops import fused_log_softmax
+
+    torch.manual_seed(0)
+    x = (torch.randn(shape, device=cuda) * 4).to(dtype)
+    xr = x.float().requires_grad_()
+    xo = x.clone().requires_grad_()
+    yr = F.log_softmax(xr, 1)
+    yo = fused_log_softmax(xo, 1)
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(yo.float(), yr, **tol)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    yo.backward(g.to(yo.dtype))
+    torch.testing.assert_close(xo.grad.float(), xr.grad, **tol)
+
+
+def test_log_softmax_autocast_outputs_fp32(cuda):
+    from distributed_compute_pytorch_amd.ops import fused_log_softmax
+
+    x = torch.randn(32, 10, device=cuda, dtype=torch.bfloat16)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = fused_log_softmax(x, 1)
+    assert y.dtype == torch.float32
+    torch.testing.assert_close(y, F.log_softmax(x.float(), 1), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_relu_pool_dropout(cuda, dtype):
+    from distributed_compute_pytorch_amd.ops import relu_max_pool2d_dropout
+
+    torch.manual_seed(0)
+    x = torch.randn(16, 64, 24, 24, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    # p = 0: exactly relu → maxpool
+    xr = x.float().requires_grad_()
+    xo = x.clone().requires_grad_()
+    yr = F.max_pool2d(F.relu(xr), 2)
+    yo = relu_max_pool2d_dropout(xo, 2, 2, 0, 0.0, True)
+    torch.testing.assert_close(yo.float(), yr, rtol=0, atol=0)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    yo.backward(g.to(dtype))
+    torch.testing.assert_close(xo.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+    # p = 0.25: whole (n, c) planes dropped, kept ones scaled by 4/3, and the
+    # backward applies the same mask
+    xo2 = x.clone().requires_grad_()
+    yd = relu_max_pool2d_dropout(xo2, 2, 2, 0, 0.25, True)
+    base = F.max_pool2d(F.relu(x.float()), 2)
+    nz = base.abs().sum((2, 3)) > 0
+    kept = yd.float().abs().sum((2, 3)) > 0
+    frac = (kept & nz).sum().item() / nz.sum().item()
+    assert 0.65 < frac < 0.85, frac
+    scale = torch.where(kept, torch.full_like(base[:, :, 0, 0], 4.0 / 3.0), torch.zeros_like(base[:, :, 0, 0]))
+    torch.testing.assert_close(yd.float(), base * scale[:, :, None, None], rtol=1e-2, atol=1e-2)
+    yd.backward(torch.ones_like(yd))
+    # dropped planes get no gradient
+    gsum = xo2.grad.float().abs().sum((2, 3))
+    assert bool(((~kept) & nz).logical_and(gsum > 0).sum() == 0)
+    assert bool((kept & nz).logical_and(gsum == 0).sum() == 0)
+
+
+def test_fused_convnet_matches_stock(cuda):
+    """Same weights: eval outputs equal; one train step's gradients equal with dropout off."""
+    from distributed_compute_pytorch_amd.models import ConvNet
+
+    torch.manual_seed(0)
+    ref = ConvNet().to(cuda)
+    ours = ConvNet(fused=True).to(cuda)
+    ours.load_state_dict(ref.state_dict())
+    assert list(ours.state_dict().keys()) == list(ref.state_dict().keys())
+    x = torch.randn(64, 1, 28, 28, device=cuda)
+    y = torch.randint(0, 10, (64,), device=cuda)
+    ref.eval(), ours.eval()
+    with torch.no_grad():
+        torch.testing.assert_close(ours(x), ref(x), rtol=1e-4, atol=1e-4)
+    ref.train(), ours.train()
+    for m in (ref, ours):
+        m.dropout1.p = 0.0
+        m.dropout2.p = 0.0
+    F.nll_loss(ref(x), y).backward()
+    F.nll_loss(ours(x), y).backward()
+    for (n, p), q in zip(ref.named_parameters(), ours.parameters()):
+        rel = float((q.grad - p.grad).norm() / p.grad.norm().clamp_min(1e-12))
+        assert rel < 1e-3, (n, rel)
+    torch.testing.assert_close(ours.batchnorm.running_mean, ref.batchnorm.running_mean, rtol=1e-4, atol=1e-5)
+
+
+def test_fused_convnet_trains(cuda):
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.models import ConvNet
+
+    torch.manual_seed(0)
+    m = ConvNet(fused=True).to(cuda)
+    opt = dcp.optim.Adadelta(m.parameters(), lr=1.0)
+    x = torch.randn(128, 1, 28, 28, device=cuda)
+    y = torch.randint(0, 10, (128,), device=cuda)
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        loss = F.nll_loss(m(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < 0.5 * losses[0], losses
