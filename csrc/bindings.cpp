@@ -7,6 +7,7 @@
 #include "fused.h"
 #include "ops.h"
 #include "reducer/reducer.h"
+#include "trace/trace.h"
 #include "store/tcp_store.h"
 
 namespace py = pybind11;
@@ -128,6 +129,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("comm_dtype", &ReducerOptions::comm_dtype)
       .def_readwrite("average", &ReducerOptions::average);
 
+  m.def("trace_enabled", &trace::enabled);
+  m.def("trace_push", [](const std::string& n) { trace::push(n.c_str()); });
+  m.def("trace_pop", &trace::pop);
+  m.def("trace_mark", [](const std::string& n) { trace::mark(n.c_str()); });
   py::class_<BucketStats>(m, "BucketStats")
       .def_readonly("bytes", &BucketStats::bytes)
       .def_readonly("num_params", &BucketStats::num_params)
@@ -160,6 +165,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("bucket_indices", &Reducer::bucket_indices)
       .def("bucket_sizes_bytes", &Reducer::bucket_sizes_bytes)
       .def("bucket_stats", &Reducer::bucket_stats)
+      .def("exposed_comm_ms", &Reducer::exposed_comm_ms)
       .def("bucket_buffers", &Reducer::bucket_buffers)
       .def("ready_order", &Reducer::ready_order)
       .def("wait_all", &Reducer::wait_all, py::call_guard<py::gil_scoped_release>())

@@ -8,8 +8,14 @@
 #include <map>
 #include <unordered_set>
 
+#include <c10/hip/HIPStream.h>
+
+#include <cstdlib>
+#include <cstring>
+
 #include "../common.h"
 #include "../ops.h"
+#include "../trace/trace.h"
 
 namespace dcp {
 
@@ -76,9 +82,26 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
   ready_.assign(params_.size(), 0);
   unused_.assign(params_.size(), 0);
   build_buckets(buckets);
+  const char* t = std::getenv("DCP_COMM_TIMING");
+  timing_ = t && std::strcmp(t, "1") == 0 && !params_.empty() && params_[0].is_cuda();
+  if (timing_) {
+    DCP_CHECK(hipEventCreate(&ev_bwd_end_) == hipSuccess && hipEventCreate(&ev_final_) == hipSuccess,
+              "Reducer: event creation failed");
+  }
+}
+
+double Reducer::exposed_comm_ms() {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!timing_ || !ev_recorded_) return -1.0;
+  if (hipEventQuery(ev_final_) != hipSuccess) return -1.0;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, ev_bwd_end_, ev_final_) != hipSuccess) return -1.0;
+  return ms;
 }
 
 Reducer::~Reducer() {
+  if (ev_bwd_end_) (void)hipEventDestroy(ev_bwd_end_);
+  if (ev_final_) (void)hipEventDestroy(ev_final_);
   for (size_t i = 0; i < grad_accs_.size() && i < hook_handles_.size(); ++i)
     grad_accs_[i]->del_post_hook(hook_handles_[i]);
 }
@@ -265,6 +288,7 @@ void Reducer::launch(Bucket& b) {
   }
   for (auto& g : b.pending_grads) g = at::Tensor();
   b.stats.ready_ms = static_cast<double>(now_ms()) - backward_t0_ms_;
+  trace::Range r("dcp.reducer.bucket_allreduce");
   if (comm_hook_) {
     b.work = comm_hook_(b.wire);
   } else {
@@ -276,6 +300,7 @@ void Reducer::launch(Bucket& b) {
 void Reducer::finalize() {
   std::lock_guard<std::mutex> g(mu_);
   if (!finalize_queued_) return;
+  trace::Range range("dcp.reducer.finalize");
   // Every bucket must have been launched: an unready parameter means the
   // model produced no gradient for it and find_unused_parameters was off.
   std::vector<int64_t> missing;
@@ -305,9 +330,16 @@ void Reducer::finalize() {
     for (size_t i = 0; i < params_.size(); ++i) global_used[i] = h[i].item<int>() != 0;
   }
 
+  hipStream_t cur = nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (timing_) {
+    cur = c10::hip::getCurrentHIPStream(params_[0].device().index()).stream();
+    (void)hipStreamIsCapturing(cur, &cap);
+    if (cap == hipStreamCaptureStatusNone) (void)hipEventRecord(ev_bwd_end_, cur);
+  }
   for (auto& b : buckets_) {
     b.work->wait();
-    b.stats.comm_ms = b.work->elapsed_ms();
+    if (cap == hipStreamCaptureStatusNone) b.stats.comm_ms = b.work->elapsed_ms();
     if (!b.wire.is_same(b.flat)) ops::mt_copy({b.wire}, {b.flat}, 1.0);
     std::vector<at::Tensor> src, dst;
     for (size_t s = 0; s < b.params.size(); ++s) {
@@ -331,6 +363,10 @@ void Reducer::finalize() {
     b.work.reset();
     b.launched = false;
     b.pending = static_cast<int>(b.params.size());
+  }
+  if (timing_ && cap == hipStreamCaptureStatusNone) {
+    (void)hipEventRecord(ev_final_, cur);
+    ev_recorded_ = true;
   }
   std::fill(ready_.begin(), ready_.end(), 0);
   next_bucket_ = 0;

@@ -17,6 +17,7 @@
 #pragma once
 
 #include <ATen/ATen.h>
+#include <hip/hip_runtime.h>
 #include <torch/csrc/autograd/function.h>
 
 #include <functional>
@@ -79,6 +80,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<std::vector<int64_t>> bucket_indices() const;
   std::vector<int64_t> bucket_sizes_bytes() const;
   std::vector<BucketStats> bucket_stats() const;
+  // DCP_COMM_TIMING=1 on a GPU: device time between the end of the backward
+  // compute and the point where every bucket's reduction has landed in the
+  // last finished iteration = communication NOT hidden behind backward.
+  // -1 when unavailable (timing off, CPU, still in flight).
+  double exposed_comm_ms();
   std::vector<int64_t> ready_order() const { return ready_order_; }
   int64_t num_iterations() const { return iterations_; }
   int64_t num_rebuilds() const { return rebuilds_; }
@@ -135,6 +141,9 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   int64_t iterations_ = 0;
   int64_t rebuilds_ = 0;
   double backward_t0_ms_ = 0;
+  bool timing_ = false;
+  hipEvent_t ev_bwd_end_ = nullptr, ev_final_ = nullptr;
+  bool ev_recorded_ = false;
   at::Tensor local_used_;  // find_unused: per-param used flags (int32, on device)
 };
 

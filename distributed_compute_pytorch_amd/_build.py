@@ -95,6 +95,7 @@ def _link_cmd(objs, out):
             f"{lib / 'librccl.so'}",
             f"-Wl,-rpath,{lib}",
             "-Wl,--no-as-needed",
+            "-ldl",
         ]
     )
 

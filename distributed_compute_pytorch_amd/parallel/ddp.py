@@ -31,6 +31,7 @@ from torch import nn
 
 from .._ext import C as _C
 from .. import distributed as dist
+from ..utils.trace import trace_range
 from .comm_utils import CoalescedBroadcaster, broadcast_coalesced, verify_params_across_processes
 
 # Defaults (MiB). torch: 25 MiB cap, 1 MiB first bucket (reducer.hpp:30-31).
@@ -126,6 +127,10 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------
     def forward(self, *inputs, **kwargs):
+        with trace_range("DistributedDataParallel.forward"):
+            return self._forward(*inputs, **kwargs)
+
+    def _forward(self, *inputs, **kwargs):
         grad = torch.is_grad_enabled()
         if self.broadcast_buffers and self._buffer_bcast is not None and self.require_forward_param_sync \
                 and self.process_group.size() > 1:
@@ -186,6 +191,8 @@ class DistributedDataParallel(nn.Module):
             "rebuilds": self.reducer.num_rebuilds,
             "comm_ops": self._comm.ops_issued,
             "comm_bytes": self._comm.bytes_issued,
+            # DCP_COMM_TIMING=1: reduction time not hidden behind backward
+            "exposed_comm_ms": self.reducer.exposed_comm_ms(),
         }
 
 
