@@ -1,11 +1,12 @@
 """Counter-based Philox dropout (csrc/kernels/dropout.hip).
 
 The mask is a function of (seed, offset, element index): nothing is stored,
-the backward regenerates it. The seed is drawn from torch's CPU generator
-(``torch.manual_seed`` makes runs reproducible; SURVEY App. A14: the reference
-seeds every rank identically). The Philox offset lives in a device tensor that
-every call advances with a tiny kernel, so HIP-graph replays draw fresh masks
-(a host-side counter would be frozen into the captured graph).
+the backward regenerates it. Every call draws its seed from torch's CPU
+generator (``torch.manual_seed`` makes runs reproducible; SURVEY App. A14:
+the reference seeds every rank identically). Inside a HIP-graph capture the
+drawn seed is frozen into the graph, so the call also snapshots and advances
+a per-device Philox counter tensor (two tiny captured kernels): every replay
+reads a new counter value and draws fresh masks. Eager calls skip the counter.
 ``dropout_add(x, residual, p)`` fuses the transformer residual add.
 """
 from __future__ import annotations
@@ -19,46 +20,43 @@ from .._ext import C as _C
 _OK = (torch.float32, torch.bfloat16)
 
 
-_RNG = {}
+_COUNTER = {}
 
 
-def _rng(device):
-    """(seed, device offset tensor) for `device`; re-seeded when torch's
-    initial seed changes (torch.manual_seed)."""
-    key = (device.type, device.index)
-    cur = torch.initial_seed()
-    st = _RNG.get(key)
-    if st is None or st[2] != cur:
-        seed = int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
-        st = (seed, torch.zeros(1, dtype=torch.int64, device=device), cur)
-        _RNG[key] = st
-    return st[0], st[1]
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
 
 def _take_offset(device, n):
-    """Snapshot the device offset for this call and advance it by n/4 Philox counters."""
-    seed, base = _rng(device)
+    """(seed, device offset or None) for a call consuming ceil(n / 4) Philox counters."""
+    seed = int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+    if device.type != "cuda" or not _capturing():
+        _ensure_counter(device)
+        return seed, None
+    key = device.index
+    base = _COUNTER.get(key)
+    if base is None:
+        raise RuntimeError("dropout inside a HIP-graph capture needs an eager warmup call first")
     used = base.clone()
     base.add_((n + 3) // 4)
     return seed, used
 
 
-def _seed():
-    return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+def _ensure_counter(device):
+    if device.type == "cuda" and device.index not in _COUNTER:
+        _COUNTER[device.index] = torch.zeros(1, dtype=torch.int64, device=device)
 
 
 class _DropFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, p, rng):
         seed, off = rng
-        ctx.p, ctx.seed, ctx.has_res, ctx.xdtype = p, seed, residual is not None, x.dtype
-        ctx.save_for_backward(off)
+        ctx.p, ctx.seed, ctx.has_res, ctx.xdtype, ctx.off = p, seed, residual is not None, x.dtype, off
         return _C.dropout_fwd(x, residual, p, seed, 0, None, off)
 
     @staticmethod
     def backward(ctx, gy):
-        (off,) = ctx.saved_tensors
-        gx = _C.dropout_fwd(gy.contiguous(), None, ctx.p, ctx.seed, 0, ctx.xdtype, off)
+        gx = _C.dropout_fwd(gy.contiguous(), None, ctx.p, ctx.seed, 0, ctx.xdtype, ctx.off)
         return gx, (gy if ctx.has_res else None), None, None
 
 
@@ -66,14 +64,12 @@ class _FeatDropFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, p, rng):
         seed, off = rng
-        ctx.p, ctx.seed = p, seed
-        ctx.save_for_backward(off)
+        ctx.p, ctx.seed, ctx.off = p, seed, off
         return _C.feature_dropout_fwd(x, p, seed, 0, off)
 
     @staticmethod
     def backward(ctx, gy):
-        (off,) = ctx.saved_tensors
-        return _C.feature_dropout_fwd(gy.contiguous(), ctx.p, ctx.seed, 0, off), None, None
+        return _C.feature_dropout_fwd(gy.contiguous(), ctx.p, ctx.seed, 0, ctx.off), None, None
 
 
 def _usable(x):

@@ -45,8 +45,8 @@ def test_log_softmax_matches_aten(cuda, dtype, shape):
 
     torch.manual_seed(0)
     x = (torch.randn(shape, device=cuda) * 4).to(dtype)
-    xr = x.float().requires_grad_()
-    xo = x.clone().requires_grad_()
+    xr = x.detach().float().clone().requires_grad_()
+    xo = x.detach().clone().requires_grad_()
     yr = F.log_softmax(xr, 1)
     yo = fused_log_softmax(xo, 1)
     tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=2e-2)
@@ -74,8 +74,8 @@ def test_relu_pool_dropout(cuda, dtype):
     torch.manual_seed(0)
     x = torch.randn(16, 64, 24, 24, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
     # p = 0: exactly relu → maxpool
-    xr = x.float().requires_grad_()
-    xo = x.clone().requires_grad_()
+    xr = x.detach().float().clone().requires_grad_()
+    xo = x.detach().clone().requires_grad_()
     yr = F.max_pool2d(F.relu(xr), 2)
     yo = relu_max_pool2d_dropout(xo, 2, 2, 0, 0.0, True)
     torch.testing.assert_close(yo.float(), yr, rtol=0, atol=0)
@@ -85,7 +85,7 @@ def test_relu_pool_dropout(cuda, dtype):
     torch.testing.assert_close(xo.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
     # p = 0.25: whole (n, c) planes dropped, kept ones scaled by 4/3, and the
     # backward applies the same mask
-    xo2 = x.clone().requires_grad_()
+    xo2 = x.detach().clone().requires_grad_()
     yd = relu_max_pool2d_dropout(xo2, 2, 2, 0, 0.25, True)
     base = F.max_pool2d(F.relu(x.float()), 2)
     nz = base.abs().sum((2, 3)) > 0
@@ -122,6 +122,11 @@ def test_fused_convnet_matches_stock(cuda):
     F.nll_loss(ref(x), y).backward()
     F.nll_loss(ours(x), y).backward()
     for (n, p), q in zip(ref.named_parameters(), ours.parameters()):
+        if n == "fc1.bias":
+            # BN right after fc1 cancels any per-channel shift: this gradient is
+            # 0 up to rounding noise in both implementations
+            assert float(q.grad.abs().max()) < 1e-4 * float(ours.fc1.weight.grad.abs().max()) + 1e-6
+            continue
         rel = float((q.grad - p.grad).norm() / p.grad.norm().clamp_min(1e-12))
         assert rel < 1e-3, (n, rel)
     torch.testing.assert_close(ours.batchnorm.running_mean, ref.batchnorm.running_mean, rtol=1e-4, atol=1e-5)

@@ -3,10 +3,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python tools/grad_diag.py > gpurun_out/grad_diag.txt 2>&1
+PYTHONPATH=. timeout -k 10 300 python tools/grad_diag.py > gpurun_out/grad_diag.txt 2>&1
 echo "grad_diag rc=$?" >> gpurun_out/grad_diag.txt
-TORCH_SHOW_CPP_STACKTRACES=1 timeout -k 10 400 python tools/graph_debug.py > gpurun_out/graph_debug.txt 2>&1
-echo "graph_debug rc=$?" >> gpurun_out/graph_debug.txt
+true
+true
 timeout -k 10 900 python -m pytest tests -m gpu -q --ignore=tests/test_gpu_graphs.py > gpurun_out/pytest_gpu.log 2>&1
 echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -m pytest tests/test_gpu_graphs.py -q > gpurun_out/pytest_graphs.log 2>&1
