@@ -89,7 +89,7 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
                                    const c10::optional<at::Tensor>& running_mean,
                                    const c10::optional<at::Tensor>& running_var,
                                    const c10::optional<at::Tensor>& residual, bool training, double momentum,
-                                   double eps, bool act) {
+                                   double eps, bool act, const c10::optional<at::Tensor>& num_batches_tracked) {
   check_nhwc(x, "bn_act_fwd");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t C = x.size(1);
@@ -114,7 +114,11 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
                            static_cast<int>(C), w.defined() ? w.data_ptr<float>() : nullptr,
                            b.defined() ? b.data_ptr<float>() : nullptr, rm, rv, static_cast<float>(momentum),
                            static_cast<float>(eps), mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                           acc.data_ptr<float>(), act, s);
+                           acc.data_ptr<float>(), act,
+                           num_batches_tracked.has_value() && num_batches_tracked->defined()
+                               ? num_batches_tracked->data_ptr<int64_t>()
+                               : nullptr,
+                           s);
   } else {
     DCP_CHECK(running_mean.has_value() && running_var.has_value(), "bn_act_fwd: eval mode needs running stats");
     mean.copy_(*running_mean);
@@ -157,12 +161,15 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const c10::optional<at:
   at::Tensor gres = has_res ? at::empty_like(x, cl_fmt(x)) : at::Tensor();
   const bool has_w = weight.has_value() && weight->defined();
   at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
+  const bool has_bias = bias.has_value() && bias->defined();
+  at::Tensor bf = has_bias ? bias->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor dw = at::empty({C}, fopt);
   at::Tensor db = at::empty({C}, fopt);
   at::Tensor acc = zeroed_floats(2 * C, x, stream_of(x));
   kern::bn_backward(bn_dtype(x), g.data_ptr(), g2.defined() ? g2.data_ptr() : nullptr, y.data_ptr(), x.data_ptr(),
                     M, static_cast<int>(C),
-                    has_w ? w.data_ptr<float>() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(), act,
+                    has_w ? w.data_ptr<float>() : nullptr, bf.defined() ? bf.data_ptr<float>() : nullptr,
+                    mean.data_ptr<float>(), invstd.data_ptr<float>(), act,
                     has_res, has_res ? gres.data_ptr() : nullptr, dx.data_ptr(), dw.data_ptr<float>(),
                     db.data_ptr<float>(), acc.data_ptr<float>(), training, stream_of(x));
   at::Tensor dweight = has_w ? dw.to(weight->scalar_type()) : at::Tensor();
@@ -457,7 +464,10 @@ void bind(pybind11::module& m) {
   m.def("log_softmax_fwd", &log_softmax_fwd, pybind11::arg("x"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("log_softmax_bwd", &log_softmax_bwd);
   m.def("cross_entropy_bwd", &cross_entropy_bwd);
-  m.def("bn_act_fwd", &bn_act_fwd, "fused NHWC BatchNorm(+residual)(+ReLU) forward");
+  m.def("bn_act_fwd", &bn_act_fwd, "fused NHWC BatchNorm(+residual)(+ReLU) forward", pybind11::arg("x"),
+        pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"), pybind11::arg("running_var"),
+        pybind11::arg("residual"), pybind11::arg("training"), pybind11::arg("momentum"), pybind11::arg("eps"),
+        pybind11::arg("act"), pybind11::arg("num_batches_tracked") = pybind11::none());
   m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward");
 }
 

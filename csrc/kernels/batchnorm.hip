@@ -150,19 +150,21 @@ __global__ void __launch_bounds__(kT) bn_stats_kernel(const void* __restrict__ x
   if (cv_ok) {
     V8<D>::ld(x, static_cast<int64_t>(cvec) * kV, sh);  // shift = row 0
     int64_t r = r0 + grp;
-    // two rows in flight per iteration
-    for (; r + g.rpi < r1; r += 2 * g.rpi) {
-      float v[kV], w[kV];
-      V8<D>::ld(x, r * C + cvec * kV, v);
-      V8<D>::ld(x, (r + g.rpi) * C + cvec * kV, w);
+    // four rows in flight per iteration
+    for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) {
+      float v[4][kV];
 #pragma unroll
-      for (int k = 0; k < kV; ++k) {
-        const float d = v[k] - sh[k], e = w[k] - sh[k];
-        s[k] += d + e;
-        q[k] = fmaf(d, d, fmaf(e, e, q[k]));
-      }
+      for (int u = 0; u < 4; ++u) V8<D>::ld(x, (r + u * g.rpi) * C + cvec * kV, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < kV; ++k) {
+          const float d = v[u][k] - sh[k];
+          s[k] += d;
+          q[k] = fmaf(d, d, q[k]);
+        }
     }
-    if (r < r1) {
+    for (; r < r1; r += g.rpi) {
       float v[kV];
       V8<D>::ld(x, r * C + cvec * kV, v);
 #pragma unroll
@@ -191,6 +193,16 @@ __device__ __forceinline__ void stats_for(const float* acc, const void* x, int64
   *invstd = rsqrtf(v + eps);
 }
 
+// Folded affine coefficients y = x*sc + sf. Shared by the forward apply and
+// the backward kernels that recompute the ReLU mask from x (same expression →
+// same fp32 rounding → bit-identical mask).
+__device__ __forceinline__ void coef(const float* gamma, const float* beta, int c, float mean, float inv, float* sc,
+                                     float* sf) {
+  const float gm = gamma ? gamma[c] : 1.f;
+  *sc = gm * inv;
+  *sf = (beta ? beta[c] : 0.f) - mean * *sc;
+}
+
 // ------------------------------------------------------------- apply ----
 // y = act(x*scale[c] + shift[c] (+ res)). TRAIN: scale/shift derived in the
 // prologue from acc (batch stats); else from the given scale/shift arrays.
@@ -204,7 +216,8 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
                                                       const float* __restrict__ shift_in, void* __restrict__ y,
                                                       float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                       float* running_mean, float* running_var, float momentum,
-                                                      float eps, int64_t M, int64_t nvec, int C) {
+                                                      float eps, int64_t M, int64_t nvec, int C,
+                                                      int64_t* __restrict__ nbt) {
   const int cv = C / kV;
   const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
@@ -216,9 +229,7 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
     if (TRAIN) {
       float mean, var, inv;
       stats_for<D>(acc, x, M, C, c, eps, &mean, &var, &inv);
-      const float gm = gamma ? gamma[c] : 1.f;
-      sc[k] = gm * inv;
-      sf[k] = (beta ? beta[c] : 0.f) - mean * sc[k];
+      coef(gamma, beta, c, mean, inv, &sc[k], &sf[k]);
       if (tid < cv) {  // one writer per channel
         mean_out[c] = mean;
         invstd_out[c] = inv;
@@ -233,11 +244,9 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
       sf[k] = shift_in[c];
     }
   }
-  for (int64_t v = tid; v < nvec; v += stride) {
-    float a[kV];
-    V8<D>::ld(x, v * kV, a);
-    float r[kV];
-    if (RES) V8<D>::ld(res, v * kV, r);
+  if (TRAIN && nbt && tid == 0) *nbt += 1;  // num_batches_tracked (saves an ATen add launch per BN)
+  // two vectors per thread per iteration: twice the loads in flight
+  auto one = [&](float (&a)[kV], const float (&r)[kV]) {
 #pragma unroll
     for (int k = 0; k < kV; ++k) {
       float o = fmaf(a[k], sc[k], sf[k]);
@@ -245,6 +254,26 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
       if (ACT) o = fmaxf(o, 0.f);
       a[k] = o;
     }
+  };
+  int64_t v = tid;
+  for (; v + stride < nvec; v += 2 * stride) {
+    float a[kV], b[kV], ra[kV], rb[kV];
+    V8<D>::ld(x, v * kV, a);
+    V8<D>::ld(x, (v + stride) * kV, b);
+    if (RES) {
+      V8<D>::ld(res, v * kV, ra);
+      V8<D>::ld(res, (v + stride) * kV, rb);
+    }
+    one(a, ra);
+    one(b, rb);
+    V8<D>::st(y, v * kV, a);
+    V8<D>::st(y, (v + stride) * kV, b);
+  }
+  if (v < nvec) {
+    float a[kV], ra[kV];
+    V8<D>::ld(x, v * kV, a);
+    if (RES) V8<D>::ld(res, v * kV, ra);
+    one(a, ra);
     V8<D>::st(y, v * kV, a);
   }
 }
@@ -256,10 +285,15 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
 // consumers — next block's conv and its residual add — and the dual-output
 // autograd Function hands both gradients here instead of autograd adding
 // them with a separate elementwise pass).
-template <int D, bool ACT, bool STORE_G, bool GY2>
+// MX: ReLU mask recomputed from x (x*sc + sf > 0, the forward's own
+// expression) instead of reading y — non-residual BN+ReLU only.
+template <int D, bool ACT, bool STORE_G, bool GY2, bool MX>
 __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restrict__ gy, const void* __restrict__ gy2,
                                                            const void* __restrict__ y,
                                                            const void* __restrict__ x, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
                                                            int64_t M, int C, int64_t rows_per_blk,
                                                            float* __restrict__ acc, void* __restrict__ gout) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -271,12 +305,15 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
   const bool cv_ok = cvec < g.cv && grp < g.rpi;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_blk;
   const int64_t r1 = min(M, r0 + rows_per_blk);
-  float sb[kV], sg[kV], mu[kV];
+  float sb[kV], sg[kV], mu[kV], sc[kV], sf[kV];
 #pragma unroll
   for (int k = 0; k < kV; ++k) sb[k] = sg[k] = 0.f;
   if (cv_ok) {
 #pragma unroll
-    for (int k = 0; k < kV; ++k) mu[k] = mean[cvec * kV + k];
+    for (int k = 0; k < kV; ++k) {
+      mu[k] = mean[cvec * kV + k];
+      if (MX) coef(gamma, beta, cvec * kV + k, mu[k], invstd[cvec * kV + k], &sc[k], &sf[k]);
+    }
 #pragma unroll 2
     for (int64_t r = r0 + grp; r < r1; r += g.rpi) {
       const int64_t off = r * C + cvec * kV;
@@ -289,7 +326,10 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
         for (int k = 0; k < kV; ++k) gv[k] += g2[k];
       }
       V8<D>::ld(x, off, xv);
-      if (ACT) {
+      if (ACT && MX) {
+#pragma unroll
+        for (int k = 0; k < kV; ++k) gv[k] = fmaf(xv[k], sc[k], sf[k]) > 0.f ? gv[k] : 0.f;
+      } else if (ACT) {
         float yv[kV];
         V8<D>::ld(y, off, yv);
 #pragma unroll
@@ -310,11 +350,14 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
 // k1 = gamma*invstd, k2 = Σg/M, k3 = Σg(x-mean)/M * invstd² (training) —
 // derived per thread in the prologue from acc; the first thread group writes
 // dgamma = Σg(x-mean)*invstd and dbeta = Σg.
-template <int D, bool ACT, bool FROM_G>
+// ACT && !FROM_G: the ReLU mask is recomputed from x when MX (training-mode
+// coefficients, see bn_bwd_reduce_kernel), else read from y.
+template <int D, bool ACT, bool FROM_G, bool MX>
 __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict__ gsrc, const void* __restrict__ y,
                                                           const void* __restrict__ x, const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
-                                                          const float* __restrict__ gamma, const float* __restrict__ acc,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, const float* __restrict__ acc,
                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                           bool training, void* __restrict__ dx, int64_t M,
                                                           int64_t nvec, int C) {
@@ -322,13 +365,14 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict
   const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
   const int c0 = static_cast<int>(tid % cv) * kV;
-  float k1[kV], k2[kV], k3[kV], mu[kV];
+  float k1[kV], k2[kV], k3[kV], mu[kV], sc[kV], sf[kV];
 #pragma unroll
   for (int k = 0; k < kV; ++k) {
     const int c = c0 + k;
     const float inv = invstd[c];
     const float sb = acc[c], sg = acc[C + c];
     mu[k] = mean[c];
+    if (ACT && !FROM_G && MX) coef(gamma, beta, c, mu[k], inv, &sc[k], &sf[k]);
     k1[k] = (gamma ? gamma[c] : 1.f) * inv;
     k2[k] = training ? sb / static_cast<float>(M) : 0.f;
     k3[k] = training ? sg / static_cast<float>(M) * inv * inv : 0.f;
@@ -337,18 +381,40 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict
       if (dbeta) dbeta[c] = sb;
     }
   }
-  for (int64_t v = tid; v < nvec; v += stride) {
-    float gv[kV], xv[kV];
-    V8<D>::ld(gsrc, v * kV, gv);
-    if (ACT && !FROM_G) {
-      float yv[kV];
-      V8<D>::ld(y, v * kV, yv);
+  auto one = [&](float (&gv)[kV], const float (&xv)[kV], const float (&yv)[kV]) {
 #pragma unroll
-      for (int k = 0; k < kV; ++k) gv[k] = yv[k] > 0.f ? gv[k] : 0.f;
+    for (int k = 0; k < kV; ++k) {
+      float gk = gv[k];
+      if (ACT && !FROM_G) {
+        const bool on = MX ? fmaf(xv[k], sc[k], sf[k]) > 0.f : yv[k] > 0.f;
+        gk = on ? gk : 0.f;
+      }
+      gv[k] = k1[k] * (gk - k2[k] - (xv[k] - mu[k]) * k3[k]);
     }
+  };
+  constexpr bool kReadY = ACT && !FROM_G && !MX;
+  int64_t v = tid;
+  for (; v + stride < nvec; v += 2 * stride) {
+    float ga[kV], gb[kV], xa[kV], xb[kV], ya[kV], yb[kV];
+    V8<D>::ld(gsrc, v * kV, ga);
+    V8<D>::ld(gsrc, (v + stride) * kV, gb);
+    V8<D>::ld(x, v * kV, xa);
+    V8<D>::ld(x, (v + stride) * kV, xb);
+    if (kReadY) {
+      V8<D>::ld(y, v * kV, ya);
+      V8<D>::ld(y, (v + stride) * kV, yb);
+    }
+    one(ga, xa, ya);
+    one(gb, xb, yb);
+    V8<D>::st(dx, v * kV, ga);
+    V8<D>::st(dx, (v + stride) * kV, gb);
+  }
+  if (v < nvec) {
+    float gv[kV], xv[kV], yv[kV];
+    V8<D>::ld(gsrc, v * kV, gv);
     V8<D>::ld(x, v * kV, xv);
-#pragma unroll
-    for (int k = 0; k < kV; ++k) gv[k] = k1[k] * (gv[k] - k2[k] - (xv[k] - mu[k]) * k3[k]);
+    if (kReadY) V8<D>::ld(y, v * kV, yv);
+    one(gv, xv, yv);
     V8<D>::st(dx, v * kV, gv);
   }
 }
@@ -405,7 +471,7 @@ bool bn_supported(int C) {
 
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
-                      float* mean, float* invstd, float* acc, bool act, hipStream_t s) {
+                      float* mean, float* invstd, float* acc, bool act, int64_t* nbt, hipStream_t s) {
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
@@ -418,7 +484,7 @@ void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_
   const int grid = apply_grid(nvec, C / kV);
 #define DCP_BN_APPLY(D, R, A)                                                                                     \
   hipLaunchKernelGGL((bn_apply_kernel<D, R, A, true>), dim3(grid), dim3(kT), 0, s, x, res, acc, gamma, beta,      \
-                     nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M, nvec, C)
+                     nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M, nvec, C, nbt)
   const bool r = res != nullptr;
   if (dtype == BN_BF16) {
     if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
@@ -440,7 +506,7 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
   const int grid = apply_grid(nvec, C / kV);
 #define DCP_BN_APPLY(D, R, A)                                                                                  \
   hipLaunchKernelGGL((bn_apply_kernel<D, R, A, false>), dim3(grid), dim3(kT), 0, s, x, res, nullptr, nullptr, \
-                     nullptr, scale, shift, y, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, M, nvec, C)
+                     nullptr, scale, shift, y, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, M, nvec, C, nullptr)
   const bool r = res != nullptr;
   if (dtype == BN_BF16) {
     if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
@@ -457,27 +523,34 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 }
 
 void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, const void* x, int64_t M, int C,
-                 const float* gamma, const float* mean, const float* invstd, bool act, bool store_g, void* gout,
+                 const float* gamma, const float* beta, const float* mean, const float* invstd, bool act,
+                 bool store_g, void* gout,
                  void* dx, float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s) {
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
   const size_t sm = red_smem(C);
-#define DCP_BN_RED(D, A, G)                                                                                  \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G, false>), dim3(nblk, nchunks), dim3(kT), sm, s, gy, nullptr, y, \
-                     x, mean, M, C, rpb, acc, gout)
+#define DCP_BN_RED(D, A, G)                                                                                 \
+  do {                                                                                                        \
+    if (training)                                                                                             \
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G, false, (A && !G)>), dim3(nblk, nchunks), dim3(kT), sm, s, \
+                         gy, nullptr, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);                 \
+    else                                                                                                      \
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G, false, false>), dim3(nblk, nchunks), dim3(kT), sm, s, gy, \
+                         nullptr, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);                     \
+  } while (0)
   // the second gradient is only supported with store_g (the host sums otherwise)
   if (gy2 != nullptr) {
     if (dtype == BN_BF16) {
-      if (act) hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, true, true, true>), dim3(nblk, nchunks), dim3(kT), sm, s,
-                                  gy, gy2, y, x, mean, M, C, rpb, acc, gout);
-      else hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, false, true, true>), dim3(nblk, nchunks), dim3(kT), sm, s,
-                              gy, gy2, y, x, mean, M, C, rpb, acc, gout);
+      if (act) hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, true, true, true, false>), dim3(nblk, nchunks), dim3(kT), sm, s,
+                                  gy, gy2, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);
+      else hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, false, true, true, false>), dim3(nblk, nchunks), dim3(kT), sm, s,
+                              gy, gy2, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);
     } else {
-      if (act) hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, true, true, true>), dim3(nblk, nchunks), dim3(kT), sm, s,
-                                  gy, gy2, y, x, mean, M, C, rpb, acc, gout);
-      else hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, false, true, true>), dim3(nblk, nchunks), dim3(kT), sm, s,
-                              gy, gy2, y, x, mean, M, C, rpb, acc, gout);
+      if (act) hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, true, true, true, false>), dim3(nblk, nchunks), dim3(kT), sm, s,
+                                  gy, gy2, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);
+      else hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, false, true, true, false>), dim3(nblk, nchunks), dim3(kT), sm, s,
+                              gy, gy2, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);
     }
   } else if (dtype == BN_BF16) {
     if (act && store_g) DCP_BN_RED(BN_BF16, true, true);
@@ -495,9 +568,15 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
   const int grid = apply_grid(nvec, C / kV);
   // g source: the stored masked gradient when available, else recompute the mask
   const void* gsrc = store_g ? gout : gy;
-#define DCP_BN_BAPPLY(D, A, F)                                                                                   \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F>), dim3(grid), dim3(kT), 0, s, gsrc, y, x, mean, invstd, gamma, \
-                     acc, dgamma, dbeta, training, dx, M, nvec, C)
+#define DCP_BN_BAPPLY(D, A, F)                                                                                  \
+  do {                                                                                                          \
+    if (training)                                                                                               \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F, true>), dim3(grid), dim3(kT), 0, s, gsrc, y, x, mean, invstd, \
+                         gamma, beta, acc, dgamma, dbeta, training, dx, M, nvec, C);                           \
+    else                                                                                                        \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F, false>), dim3(grid), dim3(kT), 0, s, gsrc, y, x, mean,   \
+                         invstd, gamma, beta, acc, dgamma, dbeta, training, dx, M, nvec, C);                   \
+  } while (0)
   if (dtype == BN_BF16) {
     if (store_g) DCP_BN_BAPPLY(BN_BF16, false, true);
     else if (act) DCP_BN_BAPPLY(BN_BF16, true, false);

@@ -18,7 +18,7 @@ bool bn_supported(int C);
 // mean/invstd: [C] fp32 outputs. acc: ZEROED workspace [2*C] fp32.
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
-                      float* mean, float* invstd, float* acc, bool act, hipStream_t s);
+                      float* mean, float* invstd, float* acc, bool act, int64_t* nbt, hipStream_t s);
 
 // y = act(x * scale[c] + shift[c] [+ res])
 void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
@@ -27,8 +27,11 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 // Backward. g = gy * (y > 0) if act else gy; store_g writes g to gout (the
 // residual-branch gradient). acc: ZEROED workspace [2*C] fp32.
 // gy2 (optional, requires store_g): second output gradient, summed with gy.
+// Training mode, non-residual act: the ReLU mask is recomputed from x with the
+// forward's coefficients (gamma*invstd, beta - mean*gamma*invstd): y is not read.
 void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, const void* x, int64_t M, int C,
-                 const float* gamma, const float* mean, const float* invstd, bool act, bool store_g, void* gout,
+                 const float* gamma, const float* beta, const float* mean, const float* invstd, bool act,
+                 bool store_g, void* gout,
                  void* dx, float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s);
 
 }  // namespace kern

@@ -48,9 +48,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual):
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual,
+                nbt=None):
+        # nbt (num_batches_tracked) is incremented inside the apply kernel
         y, mean, invstd = _C.bn_act_fwd(x, weight, bias, running_mean, running_var, residual, training,
-                                        float(momentum), float(eps), bool(act))
+                                        float(momentum), float(eps), bool(act), nbt)
         ctx.save_for_backward(x, weight, bias, mean, invstd, y)
         ctx.has_res = residual is not None
         ctx.act = act
@@ -67,14 +69,17 @@ class _BNActFn(torch.autograd.Function):
             gy, gy2 = gy2, None
         gx, gw, gb, gres = _C.bn_act_bwd(gy, gy2, x, weight, bias, mean, invstd, y, ctx.act, ctx.has_res,
                                          ctx.training)
-        return gx, gw, gb, None, None, None, None, None, (gres if ctx.has_res else None), None, None
+        return gx, gw, gb, None, None, None, None, None, (gres if ctx.has_res else None), None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, num_batches_tracked, training, momentum, eps, residual,
            act, dual: bool = False):
-    if training and num_batches_tracked is not None:
-        num_batches_tracked.add_(1)
-    return _BNActFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual)
+    nbt = num_batches_tracked if (training and num_batches_tracked is not None) else None
+    if nbt is not None and (nbt.device != x.device or nbt.dtype != torch.int64):
+        nbt.add_(1)
+        nbt = None
+    return _BNActFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual,
+                          nbt)
 
 
 class BatchNormAct1d(nn.BatchNorm1d):

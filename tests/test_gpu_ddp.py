@@ -62,7 +62,9 @@ def test_ddp_matches_local_training(pg, cuda, grad_as_view):
 
 def test_resnet_grads_match_stock_fp32(pg, cuda):
     """One fp32 step: every parameter gradient through our DDP + fused BN
-    equals the stock ATen model's (relative error < 1e-3)."""
+    matches the stock ATen model's to within the stock model's OWN run-to-run
+    spread (MIOpen's backward kernels are not deterministic: two identical
+    stock runs differ by ~2 % at conv1 of a random-init ResNet-50)."""
     import distributed_compute_pytorch_amd as dcp
     from distributed_compute_pytorch_amd.models import resnet50
 
@@ -76,12 +78,17 @@ def test_resnet_grads_match_stock_fp32(pg, cuda):
     y = torch.randint(0, 100, (16,), generator=g).to(cuda)
     l1 = F.cross_entropy(ref(x), y)
     l1.backward()
+    g_ref = [p.grad.clone() for p in ref.parameters()]
+    ref.zero_grad(set_to_none=True)
+    F.cross_entropy(ref(x), y).backward()  # second stock run: the noise floor
     l2 = F.cross_entropy(ddp(x), y)
     l2.backward()
     torch.testing.assert_close(l2, l1, rtol=1e-5, atol=1e-5)
-    for (n, p), q in zip(ref.named_parameters(), model.parameters()):
-        rel = (q.grad - p.grad).norm() / p.grad.norm().clamp_min(1e-12)
-        assert rel < 1e-3, (n, float(rel))
+    for (n, p), q, g0 in zip(ref.named_parameters(), model.parameters(), g_ref):
+        den = g0.norm().clamp_min(1e-12)
+        noise = float((p.grad - g0).norm() / den)
+        rel = float((q.grad - g0).norm() / den)
+        assert rel < 3 * noise + 2e-3, (n, rel, noise)
     for (n, b), c in zip(ref.named_buffers(), model.buffers()):
         torch.testing.assert_close(c.float(), b.float(), rtol=1e-4, atol=1e-5, msg=n)
 

@@ -48,16 +48,27 @@ def test_captured_step_matches_eager(cuda):
         for _ in range(3):
             run_e(*batches[0])
         cap = CapturedStep(run_g, [t.clone() for t in batches[0]], warmup=3, stream=s)  # capture does not execute
-        le, lg = [], []
-        for b in batches[1:]:
-            le.append(run_e(*b).item())
-            lg.append(cap(*b).item())
-        torch.cuda.synchronize()
-        for a, b in zip(le, lg):
-            assert abs(a - b) < 5e-2 * max(1.0, abs(a)), (le, lg)
-        for p, q in zip(m_eager.parameters(), m_graph.parameters()):
-            rel = (p - q).norm() / p.norm().clamp_min(1e-12)
-            assert rel < 5e-2
+
+        def sync_state():
+            # start every compared step from identical state (in place: the
+            # graph keeps its addresses); chaotic drift of two independent
+            # runs (MIOpen / atomic-order noise) is not what this test checks
+            with torch.no_grad():
+                for a, b in zip(m_eager.state_dict().values(), m_graph.state_dict().values()):
+                    b.copy_(a)
+                for pe, pg in zip(m_eager.parameters(), m_graph.parameters()):
+                    o_g.state[pg]["momentum_buffer"].copy_(o_e.state[pe]["momentum_buffer"])
+
+        for b in batches[1:5]:
+            sync_state()
+            torch.cuda.synchronize()
+            le = run_e(*b).item()
+            lg = cap(*b).item()
+            torch.cuda.synchronize()
+            assert abs(le - lg) < 1e-2 * max(1.0, abs(le)), (le, lg)
+            for p, q in zip(m_eager.parameters(), m_graph.parameters()):
+                rel = float((p - q).norm() / p.norm().clamp_min(1e-12))
+                assert rel < 1e-3, rel
     finally:
         dcp.distributed.destroy_process_group()
 

@@ -1,11 +1,21 @@
 """Summarise a rocprofv3 kernel trace over the last N optimizer steps.
 
 A step boundary is the fused-SGD launch (or a user-given kernel-name substring).
-Usage: python tools/trace_summary.py run_kernel_trace.csv [--steps 5] [--marker mt_sgd]
+Usage: python tools/trace_summary.py run_kernel_trace.csv|prof_results.db [--steps 5] [--marker mt_sgd]
+(rocprofv3 writes a rocpd SQLite database by default; CSV with --output-format csv.)
 """
 import argparse
 import csv
+import sqlite3
 from collections import defaultdict
+
+
+def _load(path):
+    if path.endswith(".db"):
+        con = sqlite3.connect(path)
+        return [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                for n, s, e in con.execute("select name, start, end from kernels")]
+    return list(csv.DictReader(open(path)))
 
 
 def main():
@@ -15,7 +25,7 @@ def main():
     ap.add_argument("--marker", default="mt_sgd_kernel")
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.csv)))
+    rows = _load(a.csv)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     if len(marks) < a.steps + 1:
