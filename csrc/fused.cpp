@@ -82,7 +82,8 @@ at::Tensor zeroed_floats(int64_t n, const at::Tensor& like, hipStream_t st) {
 
 }  // namespace
 
-// Returns (y, mean, invstd). Training: batch statistics (+ running-stat update).
+// Returns (y, mean, invstd, relu_bits). Training: batch statistics (+ running-
+// stat update); relu_bits = 1-bit ReLU mask for residual+act (else empty).
 // Eval: running statistics.
 std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
                                    const c10::optional<at::Tensor>& bias,
@@ -105,8 +106,10 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
   at::Tensor b = bias.has_value() && bias->defined() ? bias->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor mean = at::empty({C}, fopt);
   at::Tensor invstd = at::empty({C}, fopt);
+  at::Tensor mbits;
   auto s = stream_of(x);
   if (training) {
+    if (res.defined() && act) mbits = at::empty({M * C / 8}, x.options().dtype(at::kByte));
     at::Tensor acc = zeroed_floats(2 * C, x, s);
     float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
     float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
@@ -118,7 +121,7 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
                            num_batches_tracked.has_value() && num_batches_tracked->defined()
                                ? num_batches_tracked->data_ptr<int64_t>()
                                : nullptr,
-                           s);
+                           mbits.defined() ? mbits.data_ptr<uint8_t>() : nullptr, s);
   } else {
     DCP_CHECK(running_mean.has_value() && running_var.has_value(), "bn_act_fwd: eval mode needs running stats");
     mean.copy_(*running_mean);
@@ -130,7 +133,8 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
     kern::bn_apply(bn_dtype(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, y.data_ptr(), M,
                    static_cast<int>(C), scale.data_ptr<float>(), shift.data_ptr<float>(), act, s);
   }
-  return {y, mean, invstd};
+  if (!mbits.defined()) mbits = at::empty({0}, x.options().dtype(at::kByte));
+  return {y, mean, invstd, mbits};
 }
 
 // Returns (dx, dweight, dbias, dresidual).
@@ -140,7 +144,7 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const c10::optional<at:
                                    const at::Tensor& x, const c10::optional<at::Tensor>& weight,
                                    const c10::optional<at::Tensor>& bias, const at::Tensor& mean,
                                    const at::Tensor& invstd, const at::Tensor& y, bool act, bool has_res,
-                                   bool training) {
+                                   bool training, const c10::optional<at::Tensor>& relu_bits) {
   check_nhwc(x, "bn_act_bwd");
   c10::hip::HIPGuard guard(x.device().index());
   at::Tensor g = gy.contiguous(cl_fmt(x));
@@ -171,7 +175,11 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const c10::optional<at:
                     has_w ? w.data_ptr<float>() : nullptr, bf.defined() ? bf.data_ptr<float>() : nullptr,
                     mean.data_ptr<float>(), invstd.data_ptr<float>(), act,
                     has_res, has_res ? gres.data_ptr() : nullptr, dx.data_ptr(), dw.data_ptr<float>(),
-                    db.data_ptr<float>(), acc.data_ptr<float>(), training, stream_of(x));
+                    db.data_ptr<float>(), acc.data_ptr<float>(), training,
+                    relu_bits.has_value() && relu_bits->defined() && relu_bits->numel() == M * C / 8
+                        ? relu_bits->data_ptr<uint8_t>()
+                        : nullptr,
+                    stream_of(x));
   at::Tensor dweight = has_w ? dw.to(weight->scalar_type()) : at::Tensor();
   const bool has_b = bias.has_value() && bias->defined();
   at::Tensor dbias = has_b ? db.to(bias->scalar_type()) : at::Tensor();
@@ -468,7 +476,10 @@ void bind(pybind11::module& m) {
         pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"), pybind11::arg("running_var"),
         pybind11::arg("residual"), pybind11::arg("training"), pybind11::arg("momentum"), pybind11::arg("eps"),
         pybind11::arg("act"), pybind11::arg("num_batches_tracked") = pybind11::none());
-  m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward");
+  m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward", pybind11::arg("gy"),
+        pybind11::arg("gy2"), pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
+        pybind11::arg("mean"), pybind11::arg("invstd"), pybind11::arg("y"), pybind11::arg("act"),
+        pybind11::arg("has_res"), pybind11::arg("training"), pybind11::arg("relu_bits") = pybind11::none());
 }
 
 }  // namespace fused

@@ -217,7 +217,7 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
                                                       float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                       float* running_mean, float* running_var, float momentum,
                                                       float eps, int64_t M, int64_t nvec, int C,
-                                                      int64_t* __restrict__ nbt) {
+                                                      int64_t* __restrict__ nbt, uint8_t* __restrict__ mbits) {
   const int cv = C / kV;
   const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
@@ -246,14 +246,21 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
   }
   if (TRAIN && nbt && tid == 0) *nbt += 1;  // num_batches_tracked (saves an ATen add launch per BN)
   // two vectors per thread per iteration: twice the loads in flight
-  auto one = [&](float (&a)[kV], const float (&r)[kV]) {
+  // mbits (RES && ACT): bit k of byte v = (y[v*8 + k] > 0), the backward's
+  // ReLU mask at 1/16 of the bytes of re-reading y
+  auto one = [&](float (&a)[kV], const float (&r)[kV], int64_t vv) {
+    uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < kV; ++k) {
       float o = fmaf(a[k], sc[k], sf[k]);
       if (RES) o += r[k];
-      if (ACT) o = fmaxf(o, 0.f);
+      if (ACT) {
+        bits |= (o > 0.f ? 1u : 0u) << k;
+        o = fmaxf(o, 0.f);
+      }
       a[k] = o;
     }
+    if (RES && ACT && mbits) mbits[vv] = static_cast<uint8_t>(bits);
   };
   int64_t v = tid;
   for (; v + stride < nvec; v += 2 * stride) {
@@ -264,8 +271,8 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
       V8<D>::ld(res, v * kV, ra);
       V8<D>::ld(res, (v + stride) * kV, rb);
     }
-    one(a, ra);
-    one(b, rb);
+    one(a, ra, v);
+    one(b, rb, v + stride);
     V8<D>::st(y, v * kV, a);
     V8<D>::st(y, (v + stride) * kV, b);
   }
@@ -273,7 +280,7 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
     float a[kV], ra[kV];
     V8<D>::ld(x, v * kV, a);
     if (RES) V8<D>::ld(res, v * kV, ra);
-    one(a, ra);
+    one(a, ra, v);
     V8<D>::st(y, v * kV, a);
   }
 }
@@ -294,6 +301,7 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta,
+                                                           const uint8_t* __restrict__ mbits,
                                                            int64_t M, int C, int64_t rows_per_blk,
                                                            float* __restrict__ acc, void* __restrict__ gout) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -329,6 +337,10 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
       if (ACT && MX) {
 #pragma unroll
         for (int k = 0; k < kV; ++k) gv[k] = fmaf(xv[k], sc[k], sf[k]) > 0.f ? gv[k] : 0.f;
+      } else if (ACT && mbits) {  // forward's 1-bit ReLU mask (1 B per 8 channels)
+        const uint32_t mb = mbits[off / kV];
+#pragma unroll
+        for (int k = 0; k < kV; ++k) gv[k] = (mb >> k) & 1u ? gv[k] : 0.f;
       } else if (ACT) {
         float yv[kV];
         V8<D>::ld(y, off, yv);
@@ -471,7 +483,8 @@ bool bn_supported(int C) {
 
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
-                      float* mean, float* invstd, float* acc, bool act, int64_t* nbt, hipStream_t s) {
+                      float* mean, float* invstd, float* acc, bool act, int64_t* nbt, uint8_t* mbits,
+                      hipStream_t s) {
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
@@ -484,7 +497,8 @@ void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_
   const int grid = apply_grid(nvec, C / kV);
 #define DCP_BN_APPLY(D, R, A)                                                                                     \
   hipLaunchKernelGGL((bn_apply_kernel<D, R, A, true>), dim3(grid), dim3(kT), 0, s, x, res, acc, gamma, beta,      \
-                     nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M, nvec, C, nbt)
+                     nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M, nvec, C, nbt, \
+                     mbits)
   const bool r = res != nullptr;
   if (dtype == BN_BF16) {
     if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
@@ -506,7 +520,8 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
   const int grid = apply_grid(nvec, C / kV);
 #define DCP_BN_APPLY(D, R, A)                                                                                  \
   hipLaunchKernelGGL((bn_apply_kernel<D, R, A, false>), dim3(grid), dim3(kT), 0, s, x, res, nullptr, nullptr, \
-                     nullptr, scale, shift, y, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, M, nvec, C, nullptr)
+                     nullptr, scale, shift, y, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, M, nvec, C, nullptr, \
+                     nullptr)
   const bool r = res != nullptr;
   if (dtype == BN_BF16) {
     if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
@@ -525,7 +540,8 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, const void* x, int64_t M, int C,
                  const float* gamma, const float* beta, const float* mean, const float* invstd, bool act,
                  bool store_g, void* gout,
-                 void* dx, float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s) {
+                 void* dx, float* dgamma, float* dbeta, float* acc, bool training, const uint8_t* mbits,
+                 hipStream_t s) {
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
@@ -534,23 +550,23 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
   do {                                                                                                        \
     if (training)                                                                                             \
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G, false, (A && !G)>), dim3(nblk, nchunks), dim3(kT), sm, s, \
-                         gy, nullptr, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);                 \
+                         gy, nullptr, y, x, mean, invstd, gamma, beta, mbits, M, C, rpb, acc, gout);                 \
     else                                                                                                      \
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G, false, false>), dim3(nblk, nchunks), dim3(kT), sm, s, gy, \
-                         nullptr, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);                     \
+                         nullptr, y, x, mean, invstd, gamma, beta, mbits, M, C, rpb, acc, gout);                     \
   } while (0)
   // the second gradient is only supported with store_g (the host sums otherwise)
   if (gy2 != nullptr) {
     if (dtype == BN_BF16) {
       if (act) hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, true, true, true, false>), dim3(nblk, nchunks), dim3(kT), sm, s,
-                                  gy, gy2, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);
+                                  gy, gy2, y, x, mean, invstd, gamma, beta, mbits, M, C, rpb, acc, gout);
       else hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, false, true, true, false>), dim3(nblk, nchunks), dim3(kT), sm, s,
-                              gy, gy2, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);
+                              gy, gy2, y, x, mean, invstd, gamma, beta, mbits, M, C, rpb, acc, gout);
     } else {
       if (act) hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, true, true, true, false>), dim3(nblk, nchunks), dim3(kT), sm, s,
-                                  gy, gy2, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);
+                                  gy, gy2, y, x, mean, invstd, gamma, beta, mbits, M, C, rpb, acc, gout);
       else hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, false, true, true, false>), dim3(nblk, nchunks), dim3(kT), sm, s,
-                              gy, gy2, y, x, mean, invstd, gamma, beta, M, C, rpb, acc, gout);
+                              gy, gy2, y, x, mean, invstd, gamma, beta, mbits, M, C, rpb, acc, gout);
     }
   } else if (dtype == BN_BF16) {
     if (act && store_g) DCP_BN_RED(BN_BF16, true, true);

@@ -18,12 +18,15 @@ bool bn_supported(int C);
 // mean/invstd: [C] fp32 outputs. acc: ZEROED workspace [2*C] fp32.
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
-                      float* mean, float* invstd, float* acc, bool act, int64_t* nbt, hipStream_t s);
+                      float* mean, float* invstd, float* acc, bool act, int64_t* nbt, uint8_t* mbits,
+                      hipStream_t s);
 
 // y = act(x * scale[c] + shift[c] [+ res])
 void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
               const float* shift, bool act, hipStream_t s);
 
+// mbits (forward, residual + act only): optional [M*C/8] bytes, bit k of byte
+// v = (y[8v + k] > 0); the backward then never reads y.
 // Backward. g = gy * (y > 0) if act else gy; store_g writes g to gout (the
 // residual-branch gradient). acc: ZEROED workspace [2*C] fp32.
 // gy2 (optional, requires store_g): second output gradient, summed with gy.
@@ -32,7 +35,8 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, const void* x, int64_t M, int C,
                  const float* gamma, const float* beta, const float* mean, const float* invstd, bool act,
                  bool store_g, void* gout,
-                 void* dx, float* dgamma, float* dbeta, float* acc, bool training, hipStream_t s);
+                 void* dx, float* dgamma, float* dbeta, float* acc, bool training, const uint8_t* mbits,
+                 hipStream_t s);
 
 }  // namespace kern
 }  // namespace dcp

@@ -51,9 +51,11 @@ class _BNActFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual,
                 nbt=None):
         # nbt (num_batches_tracked) is incremented inside the apply kernel
-        y, mean, invstd = _C.bn_act_fwd(x, weight, bias, running_mean, running_var, residual, training,
-                                        float(momentum), float(eps), bool(act), nbt)
-        ctx.save_for_backward(x, weight, bias, mean, invstd, y)
+        y, mean, invstd, bits = _C.bn_act_fwd(x, weight, bias, running_mean, running_var, residual, training,
+                                              float(momentum), float(eps), bool(act), nbt)
+        # with the 1-bit ReLU mask (residual + act, training) the backward never reads y
+        ctx.save_for_backward(x, weight, bias, mean, invstd, y if bits.numel() == 0 else bits)
+        ctx.bits = bits.numel() > 0
         ctx.has_res = residual is not None
         ctx.act = act
         ctx.training = training
@@ -64,11 +66,12 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, gy2=None):
-        x, weight, bias, mean, invstd, y = ctx.saved_tensors
+        x, weight, bias, mean, invstd, y_or_bits = ctx.saved_tensors
         if gy is None:
             gy, gy2 = gy2, None
+        y, bits = (x, y_or_bits) if ctx.bits else (y_or_bits, None)  # y unused when bits are given
         gx, gw, gb, gres = _C.bn_act_bwd(gy, gy2, x, weight, bias, mean, invstd, y, ctx.act, ctx.has_res,
-                                         ctx.training)
+                                         ctx.training, bits)
         return gx, gw, gb, None, None, None, None, None, (gres if ctx.has_res else None), None, None, None
 
 
