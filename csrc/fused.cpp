@@ -391,14 +391,21 @@ std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s,
 
 // gx: [in_shape] channels_last, gy's dtype.
 at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& idx, at::IntArrayRef in_shape, int64_t k, int64_t s,
-                         int64_t p, double drop_p, int64_t seed, const c10::optional<at::Tensor>& offset_dev) {
+                         int64_t p, double drop_p, int64_t seed, const c10::optional<at::Tensor>& offset_dev,
+                         const c10::optional<at::Tensor>& gy2) {
   DCP_CHECK(in_shape.size() == 4, "maxpool2d_bwd: 4-D input shape expected");
   c10::hip::HIPGuard guard(gy.device().index());
   at::Tensor gx = at::empty(in_shape, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto g = pool_geom(gx, k, s, p);
   at::Tensor go = gy.contiguous(at::MemoryFormat::ChannelsLast);
   DCP_CHECK(go.size(2) == g.OH && go.size(3) == g.OW && idx.numel() == go.numel(), "maxpool2d_bwd: shape mismatch");
+  at::Tensor g2;
+  if (gy2.has_value() && gy2->defined()) {
+    g2 = gy2->to(gy.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
+    DCP_CHECK(g2.sizes() == go.sizes(), "maxpool2d_bwd: gy2 shape mismatch");
+  }
   kern::maxpool2d_backward(gy.scalar_type() == at::kBFloat16 ? kern::POOL_BF16 : kern::POOL_F32, go.data_ptr(),
+                           g2.defined() ? g2.data_ptr() : nullptr,
                            idx.data_ptr<uint8_t>(), gx.data_ptr(), g, pool_epi(false, drop_p, seed, offset_dev),
                            stream_of(gy));
   return gx;
@@ -457,7 +464,8 @@ void bind(pybind11::module& m) {
         pybind11::arg("seed") = 0, pybind11::arg("offset_dev") = pybind11::none());
   m.def("maxpool2d_bwd", &maxpool2d_bwd, pybind11::arg("gy"), pybind11::arg("idx"), pybind11::arg("in_shape"),
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("drop_p") = 0.0,
-        pybind11::arg("seed") = 0, pybind11::arg("offset_dev") = pybind11::none());
+        pybind11::arg("seed") = 0, pybind11::arg("offset_dev") = pybind11::none(),
+        pybind11::arg("gy2") = pybind11::none());
   m.def("dropout_fwd", &dropout_fwd, pybind11::arg("x"), pybind11::arg("residual"), pybind11::arg("p"),
         pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("out_dtype") = pybind11::none(),
         pybind11::arg("offset_dev") = pybind11::none());

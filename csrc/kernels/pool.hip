@@ -145,8 +145,9 @@ __global__ void __launch_bounds__(kT) maxpool_fwd_kernel(const void* __restrict_
 }
 
 template <int D>
-__global__ void __launch_bounds__(kT) maxpool_bwd_kernel(const void* __restrict__ gy, const uint8_t* __restrict__ idx,
-                                                         void* __restrict__ gx, PoolGeom g, PoolEpi e) {
+__global__ void __launch_bounds__(kT) maxpool_bwd_kernel(const void* __restrict__ gy, const void* __restrict__ gy2,
+                                                         const uint8_t* __restrict__ idx, void* __restrict__ gx,
+                                                         PoolGeom g, PoolEpi e) {
   const uint64_t doff = e.offset + (e.offset_dev ? static_cast<uint64_t>(*e.offset_dev) : 0);
   const int cv = g.C / 8;
   const int64_t total = static_cast<int64_t>(g.N) * g.H * g.W * cv;
@@ -176,6 +177,12 @@ __global__ void __launch_bounds__(kT) maxpool_bwd_kernel(const void* __restrict_
         const uint32_t wv[2] = {pk.x, pk.y};
         float gv[8];
         P8<D>::ld(gy, o, gv);
+        if (gy2) {  // dual output: second consumer's gradient summed here
+          float g2[8];
+          P8<D>::ld(gy2, o, g2);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) gv[k] += g2[k];
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const uint8_t a = static_cast<uint8_t>(wv[k >> 2] >> (8 * (k & 3)));
@@ -209,13 +216,13 @@ void maxpool2d_forward(int dtype, const void* x, void* y, uint8_t* idx, const Po
   else hipLaunchKernelGGL(maxpool_fwd_kernel<POOL_F32>, grid, dim3(kT), 0, s, x, y, idx, g, e);
 }
 
-void maxpool2d_backward(int dtype, const void* gy, const uint8_t* idx, void* gx, const PoolGeom& g,
+void maxpool2d_backward(int dtype, const void* gy, const void* gy2, const uint8_t* idx, void* gx, const PoolGeom& g,
                         const PoolEpi& e, hipStream_t s) {
   const dim3 grid = grid_for(static_cast<int64_t>(g.N) * g.H * g.W * (g.C / 8));
   if (dtype == POOL_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<POOL_BF16>, grid, dim3(kT), 0, s, gy, idx, gx, g, e);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<POOL_BF16>, grid, dim3(kT), 0, s, gy, gy2, idx, gx, g, e);
   else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<POOL_F32>, grid, dim3(kT), 0, s, gy, idx, gx, g, e);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<POOL_F32>, grid, dim3(kT), 0, s, gy, gy2, idx, gx, g, e);
 }
 
 }  // namespace kern

@@ -30,7 +30,8 @@ struct PoolEpi {
 // y: [N, OH, OW, C] (NHWC), idx: uint8 window offset per output element.
 void maxpool2d_forward(int dtype, const void* x, void* y, uint8_t* idx, const PoolGeom& g, const PoolEpi& e,
                        hipStream_t s);
-void maxpool2d_backward(int dtype, const void* gy, const uint8_t* idx, void* gx, const PoolGeom& g,
+// gy2 (optional): a second output gradient (dual-output pool), summed in.
+void maxpool2d_backward(int dtype, const void* gy, const void* gy2, const uint8_t* idx, void* gx, const PoolGeom& g,
                         const PoolEpi& e, hipStream_t s);
 
 }  // namespace kern

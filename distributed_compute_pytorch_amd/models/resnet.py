@@ -49,9 +49,10 @@ class Bottleneck(nn.Module):
 
     def forward(self, x: torch.Tensor, identity: Optional[torch.Tensor] = None, dual: bool = False):
         """``identity``: alias of ``x`` produced by the previous block's
-        dual-output BN (its gradient is summed inside that BN's backward)."""
+        dual-output BN (its gradient is summed inside that BN's backward);
+        it feeds the residual add, or the downsample branch when there is one."""
         if self.downsample is not None:
-            identity = self.downsample(x)
+            identity = self.downsample(x if identity is None else identity)
         elif identity is None:
             identity = x
         out = self.bn1(self.conv1(x))
@@ -65,15 +66,17 @@ class BottleneckStage(nn.Sequential):
 
     use_dual = True
 
-    def forward(self, x):
+    def forward(self, x, ident=None, dual_out: bool = False):
+        """``ident``: alias of ``x`` from the previous stage's dual output;
+        ``dual_out``: return (y, alias) from the last block as well (for the
+        next stage's first block, whose conv1 and downsample both read y)."""
         blocks = list(self)
-        ident = None
         for i, blk in enumerate(blocks):
-            nxt = blocks[i + 1] if i + 1 < len(blocks) else None
-            dual = self.use_dual and nxt is not None and nxt.downsample is None
+            last = i + 1 == len(blocks)
+            dual = self.use_dual and (dual_out if last else True)
             out = blk(x, ident, dual=dual)
             x, ident = (out if dual else (out, None))
-        return x
+        return (x, ident) if dual_out and self.use_dual else x
 
 
 def _downsample(cin, cout, stride, fused_bn):
@@ -123,8 +126,20 @@ class ResNet(nn.Module):
         return stage
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.bn1(self.conv1(x)))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = self.bn1(self.conv1(x))
+        if self.fused_bn and self.dual_bn:
+            # thread dual-output aliases across stage boundaries: every
+            # fan-out gradient is summed inside a BN / pool backward kernel
+            if isinstance(self.maxpool, FusedMaxPool2d):
+                x, a = self.maxpool(x, dual=True)
+            else:
+                x, a = self.maxpool(x), None
+            x, a = self.layer1(x, a, True)
+            x, a = self.layer2(x, a, True)
+            x, a = self.layer3(x, a, True)
+            x = self.layer4(x, a, False)
+        else:
+            x = self.layer4(self.layer3(self.layer2(self.layer1(self.maxpool(x)))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 

@@ -12,26 +12,33 @@ from .._ext import C as _C
 
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p, relu, drop_p, rng):
+    def forward(ctx, x, k, s, p, relu, drop_p, rng, dual=False):
         seed, off = rng if rng is not None else (0, None)
         y, idx = _C.maxpool2d_fwd(x, k, s, p, relu, drop_p, seed, off)
         ctx.save_for_backward(idx, off if off is not None else idx.new_empty(0))
         ctx.geom = (k, s, p, drop_p, seed)
         ctx.shape = tuple(x.shape)
+        if dual:
+            return y, y.view_as(y)
         return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, gy2=None):
         idx, off = ctx.saved_tensors
         k, s, p, drop_p, seed = ctx.geom
-        gx = _C.maxpool2d_bwd(gy, idx, list(ctx.shape), k, s, p, drop_p, seed, off if off.numel() else None)
-        return gx, None, None, None, None, None, None
+        if gy is None:
+            gy, gy2 = gy2, None
+        gx = _C.maxpool2d_bwd(gy, idx, list(ctx.shape), k, s, p, drop_p, seed, off if off.numel() else None, gy2)
+        return gx, None, None, None, None, None, None, None
 
 
-def fused_max_pool2d(x, kernel_size: int = 3, stride: int = 2, padding: int = 0):
+def fused_max_pool2d(x, kernel_size: int = 3, stride: int = 2, padding: int = 0, dual: bool = False):
+    """``dual=True`` returns (y, alias) — two autograd outputs whose gradients
+    are summed inside the backward gather (a pooled map read by two convs)."""
     if _C.maxpool_supported(x, kernel_size, padding):
-        return _MaxPoolFn.apply(x, kernel_size, stride, padding, False, 0.0, None)
-    return F.max_pool2d(x, kernel_size, stride, padding)
+        return _MaxPoolFn.apply(x, kernel_size, stride, padding, False, 0.0, None, dual)
+    y = F.max_pool2d(x, kernel_size, stride, padding)
+    return (y, y) if dual else y
 
 
 def relu_max_pool2d_dropout(x, kernel_size: int = 2, stride: int = None, padding: int = 0, p: float = 0.0,
@@ -51,10 +58,11 @@ def relu_max_pool2d_dropout(x, kernel_size: int = 2, stride: int = None, padding
 class FusedMaxPool2d(nn.MaxPool2d):
     """nn.MaxPool2d (square kernel, no dilation / ceil_mode) on the NHWC kernel."""
 
-    def forward(self, x):
+    def forward(self, x, dual: bool = False):
         k = self.kernel_size if isinstance(self.kernel_size, int) else self.kernel_size[0]
         s = self.stride if isinstance(self.stride, int) else self.stride[0]
         p = self.padding if isinstance(self.padding, int) else self.padding[0]
         if self.dilation in (1, (1, 1)) and not self.ceil_mode and not self.return_indices:
-            return fused_max_pool2d(x, k, s, p)
-        return super().forward(x)
+            return fused_max_pool2d(x, k, s, p, dual)
+        y = super().forward(x)
+        return (y, y) if dual else y

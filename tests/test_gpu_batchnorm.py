@@ -145,3 +145,19 @@ def test_bn_dual_output_sums_gradients(cuda, dtype):
             # rounds the sum to bf16 first — compare in norm
             rel = float((u.float() - v.float()).norm() / v.float().norm())
             assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_maxpool_dual_output_sums_gradients(cuda, dtype):
+    from distributed_compute_pytorch_amd.ops import fused_max_pool2d
+
+    torch.manual_seed(0)
+    x = torch.randn(4, 64, 32, 32, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    xa = x.detach().clone().requires_grad_()
+    xb = x.detach().clone().requires_grad_()
+    y, ya = fused_max_pool2d(xa, 3, 2, 1, dual=True)
+    g1, g2 = torch.randn_like(y), torch.randn_like(y)
+    torch.autograd.backward([y, ya], [g1, g2])
+    fused_max_pool2d(xb, 3, 2, 1).backward((g1.float() + g2.float()).to(dtype))
+    rel = float((xa.grad.float() - xb.grad.float()).norm() / xb.grad.float().norm())
+    assert rel < (1e-6 if dtype == torch.float32 else 1e-2), rel
