@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--impl", choices=["ours", "torch"], default="ours")
     ap.add_argument("--fused", "--fused-bn", dest="fused", type=int, default=1)
     ap.add_argument("--channels-last", type=int, default=1)
+    ap.add_argument("--gemm", type=int, default=1, help="ResNet 1x1 convs as our MFMA GEMMs fused with BN")
     ap.add_argument("--bucket-cap-mb", type=float, default=None)
     ap.add_argument("--first-bucket-mb", type=float, default=None)
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
@@ -78,8 +79,25 @@ def parse():
     return ap.parse_args()
 
 
+def _heartbeat(period=30.0):
+    """Print a progress line every `period` s from a daemon thread: the first
+    steps on a fresh box (MIOpen kernel search / code-object loads) can run
+    for minutes without the main thread printing anything."""
+    import threading
+
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            log(f"[bench] alive t={time.time() - t0:.0f}s")
+
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     a = parse()
+    _heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -103,7 +121,7 @@ def main():
     fused = bool(a.fused) and ours
     torch.manual_seed(0)
     wl = workloads.build(a.model, dev, batch=a.batch, fused=fused, seq_len=a.seq_len, accum=a.accum,
-                         channels_last=bool(a.channels_last))
+                         channels_last=bool(a.channels_last), fused_gemm=bool(a.gemm))
 
     import contextlib
 
@@ -185,6 +203,8 @@ def main():
             "comm_dtype": a.comm_dtype,
             "hip_graph": bool(a.graph),
         }
+        if a.model == "resnet50":
+            cfg["mfma_1x1_gemm"] = bool(a.gemm) and fused
         if a.model == "resnet50":
             cfg.update(image_size=224, channels_last=bool(a.channels_last))
         if ours:

@@ -8,6 +8,7 @@
 
 #include "common.h"
 #include "kernels/bn_kernels.h"
+#include "kernels/gemm_kernels.h"
 #include "kernels/ln_kernels.h"
 #include "kernels/dropout_kernels.h"
 #include "kernels/pool_kernels.h"
@@ -90,7 +91,8 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
                                    const c10::optional<at::Tensor>& running_mean,
                                    const c10::optional<at::Tensor>& running_var,
                                    const c10::optional<at::Tensor>& residual, bool training, double momentum,
-                                   double eps, bool act, const c10::optional<at::Tensor>& num_batches_tracked) {
+                                   double eps, bool act, const c10::optional<at::Tensor>& num_batches_tracked,
+                                   const c10::optional<at::Tensor>& stats) {
   check_nhwc(x, "bn_act_fwd");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t C = x.size(1);
@@ -110,7 +112,12 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
   auto s = stream_of(x);
   if (training) {
     if (res.defined() && act) mbits = at::empty({M * C / 8}, x.options().dtype(at::kByte));
-    at::Tensor acc = zeroed_floats(2 * C, x, s);
+    // stats: (Σx, Σx²) accumulated by the producing GEMM's epilogue (conv1x1_fwd)
+    const bool ready = stats.has_value() && stats->defined();
+    if (ready)
+      DCP_CHECK(stats->scalar_type() == at::kFloat && stats->numel() == 2 * C && stats->is_contiguous(),
+                "bn_act_fwd: stats must be fp32 [2*C]");
+    at::Tensor acc = ready ? *stats : zeroed_floats(2 * C, x, s);
     float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
     float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
     kern::bn_forward_train(bn_dtype(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, y.data_ptr(), M,
@@ -121,7 +128,7 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
                            num_batches_tracked.has_value() && num_batches_tracked->defined()
                                ? num_batches_tracked->data_ptr<int64_t>()
                                : nullptr,
-                           mbits.defined() ? mbits.data_ptr<uint8_t>() : nullptr, s);
+                           mbits.defined() ? mbits.data_ptr<uint8_t>() : nullptr, ready, s);
   } else {
     DCP_CHECK(running_mean.has_value() && running_var.has_value(), "bn_act_fwd: eval mode needs running stats");
     mean.copy_(*running_mean);
@@ -135,6 +142,129 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
   }
   if (!mbits.defined()) mbits = at::empty({0}, x.options().dtype(at::kByte));
   return {y, mean, invstd, mbits};
+}
+
+// Training BN statistics without the apply (the consumer GEMM applies it):
+// returns (mean, invstd, scale, shift), updates running stats / nbt.
+std::vector<at::Tensor> bn_stats_coef(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
+                                      const c10::optional<at::Tensor>& bias,
+                                      const c10::optional<at::Tensor>& running_mean,
+                                      const c10::optional<at::Tensor>& running_var, double momentum, double eps,
+                                      const c10::optional<at::Tensor>& num_batches_tracked) {
+  check_nhwc(x, "bn_stats_coef");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor out = at::empty({4, C}, fopt);
+  auto s = stream_of(x);
+  at::Tensor acc = zeroed_floats(2 * C, x, s);
+  at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
+  at::Tensor b = bias.has_value() && bias->defined() ? bias->to(at::kFloat).contiguous() : at::Tensor();
+  kern::bn_stats_coef(bn_dtype(x), x.data_ptr(), M, static_cast<int>(C), w.defined() ? w.data_ptr<float>() : nullptr,
+                      b.defined() ? b.data_ptr<float>() : nullptr,
+                      running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr,
+                      running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr,
+                      static_cast<float>(momentum), static_cast<float>(eps), out[0].data_ptr<float>(),
+                      out[1].data_ptr<float>(), out[2].data_ptr<float>(), out[3].data_ptr<float>(),
+                      acc.data_ptr<float>(),
+                      num_batches_tracked.has_value() && num_batches_tracked->defined()
+                          ? num_batches_tracked->data_ptr<int64_t>()
+                          : nullptr,
+                      s);
+  return {out[0], out[1], out[2], out[3]};
+}
+
+// ------------------------------------------------- 1x1 conv as MFMA GEMM ---
+namespace {
+void check_gemm_act(const at::Tensor& x, const char* what) {
+  DCP_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, what, ": bf16 device tensor required");
+  DCP_CHECK((x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)) || (x.dim() == 2 && x.is_contiguous()),
+            what, ": expected a channels_last 4-D or contiguous [M, C] tensor");
+}
+const float* vec_or_null(const c10::optional<at::Tensor>& t, int64_t n, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == n && t->is_contiguous(), what,
+            ": scale/shift must be contiguous fp32 [C]");
+  return t->data_ptr<float>();
+}
+}  // namespace
+
+bool conv1x1_supported(int64_t M, int64_t cout, int64_t cin) { return kern::gemm_nt_supported(M, cout, cin); }
+
+// y = conv1x1(f(x), w) with f = relu?(x*scale + shift) per input channel when
+// scale is given; stats=True also returns the (Σy, Σy²) fp32 [2*Cout] sums.
+std::vector<at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& scale,
+                                    const c10::optional<at::Tensor>& shift, bool relu, bool stats) {
+  check_gemm_act(x, "conv1x1_fwd");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t K = x.size(1);
+  const int64_t M = x.numel() / K;
+  DCP_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() % K == 0, "conv1x1_fwd: weight");
+  const int64_t N = w.numel() / K;
+  DCP_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_fwd: unsupported shape");
+  const float* sc = vec_or_null(scale, K, "conv1x1_fwd");
+  const float* sf = vec_or_null(shift, K, "conv1x1_fwd");
+  DCP_CHECK((sc == nullptr) == (sf == nullptr), "conv1x1_fwd: scale and shift go together");
+  at::Tensor y = x.dim() == 4 ? at::empty({x.size(0), N, x.size(2), x.size(3)},
+                                          x.options().memory_format(at::MemoryFormat::ChannelsLast))
+                              : at::empty({M, N}, x.options());
+  auto s = stream_of(x);
+  at::Tensor st = stats ? zeroed_floats(2 * N, x, s) : at::empty({0}, x.options().dtype(at::kFloat));
+  kern::gemm_nt_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, static_cast<int>(N), static_cast<int>(K), sc, sf,
+                     relu, stats ? st.data_ptr<float>() : nullptr, s);
+  return {y, st};
+}
+
+// (w_bf16 [R, C], w_bf16^T [C, R]) from an fp32 (or bf16) weight viewed as [R, C]
+std::vector<at::Tensor> weight_bf16_t(const at::Tensor& w) {
+  DCP_CHECK(w.is_cuda() && w.dim() >= 2, "weight_bf16_t: device weight required");
+  c10::hip::HIPGuard guard(w.device().index());
+  const int64_t R = w.size(0);
+  const int64_t Cc = w.numel() / R;
+  at::Tensor wf = w.detach().reshape({R, Cc}).to(at::kFloat).contiguous();
+  at::Tensor wb = at::empty({R, Cc}, w.options().dtype(at::kBFloat16));
+  at::Tensor wt = at::empty({Cc, R}, w.options().dtype(at::kBFloat16));
+  kern::weight_cast_t(wf.data_ptr<float>(), wb.data_ptr(), wt.data_ptr(), static_cast<int>(R), static_cast<int>(Cc),
+                      stream_of(w));
+  return {wb, wt};
+}
+
+// dx[M, Cin] = gy[M, Cout] · w[Cout, Cin]; wt = w^T contiguous [Cin, Cout] bf16
+at::Tensor conv1x1_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
+  check_gemm_act(gy, "conv1x1_dgrad");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t K = gy.size(1);
+  const int64_t M = gy.numel() / K;
+  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % K == 0, "conv1x1_dgrad: weight");
+  const int64_t N = wt.numel() / K;
+  DCP_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_dgrad: unsupported shape");
+  at::Tensor dx = gy.dim() == 4 ? at::empty({gy.size(0), N, gy.size(2), gy.size(3)},
+                                            gy.options().memory_format(at::MemoryFormat::ChannelsLast))
+                                : at::empty({M, N}, gy.options());
+  kern::gemm_nt_bf16(gy.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, static_cast<int>(N), static_cast<int>(K),
+                     nullptr, nullptr, false, nullptr, stream_of(gy));
+  return dx;
+}
+
+// dw[Cout, Cin] (fp32) = Σ_m gy[m, :]^T ⊗ f(x)[m, :]
+at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::optional<at::Tensor>& scale,
+                         const c10::optional<at::Tensor>& shift, bool relu) {
+  check_gemm_act(gy, "conv1x1_wgrad");
+  check_gemm_act(x, "conv1x1_wgrad");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t N1 = gy.size(1), N2 = x.size(1);
+  const int64_t M = gy.numel() / N1;
+  DCP_CHECK(x.numel() / N2 == M, "conv1x1_wgrad: row mismatch");
+  DCP_CHECK(N1 % 64 == 0 && N2 % 64 == 0, "conv1x1_wgrad: channels must be multiples of 64");
+  const float* sc = vec_or_null(scale, N2, "conv1x1_wgrad");
+  const float* sf = vec_or_null(shift, N2, "conv1x1_wgrad");
+  at::Tensor dw = at::empty({N1, N2}, gy.options().dtype(at::kFloat));
+  at::Tensor ws = at::empty({kern::gemm_wgrad_workspace(M, static_cast<int>(N1), static_cast<int>(N2))},
+                            gy.options().dtype(at::kFloat));
+  kern::gemm_wgrad_bf16(gy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), M, static_cast<int>(N1),
+                        static_cast<int>(N2), sc, sf, relu, ws.data_ptr<float>(), stream_of(gy));
+  return dw;
 }
 
 // Returns (dx, dweight, dbias, dresidual).
@@ -483,7 +613,21 @@ void bind(pybind11::module& m) {
   m.def("bn_act_fwd", &bn_act_fwd, "fused NHWC BatchNorm(+residual)(+ReLU) forward", pybind11::arg("x"),
         pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"), pybind11::arg("running_var"),
         pybind11::arg("residual"), pybind11::arg("training"), pybind11::arg("momentum"), pybind11::arg("eps"),
-        pybind11::arg("act"), pybind11::arg("num_batches_tracked") = pybind11::none());
+        pybind11::arg("act"), pybind11::arg("num_batches_tracked") = pybind11::none(),
+        pybind11::arg("stats") = pybind11::none());
+  m.def("bn_stats_coef", &bn_stats_coef, "training BN statistics + folded scale/shift (no apply)",
+        pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
+        pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"),
+        pybind11::arg("num_batches_tracked") = pybind11::none());
+  m.def("conv1x1_supported", &conv1x1_supported);
+  m.def("conv1x1_fwd", &conv1x1_fwd, "NHWC 1x1 conv as an MFMA GEMM (+BN-apply prologue, +BN-stats epilogue)",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("scale") = pybind11::none(),
+        pybind11::arg("shift") = pybind11::none(), pybind11::arg("relu") = false, pybind11::arg("stats") = false);
+  m.def("conv1x1_dgrad", &conv1x1_dgrad, pybind11::arg("gy"), pybind11::arg("wt"));
+  m.def("weight_bf16_t", &weight_bf16_t, "fp32 weight -> (bf16 [R,C], bf16 transposed [C,R]) in one launch");
+  m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("gy"), pybind11::arg("x"),
+        pybind11::arg("scale") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
+        pybind11::arg("relu") = false);
   m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward", pybind11::arg("gy"),
         pybind11::arg("gy2"), pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
         pybind11::arg("mean"), pybind11::arg("invstd"), pybind11::arg("y"), pybind11::arg("act"),

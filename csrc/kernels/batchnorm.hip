@@ -181,10 +181,13 @@ __global__ void __launch_bounds__(kT) bn_stats_kernel(const void* __restrict__ x
 // Per-channel statistics from the accumulators (used by every apply thread
 // for its own 8 channels, and by the first thread group to publish
 // mean/invstd and update the running statistics).
+// zshift: acc holds unshifted sums (Σx, Σx²) — produced by a GEMM epilogue
+// (gemm.hip) instead of bn_stats_kernel.
 template <int D>
 __device__ __forceinline__ void stats_for(const float* acc, const void* x, int64_t M, int C, int c, float eps,
-                                          float* mean, float* var, float* invstd) {
-  const float sh = D == BN_BF16 ? bf2f(static_cast<const uint16_t*>(x)[c]) : static_cast<const float*>(x)[c];
+                                          float* mean, float* var, float* invstd, int zshift = 0) {
+  const float sh = zshift ? 0.f
+                          : (D == BN_BF16 ? bf2f(static_cast<const uint16_t*>(x)[c]) : static_cast<const float*>(x)[c]);
   const float dm = acc[c] / static_cast<float>(M);
   float v = acc[C + c] / static_cast<float>(M) - dm * dm;
   v = v < 0.f ? 0.f : v;
@@ -217,7 +220,8 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
                                                       float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                       float* running_mean, float* running_var, float momentum,
                                                       float eps, int64_t M, int64_t nvec, int C,
-                                                      int64_t* __restrict__ nbt, uint8_t* __restrict__ mbits) {
+                                                      int64_t* __restrict__ nbt, uint8_t* __restrict__ mbits,
+                                                      int zshift) {
   const int cv = C / kV;
   const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
@@ -228,7 +232,7 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
     const int c = c0 + k;
     if (TRAIN) {
       float mean, var, inv;
-      stats_for<D>(acc, x, M, C, c, eps, &mean, &var, &inv);
+      stats_for<D>(acc, x, M, C, c, eps, &mean, &var, &inv, zshift);
       coef(gamma, beta, c, mean, inv, &sc[k], &sf[k]);
       if (tid < cv) {  // one writer per channel
         mean_out[c] = mean;
@@ -282,6 +286,35 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
     if (RES) V8<D>::ld(res, v * kV, ra);
     one(a, ra, v);
     V8<D>::st(y, v * kV, a);
+  }
+}
+
+// ---------------------------------------------------------- finalize ----
+// Statistics only (the apply is fused into the consumer's GEMM prologue,
+// gemm.hip): per channel mean/invstd, running-stat update, folded
+// scale/shift (the same fp32 expressions as bn_apply_kernel's prologue).
+template <int D>
+__global__ void __launch_bounds__(kT) bn_finalize_kernel(const void* __restrict__ x, const float* __restrict__ acc,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ mean_out,
+                                                         float* __restrict__ invstd_out, float* __restrict__ scale_out,
+                                                         float* __restrict__ shift_out, float* running_mean,
+                                                         float* running_var, float momentum, float eps, int64_t M,
+                                                         int C, int64_t* __restrict__ nbt) {
+  const int c = blockIdx.x * kT + threadIdx.x;
+  if (nbt && c == 0) *nbt += 1;
+  if (c >= C) return;
+  float mean, var, inv, sc, sf;
+  stats_for<D>(acc, x, M, C, c, eps, &mean, &var, &inv);
+  coef(gamma, beta, c, mean, inv, &sc, &sf);
+  mean_out[c] = mean;
+  invstd_out[c] = inv;
+  scale_out[c] = sc;
+  shift_out[c] = sf;
+  if (running_mean) {
+    const float unb = M > 1 ? var * (static_cast<float>(M) / static_cast<float>(M - 1)) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
   }
 }
 
@@ -484,21 +517,25 @@ bool bn_supported(int C) {
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
                       float* mean, float* invstd, float* acc, bool act, int64_t* nbt, uint8_t* mbits,
-                      hipStream_t s) {
+                      bool acc_ready, hipStream_t s) {
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
   const size_t sm = red_smem(C);
-  if (dtype == BN_BF16)
+  if (acc_ready) {
+    // unshifted sums from the producing GEMM's epilogue: no statistics pass
+  } else if (dtype == BN_BF16) {
     hipLaunchKernelGGL(bn_stats_kernel<BN_BF16>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
-  else
+  } else {
     hipLaunchKernelGGL(bn_stats_kernel<BN_F32>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
+  }
+  const int zs = acc_ready ? 1 : 0;
   const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
 #define DCP_BN_APPLY(D, R, A)                                                                                     \
   hipLaunchKernelGGL((bn_apply_kernel<D, R, A, true>), dim3(grid), dim3(kT), 0, s, x, res, acc, gamma, beta,      \
                      nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M, nvec, C, nbt, \
-                     mbits)
+                     mbits, zs)
   const bool r = res != nullptr;
   if (dtype == BN_BF16) {
     if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
@@ -521,7 +558,7 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 #define DCP_BN_APPLY(D, R, A)                                                                                  \
   hipLaunchKernelGGL((bn_apply_kernel<D, R, A, false>), dim3(grid), dim3(kT), 0, s, x, res, nullptr, nullptr, \
                      nullptr, scale, shift, y, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, M, nvec, C, nullptr, \
-                     nullptr)
+                     nullptr, 0)
   const bool r = res != nullptr;
   if (dtype == BN_BF16) {
     if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
@@ -535,6 +572,25 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
     else DCP_BN_APPLY(BN_F32, false, false);
   }
 #undef DCP_BN_APPLY
+}
+
+void bn_stats_coef(int dtype, const void* x, int64_t M, int C, const float* gamma, const float* beta,
+                   float* running_mean, float* running_var, float momentum, float eps, float* mean, float* invstd,
+                   float* scale, float* shift, float* acc, int64_t* nbt, hipStream_t s) {
+  int nblk, nchunks;
+  int64_t rpb;
+  red_geometry(M, C, &nblk, &rpb, &nchunks);
+  const size_t sm = red_smem(C);
+  const dim3 fg((C + kT - 1) / kT);
+  if (dtype == BN_BF16) {
+    hipLaunchKernelGGL(bn_stats_kernel<BN_BF16>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
+    hipLaunchKernelGGL(bn_finalize_kernel<BN_BF16>, fg, dim3(kT), 0, s, x, acc, gamma, beta, mean, invstd, scale,
+                       shift, running_mean, running_var, momentum, eps, M, C, nbt);
+  } else {
+    hipLaunchKernelGGL(bn_stats_kernel<BN_F32>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
+    hipLaunchKernelGGL(bn_finalize_kernel<BN_F32>, fg, dim3(kT), 0, s, x, acc, gamma, beta, mean, invstd, scale,
+                       shift, running_mean, running_var, momentum, eps, M, C, nbt);
+  }
 }
 
 void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, const void* x, int64_t M, int C,

@@ -19,7 +19,16 @@ bool bn_supported(int C);
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
                       float* mean, float* invstd, float* acc, bool act, int64_t* nbt, uint8_t* mbits,
-                      hipStream_t s);
+                      bool acc_ready, hipStream_t s);
+// acc_ready: acc already holds UNSHIFTED (Σx, Σx²) from the producing GEMM's
+// epilogue (gemm.hip) — the statistics pass is skipped.
+
+// Training statistics only (no apply): mean/invstd, running-stat update,
+// folded scale = γ·invstd and shift = β − mean·scale for a consumer that
+// applies BN+ReLU in its own prologue (gemm.hip). acc: ZEROED [2*C] fp32.
+void bn_stats_coef(int dtype, const void* x, int64_t M, int C, const float* gamma, const float* beta,
+                   float* running_mean, float* running_var, float momentum, float eps, float* mean, float* invstd,
+                   float* scale, float* shift, float* acc, int64_t* nbt, hipStream_t s);
 
 // y = act(x * scale[c] + shift[c] [+ res])
 void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,

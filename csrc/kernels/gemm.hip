@@ -1,0 +1,613 @@
+// MFMA (v_mfma_f32_16x16x32_bf16) GEMMs for NHWC 1x1 convolutions on gfx950.
+//
+// Why hand-written: at ResNet-50 shapes (M = N*H*W up to 802,816 rows, K/N =
+// 64…2048 channels) a 1x1 convolution has 50–400 FLOP/byte, at or below the
+// MI355X ridge: mostly an HBM-streaming problem. The win is streaming X once
+// at full bandwidth and fusing the neighbouring BatchNorm passes:
+//   * prologue: BN-apply + ReLU of the producing layer on the X operand
+//     (per input channel scale/shift, applied to the MFMA fragment in
+//     registers) — BN's output is never written to HBM;
+//   * epilogue: per-output-channel Σy, Σy² of the bf16 output for the next
+//     BN (fp32 partials in registers across all of a block's tiles, one
+//     atomic per column per block) — its statistics pass disappears.
+//
+// Structure (both kernels): 256 threads = 4 waves (2×2), BK = 32, a 4-stage
+// LDS ring filled by global_load_lds_dwordx4 (async DMA into LDS, no VGPR
+// staging); one raw s_barrier per stage with a counted vmcnt so three stages
+// stay in flight across it. LDS images are lane-linear (the DMA's constraint),
+// so the bank-conflict swizzle is applied to the per-lane SOURCE address.
+//
+// gemm_nt_kernel   C[M,N] = f(A)[M,K]·B[N,K]^T   (forward; dgrad with B = W^T)
+//   MFMA operands swapped (W fragment as A, X fragment as B) so each lane's
+//   accumulator holds 4 consecutive output channels of one row: the epilogue
+//   stores 8-B packed bf16 straight from registers (no LDS round trip).
+//   Persistent over M tiles; grid.x a multiple of 8 so all N-tiles of an
+//   M-tile run on one XCD and share A through its L2.
+// gemm_wgrad_kernel D[N1,N2] = Σ_m A[m,:]^T ⊗ f(B)[m,:]  (reduction over M)
+//   stage = [32 m][channels] row-major as in HBM; operands (k = m) read with
+//   ds_read_b64_tr_b16 (gfx950 hardware transpose). Split over M into fp32
+//   slabs + one reduce launch (deterministic, no float atomics, no memset).
+//
+// Parity: replaces the MIOpen/CK 1x1 convolution kernels (fwd, bwd-data,
+// bwd-weights) for these layers (SURVEY §2f N8/N9, P2 "hand-written MFMA").
+#include <hip/hip_runtime.h>
+
+#include "gemm_kernels.h"
+
+namespace dcp {
+namespace kern {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kT = 256;
+constexpr int kBK = 32;  // k per stage
+constexpr int kNS = 4;   // LDS ring stages
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// two fp32 → packed bf16 (RNE) in one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  const bf16x2 v = {static_cast<__bf16>(a), static_cast<__bf16>(b)};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+// wait until at most N vector-memory ops of this wave are outstanding
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if constexpr (N == 22) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if constexpr (N == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+  else static_assert(N == 0, "add a vmcnt case");
+}
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// relu?(x*sc + sf) on one 8 x bf16 fragment
+__device__ __forceinline__ bf16x8 bn_act_frag(bf16x8 v, const float (&sc)[8], const float (&sf)[8], bool relu) {
+  uint4 u = __builtin_bit_cast(uint4, v);
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float a = fmaf(bf_lo(w[k]), sc[2 * k], sf[2 * k]);
+    float b = fmaf(bf_hi(w[k]), sc[2 * k + 1], sf[2 * k + 1]);
+    if (relu) {
+      a = fmaxf(a, 0.f);
+      b = fmaxf(b, 0.f);
+    }
+    w[k] = pack2(a, b);
+  }
+  return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
+}
+
+// ---------------------------------------------------------------- NT ----
+// Stage image: [rows][32 k] bf16, 64-B rows; physical 16-B chunk pc of row r
+// holds logical chunk pc ^ ((r>>2)&3): the 16 rows one ds_read_b128 group
+// reads at a fixed logical chunk land on 16 distinct bank slots.
+__device__ __forceinline__ int nt_swz(int r) { return (r >> 2) & 3; }
+
+template <int BM, int BN, bool PRO, bool STATS>
+__global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                     uint16_t* __restrict__ C, int64_t M, int N, int K,
+                                                     const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, int relu,
+                                                     float* __restrict__ stats, int tiles_m) {
+  constexpr int SA = BM * 64, SB = BN * 64, STAGE = SA + SB;  // bytes
+  constexpr int NA = SA / 4096, NB = SB / 4096;                // glds per wave per stage (1 KiB each)
+  constexpr int G = NA + NB;
+  constexpr int FM = BM / 32, FN = BN / 32;  // 16-row fragments per wave (2×2 waves)
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float* pro = reinterpret_cast<float*>(lds + kNS * STAGE);  // [2][K] scale, shift (PRO)
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int n0 = blockIdx.y * BN;
+  const int KT = K / kBK;
+  const int my_tiles = (tiles_m - static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) - 1) /
+                       static_cast<int>(gridDim.x);
+  const int T = my_tiles * KT;  // stages this block streams
+
+  if (PRO) {
+    for (int i = t; i < K; i += kT) {
+      pro[i] = scale[i];
+      pro[K + i] = shift[i];
+    }
+    __syncthreads();
+  }
+
+  // DMA issue for stage q into ring slot q % kNS
+  auto issue = [&](int q) {
+    if (q >= T) return;
+    const int tile = static_cast<int>(blockIdx.x) + (q / KT) * static_cast<int>(gridDim.x);
+    const int k0 = (q % KT) * kBK;
+    const int64_t m0 = static_cast<int64_t>(tile) * BM;
+    char* base = lds + (q % kNS) * STAGE;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int p = (wave * NA + j) * 64 + lane;  // 16-B unit in the A image
+      const int r = p >> 2, lc = (p & 3) ^ nt_swz(p >> 2);
+      int64_t gm = m0 + r;
+      gm = gm < M ? gm : M - 1;
+      glds16(A + gm * K + k0 + lc * 8, base + (wave * NA + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int p = (wave * NB + j) * 64 + lane;
+      const int r = p >> 2, lc = (p & 3) ^ nt_swz(p >> 2);
+      glds16(B + static_cast<int64_t>(n0 + r) * K + k0 + lc * 8, base + SA + (wave * NB + j) * 1024);
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssum[FN][4], ssq[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
+
+#pragma unroll
+  for (int q = 0; q < kNS - 1; ++q) issue(q);
+
+  const int ck = lane >> 4;  // logical 16-B chunk (k = 8ck … 8ck+7) this lane reads
+  constexpr int FS = FM * FN;  // epilogue stores per wave per tile
+  for (int q = 0; q < T; ++q) {
+    // vmcnt retires in issue order: the ops younger than stage q's DMA are the
+    // DMAs of q+1, q+2 and the epilogue stores of tile ends at q-3 … q-1
+    // (issued after q's DMA) — counting them keeps the ring full across tile
+    // boundaries instead of draining it at every epilogue.
+    if (q + kNS - 2 < T) {
+      int ends = 0;
+#pragma unroll
+      for (int d = 1; d <= kNS - 1; ++d) ends += (q - d >= 0 && (q - d) % KT == KT - 1) ? 1 : 0;
+      if (ends == 0) wait_vm<(kNS - 2) * G>();
+      else if (ends == 1) wait_vm<(kNS - 2) * G + FS>();
+      else wait_vm<(kNS - 2) * G + 2 * FS>();
+    } else {
+      wait_vm<0>();
+    }
+    barrier();  // stage q visible to all waves; all reads of slot (q-1)%kNS done
+    issue(q + kNS - 1);
+    const char* sA = lds + (q % kNS) * STAGE;
+    const char* sB = sA + SA;
+    const int kt = q % KT;
+    bf16x8 xf[FM], wf[FN];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int r = wm * (BM / 2) + j * 16 + (lane & 15);
+      xf[j] = *reinterpret_cast<const bf16x8*>(sA + r * 64 + 16 * (ck ^ nt_swz(r)));
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int r = wn * (BN / 2) + i * 16 + (lane & 15);
+      wf[i] = *reinterpret_cast<const bf16x8*>(sB + r * 64 + 16 * (ck ^ nt_swz(r)));
+    }
+    if (PRO) {
+      const int kk = kt * kBK + ck * 8;
+      float sc[8], sf[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sc[e] = pro[kk + e];
+        sf[e] = pro[K + kk + e];
+      }
+#pragma unroll
+      for (int j = 0; j < FM; ++j) xf[j] = bn_act_frag(xf[j], sc, sf, relu != 0);
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+
+    if (kt == KT - 1) {
+      // epilogue: acc[i][j][r] = C[m][n], m = … + (lane&15), n = … + 4(lane>>4) + r
+      const int64_t m0 = static_cast<int64_t>(static_cast<int>(blockIdx.x) + (q / KT) * static_cast<int>(gridDim.x)) * BM;
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int64_t m = m0 + wm * (BM / 2) + j * 16 + (lane & 15);
+        const bool ok = m < M;
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int n = n0 + wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
+          const uint32_t p01 = pack2(acc[i][j][0], acc[i][j][1]);
+          const uint32_t p23 = pack2(acc[i][j][2], acc[i][j][3]);
+          if (ok) {
+            *reinterpret_cast<uint2*>(C + m * N + n) = make_uint2(p01, p23);
+            if (STATS) {
+              const float v[4] = {bf_lo(p01), bf_hi(p01), bf_lo(p23), bf_hi(p23)};
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                ssum[i][r] += v[r];
+                ssq[i][r] = fmaf(v[r], v[r], ssq[i][r]);
+              }
+            }
+          }
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+  }
+  if (STATS) {
+    // reduce over the 16 rows (lane & 15) of each lane group, then over wm
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          ssum[i][r] += __shfl_xor(ssum[i][r], o);
+          ssq[i][r] += __shfl_xor(ssq[i][r], o);
+        }
+    wait_vm<0>();
+    __syncthreads();  // ring idle: reuse it
+    float* red = reinterpret_cast<float*>(lds);  // [sum|sq][wm][BN]
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wn * (BN / 2) + i * 16 + (lane >> 4) * 4 + r;
+          red[wm * BN + c] = ssum[i][r];
+          red[2 * BN + wm * BN + c] = ssq[i][r];
+        }
+    }
+    __syncthreads();
+    if (t < BN) {
+      atomicAdd(stats + n0 + t, red[t] + red[BN + t]);
+      atomicAdd(stats + N + n0 + t, red[2 * BN + t] + red[3 * BN + t]);
+    }
+  }
+}
+
+// ------------------------------------------------------------- wgrad ----
+// Stage image: [32 m][W channels] bf16, rows of 2W bytes; 32-B pair index
+// XOR f(row) so the 8 rows one 32-lane half reads with ds_read_b64_tr_b16
+// (rows 8g+4h+{0..3}, g = 0,1) land on 8 distinct 32-B bank slots.
+template <int W>
+__device__ __forceinline__ int tr_f(int r) {
+  if (W == 128) return (r & 3) | (((r >> 3) & 1) << 2);  // 256-B rows, 8 pairs
+  return ((r >> 1) & 1) | (((r >> 3) & 1) << 1);         // 128-B rows (W = 64), 4 pairs
+}
+
+// MFMA operand (16 channels × 8 k) for the 32-row stage at `base`, channels
+// c0 … c0+15: lane (g = lane>>4, q = (lane>>2)&3, p = lane&3) supplies row
+// 8g + 4h + q, columns c0 + 4p … +3 (h = 0, 1 → elements 0-3, 4-7).
+template <int W>
+__device__ __forceinline__ bf16x8 tr_frag(const char* base, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r0 = 8 * g + q, r1 = r0 + 4;
+  const int pair = c0 >> 4;
+  const char* a0 = base + r0 * (W * 2) + 32 * (pair ^ tr_f<W>(r0)) + 8 * p;
+  const char* a1 = base + r1 * (W * 2) + 32 * (pair ^ tr_f<W>(r1)) + 8 * p;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// zero the k-elements (m rows) at or past `valid` of an operand fragment
+__device__ __forceinline__ bf16x8 mask_rows(bf16x8 v, int valid, int lane) {
+  const int g = lane >> 4;
+  s16x8 s = __builtin_bit_cast(s16x8, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int row = 8 * g + (e & 3) + 4 * (e >> 2);
+    if (row >= valid) s[e] = 0;
+  }
+  return __builtin_bit_cast(bf16x8, s);
+}
+
+template <int BM, int BN, bool PRO>
+__global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                        float* __restrict__ ws, int64_t M, int N1, int N2,
+                                                        int64_t chunk, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, int relu, int tiles_j) {
+  constexpr int SA = 32 * BM * 2, SB = 32 * BN * 2, STAGE = SA + SB;
+  constexpr int NA = SA / 4096, NB = SB / 4096;  // glds per wave per stage
+  constexpr int G = NA + NB;
+  constexpr int ACPR = BM / 8, BCPR = BN / 8;  // 16-B chunks per stage row
+  constexpr int FM = BM / 32, FN = BN / 32;
+  __shared__ __attribute__((aligned(16))) char lds[kNS * STAGE];
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wi = wave >> 1, wj = wave & 1;
+  const int ti = blockIdx.x / tiles_j, tj = blockIdx.x % tiles_j;
+  const int i0 = ti * BM, j0 = tj * BN;
+  const int64_t mz0 = static_cast<int64_t>(blockIdx.y) * chunk;
+  const int64_t mz1 = min(M, mz0 + chunk);
+  const int T = mz0 < mz1 ? static_cast<int>((mz1 - mz0 + kBK - 1) / kBK) : 0;
+
+  // per-lane BN coefficients of its B-fragment channel (one channel per lane per fragment)
+  float psc[FN], psf[FN];
+  if (PRO) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = j0 + wj * (BN / 2) + j * 16 + (lane & 15);
+      psc[j] = scale[c];
+      psf[j] = shift[c];
+    }
+    // retire these plain loads here (compiler-visible vmcnt(0)): otherwise their
+    // first use inside the ring loop would drain the in-flight DMA every stage
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  }
+
+  auto issue = [&](int q) {
+    if (q >= T) return;
+    const int64_t mb = mz0 + static_cast<int64_t>(q) * kBK;
+    char* base = lds + (q % kNS) * STAGE;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int p = (wave * NA + j) * 64 + lane;
+      const int r = p / ACPR, pc = p % ACPR;
+      const int lc = 2 * ((pc >> 1) ^ tr_f<BM>(r)) + (pc & 1);
+      int64_t gm = mb + r;
+      gm = gm < mz1 ? gm : mz1 - 1;
+      glds16(A + gm * N1 + i0 + lc * 8, base + (wave * NA + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int p = (wave * NB + j) * 64 + lane;
+      const int r = p / BCPR, pc = p % BCPR;
+      const int lc = 2 * ((pc >> 1) ^ tr_f<BN>(r)) + (pc & 1);
+      int64_t gm = mb + r;
+      gm = gm < mz1 ? gm : mz1 - 1;
+      glds16(B + gm * N2 + j0 + lc * 8, base + SA + (wave * NB + j) * 1024);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int q = 0; q < kNS - 1; ++q) issue(q);
+  for (int q = 0; q < T; ++q) {
+    if (q + kNS - 2 < T) wait_vm<(kNS - 2) * G>();
+    else wait_vm<0>();
+    barrier();
+    issue(q + kNS - 1);
+    const char* sA = lds + (q % kNS) * STAGE;
+    const char* sB = sA + SA;
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = tr_frag<BM>(sA, wi * (BM / 2) + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bfr[j] = tr_frag<BN>(sB, wj * (BN / 2) + j * 16, lane);
+      if (PRO) {
+        float sc[8], sf[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sc[e] = psc[j];
+          sf[e] = psf[j];
+        }
+        bfr[j] = bn_act_frag(bfr[j], sc, sf, relu != 0);
+      }
+    }
+    const int64_t valid = mz1 - (mz0 + static_cast<int64_t>(q) * kBK);
+    if (valid < kBK) {  // ragged last stage: rows past the slice contribute zero (A side)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = mask_rows(af[i], static_cast<int>(valid), lane);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  float* out = ws + static_cast<int64_t>(blockIdx.y) * N1 * N2;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i0 + wi * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        const int col = j0 + wj * (BN / 2) + j * 16 + (lane & 15);
+        out[static_cast<int64_t>(row) * N2 + col] = acc[i][j][r];
+      }
+}
+
+// Slab reduction, two levels so ~S/16 × more loads are in flight than a
+// per-thread loop over all S slabs: P[y][v] = Σ_{z∈[16y,16y+16)} ws[z][v],
+// then D[v] = Σ_y P[y][v]. Deterministic (fixed order).
+constexpr int kSlabGroup = 16;
+__global__ void __launch_bounds__(kT) slab_partial_kernel(const float4* __restrict__ ws, float4* __restrict__ out,
+                                                          int64_t n4, int S) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (v >= n4) return;
+  const int z0 = blockIdx.y * kSlabGroup;
+  float4 a[kSlabGroup];
+#pragma unroll
+  for (int k = 0; k < kSlabGroup; ++k) {  // clamped index, masked after the load: no branch per load
+    const int z = min(z0 + k, S - 1);
+    a[k] = ws[static_cast<int64_t>(z) * n4 + v];
+  }
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < kSlabGroup; ++k) {
+    const float w = (z0 + k < S) ? 1.f : 0.f;
+    s.x = fmaf(a[k].x, w, s.x);
+    s.y = fmaf(a[k].y, w, s.y);
+    s.z = fmaf(a[k].z, w, s.z);
+    s.w = fmaf(a[k].w, w, s.w);
+  }
+  out[static_cast<int64_t>(blockIdx.y) * n4 + v] = s;
+}
+
+// fp32 [R][Cc] weight → bf16 w [R][Cc] and w^T [Cc][R] (RNE), one launch
+__global__ void __launch_bounds__(kT) weight_cast_t_kernel(const float* __restrict__ w, uint16_t* __restrict__ wb,
+                                                           uint16_t* __restrict__ wt, int R, int Cc) {
+  __shared__ uint16_t tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 × 8
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int r = r0 + ty + k, c = c0 + tx;
+    if (r < R && c < Cc) {
+      const __bf16 h = static_cast<__bf16>(w[static_cast<int64_t>(r) * Cc + c]);
+      const uint16_t u = __builtin_bit_cast(uint16_t, h);
+      wb[static_cast<int64_t>(r) * Cc + c] = u;
+      tile[ty + k][tx] = u;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int c = c0 + ty + k, r = r0 + tx;
+    if (r < R && c < Cc) wt[static_cast<int64_t>(c) * R + r] = tile[tx][ty + k];
+  }
+}
+
+struct WgradPlan {
+  int bm, bn, tiles, S;
+  int64_t chunk;
+};
+
+WgradPlan wgrad_plan(int64_t M, int N1, int N2) {
+  WgradPlan p;
+  p.bm = N1 % 128 == 0 ? 128 : 64;
+  p.bn = N2 % 128 == 0 ? 128 : 64;
+  p.tiles = (N1 / p.bm) * (N2 / p.bn);
+  const int64_t ksteps = (M + kBK - 1) / kBK;
+  int64_t S = 512 / p.tiles;  // ~2 blocks per CU
+  // keep the slab traffic ≤ ~1/4 of the operand traffic
+  const int64_t cap = (M * (N1 + N2) * 2 / 4) / (static_cast<int64_t>(N1) * N2 * 4);
+  if (S > cap) S = cap;
+  if (S > ksteps) S = ksteps;
+  if (S < 1) S = 1;
+  p.chunk = ((ksteps + S - 1) / S) * kBK;
+  p.S = static_cast<int>((M + p.chunk - 1) / p.chunk);
+  return p;
+}
+
+}  // namespace
+
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) {
+  return M >= 1 && N > 0 && K > 0 && N % 64 == 0 && K % 64 == 0 && K <= 4096;
+}
+
+void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                  const float* shift, bool relu, float* stats, hipStream_t s) {
+  const int BN = N % 128 == 0 ? 128 : 64;
+  constexpr int BM = 128;
+  const int tiles_m = static_cast<int>((M + BM - 1) / BM);
+  const int tn = N / BN;
+  // persistent over M tiles: ~2 workgroups per CU, grid.x a multiple of 8 (XCD-aligned N-tiles)
+  int gx = (512 / tn) & ~7;
+  if (gx < 8) gx = 8;
+  if (gx > tiles_m) gx = tiles_m;
+  const dim3 grid(gx, tn);
+  const bool pro = scale != nullptr;
+  const bool st = stats != nullptr;
+  const size_t lds = static_cast<size_t>(kNS) * (BM + BN) * 64 + (pro ? 8 * static_cast<size_t>(K) : 0);
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  auto c = static_cast<uint16_t*>(C);
+#define DCP_GNT(BN_, P, S_)                                                                                      \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P, S_>), grid, dim3(kT), lds, s, a, b, c, M, N, K, scale, shift, \
+                     relu ? 1 : 0, stats, tiles_m)
+  if (BN == 128) {
+    if (pro && st) DCP_GNT(128, true, true);
+    else if (pro) DCP_GNT(128, true, false);
+    else if (st) DCP_GNT(128, false, true);
+    else DCP_GNT(128, false, false);
+  } else {
+    if (pro && st) DCP_GNT(64, true, true);
+    else if (pro) DCP_GNT(64, true, false);
+    else if (st) DCP_GNT(64, false, true);
+    else DCP_GNT(64, false, false);
+  }
+#undef DCP_GNT
+}
+
+void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s) {
+  const dim3 grid((Cc + 31) / 32, (R + 31) / 32);
+  hipLaunchKernelGGL(weight_cast_t_kernel, grid, dim3(kT), 0, s, w, static_cast<uint16_t*>(wb),
+                     static_cast<uint16_t*>(wt), R, Cc);
+}
+
+int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2) {
+  const WgradPlan p = wgrad_plan(M, N1, N2);
+  const int64_t groups = (p.S + kSlabGroup - 1) / kSlabGroup;
+  return (static_cast<int64_t>(p.S) + (groups > 1 ? groups : 0)) * N1 * N2;
+}
+
+void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
+                     const float* shift, bool relu, float* ws, hipStream_t s) {
+  const WgradPlan p = wgrad_plan(M, N1, N2);
+  const dim3 grid(p.tiles, p.S);
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  const bool pro = scale != nullptr;
+  const int tj = N2 / p.bn;
+#define DCP_GWG(BM_, BN_, P)                                                                                     \
+  hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, p.chunk, scale, \
+                     shift, relu ? 1 : 0, tj)
+#define DCP_GWG2(BM_, BN_)        \
+  do {                            \
+    if (pro)                      \
+      DCP_GWG(BM_, BN_, true);    \
+    else                          \
+      DCP_GWG(BM_, BN_, false);   \
+  } while (0)
+  if (p.bm == 128 && p.bn == 128) DCP_GWG2(128, 128);
+  else if (p.bm == 128) DCP_GWG2(128, 64);
+  else if (p.bn == 128) DCP_GWG2(64, 128);
+  else DCP_GWG2(64, 64);
+#undef DCP_GWG2
+#undef DCP_GWG
+  const int64_t n4 = static_cast<int64_t>(N1) * N2 / 4;
+  const int gx = static_cast<int>((n4 + kT - 1) / kT);
+  const int groups = (p.S + kSlabGroup - 1) / kSlabGroup;
+  auto w4 = reinterpret_cast<const float4*>(ws);
+  if (groups == 1) {
+    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, w4, reinterpret_cast<float4*>(D), n4, p.S);
+  } else {
+    float4* part = reinterpret_cast<float4*>(ws + static_cast<int64_t>(p.S) * N1 * N2);
+    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, groups), dim3(kT), 0, s, w4, part, n4, p.S);
+    // groups ≤ 32 (S ≤ 512): ≤ 2 more levels
+    int S2 = groups;
+    const float4* src = part;
+    float4* dst = reinterpret_cast<float4*>(D);
+    if (S2 > kSlabGroup) {  // one intermediate level back into the head of ws
+      const int g2 = (S2 + kSlabGroup - 1) / kSlabGroup;
+      float4* mid = reinterpret_cast<float4*>(ws);
+      hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, g2), dim3(kT), 0, s, src, mid, n4, S2);
+      src = mid;
+      S2 = g2;
+    }
+    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, src, dst, n4, S2);
+  }
+}
+
+}  // namespace kern
+}  // namespace dcp

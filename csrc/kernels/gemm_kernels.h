@@ -1,0 +1,44 @@
+// Launch API of the MFMA GEMM kernels for NHWC 1x1 convolutions (gemm.hip).
+//
+// A stride-1 1x1 convolution over an NHWC activation is a GEMM over the
+// [M = N*H*W rows][C channels] view:
+//   forward  Y[M, Co]  = f(X)[M, Ci] · W[Co, Ci]^T
+//   dgrad    dX[M, Ci] = dY[M, Co]  · W[Co, Ci]        (B = W^T [Ci][Co])
+//   wgrad    dW[Co, Ci] = dY^T[Co, M] · f(X)[M, Ci]
+// f = optional BatchNorm-apply + ReLU of the producing layer (per input
+// channel scale/shift), applied while staging X into LDS, so that BN's
+// output is never written to HBM. The forward can also accumulate the
+// per-output-channel Σy, Σy² of the (bf16-rounded) output for the next BN.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dcp {
+namespace kern {
+
+// Shapes the kernels take: K and N multiples of 64, any M ≥ 1.
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
+
+// C[M,N] (bf16, row-major ldc=N) = f(A)[M,K] (bf16, lda=K) · B[N,K]^T (bf16, ldb=K).
+// scale/shift: [K] fp32 or null (then f = identity); relu applies with scale.
+// stats: null, or a ZEROED fp32 [2*N] accumulator += (Σ_m c, Σ_m c²).
+void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                  const float* shift, bool relu, float* stats, hipStream_t s);
+
+// fp32 weight [R][Cc] → bf16 copy wb [R][Cc] and transposed bf16 wt [Cc][R]
+// (the forward GEMM's B operand and the dgrad GEMM's B operand) in one launch.
+void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s);
+
+// Workspace (fp32 elements) gemm_wgrad_bf16 needs for this shape.
+int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2);
+
+// D[N1,N2] (fp32) = Σ_m A[m, :N1] (bf16, lda=N1) ⊗ f(B)[m, :N2] (bf16, ldb=N2)
+// (f = optional per-column scale/shift/relu). Deterministic: split over M
+// into fp32 slabs in `ws`, then one reduction launch.
+void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
+                     const float* shift, bool relu, float* ws, hipStream_t s);
+
+}  // namespace kern
+}  // namespace dcp

@@ -19,6 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv import bn_relu_conv1x1, conv1x1 as gemm_conv1x1, gemm_ok
 from ..ops.pool import FusedMaxPool2d
 
 
@@ -34,8 +35,10 @@ class Bottleneck(nn.Module):
     expansion = 4
 
     def __init__(self, cin: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None,
-                 fused_bn: bool = False):
+                 fused_bn: bool = False, fused_gemm: Optional[bool] = None):
         super().__init__()
+        # 1x1 convs as MFMA GEMMs fused with the BN passes (training, bf16 NHWC)
+        self.fused_gemm = fused_bn if fused_gemm is None else fused_gemm
         cout = width * self.expansion
         self.conv1 = conv1x1(cin, width)
         self.bn1 = BatchNormAct2d(width, act=True, fused=fused_bn)
@@ -51,6 +54,8 @@ class Bottleneck(nn.Module):
         """``identity``: alias of ``x`` produced by the previous block's
         dual-output BN (its gradient is summed inside that BN's backward);
         it feeds the residual add, or the downsample branch when there is one."""
+        if self._gemm_path(x):
+            return self._forward_gemm(x, identity, dual)
         if self.downsample is not None:
             identity = self.downsample(x if identity is None else identity)
         elif identity is None:
@@ -58,6 +63,34 @@ class Bottleneck(nn.Module):
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out), identity, dual=dual)
+
+    def _gemm_path(self, x: torch.Tensor) -> bool:
+        return (self.fused_gemm and self.training and self.bn1.fused and self.bn2.fused and self.bn3.fused
+                and gemm_ok(x, self.conv1.in_channels, self.conv1.out_channels)
+                and self.conv3.out_channels % 64 == 0 and self.conv3.in_channels % 64 == 0)
+
+    def _forward_gemm(self, x, identity, dual):
+        """conv1 (GEMM, BN1 sums in its epilogue) → BN1+ReLU apply → conv2
+        (MIOpen 3x3) → BN2 statistics → conv3 GEMM with BN2+ReLU applied in its
+        prologue and BN3 sums in its epilogue → BN3 + residual + ReLU apply.
+        Per block this drops the BN1/BN3 statistics passes and BN2's apply
+        (a full write + read of the 3x3 conv's activation)."""
+        inp = x if identity is None else identity
+        if self.downsample is not None:
+            conv, bn = self.downsample[0], self.downsample[1]
+            if conv.stride == (1, 1) and gemm_ok(inp, conv.in_channels, conv.out_channels):
+                z, st = gemm_conv1x1(inp, conv.weight, stats=True)
+                identity = bn(z, stats=st)
+            else:
+                identity = self.downsample(inp)
+        else:
+            identity = inp
+        z1, s1 = gemm_conv1x1(x, self.conv1.weight, stats=True)
+        x2 = self.conv2(self.bn1(z1, stats=s1))
+        if not x2.is_contiguous(memory_format=torch.channels_last):
+            x2 = x2.contiguous(memory_format=torch.channels_last)
+        z3, s3 = bn_relu_conv1x1(x2, self.bn2, self.conv3.weight, stats=True)
+        return self.bn3(z3, identity, dual=dual, stats=s3)
 
 
 class BottleneckStage(nn.Sequential):
@@ -87,10 +120,11 @@ def _downsample(cin, cout, stride, fused_bn):
 class ResNet(nn.Module):
     def __init__(self, block: Type[Bottleneck], layers: List[int], num_classes: int = 1000,
                  zero_init_residual: bool = False, fused_bn: bool = False, fused_pool: Optional[bool] = None,
-                 dual_bn: bool = True):
+                 dual_bn: bool = True, fused_gemm: Optional[bool] = None):
         super().__init__()
         self.inplanes = 64
         self.fused_bn = fused_bn
+        self.fused_gemm = fused_bn if fused_gemm is None else fused_gemm
         self.dual_bn = dual_bn
         fused_pool = fused_bn if fused_pool is None else fused_pool
         self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
@@ -117,10 +151,10 @@ class ResNet(nn.Module):
         downsample = None
         if stride != 1 or self.inplanes != width * block.expansion:
             downsample = _downsample(self.inplanes, width * block.expansion, stride, self.fused_bn)
-        layers = [block(self.inplanes, width, stride, downsample, self.fused_bn)]
+        layers = [block(self.inplanes, width, stride, downsample, self.fused_bn, self.fused_gemm)]
         self.inplanes = width * block.expansion
         for _ in range(1, blocks):
-            layers.append(block(self.inplanes, width, fused_bn=self.fused_bn))
+            layers.append(block(self.inplanes, width, fused_bn=self.fused_bn, fused_gemm=self.fused_gemm))
         stage = BottleneckStage(*layers)
         stage.use_dual = self.dual_bn
         return stage

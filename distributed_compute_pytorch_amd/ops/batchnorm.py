@@ -29,15 +29,17 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return (self.fused and x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
                 and x.is_contiguous(memory_format=torch.channels_last) and _C.bn_supported(x.shape[1]))
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, dual: bool = False):
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, dual: bool = False,
+                stats: Optional[torch.Tensor] = None):
         """``dual=True`` returns (y, y_alias): two autograd outputs over the same
         data for two consumers (next conv + next residual add); their gradients
         are summed inside this op's backward kernel instead of by a separate
-        autograd add."""
+        autograd add. ``stats``: (Σx, Σx²) fp32 [2*C] already accumulated by the
+        producing GEMM's epilogue (:func:`.conv.conv1x1`); training mode only."""
         if self._use_fused(x):
             return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.num_batches_tracked,
                           self.training, self.momentum, self.eps, residual if self.residual else None, self.act,
-                          dual)
+                          dual, stats if self.training else None)
         y = super().forward(x)
         if self.residual and residual is not None:
             y = y + residual
@@ -49,10 +51,10 @@ class BatchNormAct2d(nn.BatchNorm2d):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual,
-                nbt=None):
+                nbt=None, stats=None):
         # nbt (num_batches_tracked) is incremented inside the apply kernel
         y, mean, invstd, bits = _C.bn_act_fwd(x, weight, bias, running_mean, running_var, residual, training,
-                                              float(momentum), float(eps), bool(act), nbt)
+                                              float(momentum), float(eps), bool(act), nbt, stats)
         # with the 1-bit ReLU mask (residual + act, training) the backward never reads y
         ctx.save_for_backward(x, weight, bias, mean, invstd, y if bits.numel() == 0 else bits)
         ctx.bits = bits.numel() > 0
@@ -72,17 +74,17 @@ class _BNActFn(torch.autograd.Function):
         y, bits = (x, y_or_bits) if ctx.bits else (y_or_bits, None)  # y unused when bits are given
         gx, gw, gb, gres = _C.bn_act_bwd(gy, gy2, x, weight, bias, mean, invstd, y, ctx.act, ctx.has_res,
                                          ctx.training, bits)
-        return gx, gw, gb, None, None, None, None, None, (gres if ctx.has_res else None), None, None, None
+        return gx, gw, gb, None, None, None, None, None, (gres if ctx.has_res else None), None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, num_batches_tracked, training, momentum, eps, residual,
-           act, dual: bool = False):
+           act, dual: bool = False, stats=None):
     nbt = num_batches_tracked if (training and num_batches_tracked is not None) else None
     if nbt is not None and (nbt.device != x.device or nbt.dtype != torch.int64):
         nbt.add_(1)
         nbt = None
     return _BNActFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, act, dual,
-                          nbt)
+                          nbt, stats)
 
 
 class BatchNormAct1d(nn.BatchNorm1d):

@@ -1,0 +1,114 @@
+"""1x1 convolutions on NHWC bf16 activations as hand-written MFMA GEMMs
+(``csrc/kernels/gemm.hip``), fused with the neighbouring BatchNorm passes.
+
+* :func:`conv1x1` — ``y = conv1x1(x, w)``; optionally also returns the
+  per-output-channel (Σy, Σy²) accumulated in the GEMM epilogue, which the
+  following :class:`~.batchnorm.BatchNormAct2d` consumes instead of running
+  its own statistics pass over ``y``.
+* :func:`bn_relu_conv1x1` — ``z = conv1x1(relu(bn(x)), w)`` in training mode:
+  BN statistics of ``x`` (one read), then the GEMM applies BN + ReLU to ``x``
+  while staging it into LDS — BN's output is never written to HBM. Backward:
+  dgrad GEMM → BN+ReLU backward (mask recomputed from ``x``), and a wgrad
+  GEMM that re-applies BN + ReLU to ``x`` in its prologue.
+
+Weight gradients are produced in fp32 directly (no bf16→fp32 cast pass).
+These replace MIOpen's 1x1 convolution kernels + the BN statistics/apply
+kernels for ResNet-50's bottleneck 1x1 layers (the
+reference framework's cuDNN/cuBLAS role).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .._ext import C as _C
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.bfloat16:
+        t = t.to(torch.bfloat16)
+    return t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t.contiguous()
+
+
+def _w2d(weight: torch.Tensor):
+    """(bf16 [Cout, Cin], bf16 [Cin, Cout]): forward and dgrad B operands, one launch."""
+    return _C.weight_bf16_t(weight)
+
+
+def gemm_ok(x: torch.Tensor, cin: int, cout: int) -> bool:
+    """True when the MFMA 1x1 path handles this activation."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and bool(_C.conv1x1_supported(x.numel() // max(cin, 1), cout, cin)))
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stats):
+        w, wt = _w2d(weight)
+        y, st = _C.conv1x1_fwd(x, w, None, None, False, bool(stats))
+        ctx.save_for_backward(x, wt)
+        ctx.wshape, ctx.wdtype = weight.shape, weight.dtype
+        ctx.mark_non_differentiable(st)
+        ctx.set_materialize_grads(False)  # no zero-filled grad for the sums output
+        return y, st
+
+    @staticmethod
+    def backward(ctx, gy, _gst):
+        x, wt = ctx.saved_tensors
+        if gy is None:
+            return None, None, None
+        gy = _cl(gy)
+        dx = _C.conv1x1_dgrad(gy, wt) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = _C.conv1x1_wgrad(gy, x).view(ctx.wshape)
+            if dw.dtype != ctx.wdtype:
+                dw = dw.to(ctx.wdtype)
+        return dx, dw, None
+
+
+class _BNReluConv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, weight, running_mean, running_var, nbt, momentum, eps, stats):
+        mean, invstd, scale, shift = _C.bn_stats_coef(x, gamma, beta, running_mean, running_var, float(momentum),
+                                                      float(eps), nbt)
+        w, wt = _w2d(weight)
+        z, st = _C.conv1x1_fwd(x, w, scale, shift, True, bool(stats))
+        ctx.save_for_backward(x, gamma, beta, wt, mean, invstd, scale, shift)
+        ctx.wshape, ctx.wdtype = weight.shape, weight.dtype
+        ctx.mark_non_differentiable(st)
+        ctx.set_materialize_grads(False)
+        return z, st
+
+    @staticmethod
+    def backward(ctx, gz, _gst):
+        x, gamma, beta, wt, mean, invstd, scale, shift = ctx.saved_tensors
+        if gz is None:
+            return (None,) * 10
+        gz = _cl(gz)
+        dw = _C.conv1x1_wgrad(gz, x, scale, shift, True).view(ctx.wshape)
+        if dw.dtype != ctx.wdtype:
+            dw = dw.to(ctx.wdtype)
+        da = _C.conv1x1_dgrad(gz, wt)
+        # BN + ReLU backward; the ReLU mask is recomputed from x (training coefficients)
+        dx, dgamma, dbeta, _ = _C.bn_act_bwd(da, None, x, gamma, beta, mean, invstd, x, True, False, True, None)
+        return dx, dgamma, dbeta, dw, None, None, None, None, None, None
+
+
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, stats: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """NHWC bf16 1x1 stride-1 convolution (no bias). Returns (y, sums) with
+    ``sums`` = fp32 [2*Cout] (Σy, Σy²) when ``stats`` else an empty tensor."""
+    return _Conv1x1Fn.apply(x, weight, stats)
+
+
+def bn_relu_conv1x1(x: torch.Tensor, bn, weight: torch.Tensor, stats: bool = False):
+    """``conv1x1(relu(bn(x)), weight)`` for a training-mode ``BatchNorm2d``
+    ``bn`` (its running statistics and ``num_batches_tracked`` are updated)."""
+    nbt = bn.num_batches_tracked
+    if nbt is not None and (nbt.device != x.device or nbt.dtype != torch.int64):
+        nbt.add_(1)
+        nbt = None
+    return _BNReluConv1x1Fn.apply(x, bn.weight, bn.bias, weight, bn.running_mean, bn.running_var, nbt, bn.momentum,
+                                  bn.eps, stats)

@@ -71,13 +71,13 @@ class _TokenData:
 
 
 def build(name: str, device, batch: Optional[int] = None, fused: bool = True, seq_len: Optional[int] = None,
-          accum: Optional[int] = None, channels_last: bool = True) -> Workload:
+          accum: Optional[int] = None, channels_last: bool = True, fused_gemm: Optional[bool] = None) -> Workload:
     from . import models
 
     name = name.lower()
     if name == "resnet50":
         b = batch or 256
-        m = models.resnet50(fused_bn=fused).to(device)
+        m = models.resnet50(fused_bn=fused, fused_gemm=fused if fused_gemm is None else (fused and fused_gemm)).to(device)
         if channels_last:
             m = m.to(memory_format=torch.channels_last)
         data = SyntheticBatches(b, (3, 224, 224), 1000, device, channels_last=channels_last, pool=2)
