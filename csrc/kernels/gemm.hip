@@ -69,7 +69,11 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 11) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
   else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
   else if constexpr (N == 22) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
   else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
@@ -105,6 +109,8 @@ __device__ __forceinline__ bf16x8 bn_act_frag(bf16x8 v, const float (&sc)[8], co
 // reads at a fixed logical chunk land on 16 distinct bank slots.
 __device__ __forceinline__ int nt_swz(int r) { return (r >> 2) & 3; }
 
+constexpr int kNSnt = 3;  // NT ring stages (leaves LDS for the per-wave C staging at 2 blocks/CU)
+
 template <int BM, int BN, bool PRO, bool STATS>
 __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                      uint16_t* __restrict__ C, int64_t M, int N, int K,
@@ -115,8 +121,14 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
   constexpr int NA = SA / 4096, NB = SB / 4096;                // glds per wave per stage (1 KiB each)
   constexpr int G = NA + NB;
   constexpr int FM = BM / 32, FN = BN / 32;  // 16-row fragments per wave (2×2 waves)
+  constexpr int WN = BN / 2;                 // wave tile columns
+  constexpr int CST = 32 * WN * 2;           // per-wave C staging: 32 rows × WN bf16
+  constexpr int LPR = WN / 8;                // lanes per staged row (16 B each)
+  constexpr int RPI = 64 / LPR;              // staged rows per store instruction
+  constexpr int FS = 2 * (32 / RPI);         // global stores per wave per tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  float* pro = reinterpret_cast<float*>(lds + kNS * STAGE);  // [2][K] scale, shift (PRO)
+  char* cst_all = lds + kNSnt * STAGE;
+  float* pro = reinterpret_cast<float*>(cst_all + 4 * CST);  // [2][K] scale, shift (PRO)
 
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -127,6 +139,7 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
   const int my_tiles = (tiles_m - static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) - 1) /
                        static_cast<int>(gridDim.x);
   const int T = my_tiles * KT;  // stages this block streams
+  char* cst = cst_all + wave * CST;
 
   if (PRO) {
     for (int i = t; i < K; i += kT) {
@@ -136,13 +149,13 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
     __syncthreads();
   }
 
-  // DMA issue for stage q into ring slot q % kNS
+  // DMA issue for stage q into ring slot q % kNSnt
   auto issue = [&](int q) {
     if (q >= T) return;
     const int tile = static_cast<int>(blockIdx.x) + (q / KT) * static_cast<int>(gridDim.x);
     const int k0 = (q % KT) * kBK;
     const int64_t m0 = static_cast<int64_t>(tile) * BM;
-    char* base = lds + (q % kNS) * STAGE;
+    char* base = lds + (q % kNSnt) * STAGE;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int p = (wave * NA + j) * 64 + lane;  // 16-B unit in the A image
@@ -164,35 +177,32 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ssum[FN][4], ssq[FN][4];
+  // statistics: each lane owns the 8 channels wn*WN + 8*(lane % LPR) … +7
+  float ssum[8], ssq[8];
 #pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
+  for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
 
 #pragma unroll
-  for (int q = 0; q < kNS - 1; ++q) issue(q);
+  for (int q = 0; q < kNSnt - 1; ++q) issue(q);
 
   const int ck = lane >> 4;  // logical 16-B chunk (k = 8ck … 8ck+7) this lane reads
-  constexpr int FS = FM * FN;  // epilogue stores per wave per tile
   for (int q = 0; q < T; ++q) {
     // vmcnt retires in issue order: the ops younger than stage q's DMA are the
-    // DMAs of q+1, q+2 and the epilogue stores of tile ends at q-3 … q-1
-    // (issued after q's DMA) — counting them keeps the ring full across tile
-    // boundaries instead of draining it at every epilogue.
-    if (q + kNS - 2 < T) {
+    // DMA of q+1 and the epilogue stores of a tile end at q-2 or q-1 (issued
+    // after q's DMA) — counting them keeps the ring full across tile ends.
+    if (q + kNSnt - 2 < T) {
       int ends = 0;
 #pragma unroll
-      for (int d = 1; d <= kNS - 1; ++d) ends += (q - d >= 0 && (q - d) % KT == KT - 1) ? 1 : 0;
-      if (ends == 0) wait_vm<(kNS - 2) * G>();
-      else if (ends == 1) wait_vm<(kNS - 2) * G + FS>();
-      else wait_vm<(kNS - 2) * G + 2 * FS>();
+      for (int d = 1; d <= kNSnt - 1; ++d) ends += (q - d >= 0 && (q - d) % KT == KT - 1) ? 1 : 0;
+      if (ends == 0) wait_vm<(kNSnt - 2) * G>();
+      else if (ends == 1) wait_vm<(kNSnt - 2) * G + FS>();
+      else wait_vm<(kNSnt - 2) * G + 2 * FS>();
     } else {
       wait_vm<0>();
     }
-    barrier();  // stage q visible to all waves; all reads of slot (q-1)%kNS done
-    issue(q + kNS - 1);
-    const char* sA = lds + (q % kNS) * STAGE;
+    barrier();  // stage q visible to all waves; all reads of slot (q-1)%kNSnt done
+    issue(q + kNSnt - 1);
+    const char* sA = lds + (q % kNSnt) * STAGE;
     const char* sB = sA + SA;
     const int kt = q % KT;
     bf16x8 xf[FM], wf[FN];
@@ -203,7 +213,7 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
     }
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
-      const int r = wn * (BN / 2) + i * 16 + (lane & 15);
+      const int r = wn * WN + i * 16 + (lane & 15);
       wf[i] = *reinterpret_cast<const bf16x8*>(sB + r * 64 + 16 * (ck ^ nt_swz(r)));
     }
     if (PRO) {
@@ -224,56 +234,71 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
 
     if (kt == KT - 1) {
-      // epilogue: acc[i][j][r] = C[m][n], m = … + (lane&15), n = … + 4(lane>>4) + r
-      const int64_t m0 = static_cast<int64_t>(static_cast<int>(blockIdx.x) + (q / KT) * static_cast<int>(gridDim.x)) * BM;
+      // epilogue, per wave and in two 32-row halves: acc[i][j][r] = C[m][n] with
+      // m = 16j + (lane&15), n = 16i + 4(lane>>4) + r (wave-local) → 8-B packed
+      // writes into this wave's LDS staging → 16-B row-contiguous reads →
+      // global stores covering whole 128-B lines (no cross-wave sync needed:
+      // a wave's LDS ops execute in order).
+      const int64_t mt = static_cast<int64_t>(static_cast<int>(blockIdx.x) + (q / KT) * static_cast<int>(gridDim.x)) *
+                         BM + wm * (BM / 2);
 #pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        const int64_t m = m0 + wm * (BM / 2) + j * 16 + (lane & 15);
-        const bool ok = m < M;
+      for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-          const int n = n0 + wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
-          const uint32_t p01 = pack2(acc[i][j][0], acc[i][j][1]);
-          const uint32_t p23 = pack2(acc[i][j][2], acc[i][j][3]);
-          if (ok) {
-            *reinterpret_cast<uint2*>(C + m * N + n) = make_uint2(p01, p23);
+        for (int jj = 0; jj < 2; ++jj) {
+          const int j = 2 * h + jj;
+          const int row = jj * 16 + (lane & 15);
+#pragma unroll
+          for (int i = 0; i < FN; ++i) {
+            const int col = i * 16 + (lane >> 4) * 4;
+            const int chunk = (col >> 3) ^ (row & 7 & (LPR - 1));
+            *reinterpret_cast<uint2*>(cst + row * (WN * 2) + chunk * 16 + (col & 7) * 2) =
+                make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+#pragma unroll
+        for (int it = 0; it < 32 / RPI; ++it) {
+          const int row = it * RPI + lane / LPR;
+          const int c = lane % LPR;
+          const uint4 v = *reinterpret_cast<const uint4*>(cst + row * (WN * 2) + 16 * (c ^ (row & 7 & (LPR - 1))));
+          const int64_t m = mt + 32 * h + row;
+          if (m < M) {
+            *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) = v;
             if (STATS) {
-              const float v[4] = {bf_lo(p01), bf_hi(p01), bf_lo(p23), bf_hi(p23)};
+              const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                ssum[i][r] += v[r];
-                ssq[i][r] = fmaf(v[r], v[r], ssq[i][r]);
+              for (int k = 0; k < 4; ++k) {
+                const float a = bf_lo(w4[k]), b = bf_hi(w4[k]);
+                ssum[2 * k] += a;
+                ssq[2 * k] = fmaf(a, a, ssq[2 * k]);
+                ssum[2 * k + 1] += b;
+                ssq[2 * k + 1] = fmaf(b, b, ssq[2 * k + 1]);
               }
             }
           }
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
     }
   }
   if (STATS) {
-    // reduce over the 16 rows (lane & 15) of each lane group, then over wm
+    // lanes with the same channel set: lane ^ LPR, ^2LPR, ... ; then over wm via LDS
 #pragma unroll
-    for (int i = 0; i < FN; ++i)
+    for (int e = 0; e < 8; ++e)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          ssum[i][r] += __shfl_xor(ssum[i][r], o);
-          ssq[i][r] += __shfl_xor(ssq[i][r], o);
-        }
+      for (int o = LPR; o < 64; o <<= 1) {
+        ssum[e] += __shfl_xor(ssum[e], o);
+        ssq[e] += __shfl_xor(ssq[e], o);
+      }
     wait_vm<0>();
     __syncthreads();  // ring idle: reuse it
     float* red = reinterpret_cast<float*>(lds);  // [sum|sq][wm][BN]
-    if ((lane & 15) == 0) {
+    if (lane < LPR) {
 #pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = wn * (BN / 2) + i * 16 + (lane >> 4) * 4 + r;
-          red[wm * BN + c] = ssum[i][r];
-          red[2 * BN + wm * BN + c] = ssq[i][r];
-        }
+      for (int e = 0; e < 8; ++e) {
+        const int c = wn * WN + lane * 8 + e;
+        red[wm * BN + c] = ssum[e];
+        red[2 * BN + wm * BN + c] = ssq[e];
+      }
     }
     __syncthreads();
     if (t < BN) {
@@ -499,8 +524,8 @@ WgradPlan wgrad_plan(int64_t M, int N1, int N2) {
   p.tiles = (N1 / p.bm) * (N2 / p.bn);
   const int64_t ksteps = (M + kBK - 1) / kBK;
   int64_t S = 512 / p.tiles;  // ~2 blocks per CU
-  // keep the slab traffic ≤ ~1/4 of the operand traffic
-  const int64_t cap = (M * (N1 + N2) * 2 / 4) / (static_cast<int64_t>(N1) * N2 * 4);
+  // keep the slab traffic (write + read) ≤ ~the operand traffic
+  const int64_t cap = (M * (N1 + N2) * 2 / 2) / (static_cast<int64_t>(N1) * N2 * 4);
   if (S > cap) S = cap;
   if (S > ksteps) S = ksteps;
   if (S < 1) S = 1;
@@ -528,7 +553,8 @@ void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
   const dim3 grid(gx, tn);
   const bool pro = scale != nullptr;
   const bool st = stats != nullptr;
-  const size_t lds = static_cast<size_t>(kNS) * (BM + BN) * 64 + (pro ? 8 * static_cast<size_t>(K) : 0);
+  // ring + per-wave C staging (4 × 32 rows × BN/2) + BN coefficients
+  const size_t lds = static_cast<size_t>(kNSnt) * (BM + BN) * 64 + 4 * 32 * BN + (pro ? 8 * static_cast<size_t>(K) : 0);
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);

@@ -13,6 +13,7 @@ one write per activation in the forward, statistics fused).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Type
 
 import torch
@@ -21,6 +22,9 @@ from torch import nn
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv import bn_relu_conv1x1, conv1x1 as gemm_conv1x1, gemm_ok
 from ..ops.pool import FusedMaxPool2d
+
+
+GEMM_MAX_INTENSITY = float(os.environ.get("DCP_GEMM_MAX_INTENSITY", "1024"))
 
 
 def conv3x3(cin, cout, stride=1):
@@ -65,8 +69,15 @@ class Bottleneck(nn.Module):
         return self.bn3(self.conv3(out), identity, dual=dual)
 
     def _gemm_path(self, x: torch.Tensor) -> bool:
-        return (self.fused_gemm and self.training and self.bn1.fused and self.bn2.fused and self.bn3.fused
-                and gemm_ok(x, self.conv1.in_channels, self.conv1.out_channels)
+        if not (self.fused_gemm and self.training and self.bn1.fused and self.bn2.fused and self.bn3.fused):
+            return False
+        # optional cut-off on the 1x1 convs' FLOP/byte (≈ Cin·Cout/(Cin+Cout); ResNet-50:
+        # 51 / 102 / 205 / 410 for layers 1-4). Default 1024: every stage — with the
+        # split-M wgrad all four stages measured faster than MIOpen (r1_bench_gemm_*)
+        w, c = self.conv3.in_channels, self.conv3.out_channels
+        if w * c / (w + c) > GEMM_MAX_INTENSITY:
+            return False
+        return (gemm_ok(x, self.conv1.in_channels, self.conv1.out_channels)
                 and self.conv3.out_channels % 64 == 0 and self.conv3.in_channels % 64 == 0)
 
     def _forward_gemm(self, x, identity, dual):
