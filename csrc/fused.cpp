@@ -267,6 +267,40 @@ at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::o
   return dw;
 }
 
+// ≥ 256 zeroed bytes per device: the padding row of the gathered wgrad
+const at::Tensor& zero_row(const at::Tensor& like) {
+  static std::mutex mu;
+  static std::map<int, at::Tensor> rows;
+  std::lock_guard<std::mutex> g(mu);
+  at::Tensor& z = rows[static_cast<int>(like.get_device())];
+  if (!z.defined()) z = at::zeros({1024}, like.options().dtype(at::kBFloat16));
+  return z;
+}
+
+// dW (fp32, [Cout, Cin, kh, kw] with channels_last strides) of a kh×kw NHWC
+// convolution: implicit-GEMM MFMA wgrad, one tap per grid.z (gemm.hip).
+at::Tensor conv_wgrad(const at::Tensor& gy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride, int64_t pad) {
+  check_gemm_act(gy, "conv_wgrad");
+  check_gemm_act(x, "conv_wgrad");
+  DCP_CHECK(gy.dim() == 4 && x.dim() == 4 && gy.size(0) == x.size(0), "conv_wgrad: NHWC 4-D tensors required");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = gy.size(1), Ho = gy.size(2), Wo = gy.size(3);
+  DCP_CHECK(Ho == (H + 2 * pad - kh) / stride + 1 && Wo == (W + 2 * pad - kw) / stride + 1,
+            "conv_wgrad: output size does not match the geometry");
+  DCP_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "conv_wgrad: channels must be multiples of 64");
+  DCP_CHECK(N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad: tensor too large");
+  at::Tensor dw = at::empty({Cout, kh, kw, Cin}, gy.options().dtype(at::kFloat));
+  const int taps = static_cast<int>(kh * kw);
+  at::Tensor ws = at::empty({kern::gemm_wgrad_workspace(N * Ho * Wo, static_cast<int>(Cout), static_cast<int>(Cin), taps)},
+                            gy.options().dtype(at::kFloat));
+  kern::conv_wgrad_bf16(gy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), static_cast<int>(N), static_cast<int>(H),
+                        static_cast<int>(W), static_cast<int>(Cin), static_cast<int>(Ho), static_cast<int>(Wo),
+                        static_cast<int>(Cout), static_cast<int>(kh), static_cast<int>(kw), static_cast<int>(stride),
+                        static_cast<int>(pad), zero_row(gy).data_ptr(), ws.data_ptr<float>(), stream_of(gy));
+  return dw.permute({0, 3, 1, 2});
+}
+
 // Returns (dx, dweight, dbias, dresidual).
 // gy2: optional second output gradient (dual-output BN: the output feeds two
 // consumers); summed inside the reduction kernel when has_res.
@@ -624,6 +658,9 @@ void bind(pybind11::module& m) {
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("scale") = pybind11::none(),
         pybind11::arg("shift") = pybind11::none(), pybind11::arg("relu") = false, pybind11::arg("stats") = false);
   m.def("conv1x1_dgrad", &conv1x1_dgrad, pybind11::arg("gy"), pybind11::arg("wt"));
+  m.def("conv_wgrad", &conv_wgrad, "kxk NHWC conv weight gradient (implicit-GEMM MFMA, fp32 out)",
+        pybind11::arg("gy"), pybind11::arg("x"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"),
+        pybind11::arg("pad"));
   m.def("weight_bf16_t", &weight_bf16_t, "fp32 weight -> (bf16 [R,C], bf16 transposed [C,R]) in one launch");
   m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("gy"), pybind11::arg("x"),
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),

@@ -346,11 +346,21 @@ __device__ __forceinline__ bf16x8 mask_rows(bf16x8 v, int valid, int lane) {
   return __builtin_bit_cast(bf16x8, s);
 }
 
-template <int BM, int BN, bool PRO>
+// Convolution geometry for the gathered (implicit-GEMM) wgrad: B rows are the
+// input pixels under tap (dy, dx) = (blockIdx.z / kw, blockIdx.z % kw) of
+// each output pixel; out-of-image taps read a zero row.
+struct ConvGeo {
+  int H, W, Ho, Wo, stride, pad, kw;
+  const uint16_t* zero;  // ≥ 256 zero bytes
+};
+
+template <int BM, int BN, bool PRO, bool GATHER>
 __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                         float* __restrict__ ws, int64_t M, int N1, int N2,
                                                         int64_t chunk, const float* __restrict__ scale,
-                                                        const float* __restrict__ shift, int relu, int tiles_j) {
+                                                        const float* __restrict__ shift, int relu, int tiles_j,
+                                                        ConvGeo geo) {
+  static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
   constexpr int SA = 32 * BM * 2, SB = 32 * BN * 2, STAGE = SA + SB;
   constexpr int NA = SA / 4096, NB = SB / 4096;  // glds per wave per stage
   constexpr int G = NA + NB;
@@ -400,9 +410,21 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
       const int p = (wave * NB + j) * 64 + lane;
       const int r = p / BCPR, pc = p % BCPR;
       const int lc = 2 * ((pc >> 1) ^ tr_f<BN>(r)) + (pc & 1);
-      int64_t gm = mb + r;
-      gm = gm < mz1 ? gm : mz1 - 1;
-      glds16(B + gm * N2 + j0 + lc * 8, base + SA + (wave * NB + j) * 1024);
+      if (GATHER) {
+        const int gm = static_cast<int>(mb) + r;  // output pixel
+        const int dy = static_cast<int>(blockIdx.z) / geo.kw, dx = static_cast<int>(blockIdx.z) % geo.kw;
+        const int wo = gm % geo.Wo, t1 = gm / geo.Wo;
+        const int ho = t1 % geo.Ho, n = t1 / geo.Ho;
+        const int hi = ho * geo.stride + dy - geo.pad, wi = wo * geo.stride + dx - geo.pad;
+        const bool ok = gm < mz1 && hi >= 0 && hi < geo.H && wi >= 0 && wi < geo.W;
+        const uint16_t* src = ok ? B + (static_cast<int64_t>(n * geo.H + hi) * geo.W + wi) * N2 + j0 + lc * 8
+                                 : geo.zero + lc * 8;
+        glds16(src, base + SA + (wave * NB + j) * 1024);
+      } else {
+        int64_t gm = mb + r;
+        gm = gm < mz1 ? gm : mz1 - 1;
+        glds16(B + gm * N2 + j0 + lc * 8, base + SA + (wave * NB + j) * 1024);
+      }
     }
   };
 
@@ -448,7 +470,9 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
       for (int j = 0; j < FN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   }
-  float* out = ws + static_cast<int64_t>(blockIdx.y) * N1 * N2;
+  // slab z holds D in its final [N1][taps][N2] layout (taps = gridDim.z)
+  const int ntaps = static_cast<int>(gridDim.z);
+  float* out = ws + static_cast<int64_t>(blockIdx.y) * N1 * ntaps * N2 + static_cast<int64_t>(blockIdx.z) * N2;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -457,7 +481,7 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
       for (int r = 0; r < 4; ++r) {
         const int row = i0 + wi * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
         const int col = j0 + wj * (BN / 2) + j * 16 + (lane & 15);
-        out[static_cast<int64_t>(row) * N2 + col] = acc[i][j][r];
+        out[static_cast<int64_t>(row) * ntaps * N2 + col] = acc[i][j][r];
       }
 }
 
@@ -517,15 +541,15 @@ struct WgradPlan {
   int64_t chunk;
 };
 
-WgradPlan wgrad_plan(int64_t M, int N1, int N2) {
+WgradPlan wgrad_plan(int64_t M, int N1, int N2, int taps = 1) {
   WgradPlan p;
   p.bm = N1 % 128 == 0 ? 128 : 64;
   p.bn = N2 % 128 == 0 ? 128 : 64;
   p.tiles = (N1 / p.bm) * (N2 / p.bn);
   const int64_t ksteps = (M + kBK - 1) / kBK;
-  int64_t S = 512 / p.tiles;  // ~2 blocks per CU
+  int64_t S = 512 / (p.tiles * taps);  // ~2 blocks per CU
   // keep the slab traffic (write + read) ≤ ~the operand traffic
-  const int64_t cap = (M * (N1 + N2) * 2 / 2) / (static_cast<int64_t>(N1) * N2 * 4);
+  const int64_t cap = (M * (N1 + static_cast<int64_t>(taps) * N2) * 2 / 2) / (static_cast<int64_t>(N1) * taps * N2 * 4);
   if (S > cap) S = cap;
   if (S > ksteps) S = ksteps;
   if (S < 1) S = 1;
@@ -581,29 +605,36 @@ void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_
                      static_cast<uint16_t*>(wt), R, Cc);
 }
 
-int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2) {
-  const WgradPlan p = wgrad_plan(M, N1, N2);
+int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
+  const WgradPlan p = wgrad_plan(M, N1, N2, taps);
   const int64_t groups = (p.S + kSlabGroup - 1) / kSlabGroup;
-  return (static_cast<int64_t>(p.S) + (groups > 1 ? groups : 0)) * N1 * N2;
+  return (static_cast<int64_t>(p.S) + (groups > 1 ? groups : 0)) * N1 * taps * N2;
 }
 
-void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
-                     const float* shift, bool relu, float* ws, hipStream_t s) {
-  const WgradPlan p = wgrad_plan(M, N1, N2);
-  const dim3 grid(p.tiles, p.S);
+namespace {
+void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s);
+
+template <bool GATHER>
+void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
+                  const float* shift, bool relu, float* ws, int taps, const ConvGeo& geo, hipStream_t s) {
+  const WgradPlan p = wgrad_plan(M, N1, N2, taps);
+  const dim3 grid(p.tiles, p.S, taps);
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   const bool pro = scale != nullptr;
   const int tj = N2 / p.bn;
-#define DCP_GWG(BM_, BN_, P)                                                                                     \
-  hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, p.chunk, scale, \
-                     shift, relu ? 1 : 0, tj)
-#define DCP_GWG2(BM_, BN_)        \
-  do {                            \
-    if (pro)                      \
-      DCP_GWG(BM_, BN_, true);    \
-    else                          \
-      DCP_GWG(BM_, BN_, false);   \
+#define DCP_GWG(BM_, BN_, P)                                                                                   \
+  hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,   \
+                     p.chunk, scale, shift, relu ? 1 : 0, tj, geo)
+#define DCP_GWG2(BM_, BN_)                      \
+  do {                                          \
+    if constexpr (!GATHER) {                    \
+      if (pro) {                                \
+        DCP_GWG(BM_, BN_, true);                \
+        break;                                  \
+      }                                         \
+    }                                           \
+    DCP_GWG(BM_, BN_, false);                   \
   } while (0)
   if (p.bm == 128 && p.bn == 128) DCP_GWG2(128, 128);
   else if (p.bm == 128) DCP_GWG2(128, 64);
@@ -611,14 +642,33 @@ void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, 
   else DCP_GWG2(64, 64);
 #undef DCP_GWG2
 #undef DCP_GWG
-  const int64_t n4 = static_cast<int64_t>(N1) * N2 / 4;
+  slab_reduce(ws, D, static_cast<int64_t>(N1) * taps * N2 / 4, p.S, s);
+}
+}  // namespace
+
+void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
+                     const float* shift, bool relu, float* ws, hipStream_t s) {
+  ConvGeo geo{};
+  wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s);
+}
+
+void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                     int kh, int kw, int stride, int pad, const void* zero, float* ws, hipStream_t s) {
+  ConvGeo geo{H, W, Ho, Wo, stride, pad, kw, static_cast<const uint16_t*>(zero)};
+  wgrad_launch<true>(dY, X, D, static_cast<int64_t>(N) * Ho * Wo, Cout, Cin, nullptr, nullptr, false, ws, kh * kw,
+                     geo, s);
+}
+
+namespace {
+void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s) {
+  const WgradPlan p{0, 0, 0, S, 0};
   const int gx = static_cast<int>((n4 + kT - 1) / kT);
   const int groups = (p.S + kSlabGroup - 1) / kSlabGroup;
   auto w4 = reinterpret_cast<const float4*>(ws);
   if (groups == 1) {
     hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, w4, reinterpret_cast<float4*>(D), n4, p.S);
   } else {
-    float4* part = reinterpret_cast<float4*>(ws + static_cast<int64_t>(p.S) * N1 * N2);
+    float4* part = reinterpret_cast<float4*>(ws + static_cast<int64_t>(p.S) * n4 * 4);
     hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, groups), dim3(kT), 0, s, w4, part, n4, p.S);
     // groups ≤ 32 (S ≤ 512): ≤ 2 more levels
     int S2 = groups;
@@ -634,6 +684,7 @@ void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, 
     hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, src, dst, n4, S2);
   }
 }
+}  // namespace
 
 }  // namespace kern
 }  // namespace dcp

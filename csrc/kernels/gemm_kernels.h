@@ -32,13 +32,21 @@ void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
 void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s);
 
 // Workspace (fp32 elements) gemm_wgrad_bf16 needs for this shape.
-int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2);
+int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps = 1);
 
 // D[N1,N2] (fp32) = Σ_m A[m, :N1] (bf16, lda=N1) ⊗ f(B)[m, :N2] (bf16, ldb=N2)
 // (f = optional per-column scale/shift/relu). Deterministic: split over M
 // into fp32 slabs in `ws`, then one reduction launch.
 void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
                      const float* shift, bool relu, float* ws, hipStream_t s);
+
+// Weight gradient of a kh×kw NHWC convolution (implicit GEMM, one tap per
+// grid.z): D[Cout][kh][kw][Cin] (fp32; = a channels_last OIHW tensor) =
+// Σ_{output pixels} dY[m, :]^T ⊗ X[pixel under tap, :] (zero outside the image).
+// dY [N*Ho*Wo, Cout] bf16, X [N*H*W, Cin] bf16; Cout, Cin multiples of 64;
+// zero: ≥ 256 zeroed bytes; ws: gemm_wgrad_workspace(N*Ho*Wo, Cout, Cin, kh*kw).
+void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                     int kh, int kw, int stride, int pad, const void* zero, float* ws, hipStream_t s);
 
 }  // namespace kern
 }  // namespace dcp

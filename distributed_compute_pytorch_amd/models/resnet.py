@@ -20,11 +20,14 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import bn_relu_conv1x1, conv1x1 as gemm_conv1x1, gemm_ok
+from ..ops.conv import bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk, conv_kxk_ok, gemm_ok
 from ..ops.pool import FusedMaxPool2d
 
 
 GEMM_MAX_INTENSITY = float(os.environ.get("DCP_GEMM_MAX_INTENSITY", "1024"))
+KXK_WGRAD = os.environ.get("DCP_KXK_WGRAD", "0") == "1"
+# BN-apply prologue in the conv3 GEMM only while Cout ≤ this (≤ 2 N-tiles of 128)
+PRO_MAX_COUT = int(os.environ.get("DCP_PRO_MAX_COUT", "256"))
 
 
 def conv3x3(cin, cout, stride=1):
@@ -97,10 +100,23 @@ class Bottleneck(nn.Module):
         else:
             identity = inp
         z1, s1 = gemm_conv1x1(x, self.conv1.weight, stats=True)
-        x2 = self.conv2(self.bn1(z1, stats=s1))
+        y1 = self.bn1(z1, stats=s1)
+        c2 = self.conv2
+        # opt-in: MIOpen fwd/dgrad + our implicit-GEMM wgrad (ties MIOpen's wrw except at
+        # 56x56x64, where it is slower: profiles/r1_gemm1x1_vs_miopen.json "rows3x3")
+        if KXK_WGRAD and conv_kxk_ok(y1, c2):
+            x2 = conv_kxk(y1, c2.weight, c2.stride[0], c2.padding[0])
+        else:
+            x2 = c2(y1)
         if not x2.is_contiguous(memory_format=torch.channels_last):
             x2 = x2.contiguous(memory_format=torch.channels_last)
-        z3, s3 = bn_relu_conv1x1(x2, self.bn2, self.conv3.weight, stats=True)
+        if self.conv3.out_channels <= PRO_MAX_COUT:
+            # BN2+ReLU applied in the GEMM prologue (its output never hits HBM)
+            z3, s3 = bn_relu_conv1x1(x2, self.bn2, self.conv3.weight, stats=True)
+        else:
+            # wide conv3: every N-tile re-applies the prologue to the same rows,
+            # which costs more than one apply pass over the narrow input
+            z3, s3 = gemm_conv1x1(self.bn2(x2), self.conv3.weight, stats=True)
         return self.bn3(z3, identity, dual=dual, stats=s3)
 
 

@@ -21,6 +21,7 @@ from __future__ import annotations
 from typing import Optional, Tuple
 
 import torch
+import torch.nn.functional as F
 
 from .._ext import C as _C
 
@@ -112,3 +113,46 @@ def bn_relu_conv1x1(x: torch.Tensor, bn, weight: torch.Tensor, stats: bool = Fal
         nbt = None
     return _BNReluConv1x1Fn.apply(x, bn.weight, bn.bias, weight, bn.running_mean, bn.running_var, nbt, bn.momentum,
                                   bn.eps, stats)
+
+
+class _ConvKxKFn(torch.autograd.Function):
+    """kxk NHWC convolution: MIOpen forward and data gradient, our implicit-GEMM
+    MFMA weight gradient (fp32 out; no zero-fill pass, no bf16→fp32 cast)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding):
+        w = weight.detach().to(torch.bfloat16)
+        y = F.conv2d(x, w, None, stride, padding)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.padding, ctx.wdtype = stride, padding, weight.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = _cl(gy)
+        s, p = ctx.stride, ctx.padding
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = _C.conv_wgrad(gy, x, w.shape[2], w.shape[3], s, p)
+            if dw.dtype != ctx.wdtype:
+                dw = dw.to(ctx.wdtype)
+        return dx, dw, None, None
+
+
+def conv_kxk(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> torch.Tensor:
+    """NHWC bf16 kxk convolution (no bias, square stride/padding) whose weight
+    gradient runs on the gathered MFMA wgrad kernel."""
+    return _ConvKxKFn.apply(x, weight, stride, padding)
+
+
+def conv_kxk_ok(x: torch.Tensor, conv) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and conv.bias is None
+            and conv.groups == 1 and conv.dilation == (1, 1)
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
+            and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1])

@@ -158,3 +158,45 @@ def test_resnet_stage_gemm_path_matches(cuda):
         assert ea < 1.5 * eb + 0.03, (n, ea, eb)
     for (n, x1), x2 in zip(a.named_buffers(), r.buffers()):
         torch.testing.assert_close(x1.float(), x2.float(), rtol=3e-2, atol=3e-2, msg=n)
+
+
+@pytest.mark.parametrize("shape", [  # (N, H, W, Cin, Cout, k, stride, pad)
+    (2, 8, 8, 64, 64, 3, 1, 1), (3, 7, 9, 128, 64, 3, 1, 1), (4, 14, 14, 64, 128, 3, 2, 1),
+    (2, 15, 15, 128, 128, 3, 2, 1), (2, 6, 6, 64, 192, 1, 1, 0), (8, 28, 28, 128, 128, 3, 1, 1)])
+def test_conv_wgrad_gathered(cuda, shape):
+    """Implicit-GEMM kxk weight gradient vs the fp32 ATen convolution backward."""
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    n, h, w, ci, co, k, s, p = shape
+    g = torch.Generator().manual_seed(5)
+    x = _x(n, h, w, ci, cuda, g)
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    gy = _x(n, ho, wo, co, cuda, g)
+    dw = _C.conv_wgrad(gy, x, k, k, s, p)
+    wt = torch.zeros(co, ci, k, k, device=cuda)
+    ref = torch.ops.aten.convolution_backward(gy.float(), x.float(), wt, None, [s, s], [p, p], [1, 1], False, [0, 0],
+                                              1, [False, True, False])[1]
+    assert dw.shape == ref.shape and dw.dtype == torch.float32
+    assert dw.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(dw, ref) < 1e-3
+
+
+def test_conv_kxk_autograd(cuda):
+    from torch import nn
+
+    from distributed_compute_pytorch_amd.ops.conv import conv_kxk
+
+    g = torch.Generator().manual_seed(6)
+    conv = nn.Conv2d(64, 128, 3, 2, 1, bias=False).to(cuda).to(memory_format=torch.channels_last)
+    x = _x(4, 14, 14, 64, cuda, g).requires_grad_(True)
+    y = conv_kxk(x, conv.weight, 2, 1)
+    gy = _x(4, 7, 7, 128, cuda, g)
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, conv.weight.detach().to(torch.bfloat16).float(), None, 2, 1)
+    yr.backward(gy.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    F.conv2d(x.detach().float(), wr, None, 2, 1).backward(gy.float())
+    assert conv.weight.grad.dtype == torch.float32 and _rel(conv.weight.grad, wr.grad) < 1e-3

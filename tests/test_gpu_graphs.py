@@ -9,7 +9,8 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
-def test_captured_step_matches_eager(cuda):
+@pytest.mark.parametrize("gemm", [False, True])
+def test_captured_step_matches_eager(cuda, gemm):
     import distributed_compute_pytorch_amd as dcp
     from distributed_compute_pytorch_amd.distributed.launch import free_port
     from distributed_compute_pytorch_amd.models import resnet18_like
@@ -19,7 +20,8 @@ def test_captured_step_matches_eager(cuda):
     dcp.distributed.init_process_group("rccl", device_id=0)
     try:
         torch.manual_seed(0)
-        base = resnet18_like(num_classes=10, fused_bn=True).to(cuda).to(memory_format=torch.channels_last)
+        base = resnet18_like(num_classes=10, fused_bn=True, fused_gemm=gemm).to(cuda).to(
+            memory_format=torch.channels_last)
         m_eager, m_graph = copy.deepcopy(base), copy.deepcopy(base)
         d_e = dcp.parallel.DistributedDataParallel(m_eager, device_ids=[0], gradient_as_bucket_view=True)
         s = capture_stream()
@@ -49,26 +51,45 @@ def test_captured_step_matches_eager(cuda):
             run_e(*batches[0])
         cap = CapturedStep(run_g, [t.clone() for t in batches[0]], warmup=3, stream=s)  # capture does not execute
 
-        def sync_state():
-            # start every compared step from identical state (in place: the
-            # graph keeps its addresses); chaotic drift of two independent
-            # runs (MIOpen / atomic-order noise) is not what this test checks
+        def snapshot():
+            return ({k: v.detach().clone() for k, v in m_eager.state_dict().items()},
+                    [o_e.state[p]["momentum_buffer"].clone() for p in m_eager.parameters()])
+
+        def restore(model, opt, snap):
+            # in place: the graph keeps its addresses
             with torch.no_grad():
-                for a, b in zip(m_eager.state_dict().values(), m_graph.state_dict().values()):
-                    b.copy_(a)
-                for pe, pg in zip(m_eager.parameters(), m_graph.parameters()):
-                    o_g.state[pg]["momentum_buffer"].copy_(o_e.state[pe]["momentum_buffer"])
+                for (k, v), t in zip(snap[0].items(), model.state_dict().values()):
+                    t.copy_(v)
+                for p, buf in zip(model.parameters(), snap[1]):
+                    opt.state[p]["momentum_buffer"].copy_(buf)
+
+        def flat(ps):
+            return torch.cat([p.detach().float().reshape(-1) for p in ps])
 
         for b in batches[1:5]:
-            sync_state()
-            torch.cuda.synchronize()
+            snap = snapshot()
+            p0 = flat(m_eager.parameters())
             le = run_e(*b).item()
+            de1 = flat(m_eager.parameters()) - p0
+            restore(m_eager, o_e, snap)
+            run_e(*b)
+            de2 = flat(m_eager.parameters()) - p0
+            restore(m_graph, o_g, snap)
+            torch.cuda.synchronize()
             lg = cap(*b).item()
             torch.cuda.synchronize()
             assert abs(le - lg) < 1e-2 * max(1.0, abs(le)), (le, lg)
-            for p, q in zip(m_eager.parameters(), m_graph.parameters()):
-                rel = float((p - q).norm() / p.norm().clamp_min(1e-12))
-                assert rel < 1e-3, rel
+            dg = flat(m_graph.parameters()) - p0
+            # two EAGER runs of this tiny random-init bf16 net already differ
+            # (MIOpen / atomic-order noise, tools/graph_numerics.py): the replay
+            # must sit within that spread; a stale captured input gives O(1)
+            noise = float((de1 - de2).norm())
+            err = float((dg - de1).norm())
+            assert err < 3 * noise + 0.02 * float(de1.norm()), (err, noise, float(de1.norm()))
+            restore(m_eager, o_e, snap)
+            run_e(*b)  # advance both runs from the same state
+            restore(m_graph, o_g, (dict(m_eager.state_dict()),
+                                   [o_e.state[p]["momentum_buffer"] for p in m_eager.parameters()]))
     finally:
         dcp.distributed.destroy_process_group()
 

@@ -84,6 +84,25 @@ def main():
             res[f"miopen_{k}_TBps"] = round(b_fwd / (us * 1e-6) / 1e12, 2)
         rows.append(res)
         print(json.dumps(res), flush=True)
+    # 3x3 weight gradients (ResNet-50 conv2 layers): gathered implicit GEMM vs MIOpen
+    for hw, c, st in [(56, 64, 1), (56, 128, 2), (28, 128, 1), (28, 256, 2), (14, 256, 1), (14, 512, 2), (7, 512, 1)]:
+        ho = (hw + 2 - 3) // st + 1
+        x = torch.randn(a.batch, c, hw, hw, device=dev).to(bf).contiguous(memory_format=cl)
+        gy = torch.randn(a.batch, c, ho, ho, device=dev).to(bf).contiguous(memory_format=cl)
+        w4 = torch.randn(c, c, 3, 3, device=dev).to(bf).contiguous(memory_format=cl)
+        us_o = timeit(lambda: _C.conv_wgrad(gy, x, 3, 3, st, 1), a.iters)
+        us_m = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w4, None, (st, st), (1, 1), (1, 1), False,
+                                                                  (0, 0), 1, (False, True, False)), a.iters)
+        us_d = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w4, None, (st, st), (1, 1), (1, 1), False,
+                                                                  (0, 0), 1, (True, False, False)), a.iters)
+        us_f = timeit(lambda: F.conv2d(x, w4, None, st, 1), a.iters)
+        flops = 2.0 * a.batch * ho * ho * c * c * 9
+        r3 = {"shape3x3": f"{hw}x{hw} c={c} s={st}", "ours_wgrad_us": round(us_o, 1), "miopen_wgrad_us": round(us_m, 1),
+              "miopen_dgrad_us": round(us_d, 1), "miopen_fwd_us": round(us_f, 1),
+              "ours_wgrad_TFps": round(flops / (us_o * 1e-6) / 1e12, 1)}
+        print(json.dumps(r3), flush=True)
+        rows3 = locals().setdefault("rows3", [])
+        rows3.append(r3)
     tot = {k: round(sum(r[k] for r in rows), 1) for k in rows[0] if k.endswith("_us")}
     print(json.dumps({"total_us": tot}), flush=True)
     if a.json:
