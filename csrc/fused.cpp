@@ -9,6 +9,7 @@
 #include "common.h"
 #include "kernels/bn_kernels.h"
 #include "kernels/gemm_kernels.h"
+#include "kernels/attn_kernels.h"
 #include "kernels/ln_kernels.h"
 #include "kernels/dropout_kernels.h"
 #include "kernels/pool_kernels.h"
@@ -299,6 +300,88 @@ at::Tensor conv_wgrad(const at::Tensor& gy, const at::Tensor& x, int64_t kh, int
                         static_cast<int>(Cout), static_cast<int>(kh), static_cast<int>(kw), static_cast<int>(stride),
                         static_cast<int>(pad), zero_row(gy).data_ptr(), ws.data_ptr<float>(), stream_of(gy));
   return dw.permute({0, 3, 1, 2});
+}
+
+// fp32 [N] column sums of a bf16 [.., N] tensor (Linear bias gradient)
+at::Tensor colsum(const at::Tensor& x) {
+  DCP_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() >= 1,
+            "colsum: contiguous bf16 device tensor required");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t N = x.size(-1);
+  const int64_t M = x.numel() / N;
+  DCP_CHECK(N % 8 == 0, "colsum: last dim must be a multiple of 8");
+  at::Tensor out = at::empty({N}, x.options().dtype(at::kFloat));
+  at::Tensor ws = at::empty({kern::colsum_workspace(static_cast<int>(N))}, x.options().dtype(at::kFloat));
+  kern::colsum_bf16(x.data_ptr(), out.data_ptr<float>(), M, static_cast<int>(N), ws.data_ptr<float>(), stream_of(x));
+  return out;
+}
+
+// ---------------------------------------------------- flash attention ---
+namespace {
+kern::AttnTensor attn_view(const at::Tensor& t, const char* what) {
+  DCP_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 3 && t.stride(2) == 1, what,
+            ": bf16 [B, T, H*64] tensor with unit last stride required");
+  DCP_CHECK(t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+            what, ": rows must be 16-byte aligned");
+  return kern::AttnTensor{t.data_ptr(), t.stride(0), t.stride(1)};
+}
+kern::AttnOut attn_out(const at::Tensor& t, const char* what) {
+  const kern::AttnTensor v = attn_view(t, what);
+  return kern::AttnOut{t.data_ptr(), v.sb, v.st};
+}
+kern::AttnParams attn_params(const at::Tensor& q, int64_t heads, bool causal, double p_drop, int64_t seed) {
+  const int64_t B = q.size(0), T = q.size(1), C = q.size(2);
+  DCP_CHECK(heads > 0 && C == heads * 64, "attention: head dim must be 64");
+  DCP_CHECK(kern::attn_supported(static_cast<int>(T), 64), "attention: sequence length must be a multiple of 64");
+  DCP_CHECK(p_drop >= 0.0 && p_drop < 1.0, "attention: dropout p must be in [0, 1)");
+  DCP_CHECK(B * heads * T * (T / 2) < (int64_t(1) << 32), "attention: problem too large for the dropout counter");
+  kern::AttnParams p;
+  p.B = static_cast<int>(B);
+  p.H = static_cast<int>(heads);
+  p.T = static_cast<int>(T);
+  p.scale = 0.125f;  // 1/sqrt(64)
+  p.causal = causal;
+  p.p_drop = static_cast<float>(p_drop);
+  p.seed = static_cast<uint64_t>(seed);
+  return p;
+}
+void same_shape(const at::Tensor& a, const at::Tensor& b, const char* what) {
+  DCP_CHECK(a.sizes() == b.sizes(), what, ": shape mismatch");
+}
+}  // namespace
+
+bool attn_ok(int64_t T, int64_t C, int64_t heads) {
+  return heads > 0 && C == heads * 64 && kern::attn_supported(static_cast<int>(T), 64);
+}
+
+// o [B, T, H*64] (contiguous), lse [B*H, T] fp32 (log2 domain)
+std::vector<at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t heads,
+                                       bool causal, double p_drop, int64_t seed) {
+  same_shape(q, k, "flash_attn_fwd");
+  same_shape(q, v, "flash_attn_fwd");
+  c10::hip::HIPGuard guard(q.device().index());
+  const kern::AttnParams p = attn_params(q, heads, causal, p_drop, seed);
+  at::Tensor o = at::empty(q.sizes(), q.options().memory_format(at::MemoryFormat::Contiguous));
+  at::Tensor lse = at::empty({q.size(0) * heads, q.size(1)}, q.options().dtype(at::kFloat));
+  kern::attn_fwd(p, attn_view(q, "q"), attn_view(k, "k"), attn_view(v, "v"), attn_out(o, "o"), lse.data_ptr<float>(),
+                 stream_of(q));
+  return {o, lse};
+}
+
+// writes dq, dk, dv (strided views allowed, e.g. slices of one packed buffer)
+void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                    const at::Tensor& o, const at::Tensor& lse, int64_t heads, bool causal, double p_drop,
+                    int64_t seed, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&k, &v, &o, &dout, &dq, &dk, &dv})
+    same_shape(q, *t, "flash_attn_bwd");
+  c10::hip::HIPGuard guard(q.device().index());
+  const kern::AttnParams p = attn_params(q, heads, causal, p_drop, seed);
+  DCP_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == q.size(0) * heads * q.size(1),
+            "flash_attn_bwd: lse");
+  at::Tensor delta = at::empty_like(lse);
+  kern::attn_bwd(p, attn_view(q, "q"), attn_view(k, "k"), attn_view(v, "v"), attn_view(o, "o"),
+                 attn_view(dout, "dout"), lse.data_ptr<float>(), delta.data_ptr<float>(), attn_out(dq, "dq"),
+                 attn_out(dk, "dk"), attn_out(dv, "dv"), stream_of(q));
 }
 
 // Returns (dx, dweight, dbias, dresidual).
@@ -658,6 +741,12 @@ void bind(pybind11::module& m) {
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("scale") = pybind11::none(),
         pybind11::arg("shift") = pybind11::none(), pybind11::arg("relu") = false, pybind11::arg("stats") = false);
   m.def("conv1x1_dgrad", &conv1x1_dgrad, pybind11::arg("gy"), pybind11::arg("wt"));
+  m.def("attn_ok", &attn_ok);
+  m.def("colsum", &colsum, "fp32 column sums of a bf16 [.., N] tensor (bias gradient)");
+  m.def("flash_attn_fwd", &flash_attn_fwd, "MFMA flash attention forward (head dim 64)", pybind11::arg("q"),
+        pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("heads"), pybind11::arg("causal"),
+        pybind11::arg("p_drop"), pybind11::arg("seed"));
+  m.def("flash_attn_bwd", &flash_attn_bwd, "MFMA flash attention backward into dq/dk/dv");
   m.def("conv_wgrad", &conv_wgrad, "kxk NHWC conv weight gradient (implicit-GEMM MFMA, fp32 out)",
         pybind11::arg("gy"), pybind11::arg("x"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"),
         pybind11::arg("pad"));

@@ -1,0 +1,546 @@
+// Flash attention (head dim 64) for gfx950: forward, dK/dV and dQ kernels on
+// v_mfma_f32_32x32x16_bf16, bf16 I/O, fp32 online softmax, optional causal
+// mask and dropout on P regenerated from a counter hash in the backward.
+//
+// Layout choices (CDNA4, wave64):
+//  * "swapped" products: the forward computes Sᵀ = K·Qᵀ so each lane owns one
+//    query (its 32 key scores sit in the lane's accumulator registers, the
+//    other 32 in lane^32): row max / row sum are in-lane plus ONE shfl_xor(32).
+//  * the Sᵀ accumulator is directly the B operand of Oᵀ += Vᵀ·P (accumulator-
+//    as-operand, CDNA4 guide §3): no LDS round trip for P; the matching Vᵀ
+//    operand is read with ds_read_b64_tr_b16 (hardware transpose) from the
+//    row-major V tile.
+//  * every LDS tile is [64 rows][64 bf16] (128-B rows) with one XOR swizzle
+//    that is conflict-free for both the 16-B row reads (16 consecutive rows)
+//    and the transposed reads (4 rows × 32 B per 16-lane group).
+//  * K/V (or Q/dO) tiles arrive by global_load_lds (async DMA) into a 2-deep
+//    ring, one barrier per tile.
+//  * backward = two kernels (FA2 split, no float atomics): dK/dV with the key
+//    on the lane (S and dP accumulators feed dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS
+//    directly), and dQ with the query on the lane (dQᵀ += Kᵀ·dSᵀ).
+//
+// Replaces PyTorch-ROCm's scaled_dot_product_attention (aotriton Triton
+// kernels) on the BERT-base / GPT-2-small paths ("flash-style
+// fused attention HIP kernel").
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "attn_kernels.h"
+
+namespace dcp {
+namespace kern {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kT = 256;
+constexpr int kD = 64;
+constexpr int kKB = 64;               // rows per LDS tile
+constexpr int kTile = kKB * kD * 2;   // 8 KiB
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  const bf16x2 v = {static_cast<__bf16>(a), static_cast<__bf16>(b)};
+  return __builtin_bit_cast(uint32_t, v);
+}
+// registers 8s … 8s+7 of an accumulator → bf16 operand fragment of k-step s
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
+  const uint4 u = make_uint4(pack2(a[8 * s + 0], a[8 * s + 1]), pack2(a[8 * s + 2], a[8 * s + 3]),
+                             pack2(a[8 * s + 4], a[8 * s + 5]), pack2(a[8 * s + 6], a[8 * s + 7]));
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+// ---- LDS tile image [64][64] bf16: 16-B chunk c of row r at r*128 + 16*(c ^ swz(r)).
+// Row reads (16 consecutive rows, one chunk) and transposed reads (rows R..R+3
+// and R+4.., chunks 0-3 or 4-7 per 32-lane half) both hit distinct bank slots.
+__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int img(int r, int c) { return r * 128 + 16 * (c ^ swz(r)); }
+
+__device__ __forceinline__ bf16x8 row_rd(const char* base, int r, int c) {
+  return *reinterpret_cast<const bf16x8*>(base + img(r, c));
+}
+
+// Operand A[x][row] = tile[row][x] for "A · X" with X an accumulator tile used
+// as the B operand: element j of lane l ↔ tile row rbase + 8(j>>2) + 4(l>>5) +
+// (j&3), column dcol0 + (l&31) — two ds_read_b64_tr_b16.
+__device__ __forceinline__ bf16x8 tr_op(const char* base, int rbase, int dcol0, int lane) {
+  const int g = lane >> 4, hh = lane >> 5, q = (lane >> 2) & 3, p = lane & 3;
+  const int c0 = dcol0 + 16 * (g & 1);
+  const int r0 = rbase + 4 * hh + q;
+  const int ch = (c0 >> 3) + (p >> 1);
+  const char* a0 = base + img(r0, ch) + 8 * (p & 1);
+  const char* a1 = base + img(r0 + 8, ch) + 8 * (p & 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 4, 0, 0);
+}
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// DMA rows [r0, r0+64) of a strided [T][64] head slice into a tile image;
+// 4 waves × 2 wave-instructions of 1 KiB (8 rows each).
+__device__ __forceinline__ void stage_tile(const uint16_t* src, int64_t st, int r0, char* dst, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int u = (wave * 2 + j) * 64 + lane;  // 16-B unit of the image
+    const int r = u >> 3, lc = (u & 7) ^ swz(u >> 3);
+    glds16(src + static_cast<int64_t>(r0 + r) * st + lc * 8, dst + (wave * 2 + j) * 1024);
+  }
+}
+
+// ---- dropout: 16 random bits per element (q, key) from a counter hash,
+// one 32-bit hash per (q, key pair). Identical in forward and backward.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t bh, uint32_t T, uint32_t q,
+                                              uint32_t key) {
+  const uint32_t ctr = (bh * T + q) * (T >> 1) + (key >> 1);
+  return mix32((ctr ^ s0) * 0x9E3779B1u + s1);
+}
+__device__ __forceinline__ bool drop_keep(uint32_t hsh, uint32_t key, uint32_t thr) {
+  const uint32_t r16 = (key & 1) ? (hsh >> 16) : (hsh & 0xffffu);
+  return r16 >= thr;
+}
+
+struct Ptrs {
+  const uint16_t* p;
+  int64_t st;
+};
+__device__ __forceinline__ Ptrs head(const AttnTensor& t, int b, int hd) {
+  return Ptrs{static_cast<const uint16_t*>(t.ptr) + b * t.sb + hd * kD, t.st};
+}
+
+// ------------------------------------------------------------ forward ----
+template <bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q, AttnTensor k, AttnTensor v,
+                                                      AttnOut o, float* __restrict__ lse) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kTile];  // [ring][K | V]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hh = lane >> 5;
+  const int bh = blockIdx.y, b = bh / P.H, hd = bh % P.H;
+  const int T = P.T;
+  const int qi = blockIdx.x * 128 + wave * 32 + (lane & 31);  // this lane's query
+  const bool qok = qi < T;
+  const Ptrs Q = head(q, b, hd), K = head(k, b, hd), V = head(v, b, hd);
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const uint4 u = qok ? *reinterpret_cast<const uint4*>(Q.p + static_cast<int64_t>(qi) * Q.st + 16 * ks + 8 * hh) : z;
+    qf[ks] = __builtin_bit_cast(bf16x8, u);
+  }
+  const float c = P.scale * kLog2e;
+  const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
+  const float inv_keep = 1.f / (1.f - P.p_drop);
+  const uint32_t s0 = static_cast<uint32_t>(P.seed), s1 = static_cast<uint32_t>(P.seed >> 32);
+
+  float m = -INFINITY, l = 0.f;
+  f32x16 oacc[2] = {zero16(), zero16()};
+  int nkb = T / kKB;
+  if (CAUSAL) nkb = min(nkb, (static_cast<int>(blockIdx.x) * 128 + 128 + kKB - 1) / kKB);
+
+  auto issue = [&](int it) {
+    if (it >= nkb) return;
+    char* base = lds + (it & 1) * 2 * kTile;
+    stage_tile(K.p, K.st, it * kKB, base, wave, lane);
+    stage_tile(V.p, V.st, it * kKB, base + kTile, wave, lane);
+  };
+  issue(0);
+  for (int it = 0; it < nkb; ++it) {
+    wait_vm0();
+    barrier();
+    issue(it + 1);
+    const char* sK = lds + (it & 1) * 2 * kTile;
+    const char* sV = sK + kTile;
+    const int kb = it * kKB;
+    f32x16 s[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      s[kh] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s[kh] = mfma(row_rd(sK, 32 * kh + (lane & 31), 2 * ks + hh), qf[ks], s[kh]);
+    }
+    // s[kh][r]: key kb + 32kh + (r&3) + 8(r>>2) + 4hh, query qi
+    float mx = m;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float x = s[kh][r] * c;
+        if (CAUSAL) {
+          const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          x = key > qi ? -INFINITY : x;
+        }
+        s[kh][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float alpha = exp2f(m - mx);
+    float rs = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pp = exp2f(s[kh][r] - mx);
+        s[kh][r] = pp;
+        rs += pp;
+      }
+    rs += __shfl_xor(rs, 32);
+    l = l * alpha + rs;
+    m = mx;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[dh][r] *= alpha;
+    if (DROP) {
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            const uint32_t key = kb + 32 * kh + 8 * g + 4 * hh + 2 * pr;
+            const uint32_t hs = drop_hash(s0, s1, bh, T, qi, key);
+            const int r = 4 * g + 2 * pr;
+            s[kh][r] = drop_keep(hs, key, thr) ? s[kh][r] * inv_keep : 0.f;
+            s[kh][r + 1] = drop_keep(hs, key + 1, thr) ? s[kh][r + 1] * inv_keep : 0.f;
+          }
+    }
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int sg = 0; sg < 2; ++sg) {
+        const bf16x8 pf = acc_frag(s[kh], sg);
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) oacc[dh] = mfma(tr_op(sV, 32 * kh + 16 * sg, 32 * dh, lane), pf, oacc[dh]);
+      }
+  }
+  if (qok) {
+    const float inv = 1.f / l;
+    uint16_t* O = static_cast<uint16_t*>(o.ptr) + b * o.sb + hd * kD + static_cast<int64_t>(qi) * o.st;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = 32 * dh + 8 * g + 4 * hh;
+        *reinterpret_cast<uint2*>(O + d0) = make_uint2(pack2(oacc[dh][4 * g] * inv, oacc[dh][4 * g + 1] * inv),
+                                                       pack2(oacc[dh][4 * g + 2] * inv, oacc[dh][4 * g + 3] * inv));
+      }
+    if (hh == 0) lse[static_cast<int64_t>(bh) * T + qi] = m + log2f(l);
+  }
+}
+
+// ------------------------------------------------------ bwd: delta -------
+// delta[bh][t] = Σ_d dO·O (fp32)
+__global__ void __launch_bounds__(kT) attn_delta_kernel(AttnParams P, AttnTensor o, AttnTensor dout,
+                                                        float* __restrict__ delta) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;  // over B*H*T
+  const int64_t n = static_cast<int64_t>(P.B) * P.H * P.T;
+  if (row >= n) return;
+  const int t = static_cast<int>(row % P.T);
+  const int bh = static_cast<int>(row / P.T), b = bh / P.H, hd = bh % P.H;
+  const uint16_t* O = static_cast<const uint16_t*>(o.ptr) + b * o.sb + static_cast<int64_t>(t) * o.st + hd * kD;
+  const uint16_t* G = static_cast<const uint16_t*>(dout.ptr) + b * dout.sb + static_cast<int64_t>(t) * dout.st + hd * kD;
+  float acc = 0.f;
+#pragma unroll
+  for (int c8 = 0; c8 < 8; ++c8) {
+    const uint4 a = reinterpret_cast<const uint4*>(O)[c8];
+    const uint4 g = reinterpret_cast<const uint4*>(G)[c8];
+    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, gw[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc = fmaf(__uint_as_float(aw[e] << 16), __uint_as_float(gw[e] << 16), acc);
+      acc = fmaf(__uint_as_float(aw[e] & 0xffff0000u), __uint_as_float(gw[e] & 0xffff0000u), acc);
+    }
+  }
+  delta[row] = acc;
+}
+
+// --------------------------------------------------------- bwd: dQ -------
+// query on the lane (as the forward): Sᵀ = K·Qᵀ, dPᵀ = V·dOᵀ,
+// dSᵀ = Pᵀ∘(dPᵀ∘keep/(1-p) − δ), dQᵀ += Kᵀ·dSᵀ.
+template <bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTensor q, AttnTensor k, AttnTensor v,
+                                                         AttnTensor dout, const float* __restrict__ lse,
+                                                         const float* __restrict__ delta, AttnOut dq) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kTile];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hh = lane >> 5;
+  const int bh = blockIdx.y, b = bh / P.H, hd = bh % P.H;
+  const int T = P.T;
+  const int qi = blockIdx.x * 128 + wave * 32 + (lane & 31);
+  const bool qok = qi < T;
+  const Ptrs Q = head(q, b, hd), K = head(k, b, hd), V = head(v, b, hd), G = head(dout, b, hd);
+  bf16x8 qf[4], gf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const int64_t off = 16 * ks + 8 * hh;
+    qf[ks] = __builtin_bit_cast(bf16x8, qok ? *reinterpret_cast<const uint4*>(Q.p + qi * Q.st + off) : z);
+    gf[ks] = __builtin_bit_cast(bf16x8, qok ? *reinterpret_cast<const uint4*>(G.p + qi * G.st + off) : z);
+  }
+  const float lse2 = qok ? lse[static_cast<int64_t>(bh) * T + qi] : 0.f;
+  const float dlt = qok ? delta[static_cast<int64_t>(bh) * T + qi] : 0.f;
+  const float c = P.scale * kLog2e;
+  const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
+  const float inv_keep = 1.f / (1.f - P.p_drop);
+  const uint32_t s0 = static_cast<uint32_t>(P.seed), s1 = static_cast<uint32_t>(P.seed >> 32);
+
+  f32x16 dacc[2] = {zero16(), zero16()};
+  int nkb = T / kKB;
+  if (CAUSAL) nkb = min(nkb, (static_cast<int>(blockIdx.x) * 128 + 128 + kKB - 1) / kKB);
+  auto issue = [&](int it) {
+    if (it >= nkb) return;
+    char* base = lds + (it & 1) * 2 * kTile;
+    stage_tile(K.p, K.st, it * kKB, base, wave, lane);
+    stage_tile(V.p, V.st, it * kKB, base + kTile, wave, lane);
+  };
+  issue(0);
+  for (int it = 0; it < nkb; ++it) {
+    wait_vm0();
+    barrier();
+    issue(it + 1);
+    const char* sK = lds + (it & 1) * 2 * kTile;
+    const char* sV = sK + kTile;
+    const int kb = it * kKB;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma(row_rd(sK, 32 * kh + (lane & 31), 2 * ks + hh), qf[ks], s);
+        dp = mfma(row_rd(sV, 32 * kh + (lane & 31), 2 * ks + hh), gf[ks], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        float p = exp2f(s[r] * c - lse2);
+        if (CAUSAL) p = key > qi ? 0.f : p;
+        float g = dp[r];
+        if (DROP) {
+          const uint32_t hs = drop_hash(s0, s1, bh, T, qi, key);
+          g = drop_keep(hs, key, thr) ? g * inv_keep : 0.f;
+        }
+        s[r] = p * (g - dlt);  // dSᵀ (without the softmax scale)
+      }
+#pragma unroll
+      for (int sg = 0; sg < 2; ++sg) {
+        const bf16x8 df = acc_frag(s, sg);
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) dacc[dh] = mfma(tr_op(sK, 32 * kh + 16 * sg, 32 * dh, lane), df, dacc[dh]);
+      }
+    }
+  }
+  if (qok) {
+    uint16_t* D = static_cast<uint16_t*>(dq.ptr) + b * dq.sb + hd * kD + static_cast<int64_t>(qi) * dq.st;
+    const float sc = P.scale;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = 32 * dh + 8 * g + 4 * hh;
+        *reinterpret_cast<uint2*>(D + d0) = make_uint2(pack2(dacc[dh][4 * g] * sc, dacc[dh][4 * g + 1] * sc),
+                                                       pack2(dacc[dh][4 * g + 2] * sc, dacc[dh][4 * g + 3] * sc));
+      }
+  }
+}
+
+// ------------------------------------------------------ bwd: dK, dV ------
+// key on the lane: S = Q·Kᵀ, dP = dO·Vᵀ (queries in the accumulator rows),
+// dVᵀ += dOᵀ·(P∘keep/(1-p)), dKᵀ += Qᵀ·dS. Q / dO tiles (+ LSE, δ) stream
+// through LDS; each wave keeps its 32 keys' dKᵀ, dVᵀ in registers.
+template <bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTensor q, AttnTensor k, AttnTensor v,
+                                                          AttnTensor dout, const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, AttnOut dk, AttnOut dv) {
+  constexpr int kStage = 2 * kTile + 2 * kKB * 4;  // Q | dO | lse | delta
+  __shared__ __attribute__((aligned(16))) char lds[2 * kStage];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hh = lane >> 5;
+  const int bh = blockIdx.y, b = bh / P.H, hd = bh % P.H;
+  const int T = P.T;
+  const int kb0 = blockIdx.x * 128;
+  const int key = kb0 + wave * 32 + (lane & 31);  // this lane's key
+  const bool kok = key < T;
+  const Ptrs Q = head(q, b, hd), K = head(k, b, hd), V = head(v, b, hd), G = head(dout, b, hd);
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const int64_t off = 16 * ks + 8 * hh;
+    kf[ks] = __builtin_bit_cast(bf16x8, kok ? *reinterpret_cast<const uint4*>(K.p + key * K.st + off) : z);
+    vf[ks] = __builtin_bit_cast(bf16x8, kok ? *reinterpret_cast<const uint4*>(V.p + key * V.st + off) : z);
+  }
+  const float c = P.scale * kLog2e;
+  const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
+  const float inv_keep = 1.f / (1.f - P.p_drop);
+  const uint32_t s0 = static_cast<uint32_t>(P.seed), s1 = static_cast<uint32_t>(P.seed >> 32);
+  const float* L = lse + static_cast<int64_t>(bh) * T;
+  const float* DL = delta + static_cast<int64_t>(bh) * T;
+
+  f32x16 dka[2] = {zero16(), zero16()}, dva[2] = {zero16(), zero16()};
+  const int qt0 = CAUSAL ? kb0 / kKB : 0;  // first query tile that can see these keys
+  const int nqt = T / kKB;
+  auto issue = [&](int it) {
+    if (qt0 + it >= nqt) return;
+    const int qb = (qt0 + it) * kKB;
+    char* base = lds + (it & 1) * kStage;
+    stage_tile(Q.p, Q.st, qb, base, wave, lane);
+    stage_tile(G.p, G.st, qb, base + kTile, wave, lane);
+    if (wave == 0) {
+      glds4(L + qb + lane, base + 2 * kTile);
+      glds4(DL + qb + lane, base + 2 * kTile + kKB * 4);
+    }
+  };
+  issue(0);
+  for (int it = 0; qt0 + it < nqt; ++it) {
+    wait_vm0();
+    barrier();
+    issue(it + 1);
+    const char* sQ = lds + (it & 1) * kStage;
+    const char* sG = sQ + kTile;
+    const float* sL = reinterpret_cast<const float*>(sQ + 2 * kTile);
+    const float* sD = sL + kKB;
+    const int qb = (qt0 + it) * kKB;
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma(row_rd(sQ, 32 * qs + (lane & 31), 2 * ks + hh), kf[ks], s);
+        dp = mfma(row_rd(sG, 32 * qs + (lane & 31), 2 * ks + hh), vf[ks], dp);
+      }
+      // rows: query qb + 32qs + (r&3) + 8(r>>2) + 4hh; column: this lane's key.
+      // One k-step (8 rows) at a time: P∘keep and dS packed to bf16 right away
+      // (short fp32 live ranges).
+#pragma unroll
+      for (int sg = 0; sg < 2; ++sg) {
+        float pv[8], dsv[8];
+#pragma unroll
+        for (int gg2 = 0; gg2 < 2; ++gg2) {
+          const int g = 2 * sg + gg2;
+          const int rl = 32 * qs + 8 * g + 4 * hh;  // 4 consecutive rows rl … rl+3
+          const float4 l4 = *reinterpret_cast<const float4*>(sL + rl);
+          const float4 d4 = *reinterpret_cast<const float4*>(sD + rl);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            const int qrow = qb + rl + e;
+            float p = exp2f(s[r] * c - lv[e]);
+            if (CAUSAL) p = key > qrow ? 0.f : p;
+            float gg = dp[r], pk = p;
+            if (DROP) {
+              const bool kp = drop_keep(drop_hash(s0, s1, bh, T, qrow, key), key, thr);
+              gg = kp ? gg * inv_keep : 0.f;
+              pk = kp ? p * inv_keep : 0.f;
+            }
+            pv[4 * gg2 + e] = pk;
+            dsv[4 * gg2 + e] = p * (gg - dv4[e]);  // dS (without the softmax scale)
+          }
+        }
+        const bf16x8 pf = __builtin_bit_cast(
+            bf16x8, make_uint4(pack2(pv[0], pv[1]), pack2(pv[2], pv[3]), pack2(pv[4], pv[5]), pack2(pv[6], pv[7])));
+        const bf16x8 df = __builtin_bit_cast(bf16x8, make_uint4(pack2(dsv[0], dsv[1]), pack2(dsv[2], dsv[3]),
+                                                                pack2(dsv[4], dsv[5]), pack2(dsv[6], dsv[7])));
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          dva[dh] = mfma(tr_op(sG, 32 * qs + 16 * sg, 32 * dh, lane), pf, dva[dh]);
+          dka[dh] = mfma(tr_op(sQ, 32 * qs + 16 * sg, 32 * dh, lane), df, dka[dh]);
+        }
+      }
+    }
+  }
+  if (kok) {
+    uint16_t* DK = static_cast<uint16_t*>(dk.ptr) + b * dk.sb + hd * kD + static_cast<int64_t>(key) * dk.st;
+    uint16_t* DV = static_cast<uint16_t*>(dv.ptr) + b * dv.sb + hd * kD + static_cast<int64_t>(key) * dv.st;
+    const float sc = P.scale;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = 32 * dh + 8 * g + 4 * hh;
+        *reinterpret_cast<uint2*>(DK + d0) = make_uint2(pack2(dka[dh][4 * g] * sc, dka[dh][4 * g + 1] * sc),
+                                                        pack2(dka[dh][4 * g + 2] * sc, dka[dh][4 * g + 3] * sc));
+        *reinterpret_cast<uint2*>(DV + d0) = make_uint2(pack2(dva[dh][4 * g], dva[dh][4 * g + 1]),
+                                                        pack2(dva[dh][4 * g + 2], dva[dh][4 * g + 3]));
+      }
+  }
+}
+
+}  // namespace
+
+bool attn_supported(int T, int D) { return D == kD && T > 0 && T % kKB == 0; }
+
+void attn_fwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, AttnOut o, float* lse,
+              hipStream_t s) {
+  const dim3 grid((p.T + 127) / 128, p.B * p.H);
+  const bool drop = p.p_drop > 0.f;
+#define DCP_AF(C, D) hipLaunchKernelGGL((attn_fwd_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, o, lse)
+  if (p.causal && drop) DCP_AF(true, true);
+  else if (p.causal) DCP_AF(true, false);
+  else if (drop) DCP_AF(false, true);
+  else DCP_AF(false, false);
+#undef DCP_AF
+}
+
+void attn_bwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, AttnTensor o, AttnTensor dout,
+              const float* lse, float* delta, AttnOut dq, AttnOut dk, AttnOut dv, hipStream_t s) {
+  const int64_t rows = static_cast<int64_t>(p.B) * p.H * p.T;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3(static_cast<int>((rows + kT - 1) / kT)), dim3(kT), 0, s, p, o, dout,
+                     delta);
+  const dim3 grid((p.T + 127) / 128, p.B * p.H);
+  const bool drop = p.p_drop > 0.f;
+#define DCP_AB(C, D)                                                                                          \
+  do {                                                                                                        \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, dout, lse, delta, dk, dv); \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, dout, lse, delta, dq);   \
+  } while (0)
+  if (p.causal && drop) DCP_AB(true, true);
+  else if (p.causal) DCP_AB(true, false);
+  else if (drop) DCP_AB(false, true);
+  else DCP_AB(false, false);
+#undef DCP_AB
+}
+
+}  // namespace kern
+}  // namespace dcp

@@ -536,6 +536,43 @@ __global__ void __launch_bounds__(kT) weight_cast_t_kernel(const float* __restri
   }
 }
 
+// Column sums of a bf16 [M, N] matrix into fp32 (Linear bias gradients):
+// stage 1 writes one fp32 partial row per (column chunk, row slab) block,
+// stage 2 = slab_partial_kernel over the slabs. Deterministic, no atomics.
+constexpr int kColSlabs = 64;
+__global__ void __launch_bounds__(kT) colsum_partial_kernel(const uint16_t* __restrict__ x, float* __restrict__ part,
+                                                            int64_t M, int N, int64_t rows_per_slab) {
+  __shared__ float red[8][32 * 8];
+  const int cv = threadIdx.x & 31, rg = threadIdx.x >> 5;  // 32 column vectors × 8 row groups
+  const int c0 = (blockIdx.x * 32 + cv) * 8;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_slab;
+  const int64_t r1 = min(M, r0 + rows_per_slab);
+  float s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.f;
+  if (c0 < N) {
+#pragma unroll 4
+    for (int64_t r = r0 + rg; r < r1; r += 8) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + r * N + c0);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s[2 * k] += bf_lo(w[k]);
+        s[2 * k + 1] += bf_hi(w[k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rg][cv * 8 + k] = s[k];
+  __syncthreads();
+  const int c = threadIdx.x;  // 256 columns of this chunk
+  const int col = blockIdx.x * 256 + c;
+  float t = 0.f;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) t += red[g][c];
+  if (col < N) part[static_cast<int64_t>(blockIdx.y) * N + col] = t;
+}
+
 struct WgradPlan {
   int bm, bn, tiles, S;
   int64_t chunk;
@@ -604,6 +641,22 @@ void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_
   hipLaunchKernelGGL(weight_cast_t_kernel, grid, dim3(kT), 0, s, w, static_cast<uint16_t*>(wb),
                      static_cast<uint16_t*>(wt), R, Cc);
 }
+
+void colsum_bf16(const void* x, float* out, int64_t M, int N, float* ws, hipStream_t s) {
+  const int64_t rps = (M + kColSlabs - 1) / kColSlabs;
+  const dim3 g1((N + 255) / 256, kColSlabs);
+  hipLaunchKernelGGL(colsum_partial_kernel, g1, dim3(kT), 0, s, static_cast<const uint16_t*>(x), ws, M, N, rps);
+  const int64_t n4 = N / 4;
+  const int gx = static_cast<int>((n4 + kT - 1) / kT);
+  // kColSlabs = 64 = 4 groups of 16, then one more level
+  float4* mid = reinterpret_cast<float4*>(ws + static_cast<int64_t>(kColSlabs) * N);
+  hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, kColSlabs / kSlabGroup), dim3(kT), 0, s,
+                     reinterpret_cast<const float4*>(ws), mid, n4, kColSlabs);
+  hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, mid, reinterpret_cast<float4*>(out), n4,
+                     kColSlabs / kSlabGroup);
+}
+
+int64_t colsum_workspace(int N) { return static_cast<int64_t>(kColSlabs + kColSlabs / kSlabGroup) * N; }
 
 int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
   const WgradPlan p = wgrad_plan(M, N1, N2, taps);

@@ -15,8 +15,9 @@ namespace dcp {
 namespace kern {
 namespace {
 
-constexpr int kWaves = 4;  // rows per workgroup
+constexpr int kWaves = 4;  // waves per workgroup
 constexpr int kT = 64 * kWaves;
+constexpr int kRows = 2;   // rows in flight per wave
 
 __device__ __forceinline__ uint16_t f2bf(float f) {
   uint32_t u = __float_as_uint(f);
@@ -69,69 +70,88 @@ __device__ __forceinline__ float wsum(float v) {
   return v;
 }
 
-// VPL = 16-B vectors per lane (D <= VPL*512). XD: dtype of x (and dx), YD:
-// dtype of y (and dy) — x fp32 / y bf16 is the autocast residual-stream case:
-// the LayerNorm output feeds a bf16 GEMM directly, no separate cast pass.
-template <int XD, int YD, int VPL>
+// 8 consecutive fp32 affine values (or the identity when absent)
+__device__ __forceinline__ void ld_aff(const float* p, int c, float def, float (&o)[8]) {
+  if (p) {
+    const float4 a = *reinterpret_cast<const float4*>(p + c);
+    const float4 b = *reinterpret_cast<const float4*>(p + c + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+    o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = def;
+  }
+}
+
+// VPL = 16-B vectors per lane (D <= VPL*512), R rows per wave with all their
+// loads (and the affine parameters) issued before the first reduction: R× the
+// bytes in flight of a row-at-a-time wave. XD: dtype of x (and dx), YD: dtype
+// of y (and dy) — x fp32 / y bf16 is the autocast residual-stream case: the
+// LayerNorm output feeds a bf16 GEMM directly, no separate cast pass.
+template <int XD, int YD, int VPL, int R>
 __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, const float* __restrict__ w,
                                                     const float* __restrict__ b, void* __restrict__ y,
                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                     int64_t rows, int D, float eps) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * R;
+  if (row0 >= rows) return;
   const int nv = D >> 3;
-  const int64_t base = row * D;
-  float v[VPL][8];
-  float s = 0.f;
+  float wv[VPL][8], bv[VPL][8];
+  float v[R][VPL][8];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
     const int vi = lane + j * 64;
     if (vi < nv) {
-      L8<XD>::ld(x, base + vi * 8, v[j]);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s += v[j][k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[j][k] = 0.f;
+      for (int r = 0; r < R; ++r)
+        if (row0 + r < rows) L8<XD>::ld(x, (row0 + r) * D + vi * 8, v[r][j]);
+      ld_aff(w, vi * 8, 1.f, wv[j]);
+      ld_aff(b, vi * 8, 0.f, bv[j]);
     }
   }
-  const float mean = wsum(s) / static_cast<float>(D);
-  float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < VPL; ++j) {
-    if (lane + j * 64 < nv) {
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + r;
+    if (row >= rows) break;
+    float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float d = v[j][k] - mean;
-        q = fmaf(d, d, q);
-      }
+    for (int j = 0; j < VPL; ++j)
+      if (lane + j * 64 < nv)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += v[r][j][k];
+    const float mean = wsum(s) / static_cast<float>(D);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+      if (lane + j * 64 < nv)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float d = v[r][j][k] - mean;
+          q = fmaf(d, d, q);
+        }
+    const float rstd = rsqrtf(wsum(q) / static_cast<float>(D) + eps);
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
     }
-  }
-  const float rstd = rsqrtf(wsum(q) / static_cast<float>(D) + eps);
-  if (lane == 0) {
-    mean_out[row] = mean;
-    rstd_out[row] = rstd;
-  }
 #pragma unroll
-  for (int j = 0; j < VPL; ++j) {
-    const int vi = lane + j * 64;
-    if (vi < nv) {
-      float o[8];
+    for (int j = 0; j < VPL; ++j) {
+      const int vi = lane + j * 64;
+      if (vi < nv) {
+        float o[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int c = vi * 8 + k;
-        const float xn = (v[j][k] - mean) * rstd;
-        o[k] = w ? fmaf(xn, w[c], b ? b[c] : 0.f) : xn;
+        for (int k = 0; k < 8; ++k) o[k] = fmaf((v[r][j][k] - mean) * rstd, wv[j][k], bv[j][k]);
+        L8<YD>::st(y, row * D + vi * 8, o);
       }
-      L8<YD>::st(y, base + vi * 8, o);
     }
   }
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 // partial[blk][0][D] += dy * xhat (dgamma), partial[blk][1][D] += dy (dbeta)
-template <int XD, int YD, int VPL>
+// Each wave takes R rows at a time with all their loads in flight together.
+template <int XD, int YD, int VPL, int R>
 __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy, const void* __restrict__ x,
                                                     const float* __restrict__ w, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, void* __restrict__ dx,
@@ -141,47 +161,63 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nv = D >> 3;
-  float accg[VPL][8], accb[VPL][8];
+  float accg[VPL][8], accb[VPL][8], wv[VPL][8];
 #pragma unroll
-  for (int j = 0; j < VPL; ++j)
+  for (int j = 0; j < VPL; ++j) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) accg[j][k] = accb[j][k] = 0.f;
+    if (lane + j * 64 < nv) ld_aff(w, (lane + j * 64) * 8, 1.f, wv[j]);
+  }
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_blk;
   const int64_t r1 = min(rows, r0 + rows_per_blk);
-  for (int64_t row = r0 + wid; row < r1; row += kWaves) {
-    const int64_t base = row * D;
-    const float mu = mean[row], rs = rstd[row];
-    float xh[VPL][8], g[VPL][8];
-    float s1 = 0.f, s2 = 0.f;
+  for (int64_t rb = r0 + wid * R; rb < r1; rb += kWaves * R) {
+    float dv[R][VPL][8], xh[R][VPL][8], mu[R], rs[R];
 #pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-      const int vi = lane + j * 64;
-      if (vi < nv) {
-        float dv[8];
-        L8<YD>::ld(dy, base + vi * 8, dv);
-        L8<XD>::ld(x, base + vi * 8, xh[j]);
+    for (int r = 0; r < R; ++r) {
+      const int64_t row = rb + r < r1 ? rb + r : r1 - 1;  // tail: recompute a valid row, store nothing
+      mu[r] = mean[row];
+      rs[r] = rstd[row];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int c = vi * 8 + k;
-          xh[j][k] = (xh[j][k] - mu) * rs;
-          accg[j][k] = fmaf(dv[k], xh[j][k], accg[j][k]);
-          accb[j][k] += dv[k];
-          g[j][k] = w ? dv[k] * w[c] : dv[k];
-          s1 += g[j][k];
-          s2 = fmaf(g[j][k], xh[j][k], s2);
+      for (int j = 0; j < VPL; ++j) {
+        const int vi = lane + j * 64;
+        if (vi < nv) {
+          L8<YD>::ld(dy, row * D + vi * 8, dv[r][j]);
+          L8<XD>::ld(x, row * D + vi * 8, xh[r][j]);
         }
       }
     }
-    const float m1 = wsum(s1) / static_cast<float>(D);
-    const float m2 = wsum(s2) / static_cast<float>(D);
 #pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-      const int vi = lane + j * 64;
-      if (vi < nv) {
-        float o[8];
+    for (int r = 0; r < R; ++r) {
+      const bool live = rb + r < r1;
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = rs * (g[j][k] - m1 - xh[j][k] * m2);
-        L8<XD>::st(dx, base + vi * 8, o);
+      for (int j = 0; j < VPL; ++j) {
+        if (lane + j * 64 < nv) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            xh[r][j][k] = (xh[r][j][k] - mu[r]) * rs[r];
+            if (live) {
+              accg[j][k] = fmaf(dv[r][j][k], xh[r][j][k], accg[j][k]);
+              accb[j][k] += dv[r][j][k];
+            }
+            dv[r][j][k] *= wv[j][k];  // g
+            s1 += dv[r][j][k];
+            s2 = fmaf(dv[r][j][k], xh[r][j][k], s2);
+          }
+        }
+      }
+      const float m1 = wsum(s1) / static_cast<float>(D);
+      const float m2 = wsum(s2) / static_cast<float>(D);
+      if (!live) continue;
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) {
+        const int vi = lane + j * 64;
+        if (vi < nv) {
+          float o[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = rs[r] * (dv[r][j][k] - m1 - xh[r][j][k] * m2);
+          L8<XD>::st(dx, (rb + r) * D + vi * 8, o);
+        }
       }
     }
   }
@@ -214,6 +250,7 @@ __global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
   const int j = threadIdx.x % tpc;
   float sg = 0.f, sb = 0.f;
   if (c < D) {
+#pragma unroll 8
     for (int b = j; b < nblk; b += tpc) {
       sg += part[(static_cast<int64_t>(b) * 2 + 0) * D + c];
       sb += part[(static_cast<int64_t>(b) * 2 + 1) * D + c];
@@ -234,7 +271,7 @@ template <int XD, int YD>
 void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w, const float* b, void* y, float* mean,
                   float* rstd, int64_t rows, int D, float eps) {
 #define DCP_LNF(V) \
-  hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps)
+  hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V, kRows>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps)
   switch (vpl) {
     case 1: DCP_LNF(1); break;
     case 2: DCP_LNF(2); break;
@@ -248,7 +285,8 @@ template <int XD, int YD>
 void bwd_dispatch(int vpl, dim3 g, size_t sm, hipStream_t s, const void* dy, const void* x, const float* w,
                   const float* mean, const float* rstd, void* dx, float* part, int64_t rows, int D, int rpb) {
 #define DCP_LNB(V) \
-  hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb)
+  hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, kRows>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, \
+                     rpb)
   switch (vpl) {
     case 1: DCP_LNB(1); break;
     case 2: DCP_LNB(2); break;
@@ -277,7 +315,7 @@ int ln_bwd_blocks(int64_t rows) {
 
 void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const float* b, void* y, float* mean,
                 float* rstd, int64_t rows, int D, float eps, hipStream_t s) {
-  const dim3 g(static_cast<unsigned>((rows + kWaves - 1) / kWaves));
+  const dim3 g(static_cast<unsigned>((rows + kWaves * kRows - 1) / (kWaves * kRows)));
   const int vpl = vpl_for(D);
   if (xdtype == LN_BF16) fwd_dispatch<LN_BF16, LN_BF16>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
   else if (ydtype == LN_BF16) fwd_dispatch<LN_F32, LN_BF16>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);

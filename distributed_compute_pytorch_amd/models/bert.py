@@ -6,8 +6,9 @@ next-sentence prediction. Random init (std 0.02).
 
 MI355X path: every LayerNorm is the hand-written kernel; the MLM head runs
 only on the masked positions (gathered first: ~15 % of tokens), and its
-vocab cross-entropy is the fused kernel on bf16 logits; attention is
-``scaled_dot_product_attention``.
+vocab cross-entropy is the fused kernel on bf16 logits; attention is our MFMA
+flash-attention kernel (``ops/attention.py``; ``scaled_dot_product_attention``
+when a padding mask is given or with ``fused=False``).
 """
 from __future__ import annotations
 
@@ -17,7 +18,9 @@ import torch
 from torch import nn
 from torch.nn import functional as F
 
+from ..ops.attention import attn_supported, flash_attn
 from ..ops.cross_entropy import fused_cross_entropy
+from ..ops.linear import FusedLinear
 from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
 
@@ -48,14 +51,24 @@ class BertSelfAttention(nn.Module):
     def __init__(self, cfg):
         super().__init__()
         self.heads = cfg.heads
-        self.query = nn.Linear(cfg.hidden, cfg.hidden)
-        self.key = nn.Linear(cfg.hidden, cfg.hidden)
-        self.value = nn.Linear(cfg.hidden, cfg.hidden)
+        lin = FusedLinear if cfg.fused else nn.Linear
+        self.query = lin(cfg.hidden, cfg.hidden)
+        self.key = lin(cfg.hidden, cfg.hidden)
+        self.value = lin(cfg.hidden, cfg.hidden)
         self.dropout = cfg.dropout
+        self.fused = cfg.fused
 
     def forward(self, x, mask):
         B, T, C = x.shape
         h = self.heads
+        if self.fused and mask is None:
+            q, k, v = self.query(x), self.key(x), self.value(x)
+            if attn_supported(q, h):  # MFMA flash attention, [B, T, C] in and out
+                return flash_attn(q, k, v, h, causal=False, dropout_p=self.dropout if self.training else 0.0)
+            return F.scaled_dot_product_attention(
+                q.view(B, T, h, C // h).transpose(1, 2), k.view(B, T, h, C // h).transpose(1, 2),
+                v.view(B, T, h, C // h).transpose(1, 2),
+                dropout_p=self.dropout if self.training else 0.0).transpose(1, 2).reshape(B, T, C)
 
         def split(t):
             return t.view(B, T, h, C // h).transpose(1, 2)
@@ -69,10 +82,11 @@ class BertLayer(nn.Module):
     def __init__(self, cfg):
         super().__init__()
         self.attention = BertSelfAttention(cfg)
-        self.attn_out = nn.Linear(cfg.hidden, cfg.hidden)
+        lin = FusedLinear if cfg.fused else nn.Linear
+        self.attn_out = lin(cfg.hidden, cfg.hidden)
         self.attn_ln = _ln(cfg, cfg.hidden)
-        self.intermediate = nn.Linear(cfg.hidden, cfg.intermediate)
-        self.output = nn.Linear(cfg.intermediate, cfg.hidden)
+        self.intermediate = lin(cfg.hidden, cfg.intermediate)
+        self.output = lin(cfg.intermediate, cfg.hidden)
         self.out_ln = _ln(cfg, cfg.hidden)
         self.p = cfg.dropout
         self._dadd = dropout_add if cfg.fused else _plain_dropout_add
@@ -93,7 +107,7 @@ class BertForPreTraining(nn.Module):
         self.emb_drop = nn.Dropout(cfg.dropout)
         self.layers = nn.ModuleList([BertLayer(cfg) for _ in range(cfg.layers)])
         self.pooler = nn.Linear(cfg.hidden, cfg.hidden)
-        self.mlm_transform = nn.Linear(cfg.hidden, cfg.hidden)
+        self.mlm_transform = (FusedLinear if cfg.fused else nn.Linear)(cfg.hidden, cfg.hidden)
         self.mlm_ln = _ln(cfg, cfg.hidden)
         self.mlm_bias = nn.Parameter(torch.zeros(cfg.vocab_size))
         self.nsp = nn.Linear(cfg.hidden, 2)

@@ -6,8 +6,10 @@ tied LM head. Random init (std 0.02, residual projections scaled by
 (wte, wpe, h.N.ln_1, h.N.attn.c_attn, ...).
 
 MI355X path: LayerNorm = hand-written kernel (bf16 activations, fp32 stats),
-attention = ``scaled_dot_product_attention`` (flash kernels of PyTorch-ROCm),
-loss = fused vocab cross-entropy straight from bf16 logits.
+attention = our MFMA flash-attention kernels on the packed qkv projection
+(causal, in-kernel dropout; ``ops/attention.py``), loss = fused vocab
+cross-entropy straight from bf16 logits. ``fused=False`` is the stock path
+(``scaled_dot_product_attention``).
 """
 from __future__ import annotations
 
@@ -18,7 +20,9 @@ import torch
 from torch import nn
 from torch.nn import functional as F
 
+from ..ops.attention import attn_supported, flash_attn_qkv
 from ..ops.cross_entropy import fused_cross_entropy
+from ..ops.linear import FusedLinear
 from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
 
@@ -42,13 +46,21 @@ class CausalSelfAttention(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
         self.n_head = cfg.n_head
-        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
-        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+        lin = FusedLinear if cfg.fused else nn.Linear
+        self.c_attn = lin(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = lin(cfg.n_embd, cfg.n_embd)
         self.dropout = cfg.dropout
+        self.fused = cfg.fused
 
     def forward(self, x):
         B, T, C = x.shape
-        q, k, v = self.c_attn(x).split(C, dim=2)
+        qkv = self.c_attn(x)
+        if self.fused and attn_supported(qkv, self.n_head):
+            # MFMA flash attention on the packed projection: no head transposes,
+            # dq/dk/dv written straight into one packed gradient
+            y = flash_attn_qkv(qkv, self.n_head, causal=True, dropout_p=self.dropout if self.training else 0.0)
+            return self.c_proj(y)
+        q, k, v = qkv.split(C, dim=2)
         h = self.n_head
         q = q.view(B, T, h, C // h).transpose(1, 2)
         k = k.view(B, T, h, C // h).transpose(1, 2)
@@ -61,8 +73,9 @@ class CausalSelfAttention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
-        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
-        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+        lin = FusedLinear if cfg.fused else nn.Linear
+        self.c_fc = lin(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = lin(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
         return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))

@@ -1,0 +1,116 @@
+"""Flash attention on the hand-written MFMA kernels (``csrc/kernels/attention.hip``).
+
+Head dim 64, bf16 activations, fp32 softmax statistics, optional causal mask
+and dropout on the attention probabilities (mask regenerated in the backward
+from a counter hash: nothing is stored). Replaces
+``scaled_dot_product_attention`` (PyTorch-ROCm's aotriton kernels) for
+GPT-2-small and BERT-base.
+
+* :func:`flash_attn` — q, k, v as [B, T, H*64] (any row stride: slices of a
+  packed projection are read in place), output [B, T, H*64] — already the
+  layout the output projection consumes (no head transposes).
+* :func:`flash_attn_qkv` — packed [B, T, 3*H*64] input (GPT-2's ``c_attn``);
+  the backward writes dq/dk/dv straight into one packed gradient (no cat).
+"""
+from __future__ import annotations
+
+import torch
+
+from .._ext import C as _C
+
+
+def _seed() -> int:
+    # from torch's CPU generator: torch.manual_seed makes runs reproducible
+    return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+
+
+def attn_supported(x: torch.Tensor, heads: int) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 3
+            and bool(_C.attn_ok(x.shape[1], x.shape[2], heads)))
+
+
+class _FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, heads, causal, p_drop, seed):
+        o, lse = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.cfg = (heads, causal, p_drop, seed)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        heads, causal, p_drop, seed = ctx.cfg
+        do = do.contiguous()
+        if do.dtype != torch.bfloat16:
+            do = do.to(torch.bfloat16)
+        dq, dk, dv = torch.empty_like(q, memory_format=torch.contiguous_format), torch.empty_like(
+            k, memory_format=torch.contiguous_format), torch.empty_like(v, memory_format=torch.contiguous_format)
+        _C.flash_attn_bwd(do, q, k, v, o, lse, heads, causal, p_drop, seed, dq, dk, dv)
+        return dq, dk, dv, None, None, None, None
+
+
+class _FlashAttnQKVFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, heads, causal, p_drop, seed):
+        C = qkv.shape[2] // 3
+        q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+        o, lse = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.cfg = (heads, causal, p_drop, seed)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        heads, causal, p_drop, seed = ctx.cfg
+        do = do.contiguous()
+        if do.dtype != torch.bfloat16:
+            do = do.to(torch.bfloat16)
+        C = qkv.shape[2] // 3
+        dqkv = torch.empty_like(qkv, memory_format=torch.contiguous_format)
+        q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+        dq, dk, dv = dqkv[..., :C], dqkv[..., C:2 * C], dqkv[..., 2 * C:]
+        _C.flash_attn_bwd(do, q, k, v, o, lse, heads, causal, p_drop, seed, dq, dk, dv)
+        return dqkv, None, None, None, None
+
+
+def flash_attn(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, causal: bool = False,
+               dropout_p: float = 0.0, seed: int = None) -> torch.Tensor:
+    """softmax(q kᵀ / 8 [+ causal mask]) → dropout(p) → · v, per head of 64."""
+    return _FlashAttnFn.apply(q, k, v, heads, causal, float(dropout_p),
+                              _seed() if seed is None else int(seed))
+
+
+def flash_attn_qkv(qkv: torch.Tensor, heads: int, causal: bool = False, dropout_p: float = 0.0,
+                   seed: int = None) -> torch.Tensor:
+    return _FlashAttnQKVFn.apply(qkv, heads, causal, float(dropout_p), _seed() if seed is None else int(seed))
+
+
+def dropout_keep_mask(B: int, H: int, T: int, p: float, seed: int, device=None) -> torch.Tensor:
+    """The kernels' dropout keep-mask [B, H, T, T] rebuilt with integer torch
+    ops (test oracle): 16 bits of mix32((ctr ^ s0)·0x9E3779B1 + s1) per element,
+    ctr = (bh·T + q)·(T/2) + key/2, low half for even keys."""
+    M = 0xFFFFFFFF
+    dev = device or "cpu"
+
+    def mul32(x, c):  # (x * c) mod 2^32 without int64 overflow
+        lo, hi = x & 0xFFFF, x >> 16
+        return ((lo * c) + (((hi * c) & 0xFFFF) << 16)) & M
+
+    def mix32(x):
+        x = x ^ (x >> 16)
+        x = mul32(x, 0x7feb352d)
+        x = x ^ (x >> 15)
+        x = mul32(x, 0x846ca68b)
+        return x ^ (x >> 16)
+
+    s0, s1 = seed & M, (seed >> 32) & M
+    bh = torch.arange(B * H, device=dev, dtype=torch.int64)[:, None, None]
+    qq = torch.arange(T, device=dev, dtype=torch.int64)[None, :, None]
+    kk = torch.arange(T, device=dev, dtype=torch.int64)[None, None, :]
+    ctr = (((bh * T + qq) & M) * (T >> 1) + (kk >> 1)) & M
+    h = mix32((mul32(ctr ^ s0, 0x9E3779B1) + s1) & M)
+    r16 = torch.where((kk & 1) == 1, h >> 16, h & 0xFFFF)
+    thr = int(p * 65536.0 + 0.5)
+    return (r16 >= thr).view(B, H, T, T)

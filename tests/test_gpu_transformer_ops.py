@@ -164,3 +164,47 @@ def test_eval_metrics(cuda, dtype, log_probs):
     assert n == tot_n
     assert abs(avg - tot_loss / tot_n) < 1e-3 * max(1, abs(avg))
     assert abs(acc - tot_corr / tot_n) < 1e-9
+
+
+@pytest.mark.parametrize("shape", [(4096, 768), (1000, 3072), (7, 64)])
+def test_colsum_matches_torch(cuda, shape):
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(*shape, generator=g).to(cuda).to(torch.bfloat16)
+    out = _C.colsum(x)
+    ref = x.float().sum(0)
+    assert out.dtype == torch.float32
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_fused_linear_matches_fp32(cuda):
+    from torch import nn
+
+    from distributed_compute_pytorch_amd.ops.linear import FusedLinear
+
+    torch.manual_seed(0)
+    lin = FusedLinear(256, 384).to(cuda)
+    ref = nn.Linear(256, 384).to(cuda)
+    ref.load_state_dict(lin.state_dict())
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(4, 64, 256, generator=g).to(cuda)
+    gy = torch.randn(4, 64, 384, generator=g).to(cuda).to(torch.bfloat16)
+    xa = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = lin(xa)
+    y.backward(gy)
+    xr = x.to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.linear(xr, ref.weight.to(torch.bfloat16).float(), ref.bias.to(torch.bfloat16).float())
+    yr.backward(gy.float())
+    wr = ref.weight.detach().clone().requires_grad_(True)
+    br = ref.bias.detach().clone().requires_grad_(True)
+    F.linear(x.to(torch.bfloat16).float(), wr, br).backward(gy.float())
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / b.float().norm())
+
+    assert y.dtype == torch.bfloat16 and rel(y, yr) < 1e-2
+    assert rel(xa.grad, xr.grad) < 1e-2
+    assert lin.weight.grad.dtype == torch.float32 and rel(lin.weight.grad, wr.grad) < 1e-2
+    assert lin.bias.grad.dtype == torch.float32 and rel(lin.bias.grad, br.grad) < 1e-3

@@ -1,0 +1,44 @@
+"""Per-kernel call count / mean / total time from a rocprofv3 run (rocpd
+SQLite database or kernel-trace CSV), optionally with the grid size so that
+one kernel's different shapes separate.
+
+    python tools/kernel_stats.py <prof_results.db | kernel_trace.csv> [--top 30] [--grid]
+"""
+import argparse
+import csv
+import sqlite3
+from collections import defaultdict
+
+
+def rows(path, grid):
+    if path.endswith(".db"):
+        con = sqlite3.connect(path)
+        cols = [r[1] for r in con.execute("pragma table_info(kernels)")]
+        gsel = ", grid_size_x, grid_size_y, grid_size_z" if grid and "grid_size_x" in cols else ""
+        for rec in con.execute(f"select name, start, end{gsel} from kernels"):
+            yield (rec[0] + (f" grid={rec[3]}x{rec[4]}x{rec[5]}" if gsel else ""), rec[2] - rec[1])
+    else:
+        for r in csv.DictReader(open(path)):
+            n = r["Kernel_Name"]
+            if grid:
+                n += f" grid={r.get('Grid_Size_X')}x{r.get('Grid_Size_Y')}x{r.get('Grid_Size_Z')}"
+            yield n, int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("path")
+    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--grid", action="store_true")
+    a = ap.parse_args()
+    agg = defaultdict(lambda: [0, 0])
+    for n, d in rows(a.path, a.grid):
+        agg[n][0] += 1
+        agg[n][1] += d
+    print(f"{'calls':>6} {'mean us':>9} {'total ms':>9}  kernel")
+    for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
+        print(f"{c:6d} {t / c / 1e3:9.1f} {t / 1e6:9.2f}  {n[:150]}")
+
+
+if __name__ == "__main__":
+    main()
