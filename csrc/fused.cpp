@@ -310,9 +310,10 @@ at::Tensor colsum(const at::Tensor& x) {
   const int64_t N = x.size(-1);
   const int64_t M = x.numel() / N;
   DCP_CHECK(N % 8 == 0, "colsum: last dim must be a multiple of 8");
+  auto s = stream_of(x);
   at::Tensor out = at::empty({N}, x.options().dtype(at::kFloat));
-  at::Tensor ws = at::empty({kern::colsum_workspace(static_cast<int>(N))}, x.options().dtype(at::kFloat));
-  kern::colsum_bf16(x.data_ptr(), out.data_ptr<float>(), M, static_cast<int>(N), ws.data_ptr<float>(), stream_of(x));
+  DCP_CHECK(hipMemsetAsync(out.data_ptr(), 0, sizeof(float) * N, s) == hipSuccess, "memset failed");
+  kern::colsum_bf16(x.data_ptr(), out.data_ptr<float>(), M, static_cast<int>(N), s);
   return out;
 }
 

@@ -570,7 +570,7 @@ __global__ void __launch_bounds__(kT) colsum_partial_kernel(const uint16_t* __re
   float t = 0.f;
 #pragma unroll
   for (int g = 0; g < 8; ++g) t += red[g][c];
-  if (col < N) part[static_cast<int64_t>(blockIdx.y) * N + col] = t;
+  if (col < N) atomicAdd(part + col, t);  // part: ZEROED [N]
 }
 
 struct WgradPlan {
@@ -642,21 +642,13 @@ void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_
                      static_cast<uint16_t*>(wt), R, Cc);
 }
 
-void colsum_bf16(const void* x, float* out, int64_t M, int N, float* ws, hipStream_t s) {
-  const int64_t rps = (M + kColSlabs - 1) / kColSlabs;
-  const dim3 g1((N + 255) / 256, kColSlabs);
-  hipLaunchKernelGGL(colsum_partial_kernel, g1, dim3(kT), 0, s, static_cast<const uint16_t*>(x), ws, M, N, rps);
-  const int64_t n4 = N / 4;
-  const int gx = static_cast<int>((n4 + kT - 1) / kT);
-  // kColSlabs = 64 = 4 groups of 16, then one more level
-  float4* mid = reinterpret_cast<float4*>(ws + static_cast<int64_t>(kColSlabs) * N);
-  hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, kColSlabs / kSlabGroup), dim3(kT), 0, s,
-                     reinterpret_cast<const float4*>(ws), mid, n4, kColSlabs);
-  hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, mid, reinterpret_cast<float4*>(out), n4,
-                     kColSlabs / kSlabGroup);
+void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s) {
+  int64_t slabs = (M + 255) / 256;  // ≥ 32 rows per row group
+  if (slabs > kColSlabs) slabs = kColSlabs;
+  const int64_t rps = (M + slabs - 1) / slabs;
+  const dim3 g1((N + 255) / 256, static_cast<unsigned>(slabs));
+  hipLaunchKernelGGL(colsum_partial_kernel, g1, dim3(kT), 0, s, static_cast<const uint16_t*>(x), out, M, N, rps);
 }
-
-int64_t colsum_workspace(int N) { return static_cast<int64_t>(kColSlabs + kColSlabs / kSlabGroup) * N; }
 
 int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
   const WgradPlan p = wgrad_plan(M, N1, N2, taps);

@@ -31,10 +31,10 @@ void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
 // (the forward GEMM's B operand and the dgrad GEMM's B operand) in one launch.
 void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s);
 
-// out[N] (fp32) = column sums of a bf16 [M, N] matrix (N % 8 == 0); ws:
-// colsum_workspace(N) fp32 elements. Deterministic two-stage reduction.
-void colsum_bf16(const void* x, float* out, int64_t M, int N, float* ws, hipStream_t s);
-int64_t colsum_workspace(int N);
+// out[N] (fp32, ZEROED) += column sums of a bf16 [M, N] matrix (N % 8 == 0):
+// one launch, ≤ 64 row slabs × N/256 column chunks, one fp32 atomic per column
+// per block.
+void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s);
 
 // Workspace (fp32 elements) gemm_wgrad_bf16 needs for this shape.
 int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps = 1);

@@ -55,7 +55,7 @@ class CausalSelfAttention(nn.Module):
     def forward(self, x):
         B, T, C = x.shape
         qkv = self.c_attn(x)
-        if self.fused and attn_supported(qkv, self.n_head):
+        if self.fused and attn_supported(qkv[..., :C], self.n_head):
             # MFMA flash attention on the packed projection: no head transposes,
             # dq/dk/dv written straight into one packed gradient
             y = flash_attn_qkv(qkv, self.n_head, causal=True, dropout_p=self.dropout if self.training else 0.0)

@@ -6,7 +6,8 @@ gradient — ~1/6 of the non-GEMM kernel time of BERT-base / GPT-2-small
 (profiles/r1_*_prof22.txt). :class:`FusedLinear` (same parameters and
 state_dict keys) computes
 
-* dW with fp32 output straight from the hipBLASLt GEMM (``mm(..., out_dtype)``),
+* dW in fp32 straight from our split-M MFMA wgrad GEMM (``gemm.hip``; the
+  reduction over B·T rows is spread over the whole chip),
 * db with the hand-written deterministic column-sum kernel (``colsum``, fp32),
 * dX as the usual bf16 GEMM.
 """
@@ -43,7 +44,12 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (g2 @ w).view(x.shape)
         if ctx.needs_input_grad[1]:
-            dw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
+            if g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
+                # our split-M MFMA wgrad GEMM (gemm.hip): the hipBLASLt tiles picked
+                # for this K ≫ M,N shape leave most CUs idle (profiles/r1_bert_prof26.txt)
+                dw = _C.conv1x1_wgrad(g2, x2.contiguous())
+            else:
+                dw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
             if dw.dtype != ctx.wdtype:
                 dw = dw.to(ctx.wdtype)
         if ctx.bdtype is not None and ctx.needs_input_grad[2]:
