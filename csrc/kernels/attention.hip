@@ -190,6 +190,8 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
     const char* sK = lds + (it & 1) * 2 * kTile;
     const char* sV = sK + kTile;
     const int kb = it * kKB;
+    // causal: a key block wholly after this wave's last query contributes nothing
+    if (CAUSAL && kb > static_cast<int>(blockIdx.x) * 128 + wave * 32 + 31) continue;
     f32x16 s[2];
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
@@ -341,7 +343,8 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
     const char* sK = lds + (it & 1) * 2 * kTile;
     const char* sV = sK + kTile;
     const int kb = it * kKB;
-#pragma unroll
+    if (CAUSAL && kb > static_cast<int>(blockIdx.x) * 128 + wave * 32 + 31) continue;
+#pragma unroll 1
     for (int kh = 0; kh < 2; ++kh) {
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
@@ -441,8 +444,11 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
     const float* sL = reinterpret_cast<const float*>(sQ + 2 * kTile);
     const float* sD = sL + kKB;
     const int qb = (qt0 + it) * kKB;
-#pragma unroll
+    // one 32-query sub-tile at a time (unrolling both doubles the live
+    // S / dP accumulators and drops the kernel to one wave per SIMD)
+#pragma unroll 1
     for (int qs = 0; qs < 2; ++qs) {
+      if (CAUSAL && qb + 32 * qs + 31 < kb0 + wave * 32) continue;  // every query precedes every key
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {

@@ -98,17 +98,21 @@ TableEntry get_table(const std::vector<const TensorList*>& lists) {
       words.push_back(reinterpret_cast<int64_t>((*lists[d])[keep[k]].data_ptr()));
 
   std::lock_guard<std::mutex> g(g_cache_mu);
-  for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
-    if (it->key == words) {
-      g_cache.splice(g_cache.begin(), g_cache, it);
-      return g_cache.front();
-    }
-  }
   const auto dev = (*lists[0])[keep.empty() ? 0 : keep[0]].device();
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   const hipStream_t st = c10::hip::getCurrentHIPStream(dev.index()).stream();
   (void)hipStreamIsCapturing(st, &cap);
   const bool capturing = cap == hipStreamCaptureStatusActive;
+  for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
+    if (it->key == words) {
+      // a captured kernel now reads this device table on every replay: it must
+      // never be evicted (eviction frees it to the caching allocator, and a
+      // later replay would read whatever reused the memory)
+      if (capturing) it->persistent = true;
+      g_cache.splice(g_cache.begin(), g_cache, it);
+      return g_cache.front();
+    }
+  }
   at::Tensor host;
   void* src = nullptr;
   if (capturing) {
