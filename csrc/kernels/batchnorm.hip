@@ -25,6 +25,8 @@
 // ResNet-50 configs (SURVEY §2f P1 "BN2d fwd/bwd + ReLU fused").
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "bn_kernels.h"
 
 namespace dcp {
@@ -93,6 +95,7 @@ struct Geo {
 // ≤ 32 threads per row: a wide-C layer is split into channel chunks (grid.y)
 // so the grid fills the chip with few row slabs (few atomics).
 constexpr int kMaxTpr = 32;
+constexpr int kU = 8;  // bn_stats_kernel rows in flight per thread
 
 __device__ __forceinline__ Geo geo(int C) {
   Geo g;
@@ -150,13 +153,14 @@ __global__ void __launch_bounds__(kT) bn_stats_kernel(const void* __restrict__ x
   if (cv_ok) {
     V8<D>::ld(x, static_cast<int64_t>(cvec) * kV, sh);  // shift = row 0
     int64_t r = r0 + grp;
-    // four rows in flight per iteration
-    for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) {
-      float v[4][kV];
+    // kU rows (kU x 16 B per thread) in flight per iteration: the grid is kept
+    // small (few same-address atomics), so each thread must cover the latency
+    for (; r + (kU - 1) * g.rpi < r1; r += kU * g.rpi) {
+      float v[kU][kV];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) V8<D>::ld(x, (r + u * g.rpi) * C + cvec * kV, v[u]);
+      for (int u = 0; u < kU; ++u) V8<D>::ld(x, (r + u * g.rpi) * C + cvec * kV, v[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < kU; ++u)
 #pragma unroll
         for (int k = 0; k < kV; ++k) {
           const float d = v[u][k] - sh[k];
@@ -226,15 +230,17 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
   const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
   const int c0 = static_cast<int>(tid % cv) * kV;
-  float sc[kV], sf[kV];
-#pragma unroll
-  for (int k = 0; k < kV; ++k) {
-    const int c = c0 + k;
+  // per-channel coefficients once per workgroup into LDS with coalesced loads
+  // (8 strided scalar loads per thread and array made the prologue TA-bound:
+  // ~13 µs of every small-shape launch)
+  extern __shared__ __attribute__((aligned(16))) float cf[];  // [2][C]: scale, shift
+  for (int c = threadIdx.x; c < C; c += kT) {
+    float a, b;
     if (TRAIN) {
       float mean, var, inv;
       stats_for<D>(acc, x, M, C, c, eps, &mean, &var, &inv, zshift);
-      coef(gamma, beta, c, mean, inv, &sc[k], &sf[k]);
-      if (tid < cv) {  // one writer per channel
+      coef(gamma, beta, c, mean, inv, &a, &b);
+      if (blockIdx.x == 0) {  // one writer per channel
         mean_out[c] = mean;
         invstd_out[c] = inv;
         if (running_mean) {
@@ -244,9 +250,18 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
         }
       }
     } else {
-      sc[k] = scale_in[c];
-      sf[k] = shift_in[c];
+      a = scale_in[c];
+      b = shift_in[c];
     }
+    cf[c] = a;
+    cf[C + c] = b;
+  }
+  __syncthreads();
+  float sc[kV], sf[kV];
+#pragma unroll
+  for (int k = 0; k < kV; ++k) {
+    sc[k] = cf[c0 + k];
+    sf[k] = cf[C + c0 + k];
   }
   if (TRAIN && nbt && tid == 0) *nbt += 1;  // num_batches_tracked (saves an ATen add launch per BN)
   // two vectors per thread per iteration: twice the loads in flight
@@ -355,23 +370,12 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
       mu[k] = mean[cvec * kV + k];
       if (MX) coef(gamma, beta, cvec * kV + k, mu[k], invstd[cvec * kV + k], &sc[k], &sf[k]);
     }
-#pragma unroll 2
-    for (int64_t r = r0 + grp; r < r1; r += g.rpi) {
-      const int64_t off = r * C + cvec * kV;
-      float gv[kV], xv[kV];
-      V8<D>::ld(gy, off, gv);
-      if (GY2) {
-        float g2[kV];
-        V8<D>::ld(gy2, off, g2);
-#pragma unroll
-        for (int k = 0; k < kV; ++k) gv[k] += g2[k];
-      }
-      V8<D>::ld(x, off, xv);
+    // one row: loads already issued (gv = gy (+gy2 after the add), xv, mb)
+    auto row = [&](int64_t off, float (&gv)[kV], const float (&xv)[kV], uint32_t mb) {
       if (ACT && MX) {
 #pragma unroll
         for (int k = 0; k < kV; ++k) gv[k] = fmaf(xv[k], sc[k], sf[k]) > 0.f ? gv[k] : 0.f;
       } else if (ACT && mbits) {  // forward's 1-bit ReLU mask (1 B per 8 channels)
-        const uint32_t mb = mbits[off / kV];
 #pragma unroll
         for (int k = 0; k < kV; ++k) gv[k] = (mb >> k) & 1u ? gv[k] : 0.f;
       } else if (ACT) {
@@ -386,6 +390,42 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
         sb[k] += gv[k];
         sg[k] = fmaf(gv[k], xv[k] - mu[k], sg[k]);
       }
+    };
+    constexpr int kR = GY2 ? 2 : 4;  // rows in flight per thread (2-3 operands each)
+    const bool rdm = ACT && !MX && mbits;
+    int64_t r = r0 + grp;
+    for (; r + (kR - 1) * g.rpi < r1; r += kR * g.rpi) {
+      float gv[kR][kV], g2[kR][kV], xv[kR][kV];
+      uint32_t mb[kR];
+#pragma unroll
+      for (int u = 0; u < kR; ++u) {
+        const int64_t off = (r + u * g.rpi) * C + cvec * kV;
+        V8<D>::ld(gy, off, gv[u]);
+        if (GY2) V8<D>::ld(gy2, off, g2[u]);
+        V8<D>::ld(x, off, xv[u]);
+        mb[u] = rdm ? mbits[off / kV] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kR; ++u) {
+        if (GY2) {
+#pragma unroll
+          for (int k = 0; k < kV; ++k) gv[u][k] += g2[u][k];
+        }
+        row((r + u * g.rpi) * C + cvec * kV, gv[u], xv[u], mb[u]);
+      }
+    }
+    for (; r < r1; r += g.rpi) {
+      const int64_t off = r * C + cvec * kV;
+      float gv[kV], xv[kV];
+      V8<D>::ld(gy, off, gv);
+      if (GY2) {
+        float g2[kV];
+        V8<D>::ld(gy2, off, g2);
+#pragma unroll
+        for (int k = 0; k < kV; ++k) gv[k] += g2[k];
+      }
+      V8<D>::ld(x, off, xv);
+      row(off, gv, xv, rdm ? mbits[off / kV] : 0u);
     }
   }
   block_reduce_atomic(sb, sg, g, chunk * g.tpr, C, acc, smem);
@@ -410,20 +450,34 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict
   const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
   const int c0 = static_cast<int>(tid % cv) * kV;
+  constexpr bool kMX = ACT && !FROM_G && MX;
+  // coefficients through LDS, as in bn_apply_kernel: [k1, k2, k3, mean (, sc, sf)][C]
+  extern __shared__ __attribute__((aligned(16))) float cf[];
+  for (int c = threadIdx.x; c < C; c += kT) {
+    const float inv = invstd[c];
+    const float sb = acc[c], sg = acc[C + c];
+    const float m = mean[c];
+    cf[c] = (gamma ? gamma[c] : 1.f) * inv;
+    cf[C + c] = training ? sb / static_cast<float>(M) : 0.f;
+    cf[2 * C + c] = training ? sg / static_cast<float>(M) * inv * inv : 0.f;
+    cf[3 * C + c] = m;
+    if (kMX) coef(gamma, beta, c, m, inv, &cf[4 * C + c], &cf[5 * C + c]);
+    if (blockIdx.x == 0) {
+      if (dgamma) dgamma[c] = sg * inv;
+      if (dbeta) dbeta[c] = sb;
+    }
+  }
+  __syncthreads();
   float k1[kV], k2[kV], k3[kV], mu[kV], sc[kV], sf[kV];
 #pragma unroll
   for (int k = 0; k < kV; ++k) {
-    const int c = c0 + k;
-    const float inv = invstd[c];
-    const float sb = acc[c], sg = acc[C + c];
-    mu[k] = mean[c];
-    if (ACT && !FROM_G && MX) coef(gamma, beta, c, mu[k], inv, &sc[k], &sf[k]);
-    k1[k] = (gamma ? gamma[c] : 1.f) * inv;
-    k2[k] = training ? sb / static_cast<float>(M) : 0.f;
-    k3[k] = training ? sg / static_cast<float>(M) * inv * inv : 0.f;
-    if (tid < cv) {
-      if (dgamma) dgamma[c] = sg * inv;
-      if (dbeta) dbeta[c] = sb;
+    k1[k] = cf[c0 + k];
+    k2[k] = cf[C + c0 + k];
+    k3[k] = cf[2 * C + c0 + k];
+    mu[k] = cf[3 * C + c0 + k];
+    if (kMX) {
+      sc[k] = cf[4 * C + c0 + k];
+      sf[k] = cf[5 * C + c0 + k];
     }
   }
   auto one = [&](float (&gv)[kV], const float (&xv)[kV], const float (&yv)[kV]) {
@@ -464,17 +518,32 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict
   }
 }
 
-// grid for the reduction kernels: ~2048 workgroups over (row slabs × channel
-// chunks), ≥ 4 row iterations per thread, ≤ ~256K column atomics per launch.
-inline void red_geometry(int64_t M, int C, int* nblk, int64_t* rows_per_blk, int* nchunks) {
+// grid for the reduction kernels: ≤ 2048 workgroups over (row slabs × channel
+// chunks), ≥ kU row iterations per thread, ≤ ~256K column atomics per launch.
+// tunables (env, read once): total workgroups and column atomics per launch
+inline int64_t env_or(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  return v ? atoll(v) : dflt;
+}
+inline void red_geometry(int64_t M, int C, int* nblk, int64_t* rows_per_blk, int* nchunks, bool bwd = false) {
+  static const int64_t kBlkCap = env_or("DCP_BN_RED_BLOCKS", 2048);
+  static const int64_t kAtomicCap = env_or("DCP_BN_RED_ATOMICS", int64_t(128) << 10);
+  // row slabs = fp32 atomic adds landing on each accumulator address: same-
+  // address atomics serialise, so this caps the contention (measured on the
+  // ResNet-50 shapes, tools/bn_sweep.py)
+  // ResNet-50 b256 sweep: statistics best at 256 slabs, the 2-3 operand
+  // backward reduce at 512 on the large (≥ 2^19-row) shapes
+  static const int64_t kRowCapEnv = env_or("DCP_BN_RED_ROWBLK", 0);
+  const int64_t kRowCap = kRowCapEnv > 0 ? kRowCapEnv : (bwd && M >= (int64_t(1) << 19) ? 512 : 256);
   const int cv = C / kV;
   const int tpr = cv < kMaxTpr ? cv : kMaxTpr;
   const int rpi = kT / tpr;
   *nchunks = (cv + tpr - 1) / tpr;
-  int64_t want = (M + static_cast<int64_t>(rpi) * 4 - 1) / (static_cast<int64_t>(rpi) * 4);
-  int64_t cap = 2048 / *nchunks;
-  const int64_t atomic_cap = (int64_t(128) << 10) / C;
+  int64_t want = (M + static_cast<int64_t>(rpi) * kU - 1) / (static_cast<int64_t>(rpi) * kU);
+  int64_t cap = kBlkCap / *nchunks;
+  const int64_t atomic_cap = kAtomicCap / C;
   if (cap > atomic_cap) cap = atomic_cap;
+  if (cap > kRowCap) cap = kRowCap;
   if (cap < 1) cap = 1;
   if (want > cap) want = cap;
   if (want < 1) want = 1;
@@ -511,7 +580,7 @@ bool bn_supported(int C) {
   if (C % kV != 0) return false;
   const bool red_ok = cv <= kMaxTpr ? (kT % cv == 0) : (cv % kMaxTpr == 0);
   const bool app_ok = cv <= kT ? (kT % cv == 0) : (cv % kT == 0);
-  return red_ok && app_ok;
+  return red_ok && app_ok && C <= 4096;  // apply kernels stage ≤ 6·C fp32 coefficients in LDS
 }
 
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
@@ -532,8 +601,9 @@ void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_
   const int zs = acc_ready ? 1 : 0;
   const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
+  const size_t asm_ = sizeof(float) * 2 * C;
 #define DCP_BN_APPLY(D, R, A)                                                                                     \
-  hipLaunchKernelGGL((bn_apply_kernel<D, R, A, true>), dim3(grid), dim3(kT), 0, s, x, res, acc, gamma, beta,      \
+  hipLaunchKernelGGL((bn_apply_kernel<D, R, A, true>), dim3(grid), dim3(kT), asm_, s, x, res, acc, gamma, beta,   \
                      nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M, nvec, C, nbt, \
                      mbits, zs)
   const bool r = res != nullptr;
@@ -555,8 +625,9 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
               const float* shift, bool act, hipStream_t s) {
   const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
+  const size_t asm_ = sizeof(float) * 2 * C;
 #define DCP_BN_APPLY(D, R, A)                                                                                  \
-  hipLaunchKernelGGL((bn_apply_kernel<D, R, A, false>), dim3(grid), dim3(kT), 0, s, x, res, nullptr, nullptr, \
+  hipLaunchKernelGGL((bn_apply_kernel<D, R, A, false>), dim3(grid), dim3(kT), asm_, s, x, res, nullptr, nullptr, \
                      nullptr, scale, shift, y, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, M, nvec, C, nullptr, \
                      nullptr, 0)
   const bool r = res != nullptr;
@@ -600,7 +671,7 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
                  hipStream_t s) {
   int nblk, nchunks;
   int64_t rpb;
-  red_geometry(M, C, &nblk, &rpb, &nchunks);
+  red_geometry(M, C, &nblk, &rpb, &nchunks, true);
   const size_t sm = red_smem(C);
 #define DCP_BN_RED(D, A, G)                                                                                 \
   do {                                                                                                        \
@@ -640,13 +711,14 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
   const int grid = apply_grid(nvec, C / kV);
   // g source: the stored masked gradient when available, else recompute the mask
   const void* gsrc = store_g ? gout : gy;
+  auto bsm = [C](bool mx) { return sizeof(float) * (mx ? 6 : 4) * C; };
 #define DCP_BN_BAPPLY(D, A, F)                                                                                  \
   do {                                                                                                          \
     if (training)                                                                                               \
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F, true>), dim3(grid), dim3(kT), 0, s, gsrc, y, x, mean, invstd, \
-                         gamma, beta, acc, dgamma, dbeta, training, dx, M, nvec, C);                           \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F, true>), dim3(grid), dim3(kT), bsm(A && !F), s, gsrc, y, x, mean, \
+                         invstd, gamma, beta, acc, dgamma, dbeta, training, dx, M, nvec, C);                   \
     else                                                                                                        \
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F, false>), dim3(grid), dim3(kT), 0, s, gsrc, y, x, mean,   \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F, false>), dim3(grid), dim3(kT), bsm(false), s, gsrc, y, x, mean, \
                          invstd, gamma, beta, acc, dgamma, dbeta, training, dx, M, nvec, C);                   \
   } while (0)
   if (dtype == BN_BF16) {

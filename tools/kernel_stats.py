@@ -10,18 +10,34 @@ import sqlite3
 from collections import defaultdict
 
 
+def short(name):
+    """kernel name without its parameter list (template arguments kept)"""
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "", 1)
+    depth = 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0 and i > 0:
+            return name[:i]
+    return name
+
+
 def rows(path, grid):
     if path.endswith(".db"):
         con = sqlite3.connect(path)
         cols = [r[1] for r in con.execute("pragma table_info(kernels)")]
-        gsel = ", grid_size_x, grid_size_y, grid_size_z" if grid and "grid_size_x" in cols else ""
+        gcols = [c for c in cols if "grid" in c.lower()][:3] if grid else []
+        gsel = "".join(", " + c for c in gcols)
         for rec in con.execute(f"select name, start, end{gsel} from kernels"):
-            yield (rec[0] + (f" grid={rec[3]}x{rec[4]}x{rec[5]}" if gsel else ""), rec[2] - rec[1])
+            yield (("grid=" + "x".join(str(v) for v in rec[3:]) + " " if gcols else "") + short(rec[0]),
+                   rec[2] - rec[1])
     else:
         for r in csv.DictReader(open(path)):
             n = r["Kernel_Name"]
             if grid:
-                n += f" grid={r.get('Grid_Size_X')}x{r.get('Grid_Size_Y')}x{r.get('Grid_Size_Z')}"
+                n = f"grid={r.get('Grid_Size_X')}x{r.get('Grid_Size_Y')}x{r.get('Grid_Size_Z')} " + short(n)
             yield n, int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
 
 
