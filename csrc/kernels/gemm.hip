@@ -21,8 +21,8 @@
 //   MFMA operands swapped (W fragment as A, X fragment as B) so each lane's
 //   accumulator holds 4 consecutive output channels of one row: the epilogue
 //   stores 8-B packed bf16 straight from registers (no LDS round trip).
-//   Persistent over M tiles; grid.x a multiple of 8 so all N-tiles of an
-//   M-tile run on one XCD and share A through its L2.
+//   1-D grid, XCD-remapped tile ids so all N-tiles of an M-tile run on one
+//   XCD and share A through its L2; persistent when tiles exceed 512.
 // gemm_wgrad_kernel D[N1,N2] = Σ_m A[m,:]^T ⊗ f(B)[m,:]  (reduction over M)
 //   stage = [32 m][channels] row-major as in HBM; operands (k = m) read with
 //   ds_read_b64_tr_b16 (gfx950 hardware transpose). Split over M into fp32
@@ -104,10 +104,15 @@ __device__ __forceinline__ bf16x8 bn_act_frag(bf16x8 v, const float (&sc)[8], co
 }
 
 // ---------------------------------------------------------------- NT ----
-// Stage image: [rows][32 k] bf16, 64-B rows; physical 16-B chunk pc of row r
-// holds logical chunk pc ^ ((r>>2)&3): the 16 rows one ds_read_b128 group
-// reads at a fixed logical chunk land on 16 distinct bank slots.
-__device__ __forceinline__ int nt_swz(int r) { return (r >> 2) & 3; }
+// Stage image: [rows][32 k] bf16, 64-B rows (4 rows per 256-B bank row);
+// physical 16-B chunk pc of row r holds logical chunk pc ^ f(r). A fragment
+// read (lane: row lane&15, chunk lane>>4) is split by ds_read_b128 into four
+// 16-lane groups — lanes {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same
+// +32 — each conflict-free iff its lanes hit 16 distinct (r&3, pc) slots. With
+// g = (r>>2)&3 that needs {f0, f3, 1^f1, 1^f2} and {f1, f2, 1^f0, 1^f3} each
+// distinct: f = 0,0,2,2 (bit 3 of the row → chunk bit 1). The previous
+// (r>>2)&3 was 2-way on every group (SQ_LDS_BANK_CONFLICT = ½ of LDS cycles).
+__device__ __forceinline__ int nt_swz(int r) { return ((r >> 3) & 1) << 1; }
 
 constexpr int kNSnt = 3;  // NT ring stages (leaves LDS for the per-wave C staging at 2 blocks/CU)
 
@@ -116,7 +121,7 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
                                                      uint16_t* __restrict__ C, int64_t M, int N, int K,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int relu,
-                                                     float* __restrict__ stats, int tiles_m) {
+                                                     float* __restrict__ stats, int tiles_m, int tn) {
   constexpr int SA = BM * 64, SB = BN * 64, STAGE = SA + SB;  // bytes
   constexpr int NA = SA / 4096, NB = SB / 4096;                // glds per wave per stage (1 KiB each)
   constexpr int G = NA + NB;
@@ -134,10 +139,19 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int n0 = blockIdx.y * BN;
+  // 1-D grid of P workgroups over tiles_m × tn tiles (tile v = m-tile v/tn,
+  // n-tile v%tn). Workgroup id → tile id through the bijective XCD remap:
+  // dispatch puts workgroup w on XCD w%8, the remap hands each XCD a
+  // contiguous tile range, so the tn n-tiles of an m-tile run on one XCD and
+  // share A through its L2. Persistent when tiles > P: tile v, v+P, … (P % tn
+  // == 0 keeps the block's n-tile — and its STATS channels — fixed).
+  const int P = static_cast<int>(gridDim.x);
+  const int wid = static_cast<int>(blockIdx.x);
+  const int xcd = wid & 7, q8 = P >> 3, r8 = P & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
+  const int n0 = (wg % tn) * BN;
   const int KT = K / kBK;
-  const int my_tiles = (tiles_m - static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) - 1) /
-                       static_cast<int>(gridDim.x);
+  const int my_tiles = (tiles_m * tn - wg + P - 1) / P;
   const int T = my_tiles * KT;  // stages this block streams
   char* cst = cst_all + wave * CST;
 
@@ -149,26 +163,44 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
     __syncthreads();
   }
 
-  // DMA issue for stage q into ring slot q % kNSnt
-  auto issue = [&](int q) {
-    if (q >= T) return;
-    const int tile = static_cast<int>(blockIdx.x) + (q / KT) * static_cast<int>(gridDim.x);
-    const int k0 = (q % KT) * kBK;
-    const int64_t m0 = static_cast<int64_t>(tile) * BM;
-    char* base = lds + (q % kNSnt) * STAGE;
+  // DMA issue position (stage count, k-step, ring slot, tile id) advanced
+  // incrementally — per-stage divisions by the runtime KT/tn cost ~100 SALU
+  // instructions per stage, more issue time than the stage's 16 MFMAs.
+  int is_n = 0, is_kt = 0, is_slot = 0, is_v = wg;
+  const uint16_t* asrc[NA];
+  const uint16_t* bsrc[NB];
+  auto set_a = [&](int v) {
+    const int64_t m0 = static_cast<int64_t>(v / tn) * BM;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int p = (wave * NA + j) * 64 + lane;  // 16-B unit in the A image
       const int r = p >> 2, lc = (p & 3) ^ nt_swz(p >> 2);
       int64_t gm = m0 + r;
       gm = gm < M ? gm : M - 1;
-      glds16(A + gm * K + k0 + lc * 8, base + (wave * NA + j) * 1024);
+      asrc[j] = A + gm * K + lc * 8;
     }
+  };
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int p = (wave * NB + j) * 64 + lane;
-      const int r = p >> 2, lc = (p & 3) ^ nt_swz(p >> 2);
-      glds16(B + static_cast<int64_t>(n0 + r) * K + k0 + lc * 8, base + SA + (wave * NB + j) * 1024);
+  for (int j = 0; j < NB; ++j) {
+    const int p = (wave * NB + j) * 64 + lane;
+    const int r = p >> 2, lc = (p & 3) ^ nt_swz(p >> 2);
+    bsrc[j] = B + static_cast<int64_t>(n0 + r) * K + lc * 8;
+  }
+  set_a(wg);
+  auto issue = [&]() {
+    if (is_n >= T) return;
+    char* base = lds + is_slot * STAGE;
+    const int k0 = is_kt * kBK;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) glds16(asrc[j] + k0, base + (wave * NA + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) glds16(bsrc[j] + k0, base + SA + (wave * NB + j) * 1024);
+    ++is_n;
+    is_slot = is_slot + 1 == kNSnt ? 0 : is_slot + 1;
+    if (++is_kt == KT) {
+      is_kt = 0;
+      is_v += P;
+      if (is_n < T) set_a(is_v);
     }
   };
 
@@ -183,17 +215,19 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
   for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
 
 #pragma unroll
-  for (int q = 0; q < kNSnt - 1; ++q) issue(q);
+  for (int q = 0; q < kNSnt - 1; ++q) issue();
 
   const int ck = lane >> 4;  // logical 16-B chunk (k = 8ck … 8ck+7) this lane reads
+  int kt = 0, slot = 0, cv = wg;  // consumer k-step, ring slot, tile id
   for (int q = 0; q < T; ++q) {
     // vmcnt retires in issue order: the ops younger than stage q's DMA are the
     // DMA of q+1 and the epilogue stores of a tile end at q-2 or q-1 (issued
     // after q's DMA) — counting them keeps the ring full across tile ends.
+    // Stage q-d ended a tile iff kt == d-1 (KT ≥ 2 > kNSnt-2).
     if (q + kNSnt - 2 < T) {
       int ends = 0;
 #pragma unroll
-      for (int d = 1; d <= kNSnt - 1; ++d) ends += (q - d >= 0 && (q - d) % KT == KT - 1) ? 1 : 0;
+      for (int d = 1; d <= kNSnt - 1; ++d) ends += (q >= d && kt == d - 1) ? 1 : 0;
       if (ends == 0) wait_vm<(kNSnt - 2) * G>();
       else if (ends == 1) wait_vm<(kNSnt - 2) * G + FS>();
       else wait_vm<(kNSnt - 2) * G + 2 * FS>();
@@ -201,10 +235,9 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
       wait_vm<0>();
     }
     barrier();  // stage q visible to all waves; all reads of slot (q-1)%kNSnt done
-    issue(q + kNSnt - 1);
-    const char* sA = lds + (q % kNSnt) * STAGE;
+    issue();
+    const char* sA = lds + slot * STAGE;
     const char* sB = sA + SA;
-    const int kt = q % KT;
     bf16x8 xf[FM], wf[FN];
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
@@ -239,8 +272,7 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
       // writes into this wave's LDS staging → 16-B row-contiguous reads →
       // global stores covering whole 128-B lines (no cross-wave sync needed:
       // a wave's LDS ops execute in order).
-      const int64_t mt = static_cast<int64_t>(static_cast<int>(blockIdx.x) + (q / KT) * static_cast<int>(gridDim.x)) *
-                         BM + wm * (BM / 2);
+      const int64_t mt = static_cast<int64_t>(cv / tn) * BM + wm * (BM / 2);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -278,6 +310,11 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
           }
         }
       }
+    }
+    slot = slot + 1 == kNSnt ? 0 : slot + 1;
+    if (++kt == KT) {
+      kt = 0;
+      cv += P;
     }
   }
   if (STATS) {
@@ -607,11 +644,12 @@ void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
   constexpr int BM = 128;
   const int tiles_m = static_cast<int>((M + BM - 1) / BM);
   const int tn = N / BN;
-  // persistent over M tiles: ~2 workgroups per CU, grid.x a multiple of 8 (XCD-aligned N-tiles)
-  int gx = (512 / tn) & ~7;
-  if (gx < 8) gx = 8;
-  if (gx > tiles_m) gx = tiles_m;
-  const dim3 grid(gx, tn);
+  // all tiles resident at once when they fit (2 workgroups per CU), else
+  // persistent over ≤ 512 workgroups (a multiple of tn, see the kernel)
+  const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
+  int P = tiles <= 512 ? static_cast<int>(tiles) : (512 / tn) * tn;
+  if (P < tn) P = tn;
+  const dim3 grid(P);
   const bool pro = scale != nullptr;
   const bool st = stats != nullptr;
   // ring + per-wave C staging (4 × 32 rows × BN/2) + BN coefficients
@@ -621,7 +659,7 @@ void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
   auto c = static_cast<uint16_t*>(C);
 #define DCP_GNT(BN_, P, S_)                                                                                      \
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P, S_>), grid, dim3(kT), lds, s, a, b, c, M, N, K, scale, shift, \
-                     relu ? 1 : 0, stats, tiles_m)
+                     relu ? 1 : 0, stats, tiles_m, tn)
   if (BN == 128) {
     if (pro && st) DCP_GNT(128, true, true);
     else if (pro) DCP_GNT(128, true, false);

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--no3x3", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.backends.cudnn.benchmark = True
@@ -62,6 +63,8 @@ def main():
         ours = {
             "fwd": lambda: _C.conv1x1_fwd(x, w, None, None, False, False),
             "fwd+bnrelu+stats": lambda: _C.conv1x1_fwd(x, w, sc, sf, True, True),
+            "fwd+stats": lambda: _C.conv1x1_fwd(x, w, None, None, False, True),
+            "fwd+bnrelu": lambda: _C.conv1x1_fwd(x, w, sc, sf, True, False),
             "dgrad": lambda: _C.conv1x1_dgrad(gy, wt),
             "wgrad": lambda: _C.conv1x1_wgrad(gy, x),
         }
@@ -85,7 +88,7 @@ def main():
         rows.append(res)
         print(json.dumps(res), flush=True)
     # 3x3 weight gradients (ResNet-50 conv2 layers): gathered implicit GEMM vs MIOpen
-    for hw, c, st in [(56, 64, 1), (56, 128, 2), (28, 128, 1), (28, 256, 2), (14, 256, 1), (14, 512, 2), (7, 512, 1)]:
+    for hw, c, st in [] if a.no3x3 else [(56, 64, 1), (56, 128, 2), (28, 128, 1), (28, 256, 2), (14, 256, 1), (14, 512, 2), (7, 512, 1)]:
         ho = (hw + 2 - 3) // st + 1
         x = torch.randn(a.batch, c, hw, hw, device=dev).to(bf).contiguous(memory_format=cl)
         gy = torch.randn(a.batch, c, ho, ho, device=dev).to(bf).contiguous(memory_format=cl)

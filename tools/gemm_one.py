@@ -1,0 +1,44 @@
+"""One 1x1-conv GEMM shape, repeated (a small target for rocprofv3 --pmc).
+
+    python tools/gemm_one.py --m 12544 --cin 2048 --cout 512 --op fwd [--iters 10]
+op: fwd | fwd_pro | dgrad | wgrad
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import distributed_compute_pytorch_amd  # noqa: E402,F401
+from distributed_compute_pytorch_amd._ext import C as _C  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=12544)
+    ap.add_argument("--cin", type=int, default=2048)
+    ap.add_argument("--cout", type=int, default=512)
+    ap.add_argument("--op", default="fwd")
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    bf = torch.bfloat16
+    x = torch.randn(1, a.cin, a.m, 1, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(1, a.cout, a.m, 1, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(a.cout, a.cin, device=dev) / a.cin ** 0.5).to(bf)
+    wt = w.t().contiguous()
+    sc, sf = torch.ones(a.cin, device=dev), torch.zeros(a.cin, device=dev)
+    fn = {"fwd": lambda: _C.conv1x1_fwd(x, w, None, None, False, False),
+          "fwd_pro": lambda: _C.conv1x1_fwd(x, w, sc, sf, True, False),
+          "dgrad": lambda: _C.conv1x1_dgrad(gy, wt),
+          "wgrad": lambda: _C.conv1x1_wgrad(gy, x)}[a.op]
+    for _ in range(a.iters):
+        fn()
+    torch.cuda.synchronize()
+    print("ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()
