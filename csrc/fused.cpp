@@ -151,7 +151,8 @@ std::vector<at::Tensor> bn_stats_coef(const at::Tensor& x, const c10::optional<a
                                       const c10::optional<at::Tensor>& bias,
                                       const c10::optional<at::Tensor>& running_mean,
                                       const c10::optional<at::Tensor>& running_var, double momentum, double eps,
-                                      const c10::optional<at::Tensor>& num_batches_tracked) {
+                                      const c10::optional<at::Tensor>& num_batches_tracked,
+                                      const c10::optional<at::Tensor>& sums) {
   check_nhwc(x, "bn_stats_coef");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t C = x.size(1);
@@ -159,7 +160,11 @@ std::vector<at::Tensor> bn_stats_coef(const at::Tensor& x, const c10::optional<a
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor out = at::empty({4, C}, fopt);
   auto s = stream_of(x);
-  at::Tensor acc = zeroed_floats(2 * C, x, s);
+  const bool ready = sums.has_value() && sums->defined();
+  if (ready)
+    DCP_CHECK(sums->is_cuda() && sums->scalar_type() == at::kFloat && sums->is_contiguous() && sums->numel() == 2 * C,
+              "bn_stats_coef: sums must be fp32 [2*C]");
+  at::Tensor acc = ready ? *sums : zeroed_floats(2 * C, x, s);
   at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor b = bias.has_value() && bias->defined() ? bias->to(at::kFloat).contiguous() : at::Tensor();
   kern::bn_stats_coef(bn_dtype(x), x.data_ptr(), M, static_cast<int>(C), w.defined() ? w.data_ptr<float>() : nullptr,
@@ -172,7 +177,7 @@ std::vector<at::Tensor> bn_stats_coef(const at::Tensor& x, const c10::optional<a
                       num_batches_tracked.has_value() && num_batches_tracked->defined()
                           ? num_batches_tracked->data_ptr<int64_t>()
                           : nullptr,
-                      s);
+                      s, ready);
   return {out[0], out[1], out[2], out[3]};
 }
 
@@ -300,6 +305,34 @@ at::Tensor conv_wgrad(const at::Tensor& gy, const at::Tensor& x, int64_t kh, int
                         static_cast<int>(Cout), static_cast<int>(kh), static_cast<int>(kw), static_cast<int>(stride),
                         static_cast<int>(pad), zero_row(gy).data_ptr(), ws.data_ptr<float>(), stream_of(gy));
   return dw.permute({0, 3, 1, 2});
+}
+
+// y = conv(x, w) for a kh×kw NHWC convolution on the implicit-GEMM MFMA
+// kernel; wt: bf16 [Cout][kh][kw][Cin] contiguous. stats=True also returns the
+// (Σy, Σy²) fp32 [2*Cout] sums of the bf16 output (next BatchNorm).
+std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& wt, int64_t kh, int64_t kw, int64_t stride,
+                                 int64_t pad, bool stats) {
+  check_gemm_act(x, "conv_fwd");
+  DCP_CHECK(x.dim() == 4, "conv_fwd: NHWC 4-D input required");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % (kh * kw * Cin) == 0,
+            "conv_fwd: weight must be contiguous bf16 [Cout][kh][kw][Cin]");
+  const int64_t Cout = wt.numel() / (kh * kw * Cin);
+  DCP_CHECK(kern::conv_fwd_supported(static_cast<int>(Cin), static_cast<int>(Cout), static_cast<int>(kh),
+                                     static_cast<int>(kw)),
+            "conv_fwd: channels must be multiples of 64");
+  const int64_t Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
+  DCP_CHECK(Ho > 0 && Wo > 0 && N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31),
+            "conv_fwd: bad geometry or tensor too large");
+  at::Tensor y = at::empty({N, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto s = stream_of(x);
+  at::Tensor st = stats ? zeroed_floats(2 * Cout, x, s) : at::empty({0}, x.options().dtype(at::kFloat));
+  kern::conv_fwd_bf16(x.data_ptr(), wt.data_ptr(), y.data_ptr(), static_cast<int>(N), static_cast<int>(H),
+                      static_cast<int>(W), static_cast<int>(Cin), static_cast<int>(Ho), static_cast<int>(Wo),
+                      static_cast<int>(Cout), static_cast<int>(kh), static_cast<int>(kw), static_cast<int>(stride),
+                      static_cast<int>(pad), zero_row(x).data_ptr(), stats ? st.data_ptr<float>() : nullptr, s);
+  return {y, st};
 }
 
 // fp32 [N] column sums of a bf16 [.., N] tensor (Linear bias gradient)
@@ -736,7 +769,7 @@ void bind(pybind11::module& m) {
   m.def("bn_stats_coef", &bn_stats_coef, "training BN statistics + folded scale/shift (no apply)",
         pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
         pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"),
-        pybind11::arg("num_batches_tracked") = pybind11::none());
+        pybind11::arg("num_batches_tracked") = pybind11::none(), pybind11::arg("sums") = pybind11::none());
   m.def("conv1x1_supported", &conv1x1_supported);
   m.def("conv1x1_fwd", &conv1x1_fwd, "NHWC 1x1 conv as an MFMA GEMM (+BN-apply prologue, +BN-stats epilogue)",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("scale") = pybind11::none(),
@@ -748,6 +781,9 @@ void bind(pybind11::module& m) {
         pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("heads"), pybind11::arg("causal"),
         pybind11::arg("p_drop"), pybind11::arg("seed"));
   m.def("flash_attn_bwd", &flash_attn_bwd, "MFMA flash attention backward into dq/dk/dv");
+  m.def("conv_fwd", &conv_fwd, "kxk NHWC conv forward (implicit-GEMM MFMA) [+ output BN sums]", pybind11::arg("x"),
+        pybind11::arg("wt"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"), pybind11::arg("pad"),
+        pybind11::arg("stats") = false);
   m.def("conv_wgrad", &conv_wgrad, "kxk NHWC conv weight gradient (implicit-GEMM MFMA, fp32 out)",
         pybind11::arg("gy"), pybind11::arg("x"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"),
         pybind11::arg("pad"));

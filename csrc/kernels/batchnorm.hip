@@ -315,12 +315,12 @@ __global__ void __launch_bounds__(kT) bn_finalize_kernel(const void* __restrict_
                                                          float* __restrict__ invstd_out, float* __restrict__ scale_out,
                                                          float* __restrict__ shift_out, float* running_mean,
                                                          float* running_var, float momentum, float eps, int64_t M,
-                                                         int C, int64_t* __restrict__ nbt) {
+                                                         int C, int64_t* __restrict__ nbt, int zshift) {
   const int c = blockIdx.x * kT + threadIdx.x;
   if (nbt && c == 0) *nbt += 1;
   if (c >= C) return;
   float mean, var, inv, sc, sf;
-  stats_for<D>(acc, x, M, C, c, eps, &mean, &var, &inv);
+  stats_for<D>(acc, x, M, C, c, eps, &mean, &var, &inv, zshift);
   coef(gamma, beta, c, mean, inv, &sc, &sf);
   mean_out[c] = mean;
   invstd_out[c] = inv;
@@ -647,20 +647,23 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 
 void bn_stats_coef(int dtype, const void* x, int64_t M, int C, const float* gamma, const float* beta,
                    float* running_mean, float* running_var, float momentum, float eps, float* mean, float* invstd,
-                   float* scale, float* shift, float* acc, int64_t* nbt, hipStream_t s) {
+                   float* scale, float* shift, float* acc, int64_t* nbt, hipStream_t s, bool acc_ready) {
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
   const size_t sm = red_smem(C);
   const dim3 fg((C + kT - 1) / kT);
+  const int zs = acc_ready ? 1 : 0;  // acc = unshifted sums from the producer's epilogue
   if (dtype == BN_BF16) {
-    hipLaunchKernelGGL(bn_stats_kernel<BN_BF16>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
+    if (!acc_ready)
+      hipLaunchKernelGGL(bn_stats_kernel<BN_BF16>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
     hipLaunchKernelGGL(bn_finalize_kernel<BN_BF16>, fg, dim3(kT), 0, s, x, acc, gamma, beta, mean, invstd, scale,
-                       shift, running_mean, running_var, momentum, eps, M, C, nbt);
+                       shift, running_mean, running_var, momentum, eps, M, C, nbt, zs);
   } else {
-    hipLaunchKernelGGL(bn_stats_kernel<BN_F32>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
+    if (!acc_ready)
+      hipLaunchKernelGGL(bn_stats_kernel<BN_F32>, dim3(nblk, nchunks), dim3(kT), sm, s, x, M, C, rpb, acc);
     hipLaunchKernelGGL(bn_finalize_kernel<BN_F32>, fg, dim3(kT), 0, s, x, acc, gamma, beta, mean, invstd, scale,
-                       shift, running_mean, running_var, momentum, eps, M, C, nbt);
+                       shift, running_mean, running_var, momentum, eps, M, C, nbt, zs);
   }
 }
 

@@ -28,7 +28,7 @@ void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_
 // applies BN+ReLU in its own prologue (gemm.hip). acc: ZEROED [2*C] fp32.
 void bn_stats_coef(int dtype, const void* x, int64_t M, int C, const float* gamma, const float* beta,
                    float* running_mean, float* running_var, float momentum, float eps, float* mean, float* invstd,
-                   float* scale, float* shift, float* acc, int64_t* nbt, hipStream_t s);
+                   float* scale, float* shift, float* acc, int64_t* nbt, hipStream_t s, bool acc_ready = false);
 
 // y = act(x * scale[c] + shift[c] [+ res])
 void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,

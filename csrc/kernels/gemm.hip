@@ -114,14 +114,26 @@ __device__ __forceinline__ bf16x8 bn_act_frag(bf16x8 v, const float (&sc)[8], co
 // (r>>2)&3 was 2-way on every group (SQ_LDS_BANK_CONFLICT = ½ of LDS cycles).
 __device__ __forceinline__ int nt_swz(int r) { return ((r >> 3) & 1) << 1; }
 
+// Convolution geometry of the gathered (implicit-GEMM) kernels. wgrad: B rows
+// are the input pixels under tap (dy, dx) = (blockIdx.z / kw, blockIdx.z % kw)
+// of each output pixel. fwd (gemm_nt GATHER): A row m = output pixel, k =
+// (dy*kw + dx)*cin + c, so a 32-wide k-stage sits inside one tap. Out-of-image
+// taps read a zero row.
+struct ConvGeo {
+  int H, W, Ho, Wo, stride, pad, kw;
+  const uint16_t* zero;  // ≥ 256 zero bytes
+  int cin;               // input channels (gemm_nt GATHER)
+};
+
 constexpr int kNSnt = 3;  // NT ring stages (leaves LDS for the per-wave C staging at 2 blocks/CU)
 
-template <int BM, int BN, bool PRO, bool STATS>
+template <int BM, int BN, bool PRO, bool STATS, bool GATHER>
 __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                      uint16_t* __restrict__ C, int64_t M, int N, int K,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int relu,
-                                                     float* __restrict__ stats, int tiles_m, int tn) {
+                                                     float* __restrict__ stats, int tiles_m, int tn, ConvGeo geo) {
+  static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
   constexpr int SA = BM * 64, SB = BN * 64, STAGE = SA + SB;  // bytes
   constexpr int NA = SA / 4096, NB = SB / 4096;                // glds per wave per stage (1 KiB each)
   constexpr int G = NA + NB;
@@ -167,8 +179,10 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
   // incrementally — per-stage divisions by the runtime KT/tn cost ~100 SALU
   // instructions per stage, more issue time than the stage's 16 MFMAs.
   int is_n = 0, is_kt = 0, is_slot = 0, is_v = wg;
+  int is_c0 = 0, is_dy = 0, is_dx = 0;  // GATHER: channel offset and tap of the issue stage
   const uint16_t* asrc[NA];
   const uint16_t* bsrc[NB];
+  int gnb[NA], ghb[NA], gwb[NA];  // GATHER: n*H, ho*stride-pad, wo*stride-pad of each A row
   auto set_a = [&](int v) {
     const int64_t m0 = static_cast<int64_t>(v / tn) * BM;
 #pragma unroll
@@ -177,7 +191,15 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
       const int r = p >> 2, lc = (p & 3) ^ nt_swz(p >> 2);
       int64_t gm = m0 + r;
       gm = gm < M ? gm : M - 1;
-      asrc[j] = A + gm * K + lc * 8;
+      if (GATHER) {  // once per tile: the per-stage source is then two adds and a bounds test
+        const int mi = static_cast<int>(gm);
+        const int wo = mi % geo.Wo, t1 = mi / geo.Wo;
+        gnb[j] = (t1 / geo.Ho) * geo.H;
+        ghb[j] = (t1 % geo.Ho) * geo.stride - geo.pad;
+        gwb[j] = wo * geo.stride - geo.pad;
+      } else {
+        asrc[j] = A + gm * K + lc * 8;
+      }
     }
   };
 #pragma unroll
@@ -192,14 +214,38 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
     char* base = lds + is_slot * STAGE;
     const int k0 = is_kt * kBK;
 #pragma unroll
-    for (int j = 0; j < NA; ++j) glds16(asrc[j] + k0, base + (wave * NA + j) * 1024);
+    for (int j = 0; j < NA; ++j) {
+      if (GATHER) {
+        const int p = (wave * NA + j) * 64 + lane;
+        const int lc = (p & 3) ^ nt_swz(p >> 2);
+        const int hi = ghb[j] + is_dy, wi = gwb[j] + is_dx;
+        const bool ok = static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
+                        static_cast<unsigned>(wi) < static_cast<unsigned>(geo.W);
+        const uint16_t* src = ok ? A + (static_cast<int64_t>(gnb[j] + hi) * geo.W + wi) * geo.cin + is_c0 + lc * 8
+                                 : geo.zero + lc * 8;
+        glds16(src, base + (wave * NA + j) * 1024);
+      } else {
+        glds16(asrc[j] + k0, base + (wave * NA + j) * 1024);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NB; ++j) glds16(bsrc[j] + k0, base + SA + (wave * NB + j) * 1024);
     ++is_n;
     is_slot = is_slot + 1 == kNSnt ? 0 : is_slot + 1;
+    if (GATHER) {
+      is_c0 += kBK;
+      if (is_c0 == geo.cin) {
+        is_c0 = 0;
+        if (++is_dx == geo.kw) {
+          is_dx = 0;
+          ++is_dy;
+        }
+      }
+    }
     if (++is_kt == KT) {
       is_kt = 0;
       is_v += P;
+      is_c0 = is_dy = is_dx = 0;
       if (is_n < T) set_a(is_v);
     }
   };
@@ -383,14 +429,6 @@ __device__ __forceinline__ bf16x8 mask_rows(bf16x8 v, int valid, int lane) {
   return __builtin_bit_cast(bf16x8, s);
 }
 
-// Convolution geometry for the gathered (implicit-GEMM) wgrad: B rows are the
-// input pixels under tap (dy, dx) = (blockIdx.z / kw, blockIdx.z % kw) of
-// each output pixel; out-of-image taps read a zero row.
-struct ConvGeo {
-  int H, W, Ho, Wo, stride, pad, kw;
-  const uint16_t* zero;  // ≥ 256 zero bytes
-};
-
 template <int BM, int BN, bool PRO, bool GATHER>
 __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                         float* __restrict__ ws, int64_t M, int N1, int N2,
@@ -429,6 +467,23 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
     __builtin_amdgcn_s_waitcnt(0x0F70);
   }
 
+  int g_m[NB], g_n[NB], g_ho[NB], g_wo[NB];  // GATHER: output pixel of each B row at the next issue
+  const int gdy = static_cast<int>(blockIdx.z) / geo.kw - geo.pad;
+  const int gdx = static_cast<int>(blockIdx.z) % geo.kw - geo.pad;
+  const int adv_h = GATHER ? kBK / geo.Wo : 0, adv_w = GATHER ? kBK % geo.Wo : 0;
+  if (GATHER) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int p = (wave * NB + j) * 64 + lane;
+      const int m = static_cast<int>(mz0) + p / BCPR;
+      g_m[j] = m;
+      g_wo[j] = m % geo.Wo;
+      const int t1 = m / geo.Wo;
+      g_ho[j] = t1 % geo.Ho;
+      g_n[j] = t1 / geo.Ho;
+    }
+  }
+
   auto issue = [&](int q) {
     if (q >= T) return;
     const int64_t mb = mz0 + static_cast<int64_t>(q) * kBK;
@@ -448,15 +503,25 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
       const int r = p / BCPR, pc = p % BCPR;
       const int lc = 2 * ((pc >> 1) ^ tr_f<BN>(r)) + (pc & 1);
       if (GATHER) {
-        const int gm = static_cast<int>(mb) + r;  // output pixel
-        const int dy = static_cast<int>(blockIdx.z) / geo.kw, dx = static_cast<int>(blockIdx.z) % geo.kw;
-        const int wo = gm % geo.Wo, t1 = gm / geo.Wo;
-        const int ho = t1 % geo.Ho, n = t1 / geo.Ho;
-        const int hi = ho * geo.stride + dy - geo.pad, wi = wo * geo.stride + dx - geo.pad;
-        const bool ok = gm < mz1 && hi >= 0 && hi < geo.H && wi >= 0 && wi < geo.W;
-        const uint16_t* src = ok ? B + (static_cast<int64_t>(n * geo.H + hi) * geo.W + wi) * N2 + j0 + lc * 8
+        // output pixel g_m[j] = (g_n, g_ho, g_wo), advanced by kBK per stage
+        // without divisions (they cost more VALU than the stage's MFMAs)
+        const int hi = g_ho[j] * geo.stride + gdy, wi = g_wo[j] * geo.stride + gdx;
+        const bool ok = g_m[j] < mz1 && static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
+                        static_cast<unsigned>(wi) < static_cast<unsigned>(geo.W);
+        const uint16_t* src = ok ? B + (static_cast<int64_t>(g_n[j] * geo.H + hi) * geo.W + wi) * N2 + j0 + lc * 8
                                  : geo.zero + lc * 8;
         glds16(src, base + SA + (wave * NB + j) * 1024);
+        g_m[j] += kBK;
+        g_wo[j] += adv_w;
+        g_ho[j] += adv_h;
+        if (g_wo[j] >= geo.Wo) {
+          g_wo[j] -= geo.Wo;
+          ++g_ho[j];
+        }
+        while (g_ho[j] >= geo.Ho) {
+          g_ho[j] -= geo.Ho;
+          ++g_n[j];
+        }
       } else {
         int64_t gm = mb + r;
         gm = gm < mz1 ? gm : mz1 - 1;
@@ -635,11 +700,13 @@ WgradPlan wgrad_plan(int64_t M, int N1, int N2, int taps = 1) {
 }  // namespace
 
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) {
-  return M >= 1 && N > 0 && K > 0 && N % 64 == 0 && K % 64 == 0 && K <= 4096;
+  return M >= 1 && N > 0 && K > 0 && N % 64 == 0 && K % 64 == 0 && K <= 4096;  // ≤ 4096: PRO coefficients in LDS
 }
 
-void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
-                  const float* shift, bool relu, float* stats, hipStream_t s) {
+namespace {
+template <bool GATHER>
+void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                    const float* shift, bool relu, float* stats, const ConvGeo& geo, hipStream_t s) {
   const int BN = N % 128 == 0 ? 128 : 64;
   constexpr int BM = 128;
   const int tiles_m = static_cast<int>((M + BM - 1) / BM);
@@ -657,21 +724,45 @@ void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
-#define DCP_GNT(BN_, P, S_)                                                                                      \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P, S_>), grid, dim3(kT), lds, s, a, b, c, M, N, K, scale, shift, \
-                     relu ? 1 : 0, stats, tiles_m, tn)
-  if (BN == 128) {
-    if (pro && st) DCP_GNT(128, true, true);
-    else if (pro) DCP_GNT(128, true, false);
-    else if (st) DCP_GNT(128, false, true);
-    else DCP_GNT(128, false, false);
-  } else {
-    if (pro && st) DCP_GNT(64, true, true);
-    else if (pro) DCP_GNT(64, true, false);
-    else if (st) DCP_GNT(64, false, true);
-    else DCP_GNT(64, false, false);
-  }
+#define DCP_GNT(BN_, P_, S_)                                                                                      \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P_, S_, GATHER>), grid, dim3(kT), lds, s, a, b, c, M, N, K, scale, \
+                     shift, relu ? 1 : 0, stats, tiles_m, tn, geo)
+#define DCP_GNT2(BN_)                            \
+  do {                                           \
+    if constexpr (!GATHER) {                     \
+      if (pro && st) {                           \
+        DCP_GNT(BN_, true, true);                \
+        break;                                   \
+      }                                          \
+      if (pro) {                                 \
+        DCP_GNT(BN_, true, false);               \
+        break;                                   \
+      }                                          \
+    }                                            \
+    if (st) DCP_GNT(BN_, false, true);           \
+    else DCP_GNT(BN_, false, false);             \
+  } while (0)
+  if (BN == 128) DCP_GNT2(128);
+  else DCP_GNT2(64);
+#undef DCP_GNT2
 #undef DCP_GNT
+}
+}  // namespace
+
+void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                  const float* shift, bool relu, float* stats, hipStream_t s) {
+  gemm_nt_launch<false>(A, B, C, M, N, K, scale, shift, relu, stats, ConvGeo{}, s);
+}
+
+bool conv_fwd_supported(int Cin, int Cout, int kh, int kw) {
+  return Cin % 64 == 0 && Cout % 64 == 0 && kh >= 1 && kw >= 1;
+}
+
+void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                   int kh, int kw, int stride, int pad, const void* zero, float* stats, hipStream_t s) {
+  ConvGeo geo{H, W, Ho, Wo, stride, pad, kw, static_cast<const uint16_t*>(zero), Cin};
+  gemm_nt_launch<true>(X, Wt, Y, static_cast<int64_t>(N) * Ho * Wo, Cout, kh * kw * Cin, nullptr, nullptr, false,
+                       stats, geo, s);
 }
 
 void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s) {

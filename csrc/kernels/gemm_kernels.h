@@ -50,6 +50,15 @@ void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, 
 // Σ_{output pixels} dY[m, :]^T ⊗ X[pixel under tap, :] (zero outside the image).
 // dY [N*Ho*Wo, Cout] bf16, X [N*H*W, Cin] bf16; Cout, Cin multiples of 64;
 // zero: ≥ 256 zeroed bytes; ws: gemm_wgrad_workspace(N*Ho*Wo, Cout, Cin, kh*kw).
+// Implicit-GEMM kh×kw NHWC convolution forward (gemm_nt with a gathered A
+// operand): X [N,H,W,Cin] bf16, Wt [Cout][kh][kw][Cin] bf16 (channels_last
+// weight order), Y [N,Ho,Wo,Cout] bf16; stats (optional, zeroed fp32 [2*Cout])
+// += (Σy, Σy²). zero: ≥ 256 zero bytes (padding taps). Also the stride-1 data
+// gradient, run on dY with the flipped, transposed weight.
+bool conv_fwd_supported(int Cin, int Cout, int kh, int kw);
+void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                   int kh, int kw, int stride, int pad, const void* zero, float* stats, hipStream_t s);
+
 void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                      int kh, int kw, int stride, int pad, const void* zero, float* ws, hipStream_t s);
 

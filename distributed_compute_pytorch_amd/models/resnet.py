@@ -20,12 +20,15 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk, conv_kxk_ok, gemm_ok
+from ..ops.conv import (bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk, conv_kxk_gemm, conv_kxk_gemm_ok,
+                        conv_kxk_ok, gemm_ok, kxk_policy)
 from ..ops.pool import FusedMaxPool2d
 
 
 GEMM_MAX_INTENSITY = float(os.environ.get("DCP_GEMM_MAX_INTENSITY", "1024"))
 KXK_WGRAD = os.environ.get("DCP_KXK_WGRAD", "0") == "1"
+# 3x3 conv2 on the implicit-GEMM MFMA kernels (fwd + BN2 sums, stride-1 dgrad)
+KXK_GEMM = os.environ.get("DCP_KXK_GEMM", "1") == "1"
 # BN-apply prologue in the conv3 GEMM only while Cout ≤ this (≤ 2 N-tiles of 128)
 PRO_MAX_COUT = int(os.environ.get("DCP_PRO_MAX_COUT", "256"))
 
@@ -104,7 +107,15 @@ class Bottleneck(nn.Module):
         c2 = self.conv2
         # opt-in: MIOpen fwd/dgrad + our implicit-GEMM wgrad (ties MIOpen's wrw except at
         # 56x56x64, where it is slower: profiles/r1_gemm1x1_vs_miopen.json "rows3x3")
-        if KXK_WGRAD and conv_kxk_ok(y1, c2):
+        s2 = None
+        if KXK_GEMM and conv_kxk_gemm_ok(y1, c2):
+            ho = (y1.shape[2] + 2 * c2.padding[0] - c2.kernel_size[0]) // c2.stride[0] + 1
+            mi_fwd, mi_wgrad = kxk_policy(c2.in_channels, c2.out_channels, ho, c2.stride[0])
+            x2, s2 = conv_kxk_gemm(y1, c2.weight, c2.stride[0], c2.padding[0], stats=not mi_fwd,
+                                   miopen_wgrad=mi_wgrad, miopen_fwd=mi_fwd)
+            if mi_fwd:
+                s2 = None
+        elif KXK_WGRAD and conv_kxk_ok(y1, c2):
             x2 = conv_kxk(y1, c2.weight, c2.stride[0], c2.padding[0])
         else:
             x2 = c2(y1)
@@ -112,11 +123,11 @@ class Bottleneck(nn.Module):
             x2 = x2.contiguous(memory_format=torch.channels_last)
         if self.conv3.out_channels <= PRO_MAX_COUT:
             # BN2+ReLU applied in the GEMM prologue (its output never hits HBM)
-            z3, s3 = bn_relu_conv1x1(x2, self.bn2, self.conv3.weight, stats=True)
+            z3, s3 = bn_relu_conv1x1(x2, self.bn2, self.conv3.weight, stats=True, sums=s2)
         else:
             # wide conv3: every N-tile re-applies the prologue to the same rows,
             # which costs more than one apply pass over the narrow input
-            z3, s3 = gemm_conv1x1(self.bn2(x2), self.conv3.weight, stats=True)
+            z3, s3 = gemm_conv1x1(self.bn2(x2, stats=s2), self.conv3.weight, stats=True)
         return self.bn3(z3, identity, dual=dual, stats=s3)
 
 

@@ -72,9 +72,10 @@ class _Conv1x1Fn(torch.autograd.Function):
 
 class _BNReluConv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, weight, running_mean, running_var, nbt, momentum, eps, stats):
+    def forward(ctx, x, gamma, beta, weight, running_mean, running_var, nbt, momentum, eps, stats, sums):
+        # sums: (Σx, Σx²) of x from its producer's epilogue (no statistics pass)
         mean, invstd, scale, shift = _C.bn_stats_coef(x, gamma, beta, running_mean, running_var, float(momentum),
-                                                      float(eps), nbt)
+                                                      float(eps), nbt, sums)
         w, wt = _w2d(weight)
         z, st = _C.conv1x1_fwd(x, w, scale, shift, True, bool(stats))
         ctx.save_for_backward(x, gamma, beta, wt, mean, invstd, scale, shift)
@@ -87,7 +88,7 @@ class _BNReluConv1x1Fn(torch.autograd.Function):
     def backward(ctx, gz, _gst):
         x, gamma, beta, wt, mean, invstd, scale, shift = ctx.saved_tensors
         if gz is None:
-            return (None,) * 10
+            return (None,) * 11
         gz = _cl(gz)
         dw = _C.conv1x1_wgrad(gz, x, scale, shift, True).view(ctx.wshape)
         if dw.dtype != ctx.wdtype:
@@ -95,7 +96,7 @@ class _BNReluConv1x1Fn(torch.autograd.Function):
         da = _C.conv1x1_dgrad(gz, wt)
         # BN + ReLU backward; the ReLU mask is recomputed from x (training coefficients)
         dx, dgamma, dbeta, _ = _C.bn_act_bwd(da, None, x, gamma, beta, mean, invstd, x, True, False, True, None)
-        return dx, dgamma, dbeta, dw, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dw, None, None, None, None, None, None, None
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stats: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
@@ -104,15 +105,17 @@ def conv1x1(x: torch.Tensor, weight: torch.Tensor, stats: bool = False) -> Tuple
     return _Conv1x1Fn.apply(x, weight, stats)
 
 
-def bn_relu_conv1x1(x: torch.Tensor, bn, weight: torch.Tensor, stats: bool = False):
+def bn_relu_conv1x1(x: torch.Tensor, bn, weight: torch.Tensor, stats: bool = False,
+                    sums: Optional[torch.Tensor] = None):
     """``conv1x1(relu(bn(x)), weight)`` for a training-mode ``BatchNorm2d``
-    ``bn`` (its running statistics and ``num_batches_tracked`` are updated)."""
+    ``bn`` (its running statistics and ``num_batches_tracked`` are updated).
+    ``sums``: x's (Σx, Σx²) from the producing kernel's epilogue, if any."""
     nbt = bn.num_batches_tracked
     if nbt is not None and (nbt.device != x.device or nbt.dtype != torch.int64):
         nbt.add_(1)
         nbt = None
     return _BNReluConv1x1Fn.apply(x, bn.weight, bn.bias, weight, bn.running_mean, bn.running_var, nbt, bn.momentum,
-                                  bn.eps, stats)
+                                  bn.eps, stats, sums)
 
 
 class _ConvKxKFn(torch.autograd.Function):
@@ -148,6 +151,76 @@ def conv_kxk(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -
     """NHWC bf16 kxk convolution (no bias, square stride/padding) whose weight
     gradient runs on the gathered MFMA wgrad kernel."""
     return _ConvKxKFn.apply(x, weight, stride, padding)
+
+
+class _ConvKxKGemmFn(torch.autograd.Function):
+    """kxk NHWC convolution on the implicit-GEMM MFMA kernels (gemm.hip
+    GATHER): forward (+ the next BatchNorm's Σy, Σy² from the epilogue), data
+    gradient for stride 1 as the forward kernel on gy with the flipped,
+    transposed weight (MIOpen for stride > 1), weight gradient on the gathered
+    wgrad kernel (or MIOpen when ``miopen_wgrad``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding, stats, miopen_wgrad, miopen_fwd):
+        ctx.set_materialize_grads(False)
+        w = weight.detach().to(torch.bfloat16)
+        kh, kw = w.shape[2], w.shape[3]
+        if miopen_fwd:  # the caller computes the output statistics itself
+            y = _cl(F.conv2d(x, w, None, stride, padding))
+            st = torch.empty(0, device=x.device, dtype=torch.float32)
+        else:
+            y, st = _C.conv_fwd(x, w.permute(0, 2, 3, 1).contiguous(), kh, kw, stride, padding, stats)
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, padding, weight.dtype, miopen_wgrad)
+        ctx.mark_non_differentiable(st)
+        return y, st
+
+    @staticmethod
+    def backward(ctx, gy, _gst=None):
+        x, w = ctx.saved_tensors
+        s, p, wdtype, miopen_wgrad = ctx.cfg
+        gy = _cl(gy)
+        kh, kw = w.shape[2], w.shape[3]
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if s == 1 and kh - 1 - p >= 0 and kw == kh:
+                wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Cin][kh][kw][Cout]
+                dx = _C.conv_fwd(gy, wd, kh, kw, 1, kh - 1 - p, False)[0]
+            else:
+                dx = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                         [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            if miopen_wgrad:
+                dw = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                         [False, True, False])[1]
+            else:
+                dw = _C.conv_wgrad(gy, x, kh, kw, s, p)
+            if dw.dtype != wdtype:
+                dw = dw.to(wdtype)
+        return dx, dw, None, None, None, None, None
+
+
+def conv_kxk_gemm(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int, stats: bool = False,
+                  miopen_wgrad: bool = False, miopen_fwd: bool = False):
+    """NHWC bf16 kxk convolution on the implicit-GEMM MFMA kernels. Returns
+    (y, sums) — sums = fp32 [2*Cout] (Σy, Σy²) when ``stats`` (and the forward
+    is ours) else empty. ``miopen_fwd`` / ``miopen_wgrad`` route those passes
+    to MIOpen (shape policy: :func:`kxk_policy`)."""
+    return _ConvKxKGemmFn.apply(x, weight, stride, padding, stats, miopen_wgrad, miopen_fwd)
+
+
+def kxk_policy(cin: int, cout: int, ho: int, stride: int):
+    """(miopen_fwd, miopen_wgrad) for a 3x3 conv at ResNet-50 b256 shapes,
+    from tools/gemm_bench.py (profiles/r1_gemm3x3_vs_miopen.log): our forward
+    (+ the BN sums, which spares a statistics pass) wins at 28x28 and 7x7
+    outputs; MIOpen's is faster at 56x56 and 14x14 outputs. Our gathered wgrad
+    wins everywhere but cin = cout = 64 (one 64x64 tile per tap)."""
+    return ho in (56, 14), cin == 64 and cout == 64
+
+
+def conv_kxk_gemm_ok(x: torch.Tensor, conv) -> bool:
+    return (conv_kxk_ok(x, conv) and x.shape[1] % 64 == 0 and conv.out_channels % 64 == 0
+            and conv.kernel_size[0] == conv.kernel_size[1])
 
 
 def conv_kxk_ok(x: torch.Tensor, conv) -> bool:

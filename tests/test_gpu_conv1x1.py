@@ -200,3 +200,57 @@ def test_conv_kxk_autograd(cuda):
     wr = conv.weight.detach().clone().requires_grad_(True)
     F.conv2d(x.detach().float(), wr, None, 2, 1).backward(gy.float())
     assert conv.weight.grad.dtype == torch.float32 and _rel(conv.weight.grad, wr.grad) < 1e-3
+
+
+@pytest.mark.parametrize("cin,cout,hw,k,stride,pad", [(64, 128, 14, 3, 1, 1), (64, 64, 9, 3, 2, 1), (128, 64, 7, 3, 1, 1),
+                                                     (64, 128, 11, 1, 2, 0), (192, 64, 5, 3, 1, 1)])
+def test_conv_kxk_gemm(cuda, cin, cout, hw, k, stride, pad):
+    """Implicit-GEMM MFMA kxk conv (gemm.hip GATHER): forward + epilogue sums,
+    data gradient (stride 1: the forward kernel on flipped weights), weight
+    gradient, vs fp32 PyTorch on the same bf16 operands; ragged M."""
+    from torch import nn
+
+    from distributed_compute_pytorch_amd.ops.conv import conv_kxk_gemm
+
+    g = torch.Generator().manual_seed(11)
+    conv = nn.Conv2d(cin, cout, k, stride, pad, bias=False).to(cuda).to(memory_format=torch.channels_last)
+    x = _x(3, hw, hw, cin, cuda, g).requires_grad_(True)
+    y, st = conv_kxk_gemm(x, conv.weight, stride, pad, stats=True)
+    ho = (hw + 2 * pad - k) // stride + 1
+    assert y.shape == (3, cout, ho, ho) and y.is_contiguous(memory_format=torch.channels_last)
+    gy = _x(3, ho, ho, cout, cuda, g)
+    y.backward(gy)
+    wb = conv.weight.detach().to(torch.bfloat16).float()
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, wb, None, stride, pad)
+    yr.backward(gy.float())
+    assert _rel(y, yr) < 1e-2
+    yf = y.float()
+    ref_st = torch.cat([yf.sum((0, 2, 3)), (yf * yf).sum((0, 2, 3))])
+    assert _rel(st, ref_st) < 1e-4
+    assert _rel(x.grad, xr.grad) < 1e-2
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    F.conv2d(x.detach().float(), wr, None, stride, pad).backward(gy.float())
+    assert conv.weight.grad.dtype == torch.float32 and _rel(conv.weight.grad, wr.grad) < 1e-3
+
+
+def test_conv_kxk_gemm_miopen_routes(cuda):
+    """The policy's MIOpen forward / wgrad routes give the same results."""
+    from torch import nn
+
+    from distributed_compute_pytorch_amd.ops.conv import conv_kxk_gemm
+
+    g = torch.Generator().manual_seed(12)
+    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False).to(cuda).to(memory_format=torch.channels_last)
+    x = _x(2, 10, 10, 64, cuda, g)
+    gy = _x(2, 10, 10, 64, cuda, g)
+    outs = []
+    for mf, mw in ((False, False), (True, True)):
+        xa = x.clone().requires_grad_(True)
+        conv.weight.grad = None
+        y, st = conv_kxk_gemm(xa, conv.weight, 1, 1, stats=True, miopen_wgrad=mw, miopen_fwd=mf)
+        assert (st.numel() == 0) == mf
+        y.backward(gy)
+        outs.append((y.float(), xa.grad.float(), conv.weight.grad.clone()))
+    for a, b in zip(*outs):
+        assert _rel(a, b) < 1e-2

@@ -42,13 +42,14 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--json", default=None)
     ap.add_argument("--no3x3", action="store_true")
+    ap.add_argument("--only3x3", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.backends.cudnn.benchmark = True
     bf = torch.bfloat16
     cl = torch.channels_last
     rows = []
-    for hw, ci, co in SHAPES:
+    for hw, ci, co in [] if a.only3x3 else SHAPES:
         M = a.batch * hw * hw
         x = torch.randn(a.batch, ci, hw, hw, device=dev).to(bf).contiguous(memory_format=cl)
         gy = torch.randn(a.batch, co, hw, hw, device=dev).to(bf).contiguous(memory_format=cl)
@@ -99,14 +100,20 @@ def main():
         us_d = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w4, None, (st, st), (1, 1), (1, 1), False,
                                                                   (0, 0), 1, (True, False, False)), a.iters)
         us_f = timeit(lambda: F.conv2d(x, w4, None, st, 1), a.iters)
+        wf = w4.permute(0, 2, 3, 1).contiguous()
+        wd = w4.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+        us_of = timeit(lambda: _C.conv_fwd(x, wf, 3, 3, st, 1, True), a.iters)
+        us_od = timeit(lambda: _C.conv_fwd(gy, wd, 3, 3, 1, 1, False), a.iters) if st == 1 else float("nan")
         flops = 2.0 * a.batch * ho * ho * c * c * 9
         r3 = {"shape3x3": f"{hw}x{hw} c={c} s={st}", "ours_wgrad_us": round(us_o, 1), "miopen_wgrad_us": round(us_m, 1),
               "miopen_dgrad_us": round(us_d, 1), "miopen_fwd_us": round(us_f, 1),
+              "ours_fwd+stats_us": round(us_of, 1), "ours_dgrad_us": round(us_od, 1),
+              "ours_fwd_TFps": round(flops / (us_of * 1e-6) / 1e12, 1),
               "ours_wgrad_TFps": round(flops / (us_o * 1e-6) / 1e12, 1)}
         print(json.dumps(r3), flush=True)
         rows3 = locals().setdefault("rows3", [])
         rows3.append(r3)
-    tot = {k: round(sum(r[k] for r in rows), 1) for k in rows[0] if k.endswith("_us")}
+    tot = {k: round(sum(r[k] for r in rows), 1) for k in rows[0] if k.endswith("_us")} if rows else {}
     print(json.dumps({"total_us": tot}), flush=True)
     if a.json:
         with open(a.json, "w") as f:
