@@ -32,6 +32,8 @@
 // bwd-weights) for these layers (SURVEY §2f N8/N9, P2 "hand-written MFMA").
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "gemm_kernels.h"
 
 namespace dcp {
@@ -75,6 +77,7 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
   else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if constexpr (N == 22) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
   else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
   else if constexpr (N == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
@@ -113,6 +116,15 @@ __device__ __forceinline__ bf16x8 bn_act_frag(bf16x8 v, const float (&sc)[8], co
 // distinct: f = 0,0,2,2 (bit 3 of the row → chunk bit 1). The previous
 // (r>>2)&3 was 2-way on every group (SQ_LDS_BANK_CONFLICT = ½ of LDS cycles).
 __device__ __forceinline__ int nt_swz(int r) { return ((r >> 3) & 1) << 1; }
+// BK = 64 image: 128-B rows (2 per bank row), 8 chunks; the two 32-k halves
+// are read as logical chunks 4s + (lane>>4). Exhaustive search over XORs of
+// row bits (all four ds_read_b128 groups, both halves, 16 distinct slots):
+// f(r) = (r >> 1) & 7 is conflict-free.
+template <int BK>
+__device__ __forceinline__ int nt_swzk(int r) {
+  if constexpr (BK == 64) return (r >> 1) & 7;
+  else return nt_swz(r);
+}
 
 // Convolution geometry of the gathered (implicit-GEMM) kernels. wgrad: B rows
 // are the input pixels under tap (dy, dx) = (blockIdx.z / kw, blockIdx.z % kw)
@@ -125,16 +137,22 @@ struct ConvGeo {
   int cin;               // input channels (gemm_nt GATHER)
 };
 
-constexpr int kNSnt = 3;  // NT ring stages (leaves LDS for the per-wave C staging at 2 blocks/CU)
+// NT ring stages: BK=32 → 3 (two stages in flight), BK=64 → 2; either way
+// ≤ 64 KB of ring + 16 KB of per-wave C staging keeps 2 blocks per CU
+template <int BK>
+constexpr int nt_stages() { return BK == 64 ? 2 : 3; }
 
-template <int BM, int BN, bool PRO, bool STATS, bool GATHER>
+template <int BM, int BN, bool PRO, bool STATS, bool GATHER, int BK>
 __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                      uint16_t* __restrict__ C, int64_t M, int N, int K,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int relu,
                                                      float* __restrict__ stats, int tiles_m, int tn, ConvGeo geo) {
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
-  constexpr int SA = BM * 64, SB = BN * 64, STAGE = SA + SB;  // bytes
+  constexpr int kNSnt = nt_stages<BK>();
+  constexpr int RB = BK * 2;                                  // stage row bytes
+  constexpr int CPR = BK / 8;                                 // 16-B chunks per row
+  constexpr int SA = BM * RB, SB = BN * RB, STAGE = SA + SB;  // bytes
   constexpr int NA = SA / 4096, NB = SB / 4096;                // glds per wave per stage (1 KiB each)
   constexpr int G = NA + NB;
   constexpr int FM = BM / 32, FN = BN / 32;  // 16-row fragments per wave (2×2 waves)
@@ -162,7 +180,7 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
   const int xcd = wid & 7, q8 = P >> 3, r8 = P & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
   const int n0 = (wg % tn) * BN;
-  const int KT = K / kBK;
+  const int KT = K / BK;
   const int my_tiles = (tiles_m * tn - wg + P - 1) / P;
   const int T = my_tiles * KT;  // stages this block streams
   char* cst = cst_all + wave * CST;
@@ -188,7 +206,7 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int p = (wave * NA + j) * 64 + lane;  // 16-B unit in the A image
-      const int r = p >> 2, lc = (p & 3) ^ nt_swz(p >> 2);
+      const int r = p / CPR, lc = (p % CPR) ^ nt_swzk<BK>(p / CPR);
       int64_t gm = m0 + r;
       gm = gm < M ? gm : M - 1;
       if (GATHER) {  // once per tile: the per-stage source is then two adds and a bounds test
@@ -205,19 +223,19 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int p = (wave * NB + j) * 64 + lane;
-    const int r = p >> 2, lc = (p & 3) ^ nt_swz(p >> 2);
+    const int r = p / CPR, lc = (p % CPR) ^ nt_swzk<BK>(p / CPR);
     bsrc[j] = B + static_cast<int64_t>(n0 + r) * K + lc * 8;
   }
   set_a(wg);
   auto issue = [&]() {
     if (is_n >= T) return;
     char* base = lds + is_slot * STAGE;
-    const int k0 = is_kt * kBK;
+    const int k0 = is_kt * BK;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       if (GATHER) {
         const int p = (wave * NA + j) * 64 + lane;
-        const int lc = (p & 3) ^ nt_swz(p >> 2);
+        const int lc = (p % CPR) ^ nt_swzk<BK>(p / CPR);
         const int hi = ghb[j] + is_dy, wi = gwb[j] + is_dx;
         const bool ok = static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
                         static_cast<unsigned>(wi) < static_cast<unsigned>(geo.W);
@@ -233,7 +251,7 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
     ++is_n;
     is_slot = is_slot + 1 == kNSnt ? 0 : is_slot + 1;
     if (GATHER) {
-      is_c0 += kBK;
+      is_c0 += BK;
       if (is_c0 == geo.cin) {
         is_c0 = 0;
         if (++is_dx == geo.kw) {
@@ -284,33 +302,37 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
     issue();
     const char* sA = lds + slot * STAGE;
     const char* sB = sA + SA;
-    bf16x8 xf[FM], wf[FN];
 #pragma unroll
-    for (int j = 0; j < FM; ++j) {
-      const int r = wm * (BM / 2) + j * 16 + (lane & 15);
-      xf[j] = *reinterpret_cast<const bf16x8*>(sA + r * 64 + 16 * (ck ^ nt_swz(r)));
-    }
+    for (int h = 0; h < BK / 32; ++h) {  // 32-k halves of the stage
+      const int lch = 4 * h + ck;
+      bf16x8 xf[FM], wf[FN];
 #pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      const int r = wn * WN + i * 16 + (lane & 15);
-      wf[i] = *reinterpret_cast<const bf16x8*>(sB + r * 64 + 16 * (ck ^ nt_swz(r)));
-    }
-    if (PRO) {
-      const int kk = kt * kBK + ck * 8;
-      float sc[8], sf[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sc[e] = pro[kk + e];
-        sf[e] = pro[K + kk + e];
+      for (int j = 0; j < FM; ++j) {
+        const int r = wm * (BM / 2) + j * 16 + (lane & 15);
+        xf[j] = *reinterpret_cast<const bf16x8*>(sA + r * RB + 16 * (lch ^ nt_swzk<BK>(r)));
       }
 #pragma unroll
-      for (int j = 0; j < FM; ++j) xf[j] = bn_act_frag(xf[j], sc, sf, relu != 0);
+      for (int i = 0; i < FN; ++i) {
+        const int r = wn * WN + i * 16 + (lane & 15);
+        wf[i] = *reinterpret_cast<const bf16x8*>(sB + r * RB + 16 * (lch ^ nt_swzk<BK>(r)));
+      }
+      if (PRO) {
+        const int kk = kt * BK + lch * 8;
+        float sc[8], sf[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sc[e] = pro[kk + e];
+          sf[e] = pro[K + kk + e];
+        }
+#pragma unroll
+        for (int j = 0; j < FM; ++j) xf[j] = bn_act_frag(xf[j], sc, sf, relu != 0);
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int j = 0; j < FM; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
 
     if (kt == KT - 1) {
       // epilogue, per wave and in two 32-row halves: acc[i][j][r] = C[m][n] with
@@ -704,9 +726,19 @@ bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) {
 }
 
 namespace {
-template <bool GATHER>
-void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
-                    const float* shift, bool relu, float* stats, const ConvGeo& geo, hipStream_t s) {
+// k per ring stage of gemm_nt: 64 (2-stage ring) halves the barriers and
+// vmcnt waits per MFMA; 32 (3-stage ring) kept for A/B (DCP_GEMM_BK=32)
+inline int nt_bk() {
+  static const int bk = [] {
+    const char* v = getenv("DCP_GEMM_BK");
+    return v && atoi(v) == 32 ? 32 : 64;
+  }();
+  return bk;
+}
+
+template <bool GATHER, int BK>
+void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                       const float* shift, bool relu, float* stats, const ConvGeo& geo, hipStream_t s) {
   const int BN = N % 128 == 0 ? 128 : 64;
   constexpr int BM = 128;
   const int tiles_m = static_cast<int>((M + BM - 1) / BM);
@@ -720,13 +752,14 @@ void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int
   const bool pro = scale != nullptr;
   const bool st = stats != nullptr;
   // ring + per-wave C staging (4 × 32 rows × BN/2) + BN coefficients
-  const size_t lds = static_cast<size_t>(kNSnt) * (BM + BN) * 64 + 4 * 32 * BN + (pro ? 8 * static_cast<size_t>(K) : 0);
+  const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 + 4 * 32 * BN +
+                     (pro ? 8 * static_cast<size_t>(K) : 0);
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
-#define DCP_GNT(BN_, P_, S_)                                                                                      \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P_, S_, GATHER>), grid, dim3(kT), lds, s, a, b, c, M, N, K, scale, \
-                     shift, relu ? 1 : 0, stats, tiles_m, tn, geo)
+#define DCP_GNT(BN_, P_, S_)                                                                                     \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P_, S_, GATHER, BK>), grid, dim3(kT), lds, s, a, b, c, M, N, K,   \
+                     scale, shift, relu ? 1 : 0, stats, tiles_m, tn, geo)
 #define DCP_GNT2(BN_)                            \
   do {                                           \
     if constexpr (!GATHER) {                     \
@@ -746,6 +779,16 @@ void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int
   else DCP_GNT2(64);
 #undef DCP_GNT2
 #undef DCP_GNT
+}
+
+template <bool GATHER>
+void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                    const float* shift, bool relu, float* stats, const ConvGeo& geo, hipStream_t s) {
+  // the BN prologue stays on BK=32: at BK=64 its per-half coefficient loads and
+  // transforms no longer overlap the MFMAs (+20-40 % on the PRO GEMMs)
+  if (nt_bk() == 64 && scale == nullptr)
+    gemm_nt_launch_bk<GATHER, 64>(A, B, C, M, N, K, scale, shift, relu, stats, geo, s);
+  else gemm_nt_launch_bk<GATHER, 32>(A, B, C, M, N, K, scale, shift, relu, stats, geo, s);
 }
 }  // namespace
 

@@ -211,11 +211,11 @@ def conv_kxk_gemm(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: i
 
 def kxk_policy(cin: int, cout: int, ho: int, stride: int):
     """(miopen_fwd, miopen_wgrad) for a 3x3 conv at ResNet-50 b256 shapes,
-    from tools/gemm_bench.py (profiles/r1_gemm3x3_vs_miopen.log): our forward
-    (+ the BN sums, which spares a statistics pass) wins at 28x28 and 7x7
-    outputs; MIOpen's is faster at 56x56 and 14x14 outputs. Our gathered wgrad
+    from tools/gemm_bench.py (profiles/r1_gemm3x3_bk64.log): our forward with
+    the BK=64 ring (+ the BN sums, which spares a statistics pass) beats
+    MIOpen's forward + a statistics pass at every shape; our gathered wgrad
     wins everywhere but cin = cout = 64 (one 64x64 tile per tap)."""
-    return ho in (56, 14), cin == 64 and cout == 64
+    return False, cin == 64 and cout == 64
 
 
 def conv_kxk_gemm_ok(x: torch.Tensor, conv) -> bool:

@@ -1,0 +1,7 @@
+#!/bin/bash
+# BK=64 gemm_nt (non-PRO) + ours-everywhere 3x3 forward: tests + ResNet bench
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_conv1x1.py tests/test_gpu_transformer_ops.py > gpurun_out/t49.log 2>&1 || exit 1
+timeout -k 10 600 python3 bench.py --steps 30 --warmup 10 > gpurun_out/b49.log 2>&1 || exit 1
+echo done
