@@ -451,19 +451,22 @@ __device__ __forceinline__ bf16x8 mask_rows(bf16x8 v, int valid, int lane) {
   return __builtin_bit_cast(bf16x8, s);
 }
 
-template <int BM, int BN, bool PRO, bool GATHER>
+template <int BM, int BN, bool PRO, bool GATHER, int BK>
 __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                         float* __restrict__ ws, int64_t M, int N1, int N2,
                                                         int64_t chunk, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int relu, int tiles_j,
                                                         ConvGeo geo) {
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
-  constexpr int SA = 32 * BM * 2, SB = 32 * BN * 2, STAGE = SA + SB;
+  // BK m-rows per stage: 64 on a 2-deep ring (half the barriers per MFMA) or
+  // 32 on the 4-deep ring; both ≤ 64 KB of LDS (2 blocks per CU)
+  constexpr int kNSw = BK == 64 ? 2 : kNS;
+  constexpr int SA = BK * BM * 2, SB = BK * BN * 2, STAGE = SA + SB;
   constexpr int NA = SA / 4096, NB = SB / 4096;  // glds per wave per stage
   constexpr int G = NA + NB;
   constexpr int ACPR = BM / 8, BCPR = BN / 8;  // 16-B chunks per stage row
   constexpr int FM = BM / 32, FN = BN / 32;
-  __shared__ __attribute__((aligned(16))) char lds[kNS * STAGE];
+  __shared__ __attribute__((aligned(16))) char lds[kNSw * STAGE];
 
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -473,7 +476,7 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
   const int i0 = ti * BM, j0 = tj * BN;
   const int64_t mz0 = static_cast<int64_t>(blockIdx.y) * chunk;
   const int64_t mz1 = min(M, mz0 + chunk);
-  const int T = mz0 < mz1 ? static_cast<int>((mz1 - mz0 + kBK - 1) / kBK) : 0;
+  const int T = mz0 < mz1 ? static_cast<int>((mz1 - mz0 + BK - 1) / BK) : 0;
 
   // per-lane BN coefficients of its B-fragment channel (one channel per lane per fragment)
   float psc[FN], psf[FN];
@@ -492,7 +495,7 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
   int g_m[NB], g_n[NB], g_ho[NB], g_wo[NB];  // GATHER: output pixel of each B row at the next issue
   const int gdy = static_cast<int>(blockIdx.z) / geo.kw - geo.pad;
   const int gdx = static_cast<int>(blockIdx.z) % geo.kw - geo.pad;
-  const int adv_h = GATHER ? kBK / geo.Wo : 0, adv_w = GATHER ? kBK % geo.Wo : 0;
+  const int adv_h = GATHER ? BK / geo.Wo : 0, adv_w = GATHER ? BK % geo.Wo : 0;
   if (GATHER) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -508,8 +511,8 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
 
   auto issue = [&](int q) {
     if (q >= T) return;
-    const int64_t mb = mz0 + static_cast<int64_t>(q) * kBK;
-    char* base = lds + (q % kNS) * STAGE;
+    const int64_t mb = mz0 + static_cast<int64_t>(q) * BK;
+    char* base = lds + (q % kNSw) * STAGE;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int p = (wave * NA + j) * 64 + lane;
@@ -525,7 +528,7 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
       const int r = p / BCPR, pc = p % BCPR;
       const int lc = 2 * ((pc >> 1) ^ tr_f<BN>(r)) + (pc & 1);
       if (GATHER) {
-        // output pixel g_m[j] = (g_n, g_ho, g_wo), advanced by kBK per stage
+        // output pixel g_m[j] = (g_n, g_ho, g_wo), advanced by BK per stage
         // without divisions (they cost more VALU than the stage's MFMAs)
         const int hi = g_ho[j] * geo.stride + gdy, wi = g_wo[j] * geo.stride + gdx;
         const bool ok = g_m[j] < mz1 && static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
@@ -533,7 +536,7 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
         const uint16_t* src = ok ? B + (static_cast<int64_t>(g_n[j] * geo.H + hi) * geo.W + wi) * N2 + j0 + lc * 8
                                  : geo.zero + lc * 8;
         glds16(src, base + SA + (wave * NB + j) * 1024);
-        g_m[j] += kBK;
+        g_m[j] += BK;
         g_wo[j] += adv_w;
         g_ho[j] += adv_h;
         if (g_wo[j] >= geo.Wo) {
@@ -559,40 +562,44 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
-  for (int q = 0; q < kNS - 1; ++q) issue(q);
+  for (int q = 0; q < kNSw - 1; ++q) issue(q);
   for (int q = 0; q < T; ++q) {
-    if (q + kNS - 2 < T) wait_vm<(kNS - 2) * G>();
+    if (q + kNSw - 2 < T) wait_vm<(kNSw - 2) * G>();
     else wait_vm<0>();
     barrier();
-    issue(q + kNS - 1);
-    const char* sA = lds + (q % kNS) * STAGE;
-    const char* sB = sA + SA;
-    bf16x8 af[FM], bfr[FN];
+    issue(q + kNSw - 1);
+    const int64_t valid = mz1 - (mz0 + static_cast<int64_t>(q) * BK);
 #pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = tr_frag<BM>(sA, wi * (BM / 2) + i * 16, lane);
+    for (int h = 0; h < BK / 32; ++h) {  // 32-row halves of the stage
+      const char* sA = lds + (q % kNSw) * STAGE + h * 32 * BM * 2;
+      const char* sB = lds + (q % kNSw) * STAGE + SA + h * 32 * BN * 2;
+      bf16x8 af[FM], bfr[FN];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      bfr[j] = tr_frag<BN>(sB, wj * (BN / 2) + j * 16, lane);
-      if (PRO) {
-        float sc[8], sf[8];
+      for (int i = 0; i < FM; ++i) af[i] = tr_frag<BM>(sA, wi * (BM / 2) + i * 16, lane);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          sc[e] = psc[j];
-          sf[e] = psf[j];
+      for (int j = 0; j < FN; ++j) {
+        bfr[j] = tr_frag<BN>(sB, wj * (BN / 2) + j * 16, lane);
+        if (PRO) {
+          float sc[8], sf[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            sc[e] = psc[j];
+            sf[e] = psf[j];
+          }
+          bfr[j] = bn_act_frag(bfr[j], sc, sf, relu != 0);
         }
-        bfr[j] = bn_act_frag(bfr[j], sc, sf, relu != 0);
       }
+      const int64_t vh = valid - 32 * h;
+      if (vh < 32) {  // ragged last stage: rows past the slice contribute zero (A side)
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = mask_rows(af[i], vh < 0 ? 0 : static_cast<int>(vh), lane);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    const int64_t valid = mz1 - (mz0 + static_cast<int64_t>(q) * kBK);
-    if (valid < kBK) {  // ragged last stage: rows past the slice contribute zero (A side)
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = mask_rows(af[i], static_cast<int>(valid), lane);
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   }
   // slab z holds D in its final [N1][taps][N2] layout (taps = gridDim.z)
   const int ntaps = static_cast<int>(gridDim.z);
@@ -707,14 +714,15 @@ WgradPlan wgrad_plan(int64_t M, int N1, int N2, int taps = 1) {
   p.bm = N1 % 128 == 0 ? 128 : 64;
   p.bn = N2 % 128 == 0 ? 128 : 64;
   p.tiles = (N1 / p.bm) * (N2 / p.bn);
-  const int64_t ksteps = (M + kBK - 1) / kBK;
+  constexpr int kStep = 64;  // chunk granularity: whole stages at BK = 64 and 32
+  const int64_t ksteps = (M + kStep - 1) / kStep;
   int64_t S = 512 / (p.tiles * taps);  // ~2 blocks per CU
   // keep the slab traffic (write + read) ≤ ~the operand traffic
   const int64_t cap = (M * (N1 + static_cast<int64_t>(taps) * N2) * 2 / 2) / (static_cast<int64_t>(N1) * taps * N2 * 4);
   if (S > cap) S = cap;
   if (S > ksteps) S = ksteps;
   if (S < 1) S = 1;
-  p.chunk = ((ksteps + S - 1) / S) * kBK;
+  p.chunk = ((ksteps + S - 1) / S) * kStep;
   p.S = static_cast<int>((M + p.chunk - 1) / p.chunk);
   return p;
 }
@@ -840,9 +848,19 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   auto b = static_cast<const uint16_t*>(B);
   const bool pro = scale != nullptr;
   const int tj = N2 / p.bn;
-#define DCP_GWG(BM_, BN_, P)                                                                                   \
-  hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,   \
-                     p.chunk, scale, shift, relu ? 1 : 0, tj, geo)
+  static const bool bk64 = [] {
+    const char* v = getenv("DCP_WGRAD_BK");
+    return !(v && atoi(v) == 32);
+  }();
+#define DCP_GWG(BM_, BN_, P)                                                                                     \
+  do {                                                                                                          \
+    if (bk64 && !P)                                                                                             \
+      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 64>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                         \
+    else                                                                                                        \
+      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                         \
+  } while (0)
 #define DCP_GWG2(BM_, BN_)                      \
   do {                                          \
     if constexpr (!GATHER) {                    \

@@ -214,8 +214,10 @@ def kxk_policy(cin: int, cout: int, ho: int, stride: int):
     from tools/gemm_bench.py (profiles/r1_gemm3x3_bk64.log): our forward with
     the BK=64 ring (+ the BN sums, which spares a statistics pass) beats
     MIOpen's forward + a statistics pass at every shape; our gathered wgrad
-    wins everywhere but cin = cout = 64 (one 64x64 tile per tap)."""
-    return False, cin == 64 and cout == 64
+    (BK=64 ring, profiles/r1_gemm_bench_wgrad_bk64.log) is faster than
+    MIOpen's wrw everywhere but 56x56 with cin = cout = 64, where it ties —
+    and it skips MIOpen's zero-fill and fp32→bf16 cast passes."""
+    return False, False
 
 
 def conv_kxk_gemm_ok(x: torch.Tensor, conv) -> bool:
