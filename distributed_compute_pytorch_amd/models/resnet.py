@@ -98,6 +98,10 @@ class Bottleneck(nn.Module):
             if conv.stride == (1, 1) and gemm_ok(inp, conv.in_channels, conv.out_channels):
                 z, st = gemm_conv1x1(inp, conv.weight, stats=True)
                 identity = bn(z, stats=st)
+            elif KXK_GEMM and conv_kxk_gemm_ok(inp, conv):
+                # strided 1x1: gathered implicit GEMM (+ BN sums); dgrad on MIOpen
+                z, st = conv_kxk_gemm(inp, conv.weight, conv.stride[0], conv.padding[0], stats=True)
+                identity = bn(z, stats=st)
             else:
                 identity = self.downsample(inp)
         else:
