@@ -335,6 +335,89 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& wt, int6
   return {y, st};
 }
 
+namespace {
+struct BnRedIn {
+  at::Tensor w, b;  // fp32 copies (or undefined)
+  const float* mean;
+  const float* invstd;
+};
+BnRedIn bnred_in(const at::Tensor& x, const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                 const at::Tensor& mean, const at::Tensor& invstd, int64_t C, const char* what) {
+  check_gemm_act(x, what);
+  DCP_CHECK(x.dim() == 4 && x.size(1) == C, what, ": x must be the [N, C, H, W] BN input of the gradient");
+  DCP_CHECK(mean.numel() == C && invstd.numel() == C && mean.scalar_type() == at::kFloat, what, ": BN statistics");
+  BnRedIn r;
+  if (gamma.has_value() && gamma->defined()) r.w = gamma->to(at::kFloat).contiguous();
+  if (beta.has_value() && beta->defined()) r.b = beta->to(at::kFloat).contiguous();
+  r.mean = mean.data_ptr<float>();
+  r.invstd = invstd.data_ptr<float>();
+  return r;
+}
+}  // namespace
+
+// dy = gy @ W (1x1 conv data gradient) whose epilogue also reduces the
+// BN+ReLU backward of x (the layer input): returns (dy, acc [2*Cin]) for
+// bn_act_bwd_apply — no separate reduce pass.
+std::vector<at::Tensor> conv1x1_dgrad_bnred(const at::Tensor& gy, const at::Tensor& wt, const at::Tensor& x,
+                                            const c10::optional<at::Tensor>& gamma,
+                                            const c10::optional<at::Tensor>& beta, const at::Tensor& mean,
+                                            const at::Tensor& invstd) {
+  check_gemm_act(gy, "conv1x1_dgrad_bnred");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t K = gy.size(1);
+  const int64_t M = gy.numel() / K;
+  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % K == 0,
+            "conv1x1_dgrad_bnred: weight");
+  const int64_t N = wt.numel() / K;
+  DCP_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_dgrad_bnred: unsupported shape");
+  const BnRedIn r = bnred_in(x, gamma, beta, mean, invstd, N, "conv1x1_dgrad_bnred");
+  DCP_CHECK(x.numel() == M * N, "conv1x1_dgrad_bnred: x / gy pixel count mismatch");
+  at::Tensor dy = at::empty({gy.size(0), N, gy.size(2), gy.size(3)},
+                            gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto s = stream_of(gy);
+  at::Tensor acc = zeroed_floats(2 * N, gy, s);
+  kern::gemm_nt_bnred_bf16(gy.data_ptr(), wt.data_ptr(), dy.data_ptr(), M, static_cast<int>(N), static_cast<int>(K),
+                           x.data_ptr(), r.w.defined() ? r.w.data_ptr<float>() : nullptr,
+                           r.b.defined() ? r.b.data_ptr<float>() : nullptr, r.mean, r.invstd, acc.data_ptr<float>(),
+                           s);
+  return {dy, acc};
+}
+
+// stride-1 kxk conv data gradient (implicit GEMM on gy with the flipped,
+// transposed weight wd [Cin][kh][kw][Cout]) + the BN+ReLU backward reduction
+// of x in its epilogue: returns (dy, acc [2*Cin]).
+std::vector<at::Tensor> conv_dgrad_bnred(const at::Tensor& gy, const at::Tensor& wd, int64_t kh, int64_t kw,
+                                         int64_t pad, const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
+                                         const c10::optional<at::Tensor>& beta, const at::Tensor& mean,
+                                         const at::Tensor& invstd) {
+  check_gemm_act(gy, "conv_dgrad_bnred");
+  DCP_CHECK(gy.dim() == 4, "conv_dgrad_bnred: NHWC 4-D gradient required");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t N = gy.size(0), Co = gy.size(1), H = gy.size(2), W = gy.size(3);
+  DCP_CHECK(wd.scalar_type() == at::kBFloat16 && wd.is_contiguous() && wd.numel() % (kh * kw * Co) == 0,
+            "conv_dgrad_bnred: weight must be contiguous bf16 [Cin][kh][kw][Cout]");
+  const int64_t Ci = wd.numel() / (kh * kw * Co);
+  DCP_CHECK(kern::conv_fwd_supported(static_cast<int>(Co), static_cast<int>(Ci), static_cast<int>(kh),
+                                     static_cast<int>(kw)),
+            "conv_dgrad_bnred: channels must be multiples of 64");
+  const int64_t Ho = H + 2 * pad - kh + 1, Wo = W + 2 * pad - kw + 1;
+  DCP_CHECK(x.dim() == 4 && x.size(0) == N && x.size(2) == Ho && x.size(3) == Wo,
+            "conv_dgrad_bnred: x does not match the data-gradient geometry");
+  DCP_CHECK(N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31), "conv_dgrad_bnred: too large");
+  const BnRedIn r = bnred_in(x, gamma, beta, mean, invstd, Ci, "conv_dgrad_bnred");
+  at::Tensor dy = at::empty({N, Ci, Ho, Wo}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto s = stream_of(gy);
+  at::Tensor acc = zeroed_floats(2 * Ci, gy, s);
+  kern::conv_fwd_bnred_bf16(gy.data_ptr(), wd.data_ptr(), dy.data_ptr(), static_cast<int>(N), static_cast<int>(H),
+                            static_cast<int>(W), static_cast<int>(Co), static_cast<int>(Ho), static_cast<int>(Wo),
+                            static_cast<int>(Ci), static_cast<int>(kh), static_cast<int>(kw), 1,
+                            static_cast<int>(pad), zero_row(gy).data_ptr(), x.data_ptr(),
+                            r.w.defined() ? r.w.data_ptr<float>() : nullptr,
+                            r.b.defined() ? r.b.data_ptr<float>() : nullptr, r.mean, r.invstd,
+                            acc.data_ptr<float>(), s);
+  return {dy, acc};
+}
+
 // fp32 [N] column sums of a bf16 [.., N] tensor (Linear bias gradient)
 at::Tensor colsum(const at::Tensor& x) {
   DCP_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() >= 1,
@@ -465,6 +548,35 @@ std::vector<at::Tensor> bn_act_bwd(const at::Tensor& gy, const c10::optional<at:
   const bool has_b = bias.has_value() && bias->defined();
   at::Tensor dbias = has_b ? db.to(bias->scalar_type()) : at::Tensor();
   return {dx, dweight, dbias, gres};
+}
+
+// BN(+ReLU) training backward apply from a reduction acc [2*C] made by a
+// data-gradient GEMM epilogue (conv1x1_dgrad_bnred / conv_dgrad_bnred).
+std::vector<at::Tensor> bn_act_bwd_apply(const at::Tensor& gy, const at::Tensor& x,
+                                         const c10::optional<at::Tensor>& weight,
+                                         const c10::optional<at::Tensor>& bias, const at::Tensor& mean,
+                                         const at::Tensor& invstd, const at::Tensor& acc) {
+  check_nhwc(x, "bn_act_bwd_apply");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  DCP_CHECK(gy.sizes() == x.sizes() && gy.scalar_type() == x.scalar_type() && gy.is_contiguous(cl_fmt(x)),
+            "bn_act_bwd_apply: gy must match x");
+  DCP_CHECK(acc.scalar_type() == at::kFloat && acc.numel() == 2 * C && acc.is_contiguous(),
+            "bn_act_bwd_apply: acc must be fp32 [2*C]");
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x, cl_fmt(x));
+  const bool has_w = weight.has_value() && weight->defined();
+  at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
+  const bool has_b = bias.has_value() && bias->defined();
+  at::Tensor bf = has_b ? bias->to(at::kFloat).contiguous() : at::Tensor();
+  at::Tensor dw = at::empty({C}, fopt);
+  at::Tensor db = at::empty({C}, fopt);
+  kern::bn_backward_apply(bn_dtype(x), gy.data_ptr(), x.data_ptr(), M, static_cast<int>(C),
+                          has_w ? w.data_ptr<float>() : nullptr, has_b ? bf.data_ptr<float>() : nullptr,
+                          mean.data_ptr<float>(), invstd.data_ptr<float>(), acc.data_ptr<float>(), dx.data_ptr(),
+                          dw.data_ptr<float>(), db.data_ptr<float>(), stream_of(x));
+  return {dx, has_w ? dw.to(weight->scalar_type()) : at::Tensor(), has_b ? db.to(bias->scalar_type()) : at::Tensor()};
 }
 
 // ------------------------------------------------------------ LayerNorm ---
@@ -784,6 +896,9 @@ void bind(pybind11::module& m) {
   m.def("conv_fwd", &conv_fwd, "kxk NHWC conv forward (implicit-GEMM MFMA) [+ output BN sums]", pybind11::arg("x"),
         pybind11::arg("wt"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"), pybind11::arg("pad"),
         pybind11::arg("stats") = false);
+  m.def("conv1x1_dgrad_bnred", &conv1x1_dgrad_bnred, "1x1 data gradient + BN/ReLU backward reduction epilogue");
+  m.def("conv_dgrad_bnred", &conv_dgrad_bnred, "stride-1 kxk data gradient + BN/ReLU backward reduction epilogue");
+  m.def("bn_act_bwd_apply", &bn_act_bwd_apply, "BN/ReLU training backward apply from a precomputed reduction");
   m.def("conv_wgrad", &conv_wgrad, "kxk NHWC conv weight gradient (implicit-GEMM MFMA, fp32 out)",
         pybind11::arg("gy"), pybind11::arg("x"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"),
         pybind11::arg("pad"));

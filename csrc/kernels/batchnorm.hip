@@ -736,5 +736,22 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
 #undef DCP_BN_BAPPLY
 }
 
+// BN(+ReLU) backward apply only, training mode, mask recomputed from x: acc
+// (Σg, Σg·(x-mean)) was reduced by the data-gradient GEMM's epilogue (gemm.hip
+// RED), so the reduce pass over gy and x is skipped.
+void bn_backward_apply(int dtype, const void* gy, const void* x, int64_t M, int C, const float* gamma,
+                       const float* beta, const float* mean, const float* invstd, const float* acc, void* dx,
+                       float* dgamma, float* dbeta, hipStream_t s) {
+  const int64_t nvec = M * C / kV;
+  const int grid = apply_grid(nvec, C / kV);
+  const size_t sm = sizeof(float) * 6 * C;
+  if (dtype == BN_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<BN_BF16, true, false, true>), dim3(grid), dim3(kT), sm, s, gy, nullptr,
+                       x, mean, invstd, gamma, beta, acc, dgamma, dbeta, true, dx, M, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<BN_F32, true, false, true>), dim3(grid), dim3(kT), sm, s, gy, nullptr,
+                       x, mean, invstd, gamma, beta, acc, dgamma, dbeta, true, dx, M, nvec, C);
+}
+
 }  // namespace kern
 }  // namespace dcp

@@ -47,5 +47,10 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
                  void* dx, float* dgamma, float* dbeta, float* acc, bool training, const uint8_t* mbits,
                  hipStream_t s);
 
+// training BN+ReLU backward apply with a precomputed reduction acc [2*C]
+void bn_backward_apply(int dtype, const void* gy, const void* x, int64_t M, int C, const float* gamma,
+                       const float* beta, const float* mean, const float* invstd, const float* acc, void* dx,
+                       float* dgamma, float* dbeta, hipStream_t s);
+
 }  // namespace kern
 }  // namespace dcp

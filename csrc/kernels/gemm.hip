@@ -137,18 +137,38 @@ struct ConvGeo {
   int cin;               // input channels (gemm_nt GATHER)
 };
 
+// BatchNorm (training) of the tensor whose gradient a gemm_nt RED epilogue
+// produces: x [M, N] bf16 (its input) and its statistics / affine.
+struct BnRedArgs {
+  const uint16_t* x;
+  const float* gamma;
+  const float* beta;
+  const float* mean;
+  const float* invstd;
+};
+
 // NT ring stages: BK=32 → 3 (two stages in flight), BK=64 → 2; either way
 // ≤ 64 KB of ring + 16 KB of per-wave C staging keeps 2 blocks per CU
 template <int BK>
 constexpr int nt_stages() { return BK == 64 ? 2 : 3; }
 
-template <int BM, int BN, bool PRO, bool STATS, bool GATHER, int BK>
-__global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+// EPI: 0 = plain store; 1 = STATS (Σy, Σy² of the bf16 output per column into
+// stats[2N]); 2 = RED, the BatchNorm+ReLU backward reduction of a data-gradient
+// GEMM: C = dy (grad of y = relu(bn(x))), g = dy·[x·sc + sf > 0] (the
+// forward's own mask expression, sc/sf from gamma/beta/mean/invstd exactly as
+// batchnorm.hip's coef()), stats[0][c] += Σg, stats[1][c] += Σg·(x - mean):
+// the BN backward's separate reduce pass (re-reading dy and x) disappears.
+template <int BM, int BN, bool PRO, int EPI, bool GATHER, int BK>
+__global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                      uint16_t* __restrict__ C, int64_t M, int N, int K,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int relu,
-                                                     float* __restrict__ stats, int tiles_m, int tn, ConvGeo geo) {
+                                                     float* __restrict__ stats, int tiles_m, int tn, ConvGeo geo,
+                                                     BnRedArgs bnr) {
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
+  constexpr bool STATS = EPI == 1;
+  constexpr bool RED = EPI == 2;
+  static_assert(!(PRO && RED), "RED is a data-gradient epilogue");
   constexpr int kNSnt = nt_stages<BK>();
   constexpr int RB = BK * 2;                                  // stage row bytes
   constexpr int CPR = BK / 8;                                 // 16-B chunks per row
@@ -277,6 +297,20 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
   float ssum[8], ssq[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
+  // RED: mean and the forward's folded affine of the block's BN columns, in
+  // LDS (registers would push the kernel past 256 and halve occupancy)
+  float* redc = pro;  // [3][BN]: mean, scale, shift
+  if (RED) {
+    if (t < BN) {
+      const int c = n0 + t;
+      const float mu = bnr.mean[c];
+      const float sc = (bnr.gamma ? bnr.gamma[c] : 1.f) * bnr.invstd[c];
+      redc[t] = mu;
+      redc[BN + t] = sc;
+      redc[2 * BN + t] = (bnr.beta ? bnr.beta[c] : 0.f) - mu * sc;
+    }
+    __syncthreads();  // nothing in flight yet
+  }
 
 #pragma unroll
   for (int q = 0; q < kNSnt - 1; ++q) issue();
@@ -356,6 +390,16 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
             acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
         }
+        // RED: this half's x rows, all loads issued before the first use (one wait)
+        uint4 xr[RED ? 32 / RPI : 1];
+        if (RED) {
+#pragma unroll
+          for (int it = 0; it < 32 / RPI; ++it) {
+            const int64_t m = mt + 32 * h + it * RPI + lane / LPR;
+            xr[it] = m < M ? *reinterpret_cast<const uint4*>(bnr.x + m * N + n0 + wn * WN + (lane % LPR) * 8)
+                           : make_uint4(0, 0, 0, 0);
+          }
+        }
 #pragma unroll
         for (int it = 0; it < 32 / RPI; ++it) {
           const int row = it * RPI + lane / LPR;
@@ -375,6 +419,20 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
                 ssq[2 * k + 1] = fmaf(b, b, ssq[2 * k + 1]);
               }
             }
+            if (RED) {
+              const uint4 xv = xr[RED ? it : 0];
+              const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+              const uint32_t x4[4] = {xv.x, xv.y, xv.z, xv.w};
+              const int cb = wn * WN + c * 8;
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const float xk = (k & 1) ? bf_hi(x4[k >> 1]) : bf_lo(x4[k >> 1]);
+                float gk = (k & 1) ? bf_hi(w4[k >> 1]) : bf_lo(w4[k >> 1]);
+                gk = fmaf(xk, redc[BN + cb + k], redc[2 * BN + cb + k]) > 0.f ? gk : 0.f;
+                ssum[k] += gk;
+                ssq[k] = fmaf(gk, xk - redc[cb + k], ssq[k]);
+              }
+            }
           }
         }
       }
@@ -385,7 +443,7 @@ __global__ void __launch_bounds__(kT) gemm_nt_kernel(const uint16_t* __restrict_
       cv += P;
     }
   }
-  if (STATS) {
+  if (STATS || RED) {
     // lanes with the same channel set: lane ^ LPR, ^2LPR, ... ; then over wm via LDS
 #pragma unroll
     for (int e = 0; e < 8; ++e)
@@ -746,7 +804,8 @@ inline int nt_bk() {
 
 template <bool GATHER, int BK>
 void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
-                       const float* shift, bool relu, float* stats, const ConvGeo& geo, hipStream_t s) {
+                       const float* shift, bool relu, float* stats, const ConvGeo& geo, const BnRedArgs* red,
+                       hipStream_t s) {
   const int BN = N % 128 == 0 ? 128 : 64;
   constexpr int BM = 128;
   const int tiles_m = static_cast<int>((M + BM - 1) / BM);
@@ -761,27 +820,32 @@ void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, 
   const bool st = stats != nullptr;
   // ring + per-wave C staging (4 × 32 rows × BN/2) + BN coefficients
   const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 + 4 * 32 * BN +
-                     (pro ? 8 * static_cast<size_t>(K) : 0);
+                     (pro ? 8 * static_cast<size_t>(K) : 0) + (red ? 12 * static_cast<size_t>(BN) : 0);
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
+  const BnRedArgs bnr = red ? *red : BnRedArgs{};
 #define DCP_GNT(BN_, P_, S_)                                                                                     \
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P_, S_, GATHER, BK>), grid, dim3(kT), lds, s, a, b, c, M, N, K,   \
-                     scale, shift, relu ? 1 : 0, stats, tiles_m, tn, geo)
+                     scale, shift, relu ? 1 : 0, stats, tiles_m, tn, geo, bnr)
 #define DCP_GNT2(BN_)                            \
   do {                                           \
+    if (red) {                                   \
+      DCP_GNT(BN_, false, 2);                    \
+      break;                                     \
+    }                                            \
     if constexpr (!GATHER) {                     \
       if (pro && st) {                           \
-        DCP_GNT(BN_, true, true);                \
+        DCP_GNT(BN_, true, 1);                   \
         break;                                   \
       }                                          \
       if (pro) {                                 \
-        DCP_GNT(BN_, true, false);               \
+        DCP_GNT(BN_, true, 0);                   \
         break;                                   \
       }                                          \
     }                                            \
-    if (st) DCP_GNT(BN_, false, true);           \
-    else DCP_GNT(BN_, false, false);             \
+    if (st) DCP_GNT(BN_, false, 1);              \
+    else DCP_GNT(BN_, false, 0);                 \
   } while (0)
   if (BN == 128) DCP_GNT2(128);
   else DCP_GNT2(64);
@@ -791,18 +855,36 @@ void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, 
 
 template <bool GATHER>
 void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
-                    const float* shift, bool relu, float* stats, const ConvGeo& geo, hipStream_t s) {
+                    const float* shift, bool relu, float* stats, const ConvGeo& geo, hipStream_t s,
+                    const BnRedArgs* red = nullptr) {
   // the BN prologue stays on BK=32: at BK=64 its per-half coefficient loads and
   // transforms no longer overlap the MFMAs (+20-40 % on the PRO GEMMs)
   if (nt_bk() == 64 && scale == nullptr)
-    gemm_nt_launch_bk<GATHER, 64>(A, B, C, M, N, K, scale, shift, relu, stats, geo, s);
-  else gemm_nt_launch_bk<GATHER, 32>(A, B, C, M, N, K, scale, shift, relu, stats, geo, s);
+    gemm_nt_launch_bk<GATHER, 64>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s);
+  else gemm_nt_launch_bk<GATHER, 32>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s);
 }
 }  // namespace
 
 void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                   const float* shift, bool relu, float* stats, hipStream_t s) {
   gemm_nt_launch<false>(A, B, C, M, N, K, scale, shift, relu, stats, ConvGeo{}, s);
+}
+
+void gemm_nt_bnred_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
+                        const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,
+                        hipStream_t s) {
+  const BnRedArgs r{static_cast<const uint16_t*>(x), gamma, beta, mean, invstd};
+  gemm_nt_launch<false>(A, B, C, M, N, K, nullptr, nullptr, false, acc, ConvGeo{}, s, &r);
+}
+
+void conv_fwd_bnred_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo,
+                         int Cout, int kh, int kw, int stride, int pad, const void* zero, const void* x,
+                         const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,
+                         hipStream_t s) {
+  ConvGeo geo{H, W, Ho, Wo, stride, pad, kw, static_cast<const uint16_t*>(zero), Cin};
+  const BnRedArgs r{static_cast<const uint16_t*>(x), gamma, beta, mean, invstd};
+  gemm_nt_launch<true>(X, Wt, Y, static_cast<int64_t>(N) * Ho * Wo, Cout, kh * kw * Cin, nullptr, nullptr, false,
+                       acc, geo, s, &r);
 }
 
 bool conv_fwd_supported(int Cin, int Cout, int kh, int kw) {

@@ -55,6 +55,17 @@ void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, 
 // weight order), Y [N,Ho,Wo,Cout] bf16; stats (optional, zeroed fp32 [2*Cout])
 // += (Σy, Σy²). zero: ≥ 256 zero bytes (padding taps). Also the stride-1 data
 // gradient, run on dY with the flipped, transposed weight.
+// Data-gradient GEMM / stride-1 implicit-GEMM conv whose epilogue also
+// reduces the BatchNorm(+ReLU) backward of the layer that produced the GEMM's
+// output side: C = dy; acc (zeroed fp32 [2*N]) += (Σg, Σg·(x-mean)) with
+// g = dy·[x·sc+sf > 0], x [M, N] bf16 the BN input, sc/sf its folded affine.
+void gemm_nt_bnred_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
+                        const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,
+                        hipStream_t s);
+void conv_fwd_bnred_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo,
+                         int Cout, int kh, int kw, int stride, int pad, const void* zero, const void* x,
+                         const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,
+                         hipStream_t s);
 bool conv_fwd_supported(int Cin, int Cout, int kh, int kw);
 void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                    int kh, int kw, int stride, int pad, const void* zero, float* stats, hipStream_t s);

@@ -20,8 +20,8 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import (bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk, conv_kxk_gemm, conv_kxk_gemm_ok,
-                        conv_kxk_ok, gemm_ok, kxk_policy)
+from ..ops.conv import (bn_relu_conv, bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk, conv_kxk_gemm,
+                        conv_kxk_gemm_ok, conv_kxk_ok, gemm_ok, kxk_policy)
 from ..ops.pool import FusedMaxPool2d
 
 
@@ -29,6 +29,11 @@ GEMM_MAX_INTENSITY = float(os.environ.get("DCP_GEMM_MAX_INTENSITY", "1024"))
 KXK_WGRAD = os.environ.get("DCP_KXK_WGRAD", "0") == "1"
 # 3x3 conv2 on the implicit-GEMM MFMA kernels (fwd + BN2 sums, stride-1 dgrad)
 KXK_GEMM = os.environ.get("DCP_KXK_GEMM", "1") == "1"
+# opt-in: BN1→conv2 and BN2→conv3 as one autograd node whose data-gradient GEMM
+# reduces the BN backward in its epilogue (gemm.hip RED). Measured −1 % on
+# ResNet-50 b256 (profiles/r1_bn_conv_fuse.log): the epilogue's per-element
+# VALU (~6 ops) costs the GEMM more than the separate 5 TB/s reduce pass.
+BN_CONV_FUSE = os.environ.get("DCP_BN_CONV_FUSE", "0") == "1"
 # BN-apply prologue in the conv3 GEMM only while Cout ≤ this (≤ 2 N-tiles of 128)
 PRO_MAX_COUT = int(os.environ.get("DCP_PRO_MAX_COUT", "256"))
 
@@ -107,11 +112,13 @@ class Bottleneck(nn.Module):
         else:
             identity = inp
         z1, s1 = gemm_conv1x1(x, self.conv1.weight, stats=True)
-        y1 = self.bn1(z1, stats=s1)
         c2 = self.conv2
-        # opt-in: MIOpen fwd/dgrad + our implicit-GEMM wgrad (ties MIOpen's wrw except at
-        # 56x56x64, where it is slower: profiles/r1_gemm1x1_vs_miopen.json "rows3x3")
         s2 = None
+        if KXK_GEMM and BN_CONV_FUSE and conv_kxk_gemm_ok(z1, c2):
+            x2, s2 = bn_relu_conv(z1, self.bn1, c2.weight, c2.kernel_size[0], c2.stride[0], c2.padding[0], sums=s1,
+                                  stats=True)
+            return self._tail(x2, s2, identity, dual, True)
+        y1 = self.bn1(z1, stats=s1)
         if KXK_GEMM and conv_kxk_gemm_ok(y1, c2):
             ho = (y1.shape[2] + 2 * c2.padding[0] - c2.kernel_size[0]) // c2.stride[0] + 1
             mi_fwd, mi_wgrad = kxk_policy(c2.in_channels, c2.out_channels, ho, c2.stride[0])
@@ -125,9 +132,16 @@ class Bottleneck(nn.Module):
             x2 = c2(y1)
         if not x2.is_contiguous(memory_format=torch.channels_last):
             x2 = x2.contiguous(memory_format=torch.channels_last)
+        return self._tail(x2, s2, identity, dual, False)
+
+    def _tail(self, x2, s2, identity, dual, fuse):
+        """BN2 → conv3 → BN3 (+ residual, ReLU)."""
         if self.conv3.out_channels <= PRO_MAX_COUT:
             # BN2+ReLU applied in the GEMM prologue (its output never hits HBM)
             z3, s3 = bn_relu_conv1x1(x2, self.bn2, self.conv3.weight, stats=True, sums=s2)
+        elif fuse:
+            # BN2 output materialised once; BN2's backward reduce in conv3's dgrad epilogue
+            z3, s3 = bn_relu_conv(x2, self.bn2, self.conv3.weight, 1, 1, 0, sums=s2, stats=True)
         else:
             # wide conv3: every N-tile re-applies the prologue to the same rows,
             # which costs more than one apply pass over the narrow input

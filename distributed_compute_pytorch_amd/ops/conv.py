@@ -118,6 +118,75 @@ def bn_relu_conv1x1(x: torch.Tensor, bn, weight: torch.Tensor, stats: bool = Fal
                                   bn.eps, stats, sums)
 
 
+class _BNReluConvFn(torch.autograd.Function):
+    """conv(relu(bn(x))) for a training-mode BatchNorm whose output is
+    materialised (wide consumers, or gathered kxk convs where padding taps
+    must stay zero): BN apply kernel (statistics from the producer's GEMM
+    epilogue when given) → 1x1 GEMM or implicit-GEMM kxk conv (+ the next BN's
+    sums). Backward: the data-gradient GEMM reduces the BN backward in its
+    epilogue (gemm.hip RED), so BN's reduce pass over dy and x disappears;
+    stride > 1 kxk falls back to MIOpen's data gradient + the full BN backward."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, weight, running_mean, running_var, nbt, momentum, eps, sums, k, stride, pad,
+                stats):
+        ctx.set_materialize_grads(False)
+        y, mean, invstd, _ = _C.bn_act_fwd(x, gamma, beta, running_mean, running_var, None, True, float(momentum),
+                                           float(eps), True, nbt, sums)
+        if k == 1 and stride == 1:
+            w, wt = _w2d(weight)
+            z, st = _C.conv1x1_fwd(y, w, None, None, False, bool(stats))
+        else:
+            w = weight.detach().to(torch.bfloat16)
+            wt = None
+            z, st = _C.conv_fwd(y, w.permute(0, 2, 3, 1).contiguous(), k, k, stride, pad, bool(stats))
+        ctx.save_for_backward(x, y, gamma, beta, mean, invstd, w, wt)
+        ctx.cfg = (k, stride, pad, weight.shape, weight.dtype)
+        ctx.mark_non_differentiable(st)
+        return z, st
+
+    @staticmethod
+    def backward(ctx, gz, _gst):
+        if gz is None:
+            return (None,) * 14
+        x, y, gamma, beta, mean, invstd, w, wt = ctx.saved_tensors
+        k, stride, pad, wshape, wdtype = ctx.cfg
+        gz = _cl(gz)
+        if k == 1 and stride == 1:
+            dw = _C.conv1x1_wgrad(gz, y).view(wshape)
+            dy, acc = _C.conv1x1_dgrad_bnred(gz, wt, x, gamma, beta, mean, invstd)
+        else:
+            dw = _C.conv_wgrad(gz, y, k, k, stride, pad)
+            if stride == 1:
+                wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Cin][k][k][Cout]
+                dy, acc = _C.conv_dgrad_bnred(gz, wd, k, k, k - 1 - pad, x, gamma, beta, mean, invstd)
+            else:
+                dy = torch.ops.aten.convolution_backward(gz, y, w, None, [stride, stride], [pad, pad], [1, 1],
+                                                         False, [0, 0], 1, [True, False, False])[0]
+                dy = _cl(dy)
+                acc = None
+        if dw.dtype != wdtype:
+            dw = dw.to(wdtype)
+        if acc is None:
+            dx, dgamma, dbeta, _ = _C.bn_act_bwd(dy, None, x, gamma, beta, mean, invstd, y, True, False, True, None)
+        else:
+            dx, dgamma, dbeta = _C.bn_act_bwd_apply(dy, x, gamma, beta, mean, invstd, acc)
+        return dx, dgamma, dbeta, dw, None, None, None, None, None, None, None, None, None, None
+
+
+def bn_relu_conv(x: torch.Tensor, bn, weight: torch.Tensor, k: int, stride: int, pad: int,
+                 sums: Optional[torch.Tensor] = None, stats: bool = False):
+    """``conv(relu(bn(x)), weight)`` (square k, no bias) for a training-mode
+    BatchNorm ``bn`` on the MFMA kernels, BN backward reduced in the
+    data-gradient GEMM's epilogue. Returns (z, sums of z when ``stats``)."""
+    nbt = bn.num_batches_tracked
+    if nbt is not None and (nbt.device != x.device or nbt.dtype != torch.int64):
+        nbt.add_(1)
+        nbt = None
+    return _BNReluConvFn.apply(x, bn.weight, bn.bias, weight, bn.running_mean, bn.running_var, nbt, bn.momentum,
+                               bn.eps, sums, k, stride, pad, stats)
+
+
 class _ConvKxKFn(torch.autograd.Function):
     """kxk NHWC convolution: MIOpen forward and data gradient, our implicit-GEMM
     MFMA weight gradient (fp32 out; no zero-fill pass, no bf16→fp32 cast)."""

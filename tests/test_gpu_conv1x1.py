@@ -254,3 +254,49 @@ def test_conv_kxk_gemm_miopen_routes(cuda):
         outs.append((y.float(), xa.grad.float(), conv.weight.grad.clone()))
     for a, b in zip(*outs):
         assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.parametrize("k,stride,pad,sums", [(3, 1, 1, True), (3, 2, 1, False), (1, 1, 0, True)])
+def test_bn_relu_conv_fused_autograd(cuda, k, stride, pad, sums):
+    """BN(train)→ReLU→conv as one node (BN backward reduced in the dgrad GEMM's
+    epilogue) vs the fp32 ATen composition on the same bf16 input."""
+    from torch import nn
+
+    from distributed_compute_pytorch_amd.ops.batchnorm import BatchNormAct2d
+    from distributed_compute_pytorch_amd.ops.conv import bn_relu_conv
+
+    g = torch.Generator().manual_seed(13)
+    n, h, w, ci, co = 4, 12, 12, 64, 128
+    x = (_x(n, h, w, ci, cuda, g).float() * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bn = BatchNormAct2d(ci, act=True, fused=True).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    conv = nn.Conv2d(ci, co, k, stride, pad, bias=False).to(cuda).to(memory_format=torch.channels_last)
+    ref_bn = nn.BatchNorm2d(ci).to(cuda)
+    ref_bn.load_state_dict(bn.state_dict())
+    ref_conv = nn.Conv2d(ci, co, k, stride, pad, bias=False).to(cuda)
+    ref_conv.load_state_dict(conv.state_dict())
+
+    xa = x.detach().clone().requires_grad_(True)
+    s_in = None
+    if sums:
+        xf = x.float()
+        s_in = torch.cat([xf.sum((0, 2, 3)), (xf * xf).sum((0, 2, 3))]).contiguous()
+    z, st = bn_relu_conv(xa, bn, conv.weight, k, stride, pad, sums=s_in, stats=True)
+    gz = _x(n, z.shape[2], z.shape[3], co, cuda, g)
+    z.backward(gz)
+
+    xr = x.detach().float().clone().requires_grad_(True)
+    zr = ref_conv(torch.relu(ref_bn(xr)).to(torch.bfloat16).float())
+    zr.backward(gz.float())
+
+    assert _rel(z, zr) < 1.5e-2
+    zf = z.float()
+    assert _rel(st, torch.cat([zf.sum((0, 2, 3)), (zf * zf).sum((0, 2, 3))])) < 1e-3
+    assert _rel(xa.grad, xr.grad) < 3e-2
+    assert _rel(bn.weight.grad, ref_bn.weight.grad) < 3e-2
+    assert _rel(bn.bias.grad, ref_bn.bias.grad) < 3e-2
+    assert conv.weight.grad.dtype == torch.float32 and _rel(conv.weight.grad, ref_conv.weight.grad) < 2e-2
+    torch.testing.assert_close(bn.running_mean, ref_bn.running_mean, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(bn.running_var, ref_bn.running_var, rtol=1e-3, atol=1e-3)
