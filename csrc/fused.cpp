@@ -236,6 +236,22 @@ std::vector<at::Tensor> weight_bf16_t(const at::Tensor& w) {
   return {wb, wt};
 }
 
+// kxk conv weight (fp32 [Cout, Cin, kh, kw], any memory format) → (bf16
+// [Cout][kh][kw][Cin]: the implicit-GEMM forward operand, bf16
+// [Cin][kh][kw][Cout] spatially flipped: the stride-1 data-gradient operand),
+// one launch.
+std::vector<at::Tensor> conv_weight_bf16(const at::Tensor& w) {
+  DCP_CHECK(w.is_cuda() && w.dim() == 4, "conv_weight_bf16: 4-D device weight required");
+  c10::hip::HIPGuard guard(w.device().index());
+  const int64_t Co = w.size(0), Ci = w.size(1), kh = w.size(2), kw = w.size(3);
+  at::Tensor wf = w.detach().permute({0, 2, 3, 1}).to(at::kFloat).contiguous();  // [Co][kh][kw][Ci]
+  at::Tensor wb = at::empty({Co, kh, kw, Ci}, w.options().dtype(at::kBFloat16));
+  at::Tensor wd = at::empty({Ci, kh, kw, Co}, w.options().dtype(at::kBFloat16));
+  kern::weight_cast_t(wf.data_ptr<float>(), wb.data_ptr(), wd.data_ptr(), static_cast<int>(Co), static_cast<int>(Ci),
+                      stream_of(w), static_cast<int>(kh * kw));
+  return {wb, wd};
+}
+
 // dx[M, Cin] = gy[M, Cout] · w[Cout, Cin]; wt = w^T contiguous [Cin, Cout] bf16
 at::Tensor conv1x1_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
   check_gemm_act(gy, "conv1x1_dgrad");
@@ -749,7 +765,9 @@ kern::PoolGeom pool_geom(const at::Tensor& x, int64_t k, int64_t s, int64_t p) {
 }
 
 bool maxpool_supported(const at::Tensor& x, int64_t k, int64_t p) {
+  // kernels index (pixel, 8-channel group) in 32 bits
   return x.is_cuda() && x.dim() == 4 && x.size(1) % 8 == 0 && k * k <= 255 && 2 * p <= k &&
+         x.numel() / 8 < (int64_t(1) << 31) &&
          (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) &&
          x.is_contiguous(at::MemoryFormat::ChannelsLast);
 }
@@ -903,6 +921,7 @@ void bind(pybind11::module& m) {
         pybind11::arg("gy"), pybind11::arg("x"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"),
         pybind11::arg("pad"));
   m.def("weight_bf16_t", &weight_bf16_t, "fp32 weight -> (bf16 [R,C], bf16 transposed [C,R]) in one launch");
+  m.def("conv_weight_bf16", &conv_weight_bf16, "kxk weight -> (bf16 fwd [Co][kh][kw][Ci], bf16 flipped [Ci][kh][kw][Co])");
   m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("gy"), pybind11::arg("x"),
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
         pybind11::arg("relu") = false);

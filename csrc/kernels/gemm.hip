@@ -702,18 +702,23 @@ __global__ void __launch_bounds__(kT) slab_partial_kernel(const float4* __restri
 }
 
 // fp32 [R][Cc] weight → bf16 w [R][Cc] and w^T [Cc][R] (RNE), one launch
+// w fp32 [R][T][Cc] → wb bf16 (same layout) and wt bf16 [Cc][T][R] with the
+// tap index reversed (t → T-1-t): for T = 1 the plain transpose (1x1 dgrad
+// operand), for a kxk conv weight [Cout][kh][kw][Cin] the flipped, transposed
+// [Cin][kh][kw][Cout] operand of the stride-1 data gradient. grid.z = tap.
 __global__ void __launch_bounds__(kT) weight_cast_t_kernel(const float* __restrict__ w, uint16_t* __restrict__ wb,
-                                                           uint16_t* __restrict__ wt, int R, int Cc) {
+                                                           uint16_t* __restrict__ wt, int R, int Cc, int T) {
   __shared__ uint16_t tile[32][33];
-  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32, tap = blockIdx.z;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 × 8
 #pragma unroll
   for (int k = 0; k < 32; k += 8) {
     const int r = r0 + ty + k, c = c0 + tx;
     if (r < R && c < Cc) {
-      const __bf16 h = static_cast<__bf16>(w[static_cast<int64_t>(r) * Cc + c]);
+      const int64_t i = (static_cast<int64_t>(r) * T + tap) * Cc + c;
+      const __bf16 h = static_cast<__bf16>(w[i]);
       const uint16_t u = __builtin_bit_cast(uint16_t, h);
-      wb[static_cast<int64_t>(r) * Cc + c] = u;
+      wb[i] = u;
       tile[ty + k][tx] = u;
     }
   }
@@ -721,7 +726,7 @@ __global__ void __launch_bounds__(kT) weight_cast_t_kernel(const float* __restri
 #pragma unroll
   for (int k = 0; k < 32; k += 8) {
     const int c = c0 + ty + k, r = r0 + tx;
-    if (r < R && c < Cc) wt[static_cast<int64_t>(c) * R + r] = tile[tx][ty + k];
+    if (r < R && c < Cc) wt[(static_cast<int64_t>(c) * T + (T - 1 - tap)) * R + r] = tile[tx][ty + k];
   }
 }
 
@@ -898,10 +903,10 @@ void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, 
                        stats, geo, s);
 }
 
-void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s) {
-  const dim3 grid((Cc + 31) / 32, (R + 31) / 32);
+void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s, int taps) {
+  const dim3 grid((Cc + 31) / 32, (R + 31) / 32, taps);
   hipLaunchKernelGGL(weight_cast_t_kernel, grid, dim3(kT), 0, s, w, static_cast<uint16_t*>(wb),
-                     static_cast<uint16_t*>(wt), R, Cc);
+                     static_cast<uint16_t*>(wt), R, Cc, taps);
 }
 
 void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s) {

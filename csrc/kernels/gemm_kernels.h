@@ -29,7 +29,7 @@ void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
 
 // fp32 weight [R][Cc] → bf16 copy wb [R][Cc] and transposed bf16 wt [Cc][R]
 // (the forward GEMM's B operand and the dgrad GEMM's B operand) in one launch.
-void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s);
+void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s, int taps = 1);
 
 // out[N] (fp32, ZEROED) += column sums of a bf16 [M, N] matrix (N % 8 == 0):
 // one launch, ≤ 64 row slabs × N/256 column chunks, one fp32 atomic per column

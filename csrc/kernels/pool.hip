@@ -86,16 +86,18 @@ template <int D>
 __global__ void __launch_bounds__(kT) maxpool_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
                                                          uint8_t* __restrict__ idx, PoolGeom g, PoolEpi e) {
   const uint64_t doff = e.offset + (e.offset_dev ? static_cast<uint64_t>(*e.offset_dev) : 0);
+  // flat (n, oh, ow, 8-channel group) index in 32-bit math (the host checks the
+  // element count fits): 64-bit divisions cost more than the window loads
   const int cv = g.C / 8;
-  const int64_t total = static_cast<int64_t>(g.N) * g.OH * g.OW * cv;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x; t < total;
-       t += static_cast<int64_t>(gridDim.x) * kT) {
-    const int c8 = static_cast<int>(t % cv);
-    int64_t r = t / cv;
-    const int ow = static_cast<int>(r % g.OW);
+  const int total = g.N * g.OH * g.OW * cv;
+  for (int ti = blockIdx.x * kT + threadIdx.x; ti < total; ti += gridDim.x * kT) {
+    const int c8 = ti % cv;
+    int r = ti / cv;
+    const int ow = r % g.OW;
     r /= g.OW;
-    const int oh = static_cast<int>(r % g.OH);
-    const int n = static_cast<int>(r / g.OH);
+    const int oh = r % g.OH;
+    const int n = r / g.OH;
+    const int64_t t = ti;
     float m[8];
     uint8_t a[8];
 #pragma unroll
@@ -144,25 +146,101 @@ __global__ void __launch_bounds__(kT) maxpool_fwd_kernel(const void* __restrict_
   }
 }
 
+// 3x3 / stride 2 / pad 1 backward (the ResNet stem pool): thread per output
+// position (n, oh, ow, 8 channels) owning the 2x2 input block (2oh + {0,1},
+// 2ow + {0,1}); its gradient comes only from outputs (oh + {0,1}, ow + {0,1}),
+// whose window offsets say which block pixel (if any) each argmax hits. No
+// data-dependent loop bounds (the generic gather diverges on w's parity), each
+// input pixel written exactly once, no atomics.
+template <int D>
+__global__ void __launch_bounds__(kT) maxpool_bwd_k3s2_kernel(const void* __restrict__ gy,
+                                                              const void* __restrict__ gy2,
+                                                              const uint8_t* __restrict__ idx, void* __restrict__ gx,
+                                                              PoolGeom g, PoolEpi e) {
+  const uint64_t doff = e.offset + (e.offset_dev ? static_cast<uint64_t>(*e.offset_dev) : 0);
+  const int cv = g.C / 8;
+  const int total = g.N * g.OH * g.OW * cv;
+  for (int ti = blockIdx.x * kT + threadIdx.x; ti < total; ti += gridDim.x * kT) {
+    const int c8 = ti % cv;
+    int r = ti / cv;
+    const int ow = r % g.OW;
+    r /= g.OW;
+    const int oh = r % g.OH;
+    const int n = r / g.OH;
+    float acc[2][2][8];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[a][b][k] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const int oy = oh + dy, ox = ow + dx;
+        if (oy >= g.OH || ox >= g.OW) continue;
+        const int64_t o = ((static_cast<int64_t>(n) * g.OH + oy) * g.OW + ox) * g.C + c8 * 8;
+        const uint2 pk = *reinterpret_cast<const uint2*>(idx + o);
+        const uint32_t wv[2] = {pk.x, pk.y};
+        float gv[8];
+        P8<D>::ld(gy, o, gv);
+        if (gy2) {
+          float g2[8];
+          P8<D>::ld(gy2, o, g2);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) gv[k] += g2[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int a = static_cast<int>((wv[k >> 2] >> (8 * (k & 3))) & 0xff);
+          const int ii = a / 3, jj = a - 3 * (a / 3);
+          // block-local pixel of input (2oy - 1 + ii, 2ox - 1 + jj)
+          const int li = 2 * dy - 1 + ii, lj = 2 * dx - 1 + jj;
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) acc[bi][bj][k] += (li == bi && lj == bj) ? gv[k] : 0.f;
+        }
+      }
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        const int h = 2 * oh + bi, w = 2 * ow + bj;
+        if (h >= g.H || w >= g.W) continue;
+        if (e.thr) {
+          float sc[8];
+          drop_scales(e, doff, n, g.C, c8 * 8, sc);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[bi][bj][k] *= sc[k];
+        }
+        P8<D>::st(gx, ((static_cast<int64_t>(n) * g.H + h) * g.W + w) * g.C + c8 * 8, acc[bi][bj]);
+      }
+  }
+}
+
 template <int D>
 __global__ void __launch_bounds__(kT) maxpool_bwd_kernel(const void* __restrict__ gy, const void* __restrict__ gy2,
                                                          const uint8_t* __restrict__ idx, void* __restrict__ gx,
                                                          PoolGeom g, PoolEpi e) {
   const uint64_t doff = e.offset + (e.offset_dev ? static_cast<uint64_t>(*e.offset_dev) : 0);
+  // grid: y over input rows (n, h), x over (w, 8-channel group) of the row —
+  // 32-bit index math only (the flat 64-bit t → (n, h, w, c) divisions cost
+  // more than the memory traffic)
   const int cv = g.C / 8;
-  const int64_t total = static_cast<int64_t>(g.N) * g.H * g.W * cv;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x; t < total;
-       t += static_cast<int64_t>(gridDim.x) * kT) {
-    const int c8 = static_cast<int>(t % cv);
-    int64_t r = t / cv;
-    const int w = static_cast<int>(r % g.W);
-    r /= g.W;
-    const int h = static_cast<int>(r % g.H);
-    const int n = static_cast<int>(r / g.H);
+  const int per_row = g.W * cv;
+  for (int row = blockIdx.y; row < g.N * g.H; row += gridDim.y) {
+  const int h = row % g.H;
+  const int n = row / g.H;
+  // output rows whose window [oh*S-P, oh*S-P+K) contains h
+  const int oh_lo = max(0, (h + g.P - g.K + g.S) / g.S);
+  const int oh_hi = min(g.OH - 1, (h + g.P) / g.S);
+  for (int tt = blockIdx.x * kT + threadIdx.x; tt < per_row; tt += gridDim.x * kT) {
+    const int c8 = tt % cv;
+    const int w = tt / cv;
+    const int64_t t = static_cast<int64_t>(row) * per_row + tt;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    // output rows whose window [oh*S-P, oh*S-P+K) contains h
-    const int oh_lo = max(0, (h + g.P - g.K + g.S) / g.S);
-    const int oh_hi = min(g.OH - 1, (h + g.P) / g.S);
     const int ow_lo = max(0, (w + g.P - g.K + g.S) / g.S);
     const int ow_hi = min(g.OW - 1, (w + g.P) / g.S);
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
@@ -198,7 +276,9 @@ __global__ void __launch_bounds__(kT) maxpool_bwd_kernel(const void* __restrict_
     }
     P8<D>::st(gx, t * 8, acc);
   }
+  }
 }
+
 
 inline dim3 grid_for(int64_t work) {
   int64_t g = (work + kT - 1) / kT;
@@ -218,7 +298,17 @@ void maxpool2d_forward(int dtype, const void* x, void* y, uint8_t* idx, const Po
 
 void maxpool2d_backward(int dtype, const void* gy, const void* gy2, const uint8_t* idx, void* gx, const PoolGeom& g,
                         const PoolEpi& e, hipStream_t s) {
-  const dim3 grid = grid_for(static_cast<int64_t>(g.N) * g.H * g.W * (g.C / 8));
+  if (g.K == 3 && g.S == 2 && g.P == 1 && 2 * g.OH >= g.H && 2 * g.OW >= g.W) {
+    const dim3 grid = grid_for(static_cast<int64_t>(g.N) * g.OH * g.OW * (g.C / 8));
+    if (dtype == POOL_BF16)
+      hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<POOL_BF16>, grid, dim3(kT), 0, s, gy, gy2, idx, gx, g, e);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<POOL_F32>, grid, dim3(kT), 0, s, gy, gy2, idx, gx, g, e);
+    return;
+  }
+  const int per_row = g.W * (g.C / 8);
+  const int rows = g.N * g.H;
+  const dim3 grid((per_row + kT - 1) / kT, rows < 65535 ? rows : 65535);
   if (dtype == POOL_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<POOL_BF16>, grid, dim3(kT), 0, s, gy, gy2, idx, gx, g, e);
   else

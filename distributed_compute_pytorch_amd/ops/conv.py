@@ -234,26 +234,30 @@ class _ConvKxKGemmFn(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         w = weight.detach().to(torch.bfloat16)
         kh, kw = w.shape[2], w.shape[3]
+        wd = None
         if miopen_fwd:  # the caller computes the output statistics itself
             y = _cl(F.conv2d(x, w, None, stride, padding))
             st = torch.empty(0, device=x.device, dtype=torch.float32)
         else:
-            y, st = _C.conv_fwd(x, w.permute(0, 2, 3, 1).contiguous(), kh, kw, stride, padding, stats)
-        ctx.save_for_backward(x, w)
+            # both bf16 operands (forward, flipped data-gradient) from one cast launch
+            wf, wd = _C.conv_weight_bf16(weight) if kh == kw else (w.permute(0, 2, 3, 1).contiguous(), None)
+            y, st = _C.conv_fwd(x, wf, kh, kw, stride, padding, stats)
+        ctx.save_for_backward(x, w, wd)
         ctx.cfg = (stride, padding, weight.dtype, miopen_wgrad)
         ctx.mark_non_differentiable(st)
         return y, st
 
     @staticmethod
     def backward(ctx, gy, _gst=None):
-        x, w = ctx.saved_tensors
+        x, w, wd = ctx.saved_tensors
         s, p, wdtype, miopen_wgrad = ctx.cfg
         gy = _cl(gy)
         kh, kw = w.shape[2], w.shape[3]
         dx = dw = None
         if ctx.needs_input_grad[0]:
             if s == 1 and kh - 1 - p >= 0 and kw == kh:
-                wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Cin][kh][kw][Cout]
+                if wd is None:
+                    wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Cin][kh][kw][Cout]
                 dx = _C.conv_fwd(gy, wd, kh, kw, 1, kh - 1 - p, False)[0]
             else:
                 dx = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,

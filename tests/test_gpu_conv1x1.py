@@ -300,3 +300,14 @@ def test_bn_relu_conv_fused_autograd(cuda, k, stride, pad, sums):
     assert conv.weight.grad.dtype == torch.float32 and _rel(conv.weight.grad, ref_conv.weight.grad) < 2e-2
     torch.testing.assert_close(bn.running_mean, ref_bn.running_mean, rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(bn.running_var, ref_bn.running_var, rtol=1e-3, atol=1e-3)
+
+
+def test_conv_weight_bf16_layouts(cuda):
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    g = torch.Generator().manual_seed(14)
+    w = torch.randn(96, 64, 3, 3, generator=g).to(cuda).contiguous(memory_format=torch.channels_last)
+    wf, wd = _C.conv_weight_bf16(w)
+    wb = w.to(torch.bfloat16)
+    assert torch.equal(wf, wb.permute(0, 2, 3, 1).contiguous())
+    assert torch.equal(wd, wb.flip(2, 3).permute(1, 2, 3, 0).contiguous())
