@@ -434,6 +434,24 @@ std::vector<at::Tensor> conv_dgrad_bnred(const at::Tensor& gy, const at::Tensor&
   return {dy, acc};
 }
 
+// dx of a stride-2 pad-0 1x1 conv on an even-sized input (ResNet downsample):
+// GEMM on gy with a scattering epilogue; wt = Wᵀ bf16 [Cin][Cout].
+at::Tensor conv1x1_s2_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
+  check_gemm_act(gy, "conv1x1_s2_dgrad");
+  DCP_CHECK(gy.dim() == 4, "conv1x1_s2_dgrad: NHWC 4-D gradient required");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t N = gy.size(0), Co = gy.size(1), Ho = gy.size(2), Wo = gy.size(3);
+  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % Co == 0,
+            "conv1x1_s2_dgrad: weight");
+  const int64_t Ci = wt.numel() / Co;
+  DCP_CHECK(kern::gemm_nt_supported(N * Ho * Wo, Ci, Co) && N * 4 * Ho * Wo < (int64_t(1) << 31),
+            "conv1x1_s2_dgrad: unsupported shape");
+  at::Tensor dx = at::empty({N, Ci, 2 * Ho, 2 * Wo}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  kern::conv1x1_s2_dgrad_bf16(gy.data_ptr(), wt.data_ptr(), dx.data_ptr(), static_cast<int>(N), static_cast<int>(Ho),
+                              static_cast<int>(Wo), static_cast<int>(Co), static_cast<int>(Ci), stream_of(gy));
+  return dx;
+}
+
 // fp32 [N] column sums of a bf16 [.., N] tensor (Linear bias gradient)
 at::Tensor colsum(const at::Tensor& x) {
   DCP_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() >= 1,
@@ -917,6 +935,7 @@ void bind(pybind11::module& m) {
   m.def("conv1x1_dgrad_bnred", &conv1x1_dgrad_bnred, "1x1 data gradient + BN/ReLU backward reduction epilogue");
   m.def("conv_dgrad_bnred", &conv_dgrad_bnred, "stride-1 kxk data gradient + BN/ReLU backward reduction epilogue");
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply, "BN/ReLU training backward apply from a precomputed reduction");
+  m.def("conv1x1_s2_dgrad", &conv1x1_s2_dgrad, "stride-2 1x1 conv data gradient (GEMM + scattering epilogue)");
   m.def("conv_wgrad", &conv_wgrad, "kxk NHWC conv weight gradient (implicit-GEMM MFMA, fp32 out)",
         pybind11::arg("gy"), pybind11::arg("x"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"),
         pybind11::arg("pad"));

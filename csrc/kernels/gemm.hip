@@ -67,21 +67,10 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
 // wait until at most N vector-memory ops of this wave are outstanding
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 11) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-  else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if constexpr (N == 22) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
-  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else if constexpr (N == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-  else static_assert(N == 0, "add a vmcnt case");
+  // vmcnt is 6 bits on gfx950: a larger "allowed outstanding" is clamped,
+  // which only waits for more (older) ops — ops retire in issue order
+  constexpr int n = N > 63 ? 63 : N;
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory");
 }
 __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
@@ -168,6 +157,11 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
   constexpr bool STATS = EPI == 1;
   constexpr bool RED = EPI == 2;
+  // EPI 3 = SCATTER2: the data gradient of a stride-2 1x1 convolution. Row m =
+  // gy pixel (n, ho, wo) (geo.Ho × geo.Wo) is stored at dx pixel (n, 2ho, 2wo)
+  // of the geo.H × geo.W (= 2Ho × 2Wo) input, and the three pixels the stride
+  // skipped get zeros — dx fully written, no memset pass.
+  constexpr bool SCAT = EPI == 3;
   static_assert(!(PRO && RED), "RED is a data-gradient epilogue");
   constexpr int kNSnt = nt_stages<BK>();
   constexpr int RB = BK * 2;                                  // stage row bytes
@@ -180,7 +174,7 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
   constexpr int CST = 32 * WN * 2;           // per-wave C staging: 32 rows × WN bf16
   constexpr int LPR = WN / 8;                // lanes per staged row (16 B each)
   constexpr int RPI = 64 / LPR;              // staged rows per store instruction
-  constexpr int FS = 2 * (32 / RPI);         // global stores per wave per tile
+  constexpr int FS = 2 * (32 / RPI) * (EPI == 3 ? 4 : 1);  // global stores per wave per tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* cst_all = lds + kNSnt * STAGE;
   float* pro = reinterpret_cast<float*>(cst_all + 4 * CST);  // [2][K] scale, shift (PRO)
@@ -406,7 +400,18 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
           const int c = lane % LPR;
           const uint4 v = *reinterpret_cast<const uint4*>(cst + row * (WN * 2) + 16 * (c ^ (row & 7 & (LPR - 1))));
           const int64_t m = mt + 32 * h + row;
-          if (m < M) {
+          if (m < M && SCAT) {
+            const int mi = static_cast<int>(m);
+            const int wo = mi % geo.Wo, t1 = mi / geo.Wo;
+            const int ho = t1 % geo.Ho, nn = t1 / geo.Ho;
+            const int64_t d0 = (static_cast<int64_t>(nn * geo.H + 2 * ho) * geo.W + 2 * wo) * N + n0 + wn * WN + c * 8;
+            const int64_t rowp = static_cast<int64_t>(geo.W) * N;
+            const uint4 z = make_uint4(0, 0, 0, 0);
+            *reinterpret_cast<uint4*>(C + d0) = v;
+            *reinterpret_cast<uint4*>(C + d0 + N) = z;
+            *reinterpret_cast<uint4*>(C + d0 + rowp) = z;
+            *reinterpret_cast<uint4*>(C + d0 + rowp + N) = z;
+          } else if (m < M) {
             *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) = v;
             if (STATS) {
               const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
@@ -810,7 +815,7 @@ inline int nt_bk() {
 template <bool GATHER, int BK>
 void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                        const float* shift, bool relu, float* stats, const ConvGeo& geo, const BnRedArgs* red,
-                       hipStream_t s) {
+                       hipStream_t s, bool scatter2 = false) {
   const int BN = N % 128 == 0 ? 128 : 64;
   constexpr int BM = 128;
   const int tiles_m = static_cast<int>((M + BM - 1) / BM);
@@ -838,6 +843,12 @@ void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, 
     if (red) {                                   \
       DCP_GNT(BN_, false, 2);                    \
       break;                                     \
+    }                                            \
+    if constexpr (!GATHER) {                     \
+      if (scatter2) {                            \
+        DCP_GNT(BN_, false, 3);                  \
+        break;                                   \
+      }                                          \
     }                                            \
     if constexpr (!GATHER) {                     \
       if (pro && st) {                           \
@@ -890,6 +901,16 @@ void conv_fwd_bnred_bf16(const void* X, const void* Wt, void* Y, int N, int H, i
   const BnRedArgs r{static_cast<const uint16_t*>(x), gamma, beta, mean, invstd};
   gemm_nt_launch<true>(X, Wt, Y, static_cast<int64_t>(N) * Ho * Wo, Cout, kh * kw * Cin, nullptr, nullptr, false,
                        acc, geo, s, &r);
+}
+
+void conv1x1_s2_dgrad_bf16(const void* dY, const void* Wt, void* dX, int N, int Ho, int Wo, int Cout, int Cin,
+                           hipStream_t s) {
+  ConvGeo geo{2 * Ho, 2 * Wo, Ho, Wo, 2, 0, 1, nullptr, 0};
+  const int64_t M = static_cast<int64_t>(N) * Ho * Wo;
+  if (nt_bk() == 64)
+    gemm_nt_launch_bk<false, 64>(dY, Wt, dX, M, Cin, Cout, nullptr, nullptr, false, nullptr, geo, nullptr, s, true);
+  else
+    gemm_nt_launch_bk<false, 32>(dY, Wt, dX, M, Cin, Cout, nullptr, nullptr, false, nullptr, geo, nullptr, s, true);
 }
 
 bool conv_fwd_supported(int Cin, int Cout, int kh, int kw) {

@@ -66,6 +66,11 @@ void conv_fwd_bnred_bf16(const void* X, const void* Wt, void* Y, int N, int H, i
                          int Cout, int kh, int kw, int stride, int pad, const void* zero, const void* x,
                          const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,
                          hipStream_t s);
+// Data gradient of a stride-2, pad-0 1x1 convolution over an even 2Ho × 2Wo
+// input: dX [N, 2Ho, 2Wo, Cin] (every pixel written: the skipped 3/4 get
+// zeros) from dY [N, Ho, Wo, Cout] and Wt = Wᵀ bf16 [Cin][Cout].
+void conv1x1_s2_dgrad_bf16(const void* dY, const void* Wt, void* dX, int N, int Ho, int Wo, int Cout, int Cin,
+                           hipStream_t s);
 bool conv_fwd_supported(int Cin, int Cout, int kh, int kw);
 void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                    int kh, int kw, int stride, int pad, const void* zero, float* stats, hipStream_t s);

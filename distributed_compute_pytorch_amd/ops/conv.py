@@ -259,6 +259,10 @@ class _ConvKxKGemmFn(torch.autograd.Function):
                 if wd is None:
                     wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Cin][kh][kw][Cout]
                 dx = _C.conv_fwd(gy, wd, kh, kw, 1, kh - 1 - p, False)[0]
+            elif (kh == kw == 1 and s == 2 and p == 0 and wd is not None and x.shape[2] == 2 * gy.shape[2]
+                  and x.shape[3] == 2 * gy.shape[3]):
+                # strided 1x1 (downsample): GEMM whose epilogue scatters to the even pixels, zeros the rest
+                dx = _C.conv1x1_s2_dgrad(gy, wd)
             else:
                 dx = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]
