@@ -452,6 +452,33 @@ at::Tensor conv1x1_s2_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
   return dx;
 }
 
+// dx of a stride-2 kxk conv as four parity-class implicit GEMMs (each dx
+// pixel written exactly once). wsubs: 4 bf16 [Cin][nkh][nkw][Cout] tensors for
+// (ph, pw) = (0,0), (0,1), (1,0), (1,1); x_hw: dx's H, W.
+at::Tensor conv_dgrad_s2(const at::Tensor& gy, const std::vector<at::Tensor>& wsubs, int64_t H, int64_t W) {
+  check_gemm_act(gy, "conv_dgrad_s2");
+  DCP_CHECK(gy.dim() == 4 && wsubs.size() == 4, "conv_dgrad_s2: NHWC gy and 4 weight subsets required");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t N = gy.size(0), Co = gy.size(1), Hg = gy.size(2), Wg = gy.size(3);
+  const int64_t Ci = wsubs[0].size(0);
+  DCP_CHECK(Ci % 64 == 0 && Co % 64 == 0 && N * H * W < (int64_t(1) << 31) && H <= 2 * Hg + 1 && W <= 2 * Wg + 1,
+            "conv_dgrad_s2: unsupported shape");
+  at::Tensor dx = at::empty({N, Ci, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  for (int q = 0; q < 4; ++q) {
+    const at::Tensor& w = wsubs[q];
+    DCP_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4 && w.size(0) == Ci &&
+                  w.size(3) == Co,
+              "conv_dgrad_s2: weight subset must be bf16 [Cin][nkh][nkw][Cout]");
+    const int ph = q >> 1, pw = q & 1;
+    if (ph >= H || pw >= W) continue;
+    kern::conv_dgrad_parity_bf16(gy.data_ptr(), w.data_ptr(), dx.data_ptr(), static_cast<int>(N),
+                                 static_cast<int>(Hg), static_cast<int>(Wg), static_cast<int>(Co), static_cast<int>(H),
+                                 static_cast<int>(W), static_cast<int>(Ci), ph, pw, static_cast<int>(w.size(1)),
+                                 static_cast<int>(w.size(2)), zero_row(gy).data_ptr(), stream_of(gy));
+  }
+  return dx;
+}
+
 // fp32 [N] column sums of a bf16 [.., N] tensor (Linear bias gradient)
 at::Tensor colsum(const at::Tensor& x) {
   DCP_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() >= 1,
@@ -936,6 +963,7 @@ void bind(pybind11::module& m) {
   m.def("conv_dgrad_bnred", &conv_dgrad_bnred, "stride-1 kxk data gradient + BN/ReLU backward reduction epilogue");
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply, "BN/ReLU training backward apply from a precomputed reduction");
   m.def("conv1x1_s2_dgrad", &conv1x1_s2_dgrad, "stride-2 1x1 conv data gradient (GEMM + scattering epilogue)");
+  m.def("conv_dgrad_s2", &conv_dgrad_s2, "stride-2 kxk conv data gradient as four parity-class implicit GEMMs");
   m.def("conv_wgrad", &conv_wgrad, "kxk NHWC conv weight gradient (implicit-GEMM MFMA, fp32 out)",
         pybind11::arg("gy"), pybind11::arg("x"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"),
         pybind11::arg("pad"));

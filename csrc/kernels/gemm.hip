@@ -124,6 +124,9 @@ struct ConvGeo {
   int H, W, Ho, Wo, stride, pad, kw;
   const uint16_t* zero;  // ≥ 256 zero bytes
   int cin;               // input channels (gemm_nt GATHER)
+  // EPI 4 (parity scatter): row (n, a, b) of the Ho × Wo row grid is stored at
+  // pixel (n, 2a + ph, 2b + pw) of the oh × ow output
+  int oh, ow, ph, pw;
 };
 
 // BatchNorm (training) of the tensor whose gradient a gemm_nt RED epilogue
@@ -162,6 +165,10 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
   // of the geo.H × geo.W (= 2Ho × 2Wo) input, and the three pixels the stride
   // skipped get zeros — dx fully written, no memset pass.
   constexpr bool SCAT = EPI == 3;
+  // EPI 4 = PARITY: one of the four parity classes of a stride-2 kxk data
+  // gradient (rows = dx pixels (2a+ph, 2b+pw), gathered from gy over the taps
+  // of matching parity); stored to its pixel of the full dx
+  constexpr bool PAR = EPI == 4;
   static_assert(!(PRO && RED), "RED is a data-gradient epilogue");
   constexpr int kNSnt = nt_stages<BK>();
   constexpr int RB = BK * 2;                                  // stage row bytes
@@ -411,6 +418,13 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
             *reinterpret_cast<uint4*>(C + d0 + N) = z;
             *reinterpret_cast<uint4*>(C + d0 + rowp) = z;
             *reinterpret_cast<uint4*>(C + d0 + rowp + N) = z;
+          } else if (m < M && PAR) {
+            const int mi = static_cast<int>(m);
+            const int b = mi % geo.Wo, t1 = mi / geo.Wo;
+            const int a = t1 % geo.Ho, nn = t1 / geo.Ho;
+            *reinterpret_cast<uint4*>(
+                C + (static_cast<int64_t>(nn * geo.oh + 2 * a + geo.ph) * geo.ow + 2 * b + geo.pw) * N + n0 + wn * WN +
+                c * 8) = v;
           } else if (m < M) {
             *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) = v;
             if (STATS) {
@@ -815,7 +829,7 @@ inline int nt_bk() {
 template <bool GATHER, int BK>
 void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                        const float* shift, bool relu, float* stats, const ConvGeo& geo, const BnRedArgs* red,
-                       hipStream_t s, bool scatter2 = false) {
+                       hipStream_t s, bool scatter2 = false, bool parity = false) {
   const int BN = N % 128 == 0 ? 128 : 64;
   constexpr int BM = 128;
   const int tiles_m = static_cast<int>((M + BM - 1) / BM);
@@ -847,6 +861,11 @@ void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, 
     if constexpr (!GATHER) {                     \
       if (scatter2) {                            \
         DCP_GNT(BN_, false, 3);                  \
+        break;                                   \
+      }                                          \
+    } else {                                     \
+      if (parity) {                              \
+        DCP_GNT(BN_, false, 4);                  \
         break;                                   \
       }                                          \
     }                                            \
@@ -911,6 +930,20 @@ void conv1x1_s2_dgrad_bf16(const void* dY, const void* Wt, void* dX, int N, int 
     gemm_nt_launch_bk<false, 64>(dY, Wt, dX, M, Cin, Cout, nullptr, nullptr, false, nullptr, geo, nullptr, s, true);
   else
     gemm_nt_launch_bk<false, 32>(dY, Wt, dX, M, Cin, Cout, nullptr, nullptr, false, nullptr, geo, nullptr, s, true);
+}
+
+void conv_dgrad_parity_bf16(const void* dY, const void* Wsub, void* dX, int N, int Hg, int Wg, int Cout, int Hdx,
+                            int Wdx, int Cin, int ph, int pw, int nkh, int nkw, const void* zero, hipStream_t s) {
+  const int Hq = (Hdx - ph + 1) / 2, Wq = (Wdx - pw + 1) / 2;
+  ConvGeo geo{Hg, Wg, Hq, Wq, 1, 0, nkw, static_cast<const uint16_t*>(zero), Cout, Hdx, Wdx, ph, pw};
+  const int64_t M = static_cast<int64_t>(N) * Hq * Wq;
+  const int K = nkh * nkw * Cout;
+  if (nt_bk() == 64)
+    gemm_nt_launch_bk<true, 64>(dY, Wsub, dX, M, Cin, K, nullptr, nullptr, false, nullptr, geo, nullptr, s, false,
+                                true);
+  else
+    gemm_nt_launch_bk<true, 32>(dY, Wsub, dX, M, Cin, K, nullptr, nullptr, false, nullptr, geo, nullptr, s, false,
+                                true);
 }
 
 bool conv_fwd_supported(int Cin, int Cout, int kh, int kw) {

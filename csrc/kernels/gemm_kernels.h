@@ -71,6 +71,12 @@ void conv_fwd_bnred_bf16(const void* X, const void* Wt, void* Y, int N, int H, i
 // zeros) from dY [N, Ho, Wo, Cout] and Wt = Wᵀ bf16 [Cin][Cout].
 void conv1x1_s2_dgrad_bf16(const void* dY, const void* Wt, void* dX, int N, int Ho, int Wo, int Cout, int Cin,
                            hipStream_t s);
+// One parity class (ph, pw) of a stride-2 kxk data gradient: dX pixels
+// (2a+ph, 2b+pw) of the Hdx × Wdx input = implicit GEMM over gy [N,Hg,Wg,Cout]
+// with the nkh × nkw taps of matching parity (source offsets 0.., stride 1),
+// Wsub bf16 [Cin][nkh][nkw][Cout] in increasing-offset tap order.
+void conv_dgrad_parity_bf16(const void* dY, const void* Wsub, void* dX, int N, int Hg, int Wg, int Cout, int Hdx,
+                            int Wdx, int Cin, int ph, int pw, int nkh, int nkw, const void* zero, hipStream_t s);
 bool conv_fwd_supported(int Cin, int Cout, int kh, int kw);
 void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                    int kh, int kw, int stride, int pad, const void* zero, float* stats, hipStream_t s);

@@ -18,6 +18,7 @@ reference framework's cuDNN/cuBLAS role).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -222,6 +223,22 @@ def conv_kxk(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -
     return _ConvKxKFn.apply(x, weight, stride, padding)
 
 
+# stride-2 3x3 data gradient as parity-class GEMMs (opt-in until it beats MIOpen)
+_S2_PARITY = os.environ.get("DCP_S2_DGRAD_PARITY", "0") == "1"
+
+
+def _parity_weights(wd: torch.Tensor):
+    """bf16 [Cin][nkh][nkw][Cout] weight subsets of a 3x3 / stride-2 / pad-1
+    conv for dx parity classes (ph, pw) = 00, 01, 10, 11, as strided views of
+    the flipped data-gradient weight wd [Cin][3][3][Cout] (wd[.., kh', ..] =
+    w[.., 2-kh', ..]): dx row 2a+ph takes kernel rows kh ≡ ph+1 (mod 2) from gy
+    rows a + (ph+1-kh)/2, ordered by that offset (even: kh 1 → +0; odd: kh 2 →
+    +0, kh 0 → +1, i.e. kh' = 0, 2). No index tensors (list indexing copies
+    them host→device and stalls the launch stream)."""
+    sl = (slice(1, 2), slice(0, 3, 2))
+    return [wd[:, sl[ph], sl[pw], :].contiguous() for ph in (0, 1) for pw in (0, 1)]
+
+
 class _ConvKxKGemmFn(torch.autograd.Function):
     """kxk NHWC convolution on the implicit-GEMM MFMA kernels (gemm.hip
     GATHER): forward (+ the next BatchNorm's Σy, Σy² from the epilogue), data
@@ -263,6 +280,11 @@ class _ConvKxKGemmFn(torch.autograd.Function):
                   and x.shape[3] == 2 * gy.shape[3]):
                 # strided 1x1 (downsample): GEMM whose epilogue scatters to the even pixels, zeros the rest
                 dx = _C.conv1x1_s2_dgrad(gy, wd)
+            elif _S2_PARITY and kh == kw == 3 and s == 2 and p == 1 and x.shape[1] % 64 == 0:
+                # four parity classes of dx, each an implicit GEMM over its 1/2/4 matching taps
+                if wd is None:
+                    wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+                dx = _C.conv_dgrad_s2(gy, _parity_weights(wd), x.shape[2], x.shape[3])
             else:
                 dx = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]

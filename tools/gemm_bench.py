@@ -103,7 +103,12 @@ def main():
         wf = w4.permute(0, 2, 3, 1).contiguous()
         wd = w4.flip(2, 3).permute(1, 2, 3, 0).contiguous()
         us_of = timeit(lambda: _C.conv_fwd(x, wf, 3, 3, st, 1, True), a.iters)
-        us_od = timeit(lambda: _C.conv_fwd(gy, wd, 3, 3, 1, 1, False), a.iters) if st == 1 else float("nan")
+        if st == 1:
+            us_od = timeit(lambda: _C.conv_fwd(gy, wd, 3, 3, 1, 1, False), a.iters)
+        else:
+            from distributed_compute_pytorch_amd.ops.conv import _parity_weights
+            subs = _parity_weights(wd)
+            us_od = timeit(lambda: _C.conv_dgrad_s2(gy, subs, hw, hw), a.iters)
         flops = 2.0 * a.batch * ho * ho * c * c * 9
         r3 = {"shape3x3": f"{hw}x{hw} c={c} s={st}", "ours_wgrad_us": round(us_o, 1), "miopen_wgrad_us": round(us_m, 1),
               "miopen_dgrad_us": round(us_d, 1), "miopen_fwd_us": round(us_f, 1),
