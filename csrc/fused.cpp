@@ -271,7 +271,8 @@ at::Tensor conv1x1_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
 
 // dw[Cout, Cin] (fp32) = Σ_m gy[m, :]^T ⊗ f(x)[m, :]
 at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::optional<at::Tensor>& scale,
-                         const c10::optional<at::Tensor>& shift, bool relu) {
+                         const c10::optional<at::Tensor>& shift, bool relu,
+                         const c10::optional<at::Tensor>& accumulate_into) {
   check_gemm_act(gy, "conv1x1_wgrad");
   check_gemm_act(x, "conv1x1_wgrad");
   c10::hip::HIPGuard guard(gy.device().index());
@@ -281,11 +282,18 @@ at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::o
   DCP_CHECK(N1 % 64 == 0 && N2 % 64 == 0, "conv1x1_wgrad: channels must be multiples of 64");
   const float* sc = vec_or_null(scale, N2, "conv1x1_wgrad");
   const float* sf = vec_or_null(shift, N2, "conv1x1_wgrad");
-  at::Tensor dw = at::empty({N1, N2}, gy.options().dtype(at::kFloat));
+  // accumulate_into: an existing fp32 [N1, N2] gradient that receives += dW in
+  // the final slab-reduction pass (gradient-accumulation micro-steps)
+  const bool acc = accumulate_into.has_value() && accumulate_into->defined();
+  if (acc)
+    DCP_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
+                  accumulate_into->numel() == N1 * N2 && accumulate_into->device() == gy.device(),
+              "conv1x1_wgrad: accumulate_into must be a contiguous fp32 [N1, N2] tensor on the same device");
+  at::Tensor dw = acc ? *accumulate_into : at::empty({N1, N2}, gy.options().dtype(at::kFloat));
   at::Tensor ws = at::empty({kern::gemm_wgrad_workspace(M, static_cast<int>(N1), static_cast<int>(N2))},
                             gy.options().dtype(at::kFloat));
   kern::gemm_wgrad_bf16(gy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), M, static_cast<int>(N1),
-                        static_cast<int>(N2), sc, sf, relu, ws.data_ptr<float>(), stream_of(gy));
+                        static_cast<int>(N2), sc, sf, relu, ws.data_ptr<float>(), stream_of(gy), acc);
   return dw;
 }
 
@@ -480,7 +488,7 @@ at::Tensor conv_dgrad_s2(const at::Tensor& gy, const std::vector<at::Tensor>& ws
 }
 
 // fp32 [N] column sums of a bf16 [.., N] tensor (Linear bias gradient)
-at::Tensor colsum(const at::Tensor& x) {
+at::Tensor colsum(const at::Tensor& x, const c10::optional<at::Tensor>& accumulate_into) {
   DCP_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() >= 1,
             "colsum: contiguous bf16 device tensor required");
   c10::hip::HIPGuard guard(x.device().index());
@@ -488,8 +496,14 @@ at::Tensor colsum(const at::Tensor& x) {
   const int64_t M = x.numel() / N;
   DCP_CHECK(N % 8 == 0, "colsum: last dim must be a multiple of 8");
   auto s = stream_of(x);
-  at::Tensor out = at::empty({N}, x.options().dtype(at::kFloat));
-  DCP_CHECK(hipMemsetAsync(out.data_ptr(), 0, sizeof(float) * N, s) == hipSuccess, "memset failed");
+  // accumulate_into: existing fp32 [N] gradient; the kernel's atomics add into it (no memset)
+  const bool acc = accumulate_into.has_value() && accumulate_into->defined();
+  if (acc)
+    DCP_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
+                  accumulate_into->numel() == N && accumulate_into->device() == x.device(),
+              "colsum: accumulate_into must be a contiguous fp32 [N] tensor on the same device");
+  at::Tensor out = acc ? *accumulate_into : at::empty({N}, x.options().dtype(at::kFloat));
+  if (!acc) DCP_CHECK(hipMemsetAsync(out.data_ptr(), 0, sizeof(float) * N, s) == hipSuccess, "memset failed");
   kern::colsum_bf16(x.data_ptr(), out.data_ptr<float>(), M, static_cast<int>(N), s);
   return out;
 }
@@ -951,7 +965,8 @@ void bind(pybind11::module& m) {
         pybind11::arg("shift") = pybind11::none(), pybind11::arg("relu") = false, pybind11::arg("stats") = false);
   m.def("conv1x1_dgrad", &conv1x1_dgrad, pybind11::arg("gy"), pybind11::arg("wt"));
   m.def("attn_ok", &attn_ok);
-  m.def("colsum", &colsum, "fp32 column sums of a bf16 [.., N] tensor (bias gradient)");
+  m.def("colsum", &colsum, "fp32 column sums of a bf16 [.., N] tensor (bias gradient)", pybind11::arg("x"),
+        pybind11::arg("accumulate_into") = pybind11::none());
   m.def("flash_attn_fwd", &flash_attn_fwd, "MFMA flash attention forward (head dim 64)", pybind11::arg("q"),
         pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("heads"), pybind11::arg("causal"),
         pybind11::arg("p_drop"), pybind11::arg("seed"));
@@ -971,7 +986,7 @@ void bind(pybind11::module& m) {
   m.def("conv_weight_bf16", &conv_weight_bf16, "kxk weight -> (bf16 fwd [Co][kh][kw][Ci], bf16 flipped [Ci][kh][kw][Co])");
   m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("gy"), pybind11::arg("x"),
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
-        pybind11::arg("relu") = false);
+        pybind11::arg("relu") = false, pybind11::arg("accumulate_into") = pybind11::none());
   m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward", pybind11::arg("gy"),
         pybind11::arg("gy2"), pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
         pybind11::arg("mean"), pybind11::arg("invstd"), pybind11::arg("y"), pybind11::arg("act"),

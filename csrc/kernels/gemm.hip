@@ -698,7 +698,7 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
 // then D[v] = Σ_y P[y][v]. Deterministic (fixed order).
 constexpr int kSlabGroup = 16;
 __global__ void __launch_bounds__(kT) slab_partial_kernel(const float4* __restrict__ ws, float4* __restrict__ out,
-                                                          int64_t n4, int S) {
+                                                          int64_t n4, int S, int acc) {
   const int64_t v = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   if (v >= n4) return;
   const int z0 = blockIdx.y * kSlabGroup;
@@ -716,6 +716,13 @@ __global__ void __launch_bounds__(kT) slab_partial_kernel(const float4* __restri
     s.y = fmaf(a[k].y, w, s.y);
     s.z = fmaf(a[k].z, w, s.z);
     s.w = fmaf(a[k].w, w, s.w);
+  }
+  if (acc) {  // final level into an existing gradient (accumulation micro-steps)
+    const float4 o = out[v];
+    s.x += o.x;
+    s.y += o.y;
+    s.z += o.z;
+    s.w += o.w;
   }
   out[static_cast<int64_t>(blockIdx.y) * n4 + v] = s;
 }
@@ -978,11 +985,12 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
 }
 
 namespace {
-void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s);
+void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc = false);
 
 template <bool GATHER>
 void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
-                  const float* shift, bool relu, float* ws, int taps, const ConvGeo& geo, hipStream_t s) {
+                  const float* shift, bool relu, float* ws, int taps, const ConvGeo& geo, hipStream_t s,
+                  bool acc = false) {
   const WgradPlan p = wgrad_plan(M, N1, N2, taps);
   const dim3 grid(p.tiles, p.S, taps);
   auto a = static_cast<const uint16_t*>(A);
@@ -1018,14 +1026,14 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   else DCP_GWG2(64, 64);
 #undef DCP_GWG2
 #undef DCP_GWG
-  slab_reduce(ws, D, static_cast<int64_t>(N1) * taps * N2 / 4, p.S, s);
+  slab_reduce(ws, D, static_cast<int64_t>(N1) * taps * N2 / 4, p.S, s, acc);
 }
 }  // namespace
 
 void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
-                     const float* shift, bool relu, float* ws, hipStream_t s) {
+                     const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate) {
   ConvGeo geo{};
-  wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s);
+  wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s, accumulate);
 }
 
 void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
@@ -1036,16 +1044,17 @@ void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int 
 }
 
 namespace {
-void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s) {
+void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc) {
   const WgradPlan p{0, 0, 0, S, 0};
   const int gx = static_cast<int>((n4 + kT - 1) / kT);
   const int groups = (p.S + kSlabGroup - 1) / kSlabGroup;
   auto w4 = reinterpret_cast<const float4*>(ws);
+  const int a = acc ? 1 : 0;
   if (groups == 1) {
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, w4, reinterpret_cast<float4*>(D), n4, p.S);
+    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, w4, reinterpret_cast<float4*>(D), n4, p.S, a);
   } else {
     float4* part = reinterpret_cast<float4*>(ws + static_cast<int64_t>(p.S) * n4 * 4);
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, groups), dim3(kT), 0, s, w4, part, n4, p.S);
+    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, groups), dim3(kT), 0, s, w4, part, n4, p.S, 0);
     // groups ≤ 32 (S ≤ 512): ≤ 2 more levels
     int S2 = groups;
     const float4* src = part;
@@ -1053,11 +1062,11 @@ void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s) {
     if (S2 > kSlabGroup) {  // one intermediate level back into the head of ws
       const int g2 = (S2 + kSlabGroup - 1) / kSlabGroup;
       float4* mid = reinterpret_cast<float4*>(ws);
-      hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, g2), dim3(kT), 0, s, src, mid, n4, S2);
+      hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, g2), dim3(kT), 0, s, src, mid, n4, S2, 0);
       src = mid;
       S2 = g2;
     }
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, src, dst, n4, S2);
+    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, src, dst, n4, S2, a);
   }
 }
 }  // namespace

@@ -43,7 +43,7 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps = 1);
 // (f = optional per-column scale/shift/relu). Deterministic: split over M
 // into fp32 slabs in `ws`, then one reduction launch.
 void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
-                     const float* shift, bool relu, float* ws, hipStream_t s);
+                     const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate = false);
 
 // Weight gradient of a kh×kw NHWC convolution (implicit GEMM, one tap per
 // grid.z): D[Cout][kh][kw][Cin] (fp32; = a channels_last OIHW tensor) =

@@ -19,17 +19,47 @@ from torch.nn import functional as F
 
 from .._ext import C as _C
 
+# > 0 while gradients accumulate locally (DistributedDataParallel.no_sync): the
+# backward then adds dW / db straight into existing fp32 .grad tensors inside
+# the wgrad / column-sum kernels and returns None for them, skipping autograd's
+# separate AccumulateGrad add (one elementwise launch per parameter per
+# micro-step: 3.8 ms of a GPT-2 accum-4 step, profiles/r1_gpt2_prof64.txt).
+# A plain global, not thread-local: the backward runs on autograd's device
+# threads. The DDP Reducer ignores hooks under no_sync, so skipping them is safe.
+_ACCUM_IN_PLACE = [0]
+
+
+class accumulate_grads_in_place:
+    """Context manager used by ``DistributedDataParallel.no_sync``."""
+
+    def __enter__(self):
+        _ACCUM_IN_PLACE[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _ACCUM_IN_PLACE[0] -= 1
+        return False
+
+
+def _acc_target(p, shape):
+    g = p.grad if p is not None else None
+    if (_ACCUM_IN_PLACE[0] > 0 and g is not None and g.dtype == torch.float32 and g.is_contiguous()
+            and g.shape == shape and not g.requires_grad):
+        return g
+    return None
+
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
-        w = weight.to(torch.bfloat16)
-        b = bias.to(torch.bfloat16) if bias is not None else None
+    def forward(ctx, x, weight, bias, w16, b16):
+        w = w16 if w16 is not None else weight.to(torch.bfloat16)
+        b = (b16 if b16 is not None else bias.to(torch.bfloat16)) if bias is not None else None
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
         ctx.save_for_backward(x, w)
         ctx.wdtype = weight.dtype
         ctx.bdtype = bias.dtype if bias is not None else None
+        ctx.params = (weight, bias)
         return F.linear(x, w, b)
 
     @staticmethod
@@ -43,20 +73,27 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = (g2 @ w).view(x.shape)
+        weight, bias = ctx.params
         if ctx.needs_input_grad[1]:
             if g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
-                # our split-M MFMA wgrad GEMM (gemm.hip): the hipBLASLt tiles picked
-                # for this K ≫ M,N shape leave most CUs idle (profiles/r1_bert_prof26.txt)
-                dw = _C.conv1x1_wgrad(g2, x2.contiguous())
+                # our split-M MFMA wgrad GEMM (gemm.hip): faster than hipBLASLt at
+                # every BERT / GPT-2 shape (profiles/r1_linear_wgrad_bench.log)
+                tgt = _acc_target(weight, torch.Size((g2.shape[1], x2.shape[1])))
+                dw = _C.conv1x1_wgrad(g2, x2.contiguous(), accumulate_into=tgt)
+                if tgt is not None:
+                    dw = None  # added into weight.grad by the kernel
             else:
                 dw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
-            if dw.dtype != ctx.wdtype:
+            if dw is not None and dw.dtype != ctx.wdtype:
                 dw = dw.to(ctx.wdtype)
         if ctx.bdtype is not None and ctx.needs_input_grad[2]:
-            db = _C.colsum(g2)
-            if db.dtype != ctx.bdtype:
+            tgt = _acc_target(bias, torch.Size((g2.shape[1],)))
+            db = _C.colsum(g2, accumulate_into=tgt)
+            if tgt is not None:
+                db = None
+            elif db.dtype != ctx.bdtype:
                 db = db.to(ctx.bdtype)
-        return dx, dw, db
+        return dx, dw, db, None, None
 
 
 class FusedLinear(nn.Linear):
@@ -64,9 +101,28 @@ class FusedLinear(nn.Linear):
     (fp32 weight/bias gradients without cast passes); plain ``nn.Linear``
     everywhere else (CPU, fp32 without autocast)."""
 
+    def _bf16(self, p: torch.Tensor, slot: str):
+        """bf16 copy of a parameter, reused while it is unchanged (autograd
+        version, fused-optimizer epoch, storage): an accum-4 GPT-2 step casts
+        each weight once instead of four times. Never cached while a HIP graph
+        is being captured (the cast must be part of every replay)."""
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        from ..optim.fused import param_epoch
+
+        key = (p._version, param_epoch(), p.data_ptr())
+        c = self.__dict__.get(slot)
+        if c is not None and c[0] == key:
+            return c[1]
+        t = p.detach().to(torch.bfloat16)
+        self.__dict__[slot] = (key, t)
+        return t
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda and self.in_features % 8 == 0 and self.out_features % 8 == 0 and (
                 x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
                                               and torch.get_autocast_dtype("cuda") == torch.bfloat16)):
-            return _LinearFn.apply(x, self.weight, self.bias)
+            w16 = self._bf16(self.weight, "_w16_cache")
+            b16 = self._bf16(self.bias, "_b16_cache") if self.bias is not None else None
+            return _LinearFn.apply(x, self.weight, self.bias, w16, b16)
         return super().forward(x)

@@ -23,6 +23,16 @@ from torch.optim import Optimizer
 from .._ext import C as _C
 
 
+# Bumped by every fused step: the kernels update parameters through raw
+# pointers (no autograd version bump), so caches of derived tensors (the bf16
+# weight copies of ops.linear.FusedLinear) key on this as well as _version.
+_PARAM_EPOCH = [0]
+
+
+def param_epoch() -> int:
+    return _PARAM_EPOCH[0]
+
+
 def _grads_ok(p: torch.Tensor) -> bool:
     if p.grad is None:
         return False
@@ -81,6 +91,7 @@ class SGD(Optimizer):
             for (dev, dt, first), (P, G, B) in buckets.items():
                 _C.fused_sgd(P, G, B, group["lr"], mom, group["dampening"], group["weight_decay"],
                              group["nesterov"], group["maximize"], first, grad_scale)
+        _PARAM_EPOCH[0] += 1
         return loss
 
 
@@ -129,6 +140,7 @@ class Adam(Optimizer):
             for (dev, dt, step), (P, G, M, V, VM) in buckets.items():
                 _C.fused_adam(P, G, M, V, VM, group["lr"], b1, b2, group["eps"], group["weight_decay"], step, ams,
                               group["decoupled_weight_decay"], group["maximize"], grad_scale)
+        _PARAM_EPOCH[0] += 1
         return loss
 
 
@@ -173,6 +185,7 @@ class Adadelta(Optimizer):
             for _, (P, G, S, A) in buckets.items():
                 _C.fused_adadelta(P, G, S, A, group["lr"], group["rho"], group["eps"], group["weight_decay"],
                                   group["maximize"], grad_scale)
+        _PARAM_EPOCH[0] += 1
         return loss
 
 

@@ -148,10 +148,13 @@ class DistributedDataParallel(nn.Module):
     @contextlib.contextmanager
     def no_sync(self):
         """Accumulate gradients locally (no all-reduce) inside the context."""
+        from ..ops.linear import accumulate_grads_in_place
+
         old = self.require_backward_grad_sync
         self.require_backward_grad_sync = False
         try:
-            yield
+            with accumulate_grads_in_place():
+                yield
         finally:
             self.require_backward_grad_sync = old
 

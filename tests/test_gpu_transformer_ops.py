@@ -1,4 +1,6 @@
 """Fused LayerNorm and vocab cross-entropy kernels vs fp32 PyTorch references."""
+import contextlib
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -208,3 +210,39 @@ def test_fused_linear_matches_fp32(cuda):
     assert rel(xa.grad, xr.grad) < 1e-2
     assert lin.weight.grad.dtype == torch.float32 and rel(lin.weight.grad, wr.grad) < 1e-2
     assert lin.bias.grad.dtype == torch.float32 and rel(lin.bias.grad, br.grad) < 1e-3
+
+
+def test_fused_linear_in_place_accumulation_and_weight_cache(cuda):
+    """Micro-steps under ``accumulate_grads_in_place`` (what DDP.no_sync enables)
+    add dW / db inside the kernels: the accumulated .grad must equal autograd's
+    own accumulation; the cached bf16 weight must follow optimizer updates."""
+    import copy
+
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.ops.linear import FusedLinear, accumulate_grads_in_place
+
+    torch.manual_seed(0)
+    a = FusedLinear(256, 384).to(cuda)
+    b = copy.deepcopy(a)
+    g = torch.Generator().manual_seed(13)
+    xs = [torch.randn(2, 64, 256, generator=g).to(cuda) for _ in range(3)]
+    gys = [torch.randn(2, 64, 384, generator=g).to(cuda).to(torch.bfloat16) for _ in range(3)]
+    for k, (x, gy) in enumerate(zip(xs, gys)):
+        for m, inplace in ((a, True), (b, False)):
+            ctx = accumulate_grads_in_place() if (inplace and k < 2) else contextlib.nullcontext()
+            with ctx, torch.autocast("cuda", dtype=torch.bfloat16):
+                y = m(x)
+            with ctx:
+                y.backward(gy)
+    torch.testing.assert_close(a.weight.grad, b.weight.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(a.bias.grad, b.bias.grad, rtol=1e-5, atol=1e-5)
+    # weight cache: an optimizer step must invalidate the bf16 copy
+    opt = dcp.optim.SGD(a.parameters(), lr=0.5)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y0 = a(xs[0])
+    opt.step()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y1 = a(xs[0])
+    ref = F.linear(xs[0].to(torch.bfloat16), a.weight.to(torch.bfloat16), a.bias.to(torch.bfloat16))
+    assert not torch.equal(y0, y1)
+    torch.testing.assert_close(y1, ref, rtol=0, atol=0)

@@ -1,7 +1,7 @@
 """One 1x1-conv GEMM shape, repeated (a small target for rocprofv3 --pmc).
 
     python tools/gemm_one.py --m 12544 --cin 2048 --cout 512 --op fwd [--iters 10]
-op: fwd | fwd_pro | dgrad | wgrad
+op: fwd | fwd_pro | dgrad | wgrad | conv3 (3x3 stride-1 implicit GEMM fwd, --hw spatial)
 """
 import argparse
 import os
@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--cout", type=int, default=512)
     ap.add_argument("--op", default="fwd")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--hw", type=int, default=14)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     bf = torch.bfloat16
@@ -30,6 +31,15 @@ def main():
     w = (torch.randn(a.cout, a.cin, device=dev) / a.cin ** 0.5).to(bf)
     wt = w.t().contiguous()
     sc, sf = torch.ones(a.cin, device=dev), torch.zeros(a.cin, device=dev)
+    if a.op == "conv3":
+        n = a.m // (a.hw * a.hw)
+        xi = torch.randn(n, a.cin, a.hw, a.hw, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
+        w3 = (torch.randn(a.cout, 3, 3, a.cin, device=dev) / (9 * a.cin) ** 0.5).to(bf).contiguous()
+        for _ in range(a.iters):
+            _C.conv_fwd(xi, w3, 3, 3, 1, 1, True)
+        torch.cuda.synchronize()
+        print("ok", flush=True)
+        return
     fn = {"fwd": lambda: _C.conv1x1_fwd(x, w, None, None, False, False),
           "fwd_pro": lambda: _C.conv1x1_fwd(x, w, sc, sf, True, False),
           "dgrad": lambda: _C.conv1x1_dgrad(gy, wt),
