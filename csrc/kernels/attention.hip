@@ -153,9 +153,13 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hh = lane >> 5;
-  const int bh = blockIdx.y, b = bh / P.H, hd = bh % P.H;
+  // grid (B*H, tiles): heads on x, so consecutive workgroups (→ consecutive XCDs) carry
+  // every tile size; with a causal mask the heaviest query tiles launch first
+  const int bh = blockIdx.x, b = bh / P.H, hd = bh % P.H;
+  const int tile = CAUSAL ? static_cast<int>(gridDim.y) - 1 - static_cast<int>(blockIdx.y)
+                          : static_cast<int>(blockIdx.y);
   const int T = P.T;
-  const int qi = blockIdx.x * 128 + wave * 32 + (lane & 31);  // this lane's query
+  const int qi = tile * 128 + wave * 32 + (lane & 31);  // this lane's query
   const bool qok = qi < T;
   const Ptrs Q = head(q, b, hd), K = head(k, b, hd), V = head(v, b, hd);
 
@@ -174,7 +178,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
   float m = -INFINITY, l = 0.f;
   f32x16 oacc[2] = {zero16(), zero16()};
   int nkb = T / kKB;
-  if (CAUSAL) nkb = min(nkb, (static_cast<int>(blockIdx.x) * 128 + 128 + kKB - 1) / kKB);
+  if (CAUSAL) nkb = min(nkb, (tile * 128 + 128 + kKB - 1) / kKB);
 
   auto issue = [&](int it) {
     if (it >= nkb) return;
@@ -191,7 +195,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
     const char* sV = sK + kTile;
     const int kb = it * kKB;
     // causal: a key block wholly after this wave's last query contributes nothing
-    if (CAUSAL && kb > static_cast<int>(blockIdx.x) * 128 + wave * 32 + 31) continue;
+    if (CAUSAL && kb > tile * 128 + wave * 32 + 31) continue;
     f32x16 s[2];
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
@@ -306,9 +310,13 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hh = lane >> 5;
-  const int bh = blockIdx.y, b = bh / P.H, hd = bh % P.H;
+  // grid (B*H, tiles): heads on x, so consecutive workgroups (→ consecutive XCDs) carry
+  // every tile size; with a causal mask the heaviest query tiles launch first
+  const int bh = blockIdx.x, b = bh / P.H, hd = bh % P.H;
+  const int tile = CAUSAL ? static_cast<int>(gridDim.y) - 1 - static_cast<int>(blockIdx.y)
+                          : static_cast<int>(blockIdx.y);
   const int T = P.T;
-  const int qi = blockIdx.x * 128 + wave * 32 + (lane & 31);
+  const int qi = tile * 128 + wave * 32 + (lane & 31);
   const bool qok = qi < T;
   const Ptrs Q = head(q, b, hd), K = head(k, b, hd), V = head(v, b, hd), G = head(dout, b, hd);
   bf16x8 qf[4], gf[4];
@@ -328,7 +336,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
 
   f32x16 dacc[2] = {zero16(), zero16()};
   int nkb = T / kKB;
-  if (CAUSAL) nkb = min(nkb, (static_cast<int>(blockIdx.x) * 128 + 128 + kKB - 1) / kKB);
+  if (CAUSAL) nkb = min(nkb, (tile * 128 + 128 + kKB - 1) / kKB);
   auto issue = [&](int it) {
     if (it >= nkb) return;
     char* base = lds + (it & 1) * 2 * kTile;
@@ -343,7 +351,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
     const char* sK = lds + (it & 1) * 2 * kTile;
     const char* sV = sK + kTile;
     const int kb = it * kKB;
-    if (CAUSAL && kb > static_cast<int>(blockIdx.x) * 128 + wave * 32 + 31) continue;
+    if (CAUSAL && kb > tile * 128 + wave * 32 + 31) continue;
 #pragma unroll 1
     for (int kh = 0; kh < 2; ++kh) {
       f32x16 s = zero16(), dp = zero16();
@@ -399,9 +407,11 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hh = lane >> 5;
-  const int bh = blockIdx.y, b = bh / P.H, hd = bh % P.H;
+  // grid (B*H, key tiles): heads on x (XCD balance); key tile 0 is the heaviest (causal)
+  const int bh = blockIdx.x, b = bh / P.H, hd = bh % P.H;
+  const int tile = static_cast<int>(blockIdx.y);
   const int T = P.T;
-  const int kb0 = blockIdx.x * 128;
+  const int kb0 = tile * 128;
   const int key = kb0 + wave * 32 + (lane & 31);  // this lane's key
   const bool kok = key < T;
   const Ptrs Q = head(q, b, hd), K = head(k, b, hd), V = head(v, b, hd), G = head(dout, b, hd);
@@ -519,7 +529,7 @@ bool attn_supported(int T, int D) { return D == kD && T > 0 && T % kKB == 0; }
 
 void attn_fwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, AttnOut o, float* lse,
               hipStream_t s) {
-  const dim3 grid((p.T + 127) / 128, p.B * p.H);
+  const dim3 grid(p.B * p.H, (p.T + 127) / 128);
   const bool drop = p.p_drop > 0.f;
 #define DCP_AF(C, D) hipLaunchKernelGGL((attn_fwd_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, o, lse)
   if (p.causal && drop) DCP_AF(true, true);
@@ -534,7 +544,7 @@ void attn_bwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, Att
   const int64_t rows = static_cast<int64_t>(p.B) * p.H * p.T;
   hipLaunchKernelGGL(attn_delta_kernel, dim3(static_cast<int>((rows + kT - 1) / kT)), dim3(kT), 0, s, p, o, dout,
                      delta);
-  const dim3 grid((p.T + 127) / 128, p.B * p.H);
+  const dim3 grid(p.B * p.H, (p.T + 127) / 128);
   const bool drop = p.p_drop > 0.f;
 #define DCP_AB(C, D)                                                                                          \
   do {                                                                                                        \
