@@ -9,6 +9,8 @@
 // hot path (SURVEY §2f "LayerNorm fwd/bwd", BASELINE config #3/#5).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "ln_kernels.h"
 
 namespace dcp {
@@ -307,8 +309,15 @@ inline int vpl_for(int D) {
 bool ln_supported(int D) { return D % 8 == 0 && D <= 4096; }
 
 int ln_bwd_blocks(int64_t rows) {
+  // each workgroup writes one [2][D] partial row that ln_bwd_finalize_kernel
+  // re-reads column-strided: 1024 workgroups made that 6 MB pass (17 µs at
+  // BERT's 16384 x 768) cost more than the backward's own occupancy gain
+  static const int64_t cap = [] {
+    const char* v = getenv("DCP_LN_BWD_BLOCKS");
+    return v ? static_cast<int64_t>(atoll(v)) : int64_t(256);
+  }();
   int64_t nb = (rows + 15) / 16;  // >= 16 rows (4 per wave) per workgroup
-  if (nb > 1024) nb = 1024;
+  if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
   return static_cast<int>(nb);
 }
