@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <string>
 
 #include "gemm_kernels.h"
 
@@ -528,7 +529,7 @@ __device__ __forceinline__ bf16x8 mask_rows(bf16x8 v, int valid, int lane) {
   return __builtin_bit_cast(bf16x8, s);
 }
 
-template <int BM, int BN, bool PRO, bool GATHER, int BK>
+template <int BM, int BN, bool PRO, bool GATHER, int BK, int NSW = 0>
 __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                         float* __restrict__ ws, int64_t M, int N1, int N2,
                                                         int64_t chunk, const float* __restrict__ scale,
@@ -537,7 +538,7 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
   // BK m-rows per stage: 64 on a 2-deep ring (half the barriers per MFMA) or
   // 32 on the 4-deep ring; both ≤ 64 KB of LDS (2 blocks per CU)
-  constexpr int kNSw = BK == 64 ? 2 : kNS;
+  constexpr int kNSw = NSW > 0 ? NSW : (BK == 64 ? 2 : kNS);
   constexpr int SA = BK * BM * 2, SB = BK * BN * 2, STAGE = SA + SB;
   constexpr int NA = SA / 4096, NB = SB / 4096;  // glds per wave per stage
   constexpr int G = NA + NB;
@@ -997,18 +998,27 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   auto b = static_cast<const uint16_t*>(B);
   const bool pro = scale != nullptr;
   const int tj = N2 / p.bn;
-  static const bool bk64 = [] {
-    const char* v = getenv("DCP_WGRAD_BK");
-    return !(v && atoi(v) == 32);
+  // ring config (DCP_WGRAD_CFG): "64x2" (default: BK=64, 2 stages, 64 KB),
+  // "32x2" (32 KB: up to 4 workgroups per CU), "32x4" (the BK=32 4-deep ring)
+  static const int cfg = [] {
+    const char* v = getenv("DCP_WGRAD_CFG");
+    if (v && std::string(v) == "32x2") return 1;
+    if (v && std::string(v) == "32x4") return 2;
+    if (v && atoi(v) == 32) return 2;  // legacy DCP_WGRAD_BK=32 spelling
+    const char* b = getenv("DCP_WGRAD_BK");
+    return b && atoi(b) == 32 ? 2 : 0;
   }();
-#define DCP_GWG(BM_, BN_, P)                                                                                     \
-  do {                                                                                                          \
-    if (bk64 && !P)                                                                                             \
-      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 64>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                         \
-    else                                                                                                        \
-      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                         \
+#define DCP_GWG(BM_, BN_, P)                                                                                        \
+  do {                                                                                                             \
+    if (cfg == 0 && !P)                                                                                            \
+      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 64>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,    \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                            \
+    else if (cfg == 1)                                                                                             \
+      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32, 2>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                            \
+    else                                                                                                           \
+      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,    \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                            \
   } while (0)
 #define DCP_GWG2(BM_, BN_)                      \
   do {                                          \
