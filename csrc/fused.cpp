@@ -14,6 +14,7 @@
 #include "kernels/dropout_kernels.h"
 #include "kernels/pool_kernels.h"
 #include "kernels/metrics_kernels.h"
+#include "kernels/gelu_kernels.h"
 
 namespace dcp {
 namespace fused {
@@ -508,6 +509,53 @@ at::Tensor colsum(const at::Tensor& x, const c10::optional<at::Tensor>& accumula
   return out;
 }
 
+// --------------------------------------------------------------- GELU ---
+namespace {
+void check_gelu_operand(const at::Tensor& t, const char* what) {
+  DCP_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.dim() >= 1, what,
+            ": contiguous bf16 device tensor required");
+  DCP_CHECK(t.size(-1) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, what,
+            ": last dim must be a multiple of 8 and the data 16-B aligned");
+}
+}  // namespace
+
+at::Tensor gelu_fwd(const at::Tensor& h, bool tanh_approx) {
+  check_gelu_operand(h, "gelu_fwd");
+  c10::hip::HIPGuard guard(h.device().index());
+  at::Tensor y = at::empty_like(h);
+  if (h.numel()) kern::gelu_fwd(tanh_approx, h.data_ptr(), y.data_ptr(), h.numel(), stream_of(h));
+  return y;
+}
+
+// (gh, db): gh = gy * gelu'(h); db = fp32 column sums of gh when bias_grad
+// (added into accumulate_into when given, else a fresh tensor), else None.
+std::vector<at::Tensor> gelu_bwd(const at::Tensor& gy, const at::Tensor& h, bool tanh_approx, bool bias_grad,
+                                 const c10::optional<at::Tensor>& accumulate_into) {
+  check_gelu_operand(gy, "gelu_bwd");
+  check_gelu_operand(h, "gelu_bwd");
+  DCP_CHECK(gy.sizes() == h.sizes() && gy.device() == h.device(), "gelu_bwd: gy and h must match");
+  c10::hip::HIPGuard guard(h.device().index());
+  const int64_t N = h.size(-1);
+  const int64_t M = N ? h.numel() / N : 0;
+  DCP_CHECK(N < (int64_t(1) << 30), "gelu_bwd: last dim too large");
+  auto s = stream_of(h);
+  at::Tensor gh = at::empty_like(h);
+  at::Tensor db;
+  if (bias_grad) {
+    if (accumulate_into.has_value() && accumulate_into->defined()) {
+      db = *accumulate_into;
+      DCP_CHECK(db.scalar_type() == at::kFloat && db.is_contiguous() && db.numel() == N && db.device() == h.device(),
+                "gelu_bwd: accumulate_into must be a contiguous fp32 [N] tensor on the same device");
+    } else {
+      db = at::zeros({N}, h.options().dtype(at::kFloat));
+    }
+  }
+  if (M)
+    kern::gelu_bwd(tanh_approx, gy.data_ptr(), h.data_ptr(), gh.data_ptr(),
+                   bias_grad ? db.data_ptr<float>() : nullptr, M, static_cast<int>(N), s);
+  return {gh, db};
+}
+
 // ---------------------------------------------------- flash attention ---
 namespace {
 kern::AttnTensor attn_view(const at::Tensor& t, const char* what) {
@@ -966,6 +1014,11 @@ void bind(pybind11::module& m) {
   m.def("conv1x1_dgrad", &conv1x1_dgrad, pybind11::arg("gy"), pybind11::arg("wt"));
   m.def("attn_ok", &attn_ok);
   m.def("colsum", &colsum, "fp32 column sums of a bf16 [.., N] tensor (bias gradient)", pybind11::arg("x"),
+        pybind11::arg("accumulate_into") = pybind11::none());
+  m.def("gelu_fwd", &gelu_fwd, "bf16 GELU forward (erf or tanh form)", pybind11::arg("h"),
+        pybind11::arg("tanh_approx"));
+  m.def("gelu_bwd", &gelu_bwd, "bf16 GELU backward (+ fused bias-gradient column sums)", pybind11::arg("gy"),
+        pybind11::arg("h"), pybind11::arg("tanh_approx"), pybind11::arg("bias_grad"),
         pybind11::arg("accumulate_into") = pybind11::none());
   m.def("flash_attn_fwd", &flash_attn_fwd, "MFMA flash attention forward (head dim 64)", pybind11::arg("q"),
         pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("heads"), pybind11::arg("causal"),

@@ -93,7 +93,11 @@ class BertLayer(nn.Module):
 
     def forward(self, x, mask):
         x = self.attn_ln(self._dadd(self.attn_out(self.attention(x, mask)), x, self.p, self.training))
-        return self.out_ln(self._dadd(self.output(F.gelu(self.intermediate(x))), x, self.p, self.training))
+        if isinstance(self.intermediate, FusedLinear):
+            a = self.intermediate.forward_gelu(x)  # gelu.hip, bias grad fused into the GELU backward
+        else:
+            a = F.gelu(self.intermediate(x))
+        return self.out_ln(self._dadd(self.output(a), x, self.p, self.training))
 
 
 class BertForPreTraining(nn.Module):
@@ -150,7 +154,10 @@ class BertForPreTraining(nn.Module):
             sel = (flat_labels != -100).nonzero(as_tuple=True)[0]  # host sync: prefer mlm_positions
             tgt = flat_labels.index_select(0, sel)
         h = x.reshape(B * T, -1).index_select(0, sel)
-        h = self.mlm_ln(F.gelu(self.mlm_transform(h)))
+        if isinstance(self.mlm_transform, FusedLinear):
+            h = self.mlm_ln(self.mlm_transform.forward_gelu(h))
+        else:
+            h = self.mlm_ln(F.gelu(self.mlm_transform(h)))
         logits = F.linear(h, self.word_embeddings.weight, self.mlm_bias)
         if self.cfg.fused:
             mlm = fused_cross_entropy(logits, tgt)

@@ -78,6 +78,8 @@ class MLP(nn.Module):
         self.c_proj = lin(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
+        if isinstance(self.c_fc, FusedLinear):
+            return self.c_proj(self.c_fc.forward_gelu(x, approximate="tanh"))  # gelu.hip
         return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
 
 

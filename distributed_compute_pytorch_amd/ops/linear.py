@@ -13,11 +13,16 @@ state_dict keys) computes
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 from torch.nn import functional as F
 
 from .._ext import C as _C
+
+# DCP_FUSED_GELU=0: forward_gelu falls back to FusedLinear + ATen GELU (A/B switch)
+_FUSED_GELU = os.environ.get("DCP_FUSED_GELU", "1") != "0"
 
 # > 0 while gradients accumulate locally (DistributedDataParallel.no_sync): the
 # backward then adds dW / db straight into existing fp32 .grad tensors inside
@@ -52,14 +57,8 @@ def _acc_target(p, shape):
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, w16, b16):
-        w = w16 if w16 is not None else weight.to(torch.bfloat16)
-        b = (b16 if b16 is not None else bias.to(torch.bfloat16)) if bias is not None else None
-        if x.dtype != torch.bfloat16:
-            x = x.to(torch.bfloat16)
+        x, w, b = _setup(ctx, x, weight, bias, w16, b16)
         ctx.save_for_backward(x, w)
-        ctx.wdtype = weight.dtype
-        ctx.bdtype = bias.dtype if bias is not None else None
-        ctx.params = (weight, bias)
         return F.linear(x, w, b)
 
     @staticmethod
@@ -68,32 +67,79 @@ class _LinearFn(torch.autograd.Function):
         gy = gy.contiguous()
         if gy.dtype != torch.bfloat16:
             gy = gy.to(torch.bfloat16)
-        g2 = gy.view(-1, gy.shape[-1])
-        x2 = x.reshape(-1, x.shape[-1])
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = (g2 @ w).view(x.shape)
-        weight, bias = ctx.params
-        if ctx.needs_input_grad[1]:
-            if g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
-                # our split-M MFMA wgrad GEMM (gemm.hip): faster than hipBLASLt at
-                # every BERT / GPT-2 shape (profiles/r1_linear_wgrad_bench.log)
-                tgt = _acc_target(weight, torch.Size((g2.shape[1], x2.shape[1])))
-                dw = _C.conv1x1_wgrad(g2, x2.contiguous(), accumulate_into=tgt)
-                if tgt is not None:
-                    dw = None  # added into weight.grad by the kernel
-            else:
-                dw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
-            if dw is not None and dw.dtype != ctx.wdtype:
-                dw = dw.to(ctx.wdtype)
-        if ctx.bdtype is not None and ctx.needs_input_grad[2]:
-            tgt = _acc_target(bias, torch.Size((g2.shape[1],)))
-            db = _C.colsum(g2, accumulate_into=tgt)
+        return _linear_backward(ctx, gy.view(-1, gy.shape[-1]), x, w) + (None, None)
+
+
+def _setup(ctx, x, weight, bias, w16, b16):
+    w = w16 if w16 is not None else weight.to(torch.bfloat16)
+    b = (b16 if b16 is not None else bias.to(torch.bfloat16)) if bias is not None else None
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    ctx.wdtype = weight.dtype
+    ctx.bdtype = bias.dtype if bias is not None else None
+    ctx.params = (weight, bias)
+    return x, w, b
+
+
+def _linear_backward(ctx, g2, x, w, db=None, db_done=False):
+    """(dx, dW, db) of y = x Wᵀ + b from the bf16 [M, N] output gradient g2.
+    ``db_done``: the bias gradient was already produced by the caller (``db``,
+    or added into ``bias.grad`` when ``db`` is None)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    dx = dw = None
+    if ctx.needs_input_grad[0]:
+        dx = (g2 @ w).view(x.shape)
+    weight, bias = ctx.params
+    if ctx.needs_input_grad[1]:
+        if g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
+            # our split-M MFMA wgrad GEMM (gemm.hip): faster than hipBLASLt at
+            # every BERT / GPT-2 shape (profiles/r1_linear_wgrad_bench.log)
+            tgt = _acc_target(weight, torch.Size((g2.shape[1], x2.shape[1])))
+            dw = _C.conv1x1_wgrad(g2, x2.contiguous(), accumulate_into=tgt)
             if tgt is not None:
-                db = None
-            elif db.dtype != ctx.bdtype:
-                db = db.to(ctx.bdtype)
-        return dx, dw, db, None, None
+                dw = None  # added into weight.grad by the kernel
+        else:
+            dw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
+        if dw is not None and dw.dtype != ctx.wdtype:
+            dw = dw.to(ctx.wdtype)
+    if not db_done and ctx.bdtype is not None and ctx.needs_input_grad[2]:
+        tgt = _acc_target(bias, torch.Size((g2.shape[1],)))
+        db = _C.colsum(g2, accumulate_into=tgt)
+        if tgt is not None:
+            db = None
+    if db is not None and db.dtype != ctx.bdtype:
+        db = db.to(ctx.bdtype)
+    return dx, dw, db
+
+
+class _LinearGeluFn(torch.autograd.Function):
+    """y = gelu(x Wᵀ + b). Forward: bf16 GEMM (+bias epilogue) then the GELU
+    kernel (``gelu.hip``). Backward: one kernel computes gh = gy·gelu'(h) AND the
+    bias gradient's column sums (no separate column-sum pass over gh), then the
+    Linear's dX GEMM and MFMA wgrad."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, w16, b16, tanh_approx):
+        x, w, b = _setup(ctx, x, weight, bias, w16, b16)
+        h = F.linear(x, w, b)
+        ctx.tanh = tanh_approx
+        ctx.save_for_backward(x, w, h)
+        return _C.gelu_fwd(h, tanh_approx)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, h = ctx.saved_tensors
+        gy = gy.contiguous()
+        if gy.dtype != torch.bfloat16:
+            gy = gy.to(torch.bfloat16)
+        bias = ctx.params[1]
+        want_db = ctx.bdtype is not None and ctx.needs_input_grad[2]
+        tgt = _acc_target(bias, torch.Size((h.shape[-1],))) if want_db else None
+        gh, db = _C.gelu_bwd(gy, h, ctx.tanh, want_db, accumulate_into=tgt)
+        if tgt is not None:
+            db = None  # added into bias.grad by the kernel
+        g2 = gh.view(-1, gh.shape[-1])
+        return _linear_backward(ctx, g2, x, w, db=db, db_done=True) + (None, None, None)
 
 
 class FusedLinear(nn.Linear):
@@ -118,11 +164,25 @@ class FusedLinear(nn.Linear):
         self.__dict__[slot] = (key, t)
         return t
 
+    def _fast(self, x: torch.Tensor) -> bool:
+        return x.is_cuda and self.in_features % 8 == 0 and self.out_features % 8 == 0 and (
+            x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
+                                          and torch.get_autocast_dtype("cuda") == torch.bfloat16))
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if x.is_cuda and self.in_features % 8 == 0 and self.out_features % 8 == 0 and (
-                x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
-                                              and torch.get_autocast_dtype("cuda") == torch.bfloat16)):
+        if self._fast(x):
             w16 = self._bf16(self.weight, "_w16_cache")
             b16 = self._bf16(self.bias, "_b16_cache") if self.bias is not None else None
             return _LinearFn.apply(x, self.weight, self.bias, w16, b16)
         return super().forward(x)
+
+    def forward_gelu(self, x: torch.Tensor, approximate: str = "none") -> torch.Tensor:
+        """``F.gelu(self(x), approximate=approximate)`` with the GELU on our
+        kernels and the bias gradient fused into the GELU backward."""
+        if approximate not in ("none", "tanh"):
+            raise ValueError(f"approximate must be 'none' or 'tanh', got {approximate!r}")
+        if _FUSED_GELU and self._fast(x):
+            w16 = self._bf16(self.weight, "_w16_cache")
+            b16 = self._bf16(self.bias, "_b16_cache") if self.bias is not None else None
+            return _LinearGeluFn.apply(x, self.weight, self.bias, w16, b16, approximate == "tanh")
+        return F.gelu(self.forward(x), approximate=approximate)

@@ -212,6 +212,59 @@ def test_fused_linear_matches_fp32(cuda):
     assert lin.bias.grad.dtype == torch.float32 and rel(lin.bias.grad, br.grad) < 1e-3
 
 
+@pytest.mark.parametrize("approximate", ["none", "tanh"])
+@pytest.mark.parametrize("rows,fin,fout", [(4 * 64, 256, 1024), (37, 128, 520), (8192, 768, 3072)])
+def test_fused_linear_gelu_matches_fp32(cuda, approximate, rows, fin, fout):
+    """FusedLinear.forward_gelu (GEMM + gelu.hip forward; GELU backward with the
+    bias column sums fused) vs an fp32 PyTorch reference on the same bf16 inputs."""
+    from torch import nn
+
+    from distributed_compute_pytorch_amd.ops.linear import FusedLinear
+
+    torch.manual_seed(0)
+    lin = FusedLinear(fin, fout).to(cuda)
+    ref = nn.Linear(fin, fout).to(cuda)
+    ref.load_state_dict(lin.state_dict())
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(rows, fin, generator=g).to(cuda)
+    gy = torch.randn(rows, fout, generator=g).to(cuda).to(torch.bfloat16)
+    xa = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = lin.forward_gelu(xa, approximate)
+    y.backward(gy)
+    xr = x.to(torch.bfloat16).float().requires_grad_(True)
+    wr = ref.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = ref.bias.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.gelu(F.linear(xr, wr, br), approximate=approximate)
+    yr.backward(gy.float())
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / b.float().norm())
+
+    assert y.dtype == torch.bfloat16 and rel(y, yr) < 1e-2
+    assert rel(xa.grad, xr.grad) < 1e-2
+    assert lin.weight.grad.dtype == torch.float32 and rel(lin.weight.grad, wr.grad) < 1e-2
+    assert lin.bias.grad.dtype == torch.float32 and rel(lin.bias.grad, br.grad) < 1e-2
+
+
+def test_gelu_kernels_elementwise(cuda):
+    """Raw gelu_fwd / gelu_bwd vs fp32 ATen on a wide value range (no bias grad)."""
+    from distributed_compute_pytorch_amd._ext import C
+
+    h = (torch.linspace(-12, 12, 64 * 1000, device=cuda)).to(torch.bfloat16).view(1000, 64)
+    gy = torch.randn(1000, 64, device=cuda).to(torch.bfloat16)
+    for approx in ("none", "tanh"):
+        y = C.gelu_fwd(h, approx == "tanh")
+        torch.testing.assert_close(y.float(), F.gelu(h.float(), approximate=approx), rtol=1e-2, atol=1e-2)
+        hr = h.float().requires_grad_(True)
+        F.gelu(hr, approximate=approx).backward(gy.float())
+        gh, db = C.gelu_bwd(gy, h, approx == "tanh", False)
+        assert db is None
+        torch.testing.assert_close(gh.float(), hr.grad, rtol=1e-2, atol=2e-2)
+        gh2, db2 = C.gelu_bwd(gy, h, approx == "tanh", True)
+        torch.testing.assert_close(db2, gh2.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
 def test_fused_linear_in_place_accumulation_and_weight_cache(cuda):
     """Micro-steps under ``accumulate_grads_in_place`` (what DDP.no_sync enables)
     add dW / db inside the kernels: the accumulated .grad must equal autograd's
@@ -227,15 +280,18 @@ def test_fused_linear_in_place_accumulation_and_weight_cache(cuda):
     g = torch.Generator().manual_seed(13)
     xs = [torch.randn(2, 64, 256, generator=g).to(cuda) for _ in range(3)]
     gys = [torch.randn(2, 64, 384, generator=g).to(cuda).to(torch.bfloat16) for _ in range(3)]
-    for k, (x, gy) in enumerate(zip(xs, gys)):
-        for m, inplace in ((a, True), (b, False)):
-            ctx = accumulate_grads_in_place() if (inplace and k < 2) else contextlib.nullcontext()
-            with ctx, torch.autocast("cuda", dtype=torch.bfloat16):
-                y = m(x)
-            with ctx:
-                y.backward(gy)
-    torch.testing.assert_close(a.weight.grad, b.weight.grad, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(a.bias.grad, b.bias.grad, rtol=1e-5, atol=1e-5)
+    for fwd in ("forward", "forward_gelu"):  # plain Linear, Linear+GELU (bias grad in the GELU kernel)
+        a.zero_grad(set_to_none=True)
+        b.zero_grad(set_to_none=True)
+        for k, (x, gy) in enumerate(zip(xs, gys)):
+            for m, inplace in ((a, True), (b, False)):
+                ctx = accumulate_grads_in_place() if (inplace and k < 2) else contextlib.nullcontext()
+                with ctx, torch.autocast("cuda", dtype=torch.bfloat16):
+                    y = getattr(m, fwd)(x)
+                with ctx:
+                    y.backward(gy)
+        torch.testing.assert_close(a.weight.grad, b.weight.grad, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(a.bias.grad, b.bias.grad, rtol=1e-5, atol=1e-5)
     # weight cache: an optimizer step must invalidate the bf16 copy
     opt = dcp.optim.SGD(a.parameters(), lr=0.5)
     with torch.autocast("cuda", dtype=torch.bfloat16):
