@@ -175,7 +175,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // ------------------------------------------------------------- ops ---
   m.def("mt_copy", &ops::mt_copy, py::arg("src"), py::arg("dst"), py::arg("scale") = 1.0);
   m.def("fused_sgd", &ops::fused_sgd);
-  m.def("fused_adam", &ops::fused_adam);
+  m.def("fused_adam", &ops::fused_adam, pybind11::arg("params"), pybind11::arg("grads"), pybind11::arg("exp_avgs"),
+        pybind11::arg("exp_avg_sqs"), pybind11::arg("max_exp_avg_sqs"), pybind11::arg("lr"), pybind11::arg("beta1"),
+        pybind11::arg("beta2"), pybind11::arg("eps"), pybind11::arg("weight_decay"), pybind11::arg("step"),
+        pybind11::arg("amsgrad"), pybind11::arg("decoupled"), pybind11::arg("maximize"),
+        pybind11::arg("grad_scale"), pybind11::arg("shadows") = std::vector<at::Tensor>{});
   m.def("fused_adadelta", &ops::fused_adadelta);
   m.def("sumsq", &ops::sumsq);
   m.def("scale_by", &ops::scale_by);

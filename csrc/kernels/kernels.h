@@ -33,10 +33,11 @@ void mt_copy(TableView t, int64_t nchunks, DType src, DType dst, float scale, hi
 void mt_sgd(TableView t, int64_t nchunks, DType p, float lr, float momentum, float dampening, float wd,
             bool nesterov, bool maximize, bool first_step, bool has_buf, float grad_scale, hipStream_t s);
 
-// Fused Adam / AdamW. lists: 0 param, 1 grad, 2 exp_avg, 3 exp_avg_sq, 4 max_exp_avg_sq (amsgrad).
+// Fused Adam / AdamW. lists: 0 param, 1 grad, 2 exp_avg, 3 exp_avg_sq, 4 max_exp_avg_sq (amsgrad),
+// then (shadow) a bf16 copy of the updated parameter.
 void mt_adam(TableView t, int64_t nchunks, DType p, float lr, float beta1, float beta2, float eps, float wd,
              float bias_c1, float bias_c2_sqrt, bool amsgrad, bool decoupled_wd, bool maximize, float grad_scale,
-             hipStream_t s);
+             bool shadow, hipStream_t s);
 
 // Fused Adadelta. lists: 0 param, 1 grad, 2 square_avg, 3 acc_delta.
 void mt_adadelta(TableView t, int64_t nchunks, DType p, float lr, float rho, float eps, float wd, bool maximize,

@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(kThreads) mt_sgd_kernel(Tab tab, int64_t nchun
 // ------------------------------------------------------------------ Adam ---
 struct AdamArgs {
   float lr, beta1, beta2, eps, wd, bc1, bc2_sqrt, grad_scale;
-  bool amsgrad, decoupled, maximize;
+  bool amsgrad, decoupled, maximize, shadow;
 };
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float& vmax, const AdamArgs& a) {
@@ -271,12 +271,17 @@ __global__ void __launch_bounds__(kThreads) mt_adam_kernel(Tab tab, int64_t nchu
     void* M = tab.ptr(2, t);
     void* V = tab.ptr(3, t);
     void* VM = a.amsgrad ? tab.ptr(4, t) : nullptr;
+    // bf16 shadow of the updated parameter (the transformer Linears' GEMM
+    // operand): written here instead of a separate cast launch per weight
+    void* SB = a.shadow ? tab.ptr(a.amsgrad ? 5 : 4, t) : nullptr;
+    using SH = Acc<BF16>;
     const int vb = A::kVecBytes;
     const size_t es = sizeof(typename A::S);
     const bool vec = aligned(static_cast<char*>(P) + base * es, vb) &&
                      aligned(static_cast<const char*>(G) + base * es, vb) &&
                      aligned(static_cast<char*>(M) + base * es, vb) && aligned(static_cast<char*>(V) + base * es, vb) &&
-                     (!VM || aligned(static_cast<char*>(VM) + base * es, vb));
+                     (!VM || aligned(static_cast<char*>(VM) + base * es, vb)) &&
+                     (!SB || aligned(static_cast<char*>(SB) + base * 2, 8));
     int64_t i0 = 0;
     if (vec) {
       const int64_t nv = len >> 2;
@@ -294,6 +299,7 @@ __global__ void __launch_bounds__(kThreads) mt_adam_kernel(Tab tab, int64_t nchu
         A::st4(M, i, m);
         A::st4(V, i, v);
         if (VM) A::st4(VM, i, vm);
+        if (SB) SH::st4(SB, i, p);
       }
       i0 = nv << 2;
     }
@@ -305,6 +311,7 @@ __global__ void __launch_bounds__(kThreads) mt_adam_kernel(Tab tab, int64_t nchu
       A::st(M, i, m);
       A::st(V, i, v);
       if (VM) A::st(VM, i, vm);
+      if (SB) SH::st(SB, i, p);
     }
   });
 }
@@ -479,9 +486,9 @@ void mt_sgd(TableView t, int64_t nchunks, DType p, float lr, float momentum, flo
 
 void mt_adam(TableView t, int64_t nchunks, DType p, float lr, float beta1, float beta2, float eps, float wd,
              float bias_c1, float bias_c2_sqrt, bool amsgrad, bool decoupled_wd, bool maximize, float grad_scale,
-             hipStream_t s) {
+             bool shadow, hipStream_t s) {
   if (nchunks <= 0) return;
-  AdamArgs a{lr, beta1, beta2, eps, wd, bias_c1, bias_c2_sqrt, grad_scale, amsgrad, decoupled_wd, maximize};
+  AdamArgs a{lr, beta1, beta2, eps, wd, bias_c1, bias_c2_sqrt, grad_scale, amsgrad, decoupled_wd, maximize, shadow};
   DCP_DISPATCH_DTYPE(p, PD,
       hipLaunchKernelGGL((mt_adam_kernel<PD>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks, a));
 }

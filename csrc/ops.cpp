@@ -262,10 +262,19 @@ void fused_sgd(const TensorList& params, const TensorList& grads, const TensorLi
 void fused_adam(const TensorList& params, const TensorList& grads, const TensorList& exp_avgs,
                 const TensorList& exp_avg_sqs, const TensorList& max_exp_avg_sqs, double lr, double beta1,
                 double beta2, double eps, double weight_decay, double step, bool amsgrad, bool decoupled,
-                bool maximize, double grad_scale) {
+                bool maximize, double grad_scale, const TensorList& shadows) {
   if (params.empty()) return;
   std::vector<const TensorList*> lists{&params, &grads, &exp_avgs, &exp_avg_sqs};
   if (amsgrad) lists.push_back(&max_exp_avg_sqs);
+  // shadows: optional bf16 copies of fp32 params, rewritten with the updated values
+  const bool shadow = !shadows.empty();
+  if (shadow) {
+    lists.push_back(&shadows);
+    for (size_t i = 0; i < shadows.size(); ++i)
+      DCP_CHECK(shadows[i].scalar_type() == at::kBFloat16 && params[i].scalar_type() == at::kFloat &&
+                    shadows[i].is_contiguous() && params[i].is_contiguous(),
+                "fused_adam: shadows must be contiguous bf16 copies of contiguous fp32 params");
+  }
   check_lists(lists, "fused_adam");
   const double bc1 = 1.0 - std::pow(beta1, step);
   const double bc2_sqrt = std::sqrt(1.0 - std::pow(beta2, step));
@@ -276,7 +285,7 @@ void fused_adam(const TensorList& params, const TensorList& grads, const TensorL
                   static_cast<float>(lr), static_cast<float>(beta1), static_cast<float>(beta2),
                   static_cast<float>(eps), static_cast<float>(weight_decay), static_cast<float>(bc1),
                   static_cast<float>(bc2_sqrt), amsgrad, decoupled, maximize, static_cast<float>(grad_scale),
-                  cur_stream(params[0]));
+                  shadow, cur_stream(params[0]));
     return;
   }
   for (size_t t = 0; t < params.size(); ++t) {
@@ -317,6 +326,7 @@ void fused_adam(const TensorList& params, const TensorList& grads, const TensorL
       });
     });
   }
+  for (size_t t = 0; t < shadows.size(); ++t) shadows[t].copy_(params[t]);
 }
 
 // -------------------------------------------------------------- Adadelta ---

@@ -23,6 +23,8 @@ from .._ext import C as _C
 
 # DCP_FUSED_GELU=0: forward_gelu falls back to FusedLinear + ATen GELU (A/B switch)
 _FUSED_GELU = os.environ.get("DCP_FUSED_GELU", "1") != "0"
+# DCP_BF16_SHADOWS=0: do not let the fused Adam/AdamW write the bf16 weight copies (A/B switch)
+_SHADOWS = os.environ.get("DCP_BF16_SHADOWS", "1") != "0"
 
 # > 0 while gradients accumulate locally (DistributedDataParallel.no_sync): the
 # backward then adds dW / db straight into existing fp32 .grad tensors inside
@@ -154,13 +156,17 @@ class FusedLinear(nn.Linear):
         is being captured (the cast must be part of every replay)."""
         if torch.cuda.is_current_stream_capturing():
             return None
-        from ..optim.fused import param_epoch
+        from ..optim.fused import fresh_bf16_shadow, param_epoch, register_bf16_shadow
 
         key = (p._version, param_epoch(), p.data_ptr())
         c = self.__dict__.get(slot)
         if c is not None and c[0] == key:
             return c[1]
-        t = p.detach().to(torch.bfloat16)
+        t = fresh_bf16_shadow(p)  # rewritten by the fused Adam/AdamW step: no cast launch
+        if t is None:
+            t = p.detach().to(torch.bfloat16)
+            if _SHADOWS:
+                register_bf16_shadow(p, t)
         self.__dict__[slot] = (key, t)
         return t
 

@@ -15,10 +15,11 @@ dtype follows the parameter (as in torch).
 from __future__ import annotations
 
 from collections import defaultdict
-from typing import Iterable, List
+from typing import Iterable, List, Optional
 
 import torch
 from torch.optim import Optimizer
+from torch.utils.weak import WeakIdKeyDictionary
 
 from .._ext import C as _C
 
@@ -31,6 +32,28 @@ _PARAM_EPOCH = [0]
 
 def param_epoch() -> int:
     return _PARAM_EPOCH[0]
+
+
+# fp32 parameter -> [bf16 shadow, epoch, _version]: bf16 copies that the
+# consumer (ops.linear.FusedLinear) registers once; the fused Adam/AdamW kernel
+# then rewrites them with the updated weights in the same pass as the update
+# (no separate cast launch per weight per step — 150 launches / 0.7 ms of a
+# BERT-base step, profiles/r1_bert_prof71_gelu.txt). A shadow is valid only
+# while (epoch, _version) match, i.e. nobody modified the parameter since.
+_BF16_SHADOWS = WeakIdKeyDictionary()
+
+
+def register_bf16_shadow(p: torch.Tensor, shadow: torch.Tensor) -> None:
+    if p.dtype == torch.float32 and p.is_cuda and p.is_contiguous() and shadow.shape == p.shape:
+        _BF16_SHADOWS[p] = [shadow, _PARAM_EPOCH[0], p._version]
+
+
+def fresh_bf16_shadow(p: torch.Tensor) -> Optional[torch.Tensor]:
+    """The registered shadow of ``p`` if it holds p's current values."""
+    e = _BF16_SHADOWS.get(p)
+    if e is not None and e[1] == _PARAM_EPOCH[0] and e[2] == p._version:
+        return e[0]
+    return None
 
 
 def _grads_ok(p: torch.Tensor) -> bool:
@@ -117,7 +140,8 @@ class Adam(Optimizer):
         for group in self.param_groups:
             b1, b2 = group["betas"]
             ams = group["amsgrad"]
-            buckets = defaultdict(lambda: ([], [], [], [], []))
+            buckets = defaultdict(lambda: ([], [], [], [], [], []))
+            shadowed = []
             for p in group["params"]:
                 if not _grads_ok(p):
                     continue
@@ -129,18 +153,25 @@ class Adam(Optimizer):
                     if ams:
                         st["max_exp_avg_sq"] = _state_like(p)
                 st["step"] += 1
-                key = (p.device, p.dtype, float(st["step"]))
-                P, G, M, V, VM = buckets[key]
+                sh = _BF16_SHADOWS.get(p) if p.is_cuda else None
+                key = (p.device, p.dtype, float(st["step"]), sh is not None)
+                P, G, M, V, VM, S = buckets[key]
                 P.append(p)
                 G.append(_dense_like(p.grad, p))
                 M.append(st["exp_avg"])
                 V.append(st["exp_avg_sq"])
                 if ams:
                     VM.append(st["max_exp_avg_sq"])
-            for (dev, dt, step), (P, G, M, V, VM) in buckets.items():
+                if sh is not None:
+                    S.append(sh[0])
+                    shadowed.append(p)
+            for (dev, dt, step, _), (P, G, M, V, VM, S) in buckets.items():
                 _C.fused_adam(P, G, M, V, VM, group["lr"], b1, b2, group["eps"], group["weight_decay"], step, ams,
-                              group["decoupled_weight_decay"], group["maximize"], grad_scale)
+                              group["decoupled_weight_decay"], group["maximize"], grad_scale, S)
         _PARAM_EPOCH[0] += 1
+        for p in shadowed:  # rewritten by the kernel: valid for the new epoch
+            e = _BF16_SHADOWS[p]
+            e[1], e[2] = _PARAM_EPOCH[0], p._version
         return loss
 
 

@@ -302,3 +302,35 @@ def test_fused_linear_in_place_accumulation_and_weight_cache(cuda):
     ref = F.linear(xs[0].to(torch.bfloat16), a.weight.to(torch.bfloat16), a.bias.to(torch.bfloat16))
     assert not torch.equal(y0, y1)
     torch.testing.assert_close(y1, ref, rtol=0, atol=0)
+
+
+def test_adamw_writes_bf16_shadow_weights(cuda):
+    """FusedLinear registers its bf16 weight copy; the fused AdamW step rewrites
+    it in the update kernel (RNE, identical to a fresh .to(bf16)) and the next
+    forward reuses it without a cast."""
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.ops.linear import FusedLinear
+    from distributed_compute_pytorch_amd.optim.fused import fresh_bf16_shadow
+
+    torch.manual_seed(0)
+    a = FusedLinear(256, 384).to(cuda)
+    opt = dcp.optim.AdamW(a.parameters(), lr=1e-2)
+    x = torch.randn(4, 64, 256, device=cuda)
+    for _ in range(3):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = a.forward_gelu(x, "tanh")
+        y.float().square().mean().backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        sw = fresh_bf16_shadow(a.weight)
+        assert sw is not None and fresh_bf16_shadow(a.bias) is not None
+        torch.testing.assert_close(sw, a.weight.detach().to(torch.bfloat16), rtol=0, atol=0)
+        torch.testing.assert_close(fresh_bf16_shadow(a.bias), a.bias.detach().to(torch.bfloat16), rtol=0, atol=0)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = a(x)
+    assert a._w16_cache[1] is fresh_bf16_shadow(a.weight)
+    ref = F.linear(x.to(torch.bfloat16), a.weight.to(torch.bfloat16), a.bias.to(torch.bfloat16))
+    torch.testing.assert_close(y, ref, rtol=0, atol=0)
+    with torch.no_grad():  # an out-of-band write invalidates the shadow
+        a.weight.mul_(0.5)
+    assert fresh_bf16_shadow(a.weight) is None

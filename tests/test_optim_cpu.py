@@ -82,3 +82,24 @@ def test_mt_copy_cpu():
     C.mt_copy(src, dst, 2.0)
     for s, d in zip(src, dst):
         torch.testing.assert_close(d, s * 2)
+
+
+def test_fused_adam_shadow_list_cpu():
+    """fused_adam's optional bf16 shadow list holds the updated params (host path)."""
+    from distributed_compute_pytorch_amd._ext import C
+
+    torch.manual_seed(0)
+    ps = [torch.randn(37), torch.randn(8, 16)]
+    gs = [torch.randn_like(p) for p in ps]
+    ms = [torch.zeros_like(p) for p in ps]
+    vs = [torch.zeros_like(p) for p in ps]
+    sh = [torch.empty_like(p, dtype=torch.bfloat16) for p in ps]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    C.fused_adam(ps, gs, ms, vs, [], 1e-2, 0.9, 0.999, 1e-8, 0.01, 1.0, False, True, False, 1.0, sh)
+    opt = torch.optim.AdamW(ref, lr=1e-2, weight_decay=0.01)
+    for r, g in zip(ref, gs):
+        r.grad = g.clone()
+    opt.step()
+    for p, r, s in zip(ps, ref, sh):
+        torch.testing.assert_close(p, r.detach(), rtol=1e-6, atol=1e-6)
+        assert torch.equal(s, p.to(torch.bfloat16))
