@@ -734,10 +734,12 @@ std::vector<at::Tensor> layer_norm_fwd(const at::Tensor& x, const c10::optional<
   return {y, mean, rstd};
 }
 
-// Returns (dx, dweight, dbias).
+// Returns (dx, dweight, dbias). With accumulate_into = (weight.grad, bias.grad)
+// (fp32, contiguous [D]) the parameter gradients are added into those tensors by
+// the finalize kernel and returned undefined.
 std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& weight,
                                        const c10::optional<at::Tensor>& bias, const at::Tensor& mean,
-                                       const at::Tensor& rstd) {
+                                       const at::Tensor& rstd, const c10::optional<std::vector<at::Tensor>>& accumulate_into) {
   c10::hip::HIPGuard guard(x.device().index());
   at::Tensor g = dy.contiguous();
   // dy arrives in y's dtype (bf16 when the forward wrote bf16 from fp32 x)
@@ -747,13 +749,26 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
   const int64_t rows = x.numel() / D;
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor dx = at::empty_like(x);
-  at::Tensor dw = at::empty({D}, fopt), db = at::empty({D}, fopt);
+  const bool accum = accumulate_into.has_value();
+  at::Tensor dw, db;
+  if (accum) {
+    DCP_CHECK(accumulate_into->size() == 2, "layer_norm_bwd: accumulate_into = (weight.grad, bias.grad)");
+    dw = (*accumulate_into)[0];
+    db = (*accumulate_into)[1];
+    for (const auto& t : *accumulate_into)
+      DCP_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == D,
+                "layer_norm_bwd: accumulate_into tensors must be fp32 contiguous [D]");
+  } else {
+    dw = at::empty({D}, fopt);
+    db = at::empty({D}, fopt);
+  }
   at::Tensor part = at::empty({static_cast<int64_t>(kern::ln_bwd_blocks(rows)) * 2 * D}, fopt);
   const bool has_w = weight.has_value() && weight->defined();
   at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
   kern::ln_backward(ln_dtype(x), ln_dtype(g), g.data_ptr(), x.data_ptr(), has_w ? w.data_ptr<float>() : nullptr,
                     mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(),
-                    db.data_ptr<float>(), part.data_ptr<float>(), rows, static_cast<int>(D), stream_of(x));
+                    db.data_ptr<float>(), part.data_ptr<float>(), rows, static_cast<int>(D), accum, stream_of(x));
+  if (accum) return {dx, at::Tensor(), at::Tensor()};
   const bool has_b = bias.has_value() && bias->defined();
   return {dx, has_w ? dw.to(weight->scalar_type()) : at::Tensor(), has_b ? db.to(bias->scalar_type()) : at::Tensor()};
 }
@@ -993,7 +1008,9 @@ void bind(pybind11::module& m) {
   m.def("layer_norm_supported", &layer_norm_supported);
   m.def("layer_norm_fwd", &layer_norm_fwd, pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
         pybind11::arg("eps"), pybind11::arg("out_dtype") = pybind11::none());
-  m.def("layer_norm_bwd", &layer_norm_bwd);
+  m.def("layer_norm_bwd", &layer_norm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("weight"),
+        pybind11::arg("bias"), pybind11::arg("mean"), pybind11::arg("rstd"),
+        pybind11::arg("accumulate_into") = pybind11::none());
   m.def("cross_entropy_fwd", &cross_entropy_fwd);
   m.def("log_softmax_fwd", &log_softmax_fwd, pybind11::arg("x"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("log_softmax_bwd", &log_softmax_bwd);

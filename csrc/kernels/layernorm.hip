@@ -245,8 +245,9 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
   }
 }
 
+// accum != 0: add into dw / db (fp32 .grad under DistributedDataParallel.no_sync)
 __global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int D, float* __restrict__ dw,
-                                       float* __restrict__ db) {
+                                       float* __restrict__ db, int accum) {
   constexpr int tpc = 16;
   const int c = blockIdx.x * (256 / tpc) + threadIdx.x / tpc;
   const int j = threadIdx.x % tpc;
@@ -264,8 +265,8 @@ __global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
     sb += __shfl_xor(sb, off, 64);
   }
   if (c < D && j == 0) {
-    if (dw) dw[c] = sg;
-    if (db) db[c] = sb;
+    if (dw) dw[c] = accum ? dw[c] + sg : sg;
+    if (db) db[c] = accum ? db[c] + sb : sb;
   }
 }
 
@@ -332,7 +333,8 @@ void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const flo
 }
 
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
-                 const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, hipStream_t s) {
+                 const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
+                 hipStream_t s) {
   const int nblk = ln_bwd_blocks(rows);
   const int rpb = static_cast<int>((rows + nblk - 1) / nblk);
   const size_t sm = sizeof(float) * kWaves * 2 * D;
@@ -343,7 +345,7 @@ void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const fl
     bwd_dispatch<LN_F32, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
   else
     bwd_dispatch<LN_F32, LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
-  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, part, nblk, D, dw, db);
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, part, nblk, D, dw, db, accum ? 1 : 0);
 }
 
 }  // namespace kern

@@ -16,9 +16,10 @@ int ln_bwd_blocks(int64_t rows);
 // xdtype: x / dx; ydtype: y / dy (fp32->bf16 supported; bf16 x implies bf16 y)
 void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const float* b, void* y, float* mean,
                 float* rstd, int64_t rows, int D, float eps, hipStream_t s);
-// part: workspace [ln_bwd_blocks(rows) * 2 * D] fp32
+// part: workspace [ln_bwd_blocks(rows) * 2 * D] fp32; accum: dw / db += instead of =
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
-                 const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, hipStream_t s);
+                 const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
+                 hipStream_t s);
 
 // Cross-entropy over [rows, V] logits (bf16/fp32, row stride ld elements).
 // Forward: loss[row] = lse - logit[target] (0 for ignore_index), lse saved.

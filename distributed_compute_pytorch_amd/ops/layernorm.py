@@ -8,11 +8,17 @@ autocast's fp32 upcast of layer_norm. Elsewhere it is ``F.layer_norm``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 from torch.nn import functional as F
 
 from .._ext import C as _C
+from .linear import _acc_target
+
+# DCP_LN_ACCUM=0: leave dγ / dβ to autograd's AccumulateGrad under no_sync (A/B switch)
+_LN_ACCUM = os.environ.get("DCP_LN_ACCUM", "1") != "0"
 
 
 class _LNFn(torch.autograd.Function):
@@ -20,12 +26,22 @@ class _LNFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, eps, out_dtype):
         y, mean, rstd = _C.layer_norm_fwd(x, weight, bias, eps, out_dtype)
         ctx.save_for_backward(x, weight, bias, mean, rstd)
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, weight, bias, mean, rstd = ctx.saved_tensors
-        dx, dw, db = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd)
+        acc = None
+        if _LN_ACCUM and weight is not None and bias is not None and ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            # under DistributedDataParallel.no_sync: add dγ / dβ into the fp32
+            # .grad tensors in the finalize kernel (no AccumulateGrad adds; see
+            # linear.accumulate_grads_in_place)
+            D = torch.Size((x.shape[-1],))
+            tw, tb = _acc_target(ctx.params[0], D), _acc_target(ctx.params[1], D)
+            if tw is not None and tb is not None:
+                acc = [tw, tb]
+        dx, dw, db = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd, accumulate_into=acc)
         return dx, dw, db, None, None
 
 

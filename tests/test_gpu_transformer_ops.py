@@ -304,6 +304,47 @@ def test_fused_linear_in_place_accumulation_and_weight_cache(cuda):
     torch.testing.assert_close(y1, ref, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16])
+def test_layer_norm_in_place_accumulation(cuda, xdtype):
+    """Under ``accumulate_grads_in_place`` the LayerNorm finalize kernel adds
+    dγ / dβ into the existing fp32 .grad (no AccumulateGrad add): the result
+    must equal autograd's own accumulation over the same micro-steps."""
+    import copy
+
+    from distributed_compute_pytorch_amd.ops.layernorm import FusedLayerNorm
+    from distributed_compute_pytorch_amd.ops.linear import accumulate_grads_in_place
+
+    torch.manual_seed(0)
+    a = FusedLayerNorm(768).to(cuda)
+    with torch.no_grad():
+        a.weight.uniform_(0.5, 1.5)
+        a.bias.uniform_(-0.5, 0.5)
+    b = copy.deepcopy(a)
+    g = torch.Generator().manual_seed(17)
+    xs = [torch.randn(4, 100, 768, generator=g).to(cuda).to(xdtype) for _ in range(3)]
+    gys = [torch.randn(4, 100, 768, generator=g).to(cuda).to(xdtype) for _ in range(3)]
+    dxa, dxb = [], []
+    for k, (x, gy) in enumerate(zip(xs, gys)):
+        for m, inplace, dxs in ((a, True, dxa), (b, False, dxb)):
+            xx = x.clone().requires_grad_(True)
+            ctx = accumulate_grads_in_place() if (inplace and k < 2) else contextlib.nullcontext()
+            with ctx:
+                m(xx).backward(gy)
+            dxs.append(xx.grad)
+    for u, v in zip(dxa, dxb):
+        torch.testing.assert_close(u, v, rtol=0, atol=0)
+    torch.testing.assert_close(a.weight.grad, b.weight.grad, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(a.bias.grad, b.bias.grad, rtol=1e-5, atol=1e-4)
+    # the sum of the three micro-steps against an fp32 PyTorch reference
+    wr = b.weight.detach().clone().requires_grad_(True)
+    br = b.bias.detach().clone().requires_grad_(True)
+    for x, gy in zip(xs, gys):
+        F.layer_norm(x.float(), (768,), wr, br, 1e-5).backward(gy.float())
+    tol = 2e-2 if xdtype == torch.bfloat16 else 1e-3
+    torch.testing.assert_close(a.weight.grad, wr.grad, rtol=tol, atol=tol)
+    torch.testing.assert_close(a.bias.grad, br.grad, rtol=tol, atol=tol)
+
+
 def test_adamw_writes_bf16_shadow_weights(cuda):
     """FusedLinear registers its bf16 weight copy; the fused AdamW step rewrites
     it in the update kernel (RNE, identical to a fresh .to(bf16)) and the next
