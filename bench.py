@@ -43,13 +43,14 @@ def _vs_baseline(model, wl, world, total):
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "stock_baselines.json")
     try:
         with open(path) as f:
-            ref = json.load(f).get(model)
+            refs = json.load(f).get(model)
     except (OSError, ValueError):
         return None
-    if not ref or ref.get("per_gpu_batch") != wl.per_gpu_batch or ref.get("grad_accum", 1) != wl.accum \
-            or ref.get("seq_len") != wl.seq_len:
-        return None
-    return round(total / (ref["samples_per_s_per_gpu"] * world), 4)
+    for ref in (refs if isinstance(refs, list) else [refs]):
+        if ref and ref.get("per_gpu_batch") == wl.per_gpu_batch and ref.get("grad_accum", 1) == wl.accum \
+                and ref.get("seq_len") == wl.seq_len:
+            return round(total / (ref["samples_per_s_per_gpu"] * world), 4)
+    return None
 
 
 def log(*a):

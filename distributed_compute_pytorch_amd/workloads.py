@@ -76,7 +76,10 @@ def build(name: str, device, batch: Optional[int] = None, fused: bool = True, se
 
     name = name.lower()
     if name == "resnet50":
-        b = batch or 256
+        # 512 per GPU: 288 GB of HBM holds it with room to spare; +6 % over 256
+        # on one MI355X and half the all-reduce bytes per sample at N > 1
+        # (tools/gpu_run79.sh, profiles/r1_resnet50_b512_pairs79.jsonl)
+        b = batch or 512
         m = models.resnet50(fused_bn=fused, fused_gemm=fused if fused_gemm is None else (fused and fused_gemm)).to(device)
         if channels_last:
             m = m.to(memory_format=torch.channels_last)
