@@ -11,8 +11,12 @@ A step = zero_grad + forward (bf16 autocast, channels_last) + loss + backward
 Synthetic data / random-init weights of the full-size model.
 
     python bench.py                                   # ResNet-50, 1 GPU
+    python bench.py --gpus 8                          # self-launches 8 ranks (parent never touches a GPU)
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
-        --master-port 29500 bench.py --gpus 8
+        --master-port 29500 bench.py --gpus 8         # same, under torchrun (the driver's form)
+    python bench.py --comm-timing 1                   # + per-bucket ready/comm ms, exposed comm ms
+    python bench.py --bucket-sweep 4,8,16,25,50,100   # config #4: one JSON line per bucket cap (MiB)
+    python bench.py --gpus 8 --ref-1gpu 11200         # + scaling_efficiency vs a 1-GPU samples/s
     python bench.py --impl torch                      # stock torch DDP + torch.optim baseline
     python bench.py --model gpt2                      # GPT-2-small + grad accumulation (config #5)
     python bench.py --model bert                      # BERT-base pre-training (config #3)
@@ -77,7 +81,36 @@ def parse():
     ap.add_argument("--benchmark-cudnn", type=int, default=1)
     ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a HIP graph")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--comm-timing", type=int, default=0,
+                    help="record per-bucket device comm time + exposed (un-overlapped) comm ms in the JSON")
+    ap.add_argument("--bucket-sweep", default=None,
+                    help="comma-separated bucket caps in MiB: one timed run and one JSON line per cap")
+    ap.add_argument("--ref-1gpu", type=float, default=None,
+                    help="1-GPU samples/s of the same config: adds scaling_efficiency = value / (N * ref)")
     return ap.parse_args()
+
+
+def _self_launch(a) -> int:
+    """``--gpus N`` without a launcher: start N ranks of this script (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set, one process per GPU) and return the
+    job's exit code; rank 0 prints the JSON line. The parent never initialises
+    the GPU (device_count() does not, on this image) and does not import the
+    package (its extension links the HIP runtime)."""
+    import importlib.util
+
+    n = torch.cuda.device_count()
+    if n < a.gpus:
+        log(f"[bench] --gpus {a.gpus} requested but only {n} GPU(s) are visible; refusing to oversubscribe "
+            f"(RCCL needs one device per rank)")
+        return 2
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location(
+        "_dcp_launch", os.path.join(here, "distributed_compute_pytorch_amd", "distributed", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    log(f"[bench] self-launching {a.gpus} ranks")
+    return mod.launch_env([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], a.gpus,
+                          master_addr="127.0.0.1")
 
 
 def _heartbeat(period=30.0):
@@ -98,12 +131,17 @@ def _heartbeat(period=30.0):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # decided before ANY torch.cuda call: the parent must not own a GPU context
+        raise SystemExit(_self_launch(a))
     _heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         log(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if a.comm_timing:
+        os.environ["DCP_COMM_TIMING"] = "1"  # read by the communicator / Reducer at construction
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
     torch.cuda.set_device(local)
@@ -130,115 +168,140 @@ def main():
 
     # graph capture: build DDP / optimizer under the capture stream (AccumulateGrad
     # nodes are bound to the stream current at their creation)
-    stream_ctx = torch.cuda.stream(capture_stream()) if a.graph else contextlib.nullcontext()
+    stream_ctx = (lambda: torch.cuda.stream(capture_stream())) if a.graph else contextlib.nullcontext
     if ours:
         dcp.distributed.init_process_group("rccl", device_id=local)
-        kw = {}
-        if a.bucket_cap_mb is not None:
-            kw["bucket_cap_mb"] = a.bucket_cap_mb
-        if a.first_bucket_mb is not None:
-            kw["first_bucket_mb"] = a.first_bucket_mb
-        if a.comm_dtype == "bf16":
-            kw["comm_dtype"] = torch.bfloat16
-        with stream_ctx:
-            ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[local],
-                                                       gradient_as_bucket_view=bool(a.grad_as_view), **kw)
-            opt = wl.make_optimizer(ddp.parameters())
         barrier = dcp.distributed.barrier
-
-        def max_over_ranks(x):
-            t = torch.tensor([x], device=dev)
-            dcp.distributed.all_reduce(t, dcp.distributed.ReduceOp.MAX)
-            return float(t.item())
+        all_reduce, MAX = dcp.distributed.all_reduce, dcp.distributed.ReduceOp.MAX
     else:
         import torch.distributed as tdist
 
         tdist.init_process_group("nccl", device_id=dev)
+        barrier = tdist.barrier
+        all_reduce, MAX = tdist.all_reduce, tdist.ReduceOp.MAX
+
+    def max_over_ranks(x):
+        t = torch.tensor([x], device=dev)
+        all_reduce(t, MAX)
+        return float(t.item())
+
+    def build_ddp(cap_mb):
         kw = {}
-        if a.bucket_cap_mb is not None:
-            kw["bucket_cap_mb"] = a.bucket_cap_mb
-        with stream_ctx:
+        if cap_mb is not None:
+            kw["bucket_cap_mb"] = cap_mb
+        if ours:
+            if a.first_bucket_mb is not None:
+                kw["first_bucket_mb"] = a.first_bucket_mb
+            if a.comm_dtype == "bf16":
+                kw["comm_dtype"] = torch.bfloat16
+            with stream_ctx():
+                ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[local],
+                                                           gradient_as_bucket_view=bool(a.grad_as_view), **kw)
+                opt = wl.make_optimizer(ddp.parameters())
+            return ddp, opt
+        with stream_ctx():
             ddp = torch.nn.parallel.DistributedDataParallel(wl.model, device_ids=[local], **kw)
         ours_opt = wl.make_optimizer([torch.nn.Parameter(torch.zeros(1, device=dev))])
         cls = getattr(torch.optim, type(ours_opt).__name__)
         opt = cls(ddp.parameters(), **{k: v for k, v in ours_opt.defaults.items()
                                        if k not in ("decoupled_weight_decay",)})
-        barrier = tdist.barrier
+        return ddp, opt
 
-        def max_over_ranks(x):
-            t = torch.tensor([x], device=dev)
-            tdist.all_reduce(t, tdist.ReduceOp.MAX)
-            return float(t.item())
-
-    step = workloads.make_step(wl, ddp, opt, graph=bool(a.graph))
-    t_w = time.time()
-    for i in range(a.warmup):
-        loss = step()
-        if rank == 0 and (i == 0 or (i + 1) % 5 == 0):
-            torch.cuda.synchronize()
-            log(f"[bench] warmup {i + 1}/{a.warmup} loss={loss.item():.4f} t={time.time() - t_w:.1f}s")
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
-    ms = elapsed / a.steps * 1000.0
-    samples_per_step = wl.per_gpu_batch * wl.accum * world
-    total = samples_per_step * a.steps / elapsed
-    if rank == 0:
-        cfg = {
-            "model": a.model,
-            "global_batch": samples_per_step,
-            "per_gpu_batch": wl.per_gpu_batch,
-            "grad_accum": wl.accum,
-            "seq_len": wl.seq_len,
-            "parallelism": f"dp{world}",
-            "impl": a.impl,
-            "fused_kernels": fused,
-            "optimizer": type(opt).__name__,
-            "comm_dtype": a.comm_dtype,
-            "hip_graph": bool(a.graph),
-        }
-        if a.model == "resnet50":
-            cfg["mfma_1x1_gemm"] = bool(a.gemm) and fused
-        if a.model == "resnet50":
-            cfg.update(image_size=224, channels_last=bool(a.channels_last))
+    def timed_run(cap_mb):
+        ddp, opt = build_ddp(cap_mb)
+        step = workloads.make_step(wl, ddp, opt, graph=bool(a.graph))
+        t_w = time.time()
+        for i in range(a.warmup):
+            loss = step()
+            if rank == 0 and (i == 0 or (i + 1) % 5 == 0):
+                torch.cuda.synchronize()
+                log(f"[bench] warmup {i + 1}/{a.warmup} loss={loss.item():.4f} t={time.time() - t_w:.1f}s")
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            loss = step()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        elapsed = max_over_ranks(time.perf_counter() - t0)
+        ms = elapsed / a.steps * 1000.0
+        samples_per_step = wl.per_gpu_batch * wl.accum * world
+        total = samples_per_step * a.steps / elapsed
+        rec = None
         if ours:
             info = ddp.ddp_logging_data()
-            cfg["buckets_mb"] = [round(b / 2**20, 2) for b in info["bucket_sizes"]]
-        rec = {
-            "metric": METRICS[a.model],
-            "value": round(total, 2),
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16" if wl.amp else "fp32",
-            "data": "synthetic (on-device random inputs/labels); random-init weights",
-            "config": cfg,
-        }
-        if wl.seq_len:
-            rec["tokens_per_s"] = round(total * wl.seq_len, 1)
-        rec["vs_baseline"] = _vs_baseline(a.model, wl, world, total)
-        line = json.dumps(rec)
-        print(line, flush=True)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                f.write(line + "\n")
+        if rank == 0:
+            cfg = {
+                "model": a.model,
+                "global_batch": samples_per_step,
+                "per_gpu_batch": wl.per_gpu_batch,
+                "grad_accum": wl.accum,
+                "seq_len": wl.seq_len,
+                "parallelism": f"dp{world}",
+                "impl": a.impl,
+                "fused_kernels": fused,
+                "optimizer": type(opt).__name__,
+                "comm_dtype": a.comm_dtype,
+                "hip_graph": bool(a.graph),
+            }
+            if a.model == "resnet50":
+                cfg.update(mfma_1x1_gemm=bool(a.gemm) and fused, image_size=224, channels_last=bool(a.channels_last))
+            if ours:
+                cfg["bucket_cap_mb"] = round(info["bucket_cap_bytes"] / 2**20, 3)
+                cfg["first_bucket_mb"] = round(info["first_bucket_bytes"] / 2**20, 3)
+                cfg["buckets_mb"] = [round(b / 2**20, 2) for b in info["bucket_sizes"]]
+            elif cap_mb is not None:
+                cfg["bucket_cap_mb"] = cap_mb
+            rec = {
+                "metric": METRICS[a.model],
+                "value": round(total, 2),
+                "unit": "samples/s",
+                "n_gpus": world,
+                "steps": a.steps,
+                "warmup": a.warmup,
+                "ms_per_step": round(ms, 3),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "bf16" if wl.amp else "fp32",
+                "data": "synthetic (on-device random inputs/labels); random-init weights",
+                "config": cfg,
+            }
+            if wl.seq_len:
+                rec["tokens_per_s"] = round(total * wl.seq_len, 1)
+            rec["vs_baseline"] = _vs_baseline(a.model, wl, world, total)
+            if a.ref_1gpu:
+                rec["scaling_efficiency"] = round(total / (world * a.ref_1gpu), 4)
+            if ours and a.comm_timing:
+                # last timed iteration: when each bucket became ready (host ms
+                # since backward start), its collective's device time, and the
+                # device time the step waited for communication after backward
+                rec["comm"] = {
+                    "bucket_ready_ms": [round(x, 3) for x in info["bucket_ready_ms"]],
+                    "bucket_comm_ms": [round(x, 4) for x in info["bucket_comm_ms"]],
+                    "exposed_comm_ms": round(info["exposed_comm_ms"], 4),
+                    "comm_bytes_per_step": sum(info["bucket_sizes"]),
+                }
+        del step, ddp, opt
+        return rec
+
+    caps = [float(c) for c in a.bucket_sweep.split(",")] if a.bucket_sweep else [a.bucket_cap_mb]
+    for cap in caps:
+        rec = timed_run(cap)
+        if rec is not None:
+            line = json.dumps(rec)
+            print(line, flush=True)
+            if a.json_out:
+                with open(a.json_out, "a" if a.bucket_sweep else "w") as f:
+                    f.write(line + "\n")
+        import gc
+
+        gc.collect()
     if ours:
         dcp.distributed.destroy_process_group()
     else:
-        import torch.distributed as tdist
-
         tdist.destroy_process_group()
 
 

@@ -103,6 +103,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("recv", &Communicator::recv, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &Communicator::barrier, py::call_guard<py::gil_scoped_release>())
       .def("abort", &Communicator::abort)
+      .def("split", &Communicator::split, py::arg("color"), py::arg("key"), py::arg("prefix"),
+           py::call_guard<py::gil_scoped_release>())
       .def("error", &Communicator::error)
       .def("set_debug_fingerprint", &Communicator::set_debug_fingerprint)
       .def_property_readonly("ops_issued", &Communicator::ops_issued)
@@ -119,6 +121,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("compute_bucket_assignment", &compute_bucket_assignment, py::arg("sizes_bytes"), py::arg("keys"),
         py::arg("limits"), py::arg("order") = std::vector<int64_t>{});
 
+  m.def("split_tail_bucket", &split_tail_bucket, py::arg("assignment"), py::arg("sizes_bytes"),
+        py::arg("tail_bytes"));
+
   py::class_<ReducerOptions>(m, "ReducerOptions")
       .def(py::init<>())
       .def_readwrite("gradient_as_bucket_view", &ReducerOptions::gradient_as_bucket_view)
@@ -126,6 +131,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("rebuild_buckets", &ReducerOptions::rebuild_buckets)
       .def_readwrite("first_bucket_bytes", &ReducerOptions::first_bucket_bytes)
       .def_readwrite("bucket_bytes_cap", &ReducerOptions::bucket_bytes_cap)
+      .def_readwrite("tail_bucket_bytes", &ReducerOptions::tail_bucket_bytes)
       .def_readwrite("comm_dtype", &ReducerOptions::comm_dtype)
       .def_readwrite("average", &ReducerOptions::average);
 
@@ -155,9 +161,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                return;
              }
              auto holder = std::make_shared<py::object>(fn);
-             r.set_comm_hook([holder](at::Tensor& bucket) -> WorkPtr {
+             r.set_comm_hook([holder](at::Tensor& bucket, int64_t index) -> WorkPtr {
                py::gil_scoped_acquire g;
-               py::object res = (*holder)(bucket);
+               py::object res = (*holder)(bucket, index);
                if (res.is_none()) return std::make_shared<DoneWork>();
                return res.cast<WorkPtr>();
              });
@@ -179,7 +185,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("exp_avg_sqs"), pybind11::arg("max_exp_avg_sqs"), pybind11::arg("lr"), pybind11::arg("beta1"),
         pybind11::arg("beta2"), pybind11::arg("eps"), pybind11::arg("weight_decay"), pybind11::arg("step"),
         pybind11::arg("amsgrad"), pybind11::arg("decoupled"), pybind11::arg("maximize"),
-        pybind11::arg("grad_scale"), pybind11::arg("shadows") = std::vector<at::Tensor>{});
+        pybind11::arg("grad_scale"), pybind11::arg("shadows") = std::vector<at::Tensor>{},
+        pybind11::arg("steps") = std::vector<at::Tensor>{});
   m.def("fused_adadelta", &ops::fused_adadelta);
   m.def("sumsq", &ops::sumsq);
   m.def("scale_by", &ops::scale_by);

@@ -11,6 +11,7 @@
 #include <atomic>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -61,6 +62,13 @@ class Communicator {
   virtual WorkPtr barrier() = 0;
   // Tear down without waiting for peers (failure path).
   virtual void abort() {}
+  // Collective over this communicator: ranks with the same color >= 0 form a
+  // new communicator (rank order by key); color < 0 returns nullptr. The
+  // default (host backend) is unsupported: new_group builds a fresh host
+  // communicator through the store instead.
+  virtual std::shared_ptr<Communicator> split(int color, int key, const std::string& prefix) {
+    throw std::runtime_error(backend() + " communicator does not support split()");
+  }
   // raw handle of the device stream collectives run on (0 = none / host)
   virtual int64_t stream_handle() const { return 0; }
   // Non-empty once the communicator hit an unrecoverable error.

@@ -97,23 +97,27 @@ class RcclWork : public Work {
 class RcclCommunicator : public Communicator {
  public:
   RcclCommunicator(std::shared_ptr<TCPStore> store, const std::string& prefix, int rank, int size, int device,
-                   int64_t timeout_ms)
+                   int64_t timeout_ms, ncclComm_t existing = nullptr)
       : Communicator(std::move(store), prefix, rank, size),
         device_(device),
         timeout_ms_(timeout_ms),
         stream_(c10::hip::getStreamFromPool(comm_stream_high_priority(), static_cast<c10::DeviceIndex>(device))) {
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
-    ncclUniqueId id;
-    const std::string key = prefix_ + "/rccl/uid";
-    if (rank_ == 0) {
-      NCCL_OK(ncclGetUniqueId(&id));
-      store_->set(key, std::string(reinterpret_cast<const char*>(&id), sizeof(id)));
+    if (existing) {
+      comm_ = existing;  // produced by ncclCommSplit of a parent communicator
     } else {
-      const std::string v = store_->get(key);
-      DCP_CHECK(v.size() == sizeof(id), "RCCL unique id has wrong size");
-      std::memcpy(&id, v.data(), sizeof(id));
+      ncclUniqueId id;
+      const std::string key = prefix_ + "/rccl/uid";
+      if (rank_ == 0) {
+        NCCL_OK(ncclGetUniqueId(&id));
+        store_->set(key, std::string(reinterpret_cast<const char*>(&id), sizeof(id)));
+      } else {
+        const std::string v = store_->get(key);
+        DCP_CHECK(v.size() == sizeof(id), "RCCL unique id has wrong size");
+        std::memcpy(&id, v.data(), sizeof(id));
+      }
+      NCCL_OK(ncclCommInitRank(&comm_, size_, id, rank_));
     }
-    NCCL_OK(ncclCommInitRank(&comm_, size_, id, rank_));
     const char* t = std::getenv("DCP_COMM_TIMING");
     timing_ = t && std::string(t) == "1";
     const char* h = std::getenv("DCP_SINGLE_RANK_HOP");
@@ -145,7 +149,7 @@ class RcclCommunicator : public Communicator {
     check_tensor(t);
     account("all_reduce", t, static_cast<int>(op));
     return launch({t}, [&](hipStream_t s) {
-      if (size_ == 1) return;  // identity for every op on one rank (in place)
+      if (size_ == 1 && !single_rank_hop_) return;  // identity for every op on one rank (in place)
       NCCL_OK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
                             to_nccl(op, t.scalar_type()), comm_, s));
     });
@@ -155,7 +159,7 @@ class RcclCommunicator : public Communicator {
     check_tensor(t);
     account("broadcast", t, root);
     return launch({t}, [&](hipStream_t s) {
-      if (size_ == 1) return;
+      if (size_ == 1 && !single_rank_hop_) return;
       NCCL_OK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, s));
     });
   }
@@ -226,6 +230,24 @@ class RcclCommunicator : public Communicator {
 
   void abort() override {
     if (!aborted_.exchange(true) && comm_) ncclCommAbort(comm_);
+  }
+
+  // Sub-communicator via ncclCommSplit (collective over this communicator:
+  // every rank calls it; color < 0 = not a member -> nullptr). Same xGMI
+  // topology discovery and channels as the parent, no new unique-id
+  // rendezvous through the store.
+  std::shared_ptr<Communicator> split(int color, int key, const std::string& prefix) override {
+    raise_if_error();
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+    ncclComm_t sub = nullptr;
+    NCCL_OK(ncclCommSplit(comm_, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &sub, nullptr));
+    if (color < 0 || sub == nullptr) return nullptr;
+    int n = 0, r = 0;
+    NCCL_OK(ncclCommCount(sub, &n));
+    NCCL_OK(ncclCommUserRank(sub, &r));
+    auto c = std::make_shared<RcclCommunicator>(store_, prefix, r, n, device_, timeout_ms_, sub);
+    c->set_debug_fingerprint(fingerprint_);
+    return c;
   }
 
   std::string error() override {

@@ -37,7 +37,7 @@ void mt_sgd(TableView t, int64_t nchunks, DType p, float lr, float momentum, flo
 // then (shadow) a bf16 copy of the updated parameter.
 void mt_adam(TableView t, int64_t nchunks, DType p, float lr, float beta1, float beta2, float eps, float wd,
              float bias_c1, float bias_c2_sqrt, bool amsgrad, bool decoupled_wd, bool maximize, float grad_scale,
-             bool shadow, hipStream_t s);
+             bool shadow, int step_list, hipStream_t s);
 
 // Fused Adadelta. lists: 0 param, 1 grad, 2 square_avg, 3 acc_delta.
 void mt_adadelta(TableView t, int64_t nchunks, DType p, float lr, float rho, float eps, float wd, bool maximize,

@@ -241,6 +241,10 @@ __global__ void __launch_bounds__(kThreads) mt_sgd_kernel(Tab tab, int64_t nchun
 struct AdamArgs {
   float lr, beta1, beta2, eps, wd, bc1, bc2_sqrt, grad_scale;
   bool amsgrad, decoupled, maximize, shadow;
+  // >= 0: table list holding one device fp32 `step` scalar per tensor
+  // (capturable mode: bias corrections derived on device, so a replayed HIP
+  // graph sees the advancing step); < 0: bc1 / bc2_sqrt above are used.
+  int step_list;
 };
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float& vmax, const AdamArgs& a) {
@@ -263,9 +267,16 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 }
 
 template <int PD>
-__global__ void __launch_bounds__(kThreads) mt_adam_kernel(Tab tab, int64_t nchunks, AdamArgs a) {
+__global__ void __launch_bounds__(kThreads) mt_adam_kernel(Tab tab, int64_t nchunks, AdamArgs a0) {
   using A = Acc<PD>;
-  for_each_chunk(tab, nchunks, [&](int t, int64_t base, int64_t len) {
+  for_each_chunk(tab, nchunks, [&](int t, int64_t base, int64_t len_) {
+    AdamArgs a = a0;
+    const int64_t len = len_;
+    if (a.step_list >= 0) {
+      const float step = *static_cast<const float*>(tab.ptr(a.step_list, t));
+      a.bc1 = 1.f - powf(a.beta1, step);
+      a.bc2_sqrt = sqrtf(1.f - powf(a.beta2, step));
+    }
     void* P = tab.ptr(0, t);
     const void* G = tab.ptr(1, t);
     void* M = tab.ptr(2, t);
@@ -486,9 +497,10 @@ void mt_sgd(TableView t, int64_t nchunks, DType p, float lr, float momentum, flo
 
 void mt_adam(TableView t, int64_t nchunks, DType p, float lr, float beta1, float beta2, float eps, float wd,
              float bias_c1, float bias_c2_sqrt, bool amsgrad, bool decoupled_wd, bool maximize, float grad_scale,
-             bool shadow, hipStream_t s) {
+             bool shadow, int step_list, hipStream_t s) {
   if (nchunks <= 0) return;
-  AdamArgs a{lr, beta1, beta2, eps, wd, bias_c1, bias_c2_sqrt, grad_scale, amsgrad, decoupled_wd, maximize, shadow};
+  AdamArgs a{lr, beta1, beta2, eps, wd, bias_c1, bias_c2_sqrt, grad_scale, amsgrad, decoupled_wd, maximize, shadow,
+             step_list};
   DCP_DISPATCH_DTYPE(p, PD,
       hipLaunchKernelGGL((mt_adam_kernel<PD>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks, a));
 }

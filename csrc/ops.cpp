@@ -262,7 +262,7 @@ void fused_sgd(const TensorList& params, const TensorList& grads, const TensorLi
 void fused_adam(const TensorList& params, const TensorList& grads, const TensorList& exp_avgs,
                 const TensorList& exp_avg_sqs, const TensorList& max_exp_avg_sqs, double lr, double beta1,
                 double beta2, double eps, double weight_decay, double step, bool amsgrad, bool decoupled,
-                bool maximize, double grad_scale, const TensorList& shadows) {
+                bool maximize, double grad_scale, const TensorList& shadows, const TensorList& steps) {
   if (params.empty()) return;
   std::vector<const TensorList*> lists{&params, &grads, &exp_avgs, &exp_avg_sqs};
   if (amsgrad) lists.push_back(&max_exp_avg_sqs);
@@ -276,6 +276,18 @@ void fused_adam(const TensorList& params, const TensorList& grads, const TensorL
                 "fused_adam: shadows must be contiguous bf16 copies of contiguous fp32 params");
   }
   check_lists(lists, "fused_adam");
+  // capturable mode: one device fp32 step scalar per tensor (already
+  // incremented by the caller), appended as an extra table list (the table
+  // sizes chunks by list 0 only, so 1-element rows are fine there)
+  int step_list = -1;
+  if (!steps.empty()) {
+    DCP_CHECK(steps.size() == params.size() && on_gpu(params), "fused_adam: steps must be one device tensor per param");
+    for (auto& t : steps)
+      DCP_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.numel() == 1 && t.device() == params[0].device(),
+                "fused_adam: each step must be a 1-element fp32 tensor on the parameters' device");
+    step_list = static_cast<int>(lists.size());
+    lists.push_back(&steps);
+  }
   const double bc1 = 1.0 - std::pow(beta1, step);
   const double bc2_sqrt = std::sqrt(1.0 - std::pow(beta2, step));
   if (on_gpu(params)) {
@@ -285,7 +297,7 @@ void fused_adam(const TensorList& params, const TensorList& grads, const TensorL
                   static_cast<float>(lr), static_cast<float>(beta1), static_cast<float>(beta2),
                   static_cast<float>(eps), static_cast<float>(weight_decay), static_cast<float>(bc1),
                   static_cast<float>(bc2_sqrt), amsgrad, decoupled, maximize, static_cast<float>(grad_scale),
-                  shadow, cur_stream(params[0]));
+                  shadow, step_list, cur_stream(params[0]));
     return;
   }
   for (size_t t = 0; t < params.size(); ++t) {

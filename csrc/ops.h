@@ -22,7 +22,7 @@ void fused_sgd(const TensorList& params, const TensorList& grads, const TensorLi
 void fused_adam(const TensorList& params, const TensorList& grads, const TensorList& exp_avgs,
                 const TensorList& exp_avg_sqs, const TensorList& max_exp_avg_sqs, double lr, double beta1,
                 double beta2, double eps, double weight_decay, double step, bool amsgrad, bool decoupled,
-                bool maximize, double grad_scale, const TensorList& shadows = {});
+                bool maximize, double grad_scale, const TensorList& shadows = {}, const TensorList& steps = {});
 
 void fused_adadelta(const TensorList& params, const TensorList& grads, const TensorList& square_avgs,
                     const TensorList& acc_deltas, double lr, double rho, double eps, double weight_decay,

@@ -6,8 +6,11 @@
 
 #include <algorithm>
 #include <map>
+#include <optional>
+#include <thread>
 #include <unordered_set>
 
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
 #include <cstdlib>
@@ -58,6 +61,22 @@ std::vector<std::vector<int64_t>> compute_bucket_assignment(const std::vector<in
   return result;
 }
 
+std::vector<std::vector<int64_t>> split_tail_bucket(std::vector<std::vector<int64_t>> assignment,
+                                                    const std::vector<int64_t>& sizes_bytes, int64_t tail_bytes) {
+  if (tail_bytes <= 0 || assignment.empty()) return assignment;
+  std::vector<int64_t>& last = assignment.back();
+  int64_t total = 0;
+  for (int64_t i : last) total += sizes_bytes.at(i);
+  if (total <= tail_bytes || last.size() < 2) return assignment;
+  size_t cut = last.size() - 1;  // the tail takes at least the last-ready parameter
+  int64_t tail = sizes_bytes.at(last[cut]);
+  while (cut > 1 && tail + sizes_bytes.at(last[cut - 1]) <= tail_bytes) tail += sizes_bytes.at(last[--cut]);
+  std::vector<int64_t> t(last.begin() + static_cast<std::ptrdiff_t>(cut), last.end());
+  last.resize(cut);
+  assignment.push_back(std::move(t));
+  return assignment;
+}
+
 namespace {
 
 int64_t bucket_key(const at::Tensor& t) {
@@ -81,6 +100,7 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
   }
   ready_.assign(params_.size(), 0);
   unused_.assign(params_.size(), 0);
+  used_since_sync_.assign(params_.size(), 0);
   build_buckets(buckets);
   const char* t = std::getenv("DCP_COMM_TIMING");
   timing_ = t && std::strcmp(t, "1") == 0 && !params_.empty() && params_[0].is_cuda();
@@ -100,6 +120,7 @@ double Reducer::exposed_comm_ms() {
 }
 
 Reducer::~Reducer() {
+  if (used_ev_) (void)hipEventDestroy(used_ev_);
   if (ev_bwd_end_) (void)hipEventDestroy(ev_bwd_end_);
   if (ev_final_) (void)hipEventDestroy(ev_final_);
   for (size_t i = 0; i < grad_accs_.size() && i < hook_handles_.size(); ++i)
@@ -211,7 +232,13 @@ void Reducer::find_unused(const std::vector<at::Tensor>& outputs) {
 
 void Reducer::autograd_hook(int64_t index) {
   std::lock_guard<std::mutex> g(mu_);
-  if (!expect_hooks_) return;
+  if (!expect_hooks_) {
+    // no_sync micro-step: remember the use (torch marks its local_used_map_
+    // before the expect-hooks check), so a parameter used only during
+    // accumulation still counts as used at the next synced step.
+    if (opts_.find_unused_parameters && params_[index].grad().defined()) used_since_sync_[index] = 1;
+    return;
+  }
   if (!finalize_queued_) {
     finalize_queued_ = true;
     backward_t0_ms_ = static_cast<double>(now_ms());
@@ -222,6 +249,8 @@ void Reducer::autograd_hook(int64_t index) {
   }
   if (opts_.find_unused_parameters && !marked_unused_) {
     marked_unused_ = true;
+    // Issued before any bucket on every rank: the collective order matches.
+    launch_used_map_reduce();
     for (int64_t u : unused_list_) mark_ready(u, /*unused=*/true);
   }
   mark_ready(index, /*unused=*/false);
@@ -238,7 +267,10 @@ void Reducer::mark_ready(int64_t i, bool unused) {
   Bucket& b = buckets_[bi];
   const at::Tensor& view = b.views[s];
   const at::Tensor& grad = params_[i].grad();
-  if (unused || !grad.defined()) {
+  // An unused parameter may still hold gradients accumulated under no_sync:
+  // they are packed like any other (torch: mark_variable_ready_dense).
+  (void)unused;
+  if (!grad.defined()) {
     b.pending_grads[s] = at::Tensor();
     view.zero_();
   } else if (grad.data_ptr() == view.data_ptr() && same_layout(grad, view)) {
@@ -290,7 +322,7 @@ void Reducer::launch(Bucket& b) {
   b.stats.ready_ms = static_cast<double>(now_ms()) - backward_t0_ms_;
   trace::Range r("dcp.reducer.bucket_allreduce");
   if (comm_hook_) {
-    b.work = comm_hook_(b.wire);
+    b.work = comm_hook_(b.wire, static_cast<int64_t>(&b - buckets_.data()));
   } else {
     b.work = comm_->all_reduce(b.wire, opts_.average ? ReduceOp::AVG : ReduceOp::SUM);
   }
@@ -309,9 +341,11 @@ void Reducer::finalize() {
       for (size_t s = 0; s < b.params.size(); ++s)
         if (!ready_[b.params[s]]) missing.push_back(b.params[s]);
   if (!missing.empty()) {
-    // reset so the next iteration can proceed after the user fixes things
-    finalize_queued_ = false;
-    expect_hooks_ = false;
+    // Reset every per-iteration field so the next forward/backward starts
+    // clean. Collectives already issued for launched buckets stay issued; if
+    // peers did not issue the same ones the communicator's watchdog deadline
+    // turns the mismatch into an error instead of a hang.
+    reset_iteration_state();
     std::string ids;
     for (size_t k = 0; k < missing.size() && k < 16; ++k) ids += (k ? ", " : "") + std::to_string(missing[k]);
     throw Error(str_cat("Reducer: expected to have finished reduction but parameters [", ids,
@@ -320,15 +354,7 @@ void Reducer::finalize() {
   }
 
   std::vector<char> global_used;
-  if (opts_.find_unused_parameters) {
-    at::Tensor used = at::empty({static_cast<int64_t>(params_.size())}, at::kInt);
-    for (size_t i = 0; i < params_.size(); ++i) used[i] = unused_[i] ? 0 : 1;
-    at::Tensor dev_used = used.to(params_[0].device());
-    comm_->all_reduce(dev_used, ReduceOp::MAX)->wait();
-    at::Tensor h = dev_used.cpu();
-    global_used.resize(params_.size());
-    for (size_t i = 0; i < params_.size(); ++i) global_used[i] = h[i].item<int>() != 0;
-  }
+  if (opts_.find_unused_parameters) global_used = collect_global_used();
 
   hipStream_t cur = nullptr;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -350,6 +376,9 @@ void Reducer::finalize() {
         if (used) grad = opts_.gradient_as_bucket_view ? b.views[s] : b.views[s].clone();
         continue;
       }
+      // Globally unused: keep the existing (e.g. no_sync-accumulated) gradient
+      // untouched (torch: copy_bucket_to_grad with global_unused).
+      if (!used && grad.data_ptr() != b.views[s].data_ptr()) continue;
       if (opts_.gradient_as_bucket_view) {
         if (grad.data_ptr() != b.views[s].data_ptr()) grad = b.views[s];
       } else if (same_layout(grad, b.views[s])) {
@@ -373,11 +402,88 @@ void Reducer::finalize() {
   finalize_queued_ = false;
   marked_unused_ = false;
   expect_hooks_ = false;
+  used_work_.reset();
   ++iterations_;
   if (record_order_) {
     record_order_ = false;
     if (opts_.rebuild_buckets) rebuild_from_ready_order();
   }
+}
+
+void Reducer::reset_iteration_state() {
+  for (auto& b : buckets_) {
+    b.work.reset();
+    b.launched = false;
+    b.pending = static_cast<int>(b.params.size());
+    for (auto& g : b.pending_grads) g = at::Tensor();
+  }
+  std::fill(ready_.begin(), ready_.end(), 0);
+  next_bucket_ = 0;
+  finalize_queued_ = false;
+  marked_unused_ = false;
+  expect_hooks_ = false;
+  used_work_.reset();
+  if (record_order_) ready_order_.clear();
+}
+
+void Reducer::launch_used_map_reduce() {
+  const int64_t n = static_cast<int64_t>(params_.size());
+  const bool cuda = params_[0].is_cuda();
+  if (cuda) {
+    hipStream_t cur = c10::hip::getCurrentHIPStream(params_[0].device().index()).stream();
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(cur, &cap);
+    DCP_CHECK(cap == hipStreamCaptureStatusNone,
+              "find_unused_parameters=True cannot be used inside HIP-graph capture (the used-parameter map "
+              "is read on the host at the end of every backward)");
+  }
+  if (!used_host_.defined()) {
+    auto host = at::TensorOptions().dtype(at::kInt).pinned_memory(cuda);
+    used_host_ = at::empty({n}, host);
+    used_back_ = at::empty({n}, host);
+    used_dev_ = cuda ? at::empty({n}, params_[0].options().dtype(at::kInt).requires_grad(false)) : used_host_;
+    if (cuda) DCP_CHECK(hipEventCreateWithFlags(&used_ev_, hipEventDisableTiming) == hipSuccess, "event create");
+  }
+  // The previous iteration's finalize waited for used_ev_, which follows the
+  // H2D copy of used_host_: rewriting it now cannot race that copy.
+  int32_t* h = used_host_.data_ptr<int32_t>();
+  for (int64_t i = 0; i < n; ++i) h[i] = (!unused_[i] || used_since_sync_[i]) ? 1 : 0;
+  std::fill(used_since_sync_.begin(), used_since_sync_.end(), 0);
+  if (cuda) used_dev_.copy_(used_host_, /*non_blocking=*/true);
+  used_work_ = comm_->all_reduce(used_dev_, ReduceOp::MAX);
+  if (!cuda) return;
+  // Copy the result back on the comm stream (not the compute stream: the
+  // backward keeps running) and remember the point to wait for.
+  std::optional<c10::hip::HIPStreamGuard> sg;
+  if (const int64_t hs = comm_->stream_handle())
+    sg.emplace(c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(hs), params_[0].device().index()));
+  used_work_->wait();
+  used_back_.copy_(used_dev_, /*non_blocking=*/true);
+  hipStream_t s = c10::hip::getCurrentHIPStream(params_[0].device().index()).stream();
+  DCP_CHECK(hipEventRecord(used_ev_, s) == hipSuccess, "event record");
+}
+
+std::vector<char> Reducer::collect_global_used() {
+  const size_t n = params_.size();
+  std::vector<char> out(n, 1);
+  if (!used_work_) launch_used_map_reduce();  // no hook fired (nothing used locally)
+  if (params_[0].is_cuda()) {
+    // Poll (not hipEventSynchronize) so a communicator abort releases us.
+    while (true) {
+      if (!comm_->error().empty()) throw Error("Reducer: communicator failed: " + comm_->error());
+      hipError_t e = hipEventQuery(used_ev_);
+      if (e == hipSuccess) break;
+      DCP_CHECK(e == hipErrorNotReady, "hipEventQuery failed: ", hipGetErrorString(e));
+      std::this_thread::sleep_for(std::chrono::microseconds(10));
+    }
+    const int32_t* h = used_back_.data_ptr<int32_t>();
+    for (size_t i = 0; i < n; ++i) out[i] = h[i] != 0;
+  } else {
+    used_work_->wait();
+    const int32_t* h = used_dev_.data_ptr<int32_t>();
+    for (size_t i = 0; i < n; ++i) out[i] = h[i] != 0;
+  }
+  return out;
 }
 
 void Reducer::rebuild_from_ready_order() {
@@ -394,15 +500,17 @@ void Reducer::rebuild_from_ready_order() {
   auto w = comm_->broadcast(dev, 0);
   w->wait();
   w->synchronize();
-  at::Tensor back = dev.cpu();
-  for (size_t k = 0; k < order.size(); ++k) order[k] = back[k].item<int64_t>();
+  at::Tensor back = dev.cpu().contiguous();
+  std::memcpy(order.data(), back.data_ptr<int64_t>(), order.size() * sizeof(int64_t));
 
   std::vector<int64_t> sizes, keys;
   for (auto& p : params_) {
     sizes.push_back(p.numel() * p.element_size());
     keys.push_back(bucket_key(p));
   }
-  auto assignment = compute_bucket_assignment(sizes, keys, {opts_.first_bucket_bytes, opts_.bucket_bytes_cap}, order);
+  auto assignment = split_tail_bucket(
+      compute_bucket_assignment(sizes, keys, {opts_.first_bucket_bytes, opts_.bucket_bytes_cap}, order), sizes,
+      opts_.tail_bucket_bytes);
   if (assignment == bucket_indices()) return;
   // Keep current gradients (bucket views in gradient_as_bucket_view mode).
   std::vector<at::Tensor> old_grads(params_.size());

@@ -39,12 +39,22 @@ std::vector<std::vector<int64_t>> compute_bucket_assignment(const std::vector<in
                                                             const std::vector<int64_t>& limits,
                                                             const std::vector<int64_t>& order);
 
+// xGMI tail bucket: split the LAST bucket of a launch-ordered plan so that
+// its final part (the parameters whose gradients are ready last, i.e. the
+// suffix of the bucket's ready-ordered list) holds at most `tail_bytes`
+// (always >= 1 parameter). The last bucket's all-reduce cannot overlap any
+// backward compute, so its size is the exposed communication (NOTES §18).
+// No-op when tail_bytes <= 0 or the last bucket already fits.
+std::vector<std::vector<int64_t>> split_tail_bucket(std::vector<std::vector<int64_t>> assignment,
+                                                    const std::vector<int64_t>& sizes_bytes, int64_t tail_bytes);
+
 struct ReducerOptions {
   bool gradient_as_bucket_view = false;
   bool find_unused_parameters = false;
   bool rebuild_buckets = true;
   int64_t first_bucket_bytes = 1 << 20;
   int64_t bucket_bytes_cap = 25 << 20;
+  int64_t tail_bucket_bytes = 0;  // see split_tail_bucket; 0 = torch behaviour
   // at::ScalarType of the wire buffer; Undefined = same as the gradient.
   at::ScalarType comm_dtype = at::ScalarType::Undefined;
   // false -> SUM instead of AVG (for custom hooks that pre-scale).
@@ -60,7 +70,8 @@ struct BucketStats {
 
 class Reducer : public std::enable_shared_from_this<Reducer> {
  public:
-  using CommHook = std::function<WorkPtr(at::Tensor& bucket)>;
+  // (bucket buffer, position of the bucket in this iteration's launch order)
+  using CommHook = std::function<WorkPtr(at::Tensor& bucket, int64_t index)>;
 
   Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t>> buckets,
           std::shared_ptr<Communicator> comm, ReducerOptions opts);
@@ -116,6 +127,9 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void finalize();
   void rebuild_from_ready_order();
   void find_unused(const std::vector<at::Tensor>& outputs);
+  void launch_used_map_reduce();
+  std::vector<char> collect_global_used();
+  void reset_iteration_state();
 
   std::vector<at::Tensor> params_;
   std::shared_ptr<Communicator> comm_;
@@ -135,6 +149,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   size_t next_bucket_ = 0;
   std::vector<char> ready_;
   std::vector<char> unused_;
+  std::vector<char> used_since_sync_;  // find_unused: got a gradient in a no_sync micro-step
   std::vector<int64_t> unused_list_;
   std::vector<int64_t> ready_order_;
   bool record_order_ = true;
@@ -144,7 +159,13 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool timing_ = false;
   hipEvent_t ev_bwd_end_ = nullptr, ev_final_ = nullptr;
   bool ev_recorded_ = false;
-  at::Tensor local_used_;  // find_unused: per-param used flags (int32, on device)
+  // find_unused_parameters: per-parameter used flags. Host staging (pinned on
+  // GPU) -> device -> async MAX all-reduce issued at the first hook ->
+  // async copy back on the comm stream; finalize waits only on that small
+  // copy's event (launched early in backward), never on the backward itself.
+  at::Tensor used_host_, used_dev_, used_back_;
+  WorkPtr used_work_;
+  hipEvent_t used_ev_ = nullptr;
 };
 
 }  // namespace dcp

@@ -9,8 +9,8 @@ from __future__ import annotations
 import argparse
 import dataclasses
 import json
-from dataclasses import dataclass, field
-from typing import List, Optional
+from dataclasses import dataclass
+from typing import Optional
 
 
 @dataclass
@@ -37,15 +37,14 @@ class TrainConfig:
     comm_dtype: str = "fp32"              # fp32 | bf16 wire compression
     grad_accum: int = 1
     clip_grad_norm: float = 0.0
-    hip_graph: bool = False
+    hip_graph: bool = False               # capture the whole step in one HIP graph (GPU)
     seed: int = 0
     log_every: int = 10
     metrics_file: Optional[str] = None    # JSON-lines metrics (rank 0)
     checkpoint: Optional[str] = None      # full checkpoint path (save every epoch)
     resume: Optional[str] = None
     save_model: Optional[str] = "model.pt"
-    profile: bool = False
-    extra: List[str] = field(default_factory=list)
+    profile: bool = False                 # torch.profiler chrome trace of the first epoch
 
     def to_json(self) -> str:
         return json.dumps(dataclasses.asdict(self), sort_keys=True)

@@ -304,16 +304,27 @@ def get_backend(group=None) -> str:
 
 
 def new_group(ranks: Optional[List[int]] = None, timeout=None, backend=None, pg_options=None):
-    """Collective over the default group: every rank must call it."""
+    """Collective over the default group: every rank must call it (torch
+    semantics). On RCCL the sub-communicator comes from ``ncclCommSplit`` of
+    the world communicator (every rank joins the split; non-members pass
+    NOCOLOR) — no second unique-id rendezvous and the parent's xGMI topology
+    is reused. The host backend builds its group communicator lazily through
+    the store."""
     world = get_default_group()
     ranks = sorted(range(world.size()) if ranks is None else ranks)
     _state["group_count"] += 1
     prefix = f"pg{_state['group_count'] - 1}"
-    if world.rank() not in ranks:
-        return GroupMember.NON_GROUP_MEMBER
+    member = world.rank() in ranks
     be = _BACKEND_ALIASES.get((backend or world.backend).lower(), world.backend)
+    sub = None
+    if be in ("rccl", "auto") and world._rccl is not None:
+        sub = world._rccl.split(0 if member else -1, ranks.index(world.rank()) if member else 0, prefix)
+    if not member:
+        return GroupMember.NON_GROUP_MEMBER
     tms = int(timeout.total_seconds() * 1000) if timeout else world.timeout_ms
     pg = ProcessGroup(world.store, prefix, ranks.index(world.rank()), len(ranks), be, tms, ranks, world.device_id)
+    if sub is not None:
+        pg._rccl = sub
     _state["groups"].append(pg)
     return pg
 
@@ -341,14 +352,37 @@ def all_gather_into_tensor(output_tensor, input_tensor, group=None, async_op=Fal
     return _ret(pg.comm_for(input_tensor).all_gather(output_tensor, input_tensor.contiguous()), async_op)
 
 
+class _ScatterBackWork:
+    """Work of a list-form all_gather: ``wait()`` orders the caller after the
+    gather, then copies the rows out (on the device stream: no host block)."""
+
+    def __init__(self, work, flat, outs):
+        self._w, self._flat, self._outs, self._done = work, flat, outs, False
+
+    def is_completed(self):
+        return self._w.is_completed()
+
+    def wait(self):
+        self._w.wait()
+        if not self._done:
+            self._done = True
+            for i, t in enumerate(self._outs):
+                t.copy_(self._flat[i])
+        return True
+
+    def synchronize(self):
+        self.wait()
+        self._w.synchronize()
+
+
 def all_gather(tensor_list: List[torch.Tensor], tensor: torch.Tensor, group=None, async_op=False):
     pg = _group(group)
     flat = torch.empty((pg.size(),) + tuple(tensor.shape), dtype=tensor.dtype, device=tensor.device)
-    w = pg.comm_for(tensor).all_gather(flat, tensor.contiguous())
+    w = _ScatterBackWork(pg.comm_for(tensor).all_gather(flat, tensor.contiguous()), flat, tensor_list)
+    if async_op:
+        return w
     w.wait()
-    for i, t in enumerate(tensor_list):
-        t.copy_(flat[i])
-    return w if async_op else None
+    return None
 
 
 def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op=False):

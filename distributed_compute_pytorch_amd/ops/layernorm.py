@@ -15,7 +15,7 @@ from torch import nn
 from torch.nn import functional as F
 
 from .._ext import C as _C
-from .linear import _acc_target
+from .linear import _acc_target, accumulating
 
 # DCP_LN_ACCUM=0: leave dγ / dβ to autograd's AccumulateGrad under no_sync (A/B switch)
 _LN_ACCUM = os.environ.get("DCP_LN_ACCUM", "1") != "0"
@@ -27,6 +27,7 @@ class _LNFn(torch.autograd.Function):
         y, mean, rstd = _C.layer_norm_fwd(x, weight, bias, eps, out_dtype)
         ctx.save_for_backward(x, weight, bias, mean, rstd)
         ctx.params = (weight, bias)
+        ctx.accum = accumulating()
         return y
 
     @staticmethod
@@ -38,7 +39,7 @@ class _LNFn(torch.autograd.Function):
             # .grad tensors in the finalize kernel (no AccumulateGrad adds; see
             # linear.accumulate_grads_in_place)
             D = torch.Size((x.shape[-1],))
-            tw, tb = _acc_target(ctx.params[0], D), _acc_target(ctx.params[1], D)
+            tw, tb = _acc_target(ctx, ctx.params[0], D), _acc_target(ctx, ctx.params[1], D)
             if tw is not None and tb is not None:
                 acc = [tw, tb]
         dx, dw, db = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd, accumulate_into=acc)

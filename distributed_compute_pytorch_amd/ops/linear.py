@@ -48,9 +48,16 @@ class accumulate_grads_in_place:
         return False
 
 
-def _acc_target(p, shape):
+def accumulating() -> bool:
+    """Sampled by each op's FORWARD into ``ctx.accum`` (like torch's no_sync,
+    whose decision is taken in DDP's forward): where ``backward()`` is called
+    does not matter."""
+    return _ACCUM_IN_PLACE[0] > 0
+
+
+def _acc_target(ctx, p, shape):
     g = p.grad if p is not None else None
-    if (_ACCUM_IN_PLACE[0] > 0 and g is not None and g.dtype == torch.float32 and g.is_contiguous()
+    if (getattr(ctx, "accum", False) and g is not None and g.dtype == torch.float32 and g.is_contiguous()
             and g.shape == shape and not g.requires_grad):
         return g
     return None
@@ -78,6 +85,7 @@ def _setup(ctx, x, weight, bias, w16, b16):
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
     ctx.wdtype = weight.dtype
+    ctx.accum = accumulating()
     ctx.bdtype = bias.dtype if bias is not None else None
     ctx.params = (weight, bias)
     return x, w, b
@@ -96,7 +104,7 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False):
         if g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
             # our split-M MFMA wgrad GEMM (gemm.hip): faster than hipBLASLt at
             # every BERT / GPT-2 shape (profiles/r1_linear_wgrad_bench.log)
-            tgt = _acc_target(weight, torch.Size((g2.shape[1], x2.shape[1])))
+            tgt = _acc_target(ctx, weight, torch.Size((g2.shape[1], x2.shape[1])))
             dw = _C.conv1x1_wgrad(g2, x2.contiguous(), accumulate_into=tgt)
             if tgt is not None:
                 dw = None  # added into weight.grad by the kernel
@@ -105,7 +113,7 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False):
         if dw is not None and dw.dtype != ctx.wdtype:
             dw = dw.to(ctx.wdtype)
     if not db_done and ctx.bdtype is not None and ctx.needs_input_grad[2]:
-        tgt = _acc_target(bias, torch.Size((g2.shape[1],)))
+        tgt = _acc_target(ctx, bias, torch.Size((g2.shape[1],)))
         db = _C.colsum(g2, accumulate_into=tgt)
         if tgt is not None:
             db = None
@@ -136,7 +144,7 @@ class _LinearGeluFn(torch.autograd.Function):
             gy = gy.to(torch.bfloat16)
         bias = ctx.params[1]
         want_db = ctx.bdtype is not None and ctx.needs_input_grad[2]
-        tgt = _acc_target(bias, torch.Size((h.shape[-1],))) if want_db else None
+        tgt = _acc_target(ctx, bias, torch.Size((h.shape[-1],))) if want_db else None
         gh, db = _C.gelu_bwd(gy, h, ctx.tanh, want_db, accumulate_into=tgt)
         if tgt is not None:
             db = None  # added into bias.grad by the kernel

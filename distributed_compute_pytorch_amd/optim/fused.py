@@ -97,14 +97,24 @@ class SGD(Optimizer):
         for group in self.param_groups:
             mom = group["momentum"]
             buckets = defaultdict(lambda: ([], [], []))
+            capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
             for p in group["params"]:
                 if not _grads_ok(p):
                     continue
                 st = self.state[p]
                 first = False
                 if mom != 0 and st.get("momentum_buffer") is None:
-                    st["momentum_buffer"] = torch.empty_like(p, memory_format=torch.preserve_format)
-                    first = True
+                    if capturing:
+                        # a captured "first step" flag would re-initialise the
+                        # buffer on every replay: start from zeros instead
+                        # (identical update when dampening == 0)
+                        if group["dampening"] != 0:
+                            raise RuntimeError("SGD with dampening cannot take its first step inside HIP-graph "
+                                               "capture: run one eager step (warmup) before capturing")
+                        st["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    else:
+                        st["momentum_buffer"] = torch.empty_like(p, memory_format=torch.preserve_format)
+                        first = True
                 key = (p.device, p.dtype, first)
                 P, G, B = buckets[key]
                 P.append(p)
@@ -119,17 +129,32 @@ class SGD(Optimizer):
 
 
 class Adam(Optimizer):
-    """torch.optim.Adam / AdamW semantics (``decoupled_weight_decay``), fused."""
+    """torch.optim.Adam / AdamW semantics (``decoupled_weight_decay``), fused.
+
+    ``capturable=True`` (torch's flag of the same name): every parameter's
+    ``step`` lives on the device, is advanced by one launch per step and the
+    kernel derives the bias corrections from it, so a step captured in a HIP
+    graph keeps advancing on replay. Without it the bias corrections are host
+    constants, and stepping inside a capture raises instead of silently
+    freezing them. A group can be switched at any time; the state migrates on
+    its next eager step.
+    """
 
     _decoupled_default = False
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 amsgrad: bool = False, *, maximize: bool = False, decoupled_weight_decay: bool = None):
+                 amsgrad: bool = False, *, maximize: bool = False, decoupled_weight_decay: bool = None,
+                 capturable: bool = False):
         if decoupled_weight_decay is None:
             decoupled_weight_decay = self._decoupled_default
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad, maximize=maximize,
-                        decoupled_weight_decay=decoupled_weight_decay)
+                        decoupled_weight_decay=decoupled_weight_decay, capturable=capturable)
         super().__init__(params, defaults)
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        for g in self.param_groups:
+            g.setdefault("capturable", False)
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):
@@ -137,25 +162,44 @@ class Adam(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         for group in self.param_groups:
             b1, b2 = group["betas"]
             ams = group["amsgrad"]
-            buckets = defaultdict(lambda: ([], [], [], [], [], []))
+            cap_mode = group.get("capturable", False)
+            if capturing and not cap_mode:
+                raise RuntimeError("Adam/AdamW stepped inside HIP-graph capture without capturable=True: the "
+                                   "bias corrections would be frozen at their capture-time step. Construct the "
+                                   "optimizer with capturable=True (or set group['capturable'] = True before the "
+                                   "eager warmup steps).")
+            buckets = defaultdict(lambda: ([], [], [], [], [], [], []))
             shadowed = []
             for p in group["params"]:
                 if not _grads_ok(p):
                     continue
                 st = self.state[p]
+                dev_step = cap_mode and p.is_cuda
                 if len(st) == 0:
-                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["step"] = (torch.zeros((), dtype=torch.float32, device=p.device) if dev_step
+                                  else torch.tensor(0.0, dtype=torch.float32))
                     st["exp_avg"] = _state_like(p)
                     st["exp_avg_sq"] = _state_like(p)
                     if ams:
                         st["max_exp_avg_sq"] = _state_like(p)
-                st["step"] += 1
+                elif dev_step and not st["step"].is_cuda:
+                    if capturing:
+                        raise RuntimeError("capturable Adam: run one eager step before capture (moves 'step' "
+                                           "to the device)")
+                    st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+                elif not dev_step and st["step"].is_cuda:
+                    st["step"] = st["step"].cpu()
                 sh = _BF16_SHADOWS.get(p) if p.is_cuda else None
-                key = (p.device, p.dtype, float(st["step"]), sh is not None)
-                P, G, M, V, VM, S = buckets[key]
+                if dev_step:
+                    key = (p.device, p.dtype, None, sh is not None)
+                else:
+                    st["step"] += 1
+                    key = (p.device, p.dtype, float(st["step"]), sh is not None)
+                P, G, M, V, VM, S, ST = buckets[key]
                 P.append(p)
                 G.append(_dense_like(p.grad, p))
                 M.append(st["exp_avg"])
@@ -165,9 +209,14 @@ class Adam(Optimizer):
                 if sh is not None:
                     S.append(sh[0])
                     shadowed.append(p)
-            for (dev, dt, step, _), (P, G, M, V, VM, S) in buckets.items():
-                _C.fused_adam(P, G, M, V, VM, group["lr"], b1, b2, group["eps"], group["weight_decay"], step, ams,
-                              group["decoupled_weight_decay"], group["maximize"], grad_scale, S)
+                if dev_step:
+                    ST.append(st["step"].view(1))
+            for (dev, dt, step, _), (P, G, M, V, VM, S, ST) in buckets.items():
+                if ST:
+                    torch._foreach_add_(ST, 1.0)  # one launch; the kernel reads the advanced steps
+                _C.fused_adam(P, G, M, V, VM, group["lr"], b1, b2, group["eps"], group["weight_decay"],
+                              step if step is not None else 0.0, ams, group["decoupled_weight_decay"],
+                              group["maximize"], grad_scale, S, ST)
         _PARAM_EPOCH[0] += 1
         for p in shadowed:  # rewritten by the kernel: valid for the new epoch
             e = _BF16_SHADOWS[p]
@@ -179,8 +228,9 @@ class AdamW(Adam):
     _decoupled_default = True
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
-                 amsgrad: bool = False, *, maximize: bool = False):
-        super().__init__(params, lr, betas, eps, weight_decay, amsgrad, maximize=maximize, decoupled_weight_decay=True)
+                 amsgrad: bool = False, *, maximize: bool = False, capturable: bool = False):
+        super().__init__(params, lr, betas, eps, weight_decay, amsgrad, maximize=maximize, decoupled_weight_decay=True,
+                         capturable=capturable)
 
 
 class Adadelta(Optimizer):

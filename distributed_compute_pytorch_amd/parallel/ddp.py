@@ -34,9 +34,19 @@ from .. import distributed as dist
 from ..utils.trace import trace_range
 from .comm_utils import CoalescedBroadcaster, broadcast_coalesced, verify_params_across_processes
 
-# Defaults (MiB). torch: 25 MiB cap, 1 MiB first bucket (reducer.hpp:30-31).
-DEFAULT_BUCKET_CAP_MB = 25.0
+# Bucket defaults (MiB) derived for 8x MI355X over xGMI (NOTES.md §18; torch:
+# 25 MiB cap, 1 MiB first bucket, no tail split — reducer.hpp:30-31):
+# * first bucket 1 MiB: the first all-reduce starts as early as possible;
+# * cap 50 MiB: every bucket but the last overlaps backward, so what matters
+#   is the per-collective latency (~tens of µs) and RCCL reaching its
+#   multi-channel bandwidth on 7 point-to-point links, which needs tens of MB
+#   — fewer, larger collectives (and pack launches) than 25 MiB;
+# * tail 2 MiB: the last bucket's all-reduce is the only one nothing can hide,
+#   so the ready-last parameters get a bucket of their own that a latency-bound
+#   all-reduce finishes in ~α instead of α + (25 MiB remainder) / bandwidth.
+DEFAULT_BUCKET_CAP_MB = 50.0
 DEFAULT_FIRST_BUCKET_MB = 1.0
+DEFAULT_TAIL_BUCKET_MB = 2.0
 
 
 _DTYPE_IDS = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3, torch.int64: 4,
@@ -44,17 +54,31 @@ _DTYPE_IDS = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat
 
 
 class GradBucket:
-    """Argument of a comm hook: the flat bucket buffer (torch-like accessors)."""
+    """Argument of a comm hook: the flat bucket buffer (torch-like accessors).
+    ``index()`` is the bucket's position in the current iteration's launch
+    order (0 = first reduced), as in torch's ``GradBucket.index()``."""
 
-    def __init__(self, buffer: torch.Tensor, index: int):
+    def __init__(self, buffer: torch.Tensor, index: int, params: Optional[List[torch.Tensor]] = None,
+                 num_buckets: int = 0):
         self._buffer = buffer
         self._index = index
+        self._params = params or []
+        self._num_buckets = num_buckets
 
     def buffer(self) -> torch.Tensor:
         return self._buffer
 
     def index(self) -> int:
         return self._index
+
+    def is_last(self) -> bool:
+        return self._index == self._num_buckets - 1
+
+    def parameters(self) -> List[torch.Tensor]:
+        return list(self._params)
+
+    def set_buffer(self, tensor: torch.Tensor) -> None:
+        self._buffer.copy_(tensor)
 
 
 class DistributedDataParallel(nn.Module):
@@ -63,7 +87,7 @@ class DistributedDataParallel(nn.Module):
                  find_unused_parameters: bool = False, check_reduction: bool = False,
                  gradient_as_bucket_view: bool = False, static_graph: bool = False,
                  first_bucket_mb: Optional[float] = None, comm_dtype: Optional[torch.dtype] = None,
-                 rebuild_buckets: bool = True, init_sync: bool = True):
+                 rebuild_buckets: bool = True, init_sync: bool = True, tail_bucket_mb: Optional[float] = None):
         super().__init__()
         self.module = module
         self.process_group = process_group if process_group is not None else dist.get_default_group()
@@ -78,6 +102,7 @@ class DistributedDataParallel(nn.Module):
         self.bucket_bytes_cap = int((bucket_cap_mb if bucket_cap_mb is not None else DEFAULT_BUCKET_CAP_MB) * 2**20)
         self.first_bucket_bytes = int(
             (first_bucket_mb if first_bucket_mb is not None else DEFAULT_FIRST_BUCKET_MB) * 2**20)
+        self.tail_bucket_bytes = int((tail_bucket_mb if tail_bucket_mb is not None else DEFAULT_TAIL_BUCKET_MB) * 2**20)
 
         # unique trainable parameters in registration order
         seen = set()
@@ -106,13 +131,17 @@ class DistributedDataParallel(nn.Module):
         sizes = [p.numel() * p.element_size() for p in params]
         keys = [self._key(p) for p in params]
         plan = _C.compute_bucket_assignment(sizes, keys, [self.first_bucket_bytes, self.bucket_bytes_cap], [])
-        plan = list(reversed(plan))
+        # expected-ready order: buckets AND their members reversed (gradients
+        # arrive roughly in reverse registration order)
+        plan = [list(reversed(b)) for b in reversed(plan)]
+        plan = _C.split_tail_bucket(plan, sizes, self.tail_bucket_bytes)
         opts = _C.ReducerOptions()
         opts.gradient_as_bucket_view = gradient_as_bucket_view
         opts.find_unused_parameters = find_unused_parameters
         opts.rebuild_buckets = rebuild_buckets
         opts.first_bucket_bytes = self.first_bucket_bytes
         opts.bucket_bytes_cap = self.bucket_bytes_cap
+        opts.tail_bucket_bytes = self.tail_bucket_bytes
         if comm_dtype is not None:
             opts.comm_dtype = comm_dtype
         self._comm = pg.comm_for(params[0])
@@ -165,12 +194,12 @@ class DistributedDataParallel(nn.Module):
         if self._comm_hook is not None:
             raise RuntimeError("register_comm_hook can only be called once")
         self._comm_hook = hook
-        counter = {"i": 0}
+        reducer, params = self.reducer, self._params
 
-        def _call(buf):
-            idx = counter["i"]
-            counter["i"] += 1
-            return hook(state, GradBucket(buf, idx))
+        def _call(buf, idx):
+            plan = reducer.bucket_indices()
+            ps = [params[i] for i in plan[idx]] if idx < len(plan) else []
+            return hook(state, GradBucket(buf, idx, ps, len(plan)))
 
         self.reducer.set_comm_hook(_call)
 
@@ -185,6 +214,7 @@ class DistributedDataParallel(nn.Module):
             "backend": self._comm.backend,
             "bucket_cap_bytes": self.bucket_bytes_cap,
             "first_bucket_bytes": self.first_bucket_bytes,
+            "tail_bucket_bytes": self.tail_bucket_bytes,
             "bucket_sizes": [s.bytes for s in st],
             "bucket_ready_ms": [s.ready_ms for s in st],
             "bucket_comm_ms": [s.comm_ms for s in st],

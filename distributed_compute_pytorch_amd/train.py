@@ -1,6 +1,7 @@
 """General trainer CLI: the reference's proc()/train()/test() loop (main.py:55-134)
 on this framework, for every model family, with structured metrics,
-checkpoint/resume and optional HIP-graph capture.
+checkpoint/resume, optional whole-step HIP-graph capture (``--hip-graph``)
+and a torch.profiler trace of the first epoch (``--profile``).
 
     python -m distributed_compute_pytorch_amd.train --model convnet --gpus 2 --epochs 1
     python -m distributed_compute_pytorch_amd.distributed.run --nproc-per-node 8 \
@@ -89,6 +90,7 @@ def run_rank(cfg: TrainConfig, rank: int, world: int, local_rank: int):
 
     if mnist:
         train_loader, train_sampler, test_loader = _mnist_loaders(cfg, rank, world)
+    step = None
     for epoch in range(start_epoch, cfg.epochs):
         model.train()
         t0 = time.time()
@@ -100,19 +102,18 @@ def run_rank(cfg: TrainConfig, rank: int, world: int, local_rank: int):
         else:
             batches = wl.data
             nsteps = cfg.steps_per_epoch or 100
+        prof = _profiler(cfg, rank, epoch == start_epoch)
         for b in range(nsteps):
-            opt.zero_grad(set_to_none=True)
-            for k in range(wl.accum):
+            flat = []
+            for _k in range(wl.accum):
                 bt = tuple(t.to(device, non_blocking=True) for t in next(batches))
-                ctx = model.no_sync() if k < wl.accum - 1 else _Null()
-                with ctx, torch.autocast(device.type, dtype=torch.bfloat16, enabled=wl.amp):
-                    loss = wl.loss_fn(model, bt) / wl.accum
-                loss.backward()
                 seen += bt[0].shape[0]
-            if cfg.clip_grad_norm > 0:
-                from .optim import clip_grad_norm_
-                clip_grad_norm_(model.parameters(), cfg.clip_grad_norm)
-            opt.step()
+                flat.extend(bt)
+            if step is None:
+                step = _make_step(cfg, wl, model, opt, device)
+            loss = step(*flat)
+            if prof is not None:
+                prof.step()
             if b % cfg.log_every == 0:
                 t = loss.detach().float().clone() * wl.accum
                 dist.all_reduce(t, dist.ReduceOp.AVG if t.is_cuda else dist.ReduceOp.SUM)
@@ -120,6 +121,11 @@ def run_rank(cfg: TrainConfig, rank: int, world: int, local_rank: int):
                     t /= world
                 log.log(event="train", epoch=epoch, step=b, steps=nsteps, loss=round(t.item(), 6),
                         lr=opt.param_groups[0]["lr"])
+        if prof is not None:
+            prof.stop()
+            path = (cfg.metrics_file or "dcp") + f".trace.rank{rank}.json"
+            prof.export_chrome_trace(path)
+            log.log(event="profile", trace=path)
         if device.type == "cuda":
             torch.cuda.synchronize()
         dt = time.time() - t0
@@ -147,6 +153,78 @@ class _Null:
 
     def __exit__(self, *a):
         return False
+
+
+def _make_step(cfg: TrainConfig, wl, model, opt, device):
+    """One optimizer step over ``wl.accum`` micro-batches (all but the last
+    under ``no_sync``; backward runs INSIDE the context, like the forward).
+    ``cfg.hip_graph`` on a GPU: the whole step (forward, backward, bucket
+    reduction, clipping, optimizer) is captured once and replayed."""
+
+    def run(*flat):
+        opt.zero_grad(set_to_none=True)
+        n = len(flat) // wl.accum
+        loss = None
+        for k in range(wl.accum):
+            bt = flat[k * n:(k + 1) * n]
+            ctx = model.no_sync() if k < wl.accum - 1 else _Null()
+            with ctx:
+                with torch.autocast(device.type, dtype=torch.bfloat16, enabled=wl.amp):
+                    loss = wl.loss_fn(model, bt) / wl.accum
+                loss.backward()
+        if cfg.clip_grad_norm > 0:
+            from .optim import clip_grad_norm_
+            clip_grad_norm_(model.parameters(), cfg.clip_grad_norm)
+        opt.step()
+        return loss
+
+    if not (cfg.hip_graph and device.type == "cuda"):
+        return run
+    from .utils.graphs import CapturedStep
+
+    for g in opt.param_groups:
+        if "capturable" in g:
+            g["capturable"] = True
+    # the DDP model was built on the current stream; capture on it too (the
+    # Reducer's AccumulateGrad nodes are bound to their creation stream)
+    # The first two steps run eagerly on real batches (bucket rebuild,
+    # optimizer state, kernel tables); the third is captured (capture executes
+    # nothing) and replayed: no extra training steps on a static batch.
+    st = {"eager": 0, "cap": None, "lr": None}
+
+    def call(*flat):
+        lrs = [g["lr"] for g in opt.param_groups]
+        if st["cap"] is None:
+            if st["eager"] < 2:
+                st["eager"] += 1
+                return run(*flat)
+            st["cap"] = CapturedStep(run, [t.clone() for t in flat], warmup=0,
+                                     stream=torch.cuda.current_stream())
+            st["lr"] = lrs
+        cap = st["cap"]
+        if lrs != st["lr"]:  # the captured kernels hold the LR as a constant
+            st["lr"] = lrs
+            cap.recapture(warmup=0)
+        if all(a.shape == b.shape for a, b in zip(flat, cap.static_inputs)):
+            return cap(*flat)
+        return run(*flat)  # ragged last batch of an epoch: eager
+
+    return call
+
+
+def _profiler(cfg: TrainConfig, rank: int, first_epoch: bool):
+    """``cfg.profile``: torch.profiler over steps 2-6 of the first epoch (CPU +
+    HIP activity, our roctx/record_function ranges included); the chrome trace
+    lands next to the metrics file."""
+    if not (cfg.profile and first_epoch):
+        return None
+    acts = [torch.profiler.ProfilerActivity.CPU]
+    if torch.cuda.is_available() and not cfg.no_cuda:
+        acts.append(torch.profiler.ProfilerActivity.CUDA)
+    p = torch.profiler.profile(activities=acts, schedule=torch.profiler.schedule(wait=1, warmup=1, active=5,
+                                                                                 repeat=1))
+    p.start()
+    return p
 
 
 def _spawn_entry(rank, cfg, world, port):

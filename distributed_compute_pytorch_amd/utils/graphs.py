@@ -68,11 +68,11 @@ class CapturedStep:
         self.static_out = None
         self._capture()
 
-    def _capture(self):
+    def _capture(self, warmup=None):
         s = self.stream
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for _ in range(self.warmup):
+            for _ in range(self.warmup if warmup is None else warmup):
                 self.step_fn(*self.static_inputs)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
@@ -91,9 +91,12 @@ class CapturedStep:
             raise
         self.graph = g
 
-    def recapture(self):
+    def recapture(self, warmup: int = 0):
+        """Capture again (e.g. after an LR change: the fused optimizers take
+        hyper-parameters as kernel arguments). No warmup by default: capture
+        itself executes nothing, so parameters are not advanced."""
         self.graph = None
-        self._capture()
+        self._capture(warmup)
 
     def __call__(self, *inputs: torch.Tensor):
         for dst, src in zip(self.static_inputs, inputs):

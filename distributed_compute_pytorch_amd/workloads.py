@@ -152,6 +152,10 @@ def make_step(wl: Workload, ddp, opt, device_type: str = "cuda", graph: bool = F
         return lambda: run(*next_flat())
     from .utils.graphs import CapturedStep, capture_stream
 
+    for g in opt.param_groups:  # Adam/AdamW: device-side step (bias corrections advance on replay)
+        if "capturable" in g:
+            g["capturable"] = True
+
     static = [t.clone() for t in next_flat()]
     captured = CapturedStep(run, static, stream=capture_stream())
     return lambda: captured(*next_flat())
