@@ -7,6 +7,12 @@
 #include "fused.h"
 #include "ops.h"
 #include "reducer/reducer.h"
+
+namespace dcp {
+namespace stem {
+void bind(pybind11::module& m);
+}
+}  // namespace dcp
 #include "trace/trace.h"
 #include "store/tcp_store.h"
 
@@ -193,4 +199,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("table_cache_size", &ops::table_cache_size);
 
   fused::bind(m);
+  stem::bind(m);
 }

@@ -36,6 +36,7 @@
 #include <string>
 
 #include "gemm_kernels.h"
+#include "stem_kernels.h"
 
 namespace dcp {
 namespace kern {
@@ -151,7 +152,12 @@ constexpr int nt_stages() { return BK == 64 ? 2 : 3; }
 // forward's own mask expression, sc/sf from gamma/beta/mean/invstd exactly as
 // batchnorm.hip's coef()), stats[0][c] += Σg, stats[1][c] += Σg·(x - mean):
 // the BN backward's separate reduce pass (re-reading dy and x) disappears.
-template <int BM, int BN, bool PRO, int EPI, bool GATHER, int BK>
+// AMODE 1 = the ResNet stem (stem.hip): A row m = output pixel (n, ho, wo) of
+// a stride-2 7x7 conv over the zero-padded 4-channel image geo.H x geo.W
+// (stem_prep); k-stage kt (BK = 32) = tap row dy = kt, 8 tap columns x 4
+// channels = the 64 contiguous bytes at pixel (2ho + kt, 2wo): the row base
+// is computed once per tile and each stage advances by one padded image row.
+template <int BM, int BN, bool PRO, int EPI, bool GATHER, int BK, int AMODE = 0>
 __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                      uint16_t* __restrict__ C, int64_t M, int N, int K,
                                                      const float* __restrict__ scale,
@@ -237,6 +243,11 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
         gnb[j] = (t1 / geo.Ho) * geo.H;
         ghb[j] = (t1 % geo.Ho) * geo.stride - geo.pad;
         gwb[j] = wo * geo.stride - geo.pad;
+      } else if (AMODE == 1) {
+        const int mi = static_cast<int>(gm);
+        const int wo = mi % geo.Wo, t1 = mi / geo.Wo;
+        const int ho = t1 % geo.Ho, nn = t1 / geo.Ho;
+        asrc[j] = A + ((static_cast<int64_t>(nn) * geo.H + 2 * ho) * geo.W + 2 * wo) * 4 + lc * 8;
       } else {
         asrc[j] = A + gm * K + lc * 8;
       }
@@ -264,6 +275,8 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
         const uint16_t* src = ok ? A + (static_cast<int64_t>(gnb[j] + hi) * geo.W + wi) * geo.cin + is_c0 + lc * 8
                                  : geo.zero + lc * 8;
         glds16(src, base + (wave * NA + j) * 1024);
+      } else if (AMODE == 1) {
+        glds16(asrc[j] + static_cast<int64_t>(is_kt) * geo.W * 4, base + (wave * NA + j) * 1024);
       } else {
         glds16(asrc[j] + k0, base + (wave * NA + j) * 1024);
       }
@@ -963,6 +976,29 @@ void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, 
   ConvGeo geo{H, W, Ho, Wo, stride, pad, kw, static_cast<const uint16_t*>(zero), Cin};
   gemm_nt_launch<true>(X, Wt, Y, static_cast<int64_t>(N) * Ho * Wo, Cout, kh * kw * Cin, nullptr, nullptr, false,
                        stats, geo, s);
+}
+
+void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W, int Cout, float* stats,
+                   hipStream_t s) {
+  // geo: padded image (stem_hp/stem_wp) and the stride-2 output grid
+  ConvGeo geo{H + 6, W + 8, H / 2, W / 2, 2, 0, 7, nullptr, 4};
+  const int64_t M = static_cast<int64_t>(N) * (H / 2) * (W / 2);
+  constexpr int BM = 128, BN = 64, BK = 32, K = 224;
+  const int tiles_m = static_cast<int>((M + BM - 1) / BM);
+  const int tn = Cout / BN;
+  const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
+  int P = tiles <= 512 ? static_cast<int>(tiles) : (512 / tn) * tn;
+  if (P < tn) P = tn;
+  const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 + 4 * 32 * BN;
+  auto a = static_cast<const uint16_t*>(xp);
+  auto b = static_cast<const uint16_t*>(wm);
+  auto c = static_cast<uint16_t*>(y);
+  if (stats)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 1, false, BK, 1>), dim3(P), dim3(kT), lds, s, a, b, c, M, Cout,
+                       K, nullptr, nullptr, 0, stats, tiles_m, tn, geo, BnRedArgs{});
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 0, false, BK, 1>), dim3(P), dim3(kT), lds, s, a, b, c, M, Cout,
+                       K, nullptr, nullptr, 0, nullptr, tiles_m, tn, geo, BnRedArgs{});
 }
 
 void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s, int taps) {

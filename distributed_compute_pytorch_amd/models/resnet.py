@@ -23,6 +23,7 @@ from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv import (bn_relu_conv, bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk, conv_kxk_gemm,
                         conv_kxk_gemm_ok, conv_kxk_ok, gemm_ok, kxk_policy)
 from ..ops.pool import FusedMaxPool2d
+from ..ops.stem import fused_stem, stem_supported
 
 
 GEMM_MAX_INTENSITY = float(os.environ.get("DCP_GEMM_MAX_INTENSITY", "1024"))
@@ -36,6 +37,8 @@ KXK_GEMM = os.environ.get("DCP_KXK_GEMM", "1") == "1"
 BN_CONV_FUSE = os.environ.get("DCP_BN_CONV_FUSE", "0") == "1"
 # BN-apply prologue in the conv3 GEMM only while Cout ≤ this (≤ 2 N-tiles of 128)
 PRO_MAX_COUT = int(os.environ.get("DCP_PRO_MAX_COUT", "256"))
+# conv1 + bn1 + relu + maxpool as one fused node (ops/stem.py); 0 = per-module path
+FUSED_STEM = os.environ.get("DCP_STEM", "1") == "1"
 
 
 def conv3x3(cin, cout, stride=1):
@@ -216,6 +219,18 @@ class ResNet(nn.Module):
         return stage
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if (FUSED_STEM and self.fused_bn and isinstance(self.maxpool, FusedMaxPool2d)
+                and stem_supported(x, self.conv1, self.bn1, self.training)):
+            # stem GEMM + BN + ReLU + max-pool in one node (no MIOpen, no ATen casts)
+            if self.dual_bn:
+                x, a = fused_stem(x, self.conv1, self.bn1, dual=True)
+                x, a = self.layer1(x, a, True)
+                x, a = self.layer2(x, a, True)
+                x, a = self.layer3(x, a, True)
+                x = self.layer4(x, a, False)
+            else:
+                x = self.layer4(self.layer3(self.layer2(self.layer1(fused_stem(x, self.conv1, self.bn1)))))
+            return self.fc(torch.flatten(self.avgpool(x), 1))
         x = self.bn1(self.conv1(x))
         if self.fused_bn and self.dual_bn:
             # thread dual-output aliases across stage boundaries: every
