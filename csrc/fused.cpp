@@ -1,5 +1,7 @@
 #include "fused.h"
 
+#include <cstring>
+
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
@@ -251,6 +253,60 @@ std::vector<at::Tensor> conv_weight_bf16(const at::Tensor& w) {
   kern::weight_cast_t(wf.data_ptr<float>(), wb.data_ptr(), wd.data_ptr(), static_cast<int>(Co), static_cast<int>(Ci),
                       stream_of(w), static_cast<int>(kh * kw));
   return {wb, wd};
+}
+
+// One-launch bf16 operands for a set of conv weights (weight_prep_kernel):
+// persistent flat bf16 buffer, per weight wb [R,kh,kw,Cin] (forward operand,
+// = the channels_last memory of the bf16 weight) and wt [Cin,kh,kw,R] (tap-
+// flipped transpose: dgrad operand), and a device descriptor table. Pointers
+// are baked in: rebuild when a weight's storage changes.
+std::tuple<at::Tensor, int64_t, std::vector<at::Tensor>, std::vector<at::Tensor>> weight_prep_plan(
+    const std::vector<at::Tensor>& ws) {
+  DCP_CHECK(!ws.empty(), "weight_prep_plan: no weights");
+  c10::hip::HIPGuard guard(ws[0].device().index());
+  int64_t E = 0;
+  for (auto& w : ws) {
+    DCP_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.device() == ws[0].device(),
+              "weight_prep_plan: fp32 4-D device conv weights on one device required");
+    DCP_CHECK(w.permute({0, 2, 3, 1}).is_contiguous(),
+              "weight_prep_plan: weights must be channels_last ([Cout][kh][kw][Cin] memory)");
+    E += w.numel();
+  }
+  at::Tensor flat = at::empty({2 * E}, ws[0].options().dtype(at::kBFloat16));
+  std::vector<at::Tensor> wbs, wts;
+  std::vector<kern::WPrepDesc> descs;
+  int64_t off = 0, tiles = 0;
+  for (auto& w : ws) {
+    const int64_t R = w.size(0), Ci = w.size(1), kh = w.size(2), kw = w.size(3), n = w.numel();
+    at::Tensor wb = flat.narrow(0, off, n).view({R, kh, kw, Ci});
+    at::Tensor wt = flat.narrow(0, E + off, n).view({Ci, kh, kw, R});
+    kern::WPrepDesc d{};
+    d.w = w.data_ptr<float>();
+    d.wb = static_cast<uint16_t*>(wb.data_ptr());
+    d.wt = static_cast<uint16_t*>(wt.data_ptr());
+    d.R = static_cast<int>(R);
+    d.Cc = static_cast<int>(Ci);
+    d.T = static_cast<int>(kh * kw);
+    d.tiles_c = static_cast<int>((Ci + 31) / 32);
+    d.tiles_r = static_cast<int>((R + 31) / 32);
+    d.tile0 = tiles;
+    tiles += static_cast<int64_t>(d.T) * d.tiles_c * d.tiles_r;
+    descs.push_back(d);
+    wbs.push_back(wb);
+    wts.push_back(wt);
+    off += n;
+  }
+  const int64_t bytes = static_cast<int64_t>(descs.size() * sizeof(kern::WPrepDesc));
+  at::Tensor host = at::empty({bytes}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(host.data_ptr(), descs.data(), bytes);
+  at::Tensor table = host.to(ws[0].device());
+  return {table, tiles, wbs, wts};
+}
+
+void weight_prep_run(const at::Tensor& table, int64_t tiles) {
+  c10::hip::HIPGuard guard(table.device().index());
+  const int n = static_cast<int>(table.numel() / static_cast<int64_t>(sizeof(kern::WPrepDesc)));
+  kern::weight_prep(table.data_ptr(), n, tiles, stream_of(table));
 }
 
 // dx[M, Cin] = gy[M, Cout] · w[Cout, Cin]; wt = w^T contiguous [Cin, Cout] bf16
@@ -622,6 +678,99 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   kern::attn_bwd(p, attn_view(q, "q"), attn_view(k, "k"), attn_view(v, "v"), attn_view(o, "o"),
                  attn_view(dout, "dout"), lse.data_ptr<float>(), delta.data_ptr<float>(), attn_out(dq, "dq"),
                  attn_out(dk, "dk"), attn_out(dv, "dv"), stream_of(q));
+}
+
+namespace {
+float* fptr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+}  // namespace
+
+// Training y = relu(bn(x) + bn2(x2)): the bottleneck's BN3 + residual + ReLU
+// with the downsample branch's BN applied inline (its output never hits HBM).
+// Both statistics come from the producing GEMMs' epilogues (stats, stats2).
+// Returns (y, mean, invstd, relu_bits, mean2, invstd2).
+std::vector<at::Tensor> bn_resbn_act_fwd(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
+                                         const c10::optional<at::Tensor>& running_mean,
+                                         const c10::optional<at::Tensor>& running_var,
+                                         const c10::optional<at::Tensor>& nbt, const at::Tensor& stats,
+                                         const at::Tensor& x2, const at::Tensor& weight2, const at::Tensor& bias2,
+                                         const c10::optional<at::Tensor>& running_mean2,
+                                         const c10::optional<at::Tensor>& running_var2,
+                                         const c10::optional<at::Tensor>& nbt2, const at::Tensor& stats2,
+                                         double momentum, double eps, double momentum2, double eps2) {
+  check_nhwc(x, "bn_resbn_act_fwd");
+  check_nhwc(x2, "bn_resbn_act_fwd(x2)");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  DCP_CHECK(x2.sizes() == x.sizes() && x2.scalar_type() == x.scalar_type(), "bn_resbn_act_fwd: x2 mismatch");
+  for (const at::Tensor* t : {&stats, &stats2})
+    DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == 2 * C && t->is_contiguous(),
+              "bn_resbn_act_fwd: stats must be fp32 [2*C]");
+  for (const at::Tensor* t : {&weight, &bias, &weight2, &bias2})
+    DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(),
+              "bn_resbn_act_fwd: affine parameters must be fp32 [C]");
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor y = at::empty_like(x, cl_fmt(x));
+  at::Tensor mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  at::Tensor mean2 = at::empty({C}, fopt), invstd2 = at::empty({C}, fopt);
+  at::Tensor bits = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  kern::ResBnArgs rb;
+  rb.acc = stats2.data_ptr<float>();
+  rb.gamma = weight2.data_ptr<float>();
+  rb.beta = bias2.data_ptr<float>();
+  rb.mean_out = mean2.data_ptr<float>();
+  rb.invstd_out = invstd2.data_ptr<float>();
+  rb.running_mean = fptr(running_mean2);
+  rb.running_var = fptr(running_var2);
+  rb.momentum = static_cast<float>(momentum2);
+  rb.eps = static_cast<float>(eps2);
+  rb.nbt = nbt2.has_value() && nbt2->defined() ? nbt2->data_ptr<int64_t>() : nullptr;
+  kern::bn_forward_train_resbn(bn_dtype(x), x.data_ptr(), x2.data_ptr(), y.data_ptr(), M, static_cast<int>(C),
+                               weight.data_ptr<float>(), bias.data_ptr<float>(), fptr(running_mean),
+                               fptr(running_var), static_cast<float>(momentum), static_cast<float>(eps),
+                               mean.data_ptr<float>(), invstd.data_ptr<float>(), stats.data_ptr<float>(),
+                               nbt.has_value() && nbt->defined() ? nbt->data_ptr<int64_t>() : nullptr,
+                               bits.data_ptr<uint8_t>(), rb, stream_of(x));
+  return {y, mean, invstd, bits, mean2, invstd2};
+}
+
+// Backward of bn_resbn_act_fwd: (dx, dweight, dbias, dx2, dweight2, dbias2).
+std::vector<at::Tensor> bn_resbn_act_bwd(const at::Tensor& gy, const c10::optional<at::Tensor>& gy2_opt,
+                                         const at::Tensor& x, const at::Tensor& weight, const at::Tensor& mean,
+                                         const at::Tensor& invstd, const at::Tensor& bits, const at::Tensor& x2,
+                                         const at::Tensor& weight2, const at::Tensor& mean2,
+                                         const at::Tensor& invstd2) {
+  check_nhwc(x, "bn_resbn_act_bwd");
+  c10::hip::HIPGuard guard(x.device().index());
+  at::Tensor g = gy.contiguous(cl_fmt(x));
+  if (g.scalar_type() != x.scalar_type()) g = g.to(x.scalar_type());
+  at::Tensor g2;
+  if (gy2_opt.has_value() && gy2_opt->defined()) {
+    g2 = gy2_opt->contiguous(cl_fmt(x));
+    if (g2.scalar_type() != x.scalar_type()) g2 = g2.to(x.scalar_type());
+  }
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  DCP_CHECK(bits.numel() == M * C / 8, "bn_resbn_act_bwd: relu bits mismatch");
+  auto fopt = x.options().dtype(at::kFloat);
+  auto s = stream_of(x);
+  at::Tensor gout = at::empty_like(x, cl_fmt(x));
+  at::Tensor dx = at::empty_like(x, cl_fmt(x)), dx2 = at::empty_like(x2, cl_fmt(x2));
+  at::Tensor dw = at::empty({C}, fopt), db = at::empty({C}, fopt), dw2 = at::empty({C}, fopt),
+             db2 = at::empty({C}, fopt);
+  at::Tensor acc = zeroed_floats(2 * C, x, s), acc2 = zeroed_floats(2 * C, x, s);
+  kern::bn_backward_resbn(bn_dtype(x), g.data_ptr(), g2.defined() ? g2.data_ptr() : nullptr, x.data_ptr(), M,
+                          static_cast<int>(C), weight.data_ptr<float>(), mean.data_ptr<float>(),
+                          invstd.data_ptr<float>(), bits.data_ptr<uint8_t>(), gout.data_ptr(), dx.data_ptr(),
+                          dw.data_ptr<float>(), db.data_ptr<float>(), acc.data_ptr<float>(), x2.data_ptr(),
+                          mean2.data_ptr<float>(), acc2.data_ptr<float>(), s);
+  kern::bn_backward_apply_plain(bn_dtype(x), gout.data_ptr(), x2.data_ptr(), M, static_cast<int>(C),
+                                weight2.data_ptr<float>(), mean2.data_ptr<float>(), invstd2.data_ptr<float>(),
+                                acc2.data_ptr<float>(), dx2.data_ptr(), dw2.data_ptr<float>(),
+                                db2.data_ptr<float>(), s);
+  return {dx, dw, db, dx2, dw2, db2};
 }
 
 // Returns (dx, dweight, dbias, dresidual).
@@ -1047,6 +1196,8 @@ void bind(pybind11::module& m) {
   m.def("conv1x1_dgrad_bnred", &conv1x1_dgrad_bnred, "1x1 data gradient + BN/ReLU backward reduction epilogue");
   m.def("conv_dgrad_bnred", &conv_dgrad_bnred, "stride-1 kxk data gradient + BN/ReLU backward reduction epilogue");
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply, "BN/ReLU training backward apply from a precomputed reduction");
+  m.def("bn_resbn_act_fwd", &bn_resbn_act_fwd, "training relu(bn(x) + bn2(x2)), both BNs fused (downsample block)");
+  m.def("bn_resbn_act_bwd", &bn_resbn_act_bwd, "backward of bn_resbn_act_fwd");
   m.def("conv1x1_s2_dgrad", &conv1x1_s2_dgrad, "stride-2 1x1 conv data gradient (GEMM + scattering epilogue)");
   m.def("conv_dgrad_s2", &conv_dgrad_s2, "stride-2 kxk conv data gradient as four parity-class implicit GEMMs");
   m.def("conv_wgrad", &conv_wgrad, "kxk NHWC conv weight gradient (implicit-GEMM MFMA, fp32 out)",
@@ -1054,6 +1205,8 @@ void bind(pybind11::module& m) {
         pybind11::arg("pad"));
   m.def("weight_bf16_t", &weight_bf16_t, "fp32 weight -> (bf16 [R,C], bf16 transposed [C,R]) in one launch");
   m.def("conv_weight_bf16", &conv_weight_bf16, "kxk weight -> (bf16 fwd [Co][kh][kw][Ci], bf16 flipped [Ci][kh][kw][Co])");
+  m.def("weight_prep_plan", &weight_prep_plan, "conv weights -> (device table, tiles, bf16 fwd views, bf16 dgrad views)");
+  m.def("weight_prep_run", &weight_prep_run, py::arg("table"), py::arg("tiles"));
   m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("gy"), pybind11::arg("x"),
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
         pybind11::arg("relu") = false, pybind11::arg("accumulate_into") = pybind11::none());

@@ -216,7 +216,10 @@ __device__ __forceinline__ void coef(const float* gamma, const float* beta, int 
 // Thread → channel mapping is constant across the grid-stride loop when
 // (grid*256) % (C/8) == 0 (always true for power-of-two C ≤ 2048), so each
 // thread keeps its 8 scale/shift values in registers.
-template <int D, bool RES, bool ACT, bool TRAIN>
+// RBN: the residual is itself BatchNorm'd (training statistics from its own
+// producing GEMM's epilogue, rb.acc) inline — the downsample branch's BN output
+// is never written to HBM (saves its write + this kernel's re-read of it).
+template <int D, bool RES, bool ACT, bool TRAIN, bool RBN = false>
 __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ res,
                                                       const float* __restrict__ acc, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, const float* __restrict__ scale_in,
@@ -225,7 +228,7 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
                                                       float* running_mean, float* running_var, float momentum,
                                                       float eps, int64_t M, int64_t nvec, int C,
                                                       int64_t* __restrict__ nbt, uint8_t* __restrict__ mbits,
-                                                      int zshift) {
+                                                      int zshift, ResBnArgs rb = ResBnArgs{}) {
   const int cv = C / kV;
   const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
@@ -255,15 +258,34 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
     }
     cf[c] = a;
     cf[C + c] = b;
+    if (RBN) {  // the residual's own BN: statistics from its GEMM epilogue (unshifted sums)
+      float rmean, rvar, rinv, ra, rbb;
+      stats_for<D>(rb.acc, res, M, C, c, rb.eps, &rmean, &rvar, &rinv, 1);
+      coef(rb.gamma, rb.beta, c, rmean, rinv, &ra, &rbb);
+      cf[2 * C + c] = ra;
+      cf[3 * C + c] = rbb;
+      if (blockIdx.x == 0) {
+        rb.mean_out[c] = rmean;
+        rb.invstd_out[c] = rinv;
+        if (rb.running_mean) {
+          const float unb = M > 1 ? rvar * (static_cast<float>(M) / static_cast<float>(M - 1)) : rvar;
+          rb.running_mean[c] = (1.f - rb.momentum) * rb.running_mean[c] + rb.momentum * rmean;
+          rb.running_var[c] = (1.f - rb.momentum) * rb.running_var[c] + rb.momentum * unb;
+        }
+      }
+    }
   }
   __syncthreads();
-  float sc[kV], sf[kV];
+  float sc[kV], sf[kV], rsc[kV], rsf[kV];
 #pragma unroll
   for (int k = 0; k < kV; ++k) {
     sc[k] = cf[c0 + k];
     sf[k] = cf[C + c0 + k];
+    rsc[k] = RBN ? cf[2 * C + c0 + k] : 1.f;
+    rsf[k] = RBN ? cf[3 * C + c0 + k] : 0.f;
   }
   if (TRAIN && nbt && tid == 0) *nbt += 1;  // num_batches_tracked (saves an ATen add launch per BN)
+  if (RBN && rb.nbt && tid == 0) *rb.nbt += 1;
   // two vectors per thread per iteration: twice the loads in flight
   // mbits (RES && ACT): bit k of byte v = (y[v*8 + k] > 0), the backward's
   // ReLU mask at 1/16 of the bytes of re-reading y
@@ -272,7 +294,7 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
 #pragma unroll
     for (int k = 0; k < kV; ++k) {
       float o = fmaf(a[k], sc[k], sf[k]);
-      if (RES) o += r[k];
+      if (RES) o += RBN ? fmaf(r[k], rsc[k], rsf[k]) : r[k];
       if (ACT) {
         bits |= (o > 0.f ? 1u : 0u) << k;
         o = fmaxf(o, 0.f);
@@ -342,7 +364,10 @@ __global__ void __launch_bounds__(kT) bn_finalize_kernel(const void* __restrict_
 // them with a separate elementwise pass).
 // MX: ReLU mask recomputed from x (x*sc + sf > 0, the forward's own
 // expression) instead of reading y — non-residual BN+ReLU only.
-template <int D, bool ACT, bool STORE_G, bool GY2, bool MX>
+// X2: the residual input was BN(x2) (RBN forward): also reduce that BN's
+// Σg·(x2 - mean2) into acc2 (with Σg again, acc2 = [Σg | Σg·(x2-mean2)]) —
+// its backward then needs only the apply pass, no reduce re-reading g.
+template <int D, bool ACT, bool STORE_G, bool GY2, bool MX, bool X2 = false>
 __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restrict__ gy, const void* __restrict__ gy2,
                                                            const void* __restrict__ y,
                                                            const void* __restrict__ x, const float* __restrict__ mean,
@@ -351,7 +376,10 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
                                                            const float* __restrict__ beta,
                                                            const uint8_t* __restrict__ mbits,
                                                            int64_t M, int C, int64_t rows_per_blk,
-                                                           float* __restrict__ acc, void* __restrict__ gout) {
+                                                           float* __restrict__ acc, void* __restrict__ gout,
+                                                           const void* __restrict__ x2 = nullptr,
+                                                           const float* __restrict__ mean2 = nullptr,
+                                                           float* __restrict__ acc2 = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const Geo g = geo(C);
   const int chunk = blockIdx.y;
@@ -361,13 +389,14 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
   const bool cv_ok = cvec < g.cv && grp < g.rpi;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_blk;
   const int64_t r1 = min(M, r0 + rows_per_blk);
-  float sb[kV], sg[kV], mu[kV], sc[kV], sf[kV];
+  float sb[kV], sg[kV], mu[kV], sc[kV], sf[kV], s2[kV], mu2[kV];
 #pragma unroll
-  for (int k = 0; k < kV; ++k) sb[k] = sg[k] = 0.f;
+  for (int k = 0; k < kV; ++k) sb[k] = sg[k] = s2[k] = 0.f;
   if (cv_ok) {
 #pragma unroll
     for (int k = 0; k < kV; ++k) {
       mu[k] = mean[cvec * kV + k];
+      if (X2) mu2[k] = mean2[cvec * kV + k];
       if (MX) coef(gamma, beta, cvec * kV + k, mu[k], invstd[cvec * kV + k], &sc[k], &sf[k]);
     }
     // one row: loads already issued (gv = gy (+gy2 after the add), xv, mb)
@@ -389,6 +418,12 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
       for (int k = 0; k < kV; ++k) {
         sb[k] += gv[k];
         sg[k] = fmaf(gv[k], xv[k] - mu[k], sg[k]);
+      }
+      if (X2) {
+        float x2v[kV];
+        V8<D>::ld(x2, off, x2v);
+#pragma unroll
+        for (int k = 0; k < kV; ++k) s2[k] = fmaf(gv[k], x2v[k] - mu2[k], s2[k]);
       }
     };
     constexpr int kR = GY2 ? 2 : 4;  // rows in flight per thread (2-3 operands each)
@@ -429,6 +464,10 @@ __global__ void __launch_bounds__(kT) bn_bwd_reduce_kernel(const void* __restric
     }
   }
   block_reduce_atomic(sb, sg, g, chunk * g.tpr, C, acc, smem);
+  if (X2) {
+    __syncthreads();  // smem reuse
+    block_reduce_atomic(sb, s2, g, chunk * g.tpr, C, acc2, smem);
+  }
 }
 
 // dx = k1 * (g - k2 - (x - mean) * k3); g from gout (FROM_G) or gy*(y>0).
@@ -734,6 +773,76 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
     else DCP_BN_BAPPLY(BN_F32, false, false);
   }
 #undef DCP_BN_BAPPLY
+}
+
+void bn_forward_train_resbn(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
+                            const float* gamma, const float* beta, float* running_mean, float* running_var,
+                            float momentum, float eps, float* mean, float* invstd, const float* acc, int64_t* nbt,
+                            uint8_t* mbits, const ResBnArgs& rb, hipStream_t s) {
+  const int64_t nvec = M * C / kV;
+  const int grid = apply_grid(nvec, C / kV);
+  const size_t asm_ = sizeof(float) * 4 * C;
+  if (dtype == BN_BF16)
+    hipLaunchKernelGGL((bn_apply_kernel<BN_BF16, true, true, true, true>), dim3(grid), dim3(kT), asm_, s, x, res, acc,
+                       gamma, beta, nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M,
+                       nvec, C, nbt, mbits, 1, rb);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<BN_F32, true, true, true, true>), dim3(grid), dim3(kT), asm_, s, x, res, acc,
+                       gamma, beta, nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M,
+                       nvec, C, nbt, mbits, 1, rb);
+}
+
+void bn_backward_resbn(int dtype, const void* gy, const void* gy2, const void* x, int64_t M, int C,
+                       const float* gamma, const float* mean, const float* invstd, const uint8_t* mbits, void* gout,
+                       void* dx, float* dgamma, float* dbeta, float* acc, const void* x2, const float* mean2,
+                       float* acc2, hipStream_t s) {
+  int nblk, nchunks;
+  int64_t rpb;
+  red_geometry(M, C, &nblk, &rpb, &nchunks, true);
+  const size_t sm = red_smem(C);
+  // g = (gy [+ gy2]) * relu-mask(bits) stored to gout; (Σg, Σg(x-μ)) -> acc, (Σg, Σg(x2-μ2)) -> acc2
+  if (dtype == BN_BF16) {
+    if (gy2)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, true, true, true, false, true>), dim3(nblk, nchunks), dim3(kT),
+                         sm, s, gy, gy2, nullptr, x, mean, invstd, gamma, nullptr, mbits, M, C, rpb, acc, gout, x2,
+                         mean2, acc2);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_BF16, true, true, false, false, true>), dim3(nblk, nchunks), dim3(kT),
+                         sm, s, gy, nullptr, nullptr, x, mean, invstd, gamma, nullptr, mbits, M, C, rpb, acc, gout,
+                         x2, mean2, acc2);
+  } else {
+    if (gy2)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, true, true, true, false, true>), dim3(nblk, nchunks), dim3(kT),
+                         sm, s, gy, gy2, nullptr, x, mean, invstd, gamma, nullptr, mbits, M, C, rpb, acc, gout, x2,
+                         mean2, acc2);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<BN_F32, true, true, false, false, true>), dim3(nblk, nchunks), dim3(kT),
+                         sm, s, gy, nullptr, nullptr, x, mean, invstd, gamma, nullptr, mbits, M, C, rpb, acc, gout,
+                         x2, mean2, acc2);
+  }
+  const int64_t nvec = M * C / kV;
+  const int grid = apply_grid(nvec, C / kV);
+  const size_t bsm = sizeof(float) * 4 * C;
+  if (dtype == BN_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<BN_BF16, false, true, true>), dim3(grid), dim3(kT), bsm, s, gout, nullptr,
+                       x, mean, invstd, gamma, nullptr, acc, dgamma, dbeta, true, dx, M, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<BN_F32, false, true, true>), dim3(grid), dim3(kT), bsm, s, gout, nullptr,
+                       x, mean, invstd, gamma, nullptr, acc, dgamma, dbeta, true, dx, M, nvec, C);
+}
+
+void bn_backward_apply_plain(int dtype, const void* g, const void* x, int64_t M, int C, const float* gamma,
+                             const float* mean, const float* invstd, const float* acc, void* dx, float* dgamma,
+                             float* dbeta, hipStream_t s) {
+  const int64_t nvec = M * C / kV;
+  const int grid = apply_grid(nvec, C / kV);
+  const size_t bsm = sizeof(float) * 4 * C;
+  if (dtype == BN_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<BN_BF16, false, true, true>), dim3(grid), dim3(kT), bsm, s, g, nullptr, x,
+                       mean, invstd, gamma, nullptr, acc, dgamma, dbeta, true, dx, M, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<BN_F32, false, true, true>), dim3(grid), dim3(kT), bsm, s, g, nullptr, x,
+                       mean, invstd, gamma, nullptr, acc, dgamma, dbeta, true, dx, M, nvec, C);
 }
 
 // BN(+ReLU) backward apply only, training mode, mask recomputed from x: acc

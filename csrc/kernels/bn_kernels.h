@@ -14,6 +14,40 @@ enum BnDType : int { BN_F32 = 0, BN_BF16 = 1 };
 // multiple of 256, e.g. every power of two ≥ 8).
 bool bn_supported(int C);
 
+// BatchNorm (training) applied to the residual operand inline (a downsample
+// branch's BN): statistics from its GEMM epilogue (unshifted Σ, Σ²).
+struct ResBnArgs {
+  const float* acc = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  float* mean_out = nullptr;
+  float* invstd_out = nullptr;
+  float* running_mean = nullptr;
+  float* running_var = nullptr;
+  float momentum = 0.1f;
+  float eps = 1e-5f;
+  int64_t* nbt = nullptr;
+};
+
+// y = relu(bn(x) + bn_res(res)), training, both statistics from GEMM epilogues
+// (acc, rb.acc); mbits as bn_forward_train (residual + act).
+void bn_forward_train_resbn(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
+                            const float* gamma, const float* beta, float* running_mean, float* running_var,
+                            float momentum, float eps, float* mean, float* invstd, const float* acc, int64_t* nbt,
+                            uint8_t* mbits, const ResBnArgs& rb, hipStream_t s);
+// Backward of bn_forward_train_resbn's first BN: g = (gy [+ gy2])·mask -> gout,
+// acc (ZEROED [2C]) = (Σg, Σg·(x-mean)), acc2 (ZEROED [2C]) = (Σg, Σg·(x2-mean2))
+// for the residual BN, dx / dgamma / dbeta of the first BN. The residual BN's
+// input gradient is then bn_backward_apply_plain(gout, x2, ..., acc2).
+void bn_backward_resbn(int dtype, const void* gy, const void* gy2, const void* x, int64_t M, int C,
+                       const float* gamma, const float* mean, const float* invstd, const uint8_t* mbits, void* gout,
+                       void* dx, float* dgamma, float* dbeta, float* acc, const void* x2, const float* mean2,
+                       float* acc2, hipStream_t s);
+// dx = BN backward apply (no activation) from upstream g and a precomputed acc [2C].
+void bn_backward_apply_plain(int dtype, const void* g, const void* x, int64_t M, int C, const float* gamma,
+                             const float* mean, const float* invstd, const float* acc, void* dx, float* dgamma,
+                             float* dbeta, hipStream_t s);
+
 // Training forward: batch statistics, running-stat update, y = act(bn(x) [+ res]).
 // mean/invstd: [C] fp32 outputs. acc: ZEROED workspace [2*C] fp32.
 void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,

@@ -770,6 +770,43 @@ __global__ void __launch_bounds__(kT) weight_cast_t_kernel(const float* __restri
   }
 }
 
+// All conv weights of a model in ONE launch (per step): the weight_cast_t
+// tile body over a table of tensors (block -> tensor by binary search over the
+// tile prefix). Replaces one cast(+transpose) launch per convolution (~5 µs of
+// mostly idle GPU each: 50+ per ResNet-50 step).
+__global__ void __launch_bounds__(kT) weight_prep_kernel(const WPrepDesc* __restrict__ d, int n) {
+  __shared__ uint16_t tile[32][33];
+  const int64_t b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].tile0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const WPrepDesc e = d[lo];
+  const int local = static_cast<int>(b - e.tile0);
+  const int per_tap = e.tiles_c * e.tiles_r;
+  const int tap = local / per_tap, rem = local % per_tap;
+  const int c0 = (rem % e.tiles_c) * 32, r0 = (rem / e.tiles_c) * 32;
+  const int R = e.R, Cc = e.Cc, T = e.T;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int r = r0 + ty + k, c = c0 + tx;
+    if (r < R && c < Cc) {
+      const int64_t i = (static_cast<int64_t>(r) * T + tap) * Cc + c;
+      const uint16_t u = __builtin_bit_cast(uint16_t, static_cast<__bf16>(e.w[i]));
+      e.wb[i] = u;
+      tile[ty + k][tx] = u;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int c = c0 + ty + k, r = r0 + tx;
+    if (r < R && c < Cc) e.wt[(static_cast<int64_t>(c) * T + (T - 1 - tap)) * R + r] = tile[tx][ty + k];
+  }
+}
+
 // Column sums of a bf16 [M, N] matrix into fp32 (Linear bias gradients):
 // stage 1 writes one fp32 partial row per (column chunk, row slab) block,
 // stage 2 = slab_partial_kernel over the slabs. Deterministic, no atomics.
@@ -999,6 +1036,12 @@ void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W,
   else
     hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 0, false, BK, 1>), dim3(P), dim3(kT), lds, s, a, b, c, M, Cout,
                        K, nullptr, nullptr, 0, nullptr, tiles_m, tn, geo, BnRedArgs{});
+}
+
+void weight_prep(const void* table, int n, int64_t tiles, hipStream_t s) {
+  if (n <= 0 || tiles <= 0) return;
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kT), 0, s,
+                     static_cast<const WPrepDesc*>(table), n);
 }
 
 void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s, int taps) {

@@ -31,6 +31,19 @@ void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
 // (the forward GEMM's B operand and the dgrad GEMM's B operand) in one launch.
 void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s, int taps = 1);
 
+// One entry per weight of weight_prep: fp32 w [R][T][Cc] -> bf16 wb (same
+// layout) and tap-flipped transpose wt [Cc][T][R]; tile0 = prefix of
+// T * ceil(R/32) * ceil(Cc/32) tiles over the table.
+struct WPrepDesc {
+  const float* w;
+  uint16_t* wb;
+  uint16_t* wt;
+  int R, Cc, T, tiles_c, tiles_r, pad;
+  int64_t tile0;
+};
+// weight_cast_t for a whole table of weights (device array of n WPrepDesc) in one launch.
+void weight_prep(const void* table, int n, int64_t tiles, hipStream_t s);
+
 // out[N] (fp32, ZEROED) += column sums of a bf16 [M, N] matrix (N % 8 == 0):
 // one launch, ≤ 64 row slabs × N/256 column chunks, one fp32 atomic per column
 // per block.

@@ -19,9 +19,9 @@ from typing import List, Optional, Type
 import torch
 from torch import nn
 
-from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import (bn_relu_conv, bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk, conv_kxk_gemm,
-                        conv_kxk_gemm_ok, conv_kxk_ok, gemm_ok, kxk_policy)
+from ..ops.batchnorm import BatchNormAct2d, bn_resbn_act, resbn_ok
+from ..ops.conv import (ConvWeightPrep, bn_relu_conv, bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk,
+                        conv_kxk_gemm, conv_kxk_gemm_ok, conv_kxk_ok, gemm_ok, kxk_policy)
 from ..ops.pool import FusedMaxPool2d
 from ..ops.stem import fused_stem, stem_supported
 
@@ -39,6 +39,10 @@ BN_CONV_FUSE = os.environ.get("DCP_BN_CONV_FUSE", "0") == "1"
 PRO_MAX_COUT = int(os.environ.get("DCP_PRO_MAX_COUT", "256"))
 # conv1 + bn1 + relu + maxpool as one fused node (ops/stem.py); 0 = per-module path
 FUSED_STEM = os.environ.get("DCP_STEM", "1") == "1"
+# every bottleneck conv's bf16 operands from ONE launch per forward (ops/conv.py ConvWeightPrep)
+WEIGHT_PREP = os.environ.get("DCP_WEIGHT_PREP", "1") == "1"
+# downsample BN applied inside BN3's residual kernel (its output never written)
+RESBN = os.environ.get("DCP_RESBN", "1") == "1"
 
 
 def conv3x3(cin, cout, stride=1):
@@ -101,17 +105,21 @@ class Bottleneck(nn.Module):
         Per block this drops the BN1/BN3 statistics passes and BN2's apply
         (a full write + read of the 3x3 conv's activation)."""
         inp = x if identity is None else identity
+        resbn = None  # (downsample BN, its raw input, its sums): applied inside BN3's kernel
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
+            z = st = None
             if conv.stride == (1, 1) and gemm_ok(inp, conv.in_channels, conv.out_channels):
                 z, st = gemm_conv1x1(inp, conv.weight, stats=True)
-                identity = bn(z, stats=st)
             elif KXK_GEMM and conv_kxk_gemm_ok(inp, conv):
                 # strided 1x1: gathered implicit GEMM (+ BN sums); dgrad on MIOpen
                 z, st = conv_kxk_gemm(inp, conv.weight, conv.stride[0], conv.padding[0], stats=True)
-                identity = bn(z, stats=st)
-            else:
+            if z is None:
                 identity = self.downsample(inp)
+            elif RESBN and resbn_ok(bn, z, st) and resbn_ok(self.bn3, z, st):
+                resbn, identity = (bn, z, st), None
+            else:
+                identity = bn(z, stats=st)
         else:
             identity = inp
         z1, s1 = gemm_conv1x1(x, self.conv1.weight, stats=True)
@@ -120,7 +128,7 @@ class Bottleneck(nn.Module):
         if KXK_GEMM and BN_CONV_FUSE and conv_kxk_gemm_ok(z1, c2):
             x2, s2 = bn_relu_conv(z1, self.bn1, c2.weight, c2.kernel_size[0], c2.stride[0], c2.padding[0], sums=s1,
                                   stats=True)
-            return self._tail(x2, s2, identity, dual, True)
+            return self._tail(x2, s2, identity, dual, True, resbn)
         y1 = self.bn1(z1, stats=s1)
         if KXK_GEMM and conv_kxk_gemm_ok(y1, c2):
             ho = (y1.shape[2] + 2 * c2.padding[0] - c2.kernel_size[0]) // c2.stride[0] + 1
@@ -135,9 +143,9 @@ class Bottleneck(nn.Module):
             x2 = c2(y1)
         if not x2.is_contiguous(memory_format=torch.channels_last):
             x2 = x2.contiguous(memory_format=torch.channels_last)
-        return self._tail(x2, s2, identity, dual, False)
+        return self._tail(x2, s2, identity, dual, False, resbn)
 
-    def _tail(self, x2, s2, identity, dual, fuse):
+    def _tail(self, x2, s2, identity, dual, fuse, resbn=None):
         """BN2 → conv3 → BN3 (+ residual, ReLU)."""
         if self.conv3.out_channels <= PRO_MAX_COUT:
             # BN2+ReLU applied in the GEMM prologue (its output never hits HBM)
@@ -149,6 +157,11 @@ class Bottleneck(nn.Module):
             # wide conv3: every N-tile re-applies the prologue to the same rows,
             # which costs more than one apply pass over the narrow input
             z3, s3 = gemm_conv1x1(self.bn2(x2, stats=s2), self.conv3.weight, stats=True)
+        if resbn is not None:
+            if resbn_ok(self.bn3, z3, s3):
+                bn, z, st = resbn
+                return bn_resbn_act(self.bn3, z3, s3, bn, z, st, dual)
+            identity = resbn[0](resbn[1], stats=resbn[2])
         return self.bn3(z3, identity, dual=dual, stats=s3)
 
 
@@ -218,7 +231,28 @@ class ResNet(nn.Module):
         stage.use_dual = self.dual_bn
         return stage
 
+    def _weight_prep(self):
+        """Context that casts every bottleneck conv weight to its bf16 GEMM
+        operands in one launch (training on the fused GEMM path), else a no-op."""
+        import contextlib
+
+        if not (WEIGHT_PREP and self.fused_gemm and self.training and self.fc.weight.is_cuda):
+            return contextlib.nullcontext()
+        prep = self.__dict__.get("_wprep")
+        if prep is None:
+            ws = [m.weight for name, m in self.named_modules()
+                  if isinstance(m, nn.Conv2d) and m is not self.conv1]
+            if not ws or not all(ConvWeightPrep.eligible(w) for w in ws):
+                return contextlib.nullcontext()
+            prep = ConvWeightPrep(ws)
+            self.__dict__["_wprep"] = prep  # not a submodule / buffer: state_dict unchanged
+        return prep
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        with self._weight_prep():
+            return self._forward(x)
+
+    def _forward(self, x: torch.Tensor) -> torch.Tensor:
         if (FUSED_STEM and self.fused_bn and isinstance(self.maxpool, FusedMaxPool2d)
                 and stem_supported(x, self.conv1, self.bn1, self.training)):
             # stem GEMM + BN + ReLU + max-pool in one node (no MIOpen, no ATen casts)

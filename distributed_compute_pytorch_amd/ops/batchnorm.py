@@ -87,6 +87,56 @@ def bn_act(x, weight, bias, running_mean, running_var, num_batches_tracked, trai
                           nbt, stats)
 
 
+class _BNResBNActFn(torch.autograd.Function):
+    """relu(bn(x) + bn2(x2)) in training mode, both BatchNorms on statistics
+    from their producing GEMMs' epilogues: the downsample branch's BN output is
+    never materialised; backward reduces bn2's sums in bn's reduce pass."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, x2, weight2, bias2, rm, rv, nbt, stats, rm2, rv2, nbt2, stats2, momentum, eps,
+                momentum2, eps2, dual):
+        y, mean, invstd, bits, mean2, invstd2 = _C.bn_resbn_act_fwd(
+            x, weight, bias, rm, rv, nbt, stats, x2, weight2, bias2, rm2, rv2, nbt2, stats2, float(momentum),
+            float(eps), float(momentum2), float(eps2))
+        ctx.save_for_backward(x, weight, mean, invstd, bits, x2, weight2, mean2, invstd2)
+        if dual:
+            return y, y.view_as(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy, gy2=None):
+        x, weight, mean, invstd, bits, x2, weight2, mean2, invstd2 = ctx.saved_tensors
+        if gy is None:
+            gy, gy2 = gy2, None
+        dx, dw, db, dx2, dw2, db2 = _C.bn_resbn_act_bwd(gy, gy2, x, weight, mean, invstd, bits, x2, weight2, mean2,
+                                                        invstd2)
+        return (dx, dw, db, dx2, dw2, db2) + (None,) * 13
+
+
+def resbn_ok(bn: nn.BatchNorm2d, x: torch.Tensor, stats) -> bool:
+    return (bn.training and bn.affine and bn.track_running_stats and bn.momentum is not None
+            and stats is not None and stats.numel() == 2 * x.shape[1] and bn.weight.dtype == torch.float32
+            and isinstance(bn, BatchNormAct2d) and bn._use_fused(x))
+
+
+def bn_resbn_act(bn: "BatchNormAct2d", x: torch.Tensor, stats: torch.Tensor, bn2: "BatchNormAct2d",
+                 x2: torch.Tensor, stats2: torch.Tensor, dual: bool = False):
+    """``relu(bn(x) + bn2(x2))`` (training; ``stats``/``stats2`` = (Σ, Σ²) of x / x2
+    from their GEMM epilogues) — same parameters, buffers and running-stat
+    updates as ``bn(x, residual=bn2(x2))``."""
+
+    def _nbt(m):
+        t = m.num_batches_tracked
+        if t is not None and (t.device != x.device or t.dtype != torch.int64):
+            t.add_(1)
+            return None
+        return t
+
+    return _BNResBNActFn.apply(x, bn.weight, bn.bias, x2, bn2.weight, bn2.bias, bn.running_mean, bn.running_var,
+                               _nbt(bn), stats, bn2.running_mean, bn2.running_var, _nbt(bn2), stats2, bn.momentum,
+                               bn.eps, bn2.momentum, bn2.eps, dual)
+
+
 class BatchNormAct1d(nn.BatchNorm1d):
     """``nn.BatchNorm1d`` over [N, C] (+ReLU) on the same fused kernels: a
     row-major [N, C] tensor is NHWC with H = W = 1 (reference ConvNet's

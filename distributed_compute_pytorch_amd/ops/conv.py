@@ -33,8 +33,58 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t.contiguous()
 
 
+# conv weight -> (bf16 [R,kh,kw,Cin], bf16 [Cin,kh,kw,R] tap-flipped) produced by
+# the model's ConvWeightPrep for the forward in flight (one launch for every
+# conv instead of one cast launch each); empty outside such a forward.
+_PREPPED = {}
+
+
+class ConvWeightPrep:
+    """bf16 GEMM operands of a set of conv weights, all written by ONE kernel
+    launch per forward (``weight_prep_kernel``) into a persistent flat buffer.
+
+    ``with prep:`` runs the launch and publishes the views to the conv ops of
+    this module for the duration of the forward; the backward keeps its own
+    references (saved tensors) to the same persistent buffer, which the next
+    forward rewrites only after the optimizer changed the weights. Rebuilt
+    when a weight's storage moves. Capture-safe: fixed addresses, the launch is
+    part of the captured forward."""
+
+    def __init__(self, weights):
+        self.weights = list(weights)
+        self._key = None
+
+    def __enter__(self):
+        key = tuple(w.data_ptr() for w in self.weights)
+        if key != self._key:
+            self.table, self.tiles, self.wb, self.wt = _C.weight_prep_plan([w.detach() for w in self.weights])
+            self._key = key
+        _C.weight_prep_run(self.table, self.tiles)
+        for w, b, t in zip(self.weights, self.wb, self.wt):
+            _PREPPED[w] = (b, t)
+        return self
+
+    def __exit__(self, *exc):
+        _PREPPED.clear()
+        return False
+
+    @staticmethod
+    def eligible(w: torch.Tensor) -> bool:
+        return (w.is_cuda and w.dtype == torch.float32 and w.dim() == 4
+                and w.permute(0, 2, 3, 1).is_contiguous())
+
+
+def _prepped(weight: torch.Tensor):
+    return _PREPPED.get(weight) if _PREPPED else None
+
+
 def _w2d(weight: torch.Tensor):
-    """(bf16 [Cout, Cin], bf16 [Cin, Cout]): forward and dgrad B operands, one launch."""
+    """(bf16 [Cout, Cin], bf16 [Cin, Cout]): forward and dgrad B operands, one launch
+    (none when the model's ConvWeightPrep already produced them this forward)."""
+    p = _prepped(weight)
+    if p is not None:
+        b, t = p
+        return b.view(b.shape[0], -1), t.view(t.shape[0], -1)
     return _C.weight_bf16_t(weight)
 
 
@@ -249,15 +299,21 @@ class _ConvKxKGemmFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride, padding, stats, miopen_wgrad, miopen_fwd):
         ctx.set_materialize_grads(False)
-        w = weight.detach().to(torch.bfloat16)
+        pre = _prepped(weight)
+        if pre is not None:  # operands from the model's one-launch ConvWeightPrep
+            wf, wd = pre
+            w = wf.permute(0, 3, 1, 2)  # channels_last bf16 [Cout, Cin, kh, kw] view
+        else:
+            w = weight.detach().to(torch.bfloat16)
+            wf = wd = None
         kh, kw = w.shape[2], w.shape[3]
-        wd = None
         if miopen_fwd:  # the caller computes the output statistics itself
             y = _cl(F.conv2d(x, w, None, stride, padding))
             st = torch.empty(0, device=x.device, dtype=torch.float32)
         else:
-            # both bf16 operands (forward, flipped data-gradient) from one cast launch
-            wf, wd = _C.conv_weight_bf16(weight) if kh == kw else (w.permute(0, 2, 3, 1).contiguous(), None)
+            if wf is None:
+                # both bf16 operands (forward, flipped data-gradient) from one cast launch
+                wf, wd = _C.conv_weight_bf16(weight) if kh == kw else (w.permute(0, 2, 3, 1).contiguous(), None)
             y, st = _C.conv_fwd(x, wf, kh, kw, stride, padding, stats)
         ctx.save_for_backward(x, w, wd)
         ctx.cfg = (stride, padding, weight.dtype, miopen_wgrad)

@@ -87,8 +87,10 @@ def test_stem_dual_output_sums_gradients(cuda):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         c = fused_stem(x, conv, bn)
     c.backward((g1.float() + g2.float()).to(torch.bfloat16))
-    torch.testing.assert_close(conv.weight.grad, dw_dual, rtol=2e-2, atol=2e-3)
-    torch.testing.assert_close(bn.weight.grad, dg_dual, rtol=2e-2, atol=2e-3)
+    # the dual path sums g1 + g2 in fp32 inside the kernels; the reference sum is
+    # rounded to bf16 first: compare as relative norms
+    for got, ref in ((conv.weight.grad, dw_dual), (bn.weight.grad, dg_dual)):
+        assert float((got - ref).norm() / ref.norm()) < 2e-2
 
 
 def test_resnet_uses_fused_stem_and_tracks_module_path(cuda, monkeypatch):
