@@ -157,8 +157,17 @@ constexpr int nt_stages() { return BK == 64 ? 2 : 3; }
 // (stem_prep); k-stage kt (BK = 32) = tap row dy = kt, 8 tap columns x 4
 // channels = the 64 contiguous bytes at pixel (2ho + kt, 2wo): the row base
 // is computed once per tile and each stage advances by one padded image row.
+// Wave layout: BM / 64 waves along M (64 rows each) x nt_wn waves along N.
+// 128 x 128 and 128 x 64: 2 x 2 waves (64 x 64 / 64 x 32 per wave); 256 x 128:
+// 4 x 2 (8 waves, one workgroup per CU: each B tile feeds twice the rows);
+// 256 x 64: 4 x 1 (every wave 64 x 64: twice the MFMAs per fragment read of
+// the 128 x 64 tile for the Cout = 64 layers).
+template <int BM, int BN>
+constexpr int nt_wn() { return (BM == 256 && BN == 64) ? 1 : 2; }
+template <int BM, int BN>
+constexpr int nt_threads() { return 64 * (BM / 64) * nt_wn<BM, BN>(); }
 template <int BM, int BN, bool PRO, int EPI, bool GATHER, int BK, int AMODE = 0>
-__global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+__global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() <= 256 ? 2 : 1)) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                      uint16_t* __restrict__ C, int64_t M, int N, int K,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int relu,
@@ -180,23 +189,27 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
   constexpr int kNSnt = nt_stages<BK>();
   constexpr int RB = BK * 2;                                  // stage row bytes
   constexpr int CPR = BK / 8;                                 // 16-B chunks per row
+  constexpr int NT = nt_threads<BM, BN>();
+  constexpr int WNW = nt_wn<BM, BN>();
+  constexpr int WM = BM / 64, NW = WNW * WM;                 // waves along M, waves
   constexpr int SA = BM * RB, SB = BN * RB, STAGE = SA + SB;  // bytes
-  constexpr int NA = SA / 4096, NB = SB / 4096;                // glds per wave per stage (1 KiB each)
+  constexpr int NA = SA / (NW * 1024), NB = SB / (NW * 1024);  // glds per wave per stage (1 KiB each)
+  static_assert(NA * NW * 1024 == SA && NB * NW * 1024 == SB && NB >= 1, "tile / wave count mismatch");
   constexpr int G = NA + NB;
-  constexpr int FM = BM / 32, FN = BN / 32;  // 16-row fragments per wave (2×2 waves)
-  constexpr int WN = BN / 2;                 // wave tile columns
+  constexpr int WN = BN / WNW;               // wave tile columns
+  constexpr int FM = 4, FN = WN / 16;        // 16-row / 16-column fragments per wave (64 rows x WN)
   constexpr int CST = 32 * WN * 2;           // per-wave C staging: 32 rows × WN bf16
   constexpr int LPR = WN / 8;                // lanes per staged row (16 B each)
   constexpr int RPI = 64 / LPR;              // staged rows per store instruction
   constexpr int FS = 2 * (32 / RPI) * (EPI == 3 ? 4 : 1);  // global stores per wave per tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* cst_all = lds + kNSnt * STAGE;
-  float* pro = reinterpret_cast<float*>(cst_all + 4 * CST);  // [2][K] scale, shift (PRO)
+  float* pro = reinterpret_cast<float*>(cst_all + NW * CST);  // [2][K] scale, shift (PRO)
 
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WNW, wn = wave % WNW;
   // 1-D grid of P workgroups over tiles_m × tn tiles (tile v = m-tile v/tn,
   // n-tile v%tn). Workgroup id → tile id through the bijective XCD remap:
   // dispatch puts workgroup w on XCD w%8, the remap hands each XCD a
@@ -214,7 +227,7 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
   char* cst = cst_all + wave * CST;
 
   if (PRO) {
-    for (int i = t; i < K; i += kT) {
+    for (int i = t; i < K; i += NT) {
       pro[i] = scale[i];
       pro[K + i] = shift[i];
     }
@@ -357,7 +370,7 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
       bf16x8 xf[FM], wf[FN];
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const int r = wm * (BM / 2) + j * 16 + (lane & 15);
+        const int r = wm * 64 + j * 16 + (lane & 15);
         xf[j] = *reinterpret_cast<const bf16x8*>(sA + r * RB + 16 * (lch ^ nt_swzk<BK>(r)));
       }
 #pragma unroll
@@ -389,7 +402,7 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
       // writes into this wave's LDS staging → 16-B row-contiguous reads →
       // global stores covering whole 128-B lines (no cross-wave sync needed:
       // a wave's LDS ops execute in order).
-      const int64_t mt = static_cast<int64_t>(cv / tn) * BM + wm * (BM / 2);
+      const int64_t mt = static_cast<int64_t>(cv / tn) * BM + wm * 64;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -493,13 +506,19 @@ __global__ void __launch_bounds__(kT, 2) gemm_nt_kernel(const uint16_t* __restri
       for (int e = 0; e < 8; ++e) {
         const int c = wn * WN + lane * 8 + e;
         red[wm * BN + c] = ssum[e];
-        red[2 * BN + wm * BN + c] = ssq[e];
+        red[WM * BN + wm * BN + c] = ssq[e];
       }
     }
     __syncthreads();
     if (t < BN) {
-      atomicAdd(stats + n0 + t, red[t] + red[BN + t]);
-      atomicAdd(stats + N + n0 + t, red[2 * BN + t] + red[3 * BN + t]);
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        a += red[w * BN + t];
+        b += red[WM * BN + w * BN + t];
+      }
+      atomicAdd(stats + n0 + t, a);
+      atomicAdd(stats + N + n0 + t, b);
     }
   }
 }
@@ -884,31 +903,55 @@ inline int nt_bk() {
   return bk;
 }
 
-template <bool GATHER, int BK>
-void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+// Tile rows per workgroup: 256 (8 waves, 1 workgroup per CU) when the M
+// tiles alone fill the chip, else 128 (4 waves, 2 per CU). DCP_GEMM_BM=128 /
+// 256 forces one (A/B switch).
+inline int nt_bm(int64_t M, int tn, int BN, bool pro) {
+  static const int force = [] {
+    const char* v = getenv("DCP_GEMM_BM");
+    return v ? atoi(v) : 0;
+  }();
+  static const int n64 = [] {  // tile rows for Cout = 64 (256: 4 x 1 waves of 64 x 64)
+    const char* v = getenv("DCP_GEMM_N64_BM");
+    return v ? atoi(v) : 128;
+  }();
+  if (force == 128 || force == 256) return force;
+  if (BN == 64) return n64 == 256 ? 256 : 128;
+  // 8 x 64 x 64 waves measured slower than 2 x 128 x 128 workgroups on every
+  // non-prologue shape (profiles/r2_gemm_bm256.txt); the BN-prologue GEMMs
+  // (one prologue per 256 rows) gain
+  return pro && (M / 256) * tn >= 256 ? 256 : 128;
+}
+
+template <bool GATHER, int BK, int BM>
+void gemm_nt_launch_bm(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                        const float* shift, bool relu, float* stats, const ConvGeo& geo, const BnRedArgs* red,
-                       hipStream_t s, bool scatter2 = false, bool parity = false) {
+                       hipStream_t s, bool scatter2, bool parity) {
   const int BN = N % 128 == 0 ? 128 : 64;
-  constexpr int BM = 128;
   const int tiles_m = static_cast<int>((M + BM - 1) / BM);
   const int tn = N / BN;
-  // all tiles resident at once when they fit (2 workgroups per CU), else
-  // persistent over ≤ 512 workgroups (a multiple of tn, see the kernel)
+  // all tiles resident at once when they fit (2 workgroups of 128 rows or one
+  // of 256 per CU), else persistent over that many workgroups (a multiple of
+  // tn, see the kernel)
+  constexpr int kRes = BM == 128 ? 512 : 256;
   const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
-  int P = tiles <= 512 ? static_cast<int>(tiles) : (512 / tn) * tn;
+  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
   if (P < tn) P = tn;
   const dim3 grid(P);
   const bool pro = scale != nullptr;
   const bool st = stats != nullptr;
-  // ring + per-wave C staging (4 × 32 rows × BN/2) + BN coefficients
-  const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 + 4 * 32 * BN +
+  // ring + per-wave C staging (NW × 32 rows × wave columns) + BN coefficients
+  const int nw = (BM / 64) * (BN == 64 && BM == 256 ? 1 : 2);
+  const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 +
+                     static_cast<size_t>(nw) * 32 * (BN * 2 / (BM == 256 && BN == 64 ? 1 : 2)) +
                      (pro ? 8 * static_cast<size_t>(K) : 0) + (red ? 12 * static_cast<size_t>(BN) : 0);
+  const int NT = 64 * nw;
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
   const BnRedArgs bnr = red ? *red : BnRedArgs{};
 #define DCP_GNT(BN_, P_, S_)                                                                                     \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P_, S_, GATHER, BK>), grid, dim3(kT), lds, s, a, b, c, M, N, K,   \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P_, S_, GATHER, BK>), grid, dim3(NT), lds, s, a, b, c, M, N, K,   \
                      scale, shift, relu ? 1 : 0, stats, tiles_m, tn, geo, bnr)
 #define DCP_GNT2(BN_)                            \
   do {                                           \
@@ -944,6 +987,18 @@ void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, 
   else DCP_GNT2(64);
 #undef DCP_GNT2
 #undef DCP_GNT
+}
+
+template <bool GATHER, int BK>
+void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                       const float* shift, bool relu, float* stats, const ConvGeo& geo, const BnRedArgs* red,
+                       hipStream_t s, bool scatter2 = false, bool parity = false) {
+  const int BN = N % 128 == 0 ? 128 : 64;
+  const int tn = N / BN;
+  if (nt_bm(M, tn, BN, scale != nullptr) == 256)
+    gemm_nt_launch_bm<GATHER, BK, 256>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s, scatter2, parity);
+  else
+    gemm_nt_launch_bm<GATHER, BK, 128>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s, scatter2, parity);
 }
 
 template <bool GATHER>
@@ -1031,10 +1086,10 @@ void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W,
   auto b = static_cast<const uint16_t*>(wm);
   auto c = static_cast<uint16_t*>(y);
   if (stats)
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 1, false, BK, 1>), dim3(P), dim3(kT), lds, s, a, b, c, M, Cout,
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 1, false, BK, 1>), dim3(P), dim3(nt_threads<BM, BN>()), lds, s, a, b, c, M, Cout,
                        K, nullptr, nullptr, 0, stats, tiles_m, tn, geo, BnRedArgs{});
   else
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 0, false, BK, 1>), dim3(P), dim3(kT), lds, s, a, b, c, M, Cout,
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 0, false, BK, 1>), dim3(P), dim3(nt_threads<BM, BN>()), lds, s, a, b, c, M, Cout,
                        K, nullptr, nullptr, 0, nullptr, tiles_m, tn, geo, BnRedArgs{});
 }
 
