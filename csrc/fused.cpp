@@ -61,14 +61,23 @@ std::mutex g_arena_mu;
 std::map<std::pair<int, hipStream_t>, ZeroArena> g_arenas;
 constexpr int64_t kArenaFloats = int64_t(4) << 20;  // 16 MiB
 
+bool arena_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("DCP_ZERO_ARENA");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 at::Tensor zeroed_floats(int64_t n, const at::Tensor& like, hipStream_t st) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(st, &cap);
   const int64_t need = (n + 63) / 64 * 64;
-  if (cap != hipStreamCaptureStatusNone || need > kArenaFloats / 4) {
-    at::Tensor t = at::empty({need}, like.options().dtype(at::kFloat));
-    DCP_CHECK(hipMemsetAsync(t.data_ptr(), 0, sizeof(float) * need, st) == hipSuccess, "memset failed");
-    return t.narrow(0, 0, n);
+  if (cap != hipStreamCaptureStatusNone || need > kArenaFloats / 4 || !arena_enabled()) {
+    // a fill KERNEL, not hipMemsetAsync: a captured memset node is not ordered
+    // before the next kernel node on replays after the first on this ROCm
+    // (tools/graph_op_check.py: the GEMM's atomics land on un-zeroed sums)
+    return at::zeros({need}, like.options().dtype(at::kFloat)).narrow(0, 0, n);
   }
   std::lock_guard<std::mutex> g(g_arena_mu);
   ZeroArena& a = g_arenas[{static_cast<int>(like.get_device()), st}];
@@ -560,7 +569,7 @@ at::Tensor colsum(const at::Tensor& x, const c10::optional<at::Tensor>& accumula
                   accumulate_into->numel() == N && accumulate_into->device() == x.device(),
               "colsum: accumulate_into must be a contiguous fp32 [N] tensor on the same device");
   at::Tensor out = acc ? *accumulate_into : at::empty({N}, x.options().dtype(at::kFloat));
-  if (!acc) DCP_CHECK(hipMemsetAsync(out.data_ptr(), 0, sizeof(float) * N, s) == hipSuccess, "memset failed");
+  if (!acc) out.zero_();  // fill kernel: graph-capture safe (see zeroed_floats)
   kern::colsum_bf16(x.data_ptr(), out.data_ptr<float>(), M, static_cast<int>(N), s);
   return out;
 }
@@ -1137,7 +1146,18 @@ bool abort_capture(int64_t stream_ptr) {
   return true;
 }
 
+// hipStreamCaptureStatus of a raw stream handle (-1: the query failed)
+int stream_capture_status(int64_t stream_ptr) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(reinterpret_cast<hipStream_t>(stream_ptr), &st) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return static_cast<int>(st);
+}
+
 void bind(pybind11::module& m) {
+  m.def("stream_capture_status", &stream_capture_status);
   m.def("abort_capture", &abort_capture, "end a dangling stream capture; true if one was open");
   m.def("eval_metrics_", &eval_metrics_);
   m.def("maxpool_supported", &maxpool_supported);

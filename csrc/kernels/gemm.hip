@@ -561,7 +561,13 @@ __device__ __forceinline__ bf16x8 mask_rows(bf16x8 v, int valid, int lane) {
   return __builtin_bit_cast(bf16x8, s);
 }
 
-template <int BM, int BN, bool PRO, bool GATHER, int BK, int NSW = 0>
+// BMODE 1 (with GATHER) = the ResNet stem's weight gradient: B row m = the
+// receptive field of output pixel (n, ho, wo) in the zero-padded 4-channel
+// image (stem_prep, geo.H x geo.W): column c = (dy, 8 tap columns x 4
+// channels) = element c & 31 of the 64 contiguous bytes at padded pixel
+// (2ho + (c >> 5), 2wo) — the same K order as the stem forward GEMM (AMODE 1);
+// dy = 7 (columns 224-255) is computed and ignored.
+template <int BM, int BN, bool PRO, bool GATHER, int BK, int NSW = 0, int BMODE = 0>
 __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                         float* __restrict__ ws, int64_t M, int N1, int N2,
                                                         int64_t chunk, const float* __restrict__ scale,
@@ -640,12 +646,23 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
       if (GATHER) {
         // output pixel g_m[j] = (g_n, g_ho, g_wo), advanced by BK per stage
         // without divisions (they cost more VALU than the stage's MFMAs)
-        const int hi = g_ho[j] * geo.stride + gdy, wi = g_wo[j] * geo.stride + gdx;
-        const bool ok = g_m[j] < mz1 && static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
-                        static_cast<unsigned>(wi) < static_cast<unsigned>(geo.W);
-        const uint16_t* src = ok ? B + (static_cast<int64_t>(g_n[j] * geo.H + hi) * geo.W + wi) * N2 + j0 + lc * 8
-                                 : geo.zero + lc * 8;
-        glds16(src, base + SA + (wave * NB + j) * 1024);
+        if constexpr (BMODE == 1) {
+          // rows past the slice read pixel 0 (finite; their A rows are masked)
+          const int c = j0 + lc * 8;
+          const uint16_t* src =
+              g_m[j] < mz1
+                  ? B + (static_cast<int64_t>(g_n[j] * geo.H + 2 * g_ho[j] + (c >> 5)) * geo.W + 2 * g_wo[j]) * 4 +
+                        (c & 31)
+                  : B + (c & 31);
+          glds16(src, base + SA + (wave * NB + j) * 1024);
+        } else {
+          const int hi = g_ho[j] * geo.stride + gdy, wi = g_wo[j] * geo.stride + gdx;
+          const bool ok = g_m[j] < mz1 && static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
+                          static_cast<unsigned>(wi) < static_cast<unsigned>(geo.W);
+          const uint16_t* src = ok ? B + (static_cast<int64_t>(g_n[j] * geo.H + hi) * geo.W + wi) * N2 + j0 + lc * 8
+                                   : geo.zero + lc * 8;
+          glds16(src, base + SA + (wave * NB + j) * 1024);
+        }
         g_m[j] += BK;
         g_wo[j] += adv_w;
         g_ho[j] += adv_h;
@@ -1178,6 +1195,25 @@ void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, 
                      const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate) {
   ConvGeo geo{};
   wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s, accumulate);
+}
+
+void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int W, int Cout, float* ws,
+                     hipStream_t s) {
+  // D [Cout][256] fp32 = Σ_m dy[m][co] · field[m][k]; M = output pixels
+  const ConvGeo geo{H + 6, W + 8, H / 2, W / 2, 2, 0, 1, nullptr, 4};
+  const int64_t M = static_cast<int64_t>(N) * (H / 2) * (W / 2);
+  const WgradPlan p = wgrad_plan(M, Cout, kStemWgradCols, 1);
+  const dim3 grid(p.tiles, p.S, 1);
+  const int tj = kStemWgradCols / p.bn;
+  auto a = static_cast<const uint16_t*>(dy);
+  auto b = static_cast<const uint16_t*>(xp);
+  if (p.bm == 128)
+    hipLaunchKernelGGL((gemm_wgrad_kernel<128, 128, false, true, 64, 0, 1>), grid, dim3(kT), 0, s, a, b, ws, M, Cout,
+                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo);
+  else
+    hipLaunchKernelGGL((gemm_wgrad_kernel<64, 128, false, true, 64, 0, 1>), grid, dim3(kT), 0, s, a, b, ws, M, Cout,
+                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo);
+  slab_reduce(ws, D, static_cast<int64_t>(Cout) * kStemWgradCols / 4, p.S, s, false);
 }
 
 void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,

@@ -50,5 +50,12 @@ void mt_sumsq(TableView t, int64_t nchunks, DType d, float* out, hipStream_t s);
 // In-place scale of every tensor: x *= scale_dev[0] (device scalar).
 void mt_scale_by(TableView t, int64_t nchunks, DType d, const float* scale_dev, hipStream_t s);
 
+// dst[i] = src[i], i < n, with the words carried in KERNEL ARGUMENTS (src is
+// host memory read at launch / capture time; 256 words per launch). Used for
+// table uploads inside a HIP-graph capture: a captured memcpy node is not
+// reliably ordered before the kernel that reads the table, and a kernel
+// node's arguments are stored in the graph itself.
+void copy_words(const int64_t* src, int64_t* dst, int64_t n, hipStream_t s);
+
 }  // namespace kern
 }  // namespace dcp

@@ -459,6 +459,14 @@ __global__ void __launch_bounds__(kThreads) mt_scale_by_kernel(Tab tab, int64_t 
   });
 }
 
+constexpr int kArgWords = 256;
+struct ArgWords {
+  int64_t w[kArgWords];
+};
+__global__ void __launch_bounds__(kThreads) copy_words_kernel(ArgWords a, int64_t* __restrict__ dst, int n) {
+  if (static_cast<int>(threadIdx.x) < n) dst[threadIdx.x] = a.w[threadIdx.x];
+}
+
 inline dim3 grid_for(int64_t nchunks) {
   return dim3(static_cast<unsigned>(nchunks < kMaxGrid ? nchunks : kMaxGrid));
 }
@@ -524,6 +532,16 @@ void mt_scale_by(TableView t, int64_t nchunks, DType d, const float* scale_dev, 
   DCP_DISPATCH_DTYPE(d, D,
       hipLaunchKernelGGL((mt_scale_by_kernel<D>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks,
                          scale_dev));
+}
+
+void copy_words(const int64_t* src, int64_t* dst, int64_t n, hipStream_t s) {
+  static_assert(kArgWords <= kThreads, "one thread per word");
+  for (int64_t o = 0; o < n; o += kArgWords) {
+    ArgWords a{};
+    const int m = static_cast<int>(n - o < kArgWords ? n - o : kArgWords);
+    for (int i = 0; i < m; ++i) a.w[i] = src[o + i];
+    hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(kThreads), 0, s, a, dst + o, m);
+  }
 }
 
 }  // namespace kern

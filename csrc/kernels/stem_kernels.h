@@ -29,6 +29,14 @@ void stem_weight(const float* w, int cl, void* wm, int Cout, hipStream_t s);
 // += (Σy, Σy²) of the bf16 output. Cout % 64 == 0.
 void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W, int Cout, float* stats,
                    hipStream_t s);
+// Weight gradient of the stem conv: D [Cout][kStemWgradCols] fp32 =
+// Σ_pixels dy[pixel][co] · Xp receptive field (k = dy*32 + dx*4 + c, the
+// forward's K order padded to 8 tap rows). ws: gemm_wgrad_workspace(
+// N*(H/2)*(W/2), Cout, kStemWgradCols, 1) floats. Same split-M MFMA kernel as
+// the conv weight gradients (gemm.hip), deterministic.
+constexpr int kStemWgradCols = 256;
+void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int W, int Cout, float* ws,
+                     hipStream_t s);
 
 // Training BN (batch statistics from stats) + ReLU + max-pool 3x3 / 2 / pad 1
 // on y [N,H,W,C] (NHWC bf16): out [N,OH,OW,C], idx (uint8 window offset of

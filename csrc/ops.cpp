@@ -33,10 +33,8 @@ struct TableEntry {
   at::Tensor dev;
   int n;
   int64_t nchunks;
-  at::Tensor host;          // pinned source of the upload (undefined for capture-slab entries)
-  bool persistent = false;  // uploaded inside a HIP-graph capture: the
-                            // captured memcpy node re-reads `host` on every
-                            // replay, so neither may ever be freed
+  at::Tensor host;          // pinned source of the upload (undefined for capture-time entries)
+  bool persistent = false;  // read by a captured kernel on every replay: never evicted
 };
 
 std::mutex g_cache_mu;
@@ -55,23 +53,6 @@ void reap_graveyard() {
       ++it;
     }
   }
-}
-
-// Pinned host slab for tables built while a HIP graph is being captured.
-// Allocating pinned memory inside a capture is not allowed (torch's host
-// allocator queries events, which invalidates a global-mode capture), so the
-// slab is reserved outside capture on the first table build and carved
-// linearly afterwards; capture-time tables live forever anyway.
-constexpr size_t kSlabWords = size_t(1) << 20;  // 8 MiB
-int64_t* g_slab = nullptr;
-size_t g_slab_used = 0;
-
-void ensure_slab() {
-  if (g_slab) return;
-  void* p = nullptr;
-  DCP_CHECK(hipHostMalloc(&p, kSlabWords * sizeof(int64_t), hipHostMallocDefault) == hipSuccess,
-            "pinned table slab allocation failed");
-  g_slab = static_cast<int64_t*>(p);
 }
 
 // lists[d][i]: tensor i of list d. All lists must have the same length; rows
@@ -114,23 +95,19 @@ TableEntry get_table(const std::vector<const TensorList*>& lists) {
     }
   }
   at::Tensor host;
-  void* src = nullptr;
-  if (capturing) {
-    DCP_CHECK(g_slab != nullptr && g_slab_used + words.size() <= kSlabWords,
-              "multi-tensor table built inside a HIP-graph capture without slab space: run the step eagerly "
-              "(warmup) before capturing");
-    src = g_slab + g_slab_used;
-    g_slab_used += (words.size() + 7) & ~size_t(7);
-  } else {
-    ensure_slab();
-    host = at::empty({static_cast<int64_t>(words.size())}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
-    src = host.data_ptr();
-  }
-  std::memcpy(src, words.data(), words.size() * sizeof(int64_t));
   at::Tensor d = at::empty({static_cast<int64_t>(words.size())}, at::TensorOptions().dtype(at::kLong).device(dev));
-  DCP_CHECK(hipMemcpyAsync(d.data_ptr(), src, words.size() * sizeof(int64_t), hipMemcpyHostToDevice, st) ==
-                hipSuccess,
-            "table upload failed");
+  if (capturing) {
+    // copy kernels carrying the words as arguments (stored in the graph): a
+    // captured memcpy node is not reliably ordered before the kernel reading
+    // the table on replays (the defect behind fused.cpp zeroed_floats)
+    kern::copy_words(words.data(), d.data_ptr<int64_t>(), static_cast<int64_t>(words.size()), st);
+  } else {
+    host = at::empty({static_cast<int64_t>(words.size())}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+    std::memcpy(host.data_ptr(), words.data(), words.size() * sizeof(int64_t));
+    DCP_CHECK(hipMemcpyAsync(d.data_ptr(), host.data_ptr(), words.size() * sizeof(int64_t), hipMemcpyHostToDevice,
+                             st) == hipSuccess,
+              "table upload failed");
+  }
   TableEntry e{std::move(words), d, n, chunks, host, capturing};
   g_cache.push_front(std::move(e));
   // evict the least recently used non-persistent entry (never while capturing:

@@ -5,6 +5,7 @@
 #include <torch/extension.h>
 
 #include "common.h"
+#include "kernels/gemm_kernels.h"
 #include "kernels/stem_kernels.h"
 
 namespace dcp {
@@ -80,6 +81,27 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& xp, const at::Tensor& wm, int
   return {y, st};
 }
 
+// weight gradient: dy [N,Cout,H/2,W/2] bf16 channels_last, xp from stem_prep
+// -> dW fp32 [Cout,3,7,7] (contiguous)
+at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& xp, int64_t H, int64_t W) {
+  check_act(dy, "stem_conv_wgrad(dy)");
+  DCP_CHECK(xp.is_cuda() && xp.scalar_type() == at::kBFloat16 && xp.dim() == 4 && xp.size(3) == 4 &&
+                xp.size(1) == kern::stem_hp(static_cast<int>(H)) && xp.size(2) == kern::stem_wp(static_cast<int>(W)) &&
+                xp.is_contiguous() && xp.size(0) == dy.size(0),
+            "stem_conv_wgrad: xp must come from stem_prep for this H, W");
+  const int64_t N = dy.size(0), Cout = dy.size(1);
+  DCP_CHECK(dy.size(2) == H / 2 && dy.size(3) == W / 2 && Cout % 64 == 0, "stem_conv_wgrad: dy shape mismatch");
+  c10::hip::HIPGuard g(dy.device().index());
+  const int64_t M = N * (H / 2) * (W / 2);
+  auto fo = dy.options().dtype(at::kFloat);
+  at::Tensor ws = at::empty({kern::gemm_wgrad_workspace(M, static_cast<int>(Cout), kern::kStemWgradCols, 1)}, fo);
+  at::Tensor D = at::empty({Cout, kern::kStemWgradCols}, fo);
+  kern::stem_conv_wgrad(dy.data_ptr(), xp.data_ptr(), D.data_ptr<float>(), static_cast<int>(N), static_cast<int>(H),
+                        static_cast<int>(W), static_cast<int>(Cout), ws.data_ptr<float>(), stream_of(dy));
+  // D[co][dy*32 + dx*4 + c] -> dW[co][c][dy][dx]
+  return D.view({Cout, 8, 8, 4}).slice(1, 0, 7).slice(2, 0, 7).slice(3, 0, 3).permute({0, 3, 1, 2}).contiguous();
+}
+
 // training BN + ReLU + max-pool 3x3/2/1: (out, idx, xsel, mean, invstd)
 std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& y, const at::Tensor& stats, const at::Tensor& gamma,
                                     const at::Tensor& beta, const c10::optional<at::Tensor>& running_mean,
@@ -152,6 +174,7 @@ void bind(pybind11::module& m) {
   m.def("stem_prep", &prep, py::arg("x"), py::arg("want_x3"));
   m.def("stem_weight", &weight);
   m.def("stem_conv_fwd", &conv_fwd, py::arg("xp"), py::arg("wm"), py::arg("H"), py::arg("W"));
+  m.def("stem_conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("xp"), py::arg("H"), py::arg("W"));
   m.def("stem_bn_pool_fwd", &bn_pool_fwd, py::arg("y"), py::arg("stats"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("momentum"),
         py::arg("eps"));

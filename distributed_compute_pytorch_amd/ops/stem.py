@@ -7,8 +7,11 @@ NHWC copy, the conv runs as an MFMA implicit GEMM whose epilogue accumulates
 the BN sums, and ONE pass applies BN + ReLU + max-pool (uint8 arg-max, and the
 BN input at the arg-max for the backward). Backward: the BN reduction runs over
 the 4x smaller pooled map, ONE gather pass writes the conv-output gradient,
-and the weight gradient is the vendor convolution-backward (MIOpen) on the
-bf16 NHWC image copy made by the same prep launch.
+and the weight gradient is the split-M MFMA weight-gradient GEMM reading the
+same padded image (receptive fields gathered straight from Xp, no im2col), so
+no vendor kernel runs in the stem — which also keeps it HIP-graph safe (the
+MIOpen backward-weights solvers for stride-2 convs are not: their output
+zeroing is not captured, tools/graph_nan_debug.py).
 
 Same parameters / buffers as ``conv1`` + ``bn1`` (state_dict unchanged);
 the running statistics and ``num_batches_tracked`` update like
@@ -25,21 +28,21 @@ class _StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, running_mean, running_var, nbt, momentum, eps, dual):
         H, W = x.shape[2], x.shape[3]
-        xp, x3 = _C.stem_prep(x, True)
+        xp, _ = _C.stem_prep(x, False)
         wm = _C.stem_weight(weight)
         y, st = _C.stem_conv_fwd(xp, wm, H, W)
-        del xp
         out, idx, xsel, mean, invstd = _C.stem_bn_pool_fwd(y, st, gamma, beta, running_mean, running_var, nbt,
                                                            float(momentum), float(eps))
-        ctx.save_for_backward(x3, weight, y, idx, xsel, mean, invstd, gamma)
+        ctx.save_for_backward(xp, weight, y, idx, xsel, mean, invstd, gamma)
         ctx.dual = dual
+        ctx.hw = (H, W)
         if dual:
             return out, out.view_as(out)
         return out
 
     @staticmethod
     def backward(ctx, gp, gp2=None):
-        x3, weight, y, idx, xsel, mean, invstd, gamma = ctx.saved_tensors
+        xp, weight, y, idx, xsel, mean, invstd, gamma = ctx.saved_tensors
         if gp is None:
             gp, gp2 = gp2, None
         gp = gp.to(torch.bfloat16)
@@ -48,9 +51,9 @@ class _StemFn(torch.autograd.Function):
         dy, dg, db = _C.stem_bn_pool_bwd(gp, gp2, idx, xsel, y, mean, invstd, gamma)
         dw = None
         if ctx.needs_input_grad[1]:
-            w16 = weight.detach().to(torch.bfloat16)
-            dw = torch.ops.aten.convolution_backward(dy, x3, w16, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
-                                                     [False, True, False])[1].to(weight.dtype)
+            dw = _C.stem_conv_wgrad(dy, xp, *ctx.hw)
+            if weight.is_contiguous(memory_format=torch.channels_last) and not weight.is_contiguous():
+                dw = dw.contiguous(memory_format=torch.channels_last)
         return None, dw, dg, db, None, None, None, None, None, None
 
 

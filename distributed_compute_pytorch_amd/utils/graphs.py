@@ -10,8 +10,11 @@ Everything the step touches is capture-safe by construction:
 * the Reducer's pack launches, RCCL collectives (RCCL supports capture) and
   comm-stream event edges are recorded into the graph; the watchdog skips
   captured work;
-* multi-tensor kernel tables uploaded during capture are kept alive forever
-  (the captured memcpy node re-reads them on each replay);
+* no memset / memcpy nodes: on this ROCm a captured hipMemsetAsync /
+  hipMemcpyAsync node is not reliably ordered before the next kernel node on
+  replays after the first (tools/graph_op_check.py), so zeroed accumulators
+  come from fill kernels under capture and multi-tensor kernel tables are
+  uploaded once, outside the graph, and kept alive for good;
 * the fused optimizers read hyper-parameters at capture time — changing the
   LR after capture requires re-capturing (``CapturedStep.recapture``).
 

@@ -1,4 +1,6 @@
-"""Whole-step HIP-graph capture: replays must equal eager execution."""
+"""Whole-step HIP-graph capture: replays must equal eager execution, and
+captured ops must not depend on state outside the graph (each replay of a
+captured op equals the eager op)."""
 import copy
 import os
 
@@ -9,10 +11,13 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.xfail(reason="open item (NOTES §9): after an in-place state sync the replayed SGD step's loss "
-                          "differs from eager by a few % from run to run; fwd+bwd replays match eager "
-                          "(tools/graph_numerics.py, test below); the bench does not use graphs", strict=False)
-@pytest.mark.parametrize("gemm", [False, True])
+# gemm=False runs MIOpen's stride-2 3x3 backward-weights, whose replays go
+# non-finite (a stock-torch ResNet shows the same, tools/graph_nan_debug.py "r18
+# plain"): its output zeroing is a captured memset node, which this ROCm does not
+# order before the next kernel on replays after the first. Our kernels never
+# capture memset / memcpy nodes (fused.cpp zeroed_floats, ops.cpp get_table).
+@pytest.mark.parametrize("gemm", [pytest.param(False, marks=pytest.mark.xfail(
+    reason="vendor: MIOpen stride-2 wgrad is not HIP-graph replay safe on this ROCm", strict=False)), True])
 def test_captured_step_matches_eager(cuda, gemm):
     import distributed_compute_pytorch_amd as dcp
     from distributed_compute_pytorch_amd.distributed.launch import free_port
@@ -174,3 +179,66 @@ def test_captured_fwd_bwd_matches_eager(cuda, gemm):
         assert err < 3 * noise + 0.02 * float(ge.norm()), (err, noise, float(ge.norm()))
     finally:
         dcp.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("op", ["conv1x1", "conv_fwd", "bn_act_fwd", "colsum", "sgd_table"])
+def test_captured_op_replays_equal_eager(cuda, op):
+    """Every replay (not just the first) of a captured op equals eager: the
+    zeroed accumulators and multi-tensor tables are built by kernels inside the
+    graph, never by memset / memcpy nodes (which this ROCm does not order
+    before the next kernel node on later replays)."""
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    torch.manual_seed(0)
+    cl = torch.channels_last
+    x = torch.randn(8, 64, 16, 16, device=cuda).to(torch.bfloat16).contiguous(memory_format=cl)
+    w1 = torch.randn(64, 64, device=cuda).to(torch.bfloat16)
+    w3 = torch.randn(64, 3, 3, 64, device=cuda).to(torch.bfloat16)
+    g = torch.rand(64, device=cuda) + 0.5
+    b = torch.randn(64, device=cuda)
+    params = [torch.randn(n, device=cuda) for n in (3000, 17, 40000)]
+    for p in params:
+        p.grad = torch.randn_like(p)
+    opt = dcp.optim.SGD(params, lr=0.1, momentum=0.9) if op == "sgd_table" else None
+    fns = {
+        "conv1x1": lambda: _C.conv1x1_fwd(x, w1, None, None, False, True),
+        "conv_fwd": lambda: _C.conv_fwd(x, w3, 3, 3, 1, 1, True),
+        "bn_act_fwd": lambda: _C.bn_act_fwd(x, g, b, None, None, None, True, 0.1, 1e-5, True, None, None)[:3],
+        "colsum": lambda: [_C.colsum(x.permute(0, 2, 3, 1).reshape(-1, 64))],
+    }
+    if op == "sgd_table":
+        opt.step()  # eager step creates the momentum buffers
+        def fn():
+            opt.step()
+            return list(params)
+    else:
+        fn = fns[op]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr, stream=s, capture_error_mode="thread_local"):
+        out = fn()
+    for i in range(3):
+        if op == "sgd_table":
+            # eager reference of one more step from the current state
+            ref_p = [p.detach().clone() for p in params]
+            ref_buf = [opt.state[p]["momentum_buffer"].clone() for p in params]
+            for rp, rb, p in zip(ref_p, ref_buf, params):
+                rb.mul_(0.9).add_(p.grad)
+                rp.add_(rb, alpha=-0.1)
+            gr.replay()
+            torch.cuda.synchronize()
+            for rp, p in zip(ref_p, params):
+                torch.testing.assert_close(p, rp, rtol=1e-5, atol=1e-5)
+        else:
+            ref = [t.float().clone() for t in fn() if torch.is_tensor(t) and t.numel()]
+            gr.replay()
+            torch.cuda.synchronize()
+            got = [t.float() for t in out if torch.is_tensor(t) and t.numel()]
+            for a, r in zip(got, ref):
+                torch.testing.assert_close(a, r, rtol=2e-3, atol=2e-3 * float(r.abs().max()) + 1e-6)
