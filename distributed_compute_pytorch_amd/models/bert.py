@@ -20,6 +20,7 @@ from torch.nn import functional as F
 
 from ..ops.attention import attn_supported, flash_attn
 from ..ops.cross_entropy import fused_cross_entropy
+from ..ops.embedding import FusedEmbedding
 from ..ops.linear import FusedLinear
 from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
@@ -104,9 +105,9 @@ class BertForPreTraining(nn.Module):
     def __init__(self, cfg: BertConfig = BertConfig()):
         super().__init__()
         self.cfg = cfg
-        self.word_embeddings = nn.Embedding(cfg.vocab_size, cfg.hidden)
-        self.position_embeddings = nn.Embedding(cfg.max_position, cfg.hidden)
-        self.token_type_embeddings = nn.Embedding(cfg.type_vocab, cfg.hidden)
+        self.word_embeddings = (FusedEmbedding if cfg.fused else nn.Embedding)(cfg.vocab_size, cfg.hidden)
+        self.position_embeddings = (FusedEmbedding if cfg.fused else nn.Embedding)(cfg.max_position, cfg.hidden)
+        self.token_type_embeddings = (FusedEmbedding if cfg.fused else nn.Embedding)(cfg.type_vocab, cfg.hidden)
         self.emb_ln = _ln(cfg, cfg.hidden)
         self.emb_drop = nn.Dropout(cfg.dropout)
         self.layers = nn.ModuleList([BertLayer(cfg) for _ in range(cfg.layers)])

@@ -22,6 +22,7 @@ from torch.nn import functional as F
 
 from ..ops.attention import attn_supported, flash_attn_qkv
 from ..ops.cross_entropy import fused_cross_entropy
+from ..ops.embedding import FusedEmbedding
 from ..ops.linear import FusedLinear
 from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
@@ -106,8 +107,8 @@ class GPT2(nn.Module):
     def __init__(self, cfg: GPT2Config = GPT2Config()):
         super().__init__()
         self.cfg = cfg
-        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
-        self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
+        self.wte = (FusedEmbedding if cfg.fused else nn.Embedding)(cfg.vocab_size, cfg.n_embd)
+        self.wpe = (FusedEmbedding if cfg.fused else nn.Embedding)(cfg.n_positions, cfg.n_embd)
         self.drop = nn.Dropout(cfg.dropout)
         self.h = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
         self.ln_f = _ln(cfg, cfg.n_embd)

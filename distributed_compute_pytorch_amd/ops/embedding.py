@@ -1,0 +1,51 @@
+"""Embedding lookup whose backward is HIP-graph capturable.
+
+ATen's dense embedding backward on ROCm sorts the indices and sizes its
+segment pass from a device->host read of the unique-index count (a rocPRIM
+partition): inside a captured step that count is frozen at capture time, so a
+replay with other token ids indexes out of bounds. Here the weight gradient is
+one fp32 ``index_add_`` scatter (atomics, no host read, no data-dependent
+sizes): same values up to fp32 summation order, capture-safe, and one kernel
+instead of sort + segment passes.
+
+Parity: ``torch.nn.Embedding`` (no padding_idx / max_norm / sparse) — same
+parameter and state_dict key.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, weight):
+        ctx.save_for_backward(idx)
+        ctx.shape = weight.shape
+        ctx.wdtype = weight.dtype
+        return F.embedding(idx, weight)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        V, D = ctx.shape
+        gw = torch.zeros(V, D, device=g.device, dtype=torch.float32)
+        gw.index_add_(0, idx.reshape(-1), g.reshape(-1, D).float())
+        return None, gw if ctx.wdtype == torch.float32 else gw.to(ctx.wdtype)
+
+
+def embedding(idx: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    if weight.requires_grad and torch.is_grad_enabled():
+        return _EmbeddingFn.apply(idx, weight)
+    return F.embedding(idx, weight)
+
+
+class FusedEmbedding(nn.Embedding):
+    """``nn.Embedding`` with the capture-safe scatter backward."""
+
+    def forward(self, idx: torch.Tensor) -> torch.Tensor:
+        if (self.padding_idx is None and self.max_norm is None and not self.sparse
+                and not self.scale_grad_by_freq):
+            return embedding(idx, self.weight)
+        return super().forward(idx)

@@ -242,3 +242,49 @@ def test_captured_op_replays_equal_eager(cuda, op):
             got = [t.float() for t in out if torch.is_tensor(t) and t.numel()]
             for a, r in zip(got, ref):
                 torch.testing.assert_close(a, r, rtol=2e-3, atol=2e-3 * float(r.abs().max()) + 1e-6)
+
+
+def test_captured_gpt2_step_matches_eager(cuda):
+    """GPT-2 (fused linears / LN / attention / vocab xent, capture-safe embedding
+    backward, capturable AdamW with device-side step counts): 4 replays of the
+    captured step track 4 eager steps from the same start."""
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_compute_pytorch_amd.utils.graphs import CapturedStep, capture_stream
+
+    torch.manual_seed(0)
+    cfg = GPT2Config(vocab_size=512, n_positions=128, n_embd=128, n_layer=2, n_head=2, dropout=0.0)
+    base = GPT2(cfg).to(cuda)
+    m_e, m_g = copy.deepcopy(base), copy.deepcopy(base)
+    o_e = dcp.optim.AdamW(m_e.parameters(), lr=1e-3, weight_decay=0.1, capturable=True)
+    s = capture_stream()
+    with torch.cuda.stream(s):
+        o_g = dcp.optim.AdamW(m_g.parameters(), lr=1e-3, weight_decay=0.1, capturable=True)
+    g = torch.Generator().manual_seed(1)
+    batches = []
+    for _ in range(6):
+        t = torch.randint(0, 512, (4, 129), generator=g)
+        batches.append((t[:, :-1].contiguous().to(cuda), t[:, 1:].contiguous().to(cuda)))
+
+    def make(m, opt):
+        def run(x, y):
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(x, y)
+            loss.backward()
+            opt.step()
+            return loss
+        return run
+
+    run_e, run_g = make(m_e, o_e), make(m_g, o_g)
+    for _ in range(2):
+        run_e(*batches[0])
+    cap = CapturedStep(run_g, [t.clone() for t in batches[0]], warmup=2, stream=s)
+    for b in batches[1:5]:
+        le = float(run_e(*b).detach())
+        lg = float(cap(*b).detach())
+        assert abs(le - lg) < 2e-2 * max(1.0, abs(le)), (le, lg)
+    pe = torch.cat([p.detach().float().reshape(-1) for p in m_e.parameters()])
+    pg = torch.cat([p.detach().float().reshape(-1) for p in m_g.parameters()])
+    assert bool(torch.isfinite(pg).all())
+    assert float((pe - pg).norm() / pe.norm()) < 1e-2
