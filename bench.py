@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--grad-as-view", type=int, default=1)
     ap.add_argument("--benchmark-cudnn", type=int, default=1)
     ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a HIP graph")
+    ap.add_argument("--backend", choices=["rccl", "gloo"], default="rccl",
+                    help="gloo: the reference's literal backend (main.py:50) — GPU tensors staged through the "
+                         "host; ours = the C++ host communicator, stock = torch's gloo")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--comm-timing", type=int, default=0,
                     help="record per-bucket device comm time + exposed (un-overlapped) comm ms in the JSON")
@@ -99,7 +102,7 @@ def _self_launch(a) -> int:
     import importlib.util
 
     n = torch.cuda.device_count()
-    if n < a.gpus:
+    if n < a.gpus and a.backend != "gloo":
         log(f"[bench] --gpus {a.gpus} requested but only {n} GPU(s) are visible; refusing to oversubscribe "
             f"(RCCL needs one device per rank)")
         return 2
@@ -144,6 +147,9 @@ def main():
         os.environ["DCP_COMM_TIMING"] = "1"  # read by the communicator / Reducer at construction
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
+    if a.backend == "gloo":
+        # host-staged collectives: ranks may share a GPU (reference-literal runs on a small box)
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     torch.backends.cudnn.benchmark = bool(a.benchmark_cudnn)
@@ -170,13 +176,16 @@ def main():
     # nodes are bound to the stream current at their creation)
     stream_ctx = (lambda: torch.cuda.stream(capture_stream())) if a.graph else contextlib.nullcontext
     if ours:
-        dcp.distributed.init_process_group("rccl", device_id=local)
+        dcp.distributed.init_process_group(a.backend, device_id=local if a.backend == "rccl" else None)
         barrier = dcp.distributed.barrier
         all_reduce, MAX = dcp.distributed.all_reduce, dcp.distributed.ReduceOp.MAX
     else:
         import torch.distributed as tdist
 
-        tdist.init_process_group("nccl", device_id=dev)
+        if a.backend == "gloo":
+            tdist.init_process_group("gloo")
+        else:
+            tdist.init_process_group("nccl", device_id=dev)
         barrier = tdist.barrier
         all_reduce, MAX = tdist.all_reduce, tdist.ReduceOp.MAX
 
@@ -245,6 +254,7 @@ def main():
                 "optimizer": type(opt).__name__,
                 "comm_dtype": a.comm_dtype,
                 "hip_graph": bool(a.graph),
+                "backend": a.backend,
             }
             if a.model == "resnet50":
                 cfg.update(mfma_1x1_gemm=bool(a.gemm) and fused, image_size=224, channels_last=bool(a.channels_last))
