@@ -572,7 +572,7 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
                                                         float* __restrict__ ws, int64_t M, int N1, int N2,
                                                         int64_t chunk, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int relu, int tiles_j,
-                                                        ConvGeo geo) {
+                                                        ConvGeo geo, int ntiles, int ntaps, int order) {
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
   // BK m-rows per stage: 64 on a 2-deep ring (half the barriers per MFMA) or
   // 32 on the 4-deep ring; both ≤ 64 KB of LDS (2 blocks per CU)
@@ -588,9 +588,32 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wi = wave >> 1, wj = wave & 1;
-  const int ti = blockIdx.x / tiles_j, tj = blockIdx.x % tiles_j;
+  // 1-D grid over (slab, tile, tap). order 1: XCD-aware — dispatch puts
+  // workgroup w on XCD w % 8; the bijective remap gives each XCD a contiguous
+  // id range with the taps fastest, so the taps (and tiles) of one M slab run
+  // together on one XCD and read its dY / X rows once from HBM into that L2
+  // (tap-slowest order re-streamed every slab once per tap). order 0: tile
+  // fastest, then slab, then tap (the former 3-D grid).
+  int bx, by, bz;
+  {
+    const int nwg = static_cast<int>(gridDim.x), wid = static_cast<int>(blockIdx.x);
+    if (order == 1) {
+      const int xcd = wid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+      const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
+      bz = lin % ntaps;
+      const int rest = lin / ntaps;
+      bx = rest % ntiles;
+      by = rest / ntiles;
+    } else {
+      bx = wid % ntiles;
+      const int rest = wid / ntiles;
+      by = rest % (nwg / (ntiles * ntaps));
+      bz = rest / (nwg / (ntiles * ntaps));
+    }
+  }
+  const int ti = bx / tiles_j, tj = bx % tiles_j;
   const int i0 = ti * BM, j0 = tj * BN;
-  const int64_t mz0 = static_cast<int64_t>(blockIdx.y) * chunk;
+  const int64_t mz0 = static_cast<int64_t>(by) * chunk;
   const int64_t mz1 = min(M, mz0 + chunk);
   const int T = mz0 < mz1 ? static_cast<int>((mz1 - mz0 + BK - 1) / BK) : 0;
 
@@ -609,8 +632,8 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
   }
 
   int g_m[NB], g_n[NB], g_ho[NB], g_wo[NB];  // GATHER: output pixel of each B row at the next issue
-  const int gdy = static_cast<int>(blockIdx.z) / geo.kw - geo.pad;
-  const int gdx = static_cast<int>(blockIdx.z) % geo.kw - geo.pad;
+  const int gdy = bz / geo.kw - geo.pad;
+  const int gdx = bz % geo.kw - geo.pad;
   const int adv_h = GATHER ? BK / geo.Wo : 0, adv_w = GATHER ? BK % geo.Wo : 0;
   if (GATHER) {
 #pragma unroll
@@ -728,9 +751,8 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
-  // slab z holds D in its final [N1][taps][N2] layout (taps = gridDim.z)
-  const int ntaps = static_cast<int>(gridDim.z);
-  float* out = ws + static_cast<int64_t>(blockIdx.y) * N1 * ntaps * N2 + static_cast<int64_t>(blockIdx.z) * N2;
+  // slab `by` holds D in its final [N1][taps][N2] layout
+  float* out = ws + static_cast<int64_t>(by) * N1 * ntaps * N2 + static_cast<int64_t>(bz) * N2;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -884,6 +906,15 @@ struct WgradPlan {
   int bm, bn, tiles, S;
   int64_t chunk;
 };
+
+// wgrad grid order (DCP_WGRAD_ORDER): 1 = XCD-aware, taps fastest (default), 0 = tap slowest
+inline int wgrad_order() {
+  static const int o = [] {
+    const char* v = getenv("DCP_WGRAD_ORDER");
+    return v ? atoi(v) : 1;
+  }();
+  return o;
+}
 
 WgradPlan wgrad_plan(int64_t M, int N1, int N2, int taps = 1) {
   WgradPlan p;
@@ -1144,7 +1175,8 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
                   const float* shift, bool relu, float* ws, int taps, const ConvGeo& geo, hipStream_t s,
                   bool acc = false) {
   const WgradPlan p = wgrad_plan(M, N1, N2, taps);
-  const dim3 grid(p.tiles, p.S, taps);
+  const dim3 grid(p.tiles * p.S * taps);
+  const int order = wgrad_order();
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   const bool pro = scale != nullptr;
@@ -1163,13 +1195,13 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   do {                                                                                                             \
     if (cfg == 0 && !P)                                                                                            \
       hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 64>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,    \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                            \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order);                     \
     else if (cfg == 1)                                                                                             \
       hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32, 2>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                            \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order);                     \
     else                                                                                                           \
       hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,    \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo);                                            \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order);                     \
   } while (0)
 #define DCP_GWG2(BM_, BN_)                      \
   do {                                          \
@@ -1203,16 +1235,17 @@ void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int
   const ConvGeo geo{H + 6, W + 8, H / 2, W / 2, 2, 0, 1, nullptr, 4};
   const int64_t M = static_cast<int64_t>(N) * (H / 2) * (W / 2);
   const WgradPlan p = wgrad_plan(M, Cout, kStemWgradCols, 1);
-  const dim3 grid(p.tiles, p.S, 1);
+  const dim3 grid(p.tiles * p.S);
+  const int order = wgrad_order();
   const int tj = kStemWgradCols / p.bn;
   auto a = static_cast<const uint16_t*>(dy);
   auto b = static_cast<const uint16_t*>(xp);
   if (p.bm == 128)
     hipLaunchKernelGGL((gemm_wgrad_kernel<128, 128, false, true, 64, 0, 1>), grid, dim3(kT), 0, s, a, b, ws, M, Cout,
-                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo);
+                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order);
   else
     hipLaunchKernelGGL((gemm_wgrad_kernel<64, 128, false, true, 64, 0, 1>), grid, dim3(kT), 0, s, a, b, ws, M, Cout,
-                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo);
+                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order);
   slab_reduce(ws, D, static_cast<int64_t>(Cout) * kStemWgradCols / 4, p.S, s, false);
 }
 
