@@ -567,12 +567,19 @@ __device__ __forceinline__ bf16x8 mask_rows(bf16x8 v, int valid, int lane) {
 // channels) = element c & 31 of the 64 contiguous bytes at padded pixel
 // (2ho + (c >> 5), 2wo) — the same K order as the stem forward GEMM (AMODE 1);
 // dy = 7 (columns 224-255) is computed and ignored.
+// BMODE 2 (with GATHER) = multi-tap: the B columns are (tap, input channel)
+// pairs of a kxk conv, column c = tap * N2 + channel, so one tile of BN
+// columns spans BN / N2 taps (N2 = 64: two taps per 128-wide tile) and every
+// dY row fetched feeds twice the MFMAs; the lane's tap is fixed for the whole
+// block (its column never changes), columns past ldo (= taps * N2) are
+// zero-filled and not stored. The grid then has no tap dimension.
+// ldo: row stride of D in floats (taps * N2) — also where D's columns end.
 template <int BM, int BN, bool PRO, bool GATHER, int BK, int NSW = 0, int BMODE = 0>
 __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                         float* __restrict__ ws, int64_t M, int N1, int N2,
                                                         int64_t chunk, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int relu, int tiles_j,
-                                                        ConvGeo geo, int ntiles, int ntaps, int order) {
+                                                        ConvGeo geo, int ntiles, int ntaps, int order, int ldo) {
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
   // BK m-rows per stage: 64 on a 2-deep ring (half the barriers per MFMA) or
   // 32 on the 4-deep ring; both ≤ 64 KB of LDS (2 blocks per CU)
@@ -635,6 +642,19 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
   const int gdy = bz / geo.kw - geo.pad;
   const int gdx = bz % geo.kw - geo.pad;
   const int adv_h = GATHER ? BK / geo.Wo : 0, adv_w = GATHER ? BK % geo.Wo : 0;
+  int mt_dy[BMODE == 2 ? NB : 1], mt_dx[BMODE == 2 ? NB : 1], mt_c[BMODE == 2 ? NB : 1];  // BMODE 2: lane's tap / channel
+  if constexpr (BMODE == 2) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int p = (wave * NB + j) * 64 + lane;
+      const int r = p / BCPR, pc = p % BCPR;
+      const int cg = j0 + 8 * (2 * ((pc >> 1) ^ tr_f<BN>(r)) + (pc & 1));
+      const int tap = cg / N2;
+      mt_c[j] = cg < ldo ? cg - tap * N2 : -1;  // -1: past the last tap, zero row
+      mt_dy[j] = tap / geo.kw - geo.pad;
+      mt_dx[j] = tap % geo.kw - geo.pad;
+    }
+  }
   if (GATHER) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -677,6 +697,13 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
                   ? B + (static_cast<int64_t>(g_n[j] * geo.H + 2 * g_ho[j] + (c >> 5)) * geo.W + 2 * g_wo[j]) * 4 +
                         (c & 31)
                   : B + (c & 31);
+          glds16(src, base + SA + (wave * NB + j) * 1024);
+        } else if constexpr (BMODE == 2) {
+          const int hi = g_ho[j] * geo.stride + mt_dy[j], wi = g_wo[j] * geo.stride + mt_dx[j];
+          const bool ok = g_m[j] < mz1 && mt_c[j] >= 0 && static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
+                          static_cast<unsigned>(wi) < static_cast<unsigned>(geo.W);
+          const uint16_t* src = ok ? B + (static_cast<int64_t>(g_n[j] * geo.H + hi) * geo.W + wi) * N2 + mt_c[j]
+                                   : geo.zero + lc * 8;
           glds16(src, base + SA + (wave * NB + j) * 1024);
         } else {
           const int hi = g_ho[j] * geo.stride + gdy, wi = g_wo[j] * geo.stride + gdx;
@@ -751,8 +778,8 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
-  // slab `by` holds D in its final [N1][taps][N2] layout
-  float* out = ws + static_cast<int64_t>(by) * N1 * ntaps * N2 + static_cast<int64_t>(bz) * N2;
+  // slab `by` holds D in its final [N1][taps][N2] layout (row stride ldo = taps * N2)
+  float* out = ws + static_cast<int64_t>(by) * N1 * ldo + static_cast<int64_t>(bz) * N2;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -761,7 +788,7 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
       for (int r = 0; r < 4; ++r) {
         const int row = i0 + wi * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
         const int col = j0 + wj * (BN / 2) + j * 16 + (lane & 15);
-        out[static_cast<int64_t>(row) * ntaps * N2 + col] = acc[i][j][r];
+        if (BMODE != 2 || col < ldo) out[static_cast<int64_t>(row) * ldo + col] = acc[i][j][r];
       }
 }
 
@@ -914,6 +941,16 @@ inline int wgrad_order() {
     return v ? atoi(v) : 1;
   }();
   return o;
+}
+
+// multi-tap wgrad (BMODE 2) for kxk convolutions with N2 = 64 input channels:
+// one 128-wide tile covers two taps (DCP_WGRAD_MTAP=0 turns it off)
+inline bool wgrad_mtap(int N2, int taps) {
+  static const bool on = [] {
+    const char* v = getenv("DCP_WGRAD_MTAP");
+    return !(v && v[0] == '0');
+  }();
+  return on && taps > 1 && N2 == 64;
 }
 
 WgradPlan wgrad_plan(int64_t M, int N1, int N2, int taps = 1) {
@@ -1161,8 +1198,17 @@ void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s) {
   hipLaunchKernelGGL(colsum_partial_kernel, g1, dim3(kT), 0, s, static_cast<const uint16_t*>(x), out, M, N, rps);
 }
 
+namespace {
+// the plan a launch uses: multi-tap runs over taps * N2 columns rounded up to
+// the 128-wide tile, as one "tap"
+WgradPlan wgrad_plan_for(int64_t M, int N1, int N2, int taps) {
+  if (wgrad_mtap(N2, taps)) return wgrad_plan(M, N1, (taps * N2 + 127) / 128 * 128, 1);
+  return wgrad_plan(M, N1, N2, taps);
+}
+}  // namespace
+
 int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
-  const WgradPlan p = wgrad_plan(M, N1, N2, taps);
+  const WgradPlan p = wgrad_plan_for(M, N1, N2, taps);
   const int64_t groups = (p.S + kSlabGroup - 1) / kSlabGroup;
   return (static_cast<int64_t>(p.S) + (groups > 1 ? groups : 0)) * N1 * taps * N2;
 }
@@ -1174,11 +1220,27 @@ template <bool GATHER>
 void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
                   const float* shift, bool relu, float* ws, int taps, const ConvGeo& geo, hipStream_t s,
                   bool acc = false) {
-  const WgradPlan p = wgrad_plan(M, N1, N2, taps);
-  const dim3 grid(p.tiles * p.S * taps);
   const int order = wgrad_order();
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
+  const int ldo = taps * N2;
+  if constexpr (GATHER) {
+    if (wgrad_mtap(N2, taps)) {
+      const WgradPlan p = wgrad_plan_for(M, N1, N2, taps);
+      const int tj = (ldo + 127) / 128;
+      const dim3 grid(p.tiles * p.S);
+      if (p.bm == 128)
+        hipLaunchKernelGGL((gemm_wgrad_kernel<128, 128, false, true, 64, 0, 2>), grid, dim3(kT), 0, s, a, b, ws, M,
+                           N1, N2, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, ldo);
+      else
+        hipLaunchKernelGGL((gemm_wgrad_kernel<64, 128, false, true, 64, 0, 2>), grid, dim3(kT), 0, s, a, b, ws, M, N1,
+                           N2, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, ldo);
+      slab_reduce(ws, D, static_cast<int64_t>(N1) * ldo / 4, p.S, s, acc);
+      return;
+    }
+  }
+  const WgradPlan p = wgrad_plan(M, N1, N2, taps);
+  const dim3 grid(p.tiles * p.S * taps);
   const bool pro = scale != nullptr;
   const int tj = N2 / p.bn;
   // ring config (DCP_WGRAD_CFG): "64x2" (default: BK=64, 2 stages, 64 KB),
@@ -1195,13 +1257,13 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   do {                                                                                                             \
     if (cfg == 0 && !P)                                                                                            \
       hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 64>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,    \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order);                     \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo);                \
     else if (cfg == 1)                                                                                             \
       hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32, 2>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order);                     \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo);                \
     else                                                                                                           \
       hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,    \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order);                     \
+                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo);                \
   } while (0)
 #define DCP_GWG2(BM_, BN_)                      \
   do {                                          \
@@ -1242,10 +1304,10 @@ void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int
   auto b = static_cast<const uint16_t*>(xp);
   if (p.bm == 128)
     hipLaunchKernelGGL((gemm_wgrad_kernel<128, 128, false, true, 64, 0, 1>), grid, dim3(kT), 0, s, a, b, ws, M, Cout,
-                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order);
+                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, kStemWgradCols);
   else
     hipLaunchKernelGGL((gemm_wgrad_kernel<64, 128, false, true, 64, 0, 1>), grid, dim3(kT), 0, s, a, b, ws, M, Cout,
-                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order);
+                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, kStemWgradCols);
   slab_reduce(ws, D, static_cast<int64_t>(Cout) * kStemWgradCols / 4, p.S, s, false);
 }
 

@@ -162,7 +162,10 @@ def test_resnet_stage_gemm_path_matches(cuda):
 
 @pytest.mark.parametrize("shape", [  # (N, H, W, Cin, Cout, k, stride, pad)
     (2, 8, 8, 64, 64, 3, 1, 1), (3, 7, 9, 128, 64, 3, 1, 1), (4, 14, 14, 64, 128, 3, 2, 1),
-    (2, 15, 15, 128, 128, 3, 2, 1), (2, 6, 6, 64, 192, 1, 1, 0), (8, 28, 28, 128, 128, 3, 1, 1)])
+    (2, 15, 15, 128, 128, 3, 2, 1), (2, 6, 6, 64, 192, 1, 1, 0), (8, 28, 28, 128, 128, 3, 1, 1),
+    # Cin = 64 kxk: the multi-tap kernel (two taps per 128-wide tile, last tile half past the taps)
+    (4, 56, 56, 64, 64, 3, 1, 1), (3, 9, 11, 64, 64, 3, 1, 1), (2, 10, 10, 64, 64, 5, 1, 2),
+    (2, 12, 12, 64, 192, 3, 2, 1)])
 def test_conv_wgrad_gathered(cuda, shape):
     """Implicit-GEMM kxk weight gradient vs the fp32 ATen convolution backward."""
     from distributed_compute_pytorch_amd._ext import C as _C

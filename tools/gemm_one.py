@@ -1,7 +1,7 @@
 """One 1x1-conv GEMM shape, repeated (a small target for rocprofv3 --pmc).
 
     python tools/gemm_one.py --m 12544 --cin 2048 --cout 512 --op fwd [--iters 10]
-op: fwd | fwd_pro | dgrad | wgrad | conv3 (3x3 stride-1 implicit GEMM fwd, --hw spatial)
+op: fwd | fwd_pro | dgrad | wgrad | conv3 (3x3 stride-1 implicit GEMM fwd, --hw spatial) | wgrad3 (its weight gradient)
 """
 import argparse
 import os
@@ -31,6 +31,15 @@ def main():
     w = (torch.randn(a.cout, a.cin, device=dev) / a.cin ** 0.5).to(bf)
     wt = w.t().contiguous()
     sc, sf = torch.ones(a.cin, device=dev), torch.zeros(a.cin, device=dev)
+    if a.op == "wgrad3":
+        n = a.m // (a.hw * a.hw)
+        xi = torch.randn(n, a.cin, a.hw, a.hw, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
+        gi = torch.randn(n, a.cout, a.hw, a.hw, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
+        for _ in range(a.iters):
+            _C.conv_wgrad(gi, xi, 3, 3, 1, 1)
+        torch.cuda.synchronize()
+        print("ok", flush=True)
+        return
     if a.op == "conv3":
         n = a.m // (a.hw * a.hw)
         xi = torch.randn(n, a.cin, a.hw, a.hw, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
