@@ -411,7 +411,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& wt, int6
   const int64_t Cout = wt.numel() / (kh * kw * Cin);
   DCP_CHECK(kern::conv_fwd_supported(static_cast<int>(Cin), static_cast<int>(Cout), static_cast<int>(kh),
                                      static_cast<int>(kw)),
-            "conv_fwd: channels must be multiples of 64");
+            "conv_fwd: channels must be multiples of 64 and the kernel at most 8x8");
   const int64_t Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
   DCP_CHECK(Ho > 0 && Wo > 0 && N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31),
             "conv_fwd: bad geometry or tensor too large");

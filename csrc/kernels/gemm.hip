@@ -239,9 +239,16 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   // instructions per stage, more issue time than the stage's 16 MFMAs.
   int is_n = 0, is_kt = 0, is_slot = 0, is_v = wg;
   int is_c0 = 0, is_dy = 0, is_dx = 0;  // GATHER: channel offset and tap of the issue stage
+  int64_t is_off = 0;                   // GATHER: (is_dy * W + is_dx) * cin + is_c0
   const uint16_t* asrc[NA];
   const uint16_t* bsrc[NB];
-  int gnb[NA], ghb[NA], gwb[NA];  // GATHER: n*H, ho*stride-pad, wo*stride-pad of each A row
+  // GATHER: per A row (fixed for a tile) the address of tap (0, 0), channel 0
+  // (may point outside the tensor: only in-bounds taps are dereferenced) and
+  // the in-bounds taps as bit masks (bits 0-7: dy, 8-15: dx) — a stage then
+  // costs a uniform offset add, two shifts and a select per load instead of
+  // the pixel arithmetic (kh, kw ≤ 8: every ResNet / VGG kernel)
+  const uint16_t* growb[GATHER ? NA : 1];
+  uint32_t gvm[GATHER ? NA : 1];
   auto set_a = [&](int v) {
     const int64_t m0 = static_cast<int64_t>(v / tn) * BM;
 #pragma unroll
@@ -250,12 +257,17 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       const int r = p / CPR, lc = (p % CPR) ^ nt_swzk<BK>(p / CPR);
       int64_t gm = m0 + r;
       gm = gm < M ? gm : M - 1;
-      if (GATHER) {  // once per tile: the per-stage source is then two adds and a bounds test
+      if (GATHER) {  // once per tile
         const int mi = static_cast<int>(gm);
         const int wo = mi % geo.Wo, t1 = mi / geo.Wo;
-        gnb[j] = (t1 / geo.Ho) * geo.H;
-        ghb[j] = (t1 % geo.Ho) * geo.stride - geo.pad;
-        gwb[j] = wo * geo.stride - geo.pad;
+        const int hb = (t1 % geo.Ho) * geo.stride - geo.pad, wb = wo * geo.stride - geo.pad;
+        growb[j] = A + (static_cast<int64_t>((t1 / geo.Ho) * geo.H + hb) * geo.W + wb) * geo.cin + lc * 8;
+        // taps d with 0 <= hb + d < H: d in [max(0, -hb), min(8, H - hb))
+        const int hlo = hb < 0 ? -hb : 0, hhi = geo.H - hb < 8 ? geo.H - hb : 8;
+        const int wlo = wb < 0 ? -wb : 0, whi = geo.W - wb < 8 ? geo.W - wb : 8;
+        const uint32_t hm = hhi > hlo ? ((1u << hhi) - 1u) & ~((1u << hlo) - 1u) : 0u;
+        const uint32_t wmk = whi > wlo ? ((1u << whi) - 1u) & ~((1u << wlo) - 1u) : 0u;
+        gvm[j] = hm | (wmk << 8);
       } else if (AMODE == 1) {
         const int mi = static_cast<int>(gm);
         const int wo = mi % geo.Wo, t1 = mi / geo.Wo;
@@ -282,11 +294,8 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       if (GATHER) {
         const int p = (wave * NA + j) * 64 + lane;
         const int lc = (p % CPR) ^ nt_swzk<BK>(p / CPR);
-        const int hi = ghb[j] + is_dy, wi = gwb[j] + is_dx;
-        const bool ok = static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
-                        static_cast<unsigned>(wi) < static_cast<unsigned>(geo.W);
-        const uint16_t* src = ok ? A + (static_cast<int64_t>(gnb[j] + hi) * geo.W + wi) * geo.cin + is_c0 + lc * 8
-                                 : geo.zero + lc * 8;
+        const bool ok = ((gvm[j] >> is_dy) & (gvm[j] >> (8 + is_dx)) & 1u) != 0u;
+        const uint16_t* src = ok ? growb[j] + is_off : geo.zero + lc * 8;
         glds16(src, base + (wave * NA + j) * 1024);
       } else if (AMODE == 1) {
         glds16(asrc[j] + static_cast<int64_t>(is_kt) * geo.W * 4, base + (wave * NA + j) * 1024);
@@ -307,11 +316,13 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
           ++is_dy;
         }
       }
+      is_off = (static_cast<int64_t>(is_dy) * geo.W + is_dx) * geo.cin + is_c0;
     }
     if (++is_kt == KT) {
       is_kt = 0;
       is_v += P;
       is_c0 = is_dy = is_dx = 0;
+      is_off = 0;
       if (is_n < T) set_a(is_v);
     }
   };
@@ -1145,7 +1156,8 @@ void conv_dgrad_parity_bf16(const void* dY, const void* Wsub, void* dX, int N, i
 }
 
 bool conv_fwd_supported(int Cin, int Cout, int kh, int kw) {
-  return Cin % 64 == 0 && Cout % 64 == 0 && kh >= 1 && kw >= 1;
+  // kh, kw <= 8: the gathered A rows keep their in-bounds taps as 8-bit masks
+  return Cin % 64 == 0 && Cout % 64 == 0 && kh >= 1 && kw >= 1 && kh <= 8 && kw <= 8;
 }
 
 void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,

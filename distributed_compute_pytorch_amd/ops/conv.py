@@ -377,7 +377,7 @@ def kxk_policy(cin: int, cout: int, ho: int, stride: int):
 
 def conv_kxk_gemm_ok(x: torch.Tensor, conv) -> bool:
     return (conv_kxk_ok(x, conv) and x.shape[1] % 64 == 0 and conv.out_channels % 64 == 0
-            and conv.kernel_size[0] == conv.kernel_size[1])
+            and conv.kernel_size[0] == conv.kernel_size[1] and conv.kernel_size[0] <= 8)
 
 
 def conv_kxk_ok(x: torch.Tensor, conv) -> bool:
