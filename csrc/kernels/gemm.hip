@@ -154,9 +154,10 @@ constexpr int nt_stages() { return BK == 64 ? 2 : 3; }
 // the BN backward's separate reduce pass (re-reading dy and x) disappears.
 // AMODE 1 = the ResNet stem (stem.hip): A row m = output pixel (n, ho, wo) of
 // a stride-2 7x7 conv over the zero-padded 4-channel image geo.H x geo.W
-// (stem_prep); k-stage kt (BK = 32) = tap row dy = kt, 8 tap columns x 4
-// channels = the 64 contiguous bytes at pixel (2ho + kt, 2wo): the row base
-// is computed once per tile and each stage advances by one padded image row.
+// (stem_prep); a 32-wide k slice = tap row dy, 8 tap columns x 4 channels =
+// the 64 contiguous bytes at pixel (2ho + dy, 2wo), so a BK-wide stage holds
+// BK / 32 tap rows: the row bases are computed once per tile and each stage
+// advances by BK / 32 padded image rows (K = 256: dy = 7 has zero weights).
 // Wave layout: BM / 64 waves along M (64 rows each) x nt_wn waves along N.
 // 128 x 128 and 128 x 64: 2 x 2 waves (64 x 64 / 64 x 32 per wave); 256 x 128:
 // 4 x 2 (8 waves, one workgroup per CU: each B tile feeds twice the rows);
@@ -269,10 +270,11 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
         const uint32_t wmk = whi > wlo ? ((1u << whi) - 1u) & ~((1u << wlo) - 1u) : 0u;
         gvm[j] = hm | (wmk << 8);
       } else if (AMODE == 1) {
+        // chunk lc = k 8lc…8lc+7: tap row lc / 4 of the stage, 8 elements at (lc % 4) * 8
         const int mi = static_cast<int>(gm);
         const int wo = mi % geo.Wo, t1 = mi / geo.Wo;
         const int ho = t1 % geo.Ho, nn = t1 / geo.Ho;
-        asrc[j] = A + ((static_cast<int64_t>(nn) * geo.H + 2 * ho) * geo.W + 2 * wo) * 4 + lc * 8;
+        asrc[j] = A + ((static_cast<int64_t>(nn) * geo.H + 2 * ho + (lc >> 2)) * geo.W + 2 * wo) * 4 + (lc & 3) * 8;
       } else {
         asrc[j] = A + gm * K + lc * 8;
       }
@@ -298,7 +300,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
         const uint16_t* src = ok ? growb[j] + is_off : geo.zero + lc * 8;
         glds16(src, base + (wave * NA + j) * 1024);
       } else if (AMODE == 1) {
-        glds16(asrc[j] + static_cast<int64_t>(is_kt) * geo.W * 4, base + (wave * NA + j) * 1024);
+        glds16(asrc[j] + static_cast<int64_t>(is_kt) * (BK / 32) * geo.W * 4, base + (wave * NA + j) * 1024);
       } else {
         glds16(asrc[j] + k0, base + (wave * NA + j) * 1024);
       }
@@ -1172,7 +1174,7 @@ void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W,
   // geo: padded image (stem_hp/stem_wp) and the stride-2 output grid
   ConvGeo geo{H + 6, W + 8, H / 2, W / 2, 2, 0, 7, nullptr, 4};
   const int64_t M = static_cast<int64_t>(N) * (H / 2) * (W / 2);
-  constexpr int BM = 128, BN = 64, BK = 32, K = 224;
+  constexpr int BM = 128, BN = 64, BK = 64, K = kStemK;
   const int tiles_m = static_cast<int>((M + BM - 1) / BM);
   const int tn = Cout / BN;
   const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;

@@ -95,11 +95,12 @@ __global__ void __launch_bounds__(kT) stem_weight_kernel(const float* __restrict
   const int co = i / kStemK, k = i % kStemK;
   const int dy = k >> 5, r = k & 31, dx = r >> 2, c = r & 3;
   float v = 0.f;
-  if (dx < 7 && c < 3) v = cl ? w[((co * 7 + dy) * 7 + dx) * 3 + c] : w[((co * 3 + c) * 7 + dy) * 7 + dx];
+  if (dy < 7 && dx < 7 && c < 3) v = cl ? w[((co * 7 + dy) * 7 + dx) * 3 + c] : w[((co * 3 + c) * 7 + dy) * 7 + dx];
   wm[i] = f2bf(v);
 }
 
 // -------------------------------------------------- BN + ReLU + max-pool ----
+constexpr int kPoolRows = 8;  // pooled rows per thread (stem_bn_pool_fwd_kernel)
 __global__ void __launch_bounds__(kT) stem_bn_pool_fwd_kernel(
     const uint16_t* __restrict__ y, const float* __restrict__ acc, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ mean_out, float* __restrict__ invstd_out,
@@ -127,60 +128,100 @@ __global__ void __launch_bounds__(kT) stem_bn_pool_fwd_kernel(
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
   __syncthreads();
+  // Thread = (n, pooled column ow, 8 channels, a run of kPoolRows pooled rows)
+  // walking down the image: pooled row oh's window rows are 2oh-1, 2oh, 2oh+1
+  // and row 2oh+1 is the next row's 2(oh+1)-1, so it is carried in registers —
+  // every input row is fetched once per thread column instead of 1.5x through
+  // other XCDs' L2s (neighbouring rows of the former row-major mapping ran on
+  // different XCDs). Same scan order (window row-major, strict >) as before, so
+  // the arg-max ties break identically.
   const int cv = C / 8;
-  const int total = N * OH * OW * cv;
+  const int nchunk = (OH + kPoolRows - 1) / kPoolRows;
+  const int total = N * nchunk * OW * cv;
   for (int ti = blockIdx.x * kT + threadIdx.x; ti < total; ti += gridDim.x * kT) {
     const int c8 = ti % cv;
     int r = ti / cv;
     const int ow = r % OW;
     r /= OW;
-    const int oh = r % OH;
-    const int n = r / OH;
-    float sc[8], sf[8], m[8], xs[8];
-    uint8_t a[8];
+    const int chunk = r % nchunk;
+    const int n = r / nchunk;
+    float sc[8], sf[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       sc[k] = cf[c8 * 8 + k];
       sf[k] = cf[C + c8 * 8 + k];
-      m[k] = -INFINITY;
-      xs[k] = 0.f;
-      a[k] = 0;
     }
-    const int h0 = 2 * oh - 1, w0 = 2 * ow - 1;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int h = h0 + i;
-      if (h < 0 || h >= H) continue;
+    const int w0 = 2 * ow - 1;
+    // one window row: the 3 columns' raw bf16 (8 channels per uint4); outside
+    // the image the column is flagged (never selected)
+    auto load_row = [&](int h, uint4 (&rv)[3], uint32_t& inb) {
+      inb = 0u;
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int w = w0 + j;
-        if (w < 0 || w >= W) continue;
-        float v[8];
-        ld8(y, ((static_cast<int64_t>(n) * H + h) * W + w) * C + c8 * 8, v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float b = fmaf(v[k], sc[k], sf[k]);
-          if (b > m[k] || b != b) {
-            m[k] = b;
-            a[k] = static_cast<uint8_t>(i * 3 + j);
-            xs[k] = v[k];
-          }
+        if (h >= 0 && h < H && w >= 0 && w < W) {
+          rv[j] = *reinterpret_cast<const uint4*>(y + ((static_cast<int64_t>(n) * H + h) * W + w) * C + c8 * 8);
+          inb |= 1u << j;
+        } else {
+          rv[j] = make_uint4(0u, 0u, 0u, 0u);
         }
       }
-    }
+    };
+    const int oh0 = chunk * kPoolRows;
+    const int oh1 = oh0 + kPoolRows < OH ? oh0 + kPoolRows : OH;
+    uint4 r0[3];  // carried window row 2oh - 1
+    uint32_t in0;
+    load_row(2 * oh0 - 1, r0, in0);
+    for (int oh = oh0; oh < oh1; ++oh) {
+      uint4 r1[3], r2[3];
+      uint32_t in1, in2;
+      load_row(2 * oh, r1, in1);
+      load_row(2 * oh + 1, r2, in2);
+      float m[8], xs[8];
+      uint8_t a[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (!(m[k] > 0.f)) {  // ReLU: max <= 0 -> 0, no gradient flows (NaN stays NaN)
-        if (m[k] == m[k]) m[k] = 0.f;
-        a[k] = 255;
+      for (int k = 0; k < 8; ++k) {
+        m[k] = -INFINITY;
+        xs[k] = 0.f;
+        a[k] = 0;
       }
-    const int64_t o = static_cast<int64_t>(ti) * 8;
-    st8(out, o, m);
-    st8(xsel, o, xs);
-    uint2 pk;
-    pk.x = a[0] | (a[1] << 8) | (a[2] << 16) | (static_cast<uint32_t>(a[3]) << 24);
-    pk.y = a[4] | (a[5] << 8) | (a[6] << 16) | (static_cast<uint32_t>(a[7]) << 24);
-    *reinterpret_cast<uint2*>(idx + o) = pk;
+      auto scan = [&](int i, const uint4 (&rv)[3], uint32_t inb) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (!((inb >> j) & 1u)) continue;
+          const uint32_t wv[4] = {rv[j].x, rv[j].y, rv[j].z, rv[j].w};
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float v = (k & 1) ? __uint_as_float(wv[k >> 1] & 0xffff0000u) : __uint_as_float(wv[k >> 1] << 16);
+            const float bv = fmaf(v, sc[k], sf[k]);
+            if (bv > m[k] || bv != bv) {
+              m[k] = bv;
+              a[k] = static_cast<uint8_t>(i * 3 + j);
+              xs[k] = v;
+            }
+          }
+        }
+      };
+      scan(0, r0, in0);
+      scan(1, r1, in1);
+      scan(2, r2, in2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (!(m[k] > 0.f)) {  // ReLU: max <= 0 -> 0, no gradient flows (NaN stays NaN)
+          if (m[k] == m[k]) m[k] = 0.f;
+          a[k] = 255;
+        }
+      const int64_t o = (((static_cast<int64_t>(n) * OH + oh) * OW + ow) * cv + c8) * 8;
+      st8(out, o, m);
+      st8(xsel, o, xs);
+      uint2 pk;
+      pk.x = a[0] | (a[1] << 8) | (a[2] << 16) | (static_cast<uint32_t>(a[3]) << 24);
+      pk.y = a[4] | (a[5] << 8) | (a[6] << 16) | (static_cast<uint32_t>(a[7]) << 24);
+      *reinterpret_cast<uint2*>(idx + o) = pk;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) r0[j] = r2[j];
+      in0 = in2;
+    }
   }
 }
 
@@ -368,7 +409,8 @@ void stem_bn_pool_fwd(const void* y, const float* stats, const float* gamma, con
                       float* invstd, float* running_mean, float* running_var, float momentum, float eps,
                       int64_t* nbt, void* out, uint8_t* idx, void* xsel, int N, int H, int W, int OH, int OW, int C,
                       hipStream_t s) {
-  const unsigned g = grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8), 4096);
+  const unsigned g =
+      grid_for(static_cast<int64_t>(N) * ((OH + kPoolRows - 1) / kPoolRows) * OW * (C / 8), 4096);
   hipLaunchKernelGGL(stem_bn_pool_fwd_kernel, dim3(g), dim3(kT), sizeof(float) * 2 * C, s,
                      static_cast<const uint16_t*>(y), stats, gamma, beta, mean, invstd, running_mean, running_var,
                      momentum, eps, nbt, static_cast<uint16_t*>(out), idx, static_cast<uint16_t*>(xsel), N, H, W, OH,

@@ -16,14 +16,16 @@ namespace kern {
 // Hp = H + 6, Wp = W + 8 (even, so pixel pairs are 16-B aligned).
 inline int stem_hp(int H) { return H + 6; }
 inline int stem_wp(int W) { return W + 8; }
-constexpr int kStemK = 224;  // 7 tap rows x (8 tap columns x 4 channels); dx = 7 and c = 3 are zero
+// 8 tap rows x (8 tap columns x 4 channels); dy = 7, dx = 7 and c = 3 are zero
+// (two tap rows per 64-wide k-stage of the stem GEMM)
+constexpr int kStemK = 256;
 
 // x: [N,3,H,W] fp32 (x_bf16 = 0) or bf16 (x_bf16 = 1), NCHW (cl = 0) or NHWC
 // memory order (cl = 1). Writes Xp and, when x3 != null, the bf16 NHWC copy
 // [N,H,W,3] (the operand of the weight-gradient convolution).
 void stem_prep(const void* x, int x_bf16, int cl, void* xp, void* x3, int N, int H, int W, hipStream_t s);
 // conv weight fp32 [Cout][3][7][7] (cl = 0) or [Cout][7][7][3] (cl = 1) ->
-// wm bf16 [Cout][224] in the GEMM's k order (dy*32 + dx*4 + c).
+// wm bf16 [Cout][256] in the GEMM's k order (dy*32 + dx*4 + c).
 void stem_weight(const float* w, int cl, void* wm, int Cout, hipStream_t s);
 // y [N*Ho*Wo][Cout] bf16 = conv(Xp, wm), stride 2; stats (zeroed fp32 [2*Cout])
 // += (Σy, Σy²) of the bf16 output. Cout % 64 == 0.

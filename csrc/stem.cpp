@@ -51,7 +51,7 @@ std::vector<at::Tensor> prep(const at::Tensor& x, bool want_x3) {
   return {xp, x3};
 }
 
-// conv weight (fp32 [Cout,3,7,7], contiguous or channels_last) -> GEMM operand bf16 [Cout][224]
+// conv weight (fp32 [Cout,3,7,7], contiguous or channels_last) -> GEMM operand bf16 [Cout][256]
 at::Tensor weight(const at::Tensor& w) {
   DCP_CHECK(w.is_cuda() && w.dim() == 4 && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
                 w.scalar_type() == at::kFloat && (w.is_contiguous() || is_nhwc(w)),
