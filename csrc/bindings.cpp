@@ -139,7 +139,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("bucket_bytes_cap", &ReducerOptions::bucket_bytes_cap)
       .def_readwrite("tail_bucket_bytes", &ReducerOptions::tail_bucket_bytes)
       .def_readwrite("comm_dtype", &ReducerOptions::comm_dtype)
-      .def_readwrite("average", &ReducerOptions::average);
+      .def_readwrite("average", &ReducerOptions::average)
+      .def_readwrite("check_streams", &ReducerOptions::check_streams);
 
   m.def("trace_enabled", &trace::enabled);
   m.def("trace_push", [](const std::string& n) { trace::push(n.c_str()); });

@@ -5,6 +5,7 @@
 #include <torch/csrc/autograd/variable.h>
 
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <optional>
 #include <thread>
@@ -104,6 +105,8 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
   build_buckets(buckets);
   const char* t = std::getenv("DCP_COMM_TIMING");
   timing_ = t && std::strcmp(t, "1") == 0 && !params_.empty() && params_[0].is_cuda();
+  const char* ds = std::getenv("DCP_DEBUG_STREAMS");
+  check_ = opts_.check_streams || (ds && std::strcmp(ds, "1") == 0);
   if (timing_) {
     DCP_CHECK(hipEventCreate(&ev_bwd_end_) == hipSuccess && hipEventCreate(&ev_final_) == hipSuccess,
               "Reducer: event creation failed");
@@ -288,6 +291,15 @@ void Reducer::launch_ready_buckets() {
   }
 }
 
+namespace {
+bool capturing(const at::Tensor& t) {
+  if (!t.is_cuda()) return false;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(c10::hip::getCurrentHIPStream(t.device().index()).stream(), &cap);
+  return cap != hipStreamCaptureStatusNone;
+}
+}  // namespace
+
 void Reducer::launch(Bucket& b) {
   // Pack: one multi-tensor launch for every gradient not already in place.
   const bool compressed = !b.wire.is_same(b.flat);
@@ -325,6 +337,12 @@ void Reducer::launch(Bucket& b) {
     b.work = comm_hook_(b.wire, static_cast<int64_t>(&b - buckets_.data()));
   } else {
     b.work = comm_->all_reduce(b.wire, opts_.average ? ReduceOp::AVG : ReduceOp::SUM);
+  }
+  if (check_ && !capturing(b.wire)) {
+    // packed-buffer checksum on the compute stream (ordered after the pack),
+    // reduced by a collective issued right after the bucket's own
+    b.check_sum = b.wire.to(at::kDouble).sum().reshape({1}).to(at::kFloat);
+    b.check_work = comm_->all_reduce(b.check_sum, opts_.average ? ReduceOp::AVG : ReduceOp::SUM);
   }
   b.launched = true;
 }
@@ -366,6 +384,23 @@ void Reducer::finalize() {
   for (auto& b : buckets_) {
     b.work->wait();
     if (cap == hipStreamCaptureStatusNone) b.stats.comm_ms = b.work->elapsed_ms();
+    if (check_ && b.check_work) {
+      b.check_work->wait();
+      // what the compute stream sees now vs what the collective must have produced
+      const double seen = b.wire.to(at::kDouble).sum().item<double>();
+      const double want = b.check_sum.to(at::kDouble).item<double>();
+      const double tol = 1e-3 * std::max(1.0, std::fabs(want)) + 1e-6 * static_cast<double>(b.wire.numel());
+      b.check_work.reset();
+      if (!(std::fabs(seen - want) <= tol)) {
+        const int64_t k = static_cast<int64_t>(&b - buckets_.data());
+        reset_iteration_state();
+        throw Error(str_cat("Reducer stream-ordering check failed for bucket ", k, " (", b.params.size(),
+                            " params): the reduced buffer sums to ", seen, " on the compute stream but the "
+                            "reduction of the packed buffers sums to ", want,
+                            " — a missing event edge between pack, collective and consumer, or a comm hook "
+                            "whose work completed before its result was written"));
+      }
+    }
     if (!b.wire.is_same(b.flat)) ops::mt_copy({b.wire}, {b.flat}, 1.0);
     std::vector<at::Tensor> src, dst;
     for (size_t s = 0; s < b.params.size(); ++s) {
@@ -413,6 +448,7 @@ void Reducer::finalize() {
 void Reducer::reset_iteration_state() {
   for (auto& b : buckets_) {
     b.work.reset();
+    b.check_work.reset();
     b.launched = false;
     b.pending = static_cast<int>(b.params.size());
     for (auto& g : b.pending_grads) g = at::Tensor();

@@ -59,6 +59,14 @@ struct ReducerOptions {
   at::ScalarType comm_dtype = at::ScalarType::Undefined;
   // false -> SUM instead of AVG (for custom hooks that pre-scale).
   bool average = true;
+  // Debug (SURVEY §5.2 "stream-ordering asserts"; also DCP_DEBUG_STREAMS=1):
+  // per bucket, a checksum of the packed wire buffer taken on the compute
+  // stream right after the pack, all-reduced over the world, must equal the
+  // checksum of the buffer the compute stream sees after waiting on the
+  // reduction. A missing pack→collective or collective→consumer event edge
+  // (or a comm hook that returns before its result is in the buffer) shows up
+  // as a mismatch, raised from finalize. Host-syncs once per bucket: debug only.
+  bool check_streams = false;
 };
 
 struct BucketStats {
@@ -117,6 +125,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     bool launched = false;
     WorkPtr work;
     BucketStats stats;
+    at::Tensor check_sum;  // check_streams: fp64 [1] checksum of the packed buffer (all-reduced)
+    WorkPtr check_work;
   };
 
   void build_buckets(const std::vector<std::vector<int64_t>>& assignment);
@@ -157,6 +167,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   int64_t rebuilds_ = 0;
   double backward_t0_ms_ = 0;
   bool timing_ = false;
+  bool check_ = false;  // ReducerOptions::check_streams / DCP_DEBUG_STREAMS=1
   hipEvent_t ev_bwd_end_ = nullptr, ev_final_ = nullptr;
   bool ev_recorded_ = false;
   // find_unused_parameters: per-parameter used flags. Host staging (pinned on

@@ -80,17 +80,20 @@ def test_resnet_grads_match_stock_fp32(pg, cuda):
     l1.backward()
     g_ref = [p.grad.clone() for p in ref.parameters()]
     buf_ref = [b.detach().clone() for b in ref.buffers()]  # before the second run updates them again
-    ref.zero_grad(set_to_none=True)
-    F.cross_entropy(ref(x), y).backward()  # second stock run: the noise floor
+    # stock re-runs: the noise floor (per parameter, the largest of 3 samples —
+    # one sample alone is itself noisy: BN grads are sums with heavy cancellation)
+    noise = [0.0] * len(g_ref)
+    for _ in range(3):
+        ref.zero_grad(set_to_none=True)
+        F.cross_entropy(ref(x), y).backward()
+        for i, (p, g0) in enumerate(zip(ref.parameters(), g_ref)):
+            noise[i] = max(noise[i], float((p.grad - g0).norm() / g0.norm().clamp_min(1e-12)))
     l2 = F.cross_entropy(ddp(x), y)
     l2.backward()
     torch.testing.assert_close(l2, l1, rtol=1e-5, atol=1e-5)
-    for (n, p), q, g0 in zip(ref.named_parameters(), model.parameters(), g_ref):
-        den = g0.norm().clamp_min(1e-12)
-        noise = float((p.grad - g0).norm() / den)
-        rel = float((q.grad - g0).norm() / den)
-        # the stock noise floor is itself one noisy sample (BN bias grads are sums with heavy cancellation)
-        assert rel < 5 * noise + 5e-3, (n, rel, noise)
+    for (n, p), q, g0, nz in zip(ref.named_parameters(), model.parameters(), g_ref, noise):
+        rel = float((q.grad - g0).norm() / g0.norm().clamp_min(1e-12))
+        assert rel < 5 * nz + 5e-3, (n, rel, nz)
     for (n, _), b, c in zip(ref.named_buffers(), buf_ref, model.buffers()):
         torch.testing.assert_close(c.float(), b.float(), rtol=1e-4, atol=1e-5, msg=n)
 

@@ -36,3 +36,18 @@ def test_single_rank_hop_real_rccl(cuda):
     assert errs["bf16_wire"] < 5e-2, errs  # bf16 gradients on the wire
     assert errs["fp32_buckets"] >= 2
     assert res["unused_ok"] and res["globally_unused_grad_none"]
+
+
+def test_single_rank_hop_with_stream_ordering_check(cuda):
+    """Same worker with the Reducer's debug stream-ordering check on
+    (DCP_DEBUG_STREAMS=1): every bucket's pack -> RCCL collective (comm stream)
+    -> consumer edge is verified by checksum; any violation raises in finalize."""
+    env = dict(os.environ, DCP_SINGLE_RANK_HOP="1", DCP_DEBUG_STREAMS="1")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "gpu_hop_worker.py")], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "stream-ordering check failed" not in r.stderr
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("HOPRESULT ")][-1]
+    res = json.loads(line[len("HOPRESULT "):])
+    assert res["ordering_ok"] and res["collectives_ok"]
+    assert res["ddp_max_abs_err"]["fp32"] < 1e-5

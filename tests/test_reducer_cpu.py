@@ -196,3 +196,39 @@ def _groups(rank, world):
 
 def test_new_group_and_async_all_gather():
     run_world(_groups, 3)
+
+
+def _ordering_check(rank, world):
+    """DCP_DEBUG_STREAMS=1: the Reducer's stream-ordering check passes on the
+    normal path and catches a 'reduction' that never reached the buffer."""
+    os.environ["DCP_DEBUG_STREAMS"] = "1"
+    import distributed_compute_pytorch_amd as dcp
+
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(32, 64), nn.Tanh(), nn.Linear(64, 8))
+    ref = copy.deepcopy(m)
+    ddp = dcp.parallel.DistributedDataParallel(m, bucket_cap_mb=0.005, first_bucket_mb=0.005, tail_bucket_mb=0)
+    g = torch.Generator().manual_seed(3)
+    xs = [torch.randn(4, 32, generator=g) for _ in range(world)]
+    for _ in range(3):
+        for p in m.parameters():
+            p.grad = None
+        ddp(xs[rank]).pow(2).sum().backward()
+    grads = []
+    for r in range(world):
+        rr = copy.deepcopy(ref)
+        rr(xs[r]).pow(2).sum().backward()
+        grads.append([p.grad for p in rr.parameters()])
+    for i, p in enumerate(m.parameters()):
+        torch.testing.assert_close(p.grad, sum(gg[i] for gg in grads) / world, rtol=1e-5, atol=1e-6)
+    # a comm hook whose work "completes" without reducing: ranks hold different
+    # gradients, so the buffer the consumer sees is not the reduction
+    ddp.register_comm_hook(None, dcp.parallel.comm_hooks.noop_hook)
+    for p in m.parameters():
+        p.grad = None
+    with pytest.raises(RuntimeError, match="stream-ordering check failed"):
+        ddp(xs[rank]).pow(2).sum().backward()
+
+
+def test_reducer_stream_ordering_check():
+    run_world(_ordering_check, 2)
