@@ -1004,17 +1004,20 @@ inline int nt_bk() {
 // Tile rows per workgroup: 256 (8 waves, 1 workgroup per CU) when the M
 // tiles alone fill the chip, else 128 (4 waves, 2 per CU). DCP_GEMM_BM=128 /
 // 256 forces one (A/B switch).
-inline int nt_bm(int64_t M, int tn, int BN, bool pro) {
+inline int nt_bm(int64_t M, int tn, int BN, bool pro, int K, bool gather) {
   static const int force = [] {
     const char* v = getenv("DCP_GEMM_BM");
     return v ? atoi(v) : 0;
   }();
   static const int n64 = [] {  // tile rows for Cout = 64 (256: 4 x 1 waves of 64 x 64)
     const char* v = getenv("DCP_GEMM_N64_BM");
-    return v ? atoi(v) : 128;
+    return v ? atoi(v) : 0;
   }();
   if (force == 128 || force == 256) return force;
-  if (BN == 64) return n64 == 256 ? 256 : 128;
+  // Cout = 64: 4 x 1 waves of 64 x 64 pay on the plain 1x1 GEMMs with K >= 256
+  // (layer-1 conv1 forward, conv3 data gradient: -7-10 %, profiles/r2_gemm_bm_ab.txt);
+  // the gathered 3x3 ones lose (their per-stage gather work doubles per wave)
+  if (BN == 64) return n64 == 128 || n64 == 256 ? n64 : (!gather && K >= 256 ? 256 : 128);
   // 8 x 64 x 64 waves measured slower than 2 x 128 x 128 workgroups on every
   // non-prologue shape (profiles/r2_gemm_bm256.txt); the BN-prologue GEMMs
   // (one prologue per 256 rows) gain
@@ -1093,7 +1096,7 @@ void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, 
                        hipStream_t s, bool scatter2 = false, bool parity = false) {
   const int BN = N % 128 == 0 ? 128 : 64;
   const int tn = N / BN;
-  if (nt_bm(M, tn, BN, scale != nullptr) == 256)
+  if (nt_bm(M, tn, BN, scale != nullptr, K, GATHER) == 256)
     gemm_nt_launch_bm<GATHER, BK, 256>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s, scatter2, parity);
   else
     gemm_nt_launch_bm<GATHER, BK, 128>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s, scatter2, parity);
