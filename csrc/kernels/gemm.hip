@@ -942,6 +942,202 @@ __global__ void __launch_bounds__(kT) colsum_partial_kernel(const uint16_t* __re
   if (col < N) atomicAdd(part + col, t);  // part: ZEROED [N]
 }
 
+// ------------------------------------------------- direct 3x3, 64 -> 64 ----
+// Stride-1 pad-1 3x3 convolution with Cin = Cout = 64 (ResNet-50 layer-1
+// conv2 forward and its data gradient), W <= 62. The gathered implicit GEMM
+// re-fetches every input row once per tap (9x the bytes of the input through
+// L2 into LDS) and spends ~8 VALU per gathered load; here a workgroup keeps
+// ALL 9 x 64 x 64 weights resident in LDS (72 KB, loaded once) and, per tile
+// of R = 128 / W whole output rows of one image, fetches the (R+2) x (W+2)
+// input halo ONCE (double-buffered: the next tile's halo is in flight while
+// this one is computed). The 9 taps are then just shifted LDS addresses of the
+// same halo: 144 MFMAs per wave per tile with no barrier inside the tile.
+// 4 waves (2 x 2: 64 pixels x 32 output channels each), one workgroup per CU
+// (~144 KB of LDS), each workgroup a contiguous run of tiles (the next tile's
+// halo shares 2 rows with this one: L2 hits). Same MFMA operand convention and
+// epilogue as gemm_nt_kernel (bf16 output through per-wave LDS staging, STATS:
+// per-channel sum / sum of squares of the bf16 output into stats[2 * 64]).
+constexpr int kD3Threads = 256;
+__device__ __forceinline__ int d3_swz(int row) { return (row >> 1) & 7; }  // 128-B rows, as nt_swzk<64>
+
+template <bool STATS>
+__global__ void __launch_bounds__(kD3Threads, 1) conv3x3_c64_kernel(const uint16_t* __restrict__ X,
+                                                                     const uint16_t* __restrict__ Wt,
+                                                                     uint16_t* __restrict__ Y, int N, int H, int W,
+                                                                     int R, int HT, int tiles, int per_block,
+                                                                     const uint16_t* __restrict__ zero,
+                                                                     float* __restrict__ stats, int halo_bytes) {
+  constexpr int C = 64, WN = 32, FM = 4, FN = 2, LPR = WN / 8, RPI = 64 / LPR, CST = 32 * WN * 2;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* wl = lds;                                // [9 * 64 rows][128 B] weights, row = tap * 64 + cout
+  char* hl0 = lds + 9 * 64 * 128;                // two halo buffers of halo_bytes
+  char* cst_all = hl0 + 2 * halo_bytes;          // per-wave C staging
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int WP = W + 2;                          // halo row length (pixels)
+  const int hq = (R + 2) * WP * 8;               // 16-B chunks in a halo
+  const int hglds = halo_bytes / (4 * 1024);     // halo glds per wave
+  char* cst = cst_all + wave * CST;
+  const int t0 = blockIdx.x * per_block;
+  const int t1 = min(tiles, t0 + per_block);
+  if (t0 >= t1) return;
+
+  // weights: 9 * 64 * 8 chunks = 72 wave-glds, 18 per wave
+#pragma unroll 2
+  for (int j = 0; j < 18; ++j) {
+    const int q = (wave * 18 + j) * 64 + lane;
+    const int row = q >> 3, pc = q & 7, lc = pc ^ d3_swz(row);
+    const int tap = row >> 6, co = row & 63;
+    glds16(Wt + (co * 9 + tap) * C + lc * 8, wl + (wave * 18 + j) * 1024);
+  }
+  auto issue_halo = [&](int tile, char* buf) {
+    const int n = tile / HT, h0 = (tile % HT) * R;
+    for (int j = 0; j < hglds; ++j) {
+      const int q = (wave * hglds + j) * 64 + lane;
+      const int hp = q >> 3, pc = q & 7, lc = pc ^ d3_swz(hp);
+      const int hr = hp / WP, hc = hp - hr * WP;
+      const int ih = h0 - 1 + hr, iw = hc - 1;
+      const bool ok = q < hq && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+      const uint16_t* src = ok ? X + ((static_cast<int64_t>(n) * H + ih) * W + iw) * C + lc * 8 : zero + lc * 8;
+      glds16(src, buf + (wave * hglds + j) * 1024);
+    }
+  };
+  issue_halo(t0, hl0);
+
+  // per-lane tile-invariant halo index of each A-fragment row at tap (0, 0)
+  const int npx_full = R * W;
+  int hp0[FM];
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const int i = wm * 64 + j * 16 + (lane & 15);
+    const int r = i / W, c = i - r * W;
+    hp0[j] = i < npx_full ? r * WP + c : 0;
+  }
+  const int ck = lane >> 4;
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
+
+  wait_vm<0>();
+  barrier();
+  int issued = 4;  // global stores of the previous tile's epilogue (per wave)
+  for (int tile = t0; tile < t1; ++tile) {
+    const int k = tile - t0;
+    char* hb = hl0 + (k & 1) * halo_bytes;
+    if (k > 0) {
+      // this tile's halo (issued before the previous epilogue's stores) has landed
+      if (issued >= 4) wait_vm<4>();
+      else if (issued == 3) wait_vm<3>();
+      else if (issued == 2) wait_vm<2>();
+      else if (issued == 1) wait_vm<1>();
+      else wait_vm<0>();
+      barrier();  // all waves: halo visible; previous tile's reads of the other buffer done
+    }
+    if (tile + 1 < t1) issue_halo(tile + 1, hl0 + ((k + 1) & 1) * halo_bytes);
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int toff = (tap / 3) * WP + (tap % 3);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int lch = 4 * h + ck;
+        bf16x8 xf[FM], wf[FN];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          const int hp = hp0[j] + toff;
+          xf[j] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + 16 * (lch ^ d3_swz(hp)));
+        }
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int row = tap * 64 + wn * WN + i * 16 + (lane & 15);
+          wf[i] = *reinterpret_cast<const bf16x8*>(wl + row * 128 + 16 * (lch ^ d3_swz(row)));
+        }
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+
+    // epilogue (gemm_nt_kernel's): acc[i][j][r] = Y[pixel 16j + (lane&15)][16i + 4(lane>>4) + r]
+    const int n = tile / HT, h0 = (tile % HT) * R;
+    const int npx = min(R, H - h0) * W;  // valid pixels of this tile
+    const int64_t rowbase = (static_cast<int64_t>(n) * H + h0) * W;
+    issued = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = 2 * h + jj;
+        const int row = jj * 16 + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int col = i * 16 + (lane >> 4) * 4;
+          const int chunk = (col >> 3) ^ (row & 7 & (LPR - 1));
+          *reinterpret_cast<uint2*>(cst + row * (WN * 2) + chunk * 16 + (col & 7) * 2) =
+              make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < 32 / RPI; ++it) {
+        const int row = it * RPI + lane / LPR;
+        const int c = lane % LPR;
+        const uint4 v = *reinterpret_cast<const uint4*>(cst + row * (WN * 2) + 16 * (c ^ (row & 7 & (LPR - 1))));
+        const int i = wm * 64 + 32 * h + row;
+        if (wm * 64 + 32 * h + it * RPI < npx) ++issued;  // uniform: this store instruction runs
+        if (i < npx) {
+          *reinterpret_cast<uint4*>(Y + (rowbase + i) * C + wn * WN + c * 8) = v;
+          if (STATS) {
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float a = bf_lo(w4[e]), b = bf_hi(w4[e]);
+              ssum[2 * e] += a;
+              ssq[2 * e] = fmaf(a, a, ssq[2 * e]);
+              ssum[2 * e + 1] += b;
+              ssq[2 * e + 1] = fmaf(b, b, ssq[2 * e + 1]);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (STATS) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        ssum[e] += __shfl_xor(ssum[e], o);
+        ssq[e] += __shfl_xor(ssq[e], o);
+      }
+    wait_vm<0>();
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(hl0);  // [sum|sq][wm][64]
+    if (lane < LPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = wn * WN + lane * 8 + e;
+        red[wm * C + c] = ssum[e];
+        red[2 * C + wm * C + c] = ssq[e];
+      }
+    }
+    __syncthreads();
+    if (t < C) {
+      atomicAdd(stats + t, red[t] + red[C + t]);
+      atomicAdd(stats + C + t, red[2 * C + t] + red[3 * C + t]);
+    }
+  }
+}
+
 struct WgradPlan {
   int bm, bn, tiles, S;
   int64_t chunk;
@@ -1165,8 +1361,53 @@ bool conv_fwd_supported(int Cin, int Cout, int kh, int kw) {
   return Cin % 64 == 0 && Cout % 64 == 0 && kh >= 1 && kw >= 1 && kh <= 8 && kw <= 8;
 }
 
+namespace {
+// direct 3x3 / 64-channel kernel (DCP_CONV3_DIRECT=0 falls back to the gathered GEMM)
+inline bool conv3x3_c64_direct(int Cin, int Cout, int kh, int kw, int stride, int pad, int W) {
+  static const bool on = [] {
+    const char* v = getenv("DCP_CONV3_DIRECT");
+    return !(v && v[0] == '0');
+  }();
+  return on && Cin == 64 && Cout == 64 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && W >= 2 && W <= 62;
+}
+
+void conv3x3_c64_launch(const void* X, const void* Wt, void* Y, int N, int H, int W, const void* zero, float* stats,
+                        hipStream_t s) {
+  const int R = 128 / W;                       // whole output rows per tile
+  const int HT = (H + R - 1) / R;
+  const int tiles = N * HT;
+  const int chunks = (R + 2) * (W + 2) * 8;    // halo 16-B chunks
+  const int halo_bytes = (chunks * 16 + 4095) / 4096 * 4096;
+  const int P = tiles < 256 ? tiles : 256;     // one workgroup per CU
+  const int per_block = (tiles + P - 1) / P;
+  const size_t lds = 9 * 64 * 128 + 2 * static_cast<size_t>(halo_bytes) + 4 * 32 * 32 * 2;
+  auto x = static_cast<const uint16_t*>(X);
+  auto w = static_cast<const uint16_t*>(Wt);
+  auto y = static_cast<uint16_t*>(Y);
+  auto z = static_cast<const uint16_t*>(zero);
+  static const bool attr = [] {  // > 64 KB of dynamic LDS
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_c64_kernel<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_c64_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  if (stats)
+    hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3(P), dim3(kD3Threads), lds, s, x, w, y, N, H, W, R, HT, tiles,
+                       per_block, z, stats, halo_bytes);
+  else
+    hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3(P), dim3(kD3Threads), lds, s, x, w, y, N, H, W, R, HT, tiles,
+                       per_block, z, stats, halo_bytes);
+}
+}  // namespace
+
 void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                    int kh, int kw, int stride, int pad, const void* zero, float* stats, hipStream_t s) {
+  if (conv3x3_c64_direct(Cin, Cout, kh, kw, stride, pad, W)) {
+    conv3x3_c64_launch(X, Wt, Y, N, H, W, zero, stats, s);
+    return;
+  }
   ConvGeo geo{H, W, Ho, Wo, stride, pad, kw, static_cast<const uint16_t*>(zero), Cin};
   gemm_nt_launch<true>(X, Wt, Y, static_cast<int64_t>(N) * Ho * Wo, Cout, kh * kw * Cin, nullptr, nullptr, false,
                        stats, geo, s);

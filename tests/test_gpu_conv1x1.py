@@ -315,3 +315,29 @@ def test_conv_weight_bf16_layouts(cuda):
     wb = w.to(torch.bfloat16)
     assert torch.equal(wf, wb.permute(0, 2, 3, 1).contiguous())
     assert torch.equal(wd, wb.flip(2, 3).permute(1, 2, 3, 0).contiguous())
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 56, 56), (3, 7, 9), (2, 5, 62), (4, 13, 2), (5, 30, 31), (2, 17, 40)])
+def test_conv3x3_c64_direct(cuda, n, h, w):
+    """Direct 3x3 / 64-channel kernel (halo in LDS, weights resident): forward +
+    BN sums and the stride-1 data gradient (same kernel on flipped weights) vs
+    fp32 PyTorch on the same bf16 operands, rectangular and ragged row tiles."""
+    from torch import nn
+
+    from distributed_compute_pytorch_amd.ops.conv import conv_kxk_gemm
+
+    g = torch.Generator().manual_seed(21)
+    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False).to(cuda).to(memory_format=torch.channels_last)
+    x = _x(n, h, w, 64, cuda, g).requires_grad_(True)
+    y, st = conv_kxk_gemm(x, conv.weight, 1, 1, stats=True)
+    gy = _x(n, h, w, 64, cuda, g)
+    y.backward(gy)
+    wb = conv.weight.detach().to(torch.bfloat16).float()
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, wb, None, 1, 1)
+    yr.backward(gy.float())
+    assert _rel(y, yr) < 1e-2
+    yf = y.float()
+    ref_st = torch.cat([yf.sum((0, 2, 3)), (yf * yf).sum((0, 2, 3))])
+    assert _rel(st, ref_st) < 1e-4
+    assert _rel(x.grad, xr.grad) < 1e-2
