@@ -958,7 +958,13 @@ __global__ void __launch_bounds__(kT) colsum_partial_kernel(const uint16_t* __re
 // epilogue as gemm_nt_kernel (bf16 output through per-wave LDS staging, STATS:
 // per-channel sum / sum of squares of the bf16 output into stats[2 * 64]).
 constexpr int kD3Threads = 256;
-__device__ __forceinline__ int d3_swz(int row) { return (row >> 1) & 7; }  // 128-B rows, as nt_swzk<64>
+// 16-B chunk swizzle of the 128-B halo / weight rows: an A fragment reads 16
+// consecutive halo pixels starting ANYWHERE (tap offsets 0..2 * (W + 2) + 2),
+// and chunk ^ (row & 7) is conflict-free for every start (exhaustive check over
+// the four ds_read_b128 lane groups; 2-way at most for the fragment that
+// straddles an image-row boundary) — nt_swzk's (row >> 1) & 7 assumes starts
+// at multiples of 16 and measured 36 % of LDS cycles in conflicts here
+__device__ __forceinline__ int d3_swz(int row) { return row & 7; }
 
 template <bool STATS>
 __global__ void __launch_bounds__(kD3Threads, 1) conv3x3_c64_kernel(const uint16_t* __restrict__ X,
