@@ -35,6 +35,9 @@ namespace {
 
 constexpr int kT = 256;
 constexpr int kV = 8;  // channels per thread
+// vectors per thread per iteration in the apply kernels (4 measured -1.2 % in
+// the step: register pressure halves the waves per SIMD)
+constexpr int kApplyU = 2;
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {
@@ -47,11 +50,30 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 template <int D>
 struct V8;
 
+// Streaming (non-temporal) 16-B loads / stores for the bf16 activations: the
+// BN passes stream tensors of 100-800 MB that no cache holds between passes,
+// and the nt hints measured +15-20 % on 2-in / 1-out streams on this MI355X
+// (tools/bw_probe.hip: 4.7 -> 5.5 TB/s at the same grid). g_bn_nt (host:
+// DCP_BN_NT=0) turns them off for A/B.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ int g_bn_nt = 1;
+
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  const u32x4* q = static_cast<const u32x4*>(p);
+  const u32x4 v = g_bn_nt ? __builtin_nontemporal_load(q) : *q;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  if (g_bn_nt) __builtin_nontemporal_store(w, static_cast<u32x4*>(p));
+  else *static_cast<u32x4*>(p) = w;
+}
+
 template <>
 struct V8<BN_BF16> {
   using S = uint16_t;
   __device__ static void ld(const void* p, int64_t i, float (&o)[kV]) {
-    const uint4 v = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + i);
+    const uint4 v = ld16(static_cast<const uint16_t*>(p) + i);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -65,7 +87,7 @@ struct V8<BN_BF16> {
     v.y = f2bf(o[2]) | (static_cast<uint32_t>(f2bf(o[3])) << 16);
     v.z = f2bf(o[4]) | (static_cast<uint32_t>(f2bf(o[5])) << 16);
     v.w = f2bf(o[6]) | (static_cast<uint32_t>(f2bf(o[7])) << 16);
-    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + i) = v;
+    st16(static_cast<uint16_t*>(p) + i, v);
   }
 };
 
@@ -303,21 +325,22 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(const void* __restrict__ x
     }
     if (RES && ACT && mbits) mbits[vv] = static_cast<uint8_t>(bits);
   };
+  // kApplyU vectors per thread per iteration, all loads issued first
   int64_t v = tid;
-  for (; v + stride < nvec; v += 2 * stride) {
-    float a[kV], b[kV], ra[kV], rb[kV];
-    V8<D>::ld(x, v * kV, a);
-    V8<D>::ld(x, (v + stride) * kV, b);
-    if (RES) {
-      V8<D>::ld(res, v * kV, ra);
-      V8<D>::ld(res, (v + stride) * kV, rb);
+  for (; v + (kApplyU - 1) * stride < nvec; v += kApplyU * stride) {
+    float a[kApplyU][kV], ra[kApplyU][kV];
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) {
+      V8<D>::ld(x, (v + u * stride) * kV, a[u]);
+      if (RES) V8<D>::ld(res, (v + u * stride) * kV, ra[u]);
     }
-    one(a, ra, v);
-    one(b, rb, v + stride);
-    V8<D>::st(y, v * kV, a);
-    V8<D>::st(y, (v + stride) * kV, b);
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) {
+      one(a[u], ra[u], v + u * stride);
+      V8<D>::st(y, (v + u * stride) * kV, a[u]);
+    }
   }
-  if (v < nvec) {
+  for (; v < nvec; v += stride) {
     float a[kV], ra[kV];
     V8<D>::ld(x, v * kV, a);
     if (RES) V8<D>::ld(res, v * kV, ra);
@@ -532,22 +555,21 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict
   };
   constexpr bool kReadY = ACT && !FROM_G && !MX;
   int64_t v = tid;
-  for (; v + stride < nvec; v += 2 * stride) {
-    float ga[kV], gb[kV], xa[kV], xb[kV], ya[kV], yb[kV];
-    V8<D>::ld(gsrc, v * kV, ga);
-    V8<D>::ld(gsrc, (v + stride) * kV, gb);
-    V8<D>::ld(x, v * kV, xa);
-    V8<D>::ld(x, (v + stride) * kV, xb);
-    if (kReadY) {
-      V8<D>::ld(y, v * kV, ya);
-      V8<D>::ld(y, (v + stride) * kV, yb);
+  for (; v + (kApplyU - 1) * stride < nvec; v += kApplyU * stride) {
+    float ga[kApplyU][kV], xa[kApplyU][kV], ya[kApplyU][kV];
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) {
+      V8<D>::ld(gsrc, (v + u * stride) * kV, ga[u]);
+      V8<D>::ld(x, (v + u * stride) * kV, xa[u]);
+      if (kReadY) V8<D>::ld(y, (v + u * stride) * kV, ya[u]);
     }
-    one(ga, xa, ya);
-    one(gb, xb, yb);
-    V8<D>::st(dx, v * kV, ga);
-    V8<D>::st(dx, (v + stride) * kV, gb);
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) {
+      one(ga[u], xa[u], ya[u]);
+      V8<D>::st(dx, (v + u * stride) * kV, ga[u]);
+    }
   }
-  if (v < nvec) {
+  for (; v < nvec; v += stride) {
     float gv[kV], xv[kV], yv[kV];
     V8<D>::ld(gsrc, v * kV, gv);
     V8<D>::ld(x, v * kV, xv);
@@ -595,8 +617,14 @@ inline void red_geometry(int64_t M, int C, int* nblk, int64_t* rows_per_blk, int
 // apply grid: multiple of nothing special (cv | 256 keeps thread→channel fixed),
 // ≤ 1024 workgroups (4 per CU) so the per-thread prologue stays cheap
 inline int apply_grid(int64_t nvec, int cv) {
+  // ≤ 1024 workgroups (4 per CU): more streamed faster in isolation
+  // (tools/bw_probe.hip) but measured -1.4 % in the ResNet-50 step (more
+  // coefficient prologues, the trailing-edge partial waves); DCP_BN_APPLY_BLOCKS
+  // overrides the cap
+  static const int64_t cap_env = env_or("DCP_BN_APPLY_BLOCKS", 0);
+  int64_t cap = cap_env > 0 ? cap_env : 1024;
   int64_t g = (nvec + kT * 2 - 1) / (kT * 2);
-  if (g > 1024) g = 1024;
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   // the prologue/channel mapping needs (g*256) % cv == 0
   if ((g * kT) % cv != 0) g = ((g * kT + cv - 1) / cv * cv + kT - 1) / kT;
@@ -613,6 +641,21 @@ inline size_t red_smem(int C) {
 
 }  // namespace
 
+namespace {
+// copy DCP_BN_NT into the device flag once per process (before the first BN launch)
+void bn_init_flags() {
+  static const bool done = [] {
+    const char* v = getenv("DCP_BN_NT");
+    if (v && v[0] == '0') {  // the device default is 1: no copy (and nothing to capture) otherwise
+      const int nt = 0;
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bn_nt), &nt, sizeof(int));
+    }
+    return true;
+  }();
+  (void)done;
+}
+}  // namespace
+
 bool bn_supported(int C) {
   // reductions: C/8 ≤ 32 must divide 256, else be a multiple of 32; apply: C/8 must divide 256 or be a multiple
   const int cv = C / kV;
@@ -626,6 +669,7 @@ void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
                       float* mean, float* invstd, float* acc, bool act, int64_t* nbt, uint8_t* mbits,
                       bool acc_ready, hipStream_t s) {
+  bn_init_flags();
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
@@ -662,6 +706,7 @@ void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_
 
 void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
               const float* shift, bool act, hipStream_t s) {
+  bn_init_flags();
   const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t asm_ = sizeof(float) * 2 * C;
@@ -687,6 +732,7 @@ void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int
 void bn_stats_coef(int dtype, const void* x, int64_t M, int C, const float* gamma, const float* beta,
                    float* running_mean, float* running_var, float momentum, float eps, float* mean, float* invstd,
                    float* scale, float* shift, float* acc, int64_t* nbt, hipStream_t s, bool acc_ready) {
+  bn_init_flags();
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
@@ -711,6 +757,7 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
                  bool store_g, void* gout,
                  void* dx, float* dgamma, float* dbeta, float* acc, bool training, const uint8_t* mbits,
                  hipStream_t s) {
+  bn_init_flags();
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks, true);
@@ -779,6 +826,7 @@ void bn_forward_train_resbn(int dtype, const void* x, const void* res, void* y, 
                             const float* gamma, const float* beta, float* running_mean, float* running_var,
                             float momentum, float eps, float* mean, float* invstd, const float* acc, int64_t* nbt,
                             uint8_t* mbits, const ResBnArgs& rb, hipStream_t s) {
+  bn_init_flags();
   const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t asm_ = sizeof(float) * 4 * C;
@@ -796,6 +844,7 @@ void bn_backward_resbn(int dtype, const void* gy, const void* gy2, const void* x
                        const float* gamma, const float* mean, const float* invstd, const uint8_t* mbits, void* gout,
                        void* dx, float* dgamma, float* dbeta, float* acc, const void* x2, const float* mean2,
                        float* acc2, hipStream_t s) {
+  bn_init_flags();
   int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks, true);
@@ -834,6 +883,7 @@ void bn_backward_resbn(int dtype, const void* gy, const void* gy2, const void* x
 void bn_backward_apply_plain(int dtype, const void* g, const void* x, int64_t M, int C, const float* gamma,
                              const float* mean, const float* invstd, const float* acc, void* dx, float* dgamma,
                              float* dbeta, hipStream_t s) {
+  bn_init_flags();
   const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t bsm = sizeof(float) * 4 * C;
@@ -851,6 +901,7 @@ void bn_backward_apply_plain(int dtype, const void* g, const void* x, int64_t M,
 void bn_backward_apply(int dtype, const void* gy, const void* x, int64_t M, int C, const float* gamma,
                        const float* beta, const float* mean, const float* invstd, const float* acc, void* dx,
                        float* dgamma, float* dbeta, hipStream_t s) {
+  bn_init_flags();
   const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t sm = sizeof(float) * 6 * C;
