@@ -22,7 +22,7 @@ from torch import nn
 from ..ops.batchnorm import BatchNormAct2d, bn_resbn_act, resbn_ok
 from ..ops.conv import (ConvWeightPrep, bn_relu_conv, bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk,
                         conv_kxk_gemm, conv_kxk_gemm_ok, conv_kxk_ok, gemm_ok, kxk_policy)
-from ..ops.pool import FusedMaxPool2d
+from ..ops.pool import FusedMaxPool2d, global_avg_pool_flat
 from ..ops.stem import fused_stem, stem_supported
 
 
@@ -264,7 +264,7 @@ class ResNet(nn.Module):
                 x = self.layer4(x, a, False)
             else:
                 x = self.layer4(self.layer3(self.layer2(self.layer1(fused_stem(x, self.conv1, self.bn1)))))
-            return self.fc(torch.flatten(self.avgpool(x), 1))
+            return self.fc(global_avg_pool_flat(x))
         x = self.bn1(self.conv1(x))
         if self.fused_bn and self.dual_bn:
             # thread dual-output aliases across stage boundaries: every
@@ -279,7 +279,7 @@ class ResNet(nn.Module):
             x = self.layer4(x, a, False)
         else:
             x = self.layer4(self.layer3(self.layer2(self.layer1(self.maxpool(x)))))
-        x = torch.flatten(self.avgpool(x), 1)
+        x = global_avg_pool_flat(x) if self.fused_bn else torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 
 

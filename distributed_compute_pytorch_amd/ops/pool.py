@@ -66,3 +66,28 @@ class FusedMaxPool2d(nn.MaxPool2d):
             return fused_max_pool2d(x, k, s, p, dual)
         y = super().forward(x)
         return (y, y) if dual else y
+
+
+class _GlobalAvgPoolNHWC(torch.autograd.Function):
+    """mean over H, W of a channels_last [N, C, H, W] tensor -> [N, C]. The
+    backward writes the broadcast gradient straight into channels_last memory
+    (one streaming write) — ATen's adaptive-avg-pool backward returns an NCHW
+    gradient that the next NHWC kernel then has to transpose-copy (a strided
+    51 M-element copy per ResNet-50 step at batch 512, ~150 µs)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return x.mean((2, 3))
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W = ctx.shape
+        return (g / (H * W))[:, :, None, None].expand(N, C, H, W).contiguous(memory_format=torch.channels_last)
+
+
+def global_avg_pool_flat(x: torch.Tensor) -> torch.Tensor:
+    """``torch.flatten(nn.AdaptiveAvgPool2d(1)(x), 1)`` for channels_last x."""
+    if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and x.requires_grad:
+        return _GlobalAvgPoolNHWC.apply(x)
+    return x.mean((2, 3))
