@@ -473,6 +473,77 @@ std::vector<at::Tensor> conv1x1_dgrad_bnred(const at::Tensor& gy, const at::Tens
   return {dy, acc};
 }
 
+// Data gradient of the next bottleneck's conv1 fused with the backward
+// reduction of the residual BN3(+downsample BN)+add+ReLU that produced its
+// input: returns (g, acc, acc2) with g = (gy·W + gy2)·relu_bits — the masked
+// gradient of BN3's output summed over both consumers, also the residual
+// branch's gradient — acc = (Σg, Σg·(x - mean)) for x = BN3's input and, when
+// x2 is given, acc2 = (Σg, Σg·(x2 - mean2)) for the downsample BN.
+std::vector<at::Tensor> conv1x1_dgrad_resred(const at::Tensor& gy, const at::Tensor& wt, const at::Tensor& x,
+                                             const c10::optional<at::Tensor>& gy2, const at::Tensor& mean,
+                                             const at::Tensor& bits, const c10::optional<at::Tensor>& x2,
+                                             const c10::optional<at::Tensor>& mean2) {
+  check_gemm_act(gy, "conv1x1_dgrad_resred");
+  check_gemm_act(x, "conv1x1_dgrad_resred");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t K = gy.size(1);
+  const int64_t M = gy.numel() / K;
+  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % K == 0,
+            "conv1x1_dgrad_resred: weight");
+  const int64_t N = wt.numel() / K;
+  DCP_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_dgrad_resred: unsupported shape");
+  DCP_CHECK(x.dim() == gy.dim() && x.size(1) == N && x.numel() == M * N, "conv1x1_dgrad_resred: x shape");
+  DCP_CHECK(mean.scalar_type() == at::kFloat && mean.numel() == N && mean.is_contiguous(),
+            "conv1x1_dgrad_resred: mean must be fp32 [N]");
+  DCP_CHECK(bits.scalar_type() == at::kByte && bits.numel() == M * N / 8 && bits.is_contiguous(),
+            "conv1x1_dgrad_resred: relu bits mismatch");
+  at::Tensor g2;
+  if (gy2.has_value() && gy2->defined()) {
+    g2 = gy2->to(at::kBFloat16).contiguous(x.dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous);
+    DCP_CHECK(g2.sizes() == x.sizes(), "conv1x1_dgrad_resred: gy2 shape");
+  }
+  const bool has_x2 = x2.has_value() && x2->defined();
+  if (has_x2) {
+    check_gemm_act(*x2, "conv1x1_dgrad_resred(x2)");
+    DCP_CHECK(x2->sizes() == x.sizes(), "conv1x1_dgrad_resred: x2 shape");
+    DCP_CHECK(mean2.has_value() && mean2->defined() && mean2->scalar_type() == at::kFloat && mean2->numel() == N,
+              "conv1x1_dgrad_resred: mean2 must be fp32 [N]");
+  }
+  at::Tensor g = at::empty_like(x, x.dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous);
+  auto s = stream_of(gy);
+  at::Tensor acc = zeroed_floats(2 * N, gy, s);
+  at::Tensor acc2 = has_x2 ? zeroed_floats(2 * N, gy, s) : at::empty({0}, gy.options().dtype(at::kFloat));
+  kern::gemm_nt_resred_bf16(gy.data_ptr(), wt.data_ptr(), g.data_ptr(), M, static_cast<int>(N), static_cast<int>(K),
+                            x.data_ptr(), mean.data_ptr<float>(), g2.defined() ? g2.data_ptr() : nullptr,
+                            bits.data_ptr<uint8_t>(), acc.data_ptr<float>(), has_x2 ? x2->data_ptr() : nullptr,
+                            has_x2 ? mean2->data_ptr<float>() : nullptr, has_x2 ? acc2.data_ptr<float>() : nullptr, s);
+  return {g, acc, acc2};
+}
+
+// BN training backward apply from an already masked gradient g and its
+// reduction acc = (Σg, Σg·(x - mean)): (dx, dweight, dbias).
+std::vector<at::Tensor> bn_bwd_apply_g(const at::Tensor& g, const at::Tensor& x, const at::Tensor& weight,
+                                       const at::Tensor& mean, const at::Tensor& invstd, const at::Tensor& acc) {
+  check_nhwc(x, "bn_bwd_apply_g");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  DCP_CHECK(g.sizes() == x.sizes() && g.scalar_type() == x.scalar_type() && g.is_contiguous(cl_fmt(x)),
+            "bn_bwd_apply_g: g must match x");
+  DCP_CHECK(acc.scalar_type() == at::kFloat && acc.numel() == 2 * C && acc.is_contiguous(),
+            "bn_bwd_apply_g: acc must be fp32 [2*C]");
+  DCP_CHECK(weight.scalar_type() == at::kFloat && weight.numel() == C && weight.is_contiguous(),
+            "bn_bwd_apply_g: weight must be fp32 [C]");
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x, cl_fmt(x));
+  at::Tensor dw = at::empty({C}, fopt), db = at::empty({C}, fopt);
+  kern::bn_backward_apply_plain(bn_dtype(x), g.data_ptr(), x.data_ptr(), M, static_cast<int>(C),
+                                weight.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                acc.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                                stream_of(x));
+  return {dx, dw, db};
+}
+
 // stride-1 kxk conv data gradient (implicit GEMM on gy with the flipped,
 // transposed weight wd [Cin][kh][kw][Cout]) + the BN+ReLU backward reduction
 // of x in its epilogue: returns (dy, acc [2*Cin]).
@@ -1215,6 +1286,11 @@ void bind(pybind11::module& m) {
         pybind11::arg("stats") = false);
   m.def("conv1x1_dgrad_bnred", &conv1x1_dgrad_bnred, "1x1 data gradient + BN/ReLU backward reduction epilogue");
   m.def("conv_dgrad_bnred", &conv_dgrad_bnred, "stride-1 kxk data gradient + BN/ReLU backward reduction epilogue");
+  m.def("conv1x1_dgrad_resred", &conv1x1_dgrad_resred,
+        "1x1 data gradient + residual BN(+RBN)/ReLU backward reduction epilogue -> (g, acc, acc2)",
+        pybind11::arg("gy"), pybind11::arg("wt"), pybind11::arg("x"), pybind11::arg("gy2"), pybind11::arg("mean"),
+        pybind11::arg("bits"), pybind11::arg("x2") = pybind11::none(), pybind11::arg("mean2") = pybind11::none());
+  m.def("bn_bwd_apply_g", &bn_bwd_apply_g, "BN training backward apply from a masked gradient + its reduction");
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply, "BN/ReLU training backward apply from a precomputed reduction");
   m.def("bn_resbn_act_fwd", &bn_resbn_act_fwd, "training relu(bn(x) + bn2(x2)), both BNs fused (downsample block)");
   m.def("bn_resbn_act_bwd", &bn_resbn_act_bwd, "backward of bn_resbn_act_fwd");

@@ -139,6 +139,12 @@ struct BnRedArgs {
   const float* beta;
   const float* mean;
   const float* invstd;
+  // EPI 5 / 6 (RESRED): the residual BN+ReLU the GEMM's output feeds
+  const uint16_t* gy2;   // second gradient of that BN's output (its residual consumer); nullable
+  const uint8_t* bits;   // the forward's 1-bit ReLU mask (1 B per 8 channels)
+  const uint16_t* x2;    // EPI 6: raw input of the residual-branch BN (downsample conv output)
+  const float* mean2;    // EPI 6: its batch mean
+  float* acc2;           // EPI 6: (Σg, Σg·(x2 - mean2)) [2N]
 };
 
 // NT ring stages: BK=32 → 3 (two stages in flight), BK=64 → 2; either way
@@ -152,6 +158,13 @@ constexpr int nt_stages() { return BK == 64 ? 2 : 3; }
 // forward's own mask expression, sc/sf from gamma/beta/mean/invstd exactly as
 // batchnorm.hip's coef()), stats[0][c] += Σg, stats[1][c] += Σg·(x - mean):
 // the BN backward's separate reduce pass (re-reading dy and x) disappears.
+// EPI 5 = RESRED, the backward of the residual BN3+add+ReLU whose output this
+// data gradient belongs to (the next bottleneck's conv1 dgrad): C = g =
+// (acc + gy2)·bit — the masked sum of both consumers' gradients, written in
+// place of the plain dgrad — and stats[0][c] += Σg, stats[1][c] += Σg·(x -
+// mean): BN3's reduce pass (re-reading dy, gy2 and x, writing g) disappears.
+// EPI 6 = RESRED with the downsample BN folded into the residual (RBN): also
+// acc2 += (Σg, Σg·(x2 - mean2)).
 // AMODE 1 = the ResNet stem (stem.hip): A row m = output pixel (n, ho, wo) of
 // a stride-2 7x7 conv over the zero-padded 4-channel image geo.H x geo.W
 // (stem_prep); a 32-wide k slice = tap row dy, 8 tap columns x 4 channels =
@@ -186,7 +199,9 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   // gradient (rows = dx pixels (2a+ph, 2b+pw), gathered from gy over the taps
   // of matching parity); stored to its pixel of the full dx
   constexpr bool PAR = EPI == 4;
-  static_assert(!(PRO && RED), "RED is a data-gradient epilogue");
+  constexpr bool RR = EPI == 5 || EPI == 6;  // RESRED
+  constexpr bool X2 = EPI == 6;
+  static_assert(!(PRO && (RED || RR)), "RED / RESRED are data-gradient epilogues");
   constexpr int kNSnt = nt_stages<BK>();
   constexpr int RB = BK * 2;                                  // stage row bytes
   constexpr int CPR = BK / 8;                                 // 16-B chunks per row
@@ -335,9 +350,9 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // statistics: each lane owns the 8 channels wn*WN + 8*(lane % LPR) … +7
-  float ssum[8], ssq[8];
+  float ssum[8], ssq[8], ss2[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
+  for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = ss2[e] = 0.f;
   // RED: mean and the forward's folded affine of the block's BN columns, in
   // LDS (registers would push the kernel past 256 and halve occupancy)
   float* redc = pro;  // [3][BN]: mean, scale, shift
@@ -351,6 +366,13 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       redc[2 * BN + t] = (bnr.beta ? bnr.beta[c] : 0.f) - mu * sc;
     }
     __syncthreads();  // nothing in flight yet
+  }
+  if (RR) {  // [2][BN]: mean, mean2 of the block's columns
+    if (t < BN) {
+      redc[t] = bnr.mean[n0 + t];
+      if (X2) redc[BN + t] = bnr.mean2[n0 + t];
+    }
+    __syncthreads();
   }
 
 #pragma unroll
@@ -416,8 +438,32 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       // global stores covering whole 128-B lines (no cross-wave sync needed:
       // a wave's LDS ops execute in order).
       const int64_t mt = static_cast<int64_t>(cv / tn) * BM + wm * 64;
+      // RED / RESRED: x (gy2, bits, x2) rows of both halves loaded before the
+      // first use — one wait, twice the bytes in flight per wave (the epilogue
+      // is latency-bound on these reads); per half for EPI 6 (registers)
+      constexpr int NR = 32 / RPI;
+      constexpr int HB = X2 ? 1 : 2;  // halves loaded ahead
+      uint4 xr[(RED || RR) ? HB * NR : 1], g2r[RR ? HB * NR : 1], x2r[X2 ? HB * NR : 1];
+      uint32_t mbr[RR ? HB * NR : 1];
+      auto epi_load = [&](int h0) {
+        const bool has2 = RR && bnr.gy2 != nullptr;
+#pragma unroll
+        for (int i = 0; i < HB * NR; ++i) {
+          const int64_t m = mt + 32 * (h0 + i / NR) + (i % NR) * RPI + lane / LPR;
+          const int64_t o = m * N + n0 + wn * WN + (lane % LPR) * 8;
+          const uint4 z = make_uint4(0, 0, 0, 0);
+          xr[i] = m < M ? *reinterpret_cast<const uint4*>(bnr.x + o) : z;
+          if (RR) {
+            g2r[RR ? i : 0] = (m < M && has2) ? *reinterpret_cast<const uint4*>(bnr.gy2 + o) : z;
+            mbr[RR ? i : 0] = m < M ? bnr.bits[o >> 3] : 0u;
+          }
+          if (X2) x2r[X2 ? i : 0] = m < M ? *reinterpret_cast<const uint4*>(bnr.x2 + o) : z;
+        }
+      };
+      if ((RED || RR) && HB == 2) epi_load(0);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
+        if ((RED || RR) && HB == 1) epi_load(h);
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const int j = 2 * h + jj;
@@ -429,16 +475,6 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
             *reinterpret_cast<uint2*>(cst + row * (WN * 2) + chunk * 16 + (col & 7) * 2) =
                 make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
             acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-        }
-        // RED: this half's x rows, all loads issued before the first use (one wait)
-        uint4 xr[RED ? 32 / RPI : 1];
-        if (RED) {
-#pragma unroll
-          for (int it = 0; it < 32 / RPI; ++it) {
-            const int64_t m = mt + 32 * h + it * RPI + lane / LPR;
-            xr[it] = m < M ? *reinterpret_cast<const uint4*>(bnr.x + m * N + n0 + wn * WN + (lane % LPR) * 8)
-                           : make_uint4(0, 0, 0, 0);
           }
         }
 #pragma unroll
@@ -465,6 +501,35 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
             *reinterpret_cast<uint4*>(
                 C + (static_cast<int64_t>(nn * geo.oh + 2 * a + geo.ph) * geo.ow + 2 * b + geo.pw) * N + n0 + wn * WN +
                 c * 8) = v;
+          } else if (m < M && RR) {
+            // g = (dgrad + gy2) · relu bit, in fp32 from the bf16-rounded dgrad
+            // (what the separate reduce kernel sees); bf16 g stored, fp32 g reduced
+            const uint4 g2 = g2r[RR ? (HB - 1) * h * NR + it : 0], xv = xr[(HB - 1) * h * NR + it];
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, y4[4] = {g2.x, g2.y, g2.z, g2.w};
+            const uint32_t x4[4] = {xv.x, xv.y, xv.z, xv.w};
+            const uint32_t mb = mbr[RR ? (HB - 1) * h * NR + it : 0];
+            const int cb = wn * WN + c * 8;
+            float gk[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float a = (k & 1) ? bf_hi(w4[k >> 1]) : bf_lo(w4[k >> 1]);
+              const float b = (k & 1) ? bf_hi(y4[k >> 1]) : bf_lo(y4[k >> 1]);
+              const float xk = (k & 1) ? bf_hi(x4[k >> 1]) : bf_lo(x4[k >> 1]);
+              gk[k] = (mb >> k) & 1u ? a + b : 0.f;
+              ssum[k] += gk[k];
+              ssq[k] = fmaf(gk[k], xk - redc[cb + k], ssq[k]);
+            }
+            if (X2) {
+              const uint4 x2v = x2r[X2 ? (HB - 1) * h * NR + it : 0];
+              const uint32_t z4[4] = {x2v.x, x2v.y, x2v.z, x2v.w};
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const float zk = (k & 1) ? bf_hi(z4[k >> 1]) : bf_lo(z4[k >> 1]);
+                ss2[k] = fmaf(gk[k], zk - redc[BN + cb + k], ss2[k]);
+              }
+            }
+            *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) =
+                make_uint4(pack2(gk[0], gk[1]), pack2(gk[2], gk[3]), pack2(gk[4], gk[5]), pack2(gk[6], gk[7]));
           } else if (m < M) {
             *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) = v;
             if (STATS) {
@@ -479,7 +544,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
               }
             }
             if (RED) {
-              const uint4 xv = xr[RED ? it : 0];
+              const uint4 xv = xr[RED ? (HB - 1) * h * NR + it : 0];
               const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
               const uint32_t x4[4] = {xv.x, xv.y, xv.z, xv.w};
               const int cb = wn * WN + c * 8;
@@ -502,7 +567,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       cv += P;
     }
   }
-  if (STATS || RED) {
+  if (STATS || RED || RR) {
     // lanes with the same channel set: lane ^ LPR, ^2LPR, ... ; then over wm via LDS
 #pragma unroll
     for (int e = 0; e < 8; ++e)
@@ -510,28 +575,35 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       for (int o = LPR; o < 64; o <<= 1) {
         ssum[e] += __shfl_xor(ssum[e], o);
         ssq[e] += __shfl_xor(ssq[e], o);
+        if (X2) ss2[e] += __shfl_xor(ss2[e], o);
       }
     wait_vm<0>();
     __syncthreads();  // ring idle: reuse it
-    float* red = reinterpret_cast<float*>(lds);  // [sum|sq][wm][BN]
+    float* red = reinterpret_cast<float*>(lds);  // [sum|sq|s2][wm][BN]
     if (lane < LPR) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int c = wn * WN + lane * 8 + e;
         red[wm * BN + c] = ssum[e];
         red[WM * BN + wm * BN + c] = ssq[e];
+        if (X2) red[2 * WM * BN + wm * BN + c] = ss2[e];
       }
     }
     __syncthreads();
     if (t < BN) {
-      float a = 0.f, b = 0.f;
+      float a = 0.f, b = 0.f, d = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
         a += red[w * BN + t];
         b += red[WM * BN + w * BN + t];
+        if (X2) d += red[2 * WM * BN + w * BN + t];
       }
       atomicAdd(stats + n0 + t, a);
       atomicAdd(stats + N + n0 + t, b);
+      if (X2) {
+        atomicAdd(bnr.acc2 + n0 + t, a);
+        atomicAdd(bnr.acc2 + N + n0 + t, d);
+      }
     }
   }
 }
@@ -1259,6 +1331,16 @@ void gemm_nt_launch_bm(const void* A, const void* B, void* C, int64_t M, int N, 
 #define DCP_GNT2(BN_)                            \
   do {                                           \
     if (red) {                                   \
+      if constexpr (!GATHER) {                   \
+        if (red->bits && red->x2) {              \
+          DCP_GNT(BN_, false, 6);                \
+          break;                                 \
+        }                                        \
+        if (red->bits) {                         \
+          DCP_GNT(BN_, false, 5);                \
+          break;                                 \
+        }                                        \
+      }                                          \
       DCP_GNT(BN_, false, 2);                    \
       break;                                     \
     }                                            \
@@ -1325,6 +1407,20 @@ void gemm_nt_bnred_bf16(const void* A, const void* B, void* C, int64_t M, int N,
                         const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,
                         hipStream_t s) {
   const BnRedArgs r{static_cast<const uint16_t*>(x), gamma, beta, mean, invstd};
+  gemm_nt_launch<false>(A, B, C, M, N, K, nullptr, nullptr, false, acc, ConvGeo{}, s, &r);
+}
+
+void gemm_nt_resred_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
+                         const float* mean, const void* gy2, const uint8_t* bits, float* acc, const void* x2,
+                         const float* mean2, float* acc2, hipStream_t s) {
+  BnRedArgs r{};
+  r.x = static_cast<const uint16_t*>(x);
+  r.mean = mean;
+  r.gy2 = static_cast<const uint16_t*>(gy2);
+  r.bits = bits;
+  r.x2 = static_cast<const uint16_t*>(x2);
+  r.mean2 = mean2;
+  r.acc2 = acc2;
   gemm_nt_launch<false>(A, B, C, M, N, K, nullptr, nullptr, false, acc, ConvGeo{}, s, &r);
 }
 

@@ -75,6 +75,12 @@ void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, 
 void gemm_nt_bnred_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
                         const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,
                         hipStream_t s);
+// dgrad GEMM whose epilogue is the residual BN(+RBN)+ReLU backward reduction
+// (gemm.hip EPI 5 / 6): C = g = (A·Bᵀ + gy2)·bit; acc = (Σg, Σg·(x - mean)),
+// acc2 = (Σg, Σg·(x2 - mean2)) when x2 != nullptr
+void gemm_nt_resred_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
+                         const float* mean, const void* gy2, const uint8_t* bits, float* acc, const void* x2,
+                         const float* mean2, float* acc2, hipStream_t s);
 void conv_fwd_bnred_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo,
                          int Cout, int kh, int kw, int stride, int pad, const void* zero, const void* x,
                          const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,

@@ -20,8 +20,9 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d, bn_resbn_act, resbn_ok
-from ..ops.conv import (ConvWeightPrep, bn_relu_conv, bn_relu_conv1x1, conv1x1 as gemm_conv1x1, conv_kxk,
-                        conv_kxk_gemm, conv_kxk_gemm_ok, conv_kxk_ok, gemm_ok, kxk_policy)
+from ..ops.conv import (ConvWeightPrep, bn_relu_conv, bn_relu_conv1x1, bn_res_act_conv1x1, conv1x1 as gemm_conv1x1,
+                        conv_kxk, conv_kxk_gemm, conv_kxk_gemm_ok, conv_kxk_ok, gemm_ok, kxk_policy,
+                        res_conv_fuse_ok)
 from ..ops.pool import FusedMaxPool2d, global_avg_pool_flat
 from ..ops.stem import fused_stem, stem_supported
 
@@ -43,6 +44,9 @@ FUSED_STEM = os.environ.get("DCP_STEM", "1") == "1"
 WEIGHT_PREP = os.environ.get("DCP_WEIGHT_PREP", "1") == "1"
 # downsample BN applied inside BN3's residual kernel (its output never written)
 RESBN = os.environ.get("DCP_RESBN", "1") == "1"
+# each block's BN3 + residual + ReLU and the NEXT block's conv1 as one autograd
+# node: BN3's backward reduction runs in conv1's data-gradient epilogue
+RES_CONV_FUSE = os.environ.get("DCP_RES_CONV_FUSE", "1") == "1"
 
 
 def conv3x3(cin, cout, stride=1):
@@ -77,7 +81,8 @@ class Bottleneck(nn.Module):
         dual-output BN (its gradient is summed inside that BN's backward);
         it feeds the residual add, or the downsample branch when there is one."""
         if self._gemm_path(x):
-            return self._forward_gemm(x, identity, dual)
+            y, a, _ = self._forward_gemm(x, identity, dual)
+            return (y, a) if dual else y
         if self.downsample is not None:
             identity = self.downsample(x if identity is None else identity)
         elif identity is None:
@@ -85,6 +90,23 @@ class Bottleneck(nn.Module):
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out), identity, dual=dual)
+
+    def chain(self, x, identity, head, nxt: Optional["Bottleneck"]):
+        """One step of a chained bottleneck sequence: returns (y, alias, head).
+        ``head`` = (z1, sums) of this block's conv1, already computed by the
+        previous block's fused BN3→conv1 node (then ``x`` only feeds the
+        residual / downsample branch); ``nxt`` = the following block (None
+        for the last one). The returned ``head`` is set when this block
+        fused its BN3 with ``nxt``'s conv1, else ``alias`` is the dual-output
+        alias of ``y`` for ``nxt``'s residual (or None after the last block)."""
+        if self._gemm_path(x):
+            return self._forward_gemm(x, identity, nxt is not None, head, nxt)
+        if head is not None:
+            raise RuntimeError("chained conv1 output handed to a block off the fused GEMM path")
+        if nxt is None:
+            return self.forward(x, identity, dual=False), None, None
+        y, a = self.forward(x, identity, dual=True)
+        return y, a, None
 
     def _gemm_path(self, x: torch.Tensor) -> bool:
         if not (self.fused_gemm and self.training and self.bn1.fused and self.bn2.fused and self.bn3.fused):
@@ -98,12 +120,13 @@ class Bottleneck(nn.Module):
         return (gemm_ok(x, self.conv1.in_channels, self.conv1.out_channels)
                 and self.conv3.out_channels % 64 == 0 and self.conv3.in_channels % 64 == 0)
 
-    def _forward_gemm(self, x, identity, dual):
+    def _forward_gemm(self, x, identity, dual, head=None, nxt=None):
         """conv1 (GEMM, BN1 sums in its epilogue) → BN1+ReLU apply → conv2
         (MIOpen 3x3) → BN2 statistics → conv3 GEMM with BN2+ReLU applied in its
         prologue and BN3 sums in its epilogue → BN3 + residual + ReLU apply.
         Per block this drops the BN1/BN3 statistics passes and BN2's apply
-        (a full write + read of the 3x3 conv's activation)."""
+        (a full write + read of the 3x3 conv's activation). Returns (y, alias
+        or None, next block's conv1 head or None) — see :meth:`chain`."""
         inp = x if identity is None else identity
         resbn = None  # (downsample BN, its raw input, its sums): applied inside BN3's kernel
         if self.downsample is not None:
@@ -122,13 +145,13 @@ class Bottleneck(nn.Module):
                 identity = bn(z, stats=st)
         else:
             identity = inp
-        z1, s1 = gemm_conv1x1(x, self.conv1.weight, stats=True)
+        z1, s1 = head if head is not None else gemm_conv1x1(x, self.conv1.weight, stats=True)
         c2 = self.conv2
         s2 = None
         if KXK_GEMM and BN_CONV_FUSE and conv_kxk_gemm_ok(z1, c2):
             x2, s2 = bn_relu_conv(z1, self.bn1, c2.weight, c2.kernel_size[0], c2.stride[0], c2.padding[0], sums=s1,
                                   stats=True)
-            return self._tail(x2, s2, identity, dual, True, resbn)
+            return self._tail(x2, s2, identity, dual, True, resbn, nxt)
         y1 = self.bn1(z1, stats=s1)
         if KXK_GEMM and conv_kxk_gemm_ok(y1, c2):
             ho = (y1.shape[2] + 2 * c2.padding[0] - c2.kernel_size[0]) // c2.stride[0] + 1
@@ -143,10 +166,10 @@ class Bottleneck(nn.Module):
             x2 = c2(y1)
         if not x2.is_contiguous(memory_format=torch.channels_last):
             x2 = x2.contiguous(memory_format=torch.channels_last)
-        return self._tail(x2, s2, identity, dual, False, resbn)
+        return self._tail(x2, s2, identity, dual, False, resbn, nxt)
 
-    def _tail(self, x2, s2, identity, dual, fuse, resbn=None):
-        """BN2 → conv3 → BN3 (+ residual, ReLU)."""
+    def _tail(self, x2, s2, identity, dual, fuse, resbn=None, nxt=None):
+        """BN2 → conv3 → BN3 (+ residual, ReLU) [→ nxt's conv1]: (y, alias, head)."""
         if self.conv3.out_channels <= PRO_MAX_COUT:
             # BN2+ReLU applied in the GEMM prologue (its output never hits HBM)
             z3, s3 = bn_relu_conv1x1(x2, self.bn2, self.conv3.weight, stats=True, sums=s2)
@@ -157,12 +180,18 @@ class Bottleneck(nn.Module):
             # wide conv3: every N-tile re-applies the prologue to the same rows,
             # which costs more than one apply pass over the narrow input
             z3, s3 = gemm_conv1x1(self.bn2(x2, stats=s2), self.conv3.weight, stats=True)
+        if (nxt is not None and RES_CONV_FUSE and res_conv_fuse_ok(self.bn3, z3, s3, nxt.conv1)
+                and nxt._gemm_path(z3) and (resbn is None or resbn_ok(self.bn3, z3, s3))):
+            y, z1, sums1 = bn_res_act_conv1x1(self.bn3, z3, s3, identity, nxt.conv1.weight, resbn)
+            return y, None, (z1, sums1)
         if resbn is not None:
             if resbn_ok(self.bn3, z3, s3):
                 bn, z, st = resbn
-                return bn_resbn_act(self.bn3, z3, s3, bn, z, st, dual)
+                out = bn_resbn_act(self.bn3, z3, s3, bn, z, st, dual)
+                return (out[0], out[1], None) if dual else (out, None, None)
             identity = resbn[0](resbn[1], stats=resbn[2])
-        return self.bn3(z3, identity, dual=dual, stats=s3)
+        out = self.bn3(z3, identity, dual=dual, stats=s3)
+        return (out[0], out[1], None) if dual else (out, None, None)
 
 
 class BottleneckStage(nn.Sequential):
@@ -231,6 +260,15 @@ class ResNet(nn.Module):
         stage.use_dual = self.dual_bn
         return stage
 
+    def _chain(self, x, a):
+        """Every bottleneck of the four stages as one chain (block i's BN3 fused
+        with block i+1's conv1 where both run on the GEMM path)."""
+        blocks = [b for st in (self.layer1, self.layer2, self.layer3, self.layer4) for b in st]
+        head = None
+        for i, blk in enumerate(blocks):
+            x, a, head = blk.chain(x, a, head, blocks[i + 1] if i + 1 < len(blocks) else None)
+        return x
+
     def _weight_prep(self):
         """Context that casts every bottleneck conv weight to its bf16 GEMM
         operands in one launch (training on the fused GEMM path), else a no-op."""
@@ -256,7 +294,9 @@ class ResNet(nn.Module):
         if (FUSED_STEM and self.fused_bn and isinstance(self.maxpool, FusedMaxPool2d)
                 and stem_supported(x, self.conv1, self.bn1, self.training)):
             # stem GEMM + BN + ReLU + max-pool in one node (no MIOpen, no ATen casts)
-            if self.dual_bn:
+            if self.dual_bn and RES_CONV_FUSE:
+                x = self._chain(*fused_stem(x, self.conv1, self.bn1, dual=True))
+            elif self.dual_bn:
                 x, a = fused_stem(x, self.conv1, self.bn1, dual=True)
                 x, a = self.layer1(x, a, True)
                 x, a = self.layer2(x, a, True)
@@ -273,10 +313,13 @@ class ResNet(nn.Module):
                 x, a = self.maxpool(x, dual=True)
             else:
                 x, a = self.maxpool(x), None
-            x, a = self.layer1(x, a, True)
-            x, a = self.layer2(x, a, True)
-            x, a = self.layer3(x, a, True)
-            x = self.layer4(x, a, False)
+            if RES_CONV_FUSE:
+                x = self._chain(x, a)
+            else:
+                x, a = self.layer1(x, a, True)
+                x, a = self.layer2(x, a, True)
+                x, a = self.layer3(x, a, True)
+                x = self.layer4(x, a, False)
         else:
             x = self.layer4(self.layer3(self.layer2(self.layer1(self.maxpool(x)))))
         x = global_avg_pool_flat(x) if self.fused_bn else torch.flatten(self.avgpool(x), 1)

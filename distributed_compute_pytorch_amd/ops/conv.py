@@ -169,6 +169,96 @@ def bn_relu_conv1x1(x: torch.Tensor, bn, weight: torch.Tensor, stats: bool = Fal
                                   bn.eps, stats, sums)
 
 
+class _BNResActConv1x1Fn(torch.autograd.Function):
+    """Block boundary of a bottleneck chain, training mode:
+    ``y = relu(bn3(z3) + r)`` with ``r`` the identity or ``bn_d(x2)`` (the
+    downsample BN folded in), and the NEXT block's ``z1 = conv1x1(y, w)``
+    (+ its BN1 sums). Returns (y, z1, sums): ``y`` feeds the next block's
+    residual / downsample branch, ``z1`` its BN1.
+
+    Backward: the conv1 data-gradient GEMM's epilogue adds the residual
+    branch's gradient of ``y``, applies BN3's ReLU bits and reduces BN3's
+    (and the downsample BN's) backward sums (gemm.hip RESRED) — it writes the
+    masked gradient g, which is also the identity's gradient; BN3's separate
+    reduce pass over (dy, dy2, z3) disappears and one apply pass per BN
+    remains. Reference parity: the plain ``bn3 → add → relu → conv1``
+    composition (``/root/reference/main.py`` trains through stock
+    autograd)."""
+
+    @staticmethod
+    def forward(ctx, z3, gamma, beta, residual, x2, gamma2, beta2, w_next, rm, rv, nbt, stats, rm2, rv2, nbt2,
+                stats2, momentum, eps, momentum2, eps2):
+        ctx.set_materialize_grads(False)
+        if x2 is not None:
+            y, mean, invstd, bits, mean2, invstd2 = _C.bn_resbn_act_fwd(
+                z3, gamma, beta, rm, rv, nbt, stats, x2, gamma2, beta2, rm2, rv2, nbt2, stats2, float(momentum),
+                float(eps), float(momentum2), float(eps2))
+        else:
+            y, mean, invstd, bits = _C.bn_act_fwd(z3, gamma, beta, rm, rv, residual, True, float(momentum),
+                                                  float(eps), True, nbt, stats)
+            mean2 = invstd2 = None
+        w, wt = _w2d(w_next)
+        z1, s1 = _C.conv1x1_fwd(y, w, None, None, False, True)
+        ctx.save_for_backward(z3, gamma, mean, invstd, bits, y, wt, x2, gamma2, mean2, invstd2)
+        ctx.wshape, ctx.wdtype = w_next.shape, w_next.dtype
+        ctx.mark_non_differentiable(s1)
+        return y, z1, s1
+
+    @staticmethod
+    def backward(ctx, gy, gz, _gs):
+        z3, gamma, mean, invstd, bits, y, wt, x2, gamma2, mean2, invstd2 = ctx.saved_tensors
+        if gz is None:
+            gz = torch.zeros((y.shape[0], ctx.wshape[0]) + tuple(y.shape[2:]), device=y.device, dtype=y.dtype)
+        gz = _cl(gz)
+        dw = _C.conv1x1_wgrad(gz, y).view(ctx.wshape)
+        if dw.dtype != ctx.wdtype:
+            dw = dw.to(ctx.wdtype)
+        g, acc, acc2 = _C.conv1x1_dgrad_resred(gz, wt, z3, None if gy is None else _cl(gy), mean, bits, x2, mean2)
+        dz3, dgamma, dbeta = _C.bn_bwd_apply_g(g, z3, gamma, mean, invstd, acc)
+        dres = dx2 = dgamma2 = dbeta2 = None
+        if x2 is not None:
+            dx2, dgamma2, dbeta2 = _C.bn_bwd_apply_g(g, x2, gamma2, mean2, invstd2, acc2)
+        else:
+            dres = g  # relu mask already applied: the identity's gradient
+        return (dz3, dgamma, dbeta, dres, dx2, dgamma2, dbeta2, dw) + (None,) * 12
+
+
+def bn_res_act_conv1x1(bn3, z3: torch.Tensor, s3: torch.Tensor, identity: Optional[torch.Tensor], w_next,
+                       resbn=None):
+    """(y, z1, sums1) = (relu(bn3(z3) + identity-or-bn_d(x2)), conv1x1(y, w_next), Σ/Σ² of z1)
+    for training-mode BatchNorms whose input sums come from their GEMM epilogues
+    (``s3``; ``resbn`` = (bn_d, x2, s2)). Same parameters, buffers and running-
+    statistic updates as the unfused composition."""
+
+    def _nbt(m):
+        t = m.num_batches_tracked
+        if t is not None and (t.device != z3.device or t.dtype != torch.int64):
+            t.add_(1)
+            return None
+        return t
+
+    if resbn is not None:
+        bn_d, x2, s2 = resbn
+        return _BNResActConv1x1Fn.apply(z3, bn3.weight, bn3.bias, None, x2, bn_d.weight, bn_d.bias, w_next,
+                                        bn3.running_mean, bn3.running_var, _nbt(bn3), s3, bn_d.running_mean,
+                                        bn_d.running_var, _nbt(bn_d), s2, bn3.momentum, bn3.eps, bn_d.momentum,
+                                        bn_d.eps)
+    return _BNResActConv1x1Fn.apply(z3, bn3.weight, bn3.bias, identity, None, None, None, w_next, bn3.running_mean,
+                                    bn3.running_var, _nbt(bn3), s3, None, None, None, None, bn3.momentum, bn3.eps,
+                                    0.0, 0.0)
+
+
+def res_conv_fuse_ok(bn3, z3: torch.Tensor, s3, next_conv) -> bool:
+    """True when :func:`bn_res_act_conv1x1` handles BN3 ``bn3`` over ``z3`` feeding
+    the 1x1 stride-1 conv ``next_conv``."""
+    return (bn3.training and bn3.affine and bn3.track_running_stats and bn3.momentum is not None
+            and s3 is not None and s3.numel() == 2 * z3.shape[1] and bn3.weight.dtype == torch.float32
+            and next_conv.kernel_size == (1, 1) and next_conv.stride == (1, 1) and next_conv.bias is None
+            and next_conv.groups == 1 and next_conv.in_channels == z3.shape[1]
+            and next_conv.out_channels % 64 == 0 and next_conv.weight.dtype == torch.float32
+            and gemm_ok(z3, next_conv.in_channels, next_conv.out_channels))
+
+
 class _BNReluConvFn(torch.autograd.Function):
     """conv(relu(bn(x))) for a training-mode BatchNorm whose output is
     materialised (wide consumers, or gathered kxk convs where padding taps

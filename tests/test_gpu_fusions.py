@@ -4,6 +4,8 @@
   residual kernel (ops/batchnorm.py bn_resbn_act): outputs, both sets of
   running statistics, and every gradient (x, x2, both gammas / betas), with a
   dual-output (two consumers) upstream gradient;
+* the block-boundary node relu(bn3(z3) + r) → next conv1 with BN3's backward
+  reduction in the conv1 data-gradient epilogue (ops/conv.py bn_res_act_conv1x1);
 * ConvWeightPrep: every conv's bf16 GEMM operands from one launch are
   bit-identical to the per-conv cast kernels, and a ResNet step with it equals
   the step without it.
@@ -115,6 +117,95 @@ def test_resnet_step_with_prep_and_resbn_matches_plain(cuda, monkeypatch):
     # a random-init bf16 bottleneck net at batch 8 amplifies rounding-order noise
     # (atomic BN sums, MIOpen) into 10-20 % on BN-bias gradients between two
     # identical runs; a wrong kernel gives O(1) or non-finite differences
+    err = float((g1 - g2).norm() / g2.norm())
+    noise = float((g3 - g2).norm() / g2.norm())
+    assert bool(torch.isfinite(g1).all())
+    assert err < 4 * noise + 0.05, (err, noise)
+    torch.testing.assert_close(b1, b2, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("C,Co,N,hw,resbn", [(256, 64, 4, 14, False), (256, 64, 4, 14, True),
+                                             (512, 128, 3, 9, False), (1024, 256, 2, 7, True)])
+def test_bn_res_act_conv1x1_matches_reference(cuda, C, Co, N, hw, resbn):
+    """Block boundary node (ops/conv.py bn_res_act_conv1x1): relu(bn3(z3) + r)
+    → next conv1, with BN3's backward reduced in conv1's dgrad epilogue
+    (gemm.hip RESRED), against the fp32 composition: outputs, sums, running
+    statistics and every gradient. M = N·hw² is ragged for hw = 9, 7."""
+    from distributed_compute_pytorch_amd.ops.batchnorm import BatchNormAct2d
+    from distributed_compute_pytorch_amd.ops.conv import bn_res_act_conv1x1
+
+    torch.manual_seed(1)
+    cl = torch.channels_last
+    bn3 = BatchNormAct2d(C, act=True, residual=True, fused=True).to(cuda)
+    bnd = BatchNormAct2d(C, act=False, fused=True).to(cuda)
+    with torch.no_grad():
+        for m in (bn3, bnd):
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.uniform_(-0.5, 0.5)
+    ref3, refd = copy.deepcopy(bn3), copy.deepcopy(bnd)
+    w = (torch.randn(Co, C, 1, 1, device=cuda) / C ** 0.5).contiguous(memory_format=cl).requires_grad_(True)
+    z3 = (torch.randn(N, C, hw, hw, device=cuda) * 1.5 + 0.2).to(torch.bfloat16).contiguous(memory_format=cl)
+    r = (torch.randn(N, C, hw, hw, device=cuda) * 0.8).to(torch.bfloat16).contiguous(memory_format=cl)
+    gy = torch.randn(N, C, hw, hw, device=cuda).to(torch.bfloat16).contiguous(memory_format=cl)
+    gz = torch.randn(N, Co, hw, hw, device=cuda).to(torch.bfloat16).contiguous(memory_format=cl)
+
+    za = z3.detach().clone().requires_grad_(True)
+    ra = r.detach().clone().requires_grad_(True)
+    if resbn:
+        y, z1, s1 = bn_res_act_conv1x1(bn3, za, _sums(z3), None, w, (bnd, ra, _sums(r)))
+    else:
+        y, z1, s1 = bn_res_act_conv1x1(bn3, za, _sums(z3), ra, w)
+    torch.autograd.backward([y, z1], [gy, gz])
+
+    zr = z3.float().requires_grad_(True)
+    rr = r.float().requires_grad_(True)
+    wr = w.detach().float().clone().requires_grad_(True)
+    res = (F.batch_norm(rr, refd.running_mean, refd.running_var, refd.weight, refd.bias, True, 0.1, 1e-5)
+           if resbn else rr)
+    yr = F.relu(F.batch_norm(zr, ref3.running_mean, ref3.running_var, ref3.weight, ref3.bias, True, 0.1, 1e-5)
+                + res)
+    z1r = F.conv2d(yr, wr)
+    torch.autograd.backward([yr, z1r], [gy.float(), gz.float()])
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+    assert rel(y, yr) < 1e-2
+    assert rel(z1, z1r) < 2e-2
+    torch.testing.assert_close(s1, _sums(z1), rtol=1e-2, atol=1e-1)
+    torch.testing.assert_close(bn3.running_mean, ref3.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn3.running_var, ref3.running_var, rtol=1e-4, atol=1e-5)
+    assert rel(za.grad, zr.grad) < 3e-2, rel(za.grad, zr.grad)
+    assert rel(ra.grad, rr.grad) < 3e-2, rel(ra.grad, rr.grad)
+    assert rel(w.grad, wr.grad) < 2e-2
+    pairs = [(bn3, ref3)] + ([(bnd, refd)] if resbn else [])
+    for a, b in pairs:
+        assert rel(a.weight.grad, b.weight.grad) < 3e-2, rel(a.weight.grad, b.weight.grad)
+        assert rel(a.bias.grad, b.bias.grad) < 3e-2, rel(a.bias.grad, b.bias.grad)
+
+
+def test_resnet_step_chain_fusion_matches_unfused(cuda, monkeypatch):
+    """A bf16 training step of a small bottleneck ResNet with every BN3 fused
+    into the next block's conv1 node (DCP_RES_CONV_FUSE) equals the unfused
+    chain within the run-to-run noise floor."""
+    import distributed_compute_pytorch_amd.models.resnet as R
+
+    torch.manual_seed(0)
+    base = R.ResNet(R.Bottleneck, [2, 2, 1, 1], num_classes=10, fused_bn=True).to(cuda).to(
+        memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 64, 64, device=cuda).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=cuda)
+    res = []
+    for on in (True, False, False):
+        monkeypatch.setattr(R, "RES_CONV_FUSE", on)
+        m = copy.deepcopy(base)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        res.append((float(loss), torch.cat([p.grad.float().reshape(-1) for p in m.parameters()]),
+                    torch.cat([b.float().reshape(-1) for b in m.buffers()])))
+    (l1, g1, b1), (l2, g2, b2), (_, g3, _) = res
+    assert abs(l1 - l2) < 1e-2 * max(1.0, abs(l2)), (l1, l2)
     err = float((g1 - g2).norm() / g2.norm())
     noise = float((g3 - g2).norm() / g2.norm())
     assert bool(torch.isfinite(g1).all())
