@@ -353,26 +353,31 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   float ssum[8], ssq[8], ss2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = ss2[e] = 0.f;
-  // RED: mean and the forward's folded affine of the block's BN columns, in
-  // LDS (registers would push the kernel past 256 and halve occupancy)
-  float* redc = pro;  // [3][BN]: mean, scale, shift
+  // RED: mean and the forward's folded affine of this lane's 8 epilogue
+  // channels, in registers (an LDS copy takes the workgroup past 80 KB: one
+  // workgroup per CU)
+  float dmu[RED ? 8 : 1], dsc[RED ? 8 : 1], dsf[RED ? 8 : 1];
   if (RED) {
-    if (t < BN) {
-      const int c = n0 + t;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = n0 + wn * WN + (lane % LPR) * 8 + k;
       const float mu = bnr.mean[c];
       const float sc = (bnr.gamma ? bnr.gamma[c] : 1.f) * bnr.invstd[c];
-      redc[t] = mu;
-      redc[BN + t] = sc;
-      redc[2 * BN + t] = (bnr.beta ? bnr.beta[c] : 0.f) - mu * sc;
+      dmu[RED ? k : 0] = mu;
+      dsc[RED ? k : 0] = sc;
+      dsf[RED ? k : 0] = (bnr.beta ? bnr.beta[c] : 0.f) - mu * sc;
     }
-    __syncthreads();  // nothing in flight yet
   }
-  if (RR) {  // [2][BN]: mean, mean2 of the block's columns
-    if (t < BN) {
-      redc[t] = bnr.mean[n0 + t];
-      if (X2) redc[BN + t] = bnr.mean2[n0 + t];
+  // RESRED: mean (mean2) of this lane's 8 epilogue channels in registers — an
+  // LDS copy would take the workgroup past 80 KB and one workgroup per CU
+  float rmu[RR ? 8 : 1], rmu2[X2 ? 8 : 1];
+  if (RR) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = n0 + wn * WN + (lane % LPR) * 8 + k;
+      rmu[RR ? k : 0] = bnr.mean[c];
+      if (X2) rmu2[X2 ? k : 0] = bnr.mean2[c];
     }
-    __syncthreads();
   }
 
 #pragma unroll
@@ -508,7 +513,6 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, y4[4] = {g2.x, g2.y, g2.z, g2.w};
             const uint32_t x4[4] = {xv.x, xv.y, xv.z, xv.w};
             const uint32_t mb = mbr[RR ? (HB - 1) * h * NR + it : 0];
-            const int cb = wn * WN + c * 8;
             float gk[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -517,7 +521,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
               const float xk = (k & 1) ? bf_hi(x4[k >> 1]) : bf_lo(x4[k >> 1]);
               gk[k] = (mb >> k) & 1u ? a + b : 0.f;
               ssum[k] += gk[k];
-              ssq[k] = fmaf(gk[k], xk - redc[cb + k], ssq[k]);
+              ssq[k] = fmaf(gk[k], xk - rmu[RR ? k : 0], ssq[k]);
             }
             if (X2) {
               const uint4 x2v = x2r[X2 ? (HB - 1) * h * NR + it : 0];
@@ -525,7 +529,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
 #pragma unroll
               for (int k = 0; k < 8; ++k) {
                 const float zk = (k & 1) ? bf_hi(z4[k >> 1]) : bf_lo(z4[k >> 1]);
-                ss2[k] = fmaf(gk[k], zk - redc[BN + cb + k], ss2[k]);
+                ss2[k] = fmaf(gk[k], zk - rmu2[X2 ? k : 0], ss2[k]);
               }
             }
             *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) =
@@ -547,14 +551,13 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
               const uint4 xv = xr[RED ? (HB - 1) * h * NR + it : 0];
               const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
               const uint32_t x4[4] = {xv.x, xv.y, xv.z, xv.w};
-              const int cb = wn * WN + c * 8;
 #pragma unroll
               for (int k = 0; k < 8; ++k) {
                 const float xk = (k & 1) ? bf_hi(x4[k >> 1]) : bf_lo(x4[k >> 1]);
                 float gk = (k & 1) ? bf_hi(w4[k >> 1]) : bf_lo(w4[k >> 1]);
-                gk = fmaf(xk, redc[BN + cb + k], redc[2 * BN + cb + k]) > 0.f ? gk : 0.f;
+                gk = fmaf(xk, dsc[RED ? k : 0], dsf[RED ? k : 0]) > 0.f ? gk : 0.f;
                 ssum[k] += gk;
-                ssq[k] = fmaf(gk, xk - redc[cb + k], ssq[k]);
+                ssq[k] = fmaf(gk, xk - dmu[RED ? k : 0], ssq[k]);
               }
             }
           }
@@ -1319,7 +1322,7 @@ void gemm_nt_launch_bm(const void* A, const void* B, void* C, int64_t M, int N, 
   const int nw = (BM / 64) * (BN == 64 && BM == 256 ? 1 : 2);
   const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 +
                      static_cast<size_t>(nw) * 32 * (BN * 2 / (BM == 256 && BN == 64 ? 1 : 2)) +
-                     (pro ? 8 * static_cast<size_t>(K) : 0) + (red ? 12 * static_cast<size_t>(BN) : 0);
+                     (pro ? 8 * static_cast<size_t>(K) : 0);
   const int NT = 64 * nw;
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
