@@ -31,11 +31,13 @@ GEMM_MAX_INTENSITY = float(os.environ.get("DCP_GEMM_MAX_INTENSITY", "1024"))
 KXK_WGRAD = os.environ.get("DCP_KXK_WGRAD", "0") == "1"
 # 3x3 conv2 on the implicit-GEMM MFMA kernels (fwd + BN2 sums, stride-1 dgrad)
 KXK_GEMM = os.environ.get("DCP_KXK_GEMM", "1") == "1"
-# opt-in: BN1→conv2 and BN2→conv3 as one autograd node whose data-gradient GEMM
-# reduces the BN backward in its epilogue (gemm.hip RED). Measured −1 % on
-# ResNet-50 b256 (profiles/r1_bn_conv_fuse.log): the epilogue's per-element
-# VALU (~6 ops) costs the GEMM more than the separate 5 TB/s reduce pass.
-BN_CONV_FUSE = os.environ.get("DCP_BN_CONV_FUSE", "0") == "1"
+# BN1→conv2 / BN2→conv3 as one autograd node whose data-gradient GEMM reduces
+# the BN backward in its epilogue (gemm.hip RED). Bit mask: 1 = BN1→conv2
+# (stride-1 3x3 on the gathered GEMM, Cin > 64), 2 = BN2→conv3 (1x1, the wide
+# layers whose BN2 is not a GEMM prologue). Round 1 measured both −1 % (the RED
+# coefficients in LDS pushed the GEMM to one workgroup per CU); round 2 with
+# them in registers (profiles/r2_ab_bn_conv_fuse.jsonl): 2 = +0.3 %, 1 = −0.8 %.
+BN_CONV_FUSE = int(os.environ.get("DCP_BN_CONV_FUSE", "2") or 0)
 # BN-apply prologue in the conv3 GEMM only while Cout ≤ this (≤ 2 N-tiles of 128)
 PRO_MAX_COUT = int(os.environ.get("DCP_PRO_MAX_COUT", "256"))
 # conv1 + bn1 + relu + maxpool as one fused node (ops/stem.py); 0 = per-module path
@@ -148,10 +150,12 @@ class Bottleneck(nn.Module):
         z1, s1 = head if head is not None else gemm_conv1x1(x, self.conv1.weight, stats=True)
         c2 = self.conv2
         s2 = None
-        if KXK_GEMM and BN_CONV_FUSE and conv_kxk_gemm_ok(z1, c2):
+        fuse3 = bool(BN_CONV_FUSE & 2)
+        if (KXK_GEMM and BN_CONV_FUSE & 1 and conv_kxk_gemm_ok(z1, c2) and c2.stride == (1, 1)
+                and c2.in_channels > 64):
             x2, s2 = bn_relu_conv(z1, self.bn1, c2.weight, c2.kernel_size[0], c2.stride[0], c2.padding[0], sums=s1,
                                   stats=True)
-            return self._tail(x2, s2, identity, dual, True, resbn, nxt)
+            return self._tail(x2, s2, identity, dual, fuse3, resbn, nxt)
         y1 = self.bn1(z1, stats=s1)
         if KXK_GEMM and conv_kxk_gemm_ok(y1, c2):
             ho = (y1.shape[2] + 2 * c2.padding[0] - c2.kernel_size[0]) // c2.stride[0] + 1
@@ -166,7 +170,7 @@ class Bottleneck(nn.Module):
             x2 = c2(y1)
         if not x2.is_contiguous(memory_format=torch.channels_last):
             x2 = x2.contiguous(memory_format=torch.channels_last)
-        return self._tail(x2, s2, identity, dual, False, resbn, nxt)
+        return self._tail(x2, s2, identity, dual, fuse3, resbn, nxt)
 
     def _tail(self, x2, s2, identity, dual, fuse, resbn=None, nxt=None):
         """BN2 → conv3 → BN3 (+ residual, ReLU) [→ nxt's conv1]: (y, alias, head)."""
