@@ -65,3 +65,56 @@ def test_workload_steps_under_ddp(cuda, name, kw):
         assert all(torch.isfinite(torch.tensor(losses))), losses
     finally:
         dcp.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_gpt2_ddp_no_sync_accumulation_matches_local(cuda, amp):
+    """GPT-2 (fused kernels) under our DDP with no_sync gradient accumulation
+    over 2 micro-batches + fused AdamW, 2 optimizer steps, vs the same model
+    trained locally with plain autograd accumulation (world_size 1: the
+    all-reduce average is the identity, so any difference is the DDP /
+    in-kernel accumulation path). fp32: parameter updates to 1e-4; bf16:
+    updates against a noise floor of two local runs."""
+    import copy
+
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd import models
+    from distributed_compute_pytorch_amd.distributed.launch import free_port
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+    dcp.distributed.init_process_group("rccl", device_id=0)
+    try:
+        torch.manual_seed(0)
+        base = models.gpt2_small(n_layer=2, dropout=0.0, fused=True).to(cuda)  # deterministic masks
+        p0 = torch.cat([p.detach().float().reshape(-1) for p in base.parameters()])
+        data = [torch.randint(0, 50257, (2, 129), device=cuda) for _ in range(4)]
+
+        def train(use_ddp):
+            m = copy.deepcopy(base)
+            net = dcp.parallel.DistributedDataParallel(m, device_ids=[0], gradient_as_bucket_view=True) \
+                if use_ddp else m
+            opt = dcp.optim.AdamW(net.parameters(), lr=1e-3, weight_decay=0.01)
+            for s in range(2):
+                opt.zero_grad(set_to_none=True)
+                for k in range(2):
+                    seq = data[2 * s + k]
+                    ctx = net.no_sync() if (use_ddp and k == 0) else contextlib.nullcontext()
+                    with ctx:
+                        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+                            loss = net(seq[:, :-1], seq[:, 1:]) / 2
+                        loss.backward()
+                opt.step()
+            torch.cuda.synchronize()
+            return torch.cat([p.detach().float().reshape(-1) for p in m.parameters()]) - p0
+
+        import contextlib
+
+        d_ddp, d_loc, d_loc2 = train(True), train(False), train(False)
+        err = float((d_ddp - d_loc).norm() / d_loc.norm())
+        if amp:
+            noise = float((d_loc2 - d_loc).norm() / d_loc.norm())
+            assert err < 4 * noise + 2e-2, (err, noise)
+        else:
+            assert err < 1e-4, err
+    finally:
+        dcp.distributed.destroy_process_group()
