@@ -600,6 +600,28 @@ at::Tensor conv1x1_s2_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
 // dx of a stride-2 kxk conv as four parity-class implicit GEMMs (each dx
 // pixel written exactly once). wsubs: 4 bf16 [Cin][nkh][nkw][Cout] tensors for
 // (ph, pw) = (0,0), (0,1), (1,0), (1,1); x_hw: dx's H, W.
+// dx of a 3x3 / stride-2 / pad-1 NHWC conv: the four parity classes of dx as
+// ONE implicit-GEMM launch (gemm.hip MultiGeo); wperm = the flipped weight
+// bf16 [Cin][9][Cout] with its taps in class order 4 | 3 5 | 1 7 | 0 2 6 8.
+at::Tensor conv_dgrad_s2_multi(const at::Tensor& gy, const at::Tensor& wperm, int64_t H, int64_t W) {
+  check_gemm_act(gy, "conv_dgrad_s2_multi");
+  DCP_CHECK(gy.dim() == 4, "conv_dgrad_s2_multi: NHWC 4-D gradient required");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t N = gy.size(0), Co = gy.size(1), Hg = gy.size(2), Wg = gy.size(3);
+  DCP_CHECK(wperm.scalar_type() == at::kBFloat16 && wperm.is_contiguous() && wperm.dim() == 3 &&
+                wperm.size(1) == 9 && wperm.size(2) == Co,
+            "conv_dgrad_s2_multi: weight must be contiguous bf16 [Cin][9][Cout]");
+  const int64_t Ci = wperm.size(0);
+  DCP_CHECK(Ci % 64 == 0 && Co % 64 == 0 && N * H * W < (int64_t(1) << 31) && (H + 1) / 2 == Hg &&
+                (W + 1) / 2 == Wg,
+            "conv_dgrad_s2_multi: unsupported shape");
+  at::Tensor dx = at::empty({N, Ci, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  kern::conv_dgrad_s2_multi_bf16(gy.data_ptr(), wperm.data_ptr(), dx.data_ptr(), static_cast<int>(N),
+                                 static_cast<int>(Hg), static_cast<int>(Wg), static_cast<int>(Co), static_cast<int>(H),
+                                 static_cast<int>(W), static_cast<int>(Ci), zero_row(gy).data_ptr(), stream_of(gy));
+  return dx;
+}
+
 at::Tensor conv_dgrad_s2(const at::Tensor& gy, const std::vector<at::Tensor>& wsubs, int64_t H, int64_t W) {
   check_gemm_act(gy, "conv_dgrad_s2");
   DCP_CHECK(gy.dim() == 4 && wsubs.size() == 4, "conv_dgrad_s2: NHWC gy and 4 weight subsets required");
@@ -1295,6 +1317,8 @@ void bind(pybind11::module& m) {
   m.def("bn_resbn_act_fwd", &bn_resbn_act_fwd, "training relu(bn(x) + bn2(x2)), both BNs fused (downsample block)");
   m.def("bn_resbn_act_bwd", &bn_resbn_act_bwd, "backward of bn_resbn_act_fwd");
   m.def("conv1x1_s2_dgrad", &conv1x1_s2_dgrad, "stride-2 1x1 conv data gradient (GEMM + scattering epilogue)");
+  m.def("conv_dgrad_s2_multi", &conv_dgrad_s2_multi,
+        "3x3 stride-2 pad-1 conv data gradient: four parity classes in one implicit-GEMM launch");
   m.def("conv_dgrad_s2", &conv_dgrad_s2, "stride-2 kxk conv data gradient as four parity-class implicit GEMMs");
   m.def("conv_wgrad", &conv_wgrad, "kxk NHWC conv weight gradient (implicit-GEMM MFMA, fp32 out)",
         pybind11::arg("gy"), pybind11::arg("x"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"),

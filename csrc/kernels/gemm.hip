@@ -147,6 +147,22 @@ struct BnRedArgs {
   float* acc2;           // EPI 6: (Σg, Σg·(x2 - mean2)) [2N]
 };
 
+// Several parity classes of a stride-2 kxk data gradient in ONE launch
+// (EPI 4): workgroup tile ids [off[c], off[c+1]) belong to class c, one tile
+// per workgroup; each class has its own row grid / taps (g), rows (M), depth
+// (K) and weight subset (B, rows ldb apart: the classes' tap subsets are
+// consecutive tap ranges of one tap-permuted weight).
+struct MultiGeo {
+  int n;       // classes (0: a plain single-problem launch)
+  int ldb;     // B row stride (elements)
+  int off[5];  // tile-id prefix sums
+  int K[4];
+  int tiles_m[4];
+  int64_t M[4];
+  const uint16_t* B[4];
+  ConvGeo g[4];
+};
+
 // NT ring stages: BK=32 → 3 (two stages in flight), BK=64 → 2; either way
 // ≤ 64 KB of ring + 16 KB of per-wave C staging keeps 2 blocks per CU
 template <int BK>
@@ -186,7 +202,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int relu,
                                                      float* __restrict__ stats, int tiles_m, int tn, ConvGeo geo,
-                                                     BnRedArgs bnr) {
+                                                     BnRedArgs bnr, MultiGeo mg = MultiGeo{}) {
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
   constexpr bool STATS = EPI == 1;
   constexpr bool RED = EPI == 2;
@@ -232,10 +248,27 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   // contiguous tile range, so the tn n-tiles of an m-tile run on one XCD and
   // share A through its L2. Persistent when tiles > P: tile v, v+P, … (P % tn
   // == 0 keeps the block's n-tile — and its STATS channels — fixed).
-  const int P = static_cast<int>(gridDim.x);
+  int P = static_cast<int>(gridDim.x);
   const int wid = static_cast<int>(blockIdx.x);
   const int xcd = wid & 7, q8 = P >> 3, r8 = P & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
+  int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
+  int64_t ldb = K;
+  if constexpr (PAR) {
+    if (mg.n > 0) {  // multi-class launch: this workgroup's class, one tile
+      int c = 0;
+#pragma unroll
+      for (int i = 1; i < 4; ++i) c += (i < mg.n && wg >= mg.off[i]) ? 1 : 0;
+      c = __builtin_amdgcn_readfirstlane(c);
+      B = mg.B[c];
+      M = mg.M[c];
+      K = mg.K[c];
+      tiles_m = mg.tiles_m[c];
+      geo = mg.g[c];
+      ldb = mg.ldb;
+      P = mg.off[c + 1] - mg.off[c];
+      wg -= mg.off[c];
+    }
+  }
   const int n0 = (wg % tn) * BN;
   const int KT = K / BK;
   const int my_tiles = (tiles_m * tn - wg + P - 1) / P;
@@ -299,7 +332,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   for (int j = 0; j < NB; ++j) {
     const int p = (wave * NB + j) * 64 + lane;
     const int r = p / CPR, lc = (p % CPR) ^ nt_swzk<BK>(p / CPR);
-    bsrc[j] = B + static_cast<int64_t>(n0 + r) * K + lc * 8;
+    bsrc[j] = B + static_cast<int64_t>(n0 + r) * ldb + lc * 8;
   }
   set_a(wg);
   auto issue = [&]() {
@@ -450,25 +483,37 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       constexpr int HB = X2 ? 1 : 2;  // halves loaded ahead
       uint4 xr[(RED || RR) ? HB * NR : 1], g2r[RR ? HB * NR : 1], x2r[X2 ? HB * NR : 1];
       uint32_t mbr[RR ? HB * NR : 1];
-      auto epi_load = [&](int h0) {
-        const bool has2 = RR && bnr.gy2 != nullptr;
-#pragma unroll
-        for (int i = 0; i < HB * NR; ++i) {
-          const int64_t m = mt + 32 * (h0 + i / NR) + (i % NR) * RPI + lane / LPR;
-          const int64_t o = m * N + n0 + wn * WN + (lane % LPR) * 8;
-          const uint4 z = make_uint4(0, 0, 0, 0);
-          xr[i] = m < M ? *reinterpret_cast<const uint4*>(bnr.x + o) : z;
-          if (RR) {
-            g2r[RR ? i : 0] = (m < M && has2) ? *reinterpret_cast<const uint4*>(bnr.gy2 + o) : z;
-            mbr[RR ? i : 0] = m < M ? bnr.bits[o >> 3] : 0u;
-          }
-          if (X2) x2r[X2 ? i : 0] = m < M ? *reinterpret_cast<const uint4*>(bnr.x2 + o) : z;
-        }
-      };
-      if ((RED || RR) && HB == 2) epi_load(0);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        if ((RED || RR) && HB == 1) epi_load(h);
+        if ((RED || RR) && (HB == 1 || h == 0)) {
+          // (a plain loop, not a lambda: a lambda capturing the arrays by
+          // reference left dead scratch stores of them in the epilogue)
+          const int h0 = HB == 1 ? h : 0;
+          const bool has2 = RR && bnr.gy2 != nullptr;
+#pragma unroll
+          for (int i = 0; i < HB * NR; ++i) {
+            const int64_t m = mt + 32 * (h0 + i / NR) + (i % NR) * RPI + lane / LPR;
+            // rows past M load row 0 and select zero AFTER the load: a
+            // `m < M ? *p : zero` form is turned into a select of pointers
+            // to a scratch copy of the zero (flat loads + scratch stores)
+            const bool ok = m < M;
+            const int64_t o = (ok ? m : 0) * N + n0 + wn * WN + (lane % LPR) * 8;
+            const uint4 z = make_uint4(0, 0, 0, 0);
+            const uint4 xv = *reinterpret_cast<const uint4*>(bnr.x + o);
+            xr[i] = ok ? xv : z;
+            if (RR) {
+              uint4 gv = z;
+              if (has2) gv = *reinterpret_cast<const uint4*>(bnr.gy2 + o);
+              g2r[RR ? i : 0] = ok ? gv : z;
+              const uint32_t bv = bnr.bits[o >> 3];
+              mbr[RR ? i : 0] = ok ? bv : 0u;
+            }
+            if (X2) {
+              const uint4 x2v = *reinterpret_cast<const uint4*>(bnr.x2 + o);
+              x2r[X2 ? i : 0] = ok ? x2v : z;
+            }
+          }
+        }
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const int j = 2 * h + jj;
@@ -1459,6 +1504,58 @@ void conv_dgrad_parity_bf16(const void* dY, const void* Wsub, void* dX, int N, i
   else
     gemm_nt_launch_bk<true, 32>(dY, Wsub, dX, M, Cin, K, nullptr, nullptr, false, nullptr, geo, nullptr, s, false,
                                 true);
+}
+
+namespace {
+template <int BK, int BN>
+void dgrad_s2_multi_launch(const void* dY, void* dX, int64_t tiles, const MultiGeo& mg, int Cin, hipStream_t s) {
+  constexpr int BM = 128;
+  const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 + 4 * 32 * (BN * 2 / 2);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 4, true, BK>), dim3(static_cast<unsigned>(tiles)),
+                     dim3(nt_threads<BM, BN>()), lds, s, static_cast<const uint16_t*>(dY), mg.B[0],
+                     static_cast<uint16_t*>(dX), mg.M[0], Cin, mg.K[0], nullptr, nullptr, 0, nullptr, mg.tiles_m[0],
+                     Cin / BN, mg.g[0], BnRedArgs{}, mg);
+}
+}  // namespace
+
+void conv_dgrad_s2_multi_bf16(const void* dY, const void* Wperm, void* dX, int N, int Hg, int Wg, int Cout, int Hdx,
+                              int Wdx, int Cin, const void* zero, hipStream_t s) {
+  // 3x3 / stride 2 / pad 1: class (ph, pw) takes kernel rows kh' = {1} (ph = 0)
+  // or {0, 2} (ph = 1) of the flipped weight — gy row offsets +0 / +0, +1 —
+  // and the same for columns; Wperm = [Cin][9 taps: 4 | 3 5 | 1 7 | 0 2 6 8][Cout]
+  MultiGeo mg{};
+  constexpr int BM = 128;
+  const int BN = Cin % 128 == 0 ? 128 : 64;
+  const int tn = Cin / BN;
+  const auto* w = static_cast<const uint16_t*>(Wperm);
+  int64_t tiles = 0;
+  int tap0 = 0;
+  for (int q = 0; q < 4; ++q) {
+    const int ph = q >> 1, pw = q & 1;
+    const int nkh = ph ? 2 : 1, nkw = pw ? 2 : 1;
+    const int Hq = (Hdx - ph + 1) / 2, Wq = (Wdx - pw + 1) / 2;
+    if (Hq > 0 && Wq > 0) {
+      const int c = mg.n++;
+      mg.g[c] = ConvGeo{Hg, Wg, Hq, Wq, 1, 0, nkw, static_cast<const uint16_t*>(zero), Cout, Hdx, Wdx, ph, pw};
+      mg.M[c] = static_cast<int64_t>(N) * Hq * Wq;
+      mg.K[c] = nkh * nkw * Cout;
+      mg.B[c] = w + static_cast<int64_t>(tap0) * Cout;
+      mg.tiles_m[c] = static_cast<int>((mg.M[c] + BM - 1) / BM);
+      mg.off[c] = static_cast<int>(tiles);
+      tiles += static_cast<int64_t>(mg.tiles_m[c]) * tn;
+    }
+    tap0 += nkh * nkw;
+  }
+  mg.off[mg.n] = static_cast<int>(tiles);
+  mg.ldb = 9 * Cout;
+  if (tiles == 0) return;
+  if (nt_bk() == 64) {
+    if (BN == 128) dgrad_s2_multi_launch<64, 128>(dY, dX, tiles, mg, Cin, s);
+    else dgrad_s2_multi_launch<64, 64>(dY, dX, tiles, mg, Cin, s);
+  } else {
+    if (BN == 128) dgrad_s2_multi_launch<32, 128>(dY, dX, tiles, mg, Cin, s);
+    else dgrad_s2_multi_launch<32, 64>(dY, dX, tiles, mg, Cin, s);
+  }
 }
 
 bool conv_fwd_supported(int Cin, int Cout, int kh, int kw) {

@@ -81,6 +81,11 @@ void gemm_nt_bnred_bf16(const void* A, const void* B, void* C, int64_t M, int N,
 void gemm_nt_resred_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
                          const float* mean, const void* gy2, const uint8_t* bits, float* acc, const void* x2,
                          const float* mean2, float* acc2, hipStream_t s);
+// 3x3 / stride-2 / pad-1 conv data gradient, all four parity classes of dX in
+// ONE implicit-GEMM launch; Wperm = the flipped weight [Cin][9][Cout] with its
+// taps in class order (4 | 3 5 | 1 7 | 0 2 6 8). dX fully written.
+void conv_dgrad_s2_multi_bf16(const void* dY, const void* Wperm, void* dX, int N, int Hg, int Wg, int Cout, int Hdx,
+                              int Wdx, int Cin, const void* zero, hipStream_t s);
 void conv_fwd_bnred_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo,
                          int Cout, int kh, int kw, int stride, int pad, const void* zero, const void* x,
                          const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,

@@ -74,6 +74,43 @@ class ConvWeightPrep:
                 and w.permute(0, 2, 3, 1).is_contiguous())
 
 
+# Weight gradient on a side stream, concurrent with the same node's data-
+# gradient GEMM, for GEMMs of at most this many rows (0 = off): the compute-
+# bound layer-3/4 GEMMs end in a partial round of tiles that the other
+# kernel's workgroups can fill.
+WGRAD_SIDE_MAXM = int(os.environ.get("DCP_WGRAD_SIDE_MAXM", "0") or 0)
+_SIDE_STREAMS = {}
+
+
+def _noop():
+    return None
+
+
+def _wgrad_async(rows: int, fn, *inputs):
+    """``fn()`` (a weight-gradient launch reading ``inputs``) on the device's
+    side stream when ``rows <= WGRAD_SIDE_MAXM``: returns (result, join) —
+    ``join()`` makes the current stream wait for it (call before returning
+    the gradient to autograd). Capture-safe (event fork / join)."""
+    if rows > WGRAD_SIDE_MAXM or not inputs[0].is_cuda:
+        return fn(), _noop
+    dev = inputs[0].device
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE_STREAMS.get(dev.index)
+    if side is None:
+        side = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        out = fn()
+    for t in inputs:
+        t.record_stream(side)
+
+    def join():
+        main.wait_stream(side)
+        out.record_stream(main)
+
+    return out, join
+
+
 def _prepped(weight: torch.Tensor):
     return _PREPPED.get(weight) if _PREPPED else None
 
@@ -210,9 +247,7 @@ class _BNResActConv1x1Fn(torch.autograd.Function):
         if gz is None:
             gz = torch.zeros((y.shape[0], ctx.wshape[0]) + tuple(y.shape[2:]), device=y.device, dtype=y.dtype)
         gz = _cl(gz)
-        dw = _C.conv1x1_wgrad(gz, y).view(ctx.wshape)
-        if dw.dtype != ctx.wdtype:
-            dw = dw.to(ctx.wdtype)
+        dw, join = _wgrad_async(gz.numel() // gz.shape[1], lambda: _C.conv1x1_wgrad(gz, y), gz, y)
         g, acc, acc2 = _C.conv1x1_dgrad_resred(gz, wt, z3, None if gy is None else _cl(gy), mean, bits, x2, mean2)
         dz3, dgamma, dbeta = _C.bn_bwd_apply_g(g, z3, gamma, mean, invstd, acc)
         dres = dx2 = dgamma2 = dbeta2 = None
@@ -220,6 +255,10 @@ class _BNResActConv1x1Fn(torch.autograd.Function):
             dx2, dgamma2, dbeta2 = _C.bn_bwd_apply_g(g, x2, gamma2, mean2, invstd2, acc2)
         else:
             dres = g  # relu mask already applied: the identity's gradient
+        join()
+        dw = dw.view(ctx.wshape)
+        if dw.dtype != ctx.wdtype:
+            dw = dw.to(ctx.wdtype)
         return (dz3, dgamma, dbeta, dres, dx2, dgamma2, dbeta2, dw) + (None,) * 12
 
 
@@ -293,11 +332,14 @@ class _BNReluConvFn(torch.autograd.Function):
         x, y, gamma, beta, mean, invstd, w, wt = ctx.saved_tensors
         k, stride, pad, wshape, wdtype = ctx.cfg
         gz = _cl(gz)
+        rows = gz.numel() // gz.shape[1]
         if k == 1 and stride == 1:
-            dw = _C.conv1x1_wgrad(gz, y).view(wshape)
+            dw, join = _wgrad_async(rows, lambda: _C.conv1x1_wgrad(gz, y), gz, y)
             dy, acc = _C.conv1x1_dgrad_bnred(gz, wt, x, gamma, beta, mean, invstd)
+            join()
+            dw = dw.view(wshape)
         else:
-            dw = _C.conv_wgrad(gz, y, k, k, stride, pad)
+            dw, join = _wgrad_async(rows, lambda: _C.conv_wgrad(gz, y, k, k, stride, pad), gz, y)
             if stride == 1:
                 wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Cin][k][k][Cout]
                 dy, acc = _C.conv_dgrad_bnred(gz, wd, k, k, k - 1 - pad, x, gamma, beta, mean, invstd)
@@ -306,6 +348,7 @@ class _BNReluConvFn(torch.autograd.Function):
                                                          False, [0, 0], 1, [True, False, False])[0]
                 dy = _cl(dy)
                 acc = None
+            join()
         if dw.dtype != wdtype:
             dw = dw.to(wdtype)
         if acc is None:
@@ -363,8 +406,19 @@ def conv_kxk(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -
     return _ConvKxKFn.apply(x, weight, stride, padding)
 
 
-# stride-2 3x3 data gradient as parity-class GEMMs (opt-in until it beats MIOpen)
-_S2_PARITY = os.environ.get("DCP_S2_DGRAD_PARITY", "0") == "1"
+# stride-2 3x3 data gradient: "multi" = the four parity classes as ONE implicit-
+# GEMM launch (conv_dgrad_s2_multi), "parity" = four launches, "miopen"
+_S2_DGRAD = os.environ.get("DCP_S2_DGRAD", "multi")
+_S2_PARITY = os.environ.get("DCP_S2_DGRAD_PARITY", "0") == "1" or _S2_DGRAD == "parity"
+
+
+def _s2_tap_perm(wd: torch.Tensor) -> torch.Tensor:
+    """The flipped data-gradient weight wd [Cin][3][3][Cout] as [Cin][9][Cout]
+    with its taps in parity-class order 4 | 3 5 | 1 7 | 0 2 6 8 (classes
+    (ph, pw) = 00, 01, 10, 11; see :func:`_parity_weights`): one cat of strided
+    views (no index tensor, capture-safe)."""
+    w9 = wd.reshape(wd.shape[0], 9, wd.shape[3])
+    return torch.cat([w9[:, 4:5], w9[:, 3:6:2], w9[:, 1:8:6], w9[:, 0:3:2], w9[:, 6:9:2]], dim=1)
 
 
 def _parity_weights(wd: torch.Tensor):
@@ -417,6 +471,9 @@ class _ConvKxKGemmFn(torch.autograd.Function):
         gy = _cl(gy)
         kh, kw = w.shape[2], w.shape[3]
         dx = dw = None
+        join = _noop
+        if ctx.needs_input_grad[1] and not miopen_wgrad:
+            dw, join = _wgrad_async(gy.numel() // gy.shape[1], lambda: _C.conv_wgrad(gy, x, kh, kw, s, p), gy, x)
         if ctx.needs_input_grad[0]:
             if s == 1 and kh - 1 - p >= 0 and kw == kh:
                 if wd is None:
@@ -426,6 +483,11 @@ class _ConvKxKGemmFn(torch.autograd.Function):
                   and x.shape[3] == 2 * gy.shape[3]):
                 # strided 1x1 (downsample): GEMM whose epilogue scatters to the even pixels, zeros the rest
                 dx = _C.conv1x1_s2_dgrad(gy, wd)
+            elif (_S2_DGRAD == "multi" and kh == kw == 3 and s == 2 and p == 1 and x.shape[1] % 64 == 0
+                  and (x.shape[2] + 1) // 2 == gy.shape[2] and (x.shape[3] + 1) // 2 == gy.shape[3]):
+                if wd is None:
+                    wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+                dx = _C.conv_dgrad_s2_multi(gy, _s2_tap_perm(wd), x.shape[2], x.shape[3])
             elif _S2_PARITY and kh == kw == 3 and s == 2 and p == 1 and x.shape[1] % 64 == 0:
                 # four parity classes of dx, each an implicit GEMM over its 1/2/4 matching taps
                 if wd is None:
@@ -434,12 +496,11 @@ class _ConvKxKGemmFn(torch.autograd.Function):
             else:
                 dx = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]
+        join()
         if ctx.needs_input_grad[1]:
             if miopen_wgrad:
                 dw = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                          [False, True, False])[1]
-            else:
-                dw = _C.conv_wgrad(gy, x, kh, kw, s, p)
             if dw.dtype != wdtype:
                 dw = dw.to(wdtype)
         return dx, dw, None, None, None, None, None

@@ -207,11 +207,13 @@ def test_conv_kxk_autograd(cuda):
 
 @pytest.mark.parametrize("cin,cout,hw,k,stride,pad", [(64, 128, 14, 3, 1, 1), (64, 64, 9, 3, 2, 1), (128, 64, 7, 3, 1, 1),
                                                      (64, 128, 11, 1, 2, 0), (192, 64, 5, 3, 1, 1),
-                                                     (128, 256, 10, 1, 2, 0)])
+                                                     (128, 256, 10, 1, 2, 0), (128, 128, 14, 3, 2, 1),
+                                                     (256, 64, 7, 3, 2, 1)])
 def test_conv_kxk_gemm(cuda, cin, cout, hw, k, stride, pad):
     """Implicit-GEMM MFMA kxk conv (gemm.hip GATHER): forward + epilogue sums,
-    data gradient (stride 1: the forward kernel on flipped weights), weight
-    gradient, vs fp32 PyTorch on the same bf16 operands; ragged M."""
+    data gradient (stride 1: the forward kernel on flipped weights; 3x3
+    stride 2: the four parity classes in one launch, conv_dgrad_s2_multi),
+    weight gradient, vs fp32 PyTorch on the same bf16 operands; ragged M."""
     from torch import nn
 
     from distributed_compute_pytorch_amd.ops.conv import conv_kxk_gemm
