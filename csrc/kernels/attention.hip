@@ -166,9 +166,11 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
   bf16x8 qf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
+    // load (row clamped), then select: `ok ? *p : zero` becomes a pointer
+    // select to a scratch copy of the zero (flat loads + scratch stores)
     const uint4 z = make_uint4(0, 0, 0, 0);
-    const uint4 u = qok ? *reinterpret_cast<const uint4*>(Q.p + static_cast<int64_t>(qi) * Q.st + 16 * ks + 8 * hh) : z;
-    qf[ks] = __builtin_bit_cast(bf16x8, u);
+    const uint4 u = *reinterpret_cast<const uint4*>(Q.p + static_cast<int64_t>(qok ? qi : 0) * Q.st + 16 * ks + 8 * hh);
+    qf[ks] = __builtin_bit_cast(bf16x8, qok ? u : z);
   }
   const float c = P.scale * kLog2e;
   const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
@@ -324,8 +326,11 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
   for (int ks = 0; ks < 4; ++ks) {
     const uint4 z = make_uint4(0, 0, 0, 0);
     const int64_t off = 16 * ks + 8 * hh;
-    qf[ks] = __builtin_bit_cast(bf16x8, qok ? *reinterpret_cast<const uint4*>(Q.p + qi * Q.st + off) : z);
-    gf[ks] = __builtin_bit_cast(bf16x8, qok ? *reinterpret_cast<const uint4*>(G.p + qi * G.st + off) : z);
+    const int64_t qc = qok ? qi : 0;  // load (row clamped), then select
+    const uint4 uq = *reinterpret_cast<const uint4*>(Q.p + qc * Q.st + off);
+    const uint4 ug = *reinterpret_cast<const uint4*>(G.p + qc * G.st + off);
+    qf[ks] = __builtin_bit_cast(bf16x8, qok ? uq : z);
+    gf[ks] = __builtin_bit_cast(bf16x8, qok ? ug : z);
   }
   const float lse2 = qok ? lse[static_cast<int64_t>(bh) * T + qi] : 0.f;
   const float dlt = qok ? delta[static_cast<int64_t>(bh) * T + qi] : 0.f;
@@ -420,8 +425,11 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
   for (int ks = 0; ks < 4; ++ks) {
     const uint4 z = make_uint4(0, 0, 0, 0);
     const int64_t off = 16 * ks + 8 * hh;
-    kf[ks] = __builtin_bit_cast(bf16x8, kok ? *reinterpret_cast<const uint4*>(K.p + key * K.st + off) : z);
-    vf[ks] = __builtin_bit_cast(bf16x8, kok ? *reinterpret_cast<const uint4*>(V.p + key * V.st + off) : z);
+    const int64_t kc = kok ? key : 0;  // load (row clamped), then select
+    const uint4 uk = *reinterpret_cast<const uint4*>(K.p + kc * K.st + off);
+    const uint4 uv = *reinterpret_cast<const uint4*>(V.p + kc * V.st + off);
+    kf[ks] = __builtin_bit_cast(bf16x8, kok ? uk : z);
+    vf[ks] = __builtin_bit_cast(bf16x8, kok ? uv : z);
   }
   const float c = P.scale * kLog2e;
   const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);

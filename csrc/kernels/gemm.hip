@@ -1358,7 +1358,14 @@ void gemm_nt_launch_bm(const void* A, const void* B, void* C, int64_t M, int N, 
   // tn, see the kernel)
   constexpr int kRes = BM == 128 ? 512 : 256;
   const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
-  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
+  // DCP_GEMM_PERSIST=0: one tile per workgroup (the dispatcher balances the
+  // tail, and workgroups that cannot be resident — CUs held by concurrent
+  // RCCL kernels — cost one tile, not a persistent workgroup's whole share)
+  static const bool persist = [] {
+    const char* v = getenv("DCP_GEMM_PERSIST");
+    return !(v && v[0] == '0');
+  }();
+  int P = tiles <= kRes || !persist ? static_cast<int>(tiles) : (kRes / tn) * tn;
   if (P < tn) P = tn;
   const dim3 grid(P);
   const bool pro = scale != nullptr;
