@@ -1264,6 +1264,128 @@ __global__ void __launch_bounds__(kD3Threads, 1) conv3x3_c64_kernel(const uint16
   }
 }
 
+// --------------------------------------------- direct 3x3 wgrad, 64 -> 64 --
+// dW[co][tap][ci] = Σ_p dY[p][co] · X[p + shift(tap)][ci] for the stride-1
+// pad-1 3x3 conv with Cin = Cout = 64 (ResNet-50 layer-1 conv2). The gathered
+// multi-tap wgrad re-fetches every input row once per tap through L2 (354
+// TF/s at 1.2 TB/s: neither bound); here, per tile of R whole output rows, a
+// workgroup DMAs the dY rows and the (R+2) x (W+2) input halo ONCE (double-
+// buffered, next tile in flight), and the 9 taps are shifted LDS row indices
+// of the same halo. Each wave owns 32 co x 32 ci of all 9 taps (36 fp32
+// accumulators) for the whole run of tiles, so the only output is one fp32
+// slab per workgroup, summed by slab_partial_kernel. Operands are read with
+// ds_read_b64_tr_b16 (the wgrad kernels' transposed fragments, tr_f<64>
+// swizzle keyed by the LDS row: pixel for dY, halo pixel for X).
+
+// transposed 16-channel x 8-k fragment with per-lane LDS rows (the k rows
+// 8g + q and 8g + q + 4 of tr_frag<64> live at rows r0 and r1)
+__device__ __forceinline__ bf16x8 tr_frag_rows(const char* base, int r0, int r1, int c0, int lane) {
+  const int p = lane & 3;
+  const int pair = c0 >> 4;
+  const char* a0 = base + r0 * 128 + 32 * (pair ^ tr_f<64>(r0)) + 8 * p;
+  const char* a1 = base + r1 * 128 + 32 * (pair ^ tr_f<64>(r1)) + 8 * p;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__global__ void __launch_bounds__(kT, 1) conv3x3_c64_wgrad_kernel(const uint16_t* __restrict__ dY,
+                                                                   const uint16_t* __restrict__ X,
+                                                                   float* __restrict__ ws, int N, int H, int W, int R,
+                                                                   int HT, int tiles, int per_block, int KG,
+                                                                   const uint16_t* __restrict__ zero, int dy_bytes,
+                                                                   int halo_bytes) {
+  constexpr int C = 64, COLS = 9 * C;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wi = wave >> 1, wj = wave & 1;  // co half, ci half
+  const int WP = W + 2;
+  const int P = R * W;                       // pixels of a full tile
+  const int hq = (R + 2) * WP * 8;           // 16-B chunks of a halo
+  const int dglds = dy_bytes / (4 * 1024), hglds = halo_bytes / (4 * 1024);
+  const int t0 = blockIdx.x * per_block;
+  const int t1 = min(tiles, t0 + per_block);
+
+  auto issue = [&](int tile, int b) {
+    const int n = tile / HT, h0 = (tile % HT) * R;
+    const int npx = min(R, H - h0) * W;
+    const int64_t pix0 = (static_cast<int64_t>(n) * H + h0) * W;
+    char* db = lds + b * dy_bytes;
+    char* hb = lds + 2 * dy_bytes + b * halo_bytes;
+    for (int j = 0; j < dglds; ++j) {
+      const int q = (wave * dglds + j) * 64 + lane;
+      const int r = q >> 3, pc = q & 7, lc = 2 * ((pc >> 1) ^ tr_f<64>(r)) + (pc & 1);
+      const uint16_t* src = r < npx ? dY + (pix0 + r) * C + lc * 8 : zero + lc * 8;
+      glds16(src, db + (wave * dglds + j) * 1024);
+    }
+    for (int j = 0; j < hglds; ++j) {
+      const int q = (wave * hglds + j) * 64 + lane;
+      const int hp = q >> 3, pc = q & 7, lc = 2 * ((pc >> 1) ^ tr_f<64>(hp)) + (pc & 1);
+      const int hr = hp / WP, hc = hp - hr * WP;
+      const int ih = h0 - 1 + hr, iw = hc - 1;
+      const bool ok = q < hq && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+      const uint16_t* src = ok ? X + ((static_cast<int64_t>(n) * H + ih) * W + iw) * C + lc * 8 : zero + lc * 8;
+      glds16(src, hb + (wave * hglds + j) * 1024);
+    }
+  };
+
+  const int g = lane >> 4, qq = (lane >> 2) & 3;
+  f32x4 acc[2][18];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 18; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (t0 < t1) issue(t0, 0);
+  for (int tile = t0; tile < t1; ++tile) {
+    const int b = (tile - t0) & 1;
+    wait_vm<0>();
+    barrier();  // this tile's rows visible; every wave done with the other buffer
+    if (tile + 1 < t1) issue(tile + 1, b ^ 1);
+    const char* db = lds + b * dy_bytes;
+    const char* hb = lds + 2 * dy_bytes + b * halo_bytes;
+#pragma unroll 1
+    for (int kg = 0; kg < KG; ++kg) {
+      // halo rows (tap (0, 0)) of this lane's two k rows; pixels past the
+      // tile read halo row 0 (finite — their dY rows are zero)
+      const int p0 = kg * 32 + 8 * g + qq, p1 = p0 + 4;
+      const int hk0 = p0 < P ? (p0 / W) * WP + p0 % W : 0;
+      const int hk1 = p1 < P ? (p1 / W) * WP + p1 % W : 0;
+      {
+        bf16x8 af[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = tr_frag<64>(db + kg * 32 * 128, wi * 32 + i * 16, lane);
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int toff = (tap / 3) * WP + (tap % 3);
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const bf16x8 bf = tr_frag_rows(hb, hk0 + toff, hk1 + toff, wj * 32 + jj * 16, lane);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+              acc[i][tap * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][tap * 2 + jj], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  // slab blockIdx.x of D [64 co][9 taps][64 ci]
+  float* out = ws + static_cast<int64_t>(blockIdx.x) * C * COLS;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 18; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wi * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int col = (j >> 1) * C + wj * 32 + (j & 1) * 16 + (lane & 15);
+        out[static_cast<int64_t>(row) * COLS + col] = acc[i][j][r];
+      }
+}
+
 struct WgradPlan {
   int bm, bn, tiles, S;
   int64_t chunk;
@@ -1677,7 +1799,10 @@ WgradPlan wgrad_plan_for(int64_t M, int N1, int N2, int taps) {
 int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
   const WgradPlan p = wgrad_plan_for(M, N1, N2, taps);
   const int64_t groups = (p.S + kSlabGroup - 1) / kSlabGroup;
-  return (static_cast<int64_t>(p.S) + (groups > 1 ? groups : 0)) * N1 * taps * N2;
+  int64_t need = (static_cast<int64_t>(p.S) + (groups > 1 ? groups : 0)) * N1 * taps * N2;
+  // direct 3x3 / 64-channel wgrad: ≤ 256 workgroup slabs + 16 partial groups
+  if (N1 == 64 && N2 == 64 && taps == 9 && need < int64_t(272) * 64 * 576) need = int64_t(272) * 64 * 576;
+  return need;
 }
 
 namespace {
@@ -1778,8 +1903,50 @@ void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int
   slab_reduce(ws, D, static_cast<int64_t>(Cout) * kStemWgradCols / 4, p.S, s, false);
 }
 
+namespace {
+// DCP_WGRAD_DIRECT=0: the 64-channel 3x3 wgrad on the gathered multi-tap kernel
+inline bool wgrad_direct() {
+  static const bool on = [] {
+    const char* v = getenv("DCP_WGRAD_DIRECT");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+void conv3x3_c64_wgrad_launch(const void* dY, const void* X, float* D, int N, int H, int W, const void* zero,
+                              float* ws, hipStream_t s) {
+  int R = 256 / W;  // whole output rows per tile, ≤ 256 pixels (8 k-groups)
+  if (R > H) R = H;
+  if (R < 1) R = 1;
+  const int KG = (R * W + 31) / 32;
+  const int HT = (H + R - 1) / R;
+  const int tiles = N * HT;
+  int nb = tiles < 256 ? tiles : 256;  // one workgroup per CU, each a contiguous run of tiles
+  const int per_block = (tiles + nb - 1) / nb;
+  nb = (tiles + per_block - 1) / per_block;  // every workgroup has ≥ 1 tile (each writes its slab)
+  const int dy_bytes = KG * 32 * 128;
+  const int halo_bytes = ((R + 2) * (W + 2) * 128 + 4095) / 4096 * 4096;
+  const size_t lds = 2 * static_cast<size_t>(dy_bytes + halo_bytes);
+  static const bool attr = [] {  // > 64 KB of dynamic LDS
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_c64_wgrad_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(conv3x3_c64_wgrad_kernel, dim3(nb), dim3(kT), lds, s, static_cast<const uint16_t*>(dY),
+                     static_cast<const uint16_t*>(X), ws, N, H, W, R, HT, tiles, per_block, KG,
+                     static_cast<const uint16_t*>(zero), dy_bytes, halo_bytes);
+  slab_reduce(ws, D, int64_t(64) * 576 / 4, nb, s, false);
+}
+}  // namespace
+
 void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                      int kh, int kw, int stride, int pad, const void* zero, float* ws, hipStream_t s) {
+  if (wgrad_direct() && conv3x3_c64_direct(Cin, Cout, kh, kw, stride, pad, W) &&
+      2 * (((256 / W) * W + 31) / 32 * 32 * 128 + ((256 / W + 2) * (W + 2) * 128 + 4095) / 4096 * 4096) <= 160 * 1024) {
+    conv3x3_c64_wgrad_launch(dY, X, D, N, H, W, zero, ws, s);
+    return;
+  }
   ConvGeo geo{H, W, Ho, Wo, stride, pad, kw, static_cast<const uint16_t*>(zero)};
   wgrad_launch<true>(dY, X, D, static_cast<int64_t>(N) * Ho * Wo, Cout, Cin, nullptr, nullptr, false, ws, kh * kw,
                      geo, s);

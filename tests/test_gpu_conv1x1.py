@@ -321,8 +321,9 @@ def test_conv_weight_bf16_layouts(cuda):
 
 @pytest.mark.parametrize("n,h,w", [(2, 56, 56), (3, 7, 9), (2, 5, 62), (4, 13, 2), (5, 30, 31), (2, 17, 40)])
 def test_conv3x3_c64_direct(cuda, n, h, w):
-    """Direct 3x3 / 64-channel kernel (halo in LDS, weights resident): forward +
-    BN sums and the stride-1 data gradient (same kernel on flipped weights) vs
+    """Direct 3x3 / 64-channel kernels (halo in LDS): forward + BN sums, the
+    stride-1 data gradient (same kernel on flipped weights) and the weight
+    gradient (conv3x3_c64_wgrad_kernel) vs
     fp32 PyTorch on the same bf16 operands, rectangular and ragged row tiles."""
     from torch import nn
 
@@ -343,3 +344,7 @@ def test_conv3x3_c64_direct(cuda, n, h, w):
     ref_st = torch.cat([yf.sum((0, 2, 3)), (yf * yf).sum((0, 2, 3))])
     assert _rel(st, ref_st) < 1e-4
     assert _rel(x.grad, xr.grad) < 1e-2
+    # weight gradient: the direct halo kernel (conv3x3_c64_wgrad_kernel) + slab reduction
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    F.conv2d(x.detach().float(), wr, None, 1, 1).backward(gy.float())
+    assert conv.weight.grad.dtype == torch.float32 and _rel(conv.weight.grad, wr.grad) < 1e-3
