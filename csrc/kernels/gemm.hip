@@ -1333,6 +1333,11 @@ __global__ void __launch_bounds__(kT, 1) conv3x3_c64_wgrad_kernel(const uint16_t
   };
 
   const int g = lane >> 4, qq = (lane >> 2) & 3;
+  // (row, col) in the tile of this lane's k rows 8g + qq and 8g + qq + 4 at
+  // k-group 0; each k-group advances them by 32 pixels = (dr, dc)
+  const int r0i = (8 * g + qq) / W, c0i = (8 * g + qq) % W;
+  const int r1i = (8 * g + qq + 4) / W, c1i = (8 * g + qq + 4) % W;
+  const int dr = 32 / W, dc = 32 % W;
   f32x4 acc[2][18];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1347,13 +1352,21 @@ __global__ void __launch_bounds__(kT, 1) conv3x3_c64_wgrad_kernel(const uint16_t
     if (tile + 1 < t1) issue(tile + 1, b ^ 1);
     const char* db = lds + b * dy_bytes;
     const char* hb = lds + 2 * dy_bytes + b * halo_bytes;
+    int r0k = r0i, c0k = c0i, r1k = r1i, c1k = c1i;
 #pragma unroll 1
     for (int kg = 0; kg < KG; ++kg) {
       // halo rows (tap (0, 0)) of this lane's two k rows; pixels past the
       // tile read halo row 0 (finite — their dY rows are zero)
       const int p0 = kg * 32 + 8 * g + qq, p1 = p0 + 4;
-      const int hk0 = p0 < P ? (p0 / W) * WP + p0 % W : 0;
-      const int hk1 = p1 < P ? (p1 / W) * WP + p1 % W : 0;
+      const int hk0 = p0 < P ? r0k * WP + c0k : 0;
+      const int hk1 = p1 < P ? r1k * WP + c1k : 0;
+      // advance (row, col) of both k rows by 32 pixels: no divisions per k-group
+      c0k += dc;
+      r0k += dr + (c0k >= W ? 1 : 0);
+      c0k -= c0k >= W ? W : 0;
+      c1k += dc;
+      r1k += dr + (c1k >= W ? 1 : 0);
+      c1k -= c1k >= W ? W : 0;
       {
         bf16x8 af[2];
 #pragma unroll
@@ -1361,9 +1374,17 @@ __global__ void __launch_bounds__(kT, 1) conv3x3_c64_wgrad_kernel(const uint16_t
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
           const int toff = (tap / 3) * WP + (tap % 3);
+          // this tap's two halo rows: row bits and swizzle once, shared by both
+          // 16-channel fragments (tr_frag_rows' math, hoisted)
+          const int h0 = hk0 + toff, h1 = hk1 + toff;
+          const int f0 = tr_f<64>(h0), f1 = tr_f<64>(h1);
+          const int a0 = (h0 << 7) | ((lane & 3) << 3), a1 = (h1 << 7) | ((lane & 3) << 3);
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) {
-            const bf16x8 bf = tr_frag_rows(hb, hk0 + toff, hk1 + toff, wj * 32 + jj * 16, lane);
+            const int pair = 2 * wj + jj;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(hb + (a0 | ((pair ^ f0) << 5))));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(hb + (a1 | ((pair ^ f1) << 5))));
+            const bf16x8 bf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
             for (int i = 0; i < 2; ++i)
               acc[i][tap * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][tap * 2 + jj], 0, 0, 0);
