@@ -1866,9 +1866,15 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
     const char* b = getenv("DCP_WGRAD_BK");
     return b && atoi(b) == 32 ? 2 : 0;
   }();
+  // the BN-prologue wgrad on the BK=64 ring too (+0.2 % same-box,
+  // profiles/r2_ab_wgrad_pro_bk.jsonl); DCP_WGRAD_PRO_BK=32: the 4-deep BK=32 ring
+  static const bool pro64 = [] {
+    const char* v = getenv("DCP_WGRAD_PRO_BK");
+    return !(v && atoi(v) == 32);
+  }();
 #define DCP_GWG(BM_, BN_, P)                                                                                        \
   do {                                                                                                             \
-    if (cfg == 0 && !P)                                                                                            \
+    if (cfg == 0 && (!P || pro64))                                                                                 \
       hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 64>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,    \
                          p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo);                \
     else if (cfg == 1)                                                                                             \
