@@ -1765,18 +1765,23 @@ void conv_fwd_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, 
                        stats, geo, s);
 }
 
-void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W, int Cout, float* stats,
-                   hipStream_t s) {
+namespace {
+template <int BM>
+void stem_conv_fwd_bm(const void* xp, const void* wm, void* y, int N, int H, int W, int Cout, float* stats,
+                      hipStream_t s) {
   // geo: padded image (stem_hp/stem_wp) and the stride-2 output grid
   ConvGeo geo{H + 6, W + 8, H / 2, W / 2, 2, 0, 7, nullptr, 4};
   const int64_t M = static_cast<int64_t>(N) * (H / 2) * (W / 2);
-  constexpr int BM = 128, BN = 64, BK = 64, K = kStemK;
+  constexpr int BN = 64, BK = 64, K = kStemK;
+  constexpr int kRes = BM == 128 ? 512 : 256;  // resident workgroups (LDS)
   const int tiles_m = static_cast<int>((M + BM - 1) / BM);
   const int tn = Cout / BN;
   const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
-  int P = tiles <= 512 ? static_cast<int>(tiles) : (512 / tn) * tn;
+  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
   if (P < tn) P = tn;
-  const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 + 4 * 32 * BN;
+  constexpr int NW = nt_threads<BM, BN>() / 64;
+  const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 +
+                     static_cast<size_t>(NW) * 32 * (BN / nt_wn<BM, BN>()) * 2;
   auto a = static_cast<const uint16_t*>(xp);
   auto b = static_cast<const uint16_t*>(wm);
   auto c = static_cast<uint16_t*>(y);
@@ -1786,6 +1791,18 @@ void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W,
   else
     hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 0, false, BK, 1>), dim3(P), dim3(nt_threads<BM, BN>()), lds, s, a, b, c, M, Cout,
                        K, nullptr, nullptr, 0, nullptr, tiles_m, tn, geo, BnRedArgs{});
+}
+}  // namespace
+
+void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W, int Cout, float* stats,
+                   hipStream_t s) {
+  // DCP_STEM_BM=256: 256 x 64 tiles (4 x 1 waves of 64 x 64, one workgroup per CU)
+  static const int bm = [] {
+    const char* v = getenv("DCP_STEM_BM");
+    return v && atoi(v) == 256 ? 256 : 128;
+  }();
+  if (bm == 256) stem_conv_fwd_bm<256>(xp, wm, y, N, H, W, Cout, stats, s);
+  else stem_conv_fwd_bm<128>(xp, wm, y, N, H, W, Cout, stats, s);
 }
 
 void weight_prep(const void* table, int n, int64_t tiles, hipStream_t s) {
