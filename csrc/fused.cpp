@@ -544,6 +544,46 @@ std::vector<at::Tensor> bn_bwd_apply_g(const at::Tensor& g, const at::Tensor& x,
   return {dx, dw, db};
 }
 
+// Both BNs of relu(bn(x) + bn2(x2)) backward from the masked gradient g and
+// the reductions acc / acc2 (conv1x1_dgrad_resred): g is read once for both
+// (C <= 2048: 8·C fp32 coefficients in LDS; else two bn_bwd_apply_g passes).
+// Returns (dx, dweight, dbias, dx2, dweight2, dbias2).
+std::vector<at::Tensor> bn_bwd_apply2_g(const at::Tensor& g, const at::Tensor& x, const at::Tensor& weight,
+                                        const at::Tensor& mean, const at::Tensor& invstd, const at::Tensor& acc,
+                                        const at::Tensor& x2, const at::Tensor& weight2, const at::Tensor& mean2,
+                                        const at::Tensor& invstd2, const at::Tensor& acc2) {
+  check_nhwc(x, "bn_bwd_apply2_g");
+  check_nhwc(x2, "bn_bwd_apply2_g(x2)");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  DCP_CHECK(g.sizes() == x.sizes() && g.scalar_type() == x.scalar_type() && g.is_contiguous(cl_fmt(x)) &&
+                x2.sizes() == x.sizes() && x2.scalar_type() == x.scalar_type(),
+            "bn_bwd_apply2_g: g / x2 must match x");
+  for (const at::Tensor* t : {&acc, &acc2})
+    DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == 2 * C && t->is_contiguous(),
+              "bn_bwd_apply2_g: acc must be fp32 [2*C]");
+  for (const at::Tensor* t : {&weight, &weight2, &mean, &mean2, &invstd, &invstd2})
+    DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(),
+              "bn_bwd_apply2_g: per-channel tensors must be fp32 [C]");
+  if (C > 2048) {
+    auto a = bn_bwd_apply_g(g, x, weight, mean, invstd, acc);
+    auto b = bn_bwd_apply_g(g, x2, weight2, mean2, invstd2, acc2);
+    return {a[0], a[1], a[2], b[0], b[1], b[2]};
+  }
+  auto fopt = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x, cl_fmt(x)), dx2 = at::empty_like(x2, cl_fmt(x2));
+  at::Tensor dw = at::empty({C}, fopt), db = at::empty({C}, fopt), dw2 = at::empty({C}, fopt),
+             db2 = at::empty({C}, fopt);
+  kern::bn_backward_apply2(bn_dtype(x), g.data_ptr(), x.data_ptr(), x2.data_ptr(), M, static_cast<int>(C),
+                           weight.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                           acc.data_ptr<float>(), weight2.data_ptr<float>(), mean2.data_ptr<float>(),
+                           invstd2.data_ptr<float>(), acc2.data_ptr<float>(), dx.data_ptr(), dx2.data_ptr(),
+                           dw.data_ptr<float>(), db.data_ptr<float>(), dw2.data_ptr<float>(), db2.data_ptr<float>(),
+                           stream_of(x));
+  return {dx, dw, db, dx2, dw2, db2};
+}
+
 // stride-1 kxk conv data gradient (implicit GEMM on gy with the flipped,
 // transposed weight wd [Cin][kh][kw][Cout]) + the BN+ReLU backward reduction
 // of x in its epilogue: returns (dy, acc [2*Cin]).
@@ -1313,6 +1353,8 @@ void bind(pybind11::module& m) {
         pybind11::arg("gy"), pybind11::arg("wt"), pybind11::arg("x"), pybind11::arg("gy2"), pybind11::arg("mean"),
         pybind11::arg("bits"), pybind11::arg("x2") = pybind11::none(), pybind11::arg("mean2") = pybind11::none());
   m.def("bn_bwd_apply_g", &bn_bwd_apply_g, "BN training backward apply from a masked gradient + its reduction");
+  m.def("bn_bwd_apply2_g", &bn_bwd_apply2_g,
+        "both BNs of relu(bn(x) + bn2(x2)) backward from the shared masked gradient in one pass");
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply, "BN/ReLU training backward apply from a precomputed reduction");
   m.def("bn_resbn_act_fwd", &bn_resbn_act_fwd, "training relu(bn(x) + bn2(x2)), both BNs fused (downsample block)");
   m.def("bn_resbn_act_bwd", &bn_resbn_act_bwd, "backward of bn_resbn_act_fwd");

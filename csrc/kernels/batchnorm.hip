@@ -579,6 +579,68 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply_kernel(const void* __restrict
   }
 }
 
+// Both BatchNorms of relu(bn(x) + bn2(x2)) backward from the shared masked
+// gradient g in ONE pass: dx = k1 (g - k2 - (x - μ) k3), dx2 the same with
+// bn2's coefficients — g is read once instead of once per BN (the downsample
+// blocks' two apply passes). acc / acc2 = (Σg, Σg·(x - μ)) / (Σg, Σg·(x2 - μ2));
+// training mode; the first thread group writes both dgamma / dbeta.
+template <int D>
+__global__ void __launch_bounds__(kT) bn_bwd_apply2_kernel(const void* __restrict__ g, const void* __restrict__ x,
+                                                           const void* __restrict__ x2, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ acc, const float* __restrict__ mean2,
+                                                           const float* __restrict__ invstd2,
+                                                           const float* __restrict__ gamma2,
+                                                           const float* __restrict__ acc2, float* __restrict__ dgamma,
+                                                           float* __restrict__ dbeta, float* __restrict__ dgamma2,
+                                                           float* __restrict__ dbeta2, void* __restrict__ dx,
+                                                           void* __restrict__ dx2, int64_t M, int64_t nvec, int C) {
+  const int cv = C / kV;
+  const int64_t tid = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kT;
+  const int c0 = static_cast<int>(tid % cv) * kV;
+  extern __shared__ __attribute__((aligned(16))) float cf[];  // [k1, k2, k3, mean] x 2 BNs, [C] each
+  const float inv_m = 1.f / static_cast<float>(M);
+  for (int c = threadIdx.x; c < C; c += kT) {
+    const float i1 = invstd[c], i2 = invstd2[c];
+    const float sb = acc[c], sg = acc[C + c], sb2 = acc2[c], sg2 = acc2[C + c];
+    cf[c] = gamma[c] * i1;
+    cf[C + c] = sb * inv_m;
+    cf[2 * C + c] = sg * inv_m * i1 * i1;
+    cf[3 * C + c] = mean[c];
+    cf[4 * C + c] = gamma2[c] * i2;
+    cf[5 * C + c] = sb2 * inv_m;
+    cf[6 * C + c] = sg2 * inv_m * i2 * i2;
+    cf[7 * C + c] = mean2[c];
+    if (blockIdx.x == 0) {
+      dgamma[c] = sg * i1;
+      dbeta[c] = sb;
+      dgamma2[c] = sg2 * i2;
+      dbeta2[c] = sb2;
+    }
+  }
+  __syncthreads();
+  float k[8][kV];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+#pragma unroll
+    for (int e = 0; e < kV; ++e) k[q][e] = cf[q * C + c0 + e];
+  for (int64_t v = tid; v < nvec; v += stride) {
+    float gv[kV], xv[kV], zv[kV], o1[kV], o2[kV];
+    V8<D>::ld(g, v * kV, gv);
+    V8<D>::ld(x, v * kV, xv);
+    V8<D>::ld(x2, v * kV, zv);
+#pragma unroll
+    for (int e = 0; e < kV; ++e) {
+      o1[e] = k[0][e] * (gv[e] - k[1][e] - (xv[e] - k[3][e]) * k[2][e]);
+      o2[e] = k[4][e] * (gv[e] - k[5][e] - (zv[e] - k[7][e]) * k[6][e]);
+    }
+    V8<D>::st(dx, v * kV, o1);
+    V8<D>::st(dx2, v * kV, o2);
+  }
+}
+
 // grid for the reduction kernels: ≤ 2048 workgroups over (row slabs × channel
 // chunks), ≥ kU row iterations per thread, ≤ ~256K column atomics per launch.
 // tunables (env, read once): total workgroups and column atomics per launch
@@ -893,6 +955,22 @@ void bn_backward_apply_plain(int dtype, const void* g, const void* x, int64_t M,
   else
     hipLaunchKernelGGL((bn_bwd_apply_kernel<BN_F32, false, true, true>), dim3(grid), dim3(kT), bsm, s, g, nullptr, x,
                        mean, invstd, gamma, nullptr, acc, dgamma, dbeta, true, dx, M, nvec, C);
+}
+
+void bn_backward_apply2(int dtype, const void* g, const void* x, const void* x2, int64_t M, int C, const float* gamma,
+                        const float* mean, const float* invstd, const float* acc, const float* gamma2,
+                        const float* mean2, const float* invstd2, const float* acc2, void* dx, void* dx2,
+                        float* dgamma, float* dbeta, float* dgamma2, float* dbeta2, hipStream_t s) {
+  bn_init_flags();
+  const int64_t nvec = M * C / kV;
+  const int grid = apply_grid(nvec, C / kV);
+  const size_t sm = sizeof(float) * 8 * C;
+  if (dtype == BN_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply2_kernel<BN_BF16>, dim3(grid), dim3(kT), sm, s, g, x, x2, mean, invstd, gamma, acc,
+                       mean2, invstd2, gamma2, acc2, dgamma, dbeta, dgamma2, dbeta2, dx, dx2, M, nvec, C);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply2_kernel<BN_F32>, dim3(grid), dim3(kT), sm, s, g, x, x2, mean, invstd, gamma, acc,
+                       mean2, invstd2, gamma2, acc2, dgamma, dbeta, dgamma2, dbeta2, dx, dx2, M, nvec, C);
 }
 
 // BN(+ReLU) backward apply only, training mode, mask recomputed from x: acc

@@ -44,6 +44,12 @@ void bn_backward_resbn(int dtype, const void* gy, const void* gy2, const void* x
                        void* dx, float* dgamma, float* dbeta, float* acc, const void* x2, const float* mean2,
                        float* acc2, hipStream_t s);
 // dx = BN backward apply (no activation) from upstream g and a precomputed acc [2C].
+// Both BNs of relu(bn(x) + bn2(x2)) from the shared masked gradient g in one
+// pass (g read once): dx, dx2 and both (dgamma, dbeta); training mode.
+void bn_backward_apply2(int dtype, const void* g, const void* x, const void* x2, int64_t M, int C, const float* gamma,
+                        const float* mean, const float* invstd, const float* acc, const float* gamma2,
+                        const float* mean2, const float* invstd2, const float* acc2, void* dx, void* dx2,
+                        float* dgamma, float* dbeta, float* dgamma2, float* dbeta2, hipStream_t s);
 void bn_backward_apply_plain(int dtype, const void* g, const void* x, int64_t M, int C, const float* gamma,
                              const float* mean, const float* invstd, const float* acc, void* dx, float* dgamma,
                              float* dbeta, hipStream_t s);

@@ -206,6 +206,10 @@ def bn_relu_conv1x1(x: torch.Tensor, bn, weight: torch.Tensor, stats: bool = Fal
                                   bn.eps, stats, sums)
 
 
+# downsample blocks: BN3's and the downsample BN's apply passes as one kernel (g read once)
+_APPLY2 = os.environ.get("DCP_BN_APPLY2", "1") == "1"
+
+
 class _BNResActConv1x1Fn(torch.autograd.Function):
     """Block boundary of a bottleneck chain, training mode:
     ``y = relu(bn3(z3) + r)`` with ``r`` the identity or ``bn_d(x2)`` (the
@@ -249,12 +253,16 @@ class _BNResActConv1x1Fn(torch.autograd.Function):
         gz = _cl(gz)
         dw, join = _wgrad_async(gz.numel() // gz.shape[1], lambda: _C.conv1x1_wgrad(gz, y), gz, y)
         g, acc, acc2 = _C.conv1x1_dgrad_resred(gz, wt, z3, None if gy is None else _cl(gy), mean, bits, x2, mean2)
-        dz3, dgamma, dbeta = _C.bn_bwd_apply_g(g, z3, gamma, mean, invstd, acc)
         dres = dx2 = dgamma2 = dbeta2 = None
-        if x2 is not None:
-            dx2, dgamma2, dbeta2 = _C.bn_bwd_apply_g(g, x2, gamma2, mean2, invstd2, acc2)
+        if x2 is not None and _APPLY2:  # both BNs' apply passes share one read of g
+            dz3, dgamma, dbeta, dx2, dgamma2, dbeta2 = _C.bn_bwd_apply2_g(g, z3, gamma, mean, invstd, acc, x2, gamma2,
+                                                                          mean2, invstd2, acc2)
         else:
-            dres = g  # relu mask already applied: the identity's gradient
+            dz3, dgamma, dbeta = _C.bn_bwd_apply_g(g, z3, gamma, mean, invstd, acc)
+            if x2 is not None:
+                dx2, dgamma2, dbeta2 = _C.bn_bwd_apply_g(g, x2, gamma2, mean2, invstd2, acc2)
+            else:
+                dres = g  # relu mask already applied: the identity's gradient
         join()
         dw = dw.view(ctx.wshape)
         if dw.dtype != ctx.wdtype:
