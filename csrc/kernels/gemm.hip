@@ -1078,6 +1078,9 @@ __global__ void __launch_bounds__(kT) colsum_partial_kernel(const uint16_t* __re
 // epilogue as gemm_nt_kernel (bf16 output through per-wave LDS staging, STATS:
 // per-channel sum / sum of squares of the bf16 output into stats[2 * 64]).
 constexpr int kD3Threads = 256;
+// halo DMA instructions per wave per tile the direct kernels precompute for
+// (their launchers fall back to the gathered kernels above this)
+constexpr int kMaxHaloG = 16;
 // 16-B chunk swizzle of the 128-B halo / weight rows: an A fragment reads 16
 // consecutive halo pixels starting ANYWHERE (tap offsets 0..2 * (W + 2) + 2),
 // and chunk ^ (row & 7) is conflict-free for every start (exhaustive check over
@@ -1118,17 +1121,31 @@ __global__ void __launch_bounds__(kD3Threads, 1) conv3x3_c64_kernel(const uint16
     const int tap = row >> 6, co = row & 63;
     glds16(Wt + (co * 9 + tap) * C + lc * 8, wl + (wave * 18 + j) * 1024);
   }
+  // per-lane halo DMA geometry, tile-invariant (the divisions by WP once, not
+  // per tile: they were most of the kernel's VALU): halo row, element offset
+  // from the tile's (row h0 - 1, column -1) corner, column-in-range bit
+  int hg_row[kMaxHaloG], hg_off[kMaxHaloG], hg_lc[kMaxHaloG];
+  uint32_t hg_cok = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxHaloG; ++j) {
+    const int q = (wave * hglds + j) * 64 + lane;
+    const int hp = q >> 3, pc = q & 7;
+    const int hr = hp / WP, hc = hp - hr * WP;
+    hg_lc[j] = pc ^ d3_swz(hp);
+    hg_row[j] = q < hq ? hr : -(1 << 20);  // past the halo: never in range
+    hg_off[j] = ((hr - 1) * W + hc - 1) * C + hg_lc[j] * 8;
+    hg_cok |= (j < hglds && static_cast<unsigned>(hc - 1) < static_cast<unsigned>(W)) ? (1u << j) : 0u;
+  }
   auto issue_halo = [&](int tile, char* buf) {
     const int n = tile / HT, h0 = (tile % HT) * R;
-    for (int j = 0; j < hglds; ++j) {
-      const int q = (wave * hglds + j) * 64 + lane;
-      const int hp = q >> 3, pc = q & 7, lc = pc ^ d3_swz(hp);
-      const int hr = hp / WP, hc = hp - hr * WP;
-      const int ih = h0 - 1 + hr, iw = hc - 1;
-      const bool ok = q < hq && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
-      const uint16_t* src = ok ? X + ((static_cast<int64_t>(n) * H + ih) * W + iw) * C + lc * 8 : zero + lc * 8;
-      glds16(src, buf + (wave * hglds + j) * 1024);
+    const uint16_t* tb = X + (static_cast<int64_t>(n) * H + h0) * W * C;
+#pragma unroll
+    for (int j = 0; j < kMaxHaloG; ++j) {
+      if (j < hglds) {
+        const bool ok = ((hg_cok >> j) & 1u) && static_cast<unsigned>(h0 - 1 + hg_row[j]) < static_cast<unsigned>(H);
+        const uint16_t* src = ok ? tb + hg_off[j] : zero + hg_lc[j] * 8;
+        glds16(src, buf + (wave * hglds + j) * 1024);
+      }
     }
   };
   issue_halo(t0, hl0);
@@ -1320,6 +1337,9 @@ __global__ void __launch_bounds__(kT, 1) conv3x3_c64_wgrad_kernel(const uint16_t
       const uint16_t* src = r < npx ? dY + (pix0 + r) * C + lc * 8 : zero + lc * 8;
       glds16(src, db + (wave * dglds + j) * 1024);
     }
+    // (the per-tile divisions stay here: precomputing this lane's halo
+    // geometry as in conv3x3_c64_kernel measured +8 % — 36 SGPR spills at the
+    // kernel's 300 VGPRs)
     for (int j = 0; j < hglds; ++j) {
       const int q = (wave * hglds + j) * 64 + lane;
       const int hp = q >> 3, pc = q & 7, lc = 2 * ((pc >> 1) ^ tr_f<64>(hp)) + (pc & 1);
@@ -1987,7 +2007,8 @@ void conv3x3_c64_wgrad_launch(const void* dY, const void* X, float* D, int N, in
 void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
                      int kh, int kw, int stride, int pad, const void* zero, float* ws, hipStream_t s) {
   if (wgrad_direct() && conv3x3_c64_direct(Cin, Cout, kh, kw, stride, pad, W) &&
-      2 * (((256 / W) * W + 31) / 32 * 32 * 128 + ((256 / W + 2) * (W + 2) * 128 + 4095) / 4096 * 4096) <= 160 * 1024) {
+      2 * (((256 / W) * W + 31) / 32 * 32 * 128 + ((256 / W + 2) * (W + 2) * 128 + 4095) / 4096 * 4096) <= 160 * 1024 &&
+      ((256 / W + 2) * (W + 2) * 128 + 4095) / 4096 <= kMaxHaloG) {
     conv3x3_c64_wgrad_launch(dY, X, D, N, H, W, zero, ws, s);
     return;
   }
