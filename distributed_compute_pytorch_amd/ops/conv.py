@@ -158,6 +158,10 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, dw, None
 
 
+# BN-prologue 1x1 conv (ResNet layer-1 conv3): BN backward reduce in the dgrad epilogue
+_PRO_RED = os.environ.get("DCP_PRO_RED", "1") == "1"
+
+
 class _BNReluConv1x1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, weight, running_mean, running_var, nbt, momentum, eps, stats, sums):
@@ -181,9 +185,15 @@ class _BNReluConv1x1Fn(torch.autograd.Function):
         dw = _C.conv1x1_wgrad(gz, x, scale, shift, True).view(ctx.wshape)
         if dw.dtype != ctx.wdtype:
             dw = dw.to(ctx.wdtype)
-        da = _C.conv1x1_dgrad(gz, wt)
-        # BN + ReLU backward; the ReLU mask is recomputed from x (training coefficients)
-        dx, dgamma, dbeta, _ = _C.bn_act_bwd(da, None, x, gamma, beta, mean, invstd, x, True, False, True, None)
+        if _PRO_RED:
+            # BN+ReLU backward reduction in the data-gradient GEMM's epilogue
+            # (gemm.hip RED: mask recomputed from x), then the apply pass alone
+            da, acc = _C.conv1x1_dgrad_bnred(gz, wt, x, gamma, beta, mean, invstd)
+            dx, dgamma, dbeta = _C.bn_act_bwd_apply(da, x, gamma, beta, mean, invstd, acc)
+        else:
+            da = _C.conv1x1_dgrad(gz, wt)
+            # BN + ReLU backward; the ReLU mask is recomputed from x (training coefficients)
+            dx, dgamma, dbeta, _ = _C.bn_act_bwd(da, None, x, gamma, beta, mean, invstd, x, True, False, True, None)
         return dx, dgamma, dbeta, dw, None, None, None, None, None, None, None
 
 
