@@ -1089,14 +1089,20 @@ constexpr int kMaxHaloG = 16;
 // at multiples of 16 and measured 36 % of LDS cycles in conflicts here
 __device__ __forceinline__ int d3_swz(int row) { return row & 7; }
 
-template <bool STATS>
+// EPI 0 = plain; 1 = STATS (Σy, Σy² into stats); 2 = RED (gemm_nt's BN+ReLU
+// backward reduction of the data gradient: stats += (Σg, Σg·(x - mean)),
+// g = dy·[x·sc + sf > 0], x = bnr.x the BN input)
+template <int EPI>
 __global__ void __launch_bounds__(kD3Threads, 1) conv3x3_c64_kernel(const uint16_t* __restrict__ X,
                                                                      const uint16_t* __restrict__ Wt,
                                                                      uint16_t* __restrict__ Y, int N, int H, int W,
                                                                      int R, int HT, int tiles, int per_block,
                                                                      const uint16_t* __restrict__ zero,
-                                                                     float* __restrict__ stats, int halo_bytes) {
+                                                                     float* __restrict__ stats, int halo_bytes,
+                                                                     BnRedArgs bnr = BnRedArgs{}) {
+  constexpr bool STATS = EPI == 1, RED = EPI == 2;
   constexpr int C = 64, WN = 32, FM = 4, FN = 2, LPR = WN / 8, RPI = 64 / LPR, CST = 32 * WN * 2;
+  constexpr int NR = 32 / RPI;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* wl = lds;                                // [9 * 64 rows][128 B] weights, row = tap * 64 + cout
   char* hl0 = lds + 9 * 64 * 128;                // two halo buffers of halo_bytes
@@ -1163,6 +1169,19 @@ __global__ void __launch_bounds__(kD3Threads, 1) conv3x3_c64_kernel(const uint16
   float ssum[8], ssq[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
+  // RED: mean / folded affine of this lane's 8 epilogue channels
+  float rmu[RED ? 8 : 1], rsc[RED ? 8 : 1], rsf[RED ? 8 : 1];
+  if (RED) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = wn * WN + (lane % LPR) * 8 + e;
+      const float mu = bnr.mean[c];
+      const float sc = (bnr.gamma ? bnr.gamma[c] : 1.f) * bnr.invstd[c];
+      rmu[RED ? e : 0] = mu;
+      rsc[RED ? e : 0] = sc;
+      rsf[RED ? e : 0] = (bnr.beta ? bnr.beta[c] : 0.f) - mu * sc;
+    }
+  }
 
   wait_vm<0>();
   barrier();
@@ -1216,6 +1235,18 @@ __global__ void __launch_bounds__(kD3Threads, 1) conv3x3_c64_kernel(const uint16
     const int npx = min(R, H - h0) * W;  // valid pixels of this tile
     const int64_t rowbase = (static_cast<int64_t>(n) * H + h0) * W;
     issued = 0;
+    // RED: both halves' x rows, loaded (row clamped) before the staging
+    uint4 xr[RED ? 2 * NR : 1];
+    if (RED) {
+#pragma unroll
+      for (int q = 0; q < 2 * NR; ++q) {
+        const int pix = wm * 64 + 32 * (q / NR) + (q % NR) * RPI + lane / LPR;
+        const bool ok = pix < npx;
+        const uint4 xv =
+            *reinterpret_cast<const uint4*>(bnr.x + (rowbase + (ok ? pix : 0)) * C + wn * WN + (lane % LPR) * 8);
+        xr[RED ? q : 0] = ok ? xv : make_uint4(0, 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -1239,6 +1270,18 @@ __global__ void __launch_bounds__(kD3Threads, 1) conv3x3_c64_kernel(const uint16
         if (wm * 64 + 32 * h + it * RPI < npx) ++issued;  // uniform: this store instruction runs
         if (i < npx) {
           *reinterpret_cast<uint4*>(Y + (rowbase + i) * C + wn * WN + c * 8) = v;
+          if (RED) {
+            const uint4 xv = xr[RED ? h * NR + it : 0];
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, x4[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float xk = (k & 1) ? bf_hi(x4[k >> 1]) : bf_lo(x4[k >> 1]);
+              float gk = (k & 1) ? bf_hi(w4[k >> 1]) : bf_lo(w4[k >> 1]);
+              gk = fmaf(xk, rsc[RED ? k : 0], rsf[RED ? k : 0]) > 0.f ? gk : 0.f;
+              ssum[k] += gk;
+              ssq[k] = fmaf(gk, xk - rmu[RED ? k : 0], ssq[k]);
+            }
+          }
           if (STATS) {
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -1254,7 +1297,7 @@ __global__ void __launch_bounds__(kD3Threads, 1) conv3x3_c64_kernel(const uint16
       }
     }
   }
-  if (STATS) {
+  if (STATS || RED) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
 #pragma unroll
@@ -1642,12 +1685,22 @@ void gemm_nt_resred_bf16(const void* A, const void* B, void* C, int64_t M, int N
   gemm_nt_launch<false>(A, B, C, M, N, K, nullptr, nullptr, false, acc, ConvGeo{}, s, &r);
 }
 
+namespace {
+inline bool conv3x3_c64_direct(int Cin, int Cout, int kh, int kw, int stride, int pad, int W);
+void conv3x3_c64_launch(const void* X, const void* Wt, void* Y, int N, int H, int W, const void* zero, float* stats,
+                        hipStream_t s, const BnRedArgs* red = nullptr);
+}  // namespace
+
 void conv_fwd_bnred_bf16(const void* X, const void* Wt, void* Y, int N, int H, int W, int Cin, int Ho, int Wo,
                          int Cout, int kh, int kw, int stride, int pad, const void* zero, const void* x,
                          const float* gamma, const float* beta, const float* mean, const float* invstd, float* acc,
                          hipStream_t s) {
   ConvGeo geo{H, W, Ho, Wo, stride, pad, kw, static_cast<const uint16_t*>(zero), Cin};
   const BnRedArgs r{static_cast<const uint16_t*>(x), gamma, beta, mean, invstd};
+  if (conv3x3_c64_direct(Cin, Cout, kh, kw, stride, pad, W)) {  // the direct kernel's RED epilogue
+    conv3x3_c64_launch(X, Wt, Y, N, H, W, zero, acc, s, &r);
+    return;
+  }
   gemm_nt_launch<true>(X, Wt, Y, static_cast<int64_t>(N) * Ho * Wo, Cout, kh * kw * Cin, nullptr, nullptr, false,
                        acc, geo, s, &r);
 }
@@ -1744,7 +1797,7 @@ inline bool conv3x3_c64_direct(int Cin, int Cout, int kh, int kw, int stride, in
 }
 
 void conv3x3_c64_launch(const void* X, const void* Wt, void* Y, int N, int H, int W, const void* zero, float* stats,
-                        hipStream_t s) {
+                        hipStream_t s, const BnRedArgs* red) {
   const int R = 128 / W;                       // whole output rows per tile
   const int HT = (H + R - 1) / R;
   const int tiles = N * HT;
@@ -1758,19 +1811,24 @@ void conv3x3_c64_launch(const void* X, const void* Wt, void* Y, int N, int H, in
   auto y = static_cast<uint16_t*>(Y);
   auto z = static_cast<const uint16_t*>(zero);
   static const bool attr = [] {  // > 64 KB of dynamic LDS
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_c64_kernel<true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_c64_kernel<0>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_c64_kernel<false>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_c64_kernel<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3_c64_kernel<2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)attr;
-  if (stats)
-    hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3(P), dim3(kD3Threads), lds, s, x, w, y, N, H, W, R, HT, tiles,
-                       per_block, z, stats, halo_bytes);
+  if (red)
+    hipLaunchKernelGGL(conv3x3_c64_kernel<2>, dim3(P), dim3(kD3Threads), lds, s, x, w, y, N, H, W, R, HT, tiles,
+                       per_block, z, stats, halo_bytes, *red);
+  else if (stats)
+    hipLaunchKernelGGL(conv3x3_c64_kernel<1>, dim3(P), dim3(kD3Threads), lds, s, x, w, y, N, H, W, R, HT, tiles,
+                       per_block, z, stats, halo_bytes, BnRedArgs{});
   else
-    hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3(P), dim3(kD3Threads), lds, s, x, w, y, N, H, W, R, HT, tiles,
-                       per_block, z, stats, halo_bytes);
+    hipLaunchKernelGGL(conv3x3_c64_kernel<0>, dim3(P), dim3(kD3Threads), lds, s, x, w, y, N, H, W, R, HT, tiles,
+                       per_block, z, stats, halo_bytes, BnRedArgs{});
 }
 }  // namespace
 

@@ -34,10 +34,11 @@ KXK_GEMM = os.environ.get("DCP_KXK_GEMM", "1") == "1"
 # BN1→conv2 / BN2→conv3 as one autograd node whose data-gradient GEMM reduces
 # the BN backward in its epilogue (gemm.hip RED). Bit mask: 1 = BN1→conv2
 # (stride-1 3x3 on the gathered GEMM, Cin > 64), 2 = BN2→conv3 (1x1, the wide
-# layers whose BN2 is not a GEMM prologue). Round 1 measured both −1 % (the RED
+# layers whose BN2 is not a GEMM prologue), 4 = BN1→conv2 for Cin = 64 (layer 1:
+# the direct 3x3 kernel's RED epilogue). Round 1 measured both −1 % (the RED
 # coefficients in LDS pushed the GEMM to one workgroup per CU); round 2 with
 # them in registers (profiles/r2_ab_bn_conv_fuse.jsonl): 2 = +0.3 %, 1 = −0.8 %.
-BN_CONV_FUSE = int(os.environ.get("DCP_BN_CONV_FUSE", "2") or 0)
+BN_CONV_FUSE = int(os.environ.get("DCP_BN_CONV_FUSE", "6") or 0)
 # BN-apply prologue in the conv3 GEMM only while Cout ≤ this (≤ 2 N-tiles of 128)
 PRO_MAX_COUT = int(os.environ.get("DCP_PRO_MAX_COUT", "256"))
 # conv1 + bn1 + relu + maxpool as one fused node (ops/stem.py); 0 = per-module path
@@ -151,8 +152,8 @@ class Bottleneck(nn.Module):
         c2 = self.conv2
         s2 = None
         fuse3 = bool(BN_CONV_FUSE & 2)
-        if (KXK_GEMM and BN_CONV_FUSE & 1 and conv_kxk_gemm_ok(z1, c2) and c2.stride == (1, 1)
-                and c2.in_channels > 64):
+        if (KXK_GEMM and conv_kxk_gemm_ok(z1, c2) and c2.stride == (1, 1)
+                and ((BN_CONV_FUSE & 1 and c2.in_channels > 64) or (BN_CONV_FUSE & 4 and c2.in_channels == 64))):
             x2, s2 = bn_relu_conv(z1, self.bn1, c2.weight, c2.kernel_size[0], c2.stride[0], c2.padding[0], sums=s1,
                                   stats=True)
             return self._tail(x2, s2, identity, dual, fuse3, resbn, nxt)

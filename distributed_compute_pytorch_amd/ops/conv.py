@@ -335,9 +335,14 @@ class _BNReluConvFn(torch.autograd.Function):
             w, wt = _w2d(weight)
             z, st = _C.conv1x1_fwd(y, w, None, None, False, bool(stats))
         else:
-            w = weight.detach().to(torch.bfloat16)
-            wt = None
-            z, st = _C.conv_fwd(y, w.permute(0, 2, 3, 1).contiguous(), k, k, stride, pad, bool(stats))
+            pre = _prepped(weight)
+            if pre is not None:  # bf16 operands from the model's one-launch ConvWeightPrep
+                wf, wt = pre     # wt: the flipped data-gradient weight [Cin][k][k][Cout]
+                w = wf.permute(0, 3, 1, 2)
+            else:
+                w = weight.detach().to(torch.bfloat16)
+                wf, wt = w.permute(0, 2, 3, 1).contiguous(), None
+            z, st = _C.conv_fwd(y, wf, k, k, stride, pad, bool(stats))
         ctx.save_for_backward(x, y, gamma, beta, mean, invstd, w, wt)
         ctx.cfg = (k, stride, pad, weight.shape, weight.dtype)
         ctx.mark_non_differentiable(st)
@@ -359,7 +364,7 @@ class _BNReluConvFn(torch.autograd.Function):
         else:
             dw, join = _wgrad_async(rows, lambda: _C.conv_wgrad(gz, y, k, k, stride, pad), gz, y)
             if stride == 1:
-                wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Cin][k][k][Cout]
+                wd = wt if wt is not None else w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Cin][k][k][Cout]
                 dy, acc = _C.conv_dgrad_bnred(gz, wd, k, k, k - 1 - pad, x, gamma, beta, mean, invstd)
             else:
                 dy = torch.ops.aten.convolution_backward(gz, y, w, None, [stride, stride], [pad, pad], [1, 1],

@@ -262,17 +262,19 @@ def test_conv_kxk_gemm_miopen_routes(cuda):
         assert _rel(a, b) < 1e-2
 
 
-@pytest.mark.parametrize("k,stride,pad,sums", [(3, 1, 1, True), (3, 2, 1, False), (1, 1, 0, True)])
-def test_bn_relu_conv_fused_autograd(cuda, k, stride, pad, sums):
+@pytest.mark.parametrize("k,stride,pad,sums,co", [(3, 1, 1, True, 128), (3, 2, 1, False, 128), (1, 1, 0, True, 128),
+                                                  (3, 1, 1, True, 64)])
+def test_bn_relu_conv_fused_autograd(cuda, k, stride, pad, sums, co):
     """BN(train)→ReLU→conv as one node (BN backward reduced in the dgrad GEMM's
-    epilogue) vs the fp32 ATen composition on the same bf16 input."""
+    epilogue) vs the fp32 ATen composition on the same bf16 input. co = 64:
+    the direct 3x3 / 64-channel kernels, the dgrad's RED epilogue included."""
     from torch import nn
 
     from distributed_compute_pytorch_amd.ops.batchnorm import BatchNormAct2d
     from distributed_compute_pytorch_amd.ops.conv import bn_relu_conv
 
     g = torch.Generator().manual_seed(13)
-    n, h, w, ci, co = 4, 12, 12, 64, 128
+    n, h, w, ci = 4, 12, 12, 64
     x = (_x(n, h, w, ci, cuda, g).float() * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     bn = BatchNormAct2d(ci, act=True, fused=True).to(cuda)
     with torch.no_grad():
