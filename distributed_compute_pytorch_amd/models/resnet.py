@@ -37,8 +37,10 @@ KXK_GEMM = os.environ.get("DCP_KXK_GEMM", "1") == "1"
 # layers whose BN2 is not a GEMM prologue), 4 = BN1→conv2 for Cin = 64 (layer 1:
 # the direct 3x3 kernel's RED epilogue). Round 1 measured both −1 % (the RED
 # coefficients in LDS pushed the GEMM to one workgroup per CU); round 2 with
-# them in registers (profiles/r2_ab_bn_conv_fuse.jsonl): 2 = +0.3 %, 1 = −0.8 %.
-BN_CONV_FUSE = int(os.environ.get("DCP_BN_CONV_FUSE", "6") or 0)
+# them in registers (profiles/r2_ab_bn_conv_fuse.jsonl): 2 = +0.3 %, 1 = −0.8 %;
+# after the epilogue scratch fix (NOTES §20) 1 turned +0.55 % and 4 +0.27 %:
+# default 7 (profiles/r2_ab_bn_conv_fuse7.jsonl, r2_ab_bn1_red_c64.jsonl).
+BN_CONV_FUSE = int(os.environ.get("DCP_BN_CONV_FUSE", "7") or 0)
 # BN-apply prologue in the conv3 GEMM only while Cout ≤ this (≤ 2 N-tiles of 128)
 PRO_MAX_COUT = int(os.environ.get("DCP_PRO_MAX_COUT", "256"))
 # conv1 + bn1 + relu + maxpool as one fused node (ops/stem.py); 0 = per-module path
