@@ -333,15 +333,21 @@ void Reducer::launch(Bucket& b) {
   for (auto& g : b.pending_grads) g = at::Tensor();
   b.stats.ready_ms = static_cast<double>(now_ms()) - backward_t0_ms_;
   trace::Range r("dcp.reducer.bucket_allreduce");
+  const bool check = check_ && !capturing(b.wire);
+  if (check) {
+    // packed-buffer checksum, taken BEFORE the bucket's collective is issued:
+    // that collective reduces b.wire in place (on the comm stream after an
+    // event recorded now, or on the host communicator's worker), so a
+    // checksum enqueued after it would race with the reduction
+    b.check_sum = b.wire.to(at::kDouble).sum().reshape({1}).to(at::kFloat);
+  }
   if (comm_hook_) {
     b.work = comm_hook_(b.wire, static_cast<int64_t>(&b - buckets_.data()));
   } else {
     b.work = comm_->all_reduce(b.wire, opts_.average ? ReduceOp::AVG : ReduceOp::SUM);
   }
-  if (check_ && !capturing(b.wire)) {
-    // packed-buffer checksum on the compute stream (ordered after the pack),
+  if (check) {
     // reduced by a collective issued right after the bucket's own
-    b.check_sum = b.wire.to(at::kDouble).sum().reshape({1}).to(at::kFloat);
     b.check_work = comm_->all_reduce(b.check_sum, opts_.average ? ReduceOp::AVG : ReduceOp::SUM);
   }
   b.launched = true;
