@@ -124,9 +124,10 @@ def test_resnet_step_with_prep_and_resbn_matches_plain(cuda, monkeypatch):
     torch.testing.assert_close(b1, b2, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("C,Co,N,hw,resbn", [(256, 64, 4, 14, False), (256, 64, 4, 14, True),
-                                             (512, 128, 3, 9, False), (1024, 256, 2, 7, True)])
-def test_bn_res_act_conv1x1_matches_reference(cuda, C, Co, N, hw, resbn):
+@pytest.mark.parametrize("C,Co,N,hw,resbn,with_gy", [(256, 64, 4, 14, False, True), (256, 64, 4, 14, True, True),
+                                                     (512, 128, 3, 9, False, True), (1024, 256, 2, 7, True, True),
+                                                     (256, 64, 4, 14, False, False)])
+def test_bn_res_act_conv1x1_matches_reference(cuda, C, Co, N, hw, resbn, with_gy):
     """Block boundary node (ops/conv.py bn_res_act_conv1x1): relu(bn3(z3) + r)
     → next conv1, with BN3's backward reduced in conv1's dgrad epilogue
     (gemm.hip RESRED), against the fp32 composition: outputs, sums, running
@@ -155,7 +156,11 @@ def test_bn_res_act_conv1x1_matches_reference(cuda, C, Co, N, hw, resbn):
         y, z1, s1 = bn_res_act_conv1x1(bn3, za, _sums(z3), None, w, (bnd, ra, _sums(r)))
     else:
         y, z1, s1 = bn_res_act_conv1x1(bn3, za, _sums(z3), ra, w)
-    torch.autograd.backward([y, z1], [gy, gz])
+    if with_gy:
+        torch.autograd.backward([y, z1], [gy, gz])
+    else:  # y's own consumer unused: no second gradient (RESRED's gy2 = None path)
+        z1.backward(gz)
+        gy = torch.zeros_like(gy)
 
     zr = z3.float().requires_grad_(True)
     rr = r.float().requires_grad_(True)
