@@ -90,18 +90,45 @@ def parse():
                     help="comma-separated bucket caps in MiB: one timed run and one JSON line per cap")
     ap.add_argument("--ref-1gpu", type=float, default=None,
                     help="1-GPU samples/s of the same config: adds scaling_efficiency = value / (N * ref)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="1 GPU only: every bucket all-reduce is replaced by a contention emulation of an N-rank "
+                         "ring all-reduce on the comm stream (parallel/comm_hooks.py; NOTES §22)")
+    ap.add_argument("--emulate-busbw", type=float, default=300.0, help="emulated bus bandwidth, GB/s")
+    ap.add_argument("--emulate-channels", type=int, default=16, help="emulated RCCL channels (workgroups)")
+    ap.add_argument("--reserve-cus", type=int, default=None,
+                    help="CUs the persistent GEMM / conv grids leave free for collectives (DCP_RESERVE_CUS)")
     return ap.parse_args()
+
+
+def _visible_gpus() -> int:
+    """GPUs this process could use, counted WITHOUT the HIP runtime (the
+    self-launching parent must not create a device context): the KFD topology
+    nodes with a non-zero gpu_id, narrowed by a *_VISIBLE_DEVICES list."""
+    import glob
+
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+        try:
+            with open(f) as fh:
+                n += int(fh.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            pass
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([d for d in v.split(",") if d.strip() != ""]))
+    return n
 
 
 def _self_launch(a) -> int:
     """``--gpus N`` without a launcher: start N ranks of this script (RANK /
     LOCAL_RANK / WORLD_SIZE / MASTER_* set, one process per GPU) and return the
-    job's exit code; rank 0 prints the JSON line. The parent never initialises
-    the GPU (device_count() does not, on this image) and does not import the
-    package (its extension links the HIP runtime)."""
+    job's exit code; rank 0 prints the JSON line. The parent never touches the
+    HIP runtime (it counts GPUs from sysfs) and does not import the package
+    (its extension links the HIP runtime)."""
     import importlib.util
 
-    n = torch.cuda.device_count()
+    n = _visible_gpus()
     if n < a.gpus and a.backend != "gloo":
         log(f"[bench] --gpus {a.gpus} requested but only {n} GPU(s) are visible; refusing to oversubscribe "
             f"(RCCL needs one device per rank)")
@@ -145,6 +172,12 @@ def main():
         log(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if a.comm_timing:
         os.environ["DCP_COMM_TIMING"] = "1"  # read by the communicator / Reducer at construction
+    if a.emulate_world:
+        if world != 1:
+            raise SystemExit("--emulate-world stands in for the peers of a 1-GPU run")
+        os.environ["DCP_SINGLE_RANK_HOP"] = "1"  # collectives on the comm stream, as at N > 1
+    if a.reserve_cus is not None:
+        os.environ["DCP_RESERVE_CUS"] = str(a.reserve_cus)  # read when the extension loads
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
     if a.backend == "gloo":
@@ -199,6 +232,8 @@ def main():
         if cap_mb is not None:
             kw["bucket_cap_mb"] = cap_mb
         if ours:
+            # the xGMI-tuned bucket plan (NOTES §18) unless overridden on the CLI
+            kw = {**dcp.parallel.XGMI_BUCKETS, **kw}
             if a.first_bucket_mb is not None:
                 kw["first_bucket_mb"] = a.first_bucket_mb
             if a.comm_dtype == "bf16":
@@ -207,6 +242,12 @@ def main():
                 ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[local],
                                                            gradient_as_bucket_view=bool(a.grad_as_view), **kw)
                 opt = wl.make_optimizer(ddp.parameters())
+            if a.emulate_world:
+                from distributed_compute_pytorch_amd.parallel import comm_hooks
+
+                ddp.register_comm_hook(comm_hooks.ContentionEmulation(a.emulate_world, a.emulate_busbw,
+                                                                      a.emulate_channels),
+                                       comm_hooks.contention_emulation_hook)
             return ddp, opt
         with stream_ctx():
             ddp = torch.nn.parallel.DistributedDataParallel(wl.model, device_ids=[local], **kw)
@@ -258,6 +299,11 @@ def main():
             }
             if a.model == "resnet50":
                 cfg.update(mfma_1x1_gemm=bool(a.gemm) and fused, image_size=224, channels_last=bool(a.channels_last))
+            if a.emulate_world:
+                cfg["emulated_comm"] = {"world": a.emulate_world, "busbw_gbps": a.emulate_busbw,
+                                        "channels": a.emulate_channels}
+            if a.reserve_cus is not None:
+                cfg["reserve_cus"] = a.reserve_cus
             if ours:
                 cfg["bucket_cap_mb"] = round(info["bucket_cap_bytes"] / 2**20, 3)
                 cfg["first_bucket_mb"] = round(info["first_bucket_bytes"] / 2**20, 3)

@@ -5,6 +5,7 @@
 #include "comm/communicator.h"
 #include "common.h"
 #include "fused.h"
+#include "kernels/gemm_kernels.h"
 #include "ops.h"
 #include "reducer/reducer.h"
 
@@ -109,6 +110,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("recv", &Communicator::recv, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &Communicator::barrier, py::call_guard<py::gil_scoped_release>())
       .def("abort", &Communicator::abort)
+      .def("stream_fence", &Communicator::stream_fence, py::call_guard<py::gil_scoped_release>())
+      .def("emulate_all_reduce", &Communicator::emulate_all_reduce, py::arg("t"), py::arg("world"),
+           py::arg("busbw_gbps"), py::arg("channels"), py::arg("alpha_us") = 20.0,
+           py::call_guard<py::gil_scoped_release>())
       .def("split", &Communicator::split, py::arg("color"), py::arg("key"), py::arg("prefix"),
            py::call_guard<py::gil_scoped_release>())
       .def("error", &Communicator::error)
@@ -162,19 +167,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("params"), py::arg("buckets"), py::arg("comm"), py::arg("options"))
       .def("prepare_for_backward", &Reducer::prepare_for_backward, py::arg("outputs"), py::arg("require_sync"))
       .def("set_expect_backward", &Reducer::set_expect_backward)
-      .def("set_comm_hook", [](Reducer& r, py::object fn) {
+      .def("set_comm_hook", [](Reducer& r, py::object fn, py::object wire_dtype) {
              if (fn.is_none()) {
                r.set_comm_hook(nullptr);
                return;
              }
+             at::ScalarType wdt = at::ScalarType::Undefined;
+             if (!wire_dtype.is_none()) wdt = torch::python::detail::py_object_to_dtype(wire_dtype);
              auto holder = std::make_shared<py::object>(fn);
              r.set_comm_hook([holder](at::Tensor& bucket, int64_t index) -> WorkPtr {
                py::gil_scoped_acquire g;
                py::object res = (*holder)(bucket, index);
                if (res.is_none()) return std::make_shared<DoneWork>();
                return res.cast<WorkPtr>();
-             });
-           })
+             }, wdt);
+           }, py::arg("fn"), py::arg("wire_dtype") = py::none())
       .def("bucket_indices", &Reducer::bucket_indices)
       .def("bucket_sizes_bytes", &Reducer::bucket_sizes_bytes)
       .def("bucket_stats", &Reducer::bucket_stats)
@@ -198,6 +205,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq", &ops::sumsq);
   m.def("scale_by", &ops::scale_by);
   m.def("table_cache_size", &ops::table_cache_size);
+
+  m.def("gemm_tune", [](const std::string& k, int v) { kern::gemm_tune(k.c_str(), v); });
+  m.def("gemm_tune_get", [](const std::string& k) { return kern::gemm_tune_get(k.c_str()); });
 
   fused::bind(m);
   stem::bind(m);

@@ -71,6 +71,23 @@ class Communicator {
   }
   // raw handle of the device stream collectives run on (0 = none / host)
   virtual int64_t stream_handle() const { return 0; }
+  // A Work that completes when everything the caller's stream has queued so
+  // far has run, ordered through the collective stream exactly like a
+  // collective (event edge, deadline tracking, watchdog) but issuing no
+  // collective. Backs fault-injection tests of the watchdog → abort path
+  // (a stalled caller stream looks like a hung collective). Host backend:
+  // nullptr (no device stream).
+  virtual std::shared_ptr<Work> stream_fence() { return nullptr; }
+  // Contention emulation of an all-reduce of `t` among `world` ranks on a
+  // single GPU (bench.py --emulate-world): `channels` workgroups on the
+  // collective stream move the ring all-reduce's 2(world-1)/world × bytes
+  // through HBM and hold their CUs for alpha_us + those bytes / busbw_gbps —
+  // the footprint the real collective has on this GPU while backward runs.
+  // `t` is read, never written. Returns a Work like a collective's.
+  virtual std::shared_ptr<Work> emulate_all_reduce(at::Tensor& t, int world, double busbw_gbps, int channels,
+                                                   double alpha_us) {
+    throw std::runtime_error(backend() + " communicator cannot emulate collectives");
+  }
   // Non-empty once the communicator hit an unrecoverable error.
   virtual std::string error() { return {}; }
 

@@ -117,19 +117,19 @@ class HostCommunicator : public Communicator {
   }
 
   WorkPtr all_gather(at::Tensor& out, const at::Tensor& in) override {
-    DCP_CHECK(out.numel() == in.numel() * size_, "all_gather: out.numel must be size*in.numel");
+    DK_CHECK(out.numel() == in.numel() * size_, "all_gather: out.numel must be size*in.numel");
     account("all_gather", in);
     return submit({out, in}, [this](std::vector<at::Tensor>& ts) { ring_all_gather(ts[0], ts[1]); });
   }
 
   WorkPtr reduce_scatter(at::Tensor& out, const at::Tensor& in, ReduceOp op) override {
-    DCP_CHECK(in.numel() == out.numel() * size_, "reduce_scatter: in.numel must be size*out.numel");
+    DK_CHECK(in.numel() == out.numel() * size_, "reduce_scatter: in.numel must be size*out.numel");
     account("reduce_scatter", in, static_cast<int>(op));
     return submit({out, in}, [this, op](std::vector<at::Tensor>& ts) { ring_reduce_scatter(ts[0], ts[1], op); });
   }
 
   WorkPtr all_to_all(at::Tensor& out, const at::Tensor& in) override {
-    DCP_CHECK(in.numel() == out.numel() && in.numel() % size_ == 0, "all_to_all: bad sizes");
+    DK_CHECK(in.numel() == out.numel() && in.numel() % size_ == 0, "all_to_all: bad sizes");
     account("all_to_all", in);
     return submit({out, in}, [this](std::vector<at::Tensor>& ts) { do_all_to_all(ts[0], ts[1]); });
   }
@@ -138,7 +138,7 @@ class HostCommunicator : public Communicator {
     ops_.fetch_add(1);
     return submit({t}, [this, dst](std::vector<at::Tensor>& ts) {
       auto& x = ts[0];
-      DCP_CHECK(net::send_all(peers_[dst], x.data_ptr(), x.numel() * x.element_size()), "send failed");
+      DK_CHECK(net::send_all(peers_[dst], x.data_ptr(), x.numel() * x.element_size()), "send failed");
     });
   }
 
@@ -146,7 +146,7 @@ class HostCommunicator : public Communicator {
     ops_.fetch_add(1);
     return submit({t}, [this, src](std::vector<at::Tensor>& ts) {
       auto& x = ts[0];
-      DCP_CHECK(net::recv_all(peers_[src], x.data_ptr(), x.numel() * x.element_size(), timeout_ms_),
+      DK_CHECK(net::recv_all(peers_[src], x.data_ptr(), x.numel() * x.element_size(), timeout_ms_),
                 "recv failed: peer closed");
     });
   }
@@ -175,7 +175,7 @@ class HostCommunicator : public Communicator {
         staged = true;
         host[i] = ts[i].to(at::kCPU).contiguous();
       } else {
-        DCP_CHECK(ts[i].is_contiguous(), "host communicator needs contiguous tensors");
+        DK_CHECK(ts[i].is_contiguous(), "host communicator needs contiguous tensors");
         host[i] = ts[i];
       }
     }
@@ -237,15 +237,15 @@ class HostCommunicator : public Communicator {
       const auto colon = addr.rfind(':');
       int fd = net::connect_to(addr.substr(0, colon), std::stoi(addr.substr(colon + 1)), timeout_ms_);
       int32_t r = rank_;
-      DCP_CHECK(net::send_all(fd, &r, sizeof(r)), "mesh handshake failed");
+      DK_CHECK(net::send_all(fd, &r, sizeof(r)), "mesh handshake failed");
       net::set_bufsizes(fd, 4 << 20);
       peers_[j] = fd;
     }
     for (int k = rank_ + 1; k < size_; ++k) {
       int fd = net::accept_one(listen_fd_, timeout_ms_);
       int32_t r = -1;
-      DCP_CHECK(net::recv_all(fd, &r, sizeof(r), timeout_ms_), "mesh handshake failed");
-      DCP_CHECK(r > rank_ && r < size_ && peers_[r] < 0, "mesh handshake: unexpected rank ", r);
+      DK_CHECK(net::recv_all(fd, &r, sizeof(r), timeout_ms_), "mesh handshake failed");
+      DK_CHECK(r > rank_ && r < size_ && peers_[r] < 0, "mesh handshake: unexpected rank ", r);
       net::set_bufsizes(fd, 4 << 20);
       peers_[r] = fd;
     }
@@ -334,9 +334,9 @@ class HostCommunicator : public Communicator {
     const size_t bytes = static_cast<size_t>(t.numel() * t.element_size());
     if (rank_ == root) {
       for (int j = 0; j < size_; ++j)
-        if (j != root) DCP_CHECK(net::send_all(peers_[j], t.data_ptr(), bytes), "broadcast send failed");
+        if (j != root) DK_CHECK(net::send_all(peers_[j], t.data_ptr(), bytes), "broadcast send failed");
     } else {
-      DCP_CHECK(net::recv_all(peers_[root], t.data_ptr(), bytes, timeout_ms_), "broadcast recv failed");
+      DK_CHECK(net::recv_all(peers_[root], t.data_ptr(), bytes, timeout_ms_), "broadcast recv failed");
     }
   }
 

@@ -19,6 +19,7 @@
 #include <thread>
 
 #include "../common.h"
+#include "../kernels/kernels.h"
 #include "communicator.h"
 
 namespace dcp {
@@ -28,13 +29,13 @@ namespace {
 #define HIP_OK(expr)                                                                          \
   do {                                                                                        \
     hipError_t _e = (expr);                                                                   \
-    DCP_CHECK(_e == hipSuccess, #expr, " failed: ", hipGetErrorString(_e));                    \
+    DK_CHECK(_e == hipSuccess, #expr, " failed: ", hipGetErrorString(_e));                    \
   } while (0)
 
 #define NCCL_OK(expr)                                                                         \
   do {                                                                                        \
     ncclResult_t _r = (expr);                                                                 \
-    DCP_CHECK(_r == ncclSuccess || _r == ncclInProgress, #expr, " failed: ", ncclGetErrorString(_r)); \
+    DK_CHECK(_r == ncclSuccess || _r == ncclInProgress, #expr, " failed: ", ncclGetErrorString(_r)); \
   } while (0)
 
 ncclDataType_t to_nccl(at::ScalarType st) {
@@ -56,7 +57,7 @@ ncclRedOp_t to_nccl(ReduceOp op, at::ScalarType st) {
   switch (op) {
     case ReduceOp::SUM: return ncclSum;
     case ReduceOp::AVG:
-      DCP_CHECK(at::isFloatingType(st), "ReduceOp.AVG needs a floating dtype");
+      DK_CHECK(at::isFloatingType(st), "ReduceOp.AVG needs a floating dtype");
       return ncclAvg;
     case ReduceOp::PRODUCT: return ncclProd;
     case ReduceOp::MIN: return ncclMin;
@@ -113,7 +114,7 @@ class RcclCommunicator : public Communicator {
         store_->set(key, std::string(reinterpret_cast<const char*>(&id), sizeof(id)));
       } else {
         const std::string v = store_->get(key);
-        DCP_CHECK(v.size() == sizeof(id), "RCCL unique id has wrong size");
+        DK_CHECK(v.size() == sizeof(id), "RCCL unique id has wrong size");
         std::memcpy(&id, v.data(), sizeof(id));
       }
       NCCL_OK(ncclCommInitRank(&comm_, size_, id, rank_));
@@ -167,7 +168,7 @@ class RcclCommunicator : public Communicator {
   WorkPtr all_gather(at::Tensor& out, const at::Tensor& in) override {
     check_tensor(out);
     check_tensor(in);
-    DCP_CHECK(out.numel() == in.numel() * size_, "all_gather: out.numel must be size*in.numel");
+    DK_CHECK(out.numel() == in.numel() * size_, "all_gather: out.numel must be size*in.numel");
     account("all_gather", in);
     return launch({out, in}, [&](hipStream_t s) {
       NCCL_OK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm_, s));
@@ -177,7 +178,7 @@ class RcclCommunicator : public Communicator {
   WorkPtr reduce_scatter(at::Tensor& out, const at::Tensor& in, ReduceOp op) override {
     check_tensor(out);
     check_tensor(in);
-    DCP_CHECK(in.numel() == out.numel() * size_, "reduce_scatter: in.numel must be size*out.numel");
+    DK_CHECK(in.numel() == out.numel() * size_, "reduce_scatter: in.numel must be size*out.numel");
     account("reduce_scatter", in, static_cast<int>(op));
     return launch({out, in}, [&](hipStream_t s) {
       NCCL_OK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), to_nccl(in.scalar_type()),
@@ -188,7 +189,7 @@ class RcclCommunicator : public Communicator {
   WorkPtr all_to_all(at::Tensor& out, const at::Tensor& in) override {
     check_tensor(out);
     check_tensor(in);
-    DCP_CHECK(in.numel() == out.numel() && in.numel() % size_ == 0, "all_to_all: bad sizes");
+    DK_CHECK(in.numel() == out.numel() && in.numel() % size_ == 0, "all_to_all: bad sizes");
     account("all_to_all", in);
     return launch({out, in}, [&](hipStream_t s) {
       const int64_t m = in.numel() / size_;
@@ -217,6 +218,26 @@ class RcclCommunicator : public Communicator {
     return launch({t}, [&](hipStream_t s) {
       NCCL_OK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), src, comm_, s));
     });
+  }
+
+  WorkPtr emulate_all_reduce(at::Tensor& t, int world, double busbw_gbps, int channels, double alpha_us) override {
+    check_tensor(t);
+    DK_CHECK(world >= 2 && busbw_gbps > 0 && channels > 0, "emulate_all_reduce: bad parameters");
+    const int64_t bytes = t.numel() * t.element_size();
+    const double move = 2.0 * (world - 1) / world * static_cast<double>(bytes);
+    const double us = alpha_us + move / (busbw_gbps * 1e3);  // GB/s = 1e3 bytes per µs
+    if (!emu_scratch_.defined() || emu_scratch_.numel() < bytes)
+      emu_scratch_ = at::empty({bytes}, t.options().dtype(at::kByte));
+    ops_.fetch_add(1);
+    at::Tensor scratch = emu_scratch_;
+    return launch({t, scratch}, [&](hipStream_t s) {
+      kern::comm_emulate(t.data_ptr(), scratch.data_ptr(), bytes, static_cast<int64_t>(move), channels, us, s);
+    });
+  }
+
+  WorkPtr stream_fence() override {
+    ops_.fetch_add(1);
+    return launch({}, [](hipStream_t) {});
   }
 
   WorkPtr barrier() override {
@@ -270,9 +291,9 @@ class RcclCommunicator : public Communicator {
 
  private:
   void check_tensor(const at::Tensor& t) {
-    DCP_CHECK(t.is_cuda(), "RCCL communicator needs device tensors");
-    DCP_CHECK(t.get_device() == device_, "tensor on device ", t.get_device(), " but communicator on ", device_);
-    DCP_CHECK(t.is_contiguous() || t.is_non_overlapping_and_dense(), "RCCL needs dense tensors");
+    DK_CHECK(t.is_cuda(), "RCCL communicator needs device tensors");
+    DK_CHECK(t.get_device() == device_, "tensor on device ", t.get_device(), " but communicator on ", device_);
+    DK_CHECK(t.is_contiguous() || t.is_non_overlapping_and_dense(), "RCCL needs dense tensors");
   }
 
   template <typename F>
@@ -366,6 +387,7 @@ class RcclCommunicator : public Communicator {
   std::list<std::weak_ptr<RcclWork>> inflight_;
   std::thread watchdog_;
   at::Tensor barrier_buf_;
+  at::Tensor emu_scratch_;
   hipEvent_t ready_ = nullptr;
 };
 
@@ -392,7 +414,7 @@ void RcclWork::synchronize() {
     comm_->raise_if_error();
     hipError_t e = hipEventQuery(end_);
     if (e == hipSuccess) return;
-    DCP_CHECK(e == hipErrorNotReady, "hipEventQuery failed: ", hipGetErrorString(e));
+    DK_CHECK(e == hipErrorNotReady, "hipEventQuery failed: ", hipGetErrorString(e));
     std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
 }

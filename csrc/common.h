@@ -27,7 +27,7 @@ inline std::string str_cat(Args&&... args) {
   return os.str();
 }
 
-#define DCP_CHECK(cond, ...)                                                        \
+#define DK_CHECK(cond, ...)                                                        \
   do {                                                                              \
     if (!(cond)) {                                                                  \
       throw ::dcp::Error(::dcp::str_cat(__FILE__, ":", __LINE__, ": ", __VA_ARGS__)); \

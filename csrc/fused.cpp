@@ -32,11 +32,11 @@ int bn_dtype(const at::Tensor& x) {
 }
 
 void check_nhwc(const at::Tensor& x, const char* what) {
-  DCP_CHECK(x.is_cuda(), what, ": device tensor required");
-  DCP_CHECK((x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)) || (x.dim() == 2 && x.is_contiguous()),
+  DK_CHECK(x.is_cuda(), what, ": device tensor required");
+  DK_CHECK((x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)) || (x.dim() == 2 && x.is_contiguous()),
             what, ": expected a channels_last 4-D or contiguous [N, C] tensor");
-  DCP_CHECK(kern::bn_supported(static_cast<int>(x.size(1))), what, ": unsupported channel count ", x.size(1));
-  DCP_CHECK(x.numel() / 8 < (int64_t(1) << 32), what, ": tensor too large");
+  DK_CHECK(kern::bn_supported(static_cast<int>(x.size(1))), what, ": unsupported channel count ", x.size(1));
+  DK_CHECK(x.numel() / 8 < (int64_t(1) << 32), what, ": tensor too large");
 }
 
 // [N, C] row-major is NHWC with H = W = 1: both layouts are "channels innermost".
@@ -61,19 +61,11 @@ std::mutex g_arena_mu;
 std::map<std::pair<int, hipStream_t>, ZeroArena> g_arenas;
 constexpr int64_t kArenaFloats = int64_t(4) << 20;  // 16 MiB
 
-bool arena_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("DCP_ZERO_ARENA");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
 at::Tensor zeroed_floats(int64_t n, const at::Tensor& like, hipStream_t st) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(st, &cap);
   const int64_t need = (n + 63) / 64 * 64;
-  if (cap != hipStreamCaptureStatusNone || need > kArenaFloats / 4 || !arena_enabled()) {
+  if (cap != hipStreamCaptureStatusNone || need > kArenaFloats / 4) {
     // a fill KERNEL, not hipMemsetAsync: a captured memset node is not ordered
     // before the next kernel node on replays after the first on this ROCm
     // (tools/graph_op_check.py: the GEMM's atomics land on un-zeroed sums)
@@ -83,10 +75,10 @@ at::Tensor zeroed_floats(int64_t n, const at::Tensor& like, hipStream_t st) {
   ZeroArena& a = g_arenas[{static_cast<int>(like.get_device()), st}];
   if (!a.buf.defined()) {
     a.buf = at::empty({kArenaFloats}, like.options().dtype(at::kFloat));
-    DCP_CHECK(hipMemsetAsync(a.buf.data_ptr(), 0, sizeof(float) * kArenaFloats, st) == hipSuccess, "memset failed");
+    DK_CHECK(hipMemsetAsync(a.buf.data_ptr(), 0, sizeof(float) * kArenaFloats, st) == hipSuccess, "memset failed");
   }
   if (a.used + need > kArenaFloats) {
-    DCP_CHECK(hipMemsetAsync(a.buf.data_ptr(), 0, sizeof(float) * kArenaFloats, st) == hipSuccess, "memset failed");
+    DK_CHECK(hipMemsetAsync(a.buf.data_ptr(), 0, sizeof(float) * kArenaFloats, st) == hipSuccess, "memset failed");
     a.used = 0;
   }
   at::Tensor t = a.buf.narrow(0, a.used, n);
@@ -115,7 +107,7 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
   at::Tensor res;
   if (residual.has_value() && residual->defined()) {
     res = residual->contiguous(cl_fmt(x));
-    DCP_CHECK(res.sizes() == x.sizes() && res.scalar_type() == x.scalar_type(), "bn_act_fwd: residual mismatch");
+    DK_CHECK(res.sizes() == x.sizes() && res.scalar_type() == x.scalar_type(), "bn_act_fwd: residual mismatch");
   }
   at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor b = bias.has_value() && bias->defined() ? bias->to(at::kFloat).contiguous() : at::Tensor();
@@ -128,7 +120,7 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
     // stats: (Σx, Σx²) accumulated by the producing GEMM's epilogue (conv1x1_fwd)
     const bool ready = stats.has_value() && stats->defined();
     if (ready)
-      DCP_CHECK(stats->scalar_type() == at::kFloat && stats->numel() == 2 * C && stats->is_contiguous(),
+      DK_CHECK(stats->scalar_type() == at::kFloat && stats->numel() == 2 * C && stats->is_contiguous(),
                 "bn_act_fwd: stats must be fp32 [2*C]");
     at::Tensor acc = ready ? *stats : zeroed_floats(2 * C, x, s);
     float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
@@ -143,7 +135,7 @@ std::vector<at::Tensor> bn_act_fwd(const at::Tensor& x, const c10::optional<at::
                                : nullptr,
                            mbits.defined() ? mbits.data_ptr<uint8_t>() : nullptr, ready, s);
   } else {
-    DCP_CHECK(running_mean.has_value() && running_var.has_value(), "bn_act_fwd: eval mode needs running stats");
+    DK_CHECK(running_mean.has_value() && running_var.has_value(), "bn_act_fwd: eval mode needs running stats");
     mean.copy_(*running_mean);
     invstd.copy_(at::rsqrt(*running_var + eps));
     at::Tensor g = w.defined() ? w : at::ones({C}, fopt);
@@ -174,7 +166,7 @@ std::vector<at::Tensor> bn_stats_coef(const at::Tensor& x, const c10::optional<a
   auto s = stream_of(x);
   const bool ready = sums.has_value() && sums->defined();
   if (ready)
-    DCP_CHECK(sums->is_cuda() && sums->scalar_type() == at::kFloat && sums->is_contiguous() && sums->numel() == 2 * C,
+    DK_CHECK(sums->is_cuda() && sums->scalar_type() == at::kFloat && sums->is_contiguous() && sums->numel() == 2 * C,
               "bn_stats_coef: sums must be fp32 [2*C]");
   at::Tensor acc = ready ? *sums : zeroed_floats(2 * C, x, s);
   at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
@@ -196,13 +188,13 @@ std::vector<at::Tensor> bn_stats_coef(const at::Tensor& x, const c10::optional<a
 // ------------------------------------------------- 1x1 conv as MFMA GEMM ---
 namespace {
 void check_gemm_act(const at::Tensor& x, const char* what) {
-  DCP_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, what, ": bf16 device tensor required");
-  DCP_CHECK((x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)) || (x.dim() == 2 && x.is_contiguous()),
+  DK_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, what, ": bf16 device tensor required");
+  DK_CHECK((x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)) || (x.dim() == 2 && x.is_contiguous()),
             what, ": expected a channels_last 4-D or contiguous [M, C] tensor");
 }
 const float* vec_or_null(const c10::optional<at::Tensor>& t, int64_t n, const char* what) {
   if (!t.has_value() || !t->defined()) return nullptr;
-  DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == n && t->is_contiguous(), what,
+  DK_CHECK(t->scalar_type() == at::kFloat && t->numel() == n && t->is_contiguous(), what,
             ": scale/shift must be contiguous fp32 [C]");
   return t->data_ptr<float>();
 }
@@ -218,12 +210,12 @@ std::vector<at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, co
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t K = x.size(1);
   const int64_t M = x.numel() / K;
-  DCP_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() % K == 0, "conv1x1_fwd: weight");
+  DK_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() % K == 0, "conv1x1_fwd: weight");
   const int64_t N = w.numel() / K;
-  DCP_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_fwd: unsupported shape");
+  DK_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_fwd: unsupported shape");
   const float* sc = vec_or_null(scale, K, "conv1x1_fwd");
   const float* sf = vec_or_null(shift, K, "conv1x1_fwd");
-  DCP_CHECK((sc == nullptr) == (sf == nullptr), "conv1x1_fwd: scale and shift go together");
+  DK_CHECK((sc == nullptr) == (sf == nullptr), "conv1x1_fwd: scale and shift go together");
   at::Tensor y = x.dim() == 4 ? at::empty({x.size(0), N, x.size(2), x.size(3)},
                                           x.options().memory_format(at::MemoryFormat::ChannelsLast))
                               : at::empty({M, N}, x.options());
@@ -236,7 +228,7 @@ std::vector<at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, co
 
 // (w_bf16 [R, C], w_bf16^T [C, R]) from an fp32 (or bf16) weight viewed as [R, C]
 std::vector<at::Tensor> weight_bf16_t(const at::Tensor& w) {
-  DCP_CHECK(w.is_cuda() && w.dim() >= 2, "weight_bf16_t: device weight required");
+  DK_CHECK(w.is_cuda() && w.dim() >= 2, "weight_bf16_t: device weight required");
   c10::hip::HIPGuard guard(w.device().index());
   const int64_t R = w.size(0);
   const int64_t Cc = w.numel() / R;
@@ -253,7 +245,7 @@ std::vector<at::Tensor> weight_bf16_t(const at::Tensor& w) {
 // [Cin][kh][kw][Cout] spatially flipped: the stride-1 data-gradient operand),
 // one launch.
 std::vector<at::Tensor> conv_weight_bf16(const at::Tensor& w) {
-  DCP_CHECK(w.is_cuda() && w.dim() == 4, "conv_weight_bf16: 4-D device weight required");
+  DK_CHECK(w.is_cuda() && w.dim() == 4, "conv_weight_bf16: 4-D device weight required");
   c10::hip::HIPGuard guard(w.device().index());
   const int64_t Co = w.size(0), Ci = w.size(1), kh = w.size(2), kw = w.size(3);
   at::Tensor wf = w.detach().permute({0, 2, 3, 1}).to(at::kFloat).contiguous();  // [Co][kh][kw][Ci]
@@ -271,13 +263,13 @@ std::vector<at::Tensor> conv_weight_bf16(const at::Tensor& w) {
 // are baked in: rebuild when a weight's storage changes.
 std::tuple<at::Tensor, int64_t, std::vector<at::Tensor>, std::vector<at::Tensor>> weight_prep_plan(
     const std::vector<at::Tensor>& ws) {
-  DCP_CHECK(!ws.empty(), "weight_prep_plan: no weights");
+  DK_CHECK(!ws.empty(), "weight_prep_plan: no weights");
   c10::hip::HIPGuard guard(ws[0].device().index());
   int64_t E = 0;
   for (auto& w : ws) {
-    DCP_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.device() == ws[0].device(),
+    DK_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.device() == ws[0].device(),
               "weight_prep_plan: fp32 4-D device conv weights on one device required");
-    DCP_CHECK(w.permute({0, 2, 3, 1}).is_contiguous(),
+    DK_CHECK(w.permute({0, 2, 3, 1}).is_contiguous(),
               "weight_prep_plan: weights must be channels_last ([Cout][kh][kw][Cin] memory)");
     E += w.numel();
   }
@@ -324,9 +316,9 @@ at::Tensor conv1x1_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t K = gy.size(1);
   const int64_t M = gy.numel() / K;
-  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % K == 0, "conv1x1_dgrad: weight");
+  DK_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % K == 0, "conv1x1_dgrad: weight");
   const int64_t N = wt.numel() / K;
-  DCP_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_dgrad: unsupported shape");
+  DK_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_dgrad: unsupported shape");
   at::Tensor dx = gy.dim() == 4 ? at::empty({gy.size(0), N, gy.size(2), gy.size(3)},
                                             gy.options().memory_format(at::MemoryFormat::ChannelsLast))
                                 : at::empty({M, N}, gy.options());
@@ -344,15 +336,15 @@ at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::o
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t N1 = gy.size(1), N2 = x.size(1);
   const int64_t M = gy.numel() / N1;
-  DCP_CHECK(x.numel() / N2 == M, "conv1x1_wgrad: row mismatch");
-  DCP_CHECK(N1 % 64 == 0 && N2 % 64 == 0, "conv1x1_wgrad: channels must be multiples of 64");
+  DK_CHECK(x.numel() / N2 == M, "conv1x1_wgrad: row mismatch");
+  DK_CHECK(N1 % 64 == 0 && N2 % 64 == 0, "conv1x1_wgrad: channels must be multiples of 64");
   const float* sc = vec_or_null(scale, N2, "conv1x1_wgrad");
   const float* sf = vec_or_null(shift, N2, "conv1x1_wgrad");
   // accumulate_into: an existing fp32 [N1, N2] gradient that receives += dW in
   // the final slab-reduction pass (gradient-accumulation micro-steps)
   const bool acc = accumulate_into.has_value() && accumulate_into->defined();
   if (acc)
-    DCP_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
+    DK_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
                   accumulate_into->numel() == N1 * N2 && accumulate_into->device() == gy.device(),
               "conv1x1_wgrad: accumulate_into must be a contiguous fp32 [N1, N2] tensor on the same device");
   at::Tensor dw = acc ? *accumulate_into : at::empty({N1, N2}, gy.options().dtype(at::kFloat));
@@ -378,14 +370,14 @@ const at::Tensor& zero_row(const at::Tensor& like) {
 at::Tensor conv_wgrad(const at::Tensor& gy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride, int64_t pad) {
   check_gemm_act(gy, "conv_wgrad");
   check_gemm_act(x, "conv_wgrad");
-  DCP_CHECK(gy.dim() == 4 && x.dim() == 4 && gy.size(0) == x.size(0), "conv_wgrad: NHWC 4-D tensors required");
+  DK_CHECK(gy.dim() == 4 && x.dim() == 4 && gy.size(0) == x.size(0), "conv_wgrad: NHWC 4-D tensors required");
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Cout = gy.size(1), Ho = gy.size(2), Wo = gy.size(3);
-  DCP_CHECK(Ho == (H + 2 * pad - kh) / stride + 1 && Wo == (W + 2 * pad - kw) / stride + 1,
+  DK_CHECK(Ho == (H + 2 * pad - kh) / stride + 1 && Wo == (W + 2 * pad - kw) / stride + 1,
             "conv_wgrad: output size does not match the geometry");
-  DCP_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "conv_wgrad: channels must be multiples of 64");
-  DCP_CHECK(N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad: tensor too large");
+  DK_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "conv_wgrad: channels must be multiples of 64");
+  DK_CHECK(N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad: tensor too large");
   at::Tensor dw = at::empty({Cout, kh, kw, Cin}, gy.options().dtype(at::kFloat));
   const int taps = static_cast<int>(kh * kw);
   at::Tensor ws = at::empty({kern::gemm_wgrad_workspace(N * Ho * Wo, static_cast<int>(Cout), static_cast<int>(Cin), taps)},
@@ -403,17 +395,17 @@ at::Tensor conv_wgrad(const at::Tensor& gy, const at::Tensor& x, int64_t kh, int
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& wt, int64_t kh, int64_t kw, int64_t stride,
                                  int64_t pad, bool stats) {
   check_gemm_act(x, "conv_fwd");
-  DCP_CHECK(x.dim() == 4, "conv_fwd: NHWC 4-D input required");
+  DK_CHECK(x.dim() == 4, "conv_fwd: NHWC 4-D input required");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
-  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % (kh * kw * Cin) == 0,
+  DK_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % (kh * kw * Cin) == 0,
             "conv_fwd: weight must be contiguous bf16 [Cout][kh][kw][Cin]");
   const int64_t Cout = wt.numel() / (kh * kw * Cin);
-  DCP_CHECK(kern::conv_fwd_supported(static_cast<int>(Cin), static_cast<int>(Cout), static_cast<int>(kh),
+  DK_CHECK(kern::conv_fwd_supported(static_cast<int>(Cin), static_cast<int>(Cout), static_cast<int>(kh),
                                      static_cast<int>(kw)),
             "conv_fwd: channels must be multiples of 64 and the kernel at most 8x8");
   const int64_t Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
-  DCP_CHECK(Ho > 0 && Wo > 0 && N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31),
+  DK_CHECK(Ho > 0 && Wo > 0 && N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31),
             "conv_fwd: bad geometry or tensor too large");
   at::Tensor y = at::empty({N, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto s = stream_of(x);
@@ -434,8 +426,8 @@ struct BnRedIn {
 BnRedIn bnred_in(const at::Tensor& x, const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
                  const at::Tensor& mean, const at::Tensor& invstd, int64_t C, const char* what) {
   check_gemm_act(x, what);
-  DCP_CHECK(x.dim() == 4 && x.size(1) == C, what, ": x must be the [N, C, H, W] BN input of the gradient");
-  DCP_CHECK(mean.numel() == C && invstd.numel() == C && mean.scalar_type() == at::kFloat, what, ": BN statistics");
+  DK_CHECK(x.dim() == 4 && x.size(1) == C, what, ": x must be the [N, C, H, W] BN input of the gradient");
+  DK_CHECK(mean.numel() == C && invstd.numel() == C && mean.scalar_type() == at::kFloat, what, ": BN statistics");
   BnRedIn r;
   if (gamma.has_value() && gamma->defined()) r.w = gamma->to(at::kFloat).contiguous();
   if (beta.has_value() && beta->defined()) r.b = beta->to(at::kFloat).contiguous();
@@ -456,12 +448,12 @@ std::vector<at::Tensor> conv1x1_dgrad_bnred(const at::Tensor& gy, const at::Tens
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t K = gy.size(1);
   const int64_t M = gy.numel() / K;
-  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % K == 0,
+  DK_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % K == 0,
             "conv1x1_dgrad_bnred: weight");
   const int64_t N = wt.numel() / K;
-  DCP_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_dgrad_bnred: unsupported shape");
+  DK_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_dgrad_bnred: unsupported shape");
   const BnRedIn r = bnred_in(x, gamma, beta, mean, invstd, N, "conv1x1_dgrad_bnred");
-  DCP_CHECK(x.numel() == M * N, "conv1x1_dgrad_bnred: x / gy pixel count mismatch");
+  DK_CHECK(x.numel() == M * N, "conv1x1_dgrad_bnred: x / gy pixel count mismatch");
   at::Tensor dy = at::empty({gy.size(0), N, gy.size(2), gy.size(3)},
                             gy.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto s = stream_of(gy);
@@ -488,25 +480,25 @@ std::vector<at::Tensor> conv1x1_dgrad_resred(const at::Tensor& gy, const at::Ten
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t K = gy.size(1);
   const int64_t M = gy.numel() / K;
-  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % K == 0,
+  DK_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % K == 0,
             "conv1x1_dgrad_resred: weight");
   const int64_t N = wt.numel() / K;
-  DCP_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_dgrad_resred: unsupported shape");
-  DCP_CHECK(x.dim() == gy.dim() && x.size(1) == N && x.numel() == M * N, "conv1x1_dgrad_resred: x shape");
-  DCP_CHECK(mean.scalar_type() == at::kFloat && mean.numel() == N && mean.is_contiguous(),
+  DK_CHECK(kern::gemm_nt_supported(M, N, K), "conv1x1_dgrad_resred: unsupported shape");
+  DK_CHECK(x.dim() == gy.dim() && x.size(1) == N && x.numel() == M * N, "conv1x1_dgrad_resred: x shape");
+  DK_CHECK(mean.scalar_type() == at::kFloat && mean.numel() == N && mean.is_contiguous(),
             "conv1x1_dgrad_resred: mean must be fp32 [N]");
-  DCP_CHECK(bits.scalar_type() == at::kByte && bits.numel() == M * N / 8 && bits.is_contiguous(),
+  DK_CHECK(bits.scalar_type() == at::kByte && bits.numel() == M * N / 8 && bits.is_contiguous(),
             "conv1x1_dgrad_resred: relu bits mismatch");
   at::Tensor g2;
   if (gy2.has_value() && gy2->defined()) {
     g2 = gy2->to(at::kBFloat16).contiguous(x.dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous);
-    DCP_CHECK(g2.sizes() == x.sizes(), "conv1x1_dgrad_resred: gy2 shape");
+    DK_CHECK(g2.sizes() == x.sizes(), "conv1x1_dgrad_resred: gy2 shape");
   }
   const bool has_x2 = x2.has_value() && x2->defined();
   if (has_x2) {
     check_gemm_act(*x2, "conv1x1_dgrad_resred(x2)");
-    DCP_CHECK(x2->sizes() == x.sizes(), "conv1x1_dgrad_resred: x2 shape");
-    DCP_CHECK(mean2.has_value() && mean2->defined() && mean2->scalar_type() == at::kFloat && mean2->numel() == N,
+    DK_CHECK(x2->sizes() == x.sizes(), "conv1x1_dgrad_resred: x2 shape");
+    DK_CHECK(mean2.has_value() && mean2->defined() && mean2->scalar_type() == at::kFloat && mean2->numel() == N,
               "conv1x1_dgrad_resred: mean2 must be fp32 [N]");
   }
   at::Tensor g = at::empty_like(x, x.dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous);
@@ -528,11 +520,11 @@ std::vector<at::Tensor> bn_bwd_apply_g(const at::Tensor& g, const at::Tensor& x,
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
-  DCP_CHECK(g.sizes() == x.sizes() && g.scalar_type() == x.scalar_type() && g.is_contiguous(cl_fmt(x)),
+  DK_CHECK(g.sizes() == x.sizes() && g.scalar_type() == x.scalar_type() && g.is_contiguous(cl_fmt(x)),
             "bn_bwd_apply_g: g must match x");
-  DCP_CHECK(acc.scalar_type() == at::kFloat && acc.numel() == 2 * C && acc.is_contiguous(),
+  DK_CHECK(acc.scalar_type() == at::kFloat && acc.numel() == 2 * C && acc.is_contiguous(),
             "bn_bwd_apply_g: acc must be fp32 [2*C]");
-  DCP_CHECK(weight.scalar_type() == at::kFloat && weight.numel() == C && weight.is_contiguous(),
+  DK_CHECK(weight.scalar_type() == at::kFloat && weight.numel() == C && weight.is_contiguous(),
             "bn_bwd_apply_g: weight must be fp32 [C]");
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor dx = at::empty_like(x, cl_fmt(x));
@@ -557,14 +549,14 @@ std::vector<at::Tensor> bn_bwd_apply2_g(const at::Tensor& g, const at::Tensor& x
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
-  DCP_CHECK(g.sizes() == x.sizes() && g.scalar_type() == x.scalar_type() && g.is_contiguous(cl_fmt(x)) &&
+  DK_CHECK(g.sizes() == x.sizes() && g.scalar_type() == x.scalar_type() && g.is_contiguous(cl_fmt(x)) &&
                 x2.sizes() == x.sizes() && x2.scalar_type() == x.scalar_type(),
             "bn_bwd_apply2_g: g / x2 must match x");
   for (const at::Tensor* t : {&acc, &acc2})
-    DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == 2 * C && t->is_contiguous(),
+    DK_CHECK(t->scalar_type() == at::kFloat && t->numel() == 2 * C && t->is_contiguous(),
               "bn_bwd_apply2_g: acc must be fp32 [2*C]");
   for (const at::Tensor* t : {&weight, &weight2, &mean, &mean2, &invstd, &invstd2})
-    DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(),
+    DK_CHECK(t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(),
               "bn_bwd_apply2_g: per-channel tensors must be fp32 [C]");
   if (C > 2048) {
     auto a = bn_bwd_apply_g(g, x, weight, mean, invstd, acc);
@@ -592,19 +584,19 @@ std::vector<at::Tensor> conv_dgrad_bnred(const at::Tensor& gy, const at::Tensor&
                                          const c10::optional<at::Tensor>& beta, const at::Tensor& mean,
                                          const at::Tensor& invstd) {
   check_gemm_act(gy, "conv_dgrad_bnred");
-  DCP_CHECK(gy.dim() == 4, "conv_dgrad_bnred: NHWC 4-D gradient required");
+  DK_CHECK(gy.dim() == 4, "conv_dgrad_bnred: NHWC 4-D gradient required");
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t N = gy.size(0), Co = gy.size(1), H = gy.size(2), W = gy.size(3);
-  DCP_CHECK(wd.scalar_type() == at::kBFloat16 && wd.is_contiguous() && wd.numel() % (kh * kw * Co) == 0,
+  DK_CHECK(wd.scalar_type() == at::kBFloat16 && wd.is_contiguous() && wd.numel() % (kh * kw * Co) == 0,
             "conv_dgrad_bnred: weight must be contiguous bf16 [Cin][kh][kw][Cout]");
   const int64_t Ci = wd.numel() / (kh * kw * Co);
-  DCP_CHECK(kern::conv_fwd_supported(static_cast<int>(Co), static_cast<int>(Ci), static_cast<int>(kh),
+  DK_CHECK(kern::conv_fwd_supported(static_cast<int>(Co), static_cast<int>(Ci), static_cast<int>(kh),
                                      static_cast<int>(kw)),
             "conv_dgrad_bnred: channels must be multiples of 64");
   const int64_t Ho = H + 2 * pad - kh + 1, Wo = W + 2 * pad - kw + 1;
-  DCP_CHECK(x.dim() == 4 && x.size(0) == N && x.size(2) == Ho && x.size(3) == Wo,
+  DK_CHECK(x.dim() == 4 && x.size(0) == N && x.size(2) == Ho && x.size(3) == Wo,
             "conv_dgrad_bnred: x does not match the data-gradient geometry");
-  DCP_CHECK(N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31), "conv_dgrad_bnred: too large");
+  DK_CHECK(N * H * W < (int64_t(1) << 31) && N * Ho * Wo < (int64_t(1) << 31), "conv_dgrad_bnred: too large");
   const BnRedIn r = bnred_in(x, gamma, beta, mean, invstd, Ci, "conv_dgrad_bnred");
   at::Tensor dy = at::empty({N, Ci, Ho, Wo}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto s = stream_of(gy);
@@ -623,13 +615,13 @@ std::vector<at::Tensor> conv_dgrad_bnred(const at::Tensor& gy, const at::Tensor&
 // GEMM on gy with a scattering epilogue; wt = Wᵀ bf16 [Cin][Cout].
 at::Tensor conv1x1_s2_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
   check_gemm_act(gy, "conv1x1_s2_dgrad");
-  DCP_CHECK(gy.dim() == 4, "conv1x1_s2_dgrad: NHWC 4-D gradient required");
+  DK_CHECK(gy.dim() == 4, "conv1x1_s2_dgrad: NHWC 4-D gradient required");
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t N = gy.size(0), Co = gy.size(1), Ho = gy.size(2), Wo = gy.size(3);
-  DCP_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % Co == 0,
+  DK_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() % Co == 0,
             "conv1x1_s2_dgrad: weight");
   const int64_t Ci = wt.numel() / Co;
-  DCP_CHECK(kern::gemm_nt_supported(N * Ho * Wo, Ci, Co) && N * 4 * Ho * Wo < (int64_t(1) << 31),
+  DK_CHECK(kern::gemm_nt_supported(N * Ho * Wo, Ci, Co) && N * 4 * Ho * Wo < (int64_t(1) << 31),
             "conv1x1_s2_dgrad: unsupported shape");
   at::Tensor dx = at::empty({N, Ci, 2 * Ho, 2 * Wo}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
   kern::conv1x1_s2_dgrad_bf16(gy.data_ptr(), wt.data_ptr(), dx.data_ptr(), static_cast<int>(N), static_cast<int>(Ho),
@@ -645,14 +637,14 @@ at::Tensor conv1x1_s2_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
 // bf16 [Cin][9][Cout] with its taps in class order 4 | 3 5 | 1 7 | 0 2 6 8.
 at::Tensor conv_dgrad_s2_multi(const at::Tensor& gy, const at::Tensor& wperm, int64_t H, int64_t W) {
   check_gemm_act(gy, "conv_dgrad_s2_multi");
-  DCP_CHECK(gy.dim() == 4, "conv_dgrad_s2_multi: NHWC 4-D gradient required");
+  DK_CHECK(gy.dim() == 4, "conv_dgrad_s2_multi: NHWC 4-D gradient required");
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t N = gy.size(0), Co = gy.size(1), Hg = gy.size(2), Wg = gy.size(3);
-  DCP_CHECK(wperm.scalar_type() == at::kBFloat16 && wperm.is_contiguous() && wperm.dim() == 3 &&
+  DK_CHECK(wperm.scalar_type() == at::kBFloat16 && wperm.is_contiguous() && wperm.dim() == 3 &&
                 wperm.size(1) == 9 && wperm.size(2) == Co,
             "conv_dgrad_s2_multi: weight must be contiguous bf16 [Cin][9][Cout]");
   const int64_t Ci = wperm.size(0);
-  DCP_CHECK(Ci % 64 == 0 && Co % 64 == 0 && N * H * W < (int64_t(1) << 31) && (H + 1) / 2 == Hg &&
+  DK_CHECK(Ci % 64 == 0 && Co % 64 == 0 && N * H * W < (int64_t(1) << 31) && (H + 1) / 2 == Hg &&
                 (W + 1) / 2 == Wg,
             "conv_dgrad_s2_multi: unsupported shape");
   at::Tensor dx = at::empty({N, Ci, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -664,16 +656,16 @@ at::Tensor conv_dgrad_s2_multi(const at::Tensor& gy, const at::Tensor& wperm, in
 
 at::Tensor conv_dgrad_s2(const at::Tensor& gy, const std::vector<at::Tensor>& wsubs, int64_t H, int64_t W) {
   check_gemm_act(gy, "conv_dgrad_s2");
-  DCP_CHECK(gy.dim() == 4 && wsubs.size() == 4, "conv_dgrad_s2: NHWC gy and 4 weight subsets required");
+  DK_CHECK(gy.dim() == 4 && wsubs.size() == 4, "conv_dgrad_s2: NHWC gy and 4 weight subsets required");
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t N = gy.size(0), Co = gy.size(1), Hg = gy.size(2), Wg = gy.size(3);
   const int64_t Ci = wsubs[0].size(0);
-  DCP_CHECK(Ci % 64 == 0 && Co % 64 == 0 && N * H * W < (int64_t(1) << 31) && H <= 2 * Hg + 1 && W <= 2 * Wg + 1,
+  DK_CHECK(Ci % 64 == 0 && Co % 64 == 0 && N * H * W < (int64_t(1) << 31) && H <= 2 * Hg + 1 && W <= 2 * Wg + 1,
             "conv_dgrad_s2: unsupported shape");
   at::Tensor dx = at::empty({N, Ci, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
   for (int q = 0; q < 4; ++q) {
     const at::Tensor& w = wsubs[q];
-    DCP_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4 && w.size(0) == Ci &&
+    DK_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4 && w.size(0) == Ci &&
                   w.size(3) == Co,
               "conv_dgrad_s2: weight subset must be bf16 [Cin][nkh][nkw][Cout]");
     const int ph = q >> 1, pw = q & 1;
@@ -688,17 +680,17 @@ at::Tensor conv_dgrad_s2(const at::Tensor& gy, const std::vector<at::Tensor>& ws
 
 // fp32 [N] column sums of a bf16 [.., N] tensor (Linear bias gradient)
 at::Tensor colsum(const at::Tensor& x, const c10::optional<at::Tensor>& accumulate_into) {
-  DCP_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() >= 1,
+  DK_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() >= 1,
             "colsum: contiguous bf16 device tensor required");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t N = x.size(-1);
   const int64_t M = x.numel() / N;
-  DCP_CHECK(N % 8 == 0, "colsum: last dim must be a multiple of 8");
+  DK_CHECK(N % 8 == 0, "colsum: last dim must be a multiple of 8");
   auto s = stream_of(x);
   // accumulate_into: existing fp32 [N] gradient; the kernel's atomics add into it (no memset)
   const bool acc = accumulate_into.has_value() && accumulate_into->defined();
   if (acc)
-    DCP_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
+    DK_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
                   accumulate_into->numel() == N && accumulate_into->device() == x.device(),
               "colsum: accumulate_into must be a contiguous fp32 [N] tensor on the same device");
   at::Tensor out = acc ? *accumulate_into : at::empty({N}, x.options().dtype(at::kFloat));
@@ -710,9 +702,9 @@ at::Tensor colsum(const at::Tensor& x, const c10::optional<at::Tensor>& accumula
 // --------------------------------------------------------------- GELU ---
 namespace {
 void check_gelu_operand(const at::Tensor& t, const char* what) {
-  DCP_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.dim() >= 1, what,
+  DK_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.dim() >= 1, what,
             ": contiguous bf16 device tensor required");
-  DCP_CHECK(t.size(-1) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, what,
+  DK_CHECK(t.size(-1) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, what,
             ": last dim must be a multiple of 8 and the data 16-B aligned");
 }
 }  // namespace
@@ -731,18 +723,18 @@ std::vector<at::Tensor> gelu_bwd(const at::Tensor& gy, const at::Tensor& h, bool
                                  const c10::optional<at::Tensor>& accumulate_into) {
   check_gelu_operand(gy, "gelu_bwd");
   check_gelu_operand(h, "gelu_bwd");
-  DCP_CHECK(gy.sizes() == h.sizes() && gy.device() == h.device(), "gelu_bwd: gy and h must match");
+  DK_CHECK(gy.sizes() == h.sizes() && gy.device() == h.device(), "gelu_bwd: gy and h must match");
   c10::hip::HIPGuard guard(h.device().index());
   const int64_t N = h.size(-1);
   const int64_t M = N ? h.numel() / N : 0;
-  DCP_CHECK(N < (int64_t(1) << 30), "gelu_bwd: last dim too large");
+  DK_CHECK(N < (int64_t(1) << 30), "gelu_bwd: last dim too large");
   auto s = stream_of(h);
   at::Tensor gh = at::empty_like(h);
   at::Tensor db;
   if (bias_grad) {
     if (accumulate_into.has_value() && accumulate_into->defined()) {
       db = *accumulate_into;
-      DCP_CHECK(db.scalar_type() == at::kFloat && db.is_contiguous() && db.numel() == N && db.device() == h.device(),
+      DK_CHECK(db.scalar_type() == at::kFloat && db.is_contiguous() && db.numel() == N && db.device() == h.device(),
                 "gelu_bwd: accumulate_into must be a contiguous fp32 [N] tensor on the same device");
     } else {
       db = at::zeros({N}, h.options().dtype(at::kFloat));
@@ -757,9 +749,9 @@ std::vector<at::Tensor> gelu_bwd(const at::Tensor& gy, const at::Tensor& h, bool
 // ---------------------------------------------------- flash attention ---
 namespace {
 kern::AttnTensor attn_view(const at::Tensor& t, const char* what) {
-  DCP_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 3 && t.stride(2) == 1, what,
+  DK_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 3 && t.stride(2) == 1, what,
             ": bf16 [B, T, H*64] tensor with unit last stride required");
-  DCP_CHECK(t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+  DK_CHECK(t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
             what, ": rows must be 16-byte aligned");
   return kern::AttnTensor{t.data_ptr(), t.stride(0), t.stride(1)};
 }
@@ -769,10 +761,10 @@ kern::AttnOut attn_out(const at::Tensor& t, const char* what) {
 }
 kern::AttnParams attn_params(const at::Tensor& q, int64_t heads, bool causal, double p_drop, int64_t seed) {
   const int64_t B = q.size(0), T = q.size(1), C = q.size(2);
-  DCP_CHECK(heads > 0 && C == heads * 64, "attention: head dim must be 64");
-  DCP_CHECK(kern::attn_supported(static_cast<int>(T), 64), "attention: sequence length must be a multiple of 64");
-  DCP_CHECK(p_drop >= 0.0 && p_drop < 1.0, "attention: dropout p must be in [0, 1)");
-  DCP_CHECK(B * heads * T * (T / 2) < (int64_t(1) << 32), "attention: problem too large for the dropout counter");
+  DK_CHECK(heads > 0 && C == heads * 64, "attention: head dim must be 64");
+  DK_CHECK(kern::attn_supported(static_cast<int>(T), 64), "attention: sequence length must be a multiple of 64");
+  DK_CHECK(p_drop >= 0.0 && p_drop < 1.0, "attention: dropout p must be in [0, 1)");
+  DK_CHECK(B * heads * T * (T / 2) < (int64_t(1) << 32), "attention: problem too large for the dropout counter");
   kern::AttnParams p;
   p.B = static_cast<int>(B);
   p.H = static_cast<int>(heads);
@@ -784,7 +776,7 @@ kern::AttnParams attn_params(const at::Tensor& q, int64_t heads, bool causal, do
   return p;
 }
 void same_shape(const at::Tensor& a, const at::Tensor& b, const char* what) {
-  DCP_CHECK(a.sizes() == b.sizes(), what, ": shape mismatch");
+  DK_CHECK(a.sizes() == b.sizes(), what, ": shape mismatch");
 }
 }  // namespace
 
@@ -814,7 +806,7 @@ void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
     same_shape(q, *t, "flash_attn_bwd");
   c10::hip::HIPGuard guard(q.device().index());
   const kern::AttnParams p = attn_params(q, heads, causal, p_drop, seed);
-  DCP_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == q.size(0) * heads * q.size(1),
+  DK_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == q.size(0) * heads * q.size(1),
             "flash_attn_bwd: lse");
   at::Tensor delta = at::empty_like(lse);
   kern::attn_bwd(p, attn_view(q, "q"), attn_view(k, "k"), attn_view(v, "v"), attn_view(o, "o"),
@@ -846,12 +838,12 @@ std::vector<at::Tensor> bn_resbn_act_fwd(const at::Tensor& x, const at::Tensor& 
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
-  DCP_CHECK(x2.sizes() == x.sizes() && x2.scalar_type() == x.scalar_type(), "bn_resbn_act_fwd: x2 mismatch");
+  DK_CHECK(x2.sizes() == x.sizes() && x2.scalar_type() == x.scalar_type(), "bn_resbn_act_fwd: x2 mismatch");
   for (const at::Tensor* t : {&stats, &stats2})
-    DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == 2 * C && t->is_contiguous(),
+    DK_CHECK(t->scalar_type() == at::kFloat && t->numel() == 2 * C && t->is_contiguous(),
               "bn_resbn_act_fwd: stats must be fp32 [2*C]");
   for (const at::Tensor* t : {&weight, &bias, &weight2, &bias2})
-    DCP_CHECK(t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(),
+    DK_CHECK(t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(),
               "bn_resbn_act_fwd: affine parameters must be fp32 [C]");
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor y = at::empty_like(x, cl_fmt(x));
@@ -895,7 +887,7 @@ std::vector<at::Tensor> bn_resbn_act_bwd(const at::Tensor& gy, const c10::option
   }
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
-  DCP_CHECK(bits.numel() == M * C / 8, "bn_resbn_act_bwd: relu bits mismatch");
+  DK_CHECK(bits.numel() == M * C / 8, "bn_resbn_act_bwd: relu bits mismatch");
   auto fopt = x.options().dtype(at::kFloat);
   auto s = stream_of(x);
   at::Tensor gout = at::empty_like(x, cl_fmt(x));
@@ -974,9 +966,9 @@ std::vector<at::Tensor> bn_act_bwd_apply(const at::Tensor& gy, const at::Tensor&
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
-  DCP_CHECK(gy.sizes() == x.sizes() && gy.scalar_type() == x.scalar_type() && gy.is_contiguous(cl_fmt(x)),
+  DK_CHECK(gy.sizes() == x.sizes() && gy.scalar_type() == x.scalar_type() && gy.is_contiguous(cl_fmt(x)),
             "bn_act_bwd_apply: gy must match x");
-  DCP_CHECK(acc.scalar_type() == at::kFloat && acc.numel() == 2 * C && acc.is_contiguous(),
+  DK_CHECK(acc.scalar_type() == at::kFloat && acc.numel() == 2 * C && acc.is_contiguous(),
             "bn_act_bwd_apply: acc must be fp32 [2*C]");
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor dx = at::empty_like(x, cl_fmt(x));
@@ -1007,14 +999,14 @@ bool layer_norm_supported(int64_t D) { return kern::ln_supported(static_cast<int
 std::vector<at::Tensor> layer_norm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
                                        const c10::optional<at::Tensor>& bias, double eps,
                                        c10::optional<at::ScalarType> out_dtype) {
-  DCP_CHECK(x.is_cuda() && x.is_contiguous(), "layer_norm_fwd: contiguous device tensor required");
+  DK_CHECK(x.is_cuda() && x.is_contiguous(), "layer_norm_fwd: contiguous device tensor required");
   const int64_t D = x.size(-1);
-  DCP_CHECK(kern::ln_supported(static_cast<int>(D)), "layer_norm_fwd: D must be a multiple of 8 and <= 4096");
+  DK_CHECK(kern::ln_supported(static_cast<int>(D)), "layer_norm_fwd: D must be a multiple of 8 and <= 4096");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t rows = x.numel() / D;
   auto fopt = x.options().dtype(at::kFloat);
   at::Tensor y = at::empty_like(x, x.options().dtype(out_dtype.has_value() ? *out_dtype : x.scalar_type()));
-  DCP_CHECK(!(x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kFloat),
+  DK_CHECK(!(x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kFloat),
             "layer_norm_fwd: bf16 input with fp32 output is not supported");
   at::Tensor mean = at::empty({rows}, fopt), rstd = at::empty({rows}, fopt);
   at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
@@ -1043,11 +1035,11 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
   const bool accum = accumulate_into.has_value();
   at::Tensor dw, db;
   if (accum) {
-    DCP_CHECK(accumulate_into->size() == 2, "layer_norm_bwd: accumulate_into = (weight.grad, bias.grad)");
+    DK_CHECK(accumulate_into->size() == 2, "layer_norm_bwd: accumulate_into = (weight.grad, bias.grad)");
     dw = (*accumulate_into)[0];
     db = (*accumulate_into)[1];
     for (const auto& t : *accumulate_into)
-      DCP_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == D,
+      DK_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == D,
                 "layer_norm_bwd: accumulate_into tensors must be fp32 contiguous [D]");
   } else {
     dw = at::empty({D}, fopt);
@@ -1068,8 +1060,8 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
 // logits [rows, V] (row stride may exceed V), target [rows] int64.
 std::vector<at::Tensor> cross_entropy_fwd(const at::Tensor& logits, const at::Tensor& target, int64_t ignore_index,
                                           double label_smoothing) {
-  DCP_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "cross_entropy_fwd: [rows, V] row-major");
-  DCP_CHECK(target.scalar_type() == at::kLong, "cross_entropy_fwd: int64 targets");
+  DK_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "cross_entropy_fwd: [rows, V] row-major");
+  DK_CHECK(target.scalar_type() == at::kLong, "cross_entropy_fwd: int64 targets");
   c10::hip::HIPGuard guard(logits.device().index());
   const int64_t rows = logits.size(0);
   at::Tensor tg = target.contiguous();
@@ -1089,7 +1081,7 @@ at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& target,
   at::Tensor tg = target.contiguous();
   at::Tensor dl = dloss.to(at::kFloat).contiguous();
   const int stride = dl.numel() == 1 ? 0 : 1;
-  DCP_CHECK(stride == 0 || dl.numel() == rows, "cross_entropy_bwd: dloss must be [rows] or scalar");
+  DK_CHECK(stride == 0 || dl.numel() == rows, "cross_entropy_bwd: dloss must be [rows] or scalar");
   at::Tensor d = at::empty({rows, logits.size(1)}, logits.options());
   kern::xent_backward(ln_dtype(logits), logits.data_ptr(), logits.stride(0), tg.data_ptr<int64_t>(),
                       lse.data_ptr<float>(), dl.data_ptr<float>(), stride, rows, static_cast<int>(logits.size(1)),
@@ -1099,7 +1091,7 @@ at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& target,
 
 // ---------------------------------------------------------- log-softmax ---
 at::Tensor log_softmax_fwd(const at::Tensor& x, c10::optional<at::ScalarType> out_dtype) {
-  DCP_CHECK(x.is_cuda() && x.dim() >= 1, "log_softmax_fwd: device tensor required");
+  DK_CHECK(x.is_cuda() && x.dim() >= 1, "log_softmax_fwd: device tensor required");
   c10::hip::HIPGuard guard(x.device().index());
   at::Tensor xc = x.contiguous();
   const int64_t D = x.size(-1);
@@ -1132,13 +1124,13 @@ int dr_dtype(const at::Tensor& x) {
 at::Tensor dropout_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual, double p, int64_t seed,
                        int64_t offset, c10::optional<at::ScalarType> out_dtype,
                        const c10::optional<at::Tensor>& offset_dev) {
-  DCP_CHECK(x.is_cuda() && x.is_contiguous(), "dropout_fwd: contiguous device tensor required");
+  DK_CHECK(x.is_cuda() && x.is_contiguous(), "dropout_fwd: contiguous device tensor required");
   c10::hip::HIPGuard guard(x.device().index());
   at::Tensor res;
   at::ScalarType yt = out_dtype.has_value() ? *out_dtype : x.scalar_type();
   if (residual.has_value() && residual->defined()) {
     res = residual->contiguous();
-    DCP_CHECK(res.sizes() == x.sizes(), "dropout_fwd: residual shape mismatch");
+    DK_CHECK(res.sizes() == x.sizes(), "dropout_fwd: residual shape mismatch");
     yt = res.scalar_type();
   }
   at::Tensor y = at::empty_like(x, x.options().dtype(yt));
@@ -1151,7 +1143,7 @@ at::Tensor dropout_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& res
 
 at::Tensor feature_dropout_fwd(const at::Tensor& x, double p, int64_t seed, int64_t offset,
                                const c10::optional<at::Tensor>& offset_dev) {
-  DCP_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() >= 2, "feature_dropout: contiguous [N, C, ...] tensor");
+  DK_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() >= 2, "feature_dropout: contiguous [N, C, ...] tensor");
   c10::hip::HIPGuard guard(x.device().index());
   const int64_t rows = x.size(0) * x.size(1);
   at::Tensor y = at::empty_like(x);
@@ -1189,7 +1181,7 @@ kern::PoolEpi pool_epi(bool relu, double drop_p, int64_t seed, const c10::option
   kern::PoolEpi e;
   e.relu = relu ? 1 : 0;
   if (drop_p > 0.0) {
-    DCP_CHECK(drop_p < 1.0, "fused pool: dropout p must be < 1");
+    DK_CHECK(drop_p < 1.0, "fused pool: dropout p must be < 1");
     e.thr = kern::dropout_threshold(static_cast<float>(drop_p));
     e.scale = static_cast<float>(1.0 / (1.0 - drop_p));
     e.seed = static_cast<uint64_t>(seed);
@@ -1202,7 +1194,7 @@ kern::PoolEpi pool_epi(bool relu, double drop_p, int64_t seed, const c10::option
 // y = Dropout2d_p(relu(maxpool(x))) (see pool.hip).
 std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p, bool relu, double drop_p,
                                       int64_t seed, const c10::optional<at::Tensor>& offset_dev) {
-  DCP_CHECK(maxpool_supported(x, k, p), "maxpool2d_fwd: needs channels_last bf16/fp32, C % 8 == 0");
+  DK_CHECK(maxpool_supported(x, k, p), "maxpool2d_fwd: needs channels_last bf16/fp32, C % 8 == 0");
   c10::hip::HIPGuard guard(x.device().index());
   auto g = pool_geom(x, k, s, p);
   at::Tensor y = at::empty({g.N, g.C, g.OH, g.OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -1217,16 +1209,16 @@ std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s,
 at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& idx, at::IntArrayRef in_shape, int64_t k, int64_t s,
                          int64_t p, double drop_p, int64_t seed, const c10::optional<at::Tensor>& offset_dev,
                          const c10::optional<at::Tensor>& gy2) {
-  DCP_CHECK(in_shape.size() == 4, "maxpool2d_bwd: 4-D input shape expected");
+  DK_CHECK(in_shape.size() == 4, "maxpool2d_bwd: 4-D input shape expected");
   c10::hip::HIPGuard guard(gy.device().index());
   at::Tensor gx = at::empty(in_shape, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto g = pool_geom(gx, k, s, p);
   at::Tensor go = gy.contiguous(at::MemoryFormat::ChannelsLast);
-  DCP_CHECK(go.size(2) == g.OH && go.size(3) == g.OW && idx.numel() == go.numel(), "maxpool2d_bwd: shape mismatch");
+  DK_CHECK(go.size(2) == g.OH && go.size(3) == g.OW && idx.numel() == go.numel(), "maxpool2d_bwd: shape mismatch");
   at::Tensor g2;
   if (gy2.has_value() && gy2->defined()) {
     g2 = gy2->to(gy.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
-    DCP_CHECK(g2.sizes() == go.sizes(), "maxpool2d_bwd: gy2 shape mismatch");
+    DK_CHECK(g2.sizes() == go.sizes(), "maxpool2d_bwd: gy2 shape mismatch");
   }
   kern::maxpool2d_backward(gy.scalar_type() == at::kBFloat16 ? kern::POOL_BF16 : kern::POOL_F32, go.data_ptr(),
                            g2.defined() ? g2.data_ptr() : nullptr,
@@ -1239,8 +1231,8 @@ at::Tensor maxpool2d_bwd(const at::Tensor& gy, const at::Tensor& idx, at::IntArr
 // acc: fp64 [3] on the scores' device: [Σ loss, #correct, #count] += batch.
 void eval_metrics_(at::Tensor& acc, const at::Tensor& scores, const at::Tensor& target, bool log_probs,
                    int64_t ignore_index) {
-  DCP_CHECK(acc.scalar_type() == at::kDouble && acc.numel() == 3, "eval_metrics_: acc must be fp64 [3]");
-  DCP_CHECK(scores.dim() == 2 && target.dim() == 1 && target.size(0) == scores.size(0), "eval_metrics_: shapes");
+  DK_CHECK(acc.scalar_type() == at::kDouble && acc.numel() == 3, "eval_metrics_: acc must be fp64 [3]");
+  DK_CHECK(scores.dim() == 2 && target.dim() == 1 && target.size(0) == scores.size(0), "eval_metrics_: shapes");
   if (!scores.is_cuda()) {
     auto s = scores.to(at::kFloat);
     auto valid = target.ne(ignore_index);

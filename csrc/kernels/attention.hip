@@ -539,12 +539,12 @@ void attn_fwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, Att
               hipStream_t s) {
   const dim3 grid(p.B * p.H, (p.T + 127) / 128);
   const bool drop = p.p_drop > 0.f;
-#define DCP_AF(C, D) hipLaunchKernelGGL((attn_fwd_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, o, lse)
-  if (p.causal && drop) DCP_AF(true, true);
-  else if (p.causal) DCP_AF(true, false);
-  else if (drop) DCP_AF(false, true);
-  else DCP_AF(false, false);
-#undef DCP_AF
+#define DK_AF(C, D) hipLaunchKernelGGL((attn_fwd_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, o, lse)
+  if (p.causal && drop) DK_AF(true, true);
+  else if (p.causal) DK_AF(true, false);
+  else if (drop) DK_AF(false, true);
+  else DK_AF(false, false);
+#undef DK_AF
 }
 
 void attn_bwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, AttnTensor o, AttnTensor dout,
@@ -554,16 +554,16 @@ void attn_bwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, Att
                      delta);
   const dim3 grid(p.B * p.H, (p.T + 127) / 128);
   const bool drop = p.p_drop > 0.f;
-#define DCP_AB(C, D)                                                                                          \
+#define DK_AB(C, D)                                                                                          \
   do {                                                                                                        \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, dout, lse, delta, dk, dv); \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, dout, lse, delta, dq);   \
   } while (0)
-  if (p.causal && drop) DCP_AB(true, true);
-  else if (p.causal) DCP_AB(true, false);
-  else if (drop) DCP_AB(false, true);
-  else DCP_AB(false, false);
-#undef DCP_AB
+  if (p.causal && drop) DK_AB(true, true);
+  else if (p.causal) DK_AB(true, false);
+  else if (drop) DK_AB(false, true);
+  else DK_AB(false, false);
+#undef DK_AB
 }
 
 }  // namespace kern

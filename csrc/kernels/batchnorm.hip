@@ -53,20 +53,16 @@ struct V8;
 // Streaming (non-temporal) 16-B loads / stores for the bf16 activations: the
 // BN passes stream tensors of 100-800 MB that no cache holds between passes,
 // and the nt hints measured +15-20 % on 2-in / 1-out streams on this MI355X
-// (tools/bw_probe.hip: 4.7 -> 5.5 TB/s at the same grid). g_bn_nt (host:
-// DCP_BN_NT=0) turns them off for A/B.
+// (tools/bw_probe.hip: 4.7 -> 5.5 TB/s at the same grid).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ int g_bn_nt = 1;
 
 __device__ __forceinline__ uint4 ld16(const void* p) {
-  const u32x4* q = static_cast<const u32x4*>(p);
-  const u32x4 v = g_bn_nt ? __builtin_nontemporal_load(q) : *q;
+  const u32x4 v = __builtin_nontemporal_load(static_cast<const u32x4*>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st16(void* p, uint4 v) {
   const u32x4 w = {v.x, v.y, v.z, v.w};
-  if (g_bn_nt) __builtin_nontemporal_store(w, static_cast<u32x4*>(p));
-  else *static_cast<u32x4*>(p) = w;
+  __builtin_nontemporal_store(w, static_cast<u32x4*>(p));
 }
 
 template <>
@@ -642,22 +638,15 @@ __global__ void __launch_bounds__(kT) bn_bwd_apply2_kernel(const void* __restric
 }
 
 // grid for the reduction kernels: ≤ 2048 workgroups over (row slabs × channel
-// chunks), ≥ kU row iterations per thread, ≤ ~256K column atomics per launch.
-// tunables (env, read once): total workgroups and column atomics per launch
-inline int64_t env_or(const char* name, int64_t dflt) {
-  const char* v = getenv(name);
-  return v ? atoll(v) : dflt;
-}
+// chunks), ≥ kU row iterations per thread, ≤ 128K column atomics per launch.
 inline void red_geometry(int64_t M, int C, int* nblk, int64_t* rows_per_blk, int* nchunks, bool bwd = false) {
-  static const int64_t kBlkCap = env_or("DCP_BN_RED_BLOCKS", 2048);
-  static const int64_t kAtomicCap = env_or("DCP_BN_RED_ATOMICS", int64_t(128) << 10);
+  constexpr int64_t kBlkCap = 2048;
+  constexpr int64_t kAtomicCap = int64_t(128) << 10;
   // row slabs = fp32 atomic adds landing on each accumulator address: same-
   // address atomics serialise, so this caps the contention (measured on the
-  // ResNet-50 shapes, tools/bn_sweep.py)
-  // ResNet-50 b256 sweep: statistics best at 256 slabs, the 2-3 operand
-  // backward reduce at 512 on the large (≥ 2^19-row) shapes
-  static const int64_t kRowCapEnv = env_or("DCP_BN_RED_ROWBLK", 0);
-  const int64_t kRowCap = kRowCapEnv > 0 ? kRowCapEnv : (bwd && M >= (int64_t(1) << 19) ? 512 : 256);
+  // ResNet-50 shapes, tools/bn_sweep.py): statistics best at 256 slabs, the
+  // 2-3 operand backward reduce at 512 on the large (≥ 2^19-row) shapes
+  const int64_t kRowCap = bwd && M >= (int64_t(1) << 19) ? 512 : 256;
   const int cv = C / kV;
   const int tpr = cv < kMaxTpr ? cv : kMaxTpr;
   const int rpi = kT / tpr;
@@ -681,10 +670,8 @@ inline void red_geometry(int64_t M, int C, int* nblk, int64_t* rows_per_blk, int
 inline int apply_grid(int64_t nvec, int cv) {
   // ≤ 1024 workgroups (4 per CU): more streamed faster in isolation
   // (tools/bw_probe.hip) but measured -1.4 % in the ResNet-50 step (more
-  // coefficient prologues, the trailing-edge partial waves); DCP_BN_APPLY_BLOCKS
-  // overrides the cap
-  static const int64_t cap_env = env_or("DCP_BN_APPLY_BLOCKS", 0);
-  int64_t cap = cap_env > 0 ? cap_env : 1024;
+  // coefficient prologues, the trailing-edge partial waves)
+  constexpr int64_t cap = 1024;
   int64_t g = (nvec + kT * 2 - 1) / (kT * 2);
   if (g > cap) g = cap;
   if (g < 1) g = 1;
@@ -703,20 +690,6 @@ inline size_t red_smem(int C) {
 
 }  // namespace
 
-namespace {
-// copy DCP_BN_NT into the device flag once per process (before the first BN launch)
-void bn_init_flags() {
-  static const bool done = [] {
-    const char* v = getenv("DCP_BN_NT");
-    if (v && v[0] == '0') {  // the device default is 1: no copy (and nothing to capture) otherwise
-      const int nt = 0;
-      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bn_nt), &nt, sizeof(int));
-    }
-    return true;
-  }();
-  (void)done;
-}
-}  // namespace
 
 bool bn_supported(int C) {
   // reductions: C/8 ≤ 32 must divide 256, else be a multiple of 32; apply: C/8 must divide 256 or be a multiple
@@ -731,8 +704,7 @@ void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_
                       const float* beta, float* running_mean, float* running_var, float momentum, float eps,
                       float* mean, float* invstd, float* acc, bool act, int64_t* nbt, uint8_t* mbits,
                       bool acc_ready, hipStream_t s) {
-  bn_init_flags();
-  int nblk, nchunks;
+    int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
   const size_t sm = red_smem(C);
@@ -747,55 +719,53 @@ void bn_forward_train(int dtype, const void* x, const void* res, void* y, int64_
   const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t asm_ = sizeof(float) * 2 * C;
-#define DCP_BN_APPLY(D, R, A)                                                                                     \
+#define DK_BN_APPLY(D, R, A)                                                                                     \
   hipLaunchKernelGGL((bn_apply_kernel<D, R, A, true>), dim3(grid), dim3(kT), asm_, s, x, res, acc, gamma, beta,   \
                      nullptr, nullptr, y, mean, invstd, running_mean, running_var, momentum, eps, M, nvec, C, nbt, \
                      mbits, zs)
   const bool r = res != nullptr;
   if (dtype == BN_BF16) {
-    if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
-    else if (r) DCP_BN_APPLY(BN_BF16, true, false);
-    else if (act) DCP_BN_APPLY(BN_BF16, false, true);
-    else DCP_BN_APPLY(BN_BF16, false, false);
+    if (r && act) DK_BN_APPLY(BN_BF16, true, true);
+    else if (r) DK_BN_APPLY(BN_BF16, true, false);
+    else if (act) DK_BN_APPLY(BN_BF16, false, true);
+    else DK_BN_APPLY(BN_BF16, false, false);
   } else {
-    if (r && act) DCP_BN_APPLY(BN_F32, true, true);
-    else if (r) DCP_BN_APPLY(BN_F32, true, false);
-    else if (act) DCP_BN_APPLY(BN_F32, false, true);
-    else DCP_BN_APPLY(BN_F32, false, false);
+    if (r && act) DK_BN_APPLY(BN_F32, true, true);
+    else if (r) DK_BN_APPLY(BN_F32, true, false);
+    else if (act) DK_BN_APPLY(BN_F32, false, true);
+    else DK_BN_APPLY(BN_F32, false, false);
   }
-#undef DCP_BN_APPLY
+#undef DK_BN_APPLY
 }
 
 void bn_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
               const float* shift, bool act, hipStream_t s) {
-  bn_init_flags();
-  const int64_t nvec = M * C / kV;
+    const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t asm_ = sizeof(float) * 2 * C;
-#define DCP_BN_APPLY(D, R, A)                                                                                  \
+#define DK_BN_APPLY(D, R, A)                                                                                  \
   hipLaunchKernelGGL((bn_apply_kernel<D, R, A, false>), dim3(grid), dim3(kT), asm_, s, x, res, nullptr, nullptr, \
                      nullptr, scale, shift, y, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, M, nvec, C, nullptr, \
                      nullptr, 0)
   const bool r = res != nullptr;
   if (dtype == BN_BF16) {
-    if (r && act) DCP_BN_APPLY(BN_BF16, true, true);
-    else if (r) DCP_BN_APPLY(BN_BF16, true, false);
-    else if (act) DCP_BN_APPLY(BN_BF16, false, true);
-    else DCP_BN_APPLY(BN_BF16, false, false);
+    if (r && act) DK_BN_APPLY(BN_BF16, true, true);
+    else if (r) DK_BN_APPLY(BN_BF16, true, false);
+    else if (act) DK_BN_APPLY(BN_BF16, false, true);
+    else DK_BN_APPLY(BN_BF16, false, false);
   } else {
-    if (r && act) DCP_BN_APPLY(BN_F32, true, true);
-    else if (r) DCP_BN_APPLY(BN_F32, true, false);
-    else if (act) DCP_BN_APPLY(BN_F32, false, true);
-    else DCP_BN_APPLY(BN_F32, false, false);
+    if (r && act) DK_BN_APPLY(BN_F32, true, true);
+    else if (r) DK_BN_APPLY(BN_F32, true, false);
+    else if (act) DK_BN_APPLY(BN_F32, false, true);
+    else DK_BN_APPLY(BN_F32, false, false);
   }
-#undef DCP_BN_APPLY
+#undef DK_BN_APPLY
 }
 
 void bn_stats_coef(int dtype, const void* x, int64_t M, int C, const float* gamma, const float* beta,
                    float* running_mean, float* running_var, float momentum, float eps, float* mean, float* invstd,
                    float* scale, float* shift, float* acc, int64_t* nbt, hipStream_t s, bool acc_ready) {
-  bn_init_flags();
-  int nblk, nchunks;
+    int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks);
   const size_t sm = red_smem(C);
@@ -819,12 +789,11 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
                  bool store_g, void* gout,
                  void* dx, float* dgamma, float* dbeta, float* acc, bool training, const uint8_t* mbits,
                  hipStream_t s) {
-  bn_init_flags();
-  int nblk, nchunks;
+    int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks, true);
   const size_t sm = red_smem(C);
-#define DCP_BN_RED(D, A, G)                                                                                 \
+#define DK_BN_RED(D, A, G)                                                                                 \
   do {                                                                                                        \
     if (training)                                                                                             \
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<D, A, G, false, (A && !G)>), dim3(nblk, nchunks), dim3(kT), sm, s, \
@@ -847,23 +816,23 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
                               gy, gy2, y, x, mean, invstd, gamma, beta, mbits, M, C, rpb, acc, gout);
     }
   } else if (dtype == BN_BF16) {
-    if (act && store_g) DCP_BN_RED(BN_BF16, true, true);
-    else if (act) DCP_BN_RED(BN_BF16, true, false);
-    else if (store_g) DCP_BN_RED(BN_BF16, false, true);
-    else DCP_BN_RED(BN_BF16, false, false);
+    if (act && store_g) DK_BN_RED(BN_BF16, true, true);
+    else if (act) DK_BN_RED(BN_BF16, true, false);
+    else if (store_g) DK_BN_RED(BN_BF16, false, true);
+    else DK_BN_RED(BN_BF16, false, false);
   } else {
-    if (act && store_g) DCP_BN_RED(BN_F32, true, true);
-    else if (act) DCP_BN_RED(BN_F32, true, false);
-    else if (store_g) DCP_BN_RED(BN_F32, false, true);
-    else DCP_BN_RED(BN_F32, false, false);
+    if (act && store_g) DK_BN_RED(BN_F32, true, true);
+    else if (act) DK_BN_RED(BN_F32, true, false);
+    else if (store_g) DK_BN_RED(BN_F32, false, true);
+    else DK_BN_RED(BN_F32, false, false);
   }
-#undef DCP_BN_RED
+#undef DK_BN_RED
   const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   // g source: the stored masked gradient when available, else recompute the mask
   const void* gsrc = store_g ? gout : gy;
   auto bsm = [C](bool mx) { return sizeof(float) * (mx ? 6 : 4) * C; };
-#define DCP_BN_BAPPLY(D, A, F)                                                                                  \
+#define DK_BN_BAPPLY(D, A, F)                                                                                  \
   do {                                                                                                          \
     if (training)                                                                                               \
       hipLaunchKernelGGL((bn_bwd_apply_kernel<D, A, F, true>), dim3(grid), dim3(kT), bsm(A && !F), s, gsrc, y, x, mean, \
@@ -873,23 +842,22 @@ void bn_backward(int dtype, const void* gy, const void* gy2, const void* y, cons
                          invstd, gamma, beta, acc, dgamma, dbeta, training, dx, M, nvec, C);                   \
   } while (0)
   if (dtype == BN_BF16) {
-    if (store_g) DCP_BN_BAPPLY(BN_BF16, false, true);
-    else if (act) DCP_BN_BAPPLY(BN_BF16, true, false);
-    else DCP_BN_BAPPLY(BN_BF16, false, false);
+    if (store_g) DK_BN_BAPPLY(BN_BF16, false, true);
+    else if (act) DK_BN_BAPPLY(BN_BF16, true, false);
+    else DK_BN_BAPPLY(BN_BF16, false, false);
   } else {
-    if (store_g) DCP_BN_BAPPLY(BN_F32, false, true);
-    else if (act) DCP_BN_BAPPLY(BN_F32, true, false);
-    else DCP_BN_BAPPLY(BN_F32, false, false);
+    if (store_g) DK_BN_BAPPLY(BN_F32, false, true);
+    else if (act) DK_BN_BAPPLY(BN_F32, true, false);
+    else DK_BN_BAPPLY(BN_F32, false, false);
   }
-#undef DCP_BN_BAPPLY
+#undef DK_BN_BAPPLY
 }
 
 void bn_forward_train_resbn(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
                             const float* gamma, const float* beta, float* running_mean, float* running_var,
                             float momentum, float eps, float* mean, float* invstd, const float* acc, int64_t* nbt,
                             uint8_t* mbits, const ResBnArgs& rb, hipStream_t s) {
-  bn_init_flags();
-  const int64_t nvec = M * C / kV;
+    const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t asm_ = sizeof(float) * 4 * C;
   if (dtype == BN_BF16)
@@ -906,8 +874,7 @@ void bn_backward_resbn(int dtype, const void* gy, const void* gy2, const void* x
                        const float* gamma, const float* mean, const float* invstd, const uint8_t* mbits, void* gout,
                        void* dx, float* dgamma, float* dbeta, float* acc, const void* x2, const float* mean2,
                        float* acc2, hipStream_t s) {
-  bn_init_flags();
-  int nblk, nchunks;
+    int nblk, nchunks;
   int64_t rpb;
   red_geometry(M, C, &nblk, &rpb, &nchunks, true);
   const size_t sm = red_smem(C);
@@ -945,8 +912,7 @@ void bn_backward_resbn(int dtype, const void* gy, const void* gy2, const void* x
 void bn_backward_apply_plain(int dtype, const void* g, const void* x, int64_t M, int C, const float* gamma,
                              const float* mean, const float* invstd, const float* acc, void* dx, float* dgamma,
                              float* dbeta, hipStream_t s) {
-  bn_init_flags();
-  const int64_t nvec = M * C / kV;
+    const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t bsm = sizeof(float) * 4 * C;
   if (dtype == BN_BF16)
@@ -961,8 +927,7 @@ void bn_backward_apply2(int dtype, const void* g, const void* x, const void* x2,
                         const float* mean, const float* invstd, const float* acc, const float* gamma2,
                         const float* mean2, const float* invstd2, const float* acc2, void* dx, void* dx2,
                         float* dgamma, float* dbeta, float* dgamma2, float* dbeta2, hipStream_t s) {
-  bn_init_flags();
-  const int64_t nvec = M * C / kV;
+    const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t sm = sizeof(float) * 8 * C;
   if (dtype == BN_BF16)
@@ -979,8 +944,7 @@ void bn_backward_apply2(int dtype, const void* g, const void* x, const void* x2,
 void bn_backward_apply(int dtype, const void* gy, const void* x, int64_t M, int C, const float* gamma,
                        const float* beta, const float* mean, const float* invstd, const float* acc, void* dx,
                        float* dgamma, float* dbeta, hipStream_t s) {
-  bn_init_flags();
-  const int64_t nvec = M * C / kV;
+    const int64_t nvec = M * C / kV;
   const int grid = apply_grid(nvec, C / kV);
   const size_t sm = sizeof(float) * 6 * C;
   if (dtype == BN_BF16)

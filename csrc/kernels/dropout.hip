@@ -151,19 +151,19 @@ void dropout(int xdtype, int ydtype, const void* x, const void* res, void* y, in
   const uint32_t thr = dropout_threshold(p);
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   const dim3 g = grid_for((n + 3) / 4);
-#define DCP_DR(XD, RD, R) \
+#define DK_DR(XD, RD, R) \
   hipLaunchKernelGGL((dropout_kernel<XD, RD, R>), g, dim3(kT), 0, s, x, res, y, n, thr, scale, seed, offset, \
                      offset_dev)
   if (xdtype == DR_BF16 && ydtype == DR_BF16) {
-    if (res) DCP_DR(DR_BF16, DR_BF16, true); else DCP_DR(DR_BF16, DR_BF16, false);
+    if (res) DK_DR(DR_BF16, DR_BF16, true); else DK_DR(DR_BF16, DR_BF16, false);
   } else if (xdtype == DR_BF16 && ydtype == DR_F32) {
-    if (res) DCP_DR(DR_BF16, DR_F32, true); else DCP_DR(DR_BF16, DR_F32, false);
+    if (res) DK_DR(DR_BF16, DR_F32, true); else DK_DR(DR_BF16, DR_F32, false);
   } else if (xdtype == DR_F32 && ydtype == DR_BF16) {
-    if (res) DCP_DR(DR_F32, DR_BF16, true); else DCP_DR(DR_F32, DR_BF16, false);
+    if (res) DK_DR(DR_F32, DR_BF16, true); else DK_DR(DR_F32, DR_BF16, false);
   } else {
-    if (res) DCP_DR(DR_F32, DR_F32, true); else DCP_DR(DR_F32, DR_F32, false);
+    if (res) DK_DR(DR_F32, DR_F32, true); else DK_DR(DR_F32, DR_F32, false);
   }
-#undef DCP_DR
+#undef DK_DR
 }
 
 void feature_dropout(int dtype, const void* x, void* y, int64_t rows, int64_t inner, float p, uint64_t seed,

@@ -152,13 +152,13 @@ void gelu_bwd(bool tanh_approx, const void* gy, const void* h, void* gh, float* 
   const auto* g = static_cast<const uint16_t*>(gy);
   const auto* x = static_cast<const uint16_t*>(h);
   auto* o = static_cast<uint16_t*>(gh);
-#define DCP_GELU_BWD(T, B) hipLaunchKernelGGL((gelu_bwd_kernel<T, B>), grid, dim3(kT), 0, s, g, x, o, db, M, N, rps)
+#define DK_GELU_BWD(T, B) hipLaunchKernelGGL((gelu_bwd_kernel<T, B>), grid, dim3(kT), 0, s, g, x, o, db, M, N, rps)
   if (tanh_approx) {
-    if (db) DCP_GELU_BWD(true, true); else DCP_GELU_BWD(true, false);
+    if (db) DK_GELU_BWD(true, true); else DK_GELU_BWD(true, false);
   } else {
-    if (db) DCP_GELU_BWD(false, true); else DCP_GELU_BWD(false, false);
+    if (db) DK_GELU_BWD(false, true); else DK_GELU_BWD(false, false);
   }
-#undef DCP_GELU_BWD
+#undef DK_GELU_BWD
 }
 
 }  // namespace kern

@@ -192,12 +192,23 @@ constexpr int nt_stages() { return BK == 64 ? 2 : 3; }
 // 4 x 2 (8 waves, one workgroup per CU: each B tile feeds twice the rows);
 // 256 x 64: 4 x 1 (every wave 64 x 64: twice the MFMAs per fragment read of
 // the 128 x 64 tile for the Cout = 64 layers).
+// 256 x 256 ("big tile"): 2 x 4 waves of 128 x 64 each (two per SIMD, 128
+// accumulator registers each), one workgroup per CU — a 256 x 256 x 32 stage
+// is ~1,000 MFMA cycles per SIMD, so two stages of DMA in flight cover an
+// HBM miss, which a 128 x 128 tile's ~250-cycle stages do not.
 template <int BM, int BN>
-constexpr int nt_wn() { return (BM == 256 && BN == 64) ? 1 : 2; }
+constexpr int nt_wr() { return (BM == 256 && BN == 256) ? 128 : 64; }  // rows per wave
 template <int BM, int BN>
-constexpr int nt_threads() { return 64 * (BM / 64) * nt_wn<BM, BN>(); }
-template <int BM, int BN, bool PRO, int EPI, bool GATHER, int BK, int AMODE = 0>
-__global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() <= 256 ? 2 : 1)) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+constexpr int nt_wn() { return (BM == 256 && BN == 64) ? 1 : (BM == 256 && BN == 256) ? 4 : 2; }
+template <int BM, int BN>
+constexpr int nt_threads() { return 64 * (BM / nt_wr<BM, BN>()) * nt_wn<BM, BN>(); }
+// NS > 0: an NS-deep ring (one workgroup per CU) whose C staging aliases the
+// ring slot the tile's last stage was read from (one extra barrier per tile)
+// instead of a separate region: NS - 2 stages stay in flight across every
+// barrier (counted vmcnt), where the default 2-stage BK = 64 ring drains its
+// DMA at each stage and relies on a second resident workgroup to hide it.
+template <int BM, int BN, bool PRO, int EPI, bool GATHER, int BK, int AMODE = 0, int NS = 0>
+__global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() <= 256 && NS == 0 && nt_wr<BM, BN>() == 64 ? 2 : 1)) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                      uint16_t* __restrict__ C, int64_t M, int N, int K,
                                                      const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int relu,
@@ -218,25 +229,28 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   constexpr bool RR = EPI == 5 || EPI == 6;  // RESRED
   constexpr bool X2 = EPI == 6;
   static_assert(!(PRO && (RED || RR)), "RED / RESRED are data-gradient epilogues");
-  constexpr int kNSnt = nt_stages<BK>();
+  constexpr int kNSnt = NS > 0 ? NS : nt_stages<BK>();
+  constexpr bool CA = NS > 0;  // C staging aliased into the ring
   constexpr int RB = BK * 2;                                  // stage row bytes
   constexpr int CPR = BK / 8;                                 // 16-B chunks per row
   constexpr int NT = nt_threads<BM, BN>();
   constexpr int WNW = nt_wn<BM, BN>();
-  constexpr int WM = BM / 64, NW = WNW * WM;                 // waves along M, waves
+  constexpr int WR = nt_wr<BM, BN>();                        // rows per wave
+  constexpr int WM = BM / WR, NW = WNW * WM;                 // waves along M, waves
   constexpr int SA = BM * RB, SB = BN * RB, STAGE = SA + SB;  // bytes
   constexpr int NA = SA / (NW * 1024), NB = SB / (NW * 1024);  // glds per wave per stage (1 KiB each)
   static_assert(NA * NW * 1024 == SA && NB * NW * 1024 == SB && NB >= 1, "tile / wave count mismatch");
   constexpr int G = NA + NB;
   constexpr int WN = BN / WNW;               // wave tile columns
-  constexpr int FM = 4, FN = WN / 16;        // 16-row / 16-column fragments per wave (64 rows x WN)
+  constexpr int FM = WR / 16, FN = WN / 16;  // 16-row / 16-column fragments per wave (WR rows x WN)
   constexpr int CST = 32 * WN * 2;           // per-wave C staging: 32 rows × WN bf16
   constexpr int LPR = WN / 8;                // lanes per staged row (16 B each)
   constexpr int RPI = 64 / LPR;              // staged rows per store instruction
-  constexpr int FS = 2 * (32 / RPI) * (EPI == 3 ? 4 : 1);  // global stores per wave per tile
+  constexpr int FS = (FM / 2) * (32 / RPI) * (EPI == 3 ? 4 : 1);  // global stores per wave per tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  static_assert(!CA || NW * CST <= STAGE, "aliased C staging must fit one ring slot");
   char* cst_all = lds + kNSnt * STAGE;
-  float* pro = reinterpret_cast<float*>(cst_all + NW * CST);  // [2][K] scale, shift (PRO)
+  float* pro = reinterpret_cast<float*>(cst_all + (CA ? 0 : NW * CST));  // [2][K] scale, shift (PRO)
 
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -289,8 +303,14 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   int is_n = 0, is_kt = 0, is_slot = 0, is_v = wg;
   int is_c0 = 0, is_dy = 0, is_dx = 0;  // GATHER: channel offset and tap of the issue stage
   int64_t is_off = 0;                   // GATHER: (is_dy * W + is_dx) * cin + is_c0
-  const uint16_t* asrc[NA];
-  const uint16_t* bsrc[NB];
+  // LEAN (the 256 x 256 tile: 8 A + 8 B DMAs per wave per stage): source
+  // addresses recomputed at every issue from the tile's first row instead of
+  // 16 per-lane 64-bit pointers held across the loop — a few VALU per DMA
+  // against 128 MFMAs per stage, and ~32 VGPRs the accumulators need
+  constexpr bool LEAN = (NA > 4 || WR == 128) && !GATHER && AMODE == 0;
+  const uint16_t* asrc[LEAN ? 1 : NA];
+  const uint16_t* bsrc[LEAN ? 1 : NB];
+  int64_t a_m0 = 0;  // LEAN: first row of the issue tile
   // GATHER: per A row (fixed for a tile) the address of tap (0, 0), channel 0
   // (may point outside the tensor: only in-bounds taps are dereferenced) and
   // the in-bounds taps as bit masks (bits 0-7: dy, 8-15: dx) — a stage then
@@ -300,6 +320,10 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   uint32_t gvm[GATHER ? NA : 1];
   auto set_a = [&](int v) {
     const int64_t m0 = static_cast<int64_t>(v / tn) * BM;
+    if constexpr (LEAN) {
+      a_m0 = m0;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int p = (wave * NA + j) * 64 + lane;  // 16-B unit in the A image
@@ -324,21 +348,28 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
         const int ho = t1 % geo.Ho, nn = t1 / geo.Ho;
         asrc[j] = A + ((static_cast<int64_t>(nn) * geo.H + 2 * ho + (lc >> 2)) * geo.W + 2 * wo) * 4 + (lc & 3) * 8;
       } else {
-        asrc[j] = A + gm * K + lc * 8;
+        asrc[LEAN ? 0 : j] = A + gm * K + lc * 8;
       }
     }
   };
+  if constexpr (!LEAN) {
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const int p = (wave * NB + j) * 64 + lane;
-    const int r = p / CPR, lc = (p % CPR) ^ nt_swzk<BK>(p / CPR);
-    bsrc[j] = B + static_cast<int64_t>(n0 + r) * ldb + lc * 8;
+    for (int j = 0; j < NB; ++j) {
+      const int p = (wave * NB + j) * 64 + lane;
+      const int r = p / CPR, lc = (p % CPR) ^ nt_swzk<BK>(p / CPR);
+      bsrc[j] = B + static_cast<int64_t>(n0 + r) * ldb + lc * 8;
+    }
   }
   set_a(wg);
   auto issue = [&]() {
     if (is_n >= T) return;
     char* base = lds + is_slot * STAGE;
     const int k0 = is_kt * BK;
+    // LEAN: an opaque copy of the lane id, so the per-DMA row / swizzle math
+    // is redone at every issue instead of being hoisted out of the loop into
+    // 16 live 64-bit offsets (which spill at 256 accumulator registers)
+    int ln = lane;
+    if (LEAN) asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       if (GATHER) {
@@ -349,12 +380,26 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
         glds16(src, base + (wave * NA + j) * 1024);
       } else if (AMODE == 1) {
         glds16(asrc[j] + static_cast<int64_t>(is_kt) * (BK / 32) * geo.W * 4, base + (wave * NA + j) * 1024);
+      } else if (LEAN) {
+        const int p = (wave * NA + j) * 64 + ln;
+        const int r = p / CPR, lc = (p % CPR) ^ nt_swzk<BK>(r);
+        int64_t gm = a_m0 + r;
+        gm = gm < M ? gm : M - 1;
+        glds16(A + gm * K + lc * 8 + k0, base + (wave * NA + j) * 1024);
       } else {
         glds16(asrc[j] + k0, base + (wave * NA + j) * 1024);
       }
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j) glds16(bsrc[j] + k0, base + SA + (wave * NB + j) * 1024);
+    for (int j = 0; j < NB; ++j) {
+      if (LEAN) {
+        const int p = (wave * NB + j) * 64 + ln;
+        const int r = p / CPR, lc = (p % CPR) ^ nt_swzk<BK>(r);
+        glds16(B + static_cast<int64_t>(n0 + r) * ldb + lc * 8 + k0, base + SA + (wave * NB + j) * 1024);
+      } else {
+        glds16(bsrc[j] + k0, base + SA + (wave * NB + j) * 1024);
+      }
+    }
     ++is_n;
     is_slot = is_slot + 1 == kNSnt ? 0 : is_slot + 1;
     if (GATHER) {
@@ -418,6 +463,16 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
 
   const int ck = lane >> 4;  // logical 16-B chunk (k = 8ck … 8ck+7) this lane reads
   int kt = 0, slot = 0, cv = wg;  // consumer k-step, ring slot, tile id
+  // STAG (the 256 x 256 tile, BK = 64): waves 4-7 (wm = 1) share SIMDs with
+  // waves 0-3; they read the stage's second 32-k half into registers but run
+  // its MFMAs after the NEXT barrier, so right after every barrier one wave
+  // of each SIMD pair has MFMAs ready while its partner waits for LDS reads
+  // (a two-group ping-pong; MI355X_MICROARCH "two waves per SIMD", item 9).
+  // Not across a tile end: the epilogue needs the full sums.
+  constexpr bool STAG = WR == 128 && BK == 64 && !PRO;
+  const bool late = STAG && wm == 1;
+  bool pend = false;  // late group: a stage's second half waits in cx / cw
+  bf16x8 cx[STAG ? FM : 1], cw[STAG ? FN : 1];
   for (int q = 0; q < T; ++q) {
     // vmcnt retires in issue order: the ops younger than stage q's DMA are the
     // DMA of q+1 and the epilogue stores of a tile end at q-2 or q-1 (issued
@@ -435,6 +490,14 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
     }
     barrier();  // stage q visible to all waves; all reads of slot (q-1)%kNSnt done
     issue();
+    if (STAG && pend) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[i], cx[j], acc[i][j], 0, 0, 0);
+      pend = false;
+    }
     const char* sA = lds + slot * STAGE;
     const char* sB = sA + SA;
 #pragma unroll
@@ -443,7 +506,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       bf16x8 xf[FM], wf[FN];
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const int r = wm * 64 + j * 16 + (lane & 15);
+        const int r = wm * WR + j * 16 + (lane & 15);
         xf[j] = *reinterpret_cast<const bf16x8*>(sA + r * RB + 16 * (lch ^ nt_swzk<BK>(r)));
       }
 #pragma unroll
@@ -462,6 +525,14 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
 #pragma unroll
         for (int j = 0; j < FM; ++j) xf[j] = bn_act_frag(xf[j], sc, sf, relu != 0);
       }
+      if (STAG && h == 1 && late && kt != KT - 1) {
+#pragma unroll
+        for (int j = 0; j < FM; ++j) cx[STAG ? j : 0] = xf[j];
+#pragma unroll
+        for (int i = 0; i < FN; ++i) cw[STAG ? i : 0] = wf[i];
+        pend = true;
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -470,12 +541,20 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
     }
 
     if (kt == KT - 1) {
+      if (CA) {
+        // every wave's fragment reads of this slot are done before any wave
+        // stages C into it; the slot's next DMA is issued after the following
+        // stage's barrier, which every wave reaches with its staging reads
+        // consumed by its global stores
+        barrier();
+        cst = lds + slot * STAGE + wave * CST;
+      }
       // epilogue, per wave and in two 32-row halves: acc[i][j][r] = C[m][n] with
       // m = 16j + (lane&15), n = 16i + 4(lane>>4) + r (wave-local) → 8-B packed
       // writes into this wave's LDS staging → 16-B row-contiguous reads →
       // global stores covering whole 128-B lines (no cross-wave sync needed:
       // a wave's LDS ops execute in order).
-      const int64_t mt = static_cast<int64_t>(cv / tn) * BM + wm * 64;
+      const int64_t mt = static_cast<int64_t>(cv / tn) * BM + wm * WR;
       // RED / RESRED: x (gy2, bits, x2) rows of both halves loaded before the
       // first use — one wait, twice the bytes in flight per wave (the epilogue
       // is latency-bound on these reads); per half for EPI 6 (registers)
@@ -484,11 +563,11 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       uint4 xr[(RED || RR) ? HB * NR : 1], g2r[RR ? HB * NR : 1], x2r[X2 ? HB * NR : 1];
       uint32_t mbr[RR ? HB * NR : 1];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if ((RED || RR) && (HB == 1 || h == 0)) {
+      for (int h = 0; h < FM / 2; ++h) {  // 32-row halves of the wave's rows
+        if ((RED || RR) && h % HB == 0) {
           // (a plain loop, not a lambda: a lambda capturing the arrays by
           // reference left dead scratch stores of them in the epilogue)
-          const int h0 = HB == 1 ? h : 0;
+          const int h0 = h;  // first half of the group loaded here
           const bool has2 = RR && bnr.gy2 != nullptr;
 #pragma unroll
           for (int i = 0; i < HB * NR; ++i) {
@@ -554,10 +633,10 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
           } else if (m < M && RR) {
             // g = (dgrad + gy2) · relu bit, in fp32 from the bf16-rounded dgrad
             // (what the separate reduce kernel sees); bf16 g stored, fp32 g reduced
-            const uint4 g2 = g2r[RR ? (HB - 1) * h * NR + it : 0], xv = xr[(HB - 1) * h * NR + it];
+            const uint4 g2 = g2r[RR ? (h % HB) * NR + it : 0], xv = xr[(h % HB) * NR + it];
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, y4[4] = {g2.x, g2.y, g2.z, g2.w};
             const uint32_t x4[4] = {xv.x, xv.y, xv.z, xv.w};
-            const uint32_t mb = mbr[RR ? (HB - 1) * h * NR + it : 0];
+            const uint32_t mb = mbr[RR ? (h % HB) * NR + it : 0];
             float gk[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -569,7 +648,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
               ssq[k] = fmaf(gk[k], xk - rmu[RR ? k : 0], ssq[k]);
             }
             if (X2) {
-              const uint4 x2v = x2r[X2 ? (HB - 1) * h * NR + it : 0];
+              const uint4 x2v = x2r[X2 ? (h % HB) * NR + it : 0];
               const uint32_t z4[4] = {x2v.x, x2v.y, x2v.z, x2v.w};
 #pragma unroll
               for (int k = 0; k < 8; ++k) {
@@ -593,7 +672,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
               }
             }
             if (RED) {
-              const uint4 xv = xr[RED ? (HB - 1) * h * NR + it : 0];
+              const uint4 xv = xr[RED ? (h % HB) * NR + it : 0];
               const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
               const uint32_t x4[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
@@ -1475,24 +1554,13 @@ struct WgradPlan {
   int64_t chunk;
 };
 
-// wgrad grid order (DCP_WGRAD_ORDER): 1 = XCD-aware, taps fastest (default), 0 = tap slowest
-inline int wgrad_order() {
-  static const int o = [] {
-    const char* v = getenv("DCP_WGRAD_ORDER");
-    return v ? atoi(v) : 1;
-  }();
-  return o;
-}
+// wgrad grid order: 1 = XCD-aware, taps fastest (−5…18 % on the 1x1 wgrads
+// vs 0 = tap slowest, NOTES §19)
+inline int wgrad_order() { return 1; }
 
 // multi-tap wgrad (BMODE 2) for kxk convolutions with N2 = 64 input channels:
-// one 128-wide tile covers two taps (DCP_WGRAD_MTAP=0 turns it off)
-inline bool wgrad_mtap(int N2, int taps) {
-  static const bool on = [] {
-    const char* v = getenv("DCP_WGRAD_MTAP");
-    return !(v && v[0] == '0');
-  }();
-  return on && taps > 1 && N2 == 64;
-}
+// one 128-wide tile covers two taps (layer-1 455 → 373 µs, NOTES §19)
+inline bool wgrad_mtap(int N2, int taps) { return taps > 1 && N2 == 64; }
 
 WgradPlan wgrad_plan(int64_t M, int N1, int N2, int taps = 1) {
   WgradPlan p;
@@ -1520,38 +1588,58 @@ bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) {
 
 namespace {
 // k per ring stage of gemm_nt: 64 (2-stage ring) halves the barriers and
-// vmcnt waits per MFMA; 32 (3-stage ring) kept for A/B (DCP_GEMM_BK=32)
-inline int nt_bk() {
-  static const int bk = [] {
-    const char* v = getenv("DCP_GEMM_BK");
-    return v && atoi(v) == 32 ? 32 : 64;
-  }();
-  return bk;
-}
+// vmcnt waits per MFMA of the 32-deep 3-stage ring (which the BN-prologue
+// GEMMs keep: their coefficient loads overlap the MFMAs only at BK = 32)
+inline int nt_bk() { return 64; }
 
 // Tile rows per workgroup: 256 (8 waves, 1 workgroup per CU) when the M
-// tiles alone fill the chip, else 128 (4 waves, 2 per CU). DCP_GEMM_BM=128 /
-// 256 forces one (A/B switch).
+// tiles alone fill the chip, else 128 (4 waves, 2 per CU).
 inline int nt_bm(int64_t M, int tn, int BN, bool pro, int K, bool gather) {
-  static const int force = [] {
-    const char* v = getenv("DCP_GEMM_BM");
-    return v ? atoi(v) : 0;
-  }();
-  static const int n64 = [] {  // tile rows for Cout = 64 (256: 4 x 1 waves of 64 x 64)
-    const char* v = getenv("DCP_GEMM_N64_BM");
-    return v ? atoi(v) : 0;
-  }();
-  if (force == 128 || force == 256) return force;
   // Cout = 64: 4 x 1 waves of 64 x 64 pay on the plain 1x1 GEMMs with K >= 256
   // (layer-1 conv1 forward, conv3 data gradient: -7-10 %, profiles/r2_gemm_bm_ab.txt);
   // the gathered 3x3 ones lose (their per-stage gather work doubles per wave)
-  if (BN == 64) return n64 == 128 || n64 == 256 ? n64 : (!gather && K >= 256 ? 256 : 128);
+  if (BN == 64) return !gather && K >= 256 ? 256 : 128;
   // 8 x 64 x 64 waves measured slower than 2 x 128 x 128 workgroups on every
   // non-prologue shape (profiles/r2_gemm_bm256.txt); the BN-prologue GEMMs
   // (one prologue per 256 rows) gain
   return pro && (M / 256) * tn >= 256 ? 256 : 128;
 }
 
+}  // namespace
+
+// Runtime tuning table of the GEMM launchers (tools/gemm_ab.py: in-process
+// A/B without environment switches). nt_big: 256 x 256 tiles where
+// N % 256 == 0 (0 off, 1 BK 32 x 4 stages, 2 BK 64 x 2 stages).
+// (A 3-stage 128 x 128 ring at one workgroup per CU measured 20-45 % slower
+// than the 2-stage ring at two per CU on every compute-bound shape,
+// profiles/r3_gemm_ab_ns3.jsonl.)
+// reserve_cus: CUs the persistent grids (gemm_nt, the direct 3x3 kernels)
+// leave free for concurrently running collectives — a persistent workgroup
+// that cannot become resident because RCCL holds its CU delays its whole share
+// of tiles (NOTES §22; env DCP_RESERVE_CUS sets the initial value).
+namespace {
+int g_nt_big = 0;
+int g_reserve_cus = [] {
+  const char* v = getenv("DCP_RESERVE_CUS");
+  const int r = v ? atoi(v) : 0;
+  return r < 0 ? 0 : (r > 192 ? 192 : r);
+}();
+// CUs a persistent grid sizes itself for
+inline int grid_cus() { return 256 - g_reserve_cus; }
+}  // namespace
+void gemm_tune(const char* key, int value) {
+  const std::string k(key);
+  if (k == "nt_big") g_nt_big = value;
+  if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
+}
+int gemm_tune_get(const char* key) {
+  const std::string k(key);
+  if (k == "nt_big") return g_nt_big;
+  if (k == "reserve_cus") return g_reserve_cus;
+  return -1;
+}
+
+namespace {
 template <bool GATHER, int BK, int BM>
 void gemm_nt_launch_bm(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                        const float* shift, bool relu, float* stats, const ConvGeo& geo, const BnRedArgs* red,
@@ -1562,16 +1650,11 @@ void gemm_nt_launch_bm(const void* A, const void* B, void* C, int64_t M, int N, 
   // all tiles resident at once when they fit (2 workgroups of 128 rows or one
   // of 256 per CU), else persistent over that many workgroups (a multiple of
   // tn, see the kernel)
-  constexpr int kRes = BM == 128 ? 512 : 256;
+  const int kRes = (BM == 128 ? 2 : 1) * grid_cus();
   const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
-  // DCP_GEMM_PERSIST=0: one tile per workgroup (the dispatcher balances the
-  // tail, and workgroups that cannot be resident — CUs held by concurrent
-  // RCCL kernels — cost one tile, not a persistent workgroup's whole share)
-  static const bool persist = [] {
-    const char* v = getenv("DCP_GEMM_PERSIST");
-    return !(v && v[0] == '0');
-  }();
-  int P = tiles <= kRes || !persist ? static_cast<int>(tiles) : (kRes / tn) * tn;
+  // (one tile per workgroup instead — the dispatcher balancing the tail —
+  // measured −4.8 %, profiles/r2_ab_gemm_persist.jsonl)
+  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
   if (P < tn) P = tn;
   const dim3 grid(P);
   const bool pro = scale != nullptr;
@@ -1586,59 +1669,99 @@ void gemm_nt_launch_bm(const void* A, const void* B, void* C, int64_t M, int N, 
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
   const BnRedArgs bnr = red ? *red : BnRedArgs{};
-#define DCP_GNT(BN_, P_, S_)                                                                                     \
+#define DK_GNT(BN_, P_, S_)                                                                                     \
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, P_, S_, GATHER, BK>), grid, dim3(NT), lds, s, a, b, c, M, N, K,   \
                      scale, shift, relu ? 1 : 0, stats, tiles_m, tn, geo, bnr)
-#define DCP_GNT2(BN_)                            \
+#define DK_GNT2(BN_)                            \
   do {                                           \
     if (red) {                                   \
       if constexpr (!GATHER) {                   \
         if (red->bits && red->x2) {              \
-          DCP_GNT(BN_, false, 6);                \
+          DK_GNT(BN_, false, 6);                \
           break;                                 \
         }                                        \
         if (red->bits) {                         \
-          DCP_GNT(BN_, false, 5);                \
+          DK_GNT(BN_, false, 5);                \
           break;                                 \
         }                                        \
       }                                          \
-      DCP_GNT(BN_, false, 2);                    \
+      DK_GNT(BN_, false, 2);                    \
       break;                                     \
     }                                            \
     if constexpr (!GATHER) {                     \
       if (scatter2) {                            \
-        DCP_GNT(BN_, false, 3);                  \
+        DK_GNT(BN_, false, 3);                  \
         break;                                   \
       }                                          \
     } else {                                     \
       if (parity) {                              \
-        DCP_GNT(BN_, false, 4);                  \
+        DK_GNT(BN_, false, 4);                  \
         break;                                   \
       }                                          \
     }                                            \
     if constexpr (!GATHER) {                     \
       if (pro && st) {                           \
-        DCP_GNT(BN_, true, 1);                   \
+        DK_GNT(BN_, true, 1);                   \
         break;                                   \
       }                                          \
       if (pro) {                                 \
-        DCP_GNT(BN_, true, 0);                   \
+        DK_GNT(BN_, true, 0);                   \
         break;                                   \
       }                                          \
     }                                            \
-    if (st) DCP_GNT(BN_, false, 1);              \
-    else DCP_GNT(BN_, false, 0);                 \
+    if (st) DK_GNT(BN_, false, 1);              \
+    else DK_GNT(BN_, false, 0);                 \
   } while (0)
-  if (BN == 128) DCP_GNT2(128);
-  else DCP_GNT2(64);
-#undef DCP_GNT2
-#undef DCP_GNT
+  if (BN == 128) DK_GNT2(128);
+  else DK_GNT2(64);
+#undef DK_GNT2
+#undef DK_GNT
+}
+
+// 256 x 256 tiles: 2 x 4 waves of 128 x 64, one
+// workgroup per CU (persistent beyond 256 tiles), BKB-deep stages on an
+// NSB-slot ring (BKB * NSB = 128: 128 KB) with the C staging aliased into it.
+// BKB = 32 / NSB = 4: two stages (~2,000 MFMA cycles per wave) in flight
+// across every barrier and one 32-k half of fragments live at a time.
+template <bool GATHER, int BKB, int NSB>
+void gemm_nt_launch_big(const void* A, const void* B, void* C, int64_t M, int N, int K, float* stats,
+                        const ConvGeo& geo, hipStream_t s) {
+  constexpr int BM = 256, BN = 256;
+  const int tiles_m = static_cast<int>((M + BM - 1) / BM);
+  const int tn = N / BN;
+  const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
+  const int kRes = grid_cus();
+  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
+  if (P < tn) P = tn;
+  const size_t lds = static_cast<size_t>(NSB) * (BM + BN) * BKB * 2;
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  auto c = static_cast<uint16_t*>(C);
+  static const bool attr = [] {  // > 64 KB of dynamic LDS
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<BM, BN, false, 0, GATHER, BKB, 0, NSB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<BM, BN, false, 1, GATHER, BKB, 0, NSB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  if (stats)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 1, GATHER, BKB, 0, NSB>), dim3(P), dim3(nt_threads<BM, BN>()),
+                       lds, s, a, b, c, M, N, K, nullptr, nullptr, 0, stats, tiles_m, tn, geo, BnRedArgs{});
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 0, GATHER, BKB, 0, NSB>), dim3(P), dim3(nt_threads<BM, BN>()),
+                       lds, s, a, b, c, M, N, K, nullptr, nullptr, 0, stats, tiles_m, tn, geo, BnRedArgs{});
 }
 
 template <bool GATHER, int BK>
 void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                        const float* shift, bool relu, float* stats, const ConvGeo& geo, const BnRedArgs* red,
                        hipStream_t s, bool scatter2 = false, bool parity = false) {
+  if (g_nt_big && BK == 64 && N % 256 == 0 && scale == nullptr && red == nullptr && !scatter2 && !parity) {
+    if (g_nt_big == 2) gemm_nt_launch_big<GATHER, 64, 2>(A, B, C, M, N, K, stats, geo, s);
+    else gemm_nt_launch_big<GATHER, 32, 4>(A, B, C, M, N, K, stats, geo, s);
+    return;
+  }
   const int BN = N % 128 == 0 ? 128 : 64;
   const int tn = N / BN;
   if (nt_bm(M, tn, BN, scale != nullptr, K, GATHER) == 256)
@@ -1787,13 +1910,9 @@ bool conv_fwd_supported(int Cin, int Cout, int kh, int kw) {
 }
 
 namespace {
-// direct 3x3 / 64-channel kernel (DCP_CONV3_DIRECT=0 falls back to the gathered GEMM)
+// direct 3x3 / 64-channel kernel (else the gathered implicit GEMM)
 inline bool conv3x3_c64_direct(int Cin, int Cout, int kh, int kw, int stride, int pad, int W) {
-  static const bool on = [] {
-    const char* v = getenv("DCP_CONV3_DIRECT");
-    return !(v && v[0] == '0');
-  }();
-  return on && Cin == 64 && Cout == 64 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && W >= 2 && W <= 62;
+  return Cin == 64 && Cout == 64 && kh == 3 && kw == 3 && stride == 1 && pad == 1 && W >= 2 && W <= 62;
 }
 
 void conv3x3_c64_launch(const void* X, const void* Wt, void* Y, int N, int H, int W, const void* zero, float* stats,
@@ -1803,7 +1922,7 @@ void conv3x3_c64_launch(const void* X, const void* Wt, void* Y, int N, int H, in
   const int tiles = N * HT;
   const int chunks = (R + 2) * (W + 2) * 8;    // halo 16-B chunks
   const int halo_bytes = (chunks * 16 + 4095) / 4096 * 4096;
-  const int P = tiles < 256 ? tiles : 256;     // one workgroup per CU
+  const int P = tiles < grid_cus() ? tiles : grid_cus();  // one workgroup per CU
   const int per_block = (tiles + P - 1) / P;
   const size_t lds = 9 * 64 * 128 + 2 * static_cast<size_t>(halo_bytes) + 4 * 32 * 32 * 2;
   auto x = static_cast<const uint16_t*>(X);
@@ -1874,13 +1993,8 @@ void stem_conv_fwd_bm(const void* xp, const void* wm, void* y, int N, int H, int
 
 void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W, int Cout, float* stats,
                    hipStream_t s) {
-  // DCP_STEM_BM=256: 256 x 64 tiles (4 x 1 waves of 64 x 64, one workgroup per CU)
-  static const int bm = [] {
-    const char* v = getenv("DCP_STEM_BM");
-    return v && atoi(v) == 256 ? 256 : 128;
-  }();
-  if (bm == 256) stem_conv_fwd_bm<256>(xp, wm, y, N, H, W, Cout, stats, s);
-  else stem_conv_fwd_bm<128>(xp, wm, y, N, H, W, Cout, stats, s);
+  // 128 x 64 tiles (256 x 64: −, profiles/r2_ab_stem_bm.jsonl)
+  stem_conv_fwd_bm<128>(xp, wm, y, N, H, W, Cout, stats, s);
 }
 
 void weight_prep(const void* table, int n, int64_t tiles, hipStream_t s) {
@@ -1951,50 +2065,28 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   const dim3 grid(p.tiles * p.S * taps);
   const bool pro = scale != nullptr;
   const int tj = N2 / p.bn;
-  // ring config (DCP_WGRAD_CFG): "64x2" (default: BK=64, 2 stages, 64 KB),
-  // "32x2" (32 KB: up to 4 workgroups per CU), "32x4" (the BK=32 4-deep ring)
-  static const int cfg = [] {
-    const char* v = getenv("DCP_WGRAD_CFG");
-    if (v && std::string(v) == "32x2") return 1;
-    if (v && std::string(v) == "32x4") return 2;
-    if (v && atoi(v) == 32) return 2;  // legacy DCP_WGRAD_BK=32 spelling
-    const char* b = getenv("DCP_WGRAD_BK");
-    return b && atoi(b) == 32 ? 2 : 0;
-  }();
-  // the BN-prologue wgrad on the BK=64 ring too (+0.2 % same-box,
-  // profiles/r2_ab_wgrad_pro_bk.jsonl); DCP_WGRAD_PRO_BK=32: the 4-deep BK=32 ring
-  static const bool pro64 = [] {
-    const char* v = getenv("DCP_WGRAD_PRO_BK");
-    return !(v && atoi(v) == 32);
-  }();
-#define DCP_GWG(BM_, BN_, P)                                                                                        \
-  do {                                                                                                             \
-    if (cfg == 0 && (!P || pro64))                                                                                 \
-      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 64>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,    \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo);                \
-    else if (cfg == 1)                                                                                             \
-      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32, 2>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2, \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo);                \
-    else                                                                                                           \
-      hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 32>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,    \
-                         p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo);                \
-  } while (0)
-#define DCP_GWG2(BM_, BN_)                      \
+  // ring: BK = 64, 2 stages (64 KB, 2 workgroups per CU) — also for the
+  // BN-prologue wgrad (+0.2 %, profiles/r2_ab_wgrad_pro_bk.jsonl); the 32-deep
+  // 2- and 4-stage rings measured slower everywhere (NOTES §19)
+#define DK_GWG(BM_, BN_, P)                                                                                     \
+  hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 64>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,     \
+                     p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo)
+#define DK_GWG2(BM_, BN_)                      \
   do {                                          \
     if constexpr (!GATHER) {                    \
       if (pro) {                                \
-        DCP_GWG(BM_, BN_, true);                \
+        DK_GWG(BM_, BN_, true);                \
         break;                                  \
       }                                         \
     }                                           \
-    DCP_GWG(BM_, BN_, false);                   \
+    DK_GWG(BM_, BN_, false);                   \
   } while (0)
-  if (p.bm == 128 && p.bn == 128) DCP_GWG2(128, 128);
-  else if (p.bm == 128) DCP_GWG2(128, 64);
-  else if (p.bn == 128) DCP_GWG2(64, 128);
-  else DCP_GWG2(64, 64);
-#undef DCP_GWG2
-#undef DCP_GWG
+  if (p.bm == 128 && p.bn == 128) DK_GWG2(128, 128);
+  else if (p.bm == 128) DK_GWG2(128, 64);
+  else if (p.bn == 128) DK_GWG2(64, 128);
+  else DK_GWG2(64, 64);
+#undef DK_GWG2
+#undef DK_GWG
   slab_reduce(ws, D, static_cast<int64_t>(N1) * taps * N2 / 4, p.S, s, acc);
 }
 }  // namespace
@@ -2026,14 +2118,9 @@ void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int
 }
 
 namespace {
-// DCP_WGRAD_DIRECT=0: the 64-channel 3x3 wgrad on the gathered multi-tap kernel
-inline bool wgrad_direct() {
-  static const bool on = [] {
-    const char* v = getenv("DCP_WGRAD_DIRECT");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+// the 64-channel 3x3 wgrad on the direct kernel (vs the gathered multi-tap
+// kernel: 334 → 204 µs per layer-1 call, profiles/r2_ab_wgrad_direct_v2.jsonl)
+inline bool wgrad_direct() { return true; }
 
 void conv3x3_c64_wgrad_launch(const void* dY, const void* X, float* D, int N, int H, int W, const void* zero,
                               float* ws, hipStream_t s) {
@@ -2043,7 +2130,7 @@ void conv3x3_c64_wgrad_launch(const void* dY, const void* X, float* D, int N, in
   const int KG = (R * W + 31) / 32;
   const int HT = (H + R - 1) / R;
   const int tiles = N * HT;
-  int nb = tiles < 256 ? tiles : 256;  // one workgroup per CU, each a contiguous run of tiles
+  int nb = tiles < grid_cus() ? tiles : grid_cus();  // one workgroup per CU, each a contiguous run of tiles
   const int per_block = (tiles + nb - 1) / nb;
   nb = (tiles + per_block - 1) / per_block;  // every workgroup has ≥ 1 tile (each writes its slab)
   const int dy_bytes = KG * 32 * 128;

@@ -18,6 +18,11 @@
 namespace dcp {
 namespace kern {
 
+// Runtime tuning of the GEMM launchers for in-process A/B (tools/): key
+// "nt_ns" = gemm_nt ring depth at BK = 64 (0: 2-stage default, 3: 3-stage).
+void gemm_tune(const char* key, int value);
+int gemm_tune_get(const char* key);
+
 // Shapes the kernels take: K and N multiples of 64, any M ≥ 1.
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
 

@@ -57,5 +57,12 @@ void mt_scale_by(TableView t, int64_t nchunks, DType d, const float* scale_dev, 
 // node's arguments are stored in the graph itself.
 void copy_words(const int64_t* src, int64_t* dst, int64_t n, hipStream_t s);
 
+// Contention emulation of one collective on this GPU (multi_tensor.hip):
+// `channels` workgroups move bytes_move bytes from src into scratch (both
+// bytes_buf long, wrapping) and hold their CUs until `us` microseconds
+// (≤ 50 ms) have passed since they started.
+void comm_emulate(const void* src, void* scratch, int64_t bytes_buf, int64_t bytes_move, int channels, double us,
+                  hipStream_t s);
+
 }  // namespace kern
 }  // namespace dcp

@@ -273,30 +273,30 @@ __global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
 template <int XD, int YD>
 void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w, const float* b, void* y, float* mean,
                   float* rstd, int64_t rows, int D, float eps) {
-#define DCP_LNF(V) \
+#define DK_LNF(V) \
   hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V, kRows>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps)
   switch (vpl) {
-    case 1: DCP_LNF(1); break;
-    case 2: DCP_LNF(2); break;
-    case 4: DCP_LNF(4); break;
-    default: DCP_LNF(8);
+    case 1: DK_LNF(1); break;
+    case 2: DK_LNF(2); break;
+    case 4: DK_LNF(4); break;
+    default: DK_LNF(8);
   }
-#undef DCP_LNF
+#undef DK_LNF
 }
 
 template <int XD, int YD>
 void bwd_dispatch(int vpl, dim3 g, size_t sm, hipStream_t s, const void* dy, const void* x, const float* w,
                   const float* mean, const float* rstd, void* dx, float* part, int64_t rows, int D, int rpb) {
-#define DCP_LNB(V) \
+#define DK_LNB(V) \
   hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, kRows>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, \
                      rpb)
   switch (vpl) {
-    case 1: DCP_LNB(1); break;
-    case 2: DCP_LNB(2); break;
-    case 4: DCP_LNB(4); break;
-    default: DCP_LNB(8);
+    case 1: DK_LNB(1); break;
+    case 2: DK_LNB(2); break;
+    case 4: DK_LNB(4); break;
+    default: DK_LNB(8);
   }
-#undef DCP_LNB
+#undef DK_LNB
 }
 
 inline int vpl_for(int D) {
@@ -313,10 +313,7 @@ int ln_bwd_blocks(int64_t rows) {
   // each workgroup writes one [2][D] partial row that ln_bwd_finalize_kernel
   // re-reads column-strided: 1024 workgroups made that 6 MB pass (17 µs at
   // BERT's 16384 x 768) cost more than the backward's own occupancy gain
-  static const int64_t cap = [] {
-    const char* v = getenv("DCP_LN_BWD_BLOCKS");
-    return v ? static_cast<int64_t>(atoll(v)) : int64_t(256);
-  }();
+  constexpr int64_t cap = 256;
   int64_t nb = (rows + 15) / 16;  // >= 16 rows (4 per wave) per workgroup
   if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;

@@ -473,7 +473,7 @@ inline dim3 grid_for(int64_t nchunks) {
 
 inline Tab tab_of(TableView t) { return Tab{t.base, t.n}; }
 
-#define DCP_DISPATCH_DTYPE(d, D, ...)        \
+#define DK_DISPATCH_DTYPE(d, D, ...)        \
   switch (d) {                               \
     case F32: { constexpr int D = F32; __VA_ARGS__; break; }  \
     case BF16: { constexpr int D = BF16; __VA_ARGS__; break; } \
@@ -491,7 +491,7 @@ void mt_copy(TableView t, int64_t nchunks, DType src, DType dst, float scale, hi
       hipLaunchKernelGGL((mt_rawcopy_kernel<2>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks);
     return;
   }
-  DCP_DISPATCH_DTYPE(src, SD, DCP_DISPATCH_DTYPE(dst, DD,
+  DK_DISPATCH_DTYPE(src, SD, DK_DISPATCH_DTYPE(dst, DD,
       hipLaunchKernelGGL((mt_copy_kernel<SD, DD>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks, scale)));
 }
 
@@ -499,7 +499,7 @@ void mt_sgd(TableView t, int64_t nchunks, DType p, float lr, float momentum, flo
             bool nesterov, bool maximize, bool first_step, bool has_buf, float grad_scale, hipStream_t s) {
   if (nchunks <= 0) return;
   SgdArgs a{lr, momentum, dampening, wd, grad_scale, nesterov, maximize, first_step, has_buf};
-  DCP_DISPATCH_DTYPE(p, PD,
+  DK_DISPATCH_DTYPE(p, PD,
       hipLaunchKernelGGL((mt_sgd_kernel<PD>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks, a));
 }
 
@@ -509,7 +509,7 @@ void mt_adam(TableView t, int64_t nchunks, DType p, float lr, float beta1, float
   if (nchunks <= 0) return;
   AdamArgs a{lr, beta1, beta2, eps, wd, bias_c1, bias_c2_sqrt, grad_scale, amsgrad, decoupled_wd, maximize, shadow,
              step_list};
-  DCP_DISPATCH_DTYPE(p, PD,
+  DK_DISPATCH_DTYPE(p, PD,
       hipLaunchKernelGGL((mt_adam_kernel<PD>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks, a));
 }
 
@@ -517,19 +517,19 @@ void mt_adadelta(TableView t, int64_t nchunks, DType p, float lr, float rho, flo
                  float grad_scale, hipStream_t s) {
   if (nchunks <= 0) return;
   AdadeltaArgs a{lr, rho, eps, wd, grad_scale, maximize};
-  DCP_DISPATCH_DTYPE(p, PD,
+  DK_DISPATCH_DTYPE(p, PD,
       hipLaunchKernelGGL((mt_adadelta_kernel<PD>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks, a));
 }
 
 void mt_sumsq(TableView t, int64_t nchunks, DType d, float* out, hipStream_t s) {
   if (nchunks <= 0) return;
-  DCP_DISPATCH_DTYPE(d, D,
+  DK_DISPATCH_DTYPE(d, D,
       hipLaunchKernelGGL((mt_sumsq_kernel<D>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks, out));
 }
 
 void mt_scale_by(TableView t, int64_t nchunks, DType d, const float* scale_dev, hipStream_t s) {
   if (nchunks <= 0) return;
-  DCP_DISPATCH_DTYPE(d, D,
+  DK_DISPATCH_DTYPE(d, D,
       hipLaunchKernelGGL((mt_scale_by_kernel<D>), grid_for(nchunks), dim3(kThreads), 0, s, tab_of(t), nchunks,
                          scale_dev));
 }
@@ -542,6 +542,38 @@ void copy_words(const int64_t* src, int64_t* dst, int64_t n, hipStream_t s) {
     for (int i = 0; i < m; ++i) a.w[i] = src[o + i];
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(kThreads), 0, s, a, dst + o, m);
   }
+}
+
+// ---------------------------------------------------- contention emulation ---
+// An all-reduce's footprint on THIS GPU without peers (bench.py
+// --emulate-world): `channels` workgroups (RCCL runs one per ring channel)
+// stream `bytes` through HBM (read src → write scratch, wrapping over the
+// buffers: ~2(N-1)/N × bucket bytes of an N-rank ring all-reduce) and then
+// hold their CU until `ticks` of the 100 MHz realtime counter have passed
+// since they started (the collective's wall time at a given bus bandwidth;
+// capped by the launcher). Bounded by construction: every wave leaves after
+// the copy and one deadline poll loop.
+__global__ void __launch_bounds__(kThreads) comm_emulate_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                               int64_t n16, int64_t per_block16, uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const int64_t begin = static_cast<int64_t>(blockIdx.x) * per_block16;
+  for (int64_t i = threadIdx.x; i < per_block16; i += kThreads) {
+    const int64_t k = (begin + i) % n16;
+    dst[k] = src[k];
+  }
+  // hold the CU for the rest of the collective's duration
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void comm_emulate(const void* src, void* scratch, int64_t bytes_buf, int64_t bytes_move, int channels, double us,
+                  hipStream_t s) {
+  if (bytes_buf < 16 || channels <= 0) return;
+  const int64_t n16 = bytes_buf / 16;
+  const int64_t per = (bytes_move / 16 + channels - 1) / channels;
+  double cap_us = us < 0 ? 0 : (us > 50000.0 ? 50000.0 : us);
+  const uint64_t ticks = static_cast<uint64_t>(cap_us * 100.0);  // 100 MHz realtime counter
+  hipLaunchKernelGGL(comm_emulate_kernel, dim3(channels), dim3(kThreads), 0, s, static_cast<const uint4*>(src),
+                     static_cast<uint4*>(scratch), n16, per, ticks);
 }
 
 }  // namespace kern

@@ -104,7 +104,7 @@ TableEntry get_table(const std::vector<const TensorList*>& lists) {
   } else {
     host = at::empty({static_cast<int64_t>(words.size())}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
     std::memcpy(host.data_ptr(), words.data(), words.size() * sizeof(int64_t));
-    DCP_CHECK(hipMemcpyAsync(d.data_ptr(), host.data_ptr(), words.size() * sizeof(int64_t), hipMemcpyHostToDevice,
+    DK_CHECK(hipMemcpyAsync(d.data_ptr(), host.data_ptr(), words.size() * sizeof(int64_t), hipMemcpyHostToDevice,
                              st) == hipSuccess,
               "table upload failed");
   }
@@ -134,15 +134,15 @@ TableEntry get_table(const std::vector<const TensorList*>& lists) {
 
 void check_lists(const std::vector<const TensorList*>& lists, const char* what) {
   const size_t n = lists[0]->size();
-  for (auto* l : lists) DCP_CHECK(l->size() == n, what, ": tensor lists differ in length");
+  for (auto* l : lists) DK_CHECK(l->size() == n, what, ": tensor lists differ in length");
   for (size_t i = 0; i < n; ++i) {
     const at::Tensor& ref = (*lists[0])[i];
-    DCP_CHECK(ref.is_non_overlapping_and_dense(), what, ": tensor ", i, " is not dense");
+    DK_CHECK(ref.is_non_overlapping_and_dense(), what, ": tensor ", i, " is not dense");
     for (auto* l : lists) {
       const at::Tensor& t = (*l)[i];
-      DCP_CHECK(t.numel() == ref.numel(), what, ": numel mismatch at ", i);
-      DCP_CHECK(t.device() == ref.device(), what, ": device mismatch at ", i);
-      DCP_CHECK(t.strides() == ref.strides() || t.is_contiguous() && ref.is_contiguous(), what,
+      DK_CHECK(t.numel() == ref.numel(), what, ": numel mismatch at ", i);
+      DK_CHECK(t.device() == ref.device(), what, ": device mismatch at ", i);
+      DK_CHECK(t.strides() == ref.strides() || t.is_contiguous() && ref.is_contiguous(), what,
                 ": stride mismatch at ", i, " (memory formats must agree)");
     }
   }
@@ -175,7 +175,7 @@ void mt_copy(const TensorList& src, const TensorList& dst, double scale) {
     // One launch per (src dtype, dst dtype) class; buckets are single-dtype.
     const auto sd = src[0].scalar_type(), dd = dst[0].scalar_type();
     for (size_t i = 0; i < src.size(); ++i)
-      DCP_CHECK(src[i].scalar_type() == sd && dst[i].scalar_type() == dd, "mt_copy: mixed dtypes in one call");
+      DK_CHECK(src[i].scalar_type() == sd && dst[i].scalar_type() == dd, "mt_copy: mixed dtypes in one call");
     c10::hip::HIPGuard guard(src[0].device().index());
     auto tab = get_table({&src, &dst});
     kern::mt_copy(kern::TableView{tab.dev.data_ptr<int64_t>(), tab.n}, tab.nchunks, kdtype(sd), kdtype(dd),
@@ -248,7 +248,7 @@ void fused_adam(const TensorList& params, const TensorList& grads, const TensorL
   if (shadow) {
     lists.push_back(&shadows);
     for (size_t i = 0; i < shadows.size(); ++i)
-      DCP_CHECK(shadows[i].scalar_type() == at::kBFloat16 && params[i].scalar_type() == at::kFloat &&
+      DK_CHECK(shadows[i].scalar_type() == at::kBFloat16 && params[i].scalar_type() == at::kFloat &&
                     shadows[i].is_contiguous() && params[i].is_contiguous(),
                 "fused_adam: shadows must be contiguous bf16 copies of contiguous fp32 params");
   }
@@ -258,9 +258,9 @@ void fused_adam(const TensorList& params, const TensorList& grads, const TensorL
   // sizes chunks by list 0 only, so 1-element rows are fine there)
   int step_list = -1;
   if (!steps.empty()) {
-    DCP_CHECK(steps.size() == params.size() && on_gpu(params), "fused_adam: steps must be one device tensor per param");
+    DK_CHECK(steps.size() == params.size() && on_gpu(params), "fused_adam: steps must be one device tensor per param");
     for (auto& t : steps)
-      DCP_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.numel() == 1 && t.device() == params[0].device(),
+      DK_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.numel() == 1 && t.device() == params[0].device(),
                 "fused_adam: each step must be a 1-element fp32 tensor on the parameters' device");
     step_list = static_cast<int>(lists.size());
     lists.push_back(&steps);
@@ -362,14 +362,14 @@ void fused_adadelta(const TensorList& params, const TensorList& grads, const Ten
 
 // ------------------------------------------------------------- grad norm ---
 at::Tensor sumsq(const TensorList& tensors) {
-  DCP_CHECK(!tensors.empty(), "sumsq: empty list");
+  DK_CHECK(!tensors.empty(), "sumsq: empty list");
   if (on_gpu(tensors)) {
     c10::hip::HIPGuard guard(tensors[0].device().index());
     at::Tensor out = at::zeros({2}, at::TensorOptions().dtype(at::kFloat).device(tensors[0].device()));
     // group by dtype
     std::map<at::ScalarType, TensorList> by;
     for (auto& t : tensors) {
-      DCP_CHECK(t.is_non_overlapping_and_dense(), "sumsq: dense tensors required");
+      DK_CHECK(t.is_non_overlapping_and_dense(), "sumsq: dense tensors required");
       by[t.scalar_type()].push_back(t);
     }
     for (auto& kv : by) {
@@ -396,7 +396,7 @@ void scale_by(const TensorList& tensors, const at::Tensor& scale) {
   if (tensors.empty()) return;
   if (on_gpu(tensors)) {
     c10::hip::HIPGuard guard(tensors[0].device().index());
-    DCP_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat, "scale_by: scale must be fp32 on device");
+    DK_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat, "scale_by: scale must be fp32 on device");
     std::map<at::ScalarType, TensorList> by;
     for (auto& t : tensors) by[t.scalar_type()].push_back(t);
     for (auto& kv : by) {

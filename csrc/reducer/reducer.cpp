@@ -28,8 +28,8 @@ std::vector<std::vector<int64_t>> compute_bucket_assignment(const std::vector<in
                                                             const std::vector<int64_t>& keys,
                                                             const std::vector<int64_t>& limits,
                                                             const std::vector<int64_t>& order) {
-  DCP_CHECK(sizes_bytes.size() == keys.size(), "planner: sizes/keys length mismatch");
-  DCP_CHECK(!limits.empty(), "planner: empty limit list");
+  DK_CHECK(sizes_bytes.size() == keys.size(), "planner: sizes/keys length mismatch");
+  DK_CHECK(!limits.empty(), "planner: empty limit list");
   struct Acc {
     std::vector<int64_t> idx;
     int64_t size = 0;
@@ -40,7 +40,7 @@ std::vector<std::vector<int64_t>> compute_bucket_assignment(const std::vector<in
   const size_t n = order.empty() ? sizes_bytes.size() : order.size();
   for (size_t k = 0; k < n; ++k) {
     const int64_t i = order.empty() ? static_cast<int64_t>(k) : order[k];
-    DCP_CHECK(i >= 0 && i < static_cast<int64_t>(sizes_bytes.size()), "planner: bad index ", i);
+    DK_CHECK(i >= 0 && i < static_cast<int64_t>(sizes_bytes.size()), "planner: bad index ", i);
     const int64_t key = keys[i];
     Acc& b = open[key];
     b.idx.push_back(i);
@@ -96,8 +96,8 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
                  std::shared_ptr<Communicator> comm, ReducerOptions opts)
     : params_(std::move(params)), comm_(std::move(comm)), opts_(opts) {
   for (auto& p : params_) {
-    DCP_CHECK(p.requires_grad(), "Reducer: every parameter must require grad");
-    DCP_CHECK(p.is_non_overlapping_and_dense(), "Reducer: parameters must be dense");
+    DK_CHECK(p.requires_grad(), "Reducer: every parameter must require grad");
+    DK_CHECK(p.is_non_overlapping_and_dense(), "Reducer: parameters must be dense");
   }
   ready_.assign(params_.size(), 0);
   unused_.assign(params_.size(), 0);
@@ -108,7 +108,7 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
   const char* ds = std::getenv("DCP_DEBUG_STREAMS");
   check_ = opts_.check_streams || (ds && std::strcmp(ds, "1") == 0);
   if (timing_) {
-    DCP_CHECK(hipEventCreate(&ev_bwd_end_) == hipSuccess && hipEventCreate(&ev_final_) == hipSuccess,
+    DK_CHECK(hipEventCreate(&ev_bwd_end_) == hipSuccess && hipEventCreate(&ev_final_) == hipSuccess,
               "Reducer: event creation failed");
   }
 }
@@ -137,15 +137,15 @@ void Reducer::build_buckets(const std::vector<std::vector<int64_t>>& assignment)
   where_.assign(params_.size(), {-1, -1});
   for (size_t bi = 0; bi < assignment.size(); ++bi) {
     const auto& idx = assignment[bi];
-    DCP_CHECK(!idx.empty(), "Reducer: empty bucket");
+    DK_CHECK(!idx.empty(), "Reducer: empty bucket");
     Bucket b;
     b.params = idx;
     const at::Tensor& p0 = params_[idx[0]];
     int64_t total = 0;
     for (int64_t i : idx) {
-      DCP_CHECK(i >= 0 && i < static_cast<int64_t>(params_.size()) && !seen[i], "Reducer: bad bucket index ", i);
+      DK_CHECK(i >= 0 && i < static_cast<int64_t>(params_.size()) && !seen[i], "Reducer: bad bucket index ", i);
       seen[i] = 1;
-      DCP_CHECK(params_[i].scalar_type() == p0.scalar_type() && params_[i].device() == p0.device(),
+      DK_CHECK(params_[i].scalar_type() == p0.scalar_type() && params_[i].device() == p0.device(),
                 "Reducer: a bucket must be single dtype/device");
       b.offsets.push_back(total);
       total += params_[i].numel();
@@ -166,7 +166,7 @@ void Reducer::build_buckets(const std::vector<std::vector<int64_t>>& assignment)
     b.stats.num_params = static_cast<int64_t>(idx.size());
     out.push_back(std::move(b));
   }
-  for (size_t i = 0; i < params_.size(); ++i) DCP_CHECK(seen[i], "Reducer: parameter ", i, " not in any bucket");
+  for (size_t i = 0; i < params_.size(); ++i) DK_CHECK(seen[i], "Reducer: parameter ", i, " not in any bucket");
   buckets_ = std::move(out);
   next_bucket_ = 0;
 }
@@ -175,7 +175,7 @@ void Reducer::register_hooks() {
   std::weak_ptr<Reducer> weak = shared_from_this();
   for (size_t i = 0; i < params_.size(); ++i) {
     auto acc = torch::autograd::impl::grad_accumulator(params_[i]);
-    DCP_CHECK(acc, "Reducer: parameter ", i, " has no grad accumulator (not a leaf?)");
+    DK_CHECK(acc, "Reducer: parameter ", i, " has no grad accumulator (not a leaf?)");
     const int64_t idx = static_cast<int64_t>(i);
     auto handle = acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
         [weak, idx](const torch::autograd::variable_list& outputs, const torch::autograd::variable_list&) {
@@ -194,7 +194,7 @@ void Reducer::set_expect_backward(bool v) {
 
 void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs, bool require_sync) {
   std::lock_guard<std::mutex> g(mu_);
-  DCP_CHECK(!finalize_queued_, "Reducer: forward called while a backward reduction is still in progress");
+  DK_CHECK(!finalize_queued_, "Reducer: forward called while a backward reduction is still in progress");
   expect_hooks_ = require_sync;
   if (!require_sync) return;
   unused_list_.clear();
@@ -261,7 +261,7 @@ void Reducer::autograd_hook(int64_t index) {
 }
 
 void Reducer::mark_ready(int64_t i, bool unused) {
-  DCP_CHECK(!ready_[i], "Reducer: parameter ", i,
+  DK_CHECK(!ready_[i], "Reducer: parameter ", i,
             " was marked ready twice in one backward (reentrant backward / shared parameters across "
             "checkpointed regions are not supported; or find_unused_parameters misclassified it)");
   ready_[i] = 1;
@@ -335,11 +335,12 @@ void Reducer::launch(Bucket& b) {
   trace::Range r("dcp.reducer.bucket_allreduce");
   const bool check = check_ && !capturing(b.wire);
   if (check) {
-    // packed-buffer checksum, taken BEFORE the bucket's collective is issued:
-    // that collective reduces b.wire in place (on the comm stream after an
-    // event recorded now, or on the host communicator's worker), so a
-    // checksum enqueued after it would race with the reduction
-    b.check_sum = b.wire.to(at::kDouble).sum().reshape({1}).to(at::kFloat);
+    // packed-buffer checksum (Σx, Σ|x|), taken BEFORE the bucket's collective
+    // is issued: that collective reduces b.wire in place (on the comm stream
+    // after an event recorded now, or on the host communicator's worker), so
+    // a checksum enqueued after it would race with the reduction
+    const at::Tensor w = b.wire.to(at::kDouble);
+    b.check_sum = at::stack({w.sum(), w.abs().sum()}).to(at::kFloat);
   }
   if (comm_hook_) {
     b.work = comm_hook_(b.wire, static_cast<int64_t>(&b - buckets_.data()));
@@ -394,8 +395,16 @@ void Reducer::finalize() {
       b.check_work->wait();
       // what the compute stream sees now vs what the collective must have produced
       const double seen = b.wire.to(at::kDouble).sum().item<double>();
-      const double want = b.check_sum.to(at::kDouble).item<double>();
-      const double tol = 1e-3 * std::max(1.0, std::fabs(want)) + 1e-6 * static_cast<double>(b.wire.numel());
+      const at::Tensor cs = b.check_sum.to(at::kDouble).cpu();
+      const double want = cs[0].item<double>(), mag = cs[1].item<double>();
+      // rounding of the reduction itself scales with the wire dtype's epsilon
+      // times the magnitude summed (a near-zero Σx of large terms is not an
+      // ordering error): bf16 wire ~8e-3, fp32 ~1e-7 per add, ~world adds
+      const at::ScalarType wdt =
+          comm_hook_ && hook_wire_ != at::ScalarType::Undefined ? hook_wire_ : b.wire.scalar_type();
+      const double eps = wdt == at::kBFloat16 ? 7.8125e-3 : wdt == at::kHalf ? 9.77e-4 : 1.19e-7;
+      const double tol = (comm_->size() + 2) * eps * mag + 1e-6 * std::max(1.0, std::fabs(want)) +
+                         1e-6 * static_cast<double>(b.wire.numel());
       b.check_work.reset();
       if (!(std::fabs(seen - want) <= tol)) {
         const int64_t k = static_cast<int64_t>(&b - buckets_.data());
@@ -475,7 +484,7 @@ void Reducer::launch_used_map_reduce() {
     hipStream_t cur = c10::hip::getCurrentHIPStream(params_[0].device().index()).stream();
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(cur, &cap);
-    DCP_CHECK(cap == hipStreamCaptureStatusNone,
+    DK_CHECK(cap == hipStreamCaptureStatusNone,
               "find_unused_parameters=True cannot be used inside HIP-graph capture (the used-parameter map "
               "is read on the host at the end of every backward)");
   }
@@ -484,7 +493,7 @@ void Reducer::launch_used_map_reduce() {
     used_host_ = at::empty({n}, host);
     used_back_ = at::empty({n}, host);
     used_dev_ = cuda ? at::empty({n}, params_[0].options().dtype(at::kInt).requires_grad(false)) : used_host_;
-    if (cuda) DCP_CHECK(hipEventCreateWithFlags(&used_ev_, hipEventDisableTiming) == hipSuccess, "event create");
+    if (cuda) DK_CHECK(hipEventCreateWithFlags(&used_ev_, hipEventDisableTiming) == hipSuccess, "event create");
   }
   // The previous iteration's finalize waited for used_ev_, which follows the
   // H2D copy of used_host_: rewriting it now cannot race that copy.
@@ -502,7 +511,7 @@ void Reducer::launch_used_map_reduce() {
   used_work_->wait();
   used_back_.copy_(used_dev_, /*non_blocking=*/true);
   hipStream_t s = c10::hip::getCurrentHIPStream(params_[0].device().index()).stream();
-  DCP_CHECK(hipEventRecord(used_ev_, s) == hipSuccess, "event record");
+  DK_CHECK(hipEventRecord(used_ev_, s) == hipSuccess, "event record");
 }
 
 std::vector<char> Reducer::collect_global_used() {
@@ -515,7 +524,7 @@ std::vector<char> Reducer::collect_global_used() {
       if (!comm_->error().empty()) throw Error("Reducer: communicator failed: " + comm_->error());
       hipError_t e = hipEventQuery(used_ev_);
       if (e == hipSuccess) break;
-      DCP_CHECK(e == hipErrorNotReady, "hipEventQuery failed: ", hipGetErrorString(e));
+      DK_CHECK(e == hipErrorNotReady, "hipEventQuery failed: ", hipGetErrorString(e));
       std::this_thread::sleep_for(std::chrono::microseconds(10));
     }
     const int32_t* h = used_back_.data_ptr<int32_t>();

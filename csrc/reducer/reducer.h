@@ -94,7 +94,13 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void set_expect_backward(bool v);
 
   // Custom comm hook (runs on the autograd thread with the bucket buffer).
-  void set_comm_hook(CommHook hook) { comm_hook_ = std::move(hook); }
+  // wire_dtype: the precision the hook's collective carries (a compression
+  // hook declares bf16 / fp16; Undefined = the bucket's own dtype) — it sets
+  // the rounding the debug stream-ordering check tolerates
+  void set_comm_hook(CommHook hook, at::ScalarType wire_dtype = at::ScalarType::Undefined) {
+    comm_hook_ = std::move(hook);
+    hook_wire_ = wire_dtype;
+  }
 
   std::vector<std::vector<int64_t>> bucket_indices() const;
   std::vector<int64_t> bucket_sizes_bytes() const;
@@ -145,6 +151,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::shared_ptr<Communicator> comm_;
   ReducerOptions opts_;
   CommHook comm_hook_;
+  at::ScalarType hook_wire_ = at::ScalarType::Undefined;
 
   std::vector<Bucket> buckets_;
   std::vector<std::pair<int64_t, int64_t>> where_;  // param -> (bucket, slot)

@@ -23,7 +23,7 @@ at::Tensor empty_nhwc(int64_t n, int64_t c, int64_t h, int64_t w, const at::Tens
 }
 
 void check_act(const at::Tensor& t, const char* what) {
-  DCP_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && is_nhwc(t), what,
+  DK_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && is_nhwc(t), what,
             ": expected a channels_last bf16 device tensor");
 }
 
@@ -38,7 +38,7 @@ bool supported(const at::Tensor& x, int64_t cout) {
 
 // image -> (Xp [N][H+6][W+8][4] bf16, x3 [N,3,H,W] bf16 channels_last or empty)
 std::vector<at::Tensor> prep(const at::Tensor& x, bool want_x3) {
-  DCP_CHECK(supported(x, 64), "stem_prep: unsupported input");
+  DK_CHECK(supported(x, 64), "stem_prep: unsupported input");
   c10::hip::HIPGuard g(x.device().index());
   const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
   at::Tensor xp = at::empty({N, kern::stem_hp(static_cast<int>(H)), kern::stem_wp(static_cast<int>(W)), 4},
@@ -53,7 +53,7 @@ std::vector<at::Tensor> prep(const at::Tensor& x, bool want_x3) {
 
 // conv weight (fp32 [Cout,3,7,7], contiguous or channels_last) -> GEMM operand bf16 [Cout][256]
 at::Tensor weight(const at::Tensor& w) {
-  DCP_CHECK(w.is_cuda() && w.dim() == 4 && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
+  DK_CHECK(w.is_cuda() && w.dim() == 4 && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
                 w.scalar_type() == at::kFloat && (w.is_contiguous() || is_nhwc(w)),
             "stem_weight: expected fp32 [Cout,3,7,7]");
   c10::hip::HIPGuard g(w.device().index());
@@ -65,11 +65,11 @@ at::Tensor weight(const at::Tensor& w) {
 
 // (y [N,Cout,H/2,W/2] bf16 channels_last, stats fp32 [2*Cout] = (Σy, Σy²))
 std::vector<at::Tensor> conv_fwd(const at::Tensor& xp, const at::Tensor& wm, int64_t H, int64_t W) {
-  DCP_CHECK(xp.is_cuda() && xp.scalar_type() == at::kBFloat16 && xp.dim() == 4 && xp.size(3) == 4 &&
+  DK_CHECK(xp.is_cuda() && xp.scalar_type() == at::kBFloat16 && xp.dim() == 4 && xp.size(3) == 4 &&
                 xp.size(1) == kern::stem_hp(static_cast<int>(H)) && xp.size(2) == kern::stem_wp(static_cast<int>(W)) &&
                 xp.is_contiguous(),
             "stem_conv_fwd: Xp must come from stem_prep for this H, W");
-  DCP_CHECK(wm.is_cuda() && wm.scalar_type() == at::kBFloat16 && wm.dim() == 2 && wm.size(1) == kern::kStemK &&
+  DK_CHECK(wm.is_cuda() && wm.scalar_type() == at::kBFloat16 && wm.dim() == 2 && wm.size(1) == kern::kStemK &&
                 wm.size(0) % 64 == 0 && wm.is_contiguous(),
             "stem_conv_fwd: wm must come from stem_weight");
   c10::hip::HIPGuard g(xp.device().index());
@@ -85,12 +85,12 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& xp, const at::Tensor& wm, int
 // -> dW fp32 [Cout,3,7,7] (contiguous)
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& xp, int64_t H, int64_t W) {
   check_act(dy, "stem_conv_wgrad(dy)");
-  DCP_CHECK(xp.is_cuda() && xp.scalar_type() == at::kBFloat16 && xp.dim() == 4 && xp.size(3) == 4 &&
+  DK_CHECK(xp.is_cuda() && xp.scalar_type() == at::kBFloat16 && xp.dim() == 4 && xp.size(3) == 4 &&
                 xp.size(1) == kern::stem_hp(static_cast<int>(H)) && xp.size(2) == kern::stem_wp(static_cast<int>(W)) &&
                 xp.is_contiguous() && xp.size(0) == dy.size(0),
             "stem_conv_wgrad: xp must come from stem_prep for this H, W");
   const int64_t N = dy.size(0), Cout = dy.size(1);
-  DCP_CHECK(dy.size(2) == H / 2 && dy.size(3) == W / 2 && Cout % 64 == 0, "stem_conv_wgrad: dy shape mismatch");
+  DK_CHECK(dy.size(2) == H / 2 && dy.size(3) == W / 2 && Cout % 64 == 0, "stem_conv_wgrad: dy shape mismatch");
   c10::hip::HIPGuard g(dy.device().index());
   const int64_t M = N * (H / 2) * (W / 2);
   auto fo = dy.options().dtype(at::kFloat);
@@ -110,16 +110,16 @@ std::vector<at::Tensor> bn_pool_fwd(const at::Tensor& y, const at::Tensor& stats
                                     double eps) {
   check_act(y, "stem_bn_pool_fwd");
   const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
-  DCP_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "stem_bn_pool_fwd: C/8 must divide 256");
-  DCP_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 2 * C, "stem_bn_pool_fwd: stats [2C] fp32");
-  DCP_CHECK(gamma.scalar_type() == at::kFloat && beta.scalar_type() == at::kFloat && gamma.numel() == C &&
+  DK_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "stem_bn_pool_fwd: C/8 must divide 256");
+  DK_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 2 * C, "stem_bn_pool_fwd: stats [2C] fp32");
+  DK_CHECK(gamma.scalar_type() == at::kFloat && beta.scalar_type() == at::kFloat && gamma.numel() == C &&
                 beta.numel() == C,
             "stem_bn_pool_fwd: fp32 gamma / beta [C]");
   c10::hip::HIPGuard g(y.device().index());
   const int64_t OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  DCP_CHECK(N * OH * OW * (C / 8) < (int64_t(1) << 31) && N * H * W * C < (int64_t(1) << 31) * 8,
+  DK_CHECK(N * OH * OW * (C / 8) < (int64_t(1) << 31) && N * H * W * C < (int64_t(1) << 31) * 8,
             "stem_bn_pool_fwd: tensor too large for 32-bit thread indexing");
-  DCP_CHECK(2 * OH >= H && 2 * OW >= W, "stem_bn_pool_fwd: pooled map must cover the input (k3 s2 p1)");
+  DK_CHECK(2 * OH >= H && 2 * OW >= W, "stem_bn_pool_fwd: pooled map must cover the input (k3 s2 p1)");
   at::Tensor out = empty_nhwc(N, C, OH, OW, y, at::kBFloat16);
   at::Tensor xsel = empty_nhwc(N, C, OH, OW, y, at::kBFloat16);
   at::Tensor idx = at::empty({N, OH, OW, C}, y.options().dtype(at::kByte));
@@ -148,11 +148,11 @@ std::vector<at::Tensor> bn_pool_bwd(const at::Tensor& gp, const c10::optional<at
   const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
   const int64_t OH = xsel.size(2), OW = xsel.size(3);
   at::Tensor g1 = gp.contiguous(at::MemoryFormat::ChannelsLast);
-  DCP_CHECK(g1.scalar_type() == at::kBFloat16 && g1.sizes() == xsel.sizes(), "stem_bn_pool_bwd: gp mismatch");
+  DK_CHECK(g1.scalar_type() == at::kBFloat16 && g1.sizes() == xsel.sizes(), "stem_bn_pool_bwd: gp mismatch");
   at::Tensor g2;
   if (gp2_opt.has_value() && gp2_opt->defined()) {
     g2 = gp2_opt->contiguous(at::MemoryFormat::ChannelsLast);
-    DCP_CHECK(g2.scalar_type() == at::kBFloat16 && g2.sizes() == xsel.sizes(), "stem_bn_pool_bwd: gp2 mismatch");
+    DK_CHECK(g2.scalar_type() == at::kBFloat16 && g2.sizes() == xsel.sizes(), "stem_bn_pool_bwd: gp2 mismatch");
   }
   c10::hip::HIPGuard g(y.device().index());
   auto fo = y.options().dtype(at::kFloat);

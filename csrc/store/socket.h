@@ -51,7 +51,7 @@ inline std::string resolve_ipv4(const std::string& host) {
   hints.ai_socktype = SOCK_STREAM;
   addrinfo* res = nullptr;
   int rc = ::getaddrinfo(host.c_str(), nullptr, &hints, &res);
-  DCP_CHECK(rc == 0 && res != nullptr, "cannot resolve host '", host, "': ", gai_strerror(rc));
+  DK_CHECK(rc == 0 && res != nullptr, "cannot resolve host '", host, "': ", gai_strerror(rc));
   char buf[INET_ADDRSTRLEN];
   ::inet_ntop(AF_INET, &reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr, buf, sizeof(buf));
   ::freeaddrinfo(res);
@@ -61,7 +61,7 @@ inline std::string resolve_ipv4(const std::string& host) {
 // Bind + listen on host:port (port 0 = ephemeral). Returns fd; *bound_port gets the port.
 inline int listen_on(const std::string& host, int port, int* bound_port, int backlog = 512) {
   int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-  DCP_CHECK(fd >= 0, "socket() failed: ", std::strerror(errno));
+  DK_CHECK(fd >= 0, "socket() failed: ", std::strerror(errno));
   int one = 1;
   ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
   sockaddr_in addr{};
@@ -74,7 +74,7 @@ inline int listen_on(const std::string& host, int port, int* bound_port, int bac
     ::close(fd);
     throw Error(str_cat("bind(", ip, ":", port, ") failed: ", std::strerror(e)));
   }
-  DCP_CHECK(::listen(fd, backlog) == 0, "listen() failed: ", std::strerror(errno));
+  DK_CHECK(::listen(fd, backlog) == 0, "listen() failed: ", std::strerror(errno));
   socklen_t len = sizeof(addr);
   ::getsockname(fd, reinterpret_cast<sockaddr*>(&addr), &len);
   if (bound_port) *bound_port = ntohs(addr.sin_port);
@@ -92,7 +92,7 @@ inline int connect_to(const std::string& host, int port, int64_t timeout_ms) {
   int delay_ms = 2;
   while (true) {
     int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    DCP_CHECK(fd >= 0, "socket() failed: ", std::strerror(errno));
+    DK_CHECK(fd >= 0, "socket() failed: ", std::strerror(errno));
     if (::connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) == 0) {
       set_nodelay(fd);
       return fd;
@@ -111,9 +111,9 @@ inline int accept_one(int listen_fd, int64_t timeout_ms) {
   pollfd p{listen_fd, POLLIN, 0};
   int rc = ::poll(&p, 1, timeout_ms < 0 ? -1 : static_cast<int>(timeout_ms));
   if (rc == 0) throw TimeoutError("timed out waiting for peer connection");
-  DCP_CHECK(rc > 0, "poll() failed: ", std::strerror(errno));
+  DK_CHECK(rc > 0, "poll() failed: ", std::strerror(errno));
   int fd = ::accept(listen_fd, nullptr, nullptr);
-  DCP_CHECK(fd >= 0, "accept() failed: ", std::strerror(errno));
+  DK_CHECK(fd >= 0, "accept() failed: ", std::strerror(errno));
   set_nodelay(fd);
   return fd;
 }

@@ -94,7 +94,7 @@ void TCPStoreServer::serve(int fd) {
     try {
       switch (cmd) {
         case SET: {
-          DCP_CHECK(args.size() == 2, "SET arity");
+          DK_CHECK(args.size() == 2, "SET arity");
           {
             std::lock_guard<std::mutex> g(mu_);
             kv_[args[0]] = args[1];
@@ -104,7 +104,7 @@ void TCPStoreServer::serve(int fd) {
         }
         case GET:
         case WAIT: {
-          DCP_CHECK(!args.empty(), "GET/WAIT arity");
+          DK_CHECK(!args.empty(), "GET/WAIT arity");
           const int64_t timeout_ms = std::stoll(args.back());
           const size_t nkeys = args.size() - 1;
           std::unique_lock<std::mutex> lk(mu_);
@@ -124,7 +124,7 @@ void TCPStoreServer::serve(int fd) {
           break;
         }
         case ADD: {
-          DCP_CHECK(args.size() == 2, "ADD arity");
+          DK_CHECK(args.size() == 2, "ADD arity");
           int64_t v;
           {
             std::lock_guard<std::mutex> g(mu_);
@@ -145,7 +145,7 @@ void TCPStoreServer::serve(int fd) {
           break;
         }
         case DEL: {
-          DCP_CHECK(args.size() == 1, "DEL arity");
+          DK_CHECK(args.size() == 1, "DEL arity");
           std::lock_guard<std::mutex> g(mu_);
           reply = kv_.erase(args[0]) ? "1" : "0";
           break;
@@ -156,7 +156,7 @@ void TCPStoreServer::serve(int fd) {
           break;
         }
         case CAS: {
-          DCP_CHECK(args.size() == 3, "CAS arity");
+          DK_CHECK(args.size() == 3, "CAS arity");
           {
             std::lock_guard<std::mutex> g(mu_);
             auto it = kv_.find(args[0]);
@@ -223,15 +223,15 @@ std::string TCPStore::request(uint8_t cmd, const std::vector<std::string>& args,
     buf.append(reinterpret_cast<const char*>(&len), sizeof(len));
     buf.append(a);
   }
-  DCP_CHECK(net::send_all(fd_, buf.data(), buf.size()), "store: connection to server lost (send)");
+  DK_CHECK(net::send_all(fd_, buf.data(), buf.size()), "store: connection to server lost (send)");
   uint8_t status = 0;
   // Allow the server side timeout to fire first, then a grace period.
   const int64_t wait = timeout_ms < 0 ? -1 : timeout_ms + 5000;
-  DCP_CHECK(net::recv_all(fd_, &status, 1, wait), "store: connection to server lost (recv)");
+  DK_CHECK(net::recv_all(fd_, &status, 1, wait), "store: connection to server lost (recv)");
   uint64_t len = 0;
-  DCP_CHECK(net::recv_all(fd_, &len, sizeof(len), wait), "store: connection lost");
+  DK_CHECK(net::recv_all(fd_, &len, sizeof(len), wait), "store: connection lost");
   std::string payload(len, '\0');
-  if (len) DCP_CHECK(net::recv_all(fd_, &payload[0], len, wait), "store: connection lost");
+  if (len) DK_CHECK(net::recv_all(fd_, &payload[0], len, wait), "store: connection lost");
   if (status == TIMEOUT) throw TimeoutError("store: timed out waiting for key(s)");
   if (status != OK) throw Error("store: server error: " + payload);
   return payload;

@@ -13,7 +13,6 @@ one write per activation in the forward, statistics fused).
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Type
 
 import torch
@@ -21,37 +20,34 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d, bn_resbn_act, resbn_ok
 from ..ops.conv import (ConvWeightPrep, bn_relu_conv, bn_relu_conv1x1, bn_res_act_conv1x1, conv1x1 as gemm_conv1x1,
-                        conv_kxk, conv_kxk_gemm, conv_kxk_gemm_ok, conv_kxk_ok, gemm_ok, kxk_policy,
-                        res_conv_fuse_ok)
+                        conv_kxk_gemm, conv_kxk_gemm_ok, gemm_ok, res_conv_fuse_ok)
 from ..ops.pool import FusedMaxPool2d, global_avg_pool_flat
 from ..ops.stem import fused_stem, stem_supported
 
 
-GEMM_MAX_INTENSITY = float(os.environ.get("DCP_GEMM_MAX_INTENSITY", "1024"))
-KXK_WGRAD = os.environ.get("DCP_KXK_WGRAD", "0") == "1"
-# 3x3 conv2 on the implicit-GEMM MFMA kernels (fwd + BN2 sums, stride-1 dgrad)
-KXK_GEMM = os.environ.get("DCP_KXK_GEMM", "1") == "1"
+# Fusion table of the fused ResNet path (plain constants, no environment
+# switches: the A/B history of each entry is in NOTES.md / profiles/; tests
+# monkeypatch them to check every fused path against the unfused one).
+#
 # BN1→conv2 / BN2→conv3 as one autograd node whose data-gradient GEMM reduces
 # the BN backward in its epilogue (gemm.hip RED). Bit mask: 1 = BN1→conv2
 # (stride-1 3x3 on the gathered GEMM, Cin > 64), 2 = BN2→conv3 (1x1, the wide
 # layers whose BN2 is not a GEMM prologue), 4 = BN1→conv2 for Cin = 64 (layer 1:
-# the direct 3x3 kernel's RED epilogue). Round 1 measured both −1 % (the RED
-# coefficients in LDS pushed the GEMM to one workgroup per CU); round 2 with
-# them in registers (profiles/r2_ab_bn_conv_fuse.jsonl): 2 = +0.3 %, 1 = −0.8 %;
-# after the epilogue scratch fix (NOTES §20) 1 turned +0.55 % and 4 +0.27 %:
-# default 7 (profiles/r2_ab_bn_conv_fuse7.jsonl, r2_ab_bn1_red_c64.jsonl).
-BN_CONV_FUSE = int(os.environ.get("DCP_BN_CONV_FUSE", "7") or 0)
-# BN-apply prologue in the conv3 GEMM only while Cout ≤ this (≤ 2 N-tiles of 128)
-PRO_MAX_COUT = int(os.environ.get("DCP_PRO_MAX_COUT", "256"))
-# conv1 + bn1 + relu + maxpool as one fused node (ops/stem.py); 0 = per-module path
-FUSED_STEM = os.environ.get("DCP_STEM", "1") == "1"
+# the direct 3x3 kernel's RED epilogue): +0.55 % / +0.3 % / +0.27 %
+# (profiles/r2_ab_bn_conv_fuse7.jsonl, r2_ab_bn_conv_fuse.jsonl, r2_ab_bn1_red_c64.jsonl).
+BN_CONV_FUSE = 7
+# BN-apply prologue in the conv3 GEMM only while Cout ≤ this (≤ 2 N-tiles of
+# 128; 512 measured neutral, profiles/r2_ab_pro_max_cout.jsonl)
+PRO_MAX_COUT = 256
+# conv1 + bn1 + relu + maxpool as one fused node (ops/stem.py); False = per-module path
+FUSED_STEM = True
 # every bottleneck conv's bf16 operands from ONE launch per forward (ops/conv.py ConvWeightPrep)
-WEIGHT_PREP = os.environ.get("DCP_WEIGHT_PREP", "1") == "1"
+WEIGHT_PREP = True
 # downsample BN applied inside BN3's residual kernel (its output never written)
-RESBN = os.environ.get("DCP_RESBN", "1") == "1"
+RESBN = True
 # each block's BN3 + residual + ReLU and the NEXT block's conv1 as one autograd
 # node: BN3's backward reduction runs in conv1's data-gradient epilogue
-RES_CONV_FUSE = os.environ.get("DCP_RES_CONV_FUSE", "1") == "1"
+RES_CONV_FUSE = True
 
 
 def conv3x3(cin, cout, stride=1):
@@ -116,12 +112,6 @@ class Bottleneck(nn.Module):
     def _gemm_path(self, x: torch.Tensor) -> bool:
         if not (self.fused_gemm and self.training and self.bn1.fused and self.bn2.fused and self.bn3.fused):
             return False
-        # optional cut-off on the 1x1 convs' FLOP/byte (≈ Cin·Cout/(Cin+Cout); ResNet-50:
-        # 51 / 102 / 205 / 410 for layers 1-4). Default 1024: every stage — with the
-        # split-M wgrad all four stages measured faster than MIOpen (r1_bench_gemm_*)
-        w, c = self.conv3.in_channels, self.conv3.out_channels
-        if w * c / (w + c) > GEMM_MAX_INTENSITY:
-            return False
         return (gemm_ok(x, self.conv1.in_channels, self.conv1.out_channels)
                 and self.conv3.out_channels % 64 == 0 and self.conv3.in_channels % 64 == 0)
 
@@ -139,7 +129,7 @@ class Bottleneck(nn.Module):
             z = st = None
             if conv.stride == (1, 1) and gemm_ok(inp, conv.in_channels, conv.out_channels):
                 z, st = gemm_conv1x1(inp, conv.weight, stats=True)
-            elif KXK_GEMM and conv_kxk_gemm_ok(inp, conv):
+            elif conv_kxk_gemm_ok(inp, conv):
                 # strided 1x1: gathered implicit GEMM (+ BN sums); dgrad on MIOpen
                 z, st = conv_kxk_gemm(inp, conv.weight, conv.stride[0], conv.padding[0], stats=True)
             if z is None:
@@ -154,21 +144,14 @@ class Bottleneck(nn.Module):
         c2 = self.conv2
         s2 = None
         fuse3 = bool(BN_CONV_FUSE & 2)
-        if (KXK_GEMM and conv_kxk_gemm_ok(z1, c2) and c2.stride == (1, 1)
+        if (conv_kxk_gemm_ok(z1, c2) and c2.stride == (1, 1)
                 and ((BN_CONV_FUSE & 1 and c2.in_channels > 64) or (BN_CONV_FUSE & 4 and c2.in_channels == 64))):
             x2, s2 = bn_relu_conv(z1, self.bn1, c2.weight, c2.kernel_size[0], c2.stride[0], c2.padding[0], sums=s1,
                                   stats=True)
             return self._tail(x2, s2, identity, dual, fuse3, resbn, nxt)
         y1 = self.bn1(z1, stats=s1)
-        if KXK_GEMM and conv_kxk_gemm_ok(y1, c2):
-            ho = (y1.shape[2] + 2 * c2.padding[0] - c2.kernel_size[0]) // c2.stride[0] + 1
-            mi_fwd, mi_wgrad = kxk_policy(c2.in_channels, c2.out_channels, ho, c2.stride[0])
-            x2, s2 = conv_kxk_gemm(y1, c2.weight, c2.stride[0], c2.padding[0], stats=not mi_fwd,
-                                   miopen_wgrad=mi_wgrad, miopen_fwd=mi_fwd)
-            if mi_fwd:
-                s2 = None
-        elif KXK_WGRAD and conv_kxk_ok(y1, c2):
-            x2 = conv_kxk(y1, c2.weight, c2.stride[0], c2.padding[0])
+        if conv_kxk_gemm_ok(y1, c2):
+            x2, s2 = conv_kxk_gemm(y1, c2.weight, c2.stride[0], c2.padding[0], stats=True)
         else:
             x2 = c2(y1)
         if not x2.is_contiguous(memory_format=torch.channels_last):

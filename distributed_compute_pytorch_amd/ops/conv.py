@@ -18,7 +18,6 @@ reference framework's cuDNN/cuBLAS role).
 """
 from __future__ import annotations
 
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -74,43 +73,6 @@ class ConvWeightPrep:
                 and w.permute(0, 2, 3, 1).is_contiguous())
 
 
-# Weight gradient on a side stream, concurrent with the same node's data-
-# gradient GEMM, for GEMMs of at most this many rows (0 = off): the compute-
-# bound layer-3/4 GEMMs end in a partial round of tiles that the other
-# kernel's workgroups can fill.
-WGRAD_SIDE_MAXM = int(os.environ.get("DCP_WGRAD_SIDE_MAXM", "0") or 0)
-_SIDE_STREAMS = {}
-
-
-def _noop():
-    return None
-
-
-def _wgrad_async(rows: int, fn, *inputs):
-    """``fn()`` (a weight-gradient launch reading ``inputs``) on the device's
-    side stream when ``rows <= WGRAD_SIDE_MAXM``: returns (result, join) —
-    ``join()`` makes the current stream wait for it (call before returning
-    the gradient to autograd). Capture-safe (event fork / join)."""
-    if rows > WGRAD_SIDE_MAXM or not inputs[0].is_cuda:
-        return fn(), _noop
-    dev = inputs[0].device
-    main = torch.cuda.current_stream(dev)
-    side = _SIDE_STREAMS.get(dev.index)
-    if side is None:
-        side = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        out = fn()
-    for t in inputs:
-        t.record_stream(side)
-
-    def join():
-        main.wait_stream(side)
-        out.record_stream(main)
-
-    return out, join
-
-
 def _prepped(weight: torch.Tensor):
     return _PREPPED.get(weight) if _PREPPED else None
 
@@ -158,8 +120,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, dw, None
 
 
-# BN-prologue 1x1 conv (ResNet layer-1 conv3): BN backward reduce in the dgrad epilogue
-_PRO_RED = os.environ.get("DCP_PRO_RED", "1") == "1"
+# BN-prologue 1x1 conv (ResNet layer-1 conv3): BN backward reduce in the dgrad
+# epilogue (+0.6 %, profiles/r2_ab_pro_red.jsonl; False = separate reduce pass)
+_PRO_RED = True
 
 
 class _BNReluConv1x1Fn(torch.autograd.Function):
@@ -216,8 +179,9 @@ def bn_relu_conv1x1(x: torch.Tensor, bn, weight: torch.Tensor, stats: bool = Fal
                                   bn.eps, stats, sums)
 
 
-# downsample blocks: BN3's and the downsample BN's apply passes as one kernel (g read once)
-_APPLY2 = os.environ.get("DCP_BN_APPLY2", "1") == "1"
+# downsample blocks: BN3's and the downsample BN's apply passes as one kernel
+# (g read once; +0.95 %, profiles/r2_ab_bn_apply2.jsonl)
+_APPLY2 = True
 
 
 class _BNResActConv1x1Fn(torch.autograd.Function):
@@ -261,7 +225,7 @@ class _BNResActConv1x1Fn(torch.autograd.Function):
         if gz is None:
             gz = torch.zeros((y.shape[0], ctx.wshape[0]) + tuple(y.shape[2:]), device=y.device, dtype=y.dtype)
         gz = _cl(gz)
-        dw, join = _wgrad_async(gz.numel() // gz.shape[1], lambda: _C.conv1x1_wgrad(gz, y), gz, y)
+        dw = _C.conv1x1_wgrad(gz, y)
         g, acc, acc2 = _C.conv1x1_dgrad_resred(gz, wt, z3, None if gy is None else _cl(gy), mean, bits, x2, mean2)
         dres = dx2 = dgamma2 = dbeta2 = None
         if x2 is not None and _APPLY2:  # both BNs' apply passes share one read of g
@@ -357,12 +321,10 @@ class _BNReluConvFn(torch.autograd.Function):
         gz = _cl(gz)
         rows = gz.numel() // gz.shape[1]
         if k == 1 and stride == 1:
-            dw, join = _wgrad_async(rows, lambda: _C.conv1x1_wgrad(gz, y), gz, y)
+            dw = _C.conv1x1_wgrad(gz, y).view(wshape)
             dy, acc = _C.conv1x1_dgrad_bnred(gz, wt, x, gamma, beta, mean, invstd)
-            join()
-            dw = dw.view(wshape)
         else:
-            dw, join = _wgrad_async(rows, lambda: _C.conv_wgrad(gz, y, k, k, stride, pad), gz, y)
+            dw = _C.conv_wgrad(gz, y, k, k, stride, pad)
             if stride == 1:
                 wd = wt if wt is not None else w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Cin][k][k][Cout]
                 dy, acc = _C.conv_dgrad_bnred(gz, wd, k, k, k - 1 - pad, x, gamma, beta, mean, invstd)
@@ -429,10 +391,9 @@ def conv_kxk(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -
     return _ConvKxKFn.apply(x, weight, stride, padding)
 
 
-# stride-2 3x3 data gradient: "multi" = the four parity classes as ONE implicit-
-# GEMM launch (conv_dgrad_s2_multi), "parity" = four launches, "miopen"
-_S2_DGRAD = os.environ.get("DCP_S2_DGRAD", "multi")
-_S2_PARITY = os.environ.get("DCP_S2_DGRAD_PARITY", "0") == "1" or _S2_DGRAD == "parity"
+# stride-2 3x3 data gradient: the four parity classes of dx as ONE implicit-GEMM
+# launch (conv_dgrad_s2_multi; four separate launches measured −0.4 % in the
+# step, NOTES §19 — `_C.conv_dgrad_s2` stays as the op-level reference)
 
 
 def _s2_tap_perm(wd: torch.Tensor) -> torch.Tensor:
@@ -460,11 +421,11 @@ class _ConvKxKGemmFn(torch.autograd.Function):
     """kxk NHWC convolution on the implicit-GEMM MFMA kernels (gemm.hip
     GATHER): forward (+ the next BatchNorm's Σy, Σy² from the epilogue), data
     gradient for stride 1 as the forward kernel on gy with the flipped,
-    transposed weight (MIOpen for stride > 1), weight gradient on the gathered
-    wgrad kernel (or MIOpen when ``miopen_wgrad``)."""
+    transposed weight, for stride 2 the parity-class launch (3x3) or the
+    scattering GEMM (1x1), weight gradient on the gathered wgrad kernel."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, padding, stats, miopen_wgrad, miopen_fwd):
+    def forward(ctx, x, weight, stride, padding, stats):
         ctx.set_materialize_grads(False)
         pre = _prepped(weight)
         if pre is not None:  # operands from the model's one-launch ConvWeightPrep
@@ -474,29 +435,24 @@ class _ConvKxKGemmFn(torch.autograd.Function):
             w = weight.detach().to(torch.bfloat16)
             wf = wd = None
         kh, kw = w.shape[2], w.shape[3]
-        if miopen_fwd:  # the caller computes the output statistics itself
-            y = _cl(F.conv2d(x, w, None, stride, padding))
-            st = torch.empty(0, device=x.device, dtype=torch.float32)
-        else:
-            if wf is None:
-                # both bf16 operands (forward, flipped data-gradient) from one cast launch
-                wf, wd = _C.conv_weight_bf16(weight) if kh == kw else (w.permute(0, 2, 3, 1).contiguous(), None)
-            y, st = _C.conv_fwd(x, wf, kh, kw, stride, padding, stats)
+        if wf is None:
+            # both bf16 operands (forward, flipped data-gradient) from one cast launch
+            wf, wd = _C.conv_weight_bf16(weight) if kh == kw else (w.permute(0, 2, 3, 1).contiguous(), None)
+        y, st = _C.conv_fwd(x, wf, kh, kw, stride, padding, stats)
         ctx.save_for_backward(x, w, wd)
-        ctx.cfg = (stride, padding, weight.dtype, miopen_wgrad)
+        ctx.cfg = (stride, padding, weight.dtype)
         ctx.mark_non_differentiable(st)
         return y, st
 
     @staticmethod
     def backward(ctx, gy, _gst=None):
         x, w, wd = ctx.saved_tensors
-        s, p, wdtype, miopen_wgrad = ctx.cfg
+        s, p, wdtype = ctx.cfg
         gy = _cl(gy)
         kh, kw = w.shape[2], w.shape[3]
         dx = dw = None
-        join = _noop
-        if ctx.needs_input_grad[1] and not miopen_wgrad:
-            dw, join = _wgrad_async(gy.numel() // gy.shape[1], lambda: _C.conv_wgrad(gy, x, kh, kw, s, p), gy, x)
+        if ctx.needs_input_grad[1]:
+            dw = _C.conv_wgrad(gy, x, kh, kw, s, p)
         if ctx.needs_input_grad[0]:
             if s == 1 and kh - 1 - p >= 0 and kw == kh:
                 if wd is None:
@@ -506,47 +462,26 @@ class _ConvKxKGemmFn(torch.autograd.Function):
                   and x.shape[3] == 2 * gy.shape[3]):
                 # strided 1x1 (downsample): GEMM whose epilogue scatters to the even pixels, zeros the rest
                 dx = _C.conv1x1_s2_dgrad(gy, wd)
-            elif (_S2_DGRAD == "multi" and kh == kw == 3 and s == 2 and p == 1 and x.shape[1] % 64 == 0
+            elif (kh == kw == 3 and s == 2 and p == 1 and x.shape[1] % 64 == 0
                   and (x.shape[2] + 1) // 2 == gy.shape[2] and (x.shape[3] + 1) // 2 == gy.shape[3]):
                 if wd is None:
                     wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
                 dx = _C.conv_dgrad_s2_multi(gy, _s2_tap_perm(wd), x.shape[2], x.shape[3])
-            elif _S2_PARITY and kh == kw == 3 and s == 2 and p == 1 and x.shape[1] % 64 == 0:
-                # four parity classes of dx, each an implicit GEMM over its 1/2/4 matching taps
-                if wd is None:
-                    wd = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
-                dx = _C.conv_dgrad_s2(gy, _parity_weights(wd), x.shape[2], x.shape[3])
             else:
                 dx = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]
-        join()
-        if ctx.needs_input_grad[1]:
-            if miopen_wgrad:
-                dw = torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
-                                                         [False, True, False])[1]
-            if dw.dtype != wdtype:
-                dw = dw.to(wdtype)
-        return dx, dw, None, None, None, None, None
+        if dw is not None and dw.dtype != wdtype:
+            dw = dw.to(wdtype)
+        return dx, dw, None, None, None
 
 
-def conv_kxk_gemm(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int, stats: bool = False,
-                  miopen_wgrad: bool = False, miopen_fwd: bool = False):
+def conv_kxk_gemm(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int, stats: bool = False):
     """NHWC bf16 kxk convolution on the implicit-GEMM MFMA kernels. Returns
-    (y, sums) — sums = fp32 [2*Cout] (Σy, Σy²) when ``stats`` (and the forward
-    is ours) else empty. ``miopen_fwd`` / ``miopen_wgrad`` route those passes
-    to MIOpen (shape policy: :func:`kxk_policy`)."""
-    return _ConvKxKGemmFn.apply(x, weight, stride, padding, stats, miopen_wgrad, miopen_fwd)
-
-
-def kxk_policy(cin: int, cout: int, ho: int, stride: int):
-    """(miopen_fwd, miopen_wgrad) for a 3x3 conv at ResNet-50 b256 shapes,
-    from tools/gemm_bench.py (profiles/r1_gemm3x3_bk64.log): our forward with
-    the BK=64 ring (+ the BN sums, which spares a statistics pass) beats
-    MIOpen's forward + a statistics pass at every shape; our gathered wgrad
-    (BK=64 ring, profiles/r1_gemm_bench_wgrad_bk64.log) is faster than
-    MIOpen's wrw everywhere but 56x56 with cin = cout = 64, where it ties —
-    and it skips MIOpen's zero-fill and fp32→bf16 cast passes."""
-    return False, False
+    (y, sums) — sums = fp32 [2*Cout] (Σy, Σy²) when ``stats`` else empty.
+    (Round 1 kept a per-shape MIOpen routing policy; our forward + BN sums
+    and our gathered wgrad measured faster than MIOpen at every ResNet-50
+    shape, profiles/r1_gemm3x3_bk64.log, r1_gemm_bench_wgrad_bk64.log.)"""
+    return _ConvKxKGemmFn.apply(x, weight, stride, padding, stats)
 
 
 def conv_kxk_gemm_ok(x: torch.Tensor, conv) -> bool:

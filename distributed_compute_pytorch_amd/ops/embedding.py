@@ -8,6 +8,12 @@ one fp32 ``index_add_`` scatter (atomics, no host read, no data-dependent
 sizes): same values up to fp32 summation order, capture-safe, and one kernel
 instead of sort + segment passes.
 
+The scatter is nondeterministic (fp32 atomics), so under
+``torch.use_deterministic_algorithms(True)`` the lookup falls back to
+``F.embedding``'s own deterministic sort-based backward whenever no stream
+capture is in progress (a capture keeps the scatter: the sorted backward
+cannot be captured at all).
+
 Parity: ``torch.nn.Embedding`` (no padding_idx / max_norm / sparse) — same
 parameter and state_dict key.
 """
@@ -35,8 +41,14 @@ class _EmbeddingFn(torch.autograd.Function):
         return None, gw if ctx.wdtype == torch.float32 else gw.to(ctx.wdtype)
 
 
+def _capturing(t: torch.Tensor) -> bool:
+    return t.is_cuda and torch.cuda.is_current_stream_capturing()
+
+
 def embedding(idx: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     if weight.requires_grad and torch.is_grad_enabled():
+        if torch.are_deterministic_algorithms_enabled() and not _capturing(weight):
+            return F.embedding(idx, weight)
         return _EmbeddingFn.apply(idx, weight)
     return F.embedding(idx, weight)
 

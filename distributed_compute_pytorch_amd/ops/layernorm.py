@@ -8,7 +8,6 @@ autocast's fp32 upcast of layer_norm. Elsewhere it is ``F.layer_norm``.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 from torch import nn
@@ -17,8 +16,9 @@ from torch.nn import functional as F
 from .._ext import C as _C
 from .linear import _acc_target, accumulating
 
-# DCP_LN_ACCUM=0: leave dγ / dβ to autograd's AccumulateGrad under no_sync (A/B switch)
-_LN_ACCUM = os.environ.get("DCP_LN_ACCUM", "1") != "0"
+# under no_sync add dγ / dβ into the existing .grad inside the backward kernel
+# (False: leave it to autograd's AccumulateGrad; profiles/r1_ln_accum_ab74.txt)
+_LN_ACCUM = True
 
 
 class _LNFn(torch.autograd.Function):

@@ -13,7 +13,6 @@ state_dict keys) computes
 """
 from __future__ import annotations
 
-import os
 
 import torch
 from torch import nn
@@ -21,10 +20,11 @@ from torch.nn import functional as F
 
 from .._ext import C as _C
 
-# DCP_FUSED_GELU=0: forward_gelu falls back to FusedLinear + ATen GELU (A/B switch)
-_FUSED_GELU = os.environ.get("DCP_FUSED_GELU", "1") != "0"
-# DCP_BF16_SHADOWS=0: do not let the fused Adam/AdamW write the bf16 weight copies (A/B switch)
-_SHADOWS = os.environ.get("DCP_BF16_SHADOWS", "1") != "0"
+# forward_gelu: Linear + bias + GELU with the fused GELU kernels (False: FusedLinear + ATen GELU)
+_FUSED_GELU = True
+# let the fused Adam/AdamW write the bf16 weight copies the forward GEMMs read
+# (False: one cast launch per weight per forward; NOTES §15)
+_SHADOWS = True
 
 # > 0 while gradients accumulate locally (DistributedDataParallel.no_sync): the
 # backward then adds dW / db straight into existing fp32 .grad tensors inside

@@ -34,8 +34,15 @@ from .. import distributed as dist
 from ..utils.trace import trace_range
 from .comm_utils import CoalescedBroadcaster, broadcast_coalesced, verify_params_across_processes
 
-# Bucket defaults (MiB) derived for 8x MI355X over xGMI (NOTES.md §18; torch:
-# 25 MiB cap, 1 MiB first bucket, no tail split — reducer.hpp:30-31):
+# Constructor defaults = torch's (reducer.hpp:30-31): 25 MiB cap, 1 MiB first
+# bucket, no tail split — a drop-in DDP plans the same buckets (and hands comm
+# hooks the same bucket indices) as torch.nn.parallel.DistributedDataParallel.
+DEFAULT_BUCKET_CAP_MB = 25.0
+DEFAULT_FIRST_BUCKET_MB = 1.0
+DEFAULT_TAIL_BUCKET_MB = 0.0
+
+# xGMI-tuned plan for 8x MI355X (NOTES.md §18), opted into by bench.py /
+# train.py / workloads via ``DistributedDataParallel(..., **XGMI_BUCKETS)``:
 # * first bucket 1 MiB: the first all-reduce starts as early as possible;
 # * cap 50 MiB: every bucket but the last overlaps backward, so what matters
 #   is the per-collective latency (~tens of µs) and RCCL reaching its
@@ -44,9 +51,7 @@ from .comm_utils import CoalescedBroadcaster, broadcast_coalesced, verify_params
 # * tail 2 MiB: the last bucket's all-reduce is the only one nothing can hide,
 #   so the ready-last parameters get a bucket of their own that a latency-bound
 #   all-reduce finishes in ~α instead of α + (25 MiB remainder) / bandwidth.
-DEFAULT_BUCKET_CAP_MB = 50.0
-DEFAULT_FIRST_BUCKET_MB = 1.0
-DEFAULT_TAIL_BUCKET_MB = 2.0
+XGMI_BUCKETS = {"bucket_cap_mb": 50.0, "first_bucket_mb": 1.0, "tail_bucket_mb": 2.0}
 
 
 _DTYPE_IDS = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3, torch.int64: 4,
@@ -201,7 +206,9 @@ class DistributedDataParallel(nn.Module):
             ps = [params[i] for i in plan[idx]] if idx < len(plan) else []
             return hook(state, GradBucket(buf, idx, ps, len(plan)))
 
-        self.reducer.set_comm_hook(_call)
+        # a compression hook declares its wire precision (``hook.wire_dtype``):
+        # the debug stream-ordering check then tolerates that rounding
+        self.reducer.set_comm_hook(_call, getattr(hook, "wire_dtype", None))
 
     # ------------------------------------------------------------------
     def bucket_sizes(self) -> List[int]:

@@ -66,18 +66,38 @@ def run_rank(cfg: TrainConfig, rank: int, world: int, local_rank: int):
                          accum=cfg.grad_accum, channels_last=device.type == "cuda")
     if mnist:
         wl.amp = cfg.dtype == "bf16"
-    kw = {}
+    from .parallel import XGMI_BUCKETS
+
+    kw = dict(XGMI_BUCKETS)  # xGMI-tuned bucket plan (NOTES §18); the CLI overrides it
     if cfg.bucket_cap_mb:
         kw["bucket_cap_mb"] = cfg.bucket_cap_mb
     if cfg.first_bucket_mb:
         kw["first_bucket_mb"] = cfg.first_bucket_mb
     if cfg.comm_dtype == "bf16":
         kw["comm_dtype"] = torch.bfloat16
-    model = DistributedDataParallel(wl.model, device_ids=[local_rank] if device.type == "cuda" else None,
-                                    broadcast_buffers=cfg.broadcast_buffers,
-                                    find_unused_parameters=cfg.find_unused_parameters,
-                                    gradient_as_bucket_view=cfg.gradient_as_bucket_view, **kw)
-    opt = wl.make_optimizer(model.parameters())
+    # --hip-graph: the DDP model, the optimizer and every training step (eager
+    # warmups, capture, replays) live on ONE side stream — torch refuses to
+    # capture the default stream, and the autograd engine binds each
+    # parameter's AccumulateGrad node (which the Reducer hooks) to the stream
+    # current when it was created (utils/graphs.py)
+    graph = bool(cfg.hip_graph) and device.type == "cuda"
+    if graph:
+        from .utils.graphs import capture_stream
+
+        side = capture_stream(device.index)
+        side.wait_stream(torch.cuda.current_stream())
+
+        def step_ctx():
+            return torch.cuda.stream(side)
+    else:
+        side = None
+        step_ctx = _Null
+    with step_ctx():
+        model = DistributedDataParallel(wl.model, device_ids=[local_rank] if device.type == "cuda" else None,
+                                        broadcast_buffers=cfg.broadcast_buffers,
+                                        find_unused_parameters=cfg.find_unused_parameters,
+                                        gradient_as_bucket_view=cfg.gradient_as_bucket_view, **kw)
+        opt = wl.make_optimizer(model.parameters())
     for g in opt.param_groups:
         g["lr"] = cfg.lr if mnist else g["lr"]
     sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=cfg.gamma)
@@ -104,23 +124,24 @@ def run_rank(cfg: TrainConfig, rank: int, world: int, local_rank: int):
             nsteps = cfg.steps_per_epoch or 100
         prof = _profiler(cfg, rank, epoch == start_epoch)
         for b in range(nsteps):
-            flat = []
-            for _k in range(wl.accum):
-                bt = tuple(t.to(device, non_blocking=True) for t in next(batches))
-                seen += bt[0].shape[0]
-                flat.extend(bt)
-            if step is None:
-                step = _make_step(cfg, wl, model, opt, device)
-            loss = step(*flat)
-            if prof is not None:
-                prof.step()
-            if b % cfg.log_every == 0:
-                t = loss.detach().float().clone() * wl.accum
-                dist.all_reduce(t, dist.ReduceOp.AVG if t.is_cuda else dist.ReduceOp.SUM)
-                if not t.is_cuda:
-                    t /= world
-                log.log(event="train", epoch=epoch, step=b, steps=nsteps, loss=round(t.item(), 6),
-                        lr=opt.param_groups[0]["lr"])
+            with step_ctx():  # H2D copies, the step and the loss logging in one stream order
+                flat = []
+                for _k in range(wl.accum):
+                    bt = tuple(t.to(device, non_blocking=True) for t in next(batches))
+                    seen += bt[0].shape[0]
+                    flat.extend(bt)
+                if step is None:
+                    step = _make_step(cfg, wl, model, opt, device, side)
+                loss = step(*flat)
+                if prof is not None:
+                    prof.step()
+                if b % cfg.log_every == 0:
+                    t = loss.detach().float().clone() * wl.accum
+                    dist.all_reduce(t, dist.ReduceOp.AVG if t.is_cuda else dist.ReduceOp.SUM)
+                    if not t.is_cuda:
+                        t /= world
+                    log.log(event="train", epoch=epoch, step=b, steps=nsteps, loss=round(t.item(), 6),
+                            lr=opt.param_groups[0]["lr"])
         if prof is not None:
             prof.stop()
             path = (cfg.metrics_file or "dcp") + f".trace.rank{rank}.json"
@@ -155,7 +176,7 @@ class _Null:
         return False
 
 
-def _make_step(cfg: TrainConfig, wl, model, opt, device):
+def _make_step(cfg: TrainConfig, wl, model, opt, device, side=None):
     """One optimizer step over ``wl.accum`` micro-batches (all but the last
     under ``no_sync``; backward runs INSIDE the context, like the forward).
     ``cfg.hip_graph`` on a GPU: the whole step (forward, backward, bucket
@@ -185,12 +206,13 @@ def _make_step(cfg: TrainConfig, wl, model, opt, device):
     for g in opt.param_groups:
         if "capturable" in g:
             g["capturable"] = True
-    # the DDP model was built on the current stream; capture on it too (the
-    # Reducer's AccumulateGrad nodes are bound to their creation stream)
+    # the DDP model was built on the side stream (run_rank); capture on it too
+    # (the Reducer's AccumulateGrad nodes are bound to their creation stream).
     # The first two steps run eagerly on real batches (bucket rebuild,
     # optimizer state, kernel tables); the third is captured (capture executes
-    # nothing) and replayed: no extra training steps on a static batch.
-    st = {"eager": 0, "cap": None, "lr": None}
+    # nothing) and replayed: no extra training steps on a static batch. One
+    # graph memory pool serves every (re)capture.
+    st = {"eager": 0, "cap": None, "lr": None, "recaptures": 0, "calls": 0}
 
     def call(*flat):
         lrs = [g["lr"] for g in opt.param_groups]
@@ -198,12 +220,20 @@ def _make_step(cfg: TrainConfig, wl, model, opt, device):
             if st["eager"] < 2:
                 st["eager"] += 1
                 return run(*flat)
-            st["cap"] = CapturedStep(run, [t.clone() for t in flat], warmup=0,
-                                     stream=torch.cuda.current_stream())
+            st["cap"] = CapturedStep(run, [t.clone() for t in flat], warmup=0, stream=side,
+                                     pool=torch.cuda.graph_pool_handle())
             st["lr"] = lrs
         cap = st["cap"]
+        st["calls"] += 1
         if lrs != st["lr"]:  # the captured kernels hold the LR as a constant
             st["lr"] = lrs
+            st["recaptures"] += 1
+            if st["recaptures"] > 2 and st["calls"] < 20 * st["recaptures"]:
+                import warnings
+
+                warnings.warn("--hip-graph: the learning rate changes almost every step, so the step is "
+                              "re-captured each time (slower than eager); use a per-epoch schedule",
+                              stacklevel=2)
             cap.recapture(warmup=0)
         if all(a.shape == b.shape for a, b in zip(flat, cap.static_inputs)):
             return cap(*flat)

@@ -34,3 +34,18 @@ def test_fused_embedding_tied_head_accumulates():
         logits = torch.nn.functional.linear(x, m.weight)
         logits.square().mean().backward()
     torch.testing.assert_close(ours.weight.grad, ref.weight.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_fused_embedding_deterministic_mode_uses_sorted_backward():
+    torch.manual_seed(2)
+    ours = FusedEmbedding(30, 6)
+    idx = torch.randint(0, 30, (3, 9))
+    prev = torch.are_deterministic_algorithms_enabled()
+    try:
+        torch.use_deterministic_algorithms(True)
+        y = ours(idx)
+        # F.embedding's own autograd node, not the atomic scatter
+        assert "EmbeddingBackward" in type(y.grad_fn).__name__
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    assert "EmbeddingBackward" not in type(ours(idx).grad_fn).__name__

@@ -240,28 +240,6 @@ def test_conv_kxk_gemm(cuda, cin, cout, hw, k, stride, pad):
     assert conv.weight.grad.dtype == torch.float32 and _rel(conv.weight.grad, wr.grad) < 1e-3
 
 
-def test_conv_kxk_gemm_miopen_routes(cuda):
-    """The policy's MIOpen forward / wgrad routes give the same results."""
-    from torch import nn
-
-    from distributed_compute_pytorch_amd.ops.conv import conv_kxk_gemm
-
-    g = torch.Generator().manual_seed(12)
-    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False).to(cuda).to(memory_format=torch.channels_last)
-    x = _x(2, 10, 10, 64, cuda, g)
-    gy = _x(2, 10, 10, 64, cuda, g)
-    outs = []
-    for mf, mw in ((False, False), (True, True)):
-        xa = x.clone().requires_grad_(True)
-        conv.weight.grad = None
-        y, st = conv_kxk_gemm(xa, conv.weight, 1, 1, stats=True, miopen_wgrad=mw, miopen_fwd=mf)
-        assert (st.numel() == 0) == mf
-        y.backward(gy)
-        outs.append((y.float(), xa.grad.float(), conv.weight.grad.clone()))
-    for a, b in zip(*outs):
-        assert _rel(a, b) < 1e-2
-
-
 @pytest.mark.parametrize("k,stride,pad,sums,co", [(3, 1, 1, True, 128), (3, 2, 1, False, 128), (1, 1, 0, True, 128),
                                                   (3, 1, 1, True, 64)])
 def test_bn_relu_conv_fused_autograd(cuda, k, stride, pad, sums, co):

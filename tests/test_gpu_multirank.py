@@ -157,13 +157,15 @@ def _resnet(rank, world, dev):
     m_ref = resnet18_like(num_classes=10).to(dev).to(memory_format=torch.channels_last)
     m_ours = resnet18_like(num_classes=10, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
     m_ours.load_state_dict(m_ref.state_dict())
+    m_local = resnet18_like(num_classes=10, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
+    m_local.load_state_dict(m_ref.state_dict())
     ours = dcp.parallel.DistributedDataParallel(m_ours, device_ids=[dev.index], gradient_as_bucket_view=True)
     ref = nn.parallel.DistributedDataParallel(m_ref, device_ids=[dev.index])
     o1 = dcp.optim.SGD(ours.parameters(), lr=0.01, momentum=0.9)
     o2 = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9)
     g = torch.Generator().manual_seed(rank)
     l1, l2 = [], []
-    for _ in range(3):
+    for step in range(3):
         x = torch.randn(8, 3, 64, 64, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
         y = torch.randint(0, 10, (8,), generator=g).to(dev)
         for model, opt, acc in ((ours, o1, l1), (ref, o2, l2)):
@@ -171,10 +173,31 @@ def _resnet(rank, world, dev):
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 loss = F.cross_entropy(model(x), y)
             loss.backward()
+            if step == 0 and model is ours:
+                # the reduction itself, per parameter: our DDP's gradient must be
+                # the average over ranks of what the SAME fused model computes
+                # locally on each rank's batch (a missing 1/world, a bucket
+                # unpacked into the wrong parameter or a rank reducing in a
+                # different bucket order all fail this; only BN-atomics order
+                # differs between the two computations)
+                m_local.zero_grad(set_to_none=True)
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    F.cross_entropy(m_local(x), y).backward()
+                local = torch.cat([p.grad.float().reshape(-1) for p in m_local.parameters()])
+                every = [torch.empty_like(local) for _ in range(world)]
+                tdist.all_gather(every, local)
+                want = torch.stack(every).mean(0)
+                off = 0
+                for (n, p) in m_ours.named_parameters():
+                    k = p.numel()
+                    w = want[off:off + k]
+                    err = float((p.grad.float().reshape(-1) - w).norm() / w.norm().clamp_min(1e-30))
+                    assert err < 1e-3, (n, err)
+                    off += k
             opt.step()
             acc.append(float(loss))
     for a, b in zip(l1, l2):
-        assert abs(a - b) < 0.08 * max(1.0, abs(b)), (l1, l2)
+        assert abs(a - b) < 0.03 * max(1.0, abs(b)), (l1, l2)
     flat = torch.cat([p.detach().reshape(-1) for p in m_ours.parameters()])
     other = flat.clone()
     dcp.distributed.broadcast(other, 0)

@@ -154,10 +154,14 @@ def _default_plan(rank, world):
     # ~28 MB of fp32 params in 7 layers + a small first-defined layer
     m = nn.Sequential(nn.Linear(16, 256), *[nn.Linear(1024, 1024) for _ in range(7)])
     m[0] = nn.Linear(16, 1024)
-    ddp = dcp.parallel.DistributedDataParallel(m)
+    # constructor defaults are torch's (25 MiB cap, 1 MiB first bucket, no tail split)
+    plain = dcp.parallel.DistributedDataParallel(m).ddp_logging_data()
+    assert plain["bucket_cap_bytes"] == 25 * 2**20 == int(ddp_mod.DEFAULT_BUCKET_CAP_MB * 2**20)
+    assert plain["first_bucket_bytes"] == 2**20 and plain["tail_bucket_bytes"] == 0
+    ddp = dcp.parallel.DistributedDataParallel(m, **dcp.parallel.XGMI_BUCKETS)
     info = ddp.ddp_logging_data()
-    assert info["bucket_cap_bytes"] == int(ddp_mod.DEFAULT_BUCKET_CAP_MB * 2**20)
-    assert info["tail_bucket_bytes"] == int(ddp_mod.DEFAULT_TAIL_BUCKET_MB * 2**20)
+    assert info["bucket_cap_bytes"] == int(dcp.parallel.XGMI_BUCKETS["bucket_cap_mb"] * 2**20)
+    assert info["tail_bucket_bytes"] == int(dcp.parallel.XGMI_BUCKETS["tail_bucket_mb"] * 2**20) > 0
     # the last-launched bucket holds only the ready-last parameters and fits the tail cap
     assert info["bucket_sizes"][-1] <= info["tail_bucket_bytes"], info["bucket_sizes"]
     x = torch.randn(4, 16)
@@ -232,3 +236,34 @@ def _ordering_check(rank, world):
 
 def test_reducer_stream_ordering_check():
     run_world(_ordering_check, 2)
+
+
+def _compress_check(rank, world):
+    """DCP_DEBUG_STREAMS=1 with the bf16 compression hook: the hook declares
+    its wire precision, so its rounding is not reported as an ordering error
+    (and the gradients are the bf16-rounded average)."""
+    os.environ["DCP_DEBUG_STREAMS"] = "1"
+    import distributed_compute_pytorch_amd as dcp
+
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(32, 64), nn.Tanh(), nn.Linear(64, 8))
+    ref = copy.deepcopy(m)
+    ddp = dcp.parallel.DistributedDataParallel(m, bucket_cap_mb=0.005, first_bucket_mb=0.005, tail_bucket_mb=0)
+    ddp.register_comm_hook(None, dcp.parallel.comm_hooks.bf16_compress_hook)
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(4, 32, generator=g) for _ in range(world)]
+    for _ in range(3):
+        for p in m.parameters():
+            p.grad = None
+        ddp(xs[rank]).pow(2).sum().backward()
+    grads = []
+    for r in range(world):
+        rr = copy.deepcopy(ref)
+        rr(xs[r]).pow(2).sum().backward()
+        grads.append([p.grad for p in rr.parameters()])
+    for i, p in enumerate(m.parameters()):
+        torch.testing.assert_close(p.grad, sum(gg[i] for gg in grads) / world, rtol=2e-2, atol=1e-2)
+
+
+def test_reducer_stream_check_tolerates_compression_hook():
+    run_world(_compress_check, 2)

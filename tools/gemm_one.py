@@ -23,11 +23,15 @@ def main():
     ap.add_argument("--op", default="fwd")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--hw", type=int, default=14)
+    ap.add_argument("--tune", nargs="*", default=[], help="gemm_tune key=value pairs (e.g. nt_big=2)")
     a = ap.parse_args()
+    for kv in a.tune:
+        k, v = kv.split("=")
+        _C.gemm_tune(k, int(v))
     dev = torch.device("cuda", 0)
     bf = torch.bfloat16
-    x = torch.randn(1, a.cin, a.m, 1, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
-    gy = torch.randn(1, a.cout, a.m, 1, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
+    x = (torch.rand(1, a.cin, a.m, 1, device=dev) * 2 - 1).to(bf).contiguous(memory_format=torch.channels_last)
+    gy = (torch.rand(1, a.cout, a.m, 1, device=dev) * 2 - 1).to(bf).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(a.cout, a.cin, device=dev) / a.cin ** 0.5).to(bf)
     wt = w.t().contiguous()
     sc, sf = torch.ones(a.cin, device=dev), torch.zeros(a.cin, device=dev)
