@@ -226,6 +226,31 @@ std::vector<at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, co
   return {y, st};
 }
 
+// Linear forward y = x·wᵀ + b on the MFMA GEMM (bias in the epilogue, before
+// the bf16 rounding), x bf16 [.., K] contiguous, w bf16 [N, K], b fp32 [N].
+// gelu = 0: returns {y}; 1 (tanh) / 2 (erf): returns {gelu(h), h} — h is the
+// pre-activation the GELU backward reads.
+std::vector<at::Tensor> linear_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, int64_t gelu) {
+  DK_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "linear_fwd: contiguous bf16 input");
+  DK_CHECK(gelu >= 0 && gelu <= 2, "linear_fwd: gelu must be 0, 1 (tanh) or 2 (erf)");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t K = x.size(-1);
+  const int64_t M = x.numel() / K;
+  DK_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 && w.size(1) == K,
+           "linear_fwd: weight must be contiguous bf16 [N, K]");
+  const int64_t N = w.size(0);
+  DK_CHECK(b.scalar_type() == at::kFloat && b.is_contiguous() && b.numel() == N, "linear_fwd: bias must be fp32 [N]");
+  DK_CHECK(kern::gemm_nt_supported(M, N, K), "linear_fwd: unsupported shape (N, K multiples of 64, K <= 4096)");
+  std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end());
+  shape.back() = N;
+  at::Tensor y = at::empty(shape, x.options());
+  at::Tensor g = gelu ? at::empty(shape, x.options()) : at::Tensor();
+  kern::gemm_nt_bias_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, static_cast<int>(N), static_cast<int>(K),
+                          b.data_ptr<float>(), gelu ? g.data_ptr() : nullptr, static_cast<int>(gelu), stream_of(x));
+  if (gelu) return {g, y};
+  return {y};
+}
+
 // (w_bf16 [R, C], w_bf16^T [C, R]) from an fp32 (or bf16) weight viewed as [R, C]
 std::vector<at::Tensor> weight_bf16_t(const at::Tensor& w) {
   DK_CHECK(w.is_cuda() && w.dim() >= 2, "weight_bf16_t: device weight required");
@@ -1323,6 +1348,8 @@ void bind(pybind11::module& m) {
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("scale") = pybind11::none(),
         pybind11::arg("shift") = pybind11::none(), pybind11::arg("relu") = false, pybind11::arg("stats") = false);
   m.def("conv1x1_dgrad", &conv1x1_dgrad, pybind11::arg("gy"), pybind11::arg("wt"));
+  m.def("linear_fwd", &linear_fwd, "Linear forward on the MFMA GEMM: bias (+ GELU tanh/erf) in the epilogue",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("gelu") = 0);
   m.def("attn_ok", &attn_ok);
   m.def("colsum", &colsum, "fp32 column sums of a bf16 [.., N] tensor (bias gradient)", pybind11::arg("x"),
         pybind11::arg("accumulate_into") = pybind11::none());

@@ -32,6 +32,12 @@ bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
 void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                   const float* shift, bool relu, float* stats, hipStream_t s);
 
+// Linear forward on the same kernel: C[M,N] = A[M,K]·B[N,K]ᵀ + bias (fp32 [N],
+// added before the bf16 rounding). gelu = 1 (tanh) / 2 (erf): C holds h and
+// c2 [M,N] gets gelu(h) computed from the bf16 h (what the backward reads).
+void gemm_nt_bias_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* bias, void* c2,
+                       int gelu, hipStream_t s);
+
 // fp32 weight [R][Cc] → bf16 copy wb [R][Cc] and transposed bf16 wt [Cc][R]
 // (the forward GEMM's B operand and the dgrad GEMM's B operand) in one launch.
 void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s, int taps = 1);

@@ -6,10 +6,15 @@ gradient — ~1/6 of the non-GEMM kernel time of BERT-base / GPT-2-small
 (profiles/r1_*_prof22.txt). :class:`FusedLinear` (same parameters and
 state_dict keys) computes
 
-* dW in fp32 straight from our split-M MFMA wgrad GEMM (``gemm.hip``; the
-  reduction over B·T rows is spread over the whole chip),
-* db with the hand-written deterministic column-sum kernel (``colsum``, fp32),
-* dX as the usual bf16 GEMM.
+* Y = X Wᵀ + b on our MFMA GEMM (``gemm.hip`` gemm_nt) with the bias — and
+  for ``forward_gelu`` the GELU — in the epilogue (``_C.linear_fwd``): the
+  pre-activation h and gelu(h) leave the kernel together, no separate GELU pass,
+* dX = dY W on the same kernel with a cached transposed bf16 weight,
+* dW in fp32 straight from our split-M MFMA wgrad GEMM (the reduction over
+  B·T rows is spread over the whole chip),
+* db with the hand-written deterministic column-sum kernel (``colsum``, fp32).
+Shapes the GEMM does not take (in/out features not multiples of 64, > 4096
+inputs) fall back to ATen for the forward / data gradient.
 """
 from __future__ import annotations
 
@@ -63,20 +68,33 @@ def _acc_target(ctx, p, shape):
     return None
 
 
+def _gemm_ok(x: torch.Tensor, w: torch.Tensor, bias) -> bool:
+    """Shapes our gemm_nt takes (in/out features multiples of 64, ≤ 4096 in)."""
+    return (bias is not None and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and w.shape[1] <= 4096
+            and x.is_contiguous())
+
+
+def _bias32(bias: torch.Tensor) -> torch.Tensor:
+    b = bias.detach()
+    return b if b.dtype == torch.float32 and b.is_contiguous() else b.float().contiguous()
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, w16, b16):
+    def forward(ctx, x, weight, bias, w16, b16, w16t):
         x, w, b = _setup(ctx, x, weight, bias, w16, b16)
-        ctx.save_for_backward(x, w)
+        ctx.save_for_backward(x, w, w16t)
+        if _gemm_ok(x, w, bias):
+            return _C.linear_fwd(x, w, _bias32(bias), 0)[0]
         return F.linear(x, w, b)
 
     @staticmethod
     def backward(ctx, gy):
-        x, w = ctx.saved_tensors
+        x, w, wt = ctx.saved_tensors
         gy = gy.contiguous()
         if gy.dtype != torch.bfloat16:
             gy = gy.to(torch.bfloat16)
-        return _linear_backward(ctx, gy.view(-1, gy.shape[-1]), x, w) + (None, None)
+        return _linear_backward(ctx, gy.view(-1, gy.shape[-1]), x, w, wt=wt) + (None, None, None)
 
 
 def _setup(ctx, x, weight, bias, w16, b16):
@@ -91,14 +109,18 @@ def _setup(ctx, x, weight, bias, w16, b16):
     return x, w, b
 
 
-def _linear_backward(ctx, g2, x, w, db=None, db_done=False):
+def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
     """(dx, dW, db) of y = x Wᵀ + b from the bf16 [M, N] output gradient g2.
     ``db_done``: the bias gradient was already produced by the caller (``db``,
-    or added into ``bias.grad`` when ``db`` is None)."""
+    or added into ``bias.grad`` when ``db`` is None). ``wt``: bf16 Wᵀ [K, N]
+    — the data gradient then runs on our GEMM."""
     x2 = x.reshape(-1, x.shape[-1])
     dx = dw = None
     if ctx.needs_input_grad[0]:
-        dx = (g2 @ w).view(x.shape)
+        if wt is not None and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096 and wt.shape[0] % 64 == 0:
+            dx = _C.conv1x1_dgrad(g2, wt).view(x.shape)
+        else:
+            dx = (g2 @ w).view(x.shape)
     weight, bias = ctx.params
     if ctx.needs_input_grad[1]:
         if g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
@@ -129,16 +151,20 @@ class _LinearGeluFn(torch.autograd.Function):
     Linear's dX GEMM and MFMA wgrad."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, w16, b16, tanh_approx):
+    def forward(ctx, x, weight, bias, w16, b16, w16t, tanh_approx):
         x, w, b = _setup(ctx, x, weight, bias, w16, b16)
-        h = F.linear(x, w, b)
         ctx.tanh = tanh_approx
-        ctx.save_for_backward(x, w, h)
-        return _C.gelu_fwd(h, tanh_approx)
+        if _gemm_ok(x, w, bias):  # h and gelu(h) from one GEMM epilogue
+            y, h = _C.linear_fwd(x, w, _bias32(bias), 1 if tanh_approx else 2)
+        else:
+            h = F.linear(x, w, b)
+            y = _C.gelu_fwd(h, tanh_approx)
+        ctx.save_for_backward(x, w, h, w16t)
+        return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, w, h = ctx.saved_tensors
+        x, w, h, wt = ctx.saved_tensors
         gy = gy.contiguous()
         if gy.dtype != torch.bfloat16:
             gy = gy.to(torch.bfloat16)
@@ -149,7 +175,7 @@ class _LinearGeluFn(torch.autograd.Function):
         if tgt is not None:
             db = None  # added into bias.grad by the kernel
         g2 = gh.view(-1, gh.shape[-1])
-        return _linear_backward(ctx, g2, x, w, db=db, db_done=True) + (None, None, None)
+        return _linear_backward(ctx, g2, x, w, db=db, db_done=True, wt=wt) + (None, None, None, None)
 
 
 class FusedLinear(nn.Linear):
@@ -178,6 +204,21 @@ class FusedLinear(nn.Linear):
         self.__dict__[slot] = (key, t)
         return t
 
+    def _bf16t(self, w16: torch.Tensor) -> torch.Tensor:
+        """bf16 Wᵀ [in, out] for the data-gradient GEMM, cached like ``_bf16``."""
+        if torch.cuda.is_current_stream_capturing():
+            return w16.t().contiguous()
+        from ..optim.fused import param_epoch
+
+        p = self.weight
+        key = (p._version, param_epoch(), p.data_ptr(), w16.data_ptr())
+        c = self.__dict__.get("_w16t_cache")
+        if c is not None and c[0] == key:
+            return c[1]
+        t = w16.t().contiguous()
+        self.__dict__["_w16t_cache"] = (key, t)
+        return t
+
     def _fast(self, x: torch.Tensor) -> bool:
         return x.is_cuda and self.in_features % 8 == 0 and self.out_features % 8 == 0 and (
             x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
@@ -186,8 +227,10 @@ class FusedLinear(nn.Linear):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self._fast(x):
             w16 = self._bf16(self.weight, "_w16_cache")
+            if w16 is None:
+                w16 = self.weight.detach().to(torch.bfloat16)
             b16 = self._bf16(self.bias, "_b16_cache") if self.bias is not None else None
-            return _LinearFn.apply(x, self.weight, self.bias, w16, b16)
+            return _LinearFn.apply(x, self.weight, self.bias, w16, b16, self._bf16t(w16))
         return super().forward(x)
 
     def forward_gelu(self, x: torch.Tensor, approximate: str = "none") -> torch.Tensor:
@@ -197,6 +240,8 @@ class FusedLinear(nn.Linear):
             raise ValueError(f"approximate must be 'none' or 'tanh', got {approximate!r}")
         if _FUSED_GELU and self._fast(x):
             w16 = self._bf16(self.weight, "_w16_cache")
+            if w16 is None:
+                w16 = self.weight.detach().to(torch.bfloat16)
             b16 = self._bf16(self.bias, "_b16_cache") if self.bias is not None else None
-            return _LinearGeluFn.apply(x, self.weight, self.bias, w16, b16, approximate == "tanh")
+            return _LinearGeluFn.apply(x, self.weight, self.bias, w16, b16, self._bf16t(w16), approximate == "tanh")
         return F.gelu(self.forward(x), approximate=approximate)

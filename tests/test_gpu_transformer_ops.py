@@ -375,3 +375,24 @@ def test_adamw_writes_bf16_shadow_weights(cuda):
     with torch.no_grad():  # an out-of-band write invalidates the shadow
         a.weight.mul_(0.5)
     assert fresh_bf16_shadow(a.weight) is None
+
+
+@pytest.mark.parametrize("gelu", [0, 1, 2])
+@pytest.mark.parametrize("rows,fin,fout", [(1000, 256, 192), (2048, 768, 2304), (333, 64, 128)])
+def test_linear_fwd_epilogues_match_fp32(cuda, gelu, rows, fin, fout):
+    """gemm_nt's Linear epilogues (bias before the bf16 rounding; + GELU tanh /
+    erf from the rounded h) vs fp32 PyTorch on the same bf16 operands."""
+    from distributed_compute_pytorch_amd._ext import C
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(rows, fin, generator=g).to(torch.bfloat16).to(cuda)
+    w = (torch.randn(fout, fin, generator=g) / fin ** 0.5).to(torch.bfloat16).to(cuda)
+    b = torch.randn(fout, generator=g).to(cuda)
+    out = C.linear_fwd(x, w, b, gelu)
+    h_ref = x.float() @ w.float().t() + b
+    h = out[-1]
+    assert h.dtype == torch.bfloat16 and h.shape == (rows, fout)
+    torch.testing.assert_close(h.float(), h_ref, rtol=1e-2, atol=1e-2)
+    if gelu:
+        y_ref = F.gelu(h.float(), approximate="tanh" if gelu == 1 else "none")  # GELU of the stored h
+        torch.testing.assert_close(out[0].float(), y_ref, rtol=1e-2, atol=1e-2)
