@@ -13,6 +13,9 @@ namespace dcp {
 namespace stem {
 void bind(pybind11::module& m);
 }
+namespace convnet {
+void bind(pybind11::module& m);
+}
 }  // namespace dcp
 #include "trace/trace.h"
 #include "store/tcp_store.h"
@@ -211,4 +214,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   fused::bind(m);
   stem::bind(m);
+  convnet::bind(m);
 }

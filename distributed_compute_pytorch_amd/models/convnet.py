@@ -12,9 +12,11 @@ fc1 activation, which acts element-wise; ``nn.Dropout`` is
 used for ``dropout2`` so behaviour is the same without the 2.x warning.
 
 ``fused=True`` (GPU) runs the MI355X path with identical parameters and
-state_dict: conv2 → [ReLU + max-pool + Dropout2d] as one NHWC kernel each
-way, fc1 → [BatchNorm1d + ReLU] on the fused BN kernels, Philox dropout, and a
-wave-per-row log-softmax.
+state_dict: conv1 → ReLU → conv2 → ReLU → max-pool → Dropout2d → flatten as
+ONE fp32-MFMA kernel forward and one (+ reduce) backward
+(``ops/convnet.py``, ``csrc/kernels/convnet.hip``), fc1 → [BatchNorm1d +
+ReLU] on the fused BN kernels, Philox dropout, and a wave-per-row
+log-softmax.
 """
 from __future__ import annotations
 
@@ -53,12 +55,9 @@ class ConvNet(nn.Module):
         return F.log_softmax(x, dim=1)
 
     def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
-        from ..ops import fused_dropout, fused_log_softmax, relu_max_pool2d_dropout
+        from ..ops import convnet_features, fused_dropout, fused_log_softmax
 
-        x = F.relu(self.conv1(x))
-        x = self.conv2(x).contiguous(memory_format=torch.channels_last)
-        x = relu_max_pool2d_dropout(x, 2, 2, 0, self.dropout1.p, self.training)
-        x = torch.flatten(x, 1)
+        x = convnet_features(x, self.conv1, self.conv2, self.dropout1.p, self.training)
         x = self.batchnorm(self.fc1(x))  # BN1d + ReLU
         x = fused_dropout(x, self.dropout2.p, self.training)
         return fused_log_softmax(self.fc2(x), 1)

@@ -149,3 +149,59 @@ def test_fused_convnet_trains(cuda):
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+def _features_ref(x, m, drop_scale=None):
+    y = F.max_pool2d(F.relu(m.conv2(F.relu(m.conv1(x)))), 2)
+    if drop_scale is not None:
+        y = y * drop_scale[:, :, None, None]
+    return torch.flatten(y, 1)
+
+
+@pytest.mark.parametrize("B", [128, 5])
+def test_convnet_features_kernel_matches_fp32(cuda, B):
+    """The fused conv1→ReLU→conv2→ReLU→pool→flatten kernel (fp32 MFMA) and its
+    backward against the fp32 ATen composition on the same weights."""
+    from distributed_compute_pytorch_amd.models import ConvNet
+    from distributed_compute_pytorch_amd.ops import convnet_features
+
+    torch.manual_seed(0)
+    m = ConvNet().to(cuda)
+    x = torch.randn(B, 1, 28, 28, device=cuda)
+    yr = _features_ref(x, m)
+    g = torch.randn_like(yr)
+    ref = torch.autograd.grad(yr, [m.conv1.weight, m.conv1.bias, m.conv2.weight, m.conv2.bias], g)
+    yo = convnet_features(x, m.conv1, m.conv2, 0.0, True)
+    assert yo.shape == (B, 9216) and yo.dtype == torch.float32
+    torch.testing.assert_close(yo, yr, rtol=1e-5, atol=1e-5)
+    ours = torch.autograd.grad(yo, [m.conv1.weight, m.conv1.bias, m.conv2.weight, m.conv2.bias], g)
+    for name, a, b in zip(("w1", "b1", "w2", "b2"), ours, ref):
+        rel = float((a - b).norm() / b.norm())
+        assert rel < 1e-4, (name, rel)
+
+
+def test_convnet_features_dropout(cuda):
+    """Dropout2d inside the fused kernel: whole (n, c) planes dropped at rate p,
+    kept planes scaled by 1/(1-p), the backward routes gradient only through
+    kept planes (checked against the ATen composition with the same mask)."""
+    from distributed_compute_pytorch_amd.models import ConvNet
+    from distributed_compute_pytorch_amd.ops import convnet_features
+
+    torch.manual_seed(1)
+    m = ConvNet().to(cuda)
+    x = torch.randn(64, 1, 28, 28, device=cuda)
+    yo = convnet_features(x, m.conv1, m.conv2, 0.25, True)
+    base = _features_ref(x, m).detach().view(64, 64, 144)
+    planes = yo.detach().view(64, 64, 144)
+    nz = base.abs().sum(2) > 0
+    kept = planes.abs().sum(2) > 0
+    frac = (kept & nz).sum().item() / nz.sum().item()
+    assert 0.65 < frac < 0.85, frac
+    scale = kept.float() * (4.0 / 3.0)
+    torch.testing.assert_close(planes, base * scale[:, :, None], rtol=1e-5, atol=1e-5)
+    g = torch.randn_like(yo)
+    ours = torch.autograd.grad(yo, [m.conv1.weight, m.conv2.weight, m.conv2.bias], g)
+    yr = _features_ref(x, m, scale)
+    ref = torch.autograd.grad(yr, [m.conv1.weight, m.conv2.weight, m.conv2.bias], g)
+    for a, b in zip(ours, ref):
+        assert float((a - b).norm() / b.norm()) < 1e-4
