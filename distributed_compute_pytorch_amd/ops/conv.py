@@ -237,7 +237,6 @@ class _BNResActConv1x1Fn(torch.autograd.Function):
                 dx2, dgamma2, dbeta2 = _C.bn_bwd_apply_g(g, x2, gamma2, mean2, invstd2, acc2)
             else:
                 dres = g  # relu mask already applied: the identity's gradient
-        join()
         dw = dw.view(ctx.wshape)
         if dw.dtype != ctx.wdtype:
             dw = dw.to(ctx.wdtype)
@@ -319,7 +318,6 @@ class _BNReluConvFn(torch.autograd.Function):
         x, y, gamma, beta, mean, invstd, w, wt = ctx.saved_tensors
         k, stride, pad, wshape, wdtype = ctx.cfg
         gz = _cl(gz)
-        rows = gz.numel() // gz.shape[1]
         if k == 1 and stride == 1:
             dw = _C.conv1x1_wgrad(gz, y).view(wshape)
             dy, acc = _C.conv1x1_dgrad_bnred(gz, wt, x, gamma, beta, mean, invstd)
@@ -333,7 +331,6 @@ class _BNReluConvFn(torch.autograd.Function):
                                                          False, [0, 0], 1, [True, False, False])[0]
                 dy = _cl(dy)
                 acc = None
-            join()
         if dw.dtype != wdtype:
             dw = dw.to(wdtype)
         if acc is None:

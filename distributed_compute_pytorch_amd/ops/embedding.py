@@ -27,15 +27,25 @@ from torch import nn
 class _EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, weight):
+        from .linear import accumulating
+
         ctx.save_for_backward(idx)
         ctx.shape = weight.shape
         ctx.wdtype = weight.dtype
+        ctx.accum = accumulating()
+        ctx.param = weight
         return F.embedding(idx, weight)
 
     @staticmethod
     def backward(ctx, g):
+        from .linear import inplace_grad
+
         (idx,) = ctx.saved_tensors
         V, D = ctx.shape
+        tgt = inplace_grad(ctx.param, ctx.shape, ctx.accum)
+        if tgt is not None:  # scatter straight into the accumulated .grad (no zero fill, no add pass)
+            tgt.index_add_(0, idx.reshape(-1), g.reshape(-1, D).float())
+            return None, None
         gw = torch.zeros(V, D, device=g.device, dtype=torch.float32)
         gw.index_add_(0, idx.reshape(-1), g.reshape(-1, D).float())
         return None, gw if ctx.wdtype == torch.float32 else gw.to(ctx.wdtype)

@@ -37,7 +37,7 @@ _SHADOWS = True
 # separate AccumulateGrad add (one elementwise launch per parameter per
 # micro-step: 3.8 ms of a GPT-2 accum-4 step, profiles/r1_gpt2_prof64.txt).
 # A plain global, not thread-local: the backward runs on autograd's device
-# threads. The DDP Reducer ignores hooks under no_sync, so skipping them is safe.
+# threads. The synchronising micro-step adds in place too (see inplace_grad).
 _ACCUM_IN_PLACE = [0]
 
 
@@ -60,12 +60,34 @@ def accumulating() -> bool:
     return _ACCUM_IN_PLACE[0] > 0
 
 
-def _acc_target(ctx, p, shape):
+def inplace_grad(p, shape, accum: bool = False):
+    """``p.grad`` when a backward may add its fp32 contribution straight into
+    it and return None instead (skipping autograd's separate AccumulateGrad
+    add — one elementwise launch per parameter per micro-step, 2.37 ms of a
+    GPT-2 accum-4 step: profiles/r2_gpt2_kernel_stats_final.txt:11), else None.
+
+    * under ``no_sync`` (``accum``): whenever ``.grad`` holds a compatible
+      fp32 buffer (DDP ignores the hooks of these micro-steps);
+    * on any other backward only when nothing could observe the difference:
+      no gradient graph is being built (``create_graph``), and no tensor hook
+      or post-accumulate hook sits on the parameter. The AccumulateGrad node
+      still runs (with an undefined gradient) after every producer of the
+      parameter's gradient — tied weights included — so the DDP Reducer's
+      post-hook on it (``reducer.cpp`` register_hooks) fires exactly once,
+      after the in-place add, and finds the accumulated ``.grad``.
+    """
     g = p.grad if p is not None else None
-    if (getattr(ctx, "accum", False) and g is not None and g.dtype == torch.float32 and g.is_contiguous()
-            and g.shape == shape and not g.requires_grad):
+    if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != shape or g.requires_grad:
+        return None
+    if accum:
         return g
-    return None
+    if torch.is_grad_enabled() or p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None):
+        return None
+    return g
+
+
+def _acc_target(ctx, p, shape):
+    return inplace_grad(p, shape, getattr(ctx, "accum", False))
 
 
 def _gemm_ok(x: torch.Tensor, w: torch.Tensor, bias) -> bool:

@@ -49,3 +49,35 @@ def test_fused_embedding_deterministic_mode_uses_sorted_backward():
     finally:
         torch.use_deterministic_algorithms(prev)
     assert "EmbeddingBackward" not in type(ours(idx).grad_fn).__name__
+
+
+def test_fused_embedding_inplace_accumulation_sees_complete_grad():
+    """Second backward onto an existing .grad: the scatter adds in place and
+    returns None; the AccumulateGrad post-hook (what the DDP Reducer hangs on)
+    still fires once, after every contribution of the tied weight is in."""
+    import torch.nn.functional as F
+
+    torch.manual_seed(2)
+    ours = FusedEmbedding(40, 8)
+    ref = nn.Embedding(40, 8)
+    ref.load_state_dict(ours.state_dict())
+    seen = []
+    node = torch.autograd.graph.get_gradient_edge(ours.weight).node
+    node.register_hook(lambda gi, go: seen.append(ours.weight.grad.clone()))
+    for k in range(3):
+        idx = torch.randint(0, 40, (4, 9))
+        for m in (ours, ref):
+            F.linear(m(idx), m.weight).square().mean().backward()
+        assert len(seen) == k + 1
+        torch.testing.assert_close(seen[-1], ref.weight.grad, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(ours.weight.grad, ref.weight.grad, rtol=1e-5, atol=1e-6)
+    # a tensor hook on the parameter must see every contribution: no in-place shortcut then
+    h = ours.weight.register_hook(lambda g: g)
+    ours.weight.grad = None
+    ref.weight.grad = None
+    for _ in range(2):
+        idx = torch.randint(0, 40, (4, 9))
+        for m in (ours, ref):
+            F.linear(m(idx), m.weight).square().mean().backward()
+    h.remove()
+    torch.testing.assert_close(ours.weight.grad, ref.weight.grad, rtol=1e-5, atol=1e-6)

@@ -152,38 +152,51 @@ def test_fused_convnet_trains(cuda):
 
 
 def _features_ref(x, m, drop_scale=None):
-    y = F.max_pool2d(F.relu(m.conv2(F.relu(m.conv1(x)))), 2)
+    """fp64 CPU composition (exact up to fp64 rounding): ATen's fp32 GPU convs
+    may pick Winograd-type algorithms whose own error is ~1e-3 relative."""
+    import copy
+
+    m64 = copy.deepcopy(m).double().cpu()
+    y = F.max_pool2d(F.relu(m64.conv2(F.relu(m64.conv1(x.double().cpu())))), 2)
     if drop_scale is not None:
-        y = y * drop_scale[:, :, None, None]
-    return torch.flatten(y, 1)
+        y = y * drop_scale.double().cpu()[:, :, None, None]
+    return torch.flatten(y, 1), m64
+
+
+def _ref_grads(x, m, g, names, drop_scale=None):
+    y, m64 = _features_ref(x, m, drop_scale)
+    ps = [dict(m64.named_parameters())[n] for n in names]
+    return y, [t.float().to(x.device) for t in torch.autograd.grad(y, ps, g.double().cpu())]
+
+
+_NAMES = ["conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias"]
 
 
 @pytest.mark.parametrize("B", [128, 5])
 def test_convnet_features_kernel_matches_fp32(cuda, B):
     """The fused conv1→ReLU→conv2→ReLU→pool→flatten kernel (fp32 MFMA) and its
-    backward against the fp32 ATen composition on the same weights."""
+    backward against the fp64 composition on the same weights."""
     from distributed_compute_pytorch_amd.models import ConvNet
     from distributed_compute_pytorch_amd.ops import convnet_features
 
     torch.manual_seed(0)
     m = ConvNet().to(cuda)
     x = torch.randn(B, 1, 28, 28, device=cuda)
-    yr = _features_ref(x, m)
-    g = torch.randn_like(yr)
-    ref = torch.autograd.grad(yr, [m.conv1.weight, m.conv1.bias, m.conv2.weight, m.conv2.bias], g)
     yo = convnet_features(x, m.conv1, m.conv2, 0.0, True)
     assert yo.shape == (B, 9216) and yo.dtype == torch.float32
-    torch.testing.assert_close(yo, yr, rtol=1e-5, atol=1e-5)
-    ours = torch.autograd.grad(yo, [m.conv1.weight, m.conv1.bias, m.conv2.weight, m.conv2.bias], g)
-    for name, a, b in zip(("w1", "b1", "w2", "b2"), ours, ref):
+    g = torch.randn_like(yo)
+    yr, ref = _ref_grads(x, m, g, _NAMES)
+    torch.testing.assert_close(yo, yr.float().to(cuda), rtol=1e-5, atol=1e-5)
+    ours = torch.autograd.grad(yo, [dict(m.named_parameters())[n] for n in _NAMES], g)
+    for name, a, b in zip(_NAMES, ours, ref):
         rel = float((a - b).norm() / b.norm())
-        assert rel < 1e-4, (name, rel)
+        assert rel < 1e-5, (name, rel)
 
 
 def test_convnet_features_dropout(cuda):
     """Dropout2d inside the fused kernel: whole (n, c) planes dropped at rate p,
     kept planes scaled by 1/(1-p), the backward routes gradient only through
-    kept planes (checked against the ATen composition with the same mask)."""
+    kept planes (checked against the fp64 composition with the same mask)."""
     from distributed_compute_pytorch_amd.models import ConvNet
     from distributed_compute_pytorch_amd.ops import convnet_features
 
@@ -191,7 +204,7 @@ def test_convnet_features_dropout(cuda):
     m = ConvNet().to(cuda)
     x = torch.randn(64, 1, 28, 28, device=cuda)
     yo = convnet_features(x, m.conv1, m.conv2, 0.25, True)
-    base = _features_ref(x, m).detach().view(64, 64, 144)
+    base = _features_ref(x, m)[0].float().to(cuda).view(64, 64, 144)
     planes = yo.detach().view(64, 64, 144)
     nz = base.abs().sum(2) > 0
     kept = planes.abs().sum(2) > 0
@@ -200,8 +213,8 @@ def test_convnet_features_dropout(cuda):
     scale = kept.float() * (4.0 / 3.0)
     torch.testing.assert_close(planes, base * scale[:, :, None], rtol=1e-5, atol=1e-5)
     g = torch.randn_like(yo)
-    ours = torch.autograd.grad(yo, [m.conv1.weight, m.conv2.weight, m.conv2.bias], g)
-    yr = _features_ref(x, m, scale)
-    ref = torch.autograd.grad(yr, [m.conv1.weight, m.conv2.weight, m.conv2.bias], g)
-    for a, b in zip(ours, ref):
-        assert float((a - b).norm() / b.norm()) < 1e-4
+    names = ["conv1.weight", "conv2.weight", "conv2.bias"]
+    ours = torch.autograd.grad(yo, [dict(m.named_parameters())[n] for n in names], g)
+    _, ref = _ref_grads(x, m, g, names, scale)
+    for n, a, b in zip(names, ours, ref):
+        assert float((a - b).norm() / b.norm()) < 1e-5, n
