@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--emulate-channels", type=int, default=16, help="emulated RCCL channels (workgroups)")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the persistent GEMM / conv grids leave free for collectives (DCP_RESERVE_CUS)")
+    ap.add_argument("--gemm-tune", default=None,
+                    help="k=v[,k=v] entries of the GEMM launcher tuning table (_C.gemm_tune, e.g. nt_big=4)")
     return ap.parse_args()
 
 
@@ -197,6 +199,14 @@ def main():
 
     ours = a.impl == "ours"
     fused = bool(a.fused) and ours
+    tune = {}
+    if a.gemm_tune:
+        from distributed_compute_pytorch_amd._ext import C as _C
+
+        for kv in a.gemm_tune.split(","):
+            k, v = kv.split("=")
+            _C.gemm_tune(k.strip(), int(v))
+            tune[k.strip()] = _C.gemm_tune_get(k.strip())
     torch.manual_seed(0)
     wl = workloads.build(a.model, dev, batch=a.batch, fused=fused, seq_len=a.seq_len, accum=a.accum,
                          channels_last=bool(a.channels_last), fused_gemm=bool(a.gemm))
@@ -304,6 +314,8 @@ def main():
                                         "channels": a.emulate_channels}
             if a.reserve_cus is not None:
                 cfg["reserve_cus"] = a.reserve_cus
+            if tune:
+                cfg["gemm_tune"] = tune
             if ours:
                 cfg["bucket_cap_mb"] = round(info["bucket_cap_bytes"] / 2**20, 3)
                 cfg["first_bucket_mb"] = round(info["first_bucket_bytes"] / 2**20, 3)

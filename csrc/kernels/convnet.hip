@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(kT) convnet_fwd_kernel(const float* __restrict
   }
 }
 
-__global__ void __launch_bounds__(kT) convnet_bwd_kernel(const float* __restrict__ gin,
+__global__ void __launch_bounds__(kT, 2) convnet_bwd_kernel(const float* __restrict__ gin,
                                                          const uint8_t* __restrict__ mask,
                                                          const float* __restrict__ x, const float* __restrict__ w1,
                                                          const float* __restrict__ b1, const float* __restrict__ w2,
@@ -307,34 +307,37 @@ __global__ void __launch_bounds__(kT) convnet_bwd_kernel(const float* __restrict
   }
 }
 
-// grads = Σ_blocks partials, in torch layouts: dW2 [64][32][3][3] | db2 | dW1 [32][1][3][3] | db1
+// grads = Σ_blocks partials, in torch layouts: dW2 [64][32][3][3] | db2 | dW1 [32][1][3][3] | db1.
+// A workgroup = 32 partial elements x 8 strided block groups (coalesced 128-B
+// rows), combined in LDS in a fixed order: deterministic.
+constexpr int kRedCols = 32, kRedGroups = kT / kRedCols;
+
 __global__ void __launch_bounds__(kT) convnet_reduce_kernel(const float* __restrict__ part, float* __restrict__ grads,
                                                             int nb, int acc) {
-  const int e = blockIdx.x * kT + threadIdx.x;  // partial index (reads coalesce)
-  if (e >= kPart) return;
-  if ((e >= kD1 + 288 && e < kB1) || e >= kB1 + 32) return;  // wave-pair 1 copies: folded into pair 0
+  __shared__ float red[kRedGroups][kRedCols + 1];
+  const int le = threadIdx.x % kRedCols, gq = threadIdx.x / kRedCols;
+  const int e = blockIdx.x * kRedCols + le;  // partial index
+  // wave-pair 1 copies of dW1 / db1 are folded into pair 0
+  const bool live = e < kPart && !((e >= kD1 + 288 && e < kB1) || e >= kB1 + 32);
   const int e2 = e >= kB1 ? e + 32 : (e >= kD1 ? e + 288 : -1);
   float s = 0.f;
-  int b = 0;
-  for (; b + 4 <= nb; b += 4) {
-    float v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = part[static_cast<int64_t>(b + k) * kPart + e];
-    if (e2 >= 0) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] += part[static_cast<int64_t>(b + k) * kPart + e2];
+  if (live) {
+    for (int b = gq; b < nb; b += kRedGroups) {
+      float v = part[static_cast<int64_t>(b) * kPart + e];
+      if (e2 >= 0) v += part[static_cast<int64_t>(b) * kPart + e2];
+      s += v;
     }
-    s += (v[0] + v[1]) + (v[2] + v[3]);
   }
-  for (; b < nb; ++b) {
-    float v = part[static_cast<int64_t>(b) * kPart + e];
-    if (e2 >= 0) v += part[static_cast<int64_t>(b) * kPart + e2];
-    s += v;
-  }
+  red[gq][le] = s;
+  __syncthreads();
+  if (gq != 0 || !live) return;
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < kRedGroups; ++k) t += red[k][le];
   int o;
   if (e < kW2) {
-    const int co = e / 288, r = e - 288 * co, t = r >> 5, c = r & 31;
-    o = co * 288 + c * 9 + t;
+    const int co = e / 288, r = e - 288 * co, tap = r >> 5, c = r & 31;
+    o = co * 288 + c * 9 + tap;
   } else if (e < kD1) {
     o = e;  // db2
   } else if (e < kB1) {
@@ -342,12 +345,12 @@ __global__ void __launch_bounds__(kT) convnet_reduce_kernel(const float* __restr
   } else {
     o = kW2 + 64 + 288 + (e - kB1);  // db1
   }
-  grads[o] = acc ? grads[o] + s : s;
+  grads[o] = acc ? grads[o] + t : t;
 }
 
 int bwd_blocks(int B, int* per_block) {
   const int items = 4 * B;
-  const int nb0 = items < 256 ? items : 256;
+  const int nb0 = items < 512 ? items : 512;  // two workgroups per CU (LDS 70.5 KB, 256 VGPRs)
   const int pb = (items + nb0 - 1) / nb0;
   *per_block = pb;
   return (items + pb - 1) / pb;
@@ -380,7 +383,7 @@ void convnet_bwd(const float* g, const uint8_t* mask, const float* x, const floa
   const int nb = bwd_blocks(B, &pb);
   hipLaunchKernelGGL(convnet_bwd_kernel, dim3(nb), dim3(kT), kBwdLds, s, g, mask, x, w1, b1, w2, scale, ws, 4 * B,
                      pb);
-  hipLaunchKernelGGL(convnet_reduce_kernel, dim3((kPart + kT - 1) / kT), dim3(kT), 0, s, ws, grads, nb,
+  hipLaunchKernelGGL(convnet_reduce_kernel, dim3((kPart + kRedCols - 1) / kRedCols), dim3(kT), 0, s, ws, grads, nb,
                      accumulate ? 1 : 0);
 }
 

@@ -490,16 +490,9 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
 
   const int ck = lane >> 4;  // logical 16-B chunk (k = 8ck … 8ck+7) this lane reads
   int kt = 0, slot = 0, cv = wg;  // consumer k-step, ring slot, tile id
-  // STAG (the 256 x 256 tile, BK = 64): waves 4-7 (wm = 1) share SIMDs with
-  // waves 0-3; they read the stage's second 32-k half into registers but run
-  // its MFMAs after the NEXT barrier, so right after every barrier one wave
-  // of each SIMD pair has MFMAs ready while its partner waits for LDS reads
-  // (a two-group ping-pong; MI355X_MICROARCH "two waves per SIMD", item 9).
-  // Not across a tile end: the epilogue needs the full sums.
-  constexpr bool STAG = WR == 128 && BK == 64 && !PRO;
-  const bool late = STAG && wm == 1;
-  bool pend = false;  // late group: a stage's second half waits in cx / cw
-  bf16x8 cx[STAG ? FM : 1], cw[STAG ? FN : 1];
+  // (A staggered two-group variant of the 256 x 256 tile — waves 4-7 running
+  // a stage's second half after the next barrier — measured slower, on the
+  // gathered 3x3 shapes 2.3x: profiles/r3_gemm_ab_big.jsonl vs r3_gemm_ab_stag.jsonl.)
   for (int q = 0; q < T; ++q) {
     // vmcnt retires in issue order: the ops younger than stage q's DMA are the
     // DMA of q+1 and the epilogue stores of a tile end at q-2 or q-1 (issued
@@ -517,14 +510,6 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
     }
     barrier();  // stage q visible to all waves; all reads of slot (q-1)%kNSnt done
     issue();
-    if (STAG && pend) {
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[i], cx[j], acc[i][j], 0, 0, 0);
-      pend = false;
-    }
     const char* sA = lds + slot * STAGE;
     const char* sB = sA + SA;
 #pragma unroll
@@ -551,14 +536,6 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
         }
 #pragma unroll
         for (int j = 0; j < FM; ++j) xf[j] = bn_act_frag(xf[j], sc, sf, relu != 0);
-      }
-      if (STAG && h == 1 && late && kt != KT - 1) {
-#pragma unroll
-        for (int j = 0; j < FM; ++j) cx[STAG ? j : 0] = xf[j];
-#pragma unroll
-        for (int i = 0; i < FN; ++i) cw[STAG ? i : 0] = wf[i];
-        pend = true;
-        continue;
       }
 #pragma unroll
       for (int i = 0; i < FN; ++i)
@@ -774,236 +751,10 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   }
 }
 
-// ------------------------------------------------------- big4 (256²) ----
-// C[M,N] = A[M,K]·B[N,K]^T (+ the BN statistics of C) on 256 x 256 tiles with
-// FOUR waves of 128 x 128 each — one wave per SIMD, 256 accumulator
-// registers per lane (the AGPR file) — the shape of the vendor library's
-// fastest kernels on the deep-K ResNet layers. One wave per SIMD has no
-// partner to hide LDS latency behind, so the wave pipelines itself: fragment
-// registers are double-buffered (set A / set B), and each 64-deep stage runs
-//   ds_read k 32-63 → set B  ||  MFMA k 0-31 from set A
-//   vmcnt(0) + barrier       (stage q+1 landed; every wave is done with slot q)
-//   DMA stage q+2 → slot q   ||  ds_read q+1's k 0-31 → set A  ||  MFMA k 32-63 from set B
-// so every LDS read and every DMA overlaps MFMAs and the DMA has a whole
-// stage (128 MFMAs per SIMD, ~2,000 cycles) to land. LDS: 2 x 64 KB ring +
-// 32 KB C staging (the ring is busy with the next tile at a tile end).
-// Persistent over tiles with the same XCD-aware tile order as gemm_nt.
-constexpr int kB4Threads = 256;
-template <int EPI>
-__global__ void __launch_bounds__(kB4Threads, 1) gemm_nt_big4_kernel(const uint16_t* __restrict__ A,
-                                                                     const uint16_t* __restrict__ B,
-                                                                     uint16_t* __restrict__ C, int64_t M, int N,
-                                                                     int K, float* __restrict__ stats, int tiles_m,
-                                                                     int tn) {
-  constexpr bool STATS = EPI == 1;
-  constexpr int BM = 256, BN = 256, BK = 64, RB = BK * 2, CPR = BK / 8;
-  constexpr int SA = BM * RB, STAGE = SA + BN * RB;  // 32 KB + 32 KB
-  constexpr int FM = 8, FN = 8;                        // 16 x 16 fragments per wave (128 x 128)
-  constexpr int WN = 128, LPR = WN / 8, RPI = 64 / LPR, CST = 32 * WN * 2;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  char* cst = lds + 2 * STAGE;  // + wave * CST
-
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int P = static_cast<int>(gridDim.x), wid = static_cast<int>(blockIdx.x);
-  const int xcd = wid & 7, q8 = P >> 3, r8 = P & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
-  const int n0 = (wg % tn) * BN;
-  const int KT = K / BK;
-  const int my_tiles = (tiles_m * tn - wg + P - 1) / P;
-  const int T = my_tiles * KT;
-  cst += wave * CST;
-
-  // DMA of one stage: 8 + 8 x 1 KiB per wave. DMA j of a wave covers stage
-  // rows wave*64 + 8j + (lane >> 3), chunk (lane & 7) ^ nt_swzk(row), and
-  // nt_swzk(row) = (lane >> 4) | 4*(j & 1): two per-lane column offsets and
-  // one row base serve all 16. Branch-free (sched_group_barrier needs one
-  // basic block): past the last stage it re-reads clamped in-bounds rows into
-  // a slot nobody reads.
-  int is_kt = 0;
-  int a_m0 = (wg / tn) * BM;
-  const int a_step = (P / tn) * BM;  // next tile of this workgroup: P % tn == 0
-  const int rb = wave * 64 + (lane >> 3);
-  const int col0 = ((lane & 7) ^ (lane >> 4)) * 8, col1 = ((lane & 7) ^ ((lane >> 4) | 4)) * 8;
-  const uint16_t* pB0 = B + static_cast<int64_t>(n0 + rb) * K + col0;
-  const uint16_t* pB1 = B + static_cast<int64_t>(n0 + rb) * K + col1;
-  auto issue_a = [&](char* base, int j, int k0) {
-    int gm = a_m0 + rb + 8 * j;
-    gm = gm < M ? gm : static_cast<int>(M) - 1;
-    glds16(A + static_cast<int64_t>(gm) * K + ((j & 1) ? col1 : col0) + k0, base + (wave * 8 + j) * 1024);
-  };
-  auto issue_b = [&](char* base, int j, int k0) {
-    glds16(((j & 1) ? pB1 : pB0) + static_cast<int64_t>(8 * j) * K + k0, base + SA + (wave * 8 + j) * 1024);
-  };
-  auto advance = [&]() {
-    ++is_kt;
-    const bool wrap = is_kt == KT;
-    is_kt = wrap ? 0 : is_kt;
-    a_m0 += wrap ? a_step : 0;
-  };
-  auto issue = [&](int slot) {
-    char* base = lds + slot * STAGE;
-    const int k0 = is_kt * BK;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) issue_a(base, j, k0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) issue_b(base, j, k0);
-    advance();
-  };
-  // fragment j of a half: row 16j + (lane & 15) of the wave's 128, chunk
-  // lch ^ nt_swzk(row) — the swizzle depends on (lane & 15) only, so every
-  // fragment is one per-lane offset (per half) + an immediate 2 KB * j
-  const int l15 = lane & 15;
-  const int off0 = l15 * RB + 16 * ((lane >> 4) ^ nt_swzk<BK>(l15));
-  const int off1 = l15 * RB + 16 * ((4 + (lane >> 4)) ^ nt_swzk<BK>(l15));
-  auto read_frags = [&](const char* base, int h, bf16x8 (&xf)[FM], bf16x8 (&wf)[FN]) {
-    const char* pa = base + wm * 128 * RB + (h ? off1 : off0);
-    const char* pb = base + SA + wn * WN * RB + (h ? off1 : off0);
-#pragma unroll
-    for (int j = 0; j < FM; ++j) xf[j] = *reinterpret_cast<const bf16x8*>(pa + j * 16 * RB);
-#pragma unroll
-    for (int i = 0; i < FN; ++i) wf[i] = *reinterpret_cast<const bf16x8*>(pb + i * 16 * RB);
-  };
-
-  f32x4 acc[FN][FM];
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mfma_all = [&](const bf16x8 (&xf)[FM], const bf16x8 (&wf)[FN]) {
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
-  };
-  float ssum[8], ssq[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
-
-  // prologue: stages 0 and 1 in flight, stage 0's first half in set A
-  issue(0);
-  issue(1);
-  wait_vm<16>();  // stage 0 landed (stage 1's 16 DMAs may still fly)
-  barrier();
-  bf16x8 xa[FM], wa[FN], xb[FM], wb[FN];
-  read_frags(lds, 0, xa, wa);
-  int q = 0, cv = wg;
-  for (int tile = 0; tile < my_tiles; ++tile) {
-    // a nested k loop (accumulators zeroed once per tile, epilogue outside
-    // it): with the epilogue as a branch of one flat loop the compiler shuffled
-    // the 256 accumulators between AGPRs and VGPRs every stage
-    for (int kt = 0; kt < KT; ++kt, ++q) {
-      const int slot = q & 1;
-      // sched_barrier(0) pins each MFMA block between its LDS reads and the
-      // s_barrier: left free, hipcc sinks the MFMAs below the barrier (they
-      // touch no memory) and the wait for the reads it puts in front of the
-      // barrier then exposes their whole latency
-      // set A (read under the previous MFMA block) has landed: retire it here,
-      // in a form the waitcnt pass understands — with the 16 set-B reads in
-      // flight the wait it needs before MFMA(A) (lgkmcnt 16) is not encodable
-      // and it falls back to lgkmcnt(0), serialising the reads
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      read_frags(lds + slot * STAGE, 1, xb, wb);  // k 32-63 of stage q → set B
-      mfma_all(xa, wa);                           // k 0-31 from set A
-      // interleave: one LDS read per 4 MFMAs (16 + 64)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // stage q+1 landed and every wave has all of slot q in registers
-      wait_vm<0>();
-      barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // set B landed (under MFMA(A)): same reason as above
-      issue(slot);  // stage q+2 into the slot just drained
-      read_frags(lds + (slot ^ 1) * STAGE, 0, xa, wa);  // (past the last stage: unused)
-      mfma_all(xb, wb);  // k 32-63 from set B
-      // interleave: one DMA + one LDS read per 4 MFMAs (16 + 16 + 64); the
-      // DMA address VALU rides in the MFMA gaps
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);  // VMEM (global_load_lds)
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);  // DS read
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);  // MFMA
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // epilogue: acc[i][j][r] = C[m][n], m = 16j + (lane&15), n = 16i + 4(lane>>4) + r (wave-local)
-    const int64_t mt = static_cast<int64_t>(cv / tn) * BM + wm * 128;
-    // opaque lane id: the epilogue's per-lane address math is redone per tile
-    // instead of being hoisted out of the k loop into registers that the
-    // loop's 128 fragment registers push to scratch (whose reloads then put
-    // a vmcnt(0) — a full DMA drain — into the k loop)
-    int el = lane;
-    asm volatile("" : "+v"(el));
-#pragma unroll
-    for (int h = 0; h < FM / 2; ++h) {
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int j = 2 * h + jj;
-        const int row = jj * 16 + (el & 15);
-#pragma unroll
-        for (int i = 0; i < FN; ++i) {
-          const int col = i * 16 + (el >> 4) * 4;
-          const int chunk = (col >> 3) ^ (row & 7);
-          *reinterpret_cast<uint2*>(cst + row * (WN * 2) + chunk * 16 + (col & 7) * 2) =
-              make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-#pragma unroll
-      for (int it = 0; it < 32 / RPI; ++it) {
-        const int row = it * RPI + el / LPR;
-        const int c = el % LPR;
-        const uint4 v = *reinterpret_cast<const uint4*>(cst + row * (WN * 2) + 16 * (c ^ (row & 7)));
-        const int64_t m = mt + 32 * h + row;
-        if (m < M) {
-          *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) = v;
-          if (STATS) {
-            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const float a = bf_lo(w4[k]), b = bf_hi(w4[k]);
-              ssum[2 * k] += a;
-              ssq[2 * k] = fmaf(a, a, ssq[2 * k]);
-              ssum[2 * k + 1] += b;
-              ssq[2 * k + 1] = fmaf(b, b, ssq[2 * k + 1]);
-            }
-          }
-        }
-      }
-    }
-    cv += P;
-  }
-  wait_vm<0>();  // the two trailing (unused) stages' DMAs land before the waves retire
-  if (STATS) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-#pragma unroll
-      for (int o = LPR; o < 64; o <<= 1) {
-        ssum[e] += __shfl_xor(ssum[e], o);
-        ssq[e] += __shfl_xor(ssq[e], o);
-      }
-    __syncthreads();  // ring idle: reuse it
-    float* red = reinterpret_cast<float*>(lds);  // [sum|sq][wm][BN]
-    if (lane < LPR) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = wn * WN + lane * 8 + e;
-        red[wm * BN + c] = ssum[e];
-        red[2 * BN + wm * BN + c] = ssq[e];
-      }
-    }
-    __syncthreads();
-    if (t < BN) {
-      atomicAdd(stats + n0 + t, red[t] + red[BN + t]);
-      atomicAdd(stats + N + n0 + t, red[2 * BN + t] + red[3 * BN + t]);
-    }
-  }
-}
+// (A four-wave 256 x 256 variant — one wave of 128 x 128 per SIMD, AGPR
+// accumulators, double-buffered fragment sets, DMA / LDS / MFMA interleaved by
+// sched_group_barrier — measured 8-40 % slower than the 128 x 128 ring on every
+// ResNet-50 shape: profiles/r3_gemm_ab_big4.jsonl. Removed; in git history.)
 
 // ------------------------------------------------------------- wgrad ----
 // Stage image: [32 m][W channels] bf16, rows of 2W bytes; 32-B pair index
@@ -1888,7 +1639,8 @@ inline int nt_bm(int64_t M, int tn, int BN, bool pro, int K, bool gather) {
 // that cannot become resident because RCCL holds its CU delays its whole share
 // of tiles (NOTES §22; env DCP_RESERVE_CUS sets the initial value).
 namespace {
-int g_nt_big = 0;
+// 256 x 256 tiles: 0 off, 2 on every eligible shape, 4 where they measured faster (default)
+int g_nt_big = 4;
 int g_reserve_cus = [] {
   const char* v = getenv("DCP_RESERVE_CUS");
   const int r = v ? atoi(v) : 0;
@@ -1988,11 +1740,10 @@ void gemm_nt_launch_bm(const void* A, const void* B, void* C, int64_t M, int N, 
 #undef DK_GNT
 }
 
-// 256 x 256 tiles: 2 x 4 waves of 128 x 64, one
-// workgroup per CU (persistent beyond 256 tiles), BKB-deep stages on an
-// NSB-slot ring (BKB * NSB = 128: 128 KB) with the C staging aliased into it.
-// BKB = 32 / NSB = 4: two stages (~2,000 MFMA cycles per wave) in flight
-// across every barrier and one 32-k half of fragments live at a time.
+// 256 x 256 tiles: 2 x 4 waves of 128 x 64, one workgroup per CU (persistent
+// beyond grid_cus() tiles), BKB-deep stages on an NSB-slot ring (BKB * NSB =
+// 128: 128 KB) with the C staging aliased into it. Used as BKB = 64 / NSB = 2
+// (a 32-deep 4-slot ring measured equal: profiles/r3_gemm_ab_big.jsonl).
 template <bool GATHER, int BKB, int NSB>
 void gemm_nt_launch_big(const void* A, const void* B, void* C, int64_t M, int N, int K, float* stats,
                         const ConvGeo& geo, hipStream_t s) {
@@ -2023,44 +1774,22 @@ void gemm_nt_launch_big(const void* A, const void* B, void* C, int64_t M, int N,
                        lds, s, a, b, c, M, N, K, nullptr, nullptr, 0, stats, tiles_m, tn, geo, BnRedArgs{});
 }
 
-// the four-wave 256 x 256 kernel (gemm_nt_big4_kernel): 160 KB of LDS, one
-// workgroup per CU, persistent beyond grid_cus() tiles
-void gemm_nt_launch_big4(const void* A, const void* B, void* C, int64_t M, int N, int K, float* stats, hipStream_t s) {
-  const int tiles_m = static_cast<int>((M + 255) / 256);
-  const int tn = N / 256;
-  const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
-  const int kRes = grid_cus();
-  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
-  if (P < tn) P = tn;
-  const size_t lds = 2 * 65536 + 4 * 32 * 128 * 2;
-  static const bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_big4_kernel<0>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_big4_kernel<1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return true;
-  }();
-  (void)attr;
-  auto a = static_cast<const uint16_t*>(A);
-  auto b = static_cast<const uint16_t*>(B);
-  auto c = static_cast<uint16_t*>(C);
-  if (stats)
-    hipLaunchKernelGGL(gemm_nt_big4_kernel<1>, dim3(P), dim3(kB4Threads), lds, s, a, b, c, M, N, K, stats, tiles_m, tn);
-  else
-    hipLaunchKernelGGL(gemm_nt_big4_kernel<0>, dim3(P), dim3(kB4Threads), lds, s, a, b, c, M, N, K, stats, tiles_m, tn);
+// nt_big = 4: the 256 x 256 tile only where it measured faster than the
+// 128 x 128 ring (profiles/r3_gemm_ab_big.jsonl, ResNet-50 b512): every shape
+// with M >= 256 K rows (56x56 / 28x28: 4-22 % faster), and at fewer rows N = 512
+// with K >= 1024 or N = 1024 with K = 512 (3-18 %); it loses 2-10 % on the
+// 14x14 / 7x7 shapes with N = 256, N = 2048 or K = 256 (too few or too short tiles).
+inline bool big_tile_wins(int64_t M, int N, int K) {
+  return M >= 262144 || (N == 512 && K >= 1024) || (N == 1024 && K == 512);
 }
 
 template <bool GATHER, int BK>
 void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                        const float* shift, bool relu, float* stats, const ConvGeo& geo, const BnRedArgs* red,
                        hipStream_t s, bool scatter2 = false, bool parity = false) {
-  if (g_nt_big && BK == 64 && N % 256 == 0 && scale == nullptr && red == nullptr && !scatter2 && !parity) {
-    if (g_nt_big == 3 && !GATHER) {
-      gemm_nt_launch_big4(A, B, C, M, N, K, stats, s);
-      return;
-    }
-    if (g_nt_big == 2) gemm_nt_launch_big<GATHER, 64, 2>(A, B, C, M, N, K, stats, geo, s);
-    else gemm_nt_launch_big<GATHER, 32, 4>(A, B, C, M, N, K, stats, geo, s);
+  if ((g_nt_big == 2 || g_nt_big == 4) && BK == 64 && N % 256 == 0 && scale == nullptr && red == nullptr && !scatter2 && !parity &&
+      (g_nt_big != 4 || big_tile_wins(M, N, K))) {
+    gemm_nt_launch_big<GATHER, 64, 2>(A, B, C, M, N, K, stats, geo, s);
     return;
   }
   const int BN = N % 128 == 0 ? 128 : 64;

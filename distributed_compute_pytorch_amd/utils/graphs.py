@@ -97,9 +97,13 @@ class CapturedStep:
     def recapture(self, warmup: int = 0):
         """Capture again (e.g. after an LR change: the fused optimizers take
         hyper-parameters as kernel arguments). No warmup by default: capture
-        itself executes nothing, so parameters are not advanced."""
-        self.graph = None
+        itself executes nothing, so parameters are not advanced. The old graph
+        stays alive until the new one is captured: a shared ``pool`` must be
+        held by at least one graph when a capture begins into it (the caching
+        allocator asserts on a pool whose last graph was destroyed)."""
+        old = self.graph
         self._capture(warmup)
+        del old
 
     def __call__(self, *inputs: torch.Tensor):
         for dst, src in zip(self.static_inputs, inputs):

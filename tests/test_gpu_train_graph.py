@@ -1,7 +1,9 @@
 """train.py --hip-graph on the GPU: the DDP model / optimizer are built and
 every step runs on the capture side stream, step 3 is captured and replayed,
 the LR schedule re-captures at the epoch boundary. The replayed run must
-train like the eager run of the same config (same data, init and seeds)."""
+train like the eager run of the same config (same data, init and seeds).
+The MLP workload: no dropout, whose masks legitimately differ between eager
+(a host seed per call) and replays (a device Philox counter per replay)."""
 import json
 import os
 import subprocess
@@ -20,7 +22,7 @@ def _train(tmp_path, tag, extra):
         env.pop(k, None)
     out = tmp_path / f"{tag}.pt"
     r = subprocess.run([sys.executable, "-m", "distributed_compute_pytorch_amd.train", "--gpus", "1", "--model",
-                        "convnet", "--epochs", "2", "--steps-per-epoch", "6", "--log-every", "1", "--batch-size", "64",
+                        "mlp", "--epochs", "2", "--steps-per-epoch", "6", "--log-every", "1", "--batch-size", "64",
                         "--save-model", str(out)] + extra, capture_output=True, text=True, cwd=tmp_path, env=env,
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
