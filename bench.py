@@ -188,8 +188,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     torch.backends.cudnn.benchmark = bool(a.benchmark_cudnn)
-    if "MASTER_ADDR" not in os.environ:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
+    if "WORLD_SIZE" not in os.environ:  # a plain single-process run
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(29400 + (os.getpid() % 1000)))
         os.environ["RANK"] = "0"
         os.environ["WORLD_SIZE"] = "1"

@@ -114,6 +114,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("barrier", &Communicator::barrier, py::call_guard<py::gil_scoped_release>())
       .def("abort", &Communicator::abort)
       .def("stream_fence", &Communicator::stream_fence, py::call_guard<py::gil_scoped_release>())
+      .def("register_buffer", &Communicator::register_buffer, py::arg("tensor"))
+      .def("deregister_buffer", &Communicator::deregister_buffer, py::arg("handle"))
       .def("emulate_all_reduce", &Communicator::emulate_all_reduce, py::arg("t"), py::arg("world"),
            py::arg("busbw_gbps"), py::arg("channels"), py::arg("alpha_us") = 20.0,
            py::call_guard<py::gil_scoped_release>())
@@ -148,6 +150,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("tail_bucket_bytes", &ReducerOptions::tail_bucket_bytes)
       .def_readwrite("comm_dtype", &ReducerOptions::comm_dtype)
       .def_readwrite("average", &ReducerOptions::average)
+      .def_readwrite("register_buckets", &ReducerOptions::register_buckets)
       .def_readwrite("check_streams", &ReducerOptions::check_streams);
 
   m.def("trace_enabled", &trace::enabled);

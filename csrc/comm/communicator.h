@@ -78,6 +78,12 @@ class Communicator {
   // (a stalled caller stream looks like a hung collective). Host backend:
   // nullptr (no device stream).
   virtual std::shared_ptr<Work> stream_fence() { return nullptr; }
+  // Long-lived buffer registration with the collective library (RCCL
+  // ncclCommRegister: lets its intra-node paths read / write the user buffer
+  // directly instead of staging through its own FIFO buffers). Returns a
+  // handle id (0: nothing registered — one rank, or a backend without it).
+  virtual int64_t register_buffer(const at::Tensor&) { return 0; }
+  virtual void deregister_buffer(int64_t) {}
   // Contention emulation of an all-reduce of `t` among `world` ranks on a
   // single GPU (bench.py --emulate-world): `channels` workgroups on the
   // collective stream move the ring all-reduce's 2(world-1)/world × bytes

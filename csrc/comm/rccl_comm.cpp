@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <map>
+
 #include <condition_variable>
 #include <list>
 #include <thread>
@@ -134,6 +136,9 @@ class RcclCommunicator : public Communicator {
     cv_.notify_all();
     if (watchdog_.joinable()) watchdog_.join();
     if (ready_) (void)hipEventDestroy(ready_);
+    if (comm_ && !aborted_.load())
+      for (auto& kv : regs_) (void)ncclCommDeregister(comm_, kv.second.first);
+    regs_.clear();
     if (comm_) {
       if (aborted_.load()) {
         // already aborted
@@ -233,6 +238,34 @@ class RcclCommunicator : public Communicator {
     return launch({t, scratch}, [&](hipStream_t s) {
       kern::comm_emulate(t.data_ptr(), scratch.data_ptr(), bytes, static_cast<int64_t>(move), channels, us, s);
     });
+  }
+
+  int64_t register_buffer(const at::Tensor& t) override {
+    check_tensor(t);
+    if (size_ == 1 && !single_rank_hop_) return 0;  // no collective ever touches it
+    raise_if_error();
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+    void* h = nullptr;
+    NCCL_OK(ncclCommRegister(comm_, t.data_ptr(), static_cast<size_t>(t.numel()) * t.element_size(), &h));
+    std::lock_guard<std::mutex> g(mu_);
+    const int64_t id = ++next_reg_;
+    regs_[id] = {h, t};  // the tensor keeps the registered memory alive
+    return id;
+  }
+
+  void deregister_buffer(int64_t id) override {
+    std::pair<void*, at::Tensor> r;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = regs_.find(id);
+      if (it == regs_.end()) return;
+      r = it->second;
+      regs_.erase(it);
+    }
+    if (!aborted_.load()) {
+      c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+      (void)ncclCommDeregister(comm_, r.first);
+    }
   }
 
   WorkPtr stream_fence() override {
@@ -389,6 +422,8 @@ class RcclCommunicator : public Communicator {
   at::Tensor barrier_buf_;
   at::Tensor emu_scratch_;
   hipEvent_t ready_ = nullptr;
+  std::map<int64_t, std::pair<void*, at::Tensor>> regs_;  // register_buffer handles
+  int64_t next_reg_ = 0;
 };
 
 RcclWork::RcclWork(RcclCommunicator* comm, hipStream_t, int device, int64_t timeout_ms, bool timing)

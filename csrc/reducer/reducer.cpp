@@ -123,6 +123,7 @@ double Reducer::exposed_comm_ms() {
 }
 
 Reducer::~Reducer() {
+  release_registrations();
   if (used_ev_) (void)hipEventDestroy(used_ev_);
   if (ev_bwd_end_) (void)hipEventDestroy(ev_bwd_end_);
   if (ev_final_) (void)hipEventDestroy(ev_final_);
@@ -167,8 +168,20 @@ void Reducer::build_buckets(const std::vector<std::vector<int64_t>>& assignment)
     out.push_back(std::move(b));
   }
   for (size_t i = 0; i < params_.size(); ++i) DK_CHECK(seen[i], "Reducer: parameter ", i, " not in any bucket");
+  release_registrations();
   buckets_ = std::move(out);
   next_bucket_ = 0;
+  if (opts_.register_buckets && comm_)
+    for (auto& b : buckets_) {
+      const int64_t h = comm_->register_buffer(b.wire);
+      if (h) reg_handles_.push_back(h);
+    }
+}
+
+void Reducer::release_registrations() {
+  if (comm_)
+    for (int64_t h : reg_handles_) comm_->deregister_buffer(h);
+  reg_handles_.clear();
 }
 
 void Reducer::register_hooks() {

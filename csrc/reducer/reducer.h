@@ -59,6 +59,9 @@ struct ReducerOptions {
   at::ScalarType comm_dtype = at::ScalarType::Undefined;
   // false -> SUM instead of AVG (for custom hooks that pre-scale).
   bool average = true;
+  // register every bucket's wire buffer with the communicator (RCCL
+  // ncclCommRegister) for the Reducer's lifetime; released on a rebuild
+  bool register_buckets = false;
   // Debug (SURVEY §5.2 "stream-ordering asserts"; also DCP_DEBUG_STREAMS=1):
   // per bucket, a checksum of the packed wire buffer taken on the compute
   // stream right after the pack, all-reduced over the world, must equal the
@@ -149,6 +152,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
   std::vector<at::Tensor> params_;
   std::shared_ptr<Communicator> comm_;
+  std::vector<int64_t> reg_handles_;  // register_buckets handles
+  void release_registrations();
   ReducerOptions opts_;
   CommHook comm_hook_;
   at::ScalarType hook_wire_ = at::ScalarType::Undefined;

@@ -92,7 +92,8 @@ class DistributedDataParallel(nn.Module):
                  find_unused_parameters: bool = False, check_reduction: bool = False,
                  gradient_as_bucket_view: bool = False, static_graph: bool = False,
                  first_bucket_mb: Optional[float] = None, comm_dtype: Optional[torch.dtype] = None,
-                 rebuild_buckets: bool = True, init_sync: bool = True, tail_bucket_mb: Optional[float] = None):
+                 rebuild_buckets: bool = True, init_sync: bool = True, tail_bucket_mb: Optional[float] = None,
+                 register_buckets: bool = False):
         super().__init__()
         self.module = module
         self.process_group = process_group if process_group is not None else dist.get_default_group()
@@ -149,6 +150,10 @@ class DistributedDataParallel(nn.Module):
         opts.tail_bucket_bytes = self.tail_bucket_bytes
         if comm_dtype is not None:
             opts.comm_dtype = comm_dtype
+        # register_buckets: the bucket buffers are registered with RCCL
+        # (ncclCommRegister) once per bucket plan — zero-copy user-buffer paths
+        # where RCCL has them; a no-op on one rank and on gloo
+        opts.register_buckets = bool(register_buckets)
         self._comm = pg.comm_for(params[0])
         self.reducer = _C.Reducer(params, plan, self._comm, opts)
         self._comm_hook = None

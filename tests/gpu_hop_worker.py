@@ -81,7 +81,8 @@ def main():
     base = ConvNet().to(dev)
     results = {}
     for name, kw in (("fp32", {}), ("bf16_wire", {"comm_dtype": torch.bfloat16}),
-                     ("grad_view", {"gradient_as_bucket_view": True})):
+                     ("grad_view", {"gradient_as_bucket_view": True}),
+                     ("registered", {"gradient_as_bucket_view": True, "register_buckets": True})):
         local = ConvNet().to(dev)
         local.load_state_dict(base.state_dict())
         mine = ConvNet().to(dev)
@@ -107,6 +108,15 @@ def main():
         results[name + "_buckets"] = info["num_buckets"]
         del ddp
     res["ddp_max_abs_err"] = results
+    # explicit registration round trip on the communicator
+    buf = torch.randn(1 << 20, device=dev)
+    h = comm.register_buffer(buf)
+    res["register_handle"] = int(h)
+    want = buf.clone()
+    dcp.distributed.all_reduce(buf, dcp.distributed.ReduceOp.SUM)  # on the registered buffer
+    torch.cuda.synchronize()
+    res["registered_allreduce_ok"] = bool(torch.equal(buf, want))
+    comm.deregister_buffer(h)
 
     # ---- find_unused_parameters through the device used-map
     class Branchy(nn.Module):

@@ -35,6 +35,8 @@ def test_single_rank_hop_real_rccl(cuda):
     assert errs["grad_view"] < 1e-5, errs
     assert errs["bf16_wire"] < 5e-2, errs  # bf16 gradients on the wire
     assert errs["fp32_buckets"] >= 2
+    assert errs["registered"] < 1e-5, errs  # bucket buffers registered with ncclCommRegister
+    assert res["register_handle"] > 0 and res["registered_allreduce_ok"]
     assert res["unused_ok"] and res["globally_unused_grad_none"]
 
 

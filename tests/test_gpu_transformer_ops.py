@@ -299,7 +299,11 @@ def test_fused_linear_in_place_accumulation_and_weight_cache(cuda):
     opt.step()
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y1 = a(xs[0])
-    ref = F.linear(xs[0].to(torch.bfloat16), a.weight.to(torch.bfloat16), a.bias.to(torch.bfloat16))
+    # the same GEMM on a freshly cast weight: bit-equal iff the cache followed the step
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    ref = _C.linear_fwd(xs[0].to(torch.bfloat16).contiguous(), a.weight.detach().to(torch.bfloat16),
+                        a.bias.detach().float().contiguous(), 0)[0]
     assert not torch.equal(y0, y1)
     torch.testing.assert_close(y1, ref, rtol=0, atol=0)
 
