@@ -116,7 +116,7 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
 double Reducer::exposed_comm_ms() {
   std::lock_guard<std::mutex> g(mu_);
   if (!timing_ || !ev_recorded_) return -1.0;
-  if (hipEventQuery(ev_final_) != hipSuccess) return -1.0;
+  if (hipEventSynchronize(ev_final_) != hipSuccess) return -1.0;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, ev_bwd_end_, ev_final_) != hipSuccess) return -1.0;
   return ms;
@@ -403,7 +403,9 @@ void Reducer::finalize() {
   }
   for (auto& b : buckets_) {
     b.work->wait();
-    if (cap == hipStreamCaptureStatusNone) b.stats.comm_ms = b.work->elapsed_ms();
+    // the collective may still be running (wait() only orders the compute
+    // stream): keep the Work, bucket_stats() resolves its events when read
+    if (timing_ && cap == hipStreamCaptureStatusNone) b.timed_work = b.work;
     if (check_ && b.check_work) {
       b.check_work->wait();
       // what the compute stream sees now vs what the collective must have produced
@@ -609,9 +611,17 @@ std::vector<int64_t> Reducer::bucket_sizes_bytes() const {
   return r;
 }
 
-std::vector<BucketStats> Reducer::bucket_stats() const {
+std::vector<BucketStats> Reducer::bucket_stats() {
+  std::lock_guard<std::mutex> g(mu_);
   std::vector<BucketStats> r;
-  for (auto& b : buckets_) r.push_back(b.stats);
+  for (auto& b : buckets_) {
+    if (b.timed_work) {
+      b.timed_work->synchronize();
+      b.stats.comm_ms = b.timed_work->elapsed_ms();
+      b.timed_work.reset();
+    }
+    r.push_back(b.stats);
+  }
   return r;
 }
 

@@ -107,7 +107,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
   std::vector<std::vector<int64_t>> bucket_indices() const;
   std::vector<int64_t> bucket_sizes_bytes() const;
-  std::vector<BucketStats> bucket_stats() const;
+  std::vector<BucketStats> bucket_stats();
   // DCP_COMM_TIMING=1 on a GPU: device time between the end of the backward
   // compute and the point where every bucket's reduction has landed in the
   // last finished iteration = communication NOT hidden behind backward.
@@ -133,6 +133,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     int pending = 0;
     bool launched = false;
     WorkPtr work;
+    WorkPtr timed_work;  // last finished collective, its elapsed time read lazily (bucket_stats)
     BucketStats stats;
     at::Tensor check_sum;  // check_streams: fp64 [1] checksum of the packed buffer (all-reduced)
     WorkPtr check_work;
