@@ -97,6 +97,9 @@ def parse():
     ap.add_argument("--emulate-channels", type=int, default=16, help="emulated RCCL channels (workgroups)")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the persistent GEMM / conv grids leave free for collectives (DCP_RESERVE_CUS)")
+    ap.add_argument("--linear-path", choices=["ours", "aten-fwd", "aten"], default="ours",
+                    help="transformer Linear forward / data-gradient GEMMs: ours (gemm_nt + fused epilogues), "
+                         "aten-fwd (forward on hipBLASLt), aten (forward and dgrad on hipBLASLt)")
     ap.add_argument("--gemm-tune", default=None,
                     help="k=v[,k=v] entries of the GEMM launcher tuning table (_C.gemm_tune, e.g. nt_big=4)")
     return ap.parse_args()
@@ -207,6 +210,11 @@ def main():
             k, v = kv.split("=")
             _C.gemm_tune(k.strip(), int(v))
             tune[k.strip()] = _C.gemm_tune_get(k.strip())
+    if a.linear_path != "ours":
+        from distributed_compute_pytorch_amd.ops import linear as _lin
+
+        _lin._OUR_FWD = False
+        _lin._OUR_DGRAD = a.linear_path == "aten-fwd"
     torch.manual_seed(0)
     wl = workloads.build(a.model, dev, batch=a.batch, fused=fused, seq_len=a.seq_len, accum=a.accum,
                          channels_last=bool(a.channels_last), fused_gemm=bool(a.gemm))
@@ -316,6 +324,8 @@ def main():
                 cfg["reserve_cus"] = a.reserve_cus
             if tune:
                 cfg["gemm_tune"] = tune
+            if a.linear_path != "ours":
+                cfg["linear_path"] = a.linear_path
             if ours:
                 cfg["bucket_cap_mb"] = round(info["bucket_cap_bytes"] / 2**20, 3)
                 cfg["first_bucket_mb"] = round(info["first_bucket_bytes"] / 2**20, 3)

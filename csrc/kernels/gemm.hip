@@ -117,6 +117,59 @@ __device__ __forceinline__ int nt_swzk(int r) {
   else return nt_swz(r);
 }
 
+// One 32-k half of a gemm_nt stage: the wave's FM A-fragments (16 rows each)
+// and FN B-fragments from the swizzled stage image, and their MFMAs.
+template <int FM, int FN, int RB, int BK, int WR, int WN>
+__device__ __forceinline__ void nt_read_frags(const char* sA, const char* sB, int lch, int wm, int wn, int lane,
+                                              bf16x8 (&xf)[FM], bf16x8 (&wf)[FN]) {
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const int r = wm * WR + j * 16 + (lane & 15);
+    xf[j] = *reinterpret_cast<const bf16x8*>(sA + r * RB + 16 * (lch ^ nt_swzk<BK>(r)));
+  }
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int r = wn * WN + i * 16 + (lane & 15);
+    wf[i] = *reinterpret_cast<const bf16x8*>(sB + r * RB + 16 * (lch ^ nt_swzk<BK>(r)));
+  }
+}
+template <int FM, int FN>
+__device__ __forceinline__ void nt_mfma(f32x4 (&acc)[FN][FM], const bf16x8 (&xf)[FM], const bf16x8 (&wf)[FN]) {
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+}
+
+// The MFMAs of one half (xf, wf) with the reads of the next stage's first
+// half (into nx, nw) interleaved one per MFMA and pinned in that order: the
+// compiler's lgkmcnt wait for (xf, wf) then sits before the first MFMA, ahead
+// of every new read, instead of draining the new reads too.
+template <int FM, int FN, int RB, int BK, int WR, int WN>
+__device__ __forceinline__ void nt_mfma_read(f32x4 (&acc)[FN][FM], const bf16x8 (&xf)[FM], const bf16x8 (&wf)[FN],
+                                             const char* sA, const char* sB, int lch, int wm, int wn, int lane,
+                                             bf16x8 (&nx)[FM], bf16x8 (&nw)[FN]) {
+  static_assert(FM + FN <= FM * FN, "more reads than MFMAs");
+#pragma unroll
+  for (int t = 0; t < FN * FM; ++t) {
+    const int i = t / FM, j = t % FM;
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+    if (t < FM) {
+      const int r = wm * WR + t * 16 + (lane & 15);
+      nx[t] = *reinterpret_cast<const bf16x8*>(sA + r * RB + 16 * (lch ^ nt_swzk<BK>(r)));
+    } else if (t < FM + FN) {
+      const int r = wn * WN + (t - FM) * 16 + (lane & 15);
+      nw[t - FM] = *reinterpret_cast<const bf16x8*>(sB + r * RB + 16 * (lch ^ nt_swzk<BK>(r)));
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < FM + FN; ++t) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one DS read
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, FN * FM - FM - FN, 0);
+}
+
 // Convolution geometry of the gathered (implicit-GEMM) kernels. wgrad: B rows
 // are the input pixels under tap (dy, dx) = (blockIdx.z / kw, blockIdx.z % kw)
 // of each output pixel. fwd (gemm_nt GATHER): A row m = output pixel, k =
@@ -490,10 +543,56 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
 
   const int ck = lane >> 4;  // logical 16-B chunk (k = 8ck … 8ck+7) this lane reads
   int kt = 0, slot = 0, cv = wg;  // consumer k-step, ring slot, tile id
+  // PIPE (BK = 64 on the private-staging ring, no prologue): fragment reads
+  // software-pipelined one 32-k half ahead of the MFMAs, and the stage barrier
+  // moved in front of the stage's LAST half: the MFMAs of that half run while
+  // the next stage's first fragments are in flight, so neither the LDS read
+  // latency nor the barrier leave the matrix pipe idle. vm counting: at the
+  // barrier before stage nq the ops younger than nq's DMA are the DMA of the
+  // kNSnt-2 later stages and the epilogue stores of stages nq-kNSnt…nq-2
+  // (the epilogue of stage nq-1 comes after this barrier): hist bit i = stage
+  // nq-2-i ended a tile.
+  constexpr bool PIPE = NS == 0 && BK == 64 && !PRO;
+  uint32_t hist = 0;
+  auto pipe_wait = [&](int nq) {
+    if (nq + kNSnt - 2 < T) {
+      const int ends = __builtin_popcount(hist & ((1u << (kNSnt - 1)) - 1u));
+      if (ends == 0) wait_vm<(kNSnt - 2) * G>();
+      else if (ends == 1) wait_vm<(kNSnt - 2) * G + FS>();
+      else wait_vm<(kNSnt - 2) * G + 2 * FS>();
+    } else {
+      wait_vm<0>();
+    }
+  };
+  bf16x8 px0[PIPE ? FM : 1], pw0[PIPE ? FN : 1], px1[PIPE ? FM : 1], pw1[PIPE ? FN : 1];
+  if constexpr (PIPE) {
+    pipe_wait(0);
+    barrier();
+    issue();
+    nt_read_frags<FM, FN, RB, BK, WR, WN>(lds, lds + SA, ck, wm, wn, lane, px0, pw0);
+  }
   // (A staggered two-group variant of the 256 x 256 tile — waves 4-7 running
   // a stage's second half after the next barrier — measured slower, on the
   // gathered 3x3 shapes 2.3x: profiles/r3_gemm_ab_big.jsonl vs r3_gemm_ab_stag.jsonl.)
   for (int q = 0; q < T; ++q) {
+    if constexpr (PIPE) {
+      const char* sA = lds + slot * STAGE;
+      nt_read_frags<FM, FN, RB, BK, WR, WN>(sA, sA + SA, 4 + ck, wm, wn, lane, px1, pw1);
+      nt_mfma<FM, FN>(acc, px0, pw0);
+      if (q + 1 < T) {
+        // this wave's reads of slot q have landed (the DMA issued after the
+        // barrier may overwrite it), stage q+1 visible to all waves
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pipe_wait(q + 1);
+        barrier();
+        issue();
+      }
+      // (after the last stage the reads fetch a stale slot nobody consumes: one
+      // MFMA sequence for both cases keeps the accumulators in place — two
+      // branches with their own MFMAs cost a copy of every accumulator)
+      const char* nA = lds + (slot + 1 == kNSnt ? 0 : slot + 1) * STAGE;
+      nt_mfma_read<FM, FN, RB, BK, WR, WN>(acc, px1, pw1, nA, nA + SA, ck, wm, wn, lane, px0, pw0);
+    } else {
     // vmcnt retires in issue order: the ops younger than stage q's DMA are the
     // DMA of q+1 and the epilogue stores of a tile end at q-2 or q-1 (issued
     // after q's DMA) — counting them keeps the ring full across tile ends.
@@ -543,6 +642,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
         for (int j = 0; j < FM; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
     }
+    }
 
     if (kt == KT - 1) {
       if (CA) {
@@ -563,7 +663,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       // first use — one wait, twice the bytes in flight per wave (the epilogue
       // is latency-bound on these reads); per half for EPI 6 (registers)
       constexpr int NR = 32 / RPI;
-      constexpr int HB = X2 ? 1 : 2;  // halves loaded ahead
+      constexpr int HB = (X2 || PIPE) ? 1 : 2;  // halves loaded ahead (PIPE: registers hold the next fragments)
       uint4 xr[(RED || RR) ? HB * NR : 1], g2r[RR ? HB * NR : 1], x2r[X2 ? HB * NR : 1];
       uint32_t mbr[RR ? HB * NR : 1];
 #pragma unroll
@@ -704,6 +804,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
         }
       }
     }
+    if constexpr (PIPE) hist = (hist << 1) | (kt == KT - 1 ? 1u : 0u);
     slot = slot + 1 == kNSnt ? 0 : slot + 1;
     if (++kt == KT) {
       kt = 0;

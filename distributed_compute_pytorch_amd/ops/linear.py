@@ -27,6 +27,10 @@ from .._ext import C as _C
 
 # forward_gelu: Linear + bias + GELU with the fused GELU kernels (False: FusedLinear + ATen GELU)
 _FUSED_GELU = True
+# forward / data-gradient GEMMs on our gemm_nt (False: hipBLASLt through ATen;
+# bench.py --linear-path, for same-box A/Bs)
+_OUR_FWD = True
+_OUR_DGRAD = True
 # let the fused Adam/AdamW write the bf16 weight copies the forward GEMMs read
 # (False: one cast launch per weight per forward; NOTES §15)
 _SHADOWS = True
@@ -92,7 +96,7 @@ def _acc_target(ctx, p, shape):
 
 def _gemm_ok(x: torch.Tensor, w: torch.Tensor, bias) -> bool:
     """Shapes our gemm_nt takes (in/out features multiples of 64, ≤ 4096 in)."""
-    return (bias is not None and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and w.shape[1] <= 4096
+    return (_OUR_FWD and bias is not None and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and w.shape[1] <= 4096
             and x.is_contiguous())
 
 
@@ -139,7 +143,7 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
     x2 = x.reshape(-1, x.shape[-1])
     dx = dw = None
     if ctx.needs_input_grad[0]:
-        if wt is not None and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096 and wt.shape[0] % 64 == 0:
+        if _OUR_DGRAD and wt is not None and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096 and wt.shape[0] % 64 == 0:
             dx = _C.conv1x1_dgrad(g2, wt).view(x.shape)
         else:
             dx = (g2 @ w).view(x.shape)

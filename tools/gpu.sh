@@ -25,7 +25,7 @@ for step in "$@"; do
   echo "[gpu.sh] $TAG: $step"
   case $name in
     tests)
-      k=(); [[ -n "$val" ]] && k=(-k "$val")
+      k=(); [[ -n "$val" ]] && k=(-k "${val//,/ }")
       timeout -k 10 900 python3 -u -m pytest -x -v -m gpu --timeout 240 --timeout-method thread "${k[@]}" tests \
         > "$O/${TAG}_tests.log" 2>&1 || { tail -40 "$O/${TAG}_tests.log"; exit 1; }
       tail -3 "$O/${TAG}_tests.log" ;;
@@ -38,7 +38,10 @@ for step in "$@"; do
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/${TAG}_prof" -o prof -- \
         python3 "$R/bench.py" $(args "$val") > "$O/${TAG}_prof.log" 2>&1) || { tail -30 "$O/${TAG}_prof.log"; exit 1; }
-      grep '^{' "$O/${TAG}_prof.log" || true ;;
+      grep '^{' "$O/${TAG}_prof.log" || true
+      # keep the per-kernel summary, drop the (large) trace database
+      python3 "$R/tools/kernel_stats.py" "$O/${TAG}_prof/prof_results.db" --top 60 > "$O/${TAG}_kernel_stats.txt" 2>&1 || true
+      rm -rf "$O/${TAG}_prof" ;;
     pmc)
       ctr=${val%%:*}; rest=""; [[ "$val" == *:* ]] && rest=${val#*:}
       (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $(args "$ctr") --kernel-trace --stats -d "$O/${TAG}_pmc" -o pmc -- \
