@@ -49,6 +49,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int kT = 256;
+// wgrad slab plan (gemm_tune wg_slots / wg_cap): workgroups the split over M
+// aims for, and the slab traffic allowed relative to the operand traffic
+int g_wg_slots = 512;
+int g_wg_cap = 0;
 constexpr int kBK = 32;  // k per stage
 constexpr int kNS = 4;   // LDS ring stages
 
@@ -909,7 +913,7 @@ __device__ __forceinline__ bf16x8 mask_rows(bf16x8 v, int valid, int lane) {
 // zero-filled and not stored. The grid then has no tap dimension.
 // ldo: row stride of D in floats (taps * N2) — also where D's columns end.
 template <int BM, int BN, bool PRO, bool GATHER, int BK, int NSW = 0, int BMODE = 0>
-__global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+__global__ void __launch_bounds__(kT, 2) gemm_wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                         float* __restrict__ ws, int64_t M, int N1, int N2,
                                                         int64_t chunk, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int relu, int tiles_j,
@@ -1074,6 +1078,61 @@ __global__ void __launch_bounds__(kT) gemm_wgrad_kernel(const uint16_t* __restri
 
 #pragma unroll
   for (int q = 0; q < kNSw - 1; ++q) issue(q);
+  // PIPE (BK = 64, no prologue): as gemm_nt's — fragment reads one 32-row
+  // half ahead of the MFMAs, the barrier in front of each stage's last half,
+  // whose MFMAs overlap the next stage's first reads (pinned interleave)
+  constexpr bool PIPE = BK == 64 && !PRO;
+  bf16x8 pa0[PIPE ? FM : 1], pb0[PIPE ? FN : 1], pa1[PIPE ? FM : 1], pb1[PIPE ? FN : 1];
+  auto wread = [&](const char* st, int h, bf16x8 (&af)[PIPE ? FM : 1], bf16x8 (&bfr)[PIPE ? FN : 1]) {
+    const char* sA = st + h * 32 * BM * 2;
+    const char* sB = st + SA + h * 32 * BN * 2;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[PIPE ? i : 0] = tr_frag<BM>(sA, wi * (BM / 2) + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[PIPE ? j : 0] = tr_frag<BN>(sB, wj * (BN / 2) + j * 16, lane);
+  };
+  auto wmfma = [&](bf16x8 (&af)[PIPE ? FM : 1], const bf16x8 (&bfr)[PIPE ? FN : 1], int64_t vh) {
+    if (vh < 32) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[PIPE ? i : 0] = mask_rows(af[PIPE ? i : 0], vh < 0 ? 0 : static_cast<int>(vh), lane);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[PIPE ? i : 0], bfr[PIPE ? j : 0], acc[i][j], 0, 0, 0);
+  };
+  if constexpr (PIPE) {
+    if (T > 0) {
+      if (kNSw - 2 < T) wait_vm<(kNSw - 2) * G>();
+      else wait_vm<0>();
+      barrier();
+      issue(kNSw - 1);
+      wread(lds, 0, pa0, pb0);
+    }
+    for (int q = 0; q < T; ++q) {
+      const char* st = lds + (q % kNSw) * STAGE;
+      const int64_t valid = mz1 - (mz0 + static_cast<int64_t>(q) * BK);
+      wread(st, 1, pa1, pb1);
+      wmfma(pa0, pb0, valid);
+      if (q + 1 < T) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of slot q landed
+        if (q + 1 + kNSw - 2 < T) wait_vm<(kNSw - 2) * G>();
+        else wait_vm<0>();
+        barrier();
+        issue(q + kNSw);
+      }
+      // the next stage's first half (a stale slot after the last stage: never consumed)
+      wread(lds + ((q + 1) % kNSw) * STAGE, 0, pa0, pb0);
+      wmfma(pa1, pb1, valid - 32);
+#pragma unroll
+      for (int t2 = 0; t2 < 2 * (FM + FN); ++t2) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one DS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, FM * FN > 2 * (FM + FN) ? FM * FN - 2 * (FM + FN) : 0, 0);
+    }
+  } else
   for (int q = 0; q < T; ++q) {
     if (q + kNSw - 2 < T) wait_vm<(kNSw - 2) * G>();
     else wait_vm<0>();
@@ -1691,9 +1750,14 @@ WgradPlan wgrad_plan(int64_t M, int N1, int N2, int taps = 1) {
   p.tiles = (N1 / p.bm) * (N2 / p.bn);
   constexpr int kStep = 64;  // chunk granularity: whole stages at BK = 64 and 32
   const int64_t ksteps = (M + kStep - 1) / kStep;
-  int64_t S = 512 / (p.tiles * taps);  // ~2 blocks per CU
-  // keep the slab traffic (write + read) ≤ ~the operand traffic
-  const int64_t cap = (M * (N1 + static_cast<int64_t>(taps) * N2) * 2 / 2) / (static_cast<int64_t>(N1) * taps * N2 * 4);
+  int64_t S = g_wg_slots / (p.tiles * taps);  // ~2 blocks per CU
+  // keep the slab traffic (write + read) ≤ ~wg_cap x the operand traffic
+  // (wg_cap 0 = auto: 4x at M <= 64K rows — the transformer Linear shapes
+  // and ResNet's 7x7 layers, 10-30 % faster — else 1x: the 14x14-56x56
+  // shapes lose 3-8 % to the extra slab traffic; profiles/r3_wgrad_plan.jsonl)
+  const int64_t capx = g_wg_cap > 0 ? g_wg_cap : (M <= 65536 ? 4 : 1);
+  const int64_t cap = capx * (M * (N1 + static_cast<int64_t>(taps) * N2) * 2 / 2) /
+                      (static_cast<int64_t>(N1) * taps * N2 * 4);
   if (S > cap) S = cap;
   if (S > ksteps) S = ksteps;
   if (S < 1) S = 1;
@@ -1742,6 +1806,12 @@ inline int nt_bm(int64_t M, int tn, int BN, bool pro, int K, bool gather) {
 namespace {
 // 256 x 256 tiles: 0 off, 2 on every eligible shape, 4 where they measured faster (default)
 int g_nt_big = 4;
+// Linear forward epilogues (bias / bias + GELU) on 256 x 256 tiles: 0 never,
+// 1 when the tiles fill at least two rounds of the chip, 2 whenever N % 256 == 0
+int g_lin_big = 1;
+// 256 x 256 tiles on the private-staging ring with the pipelined stage loop (1)
+// instead of the C staging aliased into a ring slot (0)
+int g_big_pipe = 0;
 int g_reserve_cus = [] {
   const char* v = getenv("DCP_RESERVE_CUS");
   const int r = v ? atoi(v) : 0;
@@ -1753,11 +1823,19 @@ inline int grid_cus() { return 256 - g_reserve_cus; }
 void gemm_tune(const char* key, int value) {
   const std::string k(key);
   if (k == "nt_big") g_nt_big = value;
+  if (k == "lin_big") g_lin_big = value;
+  if (k == "big_pipe") g_big_pipe = value;
+  if (k == "wg_slots") g_wg_slots = value < 64 ? 64 : value;
+  if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
 }
 int gemm_tune_get(const char* key) {
   const std::string k(key);
   if (k == "nt_big") return g_nt_big;
+  if (k == "lin_big") return g_lin_big;
+  if (k == "big_pipe") return g_big_pipe;
+  if (k == "wg_slots") return g_wg_slots;
+  if (k == "wg_cap") return g_wg_cap;
   if (k == "reserve_cus") return g_reserve_cus;
   return -1;
 }
@@ -1855,7 +1933,10 @@ void gemm_nt_launch_big(const void* A, const void* B, void* C, int64_t M, int N,
   const int kRes = grid_cus();
   int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
   if (P < tn) P = tn;
-  const size_t lds = static_cast<size_t>(NSB) * (BM + BN) * BKB * 2;
+  // NSB = 0: the 2-slot ring plus private per-wave C staging (8 x 4 KB: 160 KB
+  // in all), which lets the stage loop software-pipeline (PIPE)
+  const size_t lds = NSB > 0 ? static_cast<size_t>(NSB) * (BM + BN) * BKB * 2
+                             : static_cast<size_t>(2) * (BM + BN) * BKB * 2 + 8 * 32 * 64 * 2;
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
@@ -1890,7 +1971,9 @@ void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, 
                        hipStream_t s, bool scatter2 = false, bool parity = false) {
   if ((g_nt_big == 2 || g_nt_big == 4) && BK == 64 && N % 256 == 0 && scale == nullptr && red == nullptr && !scatter2 && !parity &&
       (g_nt_big != 4 || big_tile_wins(M, N, K))) {
-    gemm_nt_launch_big<GATHER, 64, 2>(A, B, C, M, N, K, stats, geo, s);
+    // (the gathered variant of the pipelined loop spills: aliased staging only)
+    if (!GATHER && g_big_pipe) gemm_nt_launch_big<false, 64, 0>(A, B, C, M, N, K, stats, geo, s);
+    else gemm_nt_launch_big<GATHER, 64, 2>(A, B, C, M, N, K, stats, geo, s);
     return;
   }
   const int BN = N % 128 == 0 ? 128 : 64;
@@ -1951,8 +2034,55 @@ void gemm_nt_bias_launch(const void* A, const void* B, void* C, int64_t M, int N
 }
 }  // namespace
 
+// the Linear epilogues on the 256 x 256 tile (one workgroup per CU, C staging
+// aliased into the 2 x 64-deep ring), persistent as gemm_nt_launch_big
+template <int NSB>
+void gemm_nt_bias_launch_big(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* bias,
+                             void* c2, int gelu, hipStream_t s) {
+  constexpr int BM = 256, BN = 256, BKB = 64;
+  const int tiles_m = static_cast<int>((M + BM - 1) / BM);
+  const int tn = N / BN;
+  const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
+  const int kRes = grid_cus();
+  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
+  if (P < tn) P = tn;
+  const size_t lds = NSB > 0 ? static_cast<size_t>(NSB) * (BM + BN) * BKB * 2
+                             : static_cast<size_t>(2) * (BM + BN) * BKB * 2 + 8 * 32 * 64 * 2;
+  static const bool attr = [] {  // > 64 KB of dynamic LDS
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<BM, BN, false, 7, false, BKB, 0, NSB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<BM, BN, false, 8, false, BKB, 0, NSB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<BM, BN, false, 9, false, BKB, 0, NSB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  BnRedArgs r{};
+  r.bias = bias;
+  r.c2 = static_cast<uint16_t*>(c2);
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  auto c = static_cast<uint16_t*>(C);
+  const dim3 grid(P), block(nt_threads<BM, BN>());
+  if (gelu == 1)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 8, false, BKB, 0, NSB>), grid, block, lds, s, a, b, c, M, N, K,
+                       nullptr, nullptr, 0, nullptr, tiles_m, tn, ConvGeo{}, r);
+  else if (gelu == 2)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 9, false, BKB, 0, NSB>), grid, block, lds, s, a, b, c, M, N, K,
+                       nullptr, nullptr, 0, nullptr, tiles_m, tn, ConvGeo{}, r);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 7, false, BKB, 0, NSB>), grid, block, lds, s, a, b, c, M, N, K,
+                       nullptr, nullptr, 0, nullptr, tiles_m, tn, ConvGeo{}, r);
+}
+
 void gemm_nt_bias_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* bias, void* c2,
                        int gelu, hipStream_t s) {
+  if (g_lin_big && N % 256 == 0 && (g_lin_big == 2 || (M / 256) * (N / 256) >= 2 * grid_cus())) {
+    if (g_big_pipe) gemm_nt_bias_launch_big<0>(A, B, C, M, N, K, bias, c2, gelu, s);
+    else gemm_nt_bias_launch_big<2>(A, B, C, M, N, K, bias, c2, gelu, s);
+    return;
+  }
   if (N % 128 == 0) gemm_nt_bias_launch<128>(A, B, C, M, N, K, bias, c2, gelu, s);
   else gemm_nt_bias_launch<64>(A, B, C, M, N, K, bias, c2, gelu, s);
 }

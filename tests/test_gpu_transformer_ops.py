@@ -383,18 +383,25 @@ def test_adamw_writes_bf16_shadow_weights(cuda):
     assert fresh_bf16_shadow(a.weight) is None
 
 
+@pytest.mark.parametrize("lin_big", [0, 2])
 @pytest.mark.parametrize("gelu", [0, 1, 2])
-@pytest.mark.parametrize("rows,fin,fout", [(1000, 256, 192), (2048, 768, 2304), (333, 64, 128)])
-def test_linear_fwd_epilogues_match_fp32(cuda, gelu, rows, fin, fout):
+@pytest.mark.parametrize("rows,fin,fout", [(1000, 256, 192), (2048, 768, 2304), (333, 64, 128), (700, 128, 512)])
+def test_linear_fwd_epilogues_match_fp32(cuda, gelu, rows, fin, fout, lin_big):
     """gemm_nt's Linear epilogues (bias before the bf16 rounding; + GELU tanh /
-    erf from the rounded h) vs fp32 PyTorch on the same bf16 operands."""
+    erf from the rounded h) vs fp32 PyTorch on the same bf16 operands, on the
+    128-row tiles and (lin_big=2, N % 256 == 0) the 256 x 256 tiles."""
     from distributed_compute_pytorch_amd._ext import C
 
     g = torch.Generator().manual_seed(3)
     x = torch.randn(rows, fin, generator=g).to(torch.bfloat16).to(cuda)
     w = (torch.randn(fout, fin, generator=g) / fin ** 0.5).to(torch.bfloat16).to(cuda)
     b = torch.randn(fout, generator=g).to(cuda)
-    out = C.linear_fwd(x, w, b, gelu)
+    old = C.gemm_tune_get("lin_big")
+    C.gemm_tune("lin_big", lin_big)
+    try:
+        out = C.linear_fwd(x, w, b, gelu)
+    finally:
+        C.gemm_tune("lin_big", old)
     h_ref = x.float() @ w.float().t() + b
     h = out[-1]
     assert h.dtype == torch.bfloat16 and h.shape == (rows, fout)

@@ -10,6 +10,7 @@ pipeline, not the per-element MFMA order).
 """
 import argparse
 import json
+import re
 import os
 import statistics
 import sys
@@ -55,7 +56,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     bf, cl = torch.bfloat16, torch.channels_last
-    variants = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in v.split(",")) for v in a.variants]
+    variants = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in re.split("[,+]", v)) for v in a.variants]
     names = list(a.variants)
 
     def setv(v):

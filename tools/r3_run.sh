@@ -1,5 +1,3 @@
 #!/bin/bash
 set -eo pipefail
-bash tools/gpu.sh r3f_gpt2 prof=--model,gpt2,--steps,4,--warmup,3
-bash tools/gpu.sh r3f_bert prof=--model,bert,--steps,4,--warmup,3
-bash tools/gpu.sh r3f bench=--model,bert bench=--model,bert,--linear-path,aten-fwd bench=--model,bert,--linear-path,aten bench=--model,gpt2 bench=--model,gpt2,--linear-path,aten-fwd bench=--model,gpt2,--linear-path,aten
+bash tools/gpu.sh r3j tests=wgrad,or,conv1x1,or,transformer,or,numerics,or,fusions py=tools/linear_bench.py:--wgrad-only bench=--steps,20,--warmup,10 bench=--model,gpt2 bench=--model,bert
