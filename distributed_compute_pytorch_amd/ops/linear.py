@@ -31,6 +31,34 @@ _FUSED_GELU = True
 # bench.py --linear-path, for same-box A/Bs)
 _OUR_FWD = True
 _OUR_DGRAD = True
+# per GEMM shape, the first call (eager, not under HIP-graph capture) times our
+# kernel against hipBLASLt and keeps the faster one — as cudnn.benchmark does
+# for convolutions. Ours wins at GPT-2's 8,192 rows, hipBLASLt's 256-wide tiles
+# at BERT's 16,384 (profiles/r3_linear_fwd_dgrad_vs_blas.jsonl, NOTES §22).
+_AUTOTUNE = True
+_CHOICE: dict = {}
+
+
+def _time_ms(fn, iters: int = 3) -> float:
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e)
+
+
+def _prefer_ours(key, ours, aten) -> bool:
+    """True when our GEMM is (measured) at least as fast as ATen's for ``key``."""
+    c = _CHOICE.get(key)
+    if c is None:
+        if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
+            return True
+        with torch.no_grad():
+            c = _CHOICE[key] = _time_ms(ours) <= _time_ms(aten)
+    return c
 # let the fused Adam/AdamW write the bf16 weight copies the forward GEMMs read
 # (False: one cast launch per weight per forward; NOTES §15)
 _SHADOWS = True
@@ -111,7 +139,10 @@ class _LinearFn(torch.autograd.Function):
         x, w, b = _setup(ctx, x, weight, bias, w16, b16)
         ctx.save_for_backward(x, w, w16t)
         if _gemm_ok(x, w, bias):
-            return _C.linear_fwd(x, w, _bias32(bias), 0)[0]
+            x2, b32 = x.reshape(-1, x.shape[-1]), _bias32(bias)
+            if _prefer_ours(("fwd", x2.shape[0], w.shape[1], w.shape[0]), lambda: _C.linear_fwd(x2, w, b32, 0),
+                            lambda: F.linear(x2, w, b)):
+                return _C.linear_fwd(x, w, b32, 0)[0]
         return F.linear(x, w, b)
 
     @staticmethod
@@ -143,7 +174,9 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
     x2 = x.reshape(-1, x.shape[-1])
     dx = dw = None
     if ctx.needs_input_grad[0]:
-        if _OUR_DGRAD and wt is not None and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096 and wt.shape[0] % 64 == 0:
+        if (_OUR_DGRAD and wt is not None and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096 and wt.shape[0] % 64 == 0
+                and _prefer_ours(("dgrad", g2.shape[0], g2.shape[1], wt.shape[1]), lambda: _C.conv1x1_dgrad(g2, wt),
+                                 lambda: g2 @ w)):
             dx = _C.conv1x1_dgrad(g2, wt).view(x.shape)
         else:
             dx = (g2 @ w).view(x.shape)
@@ -180,8 +213,12 @@ class _LinearGeluFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, w16, b16, w16t, tanh_approx):
         x, w, b = _setup(ctx, x, weight, bias, w16, b16)
         ctx.tanh = tanh_approx
-        if _gemm_ok(x, w, bias):  # h and gelu(h) from one GEMM epilogue
-            y, h = _C.linear_fwd(x, w, _bias32(bias), 1 if tanh_approx else 2)
+        mode = 1 if tanh_approx else 2
+        x2 = x.reshape(-1, x.shape[-1])
+        if _gemm_ok(x, w, bias) and _prefer_ours(
+                ("fwd_gelu", x2.shape[0], w.shape[1], w.shape[0]), lambda: _C.linear_fwd(x2, w, _bias32(bias), mode),
+                lambda: _C.gelu_fwd(F.linear(x2, w, b), tanh_approx)):
+            y, h = _C.linear_fwd(x, w, _bias32(bias), mode)  # h and gelu(h) from one GEMM epilogue
         else:
             h = F.linear(x, w, b)
             y = _C.gelu_fwd(h, tanh_approx)

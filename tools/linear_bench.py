@@ -35,19 +35,25 @@ def timeit(fn, iters):
     return s.elapsed_time(e) * 1e3 / iters
 
 
-WG_VARIANTS = ["wg_cap=0", "wg_cap=1", "wg_cap=4", "wg_cap=1+wg_slots=768"]
+WG_VARIANTS = ["wg_cap=0", "wg_cap=1", "wg_cap=4"]
 
 
 def wgrad(model, M, K, N, x, gy, a):
     """dW [N, K] = gyᵀ x (fp32) — our split-M wgrad under each slab plan vs hipBLASLt."""
     fl = 2 * M * N * K
     rec = {"model": model, "M": M, "K": K, "N": N, "op": "wgrad"}
+    ref = None
     for kv in WG_VARIANTS:
         olds = {}
         for e in kv.split("+"):
             k, v = e.split("=")
             olds[k] = _C.gemm_tune_get(k)
             _C.gemm_tune(k, int(v))
+        out = _C.conv1x1_wgrad(gy, x)
+        if ref is None:
+            ref = out
+        else:
+            rec[kv + "_maxdiff"] = float((out - ref).abs().max())
         us = timeit(lambda: _C.conv1x1_wgrad(gy, x), a.iters)
         for k, v in olds.items():
             _C.gemm_tune(k, v)
