@@ -220,13 +220,13 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
         mx = fmaxf(mx, x);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float alpha = exp2f(m - mx);
+    const float alpha = __builtin_amdgcn_exp2f(m - mx);
     float rs = 0.f;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pp = exp2f(s[kh][r] - mx);
+        const float pp = __builtin_amdgcn_exp2f(s[kh][r] - mx);
         s[kh][r] = pp;
         rs += pp;
       }
@@ -368,7 +368,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        float p = exp2f(s[r] * c - lse2);
+        float p = __builtin_amdgcn_exp2f(s[r] * c - lse2);
         if (CAUSAL) p = key > qi ? 0.f : p;
         float g = dp[r];
         if (DROP) {
@@ -490,7 +490,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
             const int qrow = qb + rl + e;
-            float p = exp2f(s[r] * c - lv[e]);
+            float p = __builtin_amdgcn_exp2f(s[r] * c - lv[e]);
             if (CAUSAL) p = key > qrow ? 0.f : p;
             float gg = dp[r], pk = p;
             if (DROP) {

@@ -65,7 +65,12 @@ def _flags():
     common = ["-O3", "-fPIC", "-std=c++17", "-Wno-unused-parameter", "-Wno-deprecated-declarations"]
     cxx = ["g++"] + common + defs + incs + ["-fvisibility=hidden"]
     hip = (
-        [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+        # VGPR-form MFMA: accumulators in the unified VGPR file instead of
+        # AGPRs — the attention kernels' softmax / rescale no longer pays a
+        # v_accvgpr read + write per element (fwd VALU -26 %, dK/dV 332 → 199
+        # registers: two waves per SIMD instead of one; NOTES §22)
+        [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-mllvm",
+         "-amdgpu-mfma-vgpr-form"]
         + common
         + defs
         + incs

@@ -20,7 +20,7 @@ def main():
         co = src if src.endswith(".co") else os.path.join(d, "k.co")
         if co != src:
             subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "--offload-device-only", "--no-gpu-bundle-output", "-O3", "-std=c++17",
-                        "-munsafe-fp-atomics", f"-I{R}/csrc", "-I/opt/rocm/include", src, "-o", co],
+                        "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form", f"-I{R}/csrc", "-I/opt/rocm/include", src, "-o", co],
                            check=True)
         notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True,
                                check=True).stdout

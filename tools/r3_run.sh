@@ -1,3 +1,3 @@
 #!/bin/bash
 set -eo pipefail
-bash tools/gpu.sh r3n tests=transformer,or,models bench=--model,bert bench=--model,gpt2 bench=--model,bert,--linear-path,aten
+bash tools/gpu.sh r3p tests py=tools/attn_bench.py:--iters,10 bench=--model,gpt2 bench=--model,bert bench=--steps,20,--warmup,10 smoke
