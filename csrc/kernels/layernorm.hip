@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
                                                     const float* __restrict__ w, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, void* __restrict__ dx,
                                                     float* __restrict__ part, int64_t rows, int D,
-                                                    int rows_per_blk) {
+                                                    int rows_per_blk, const void* __restrict__ gres) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kWaves][2][D]
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -218,6 +218,12 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
           float o[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] = rs[r] * (dv[r][j][k] - m1 - xh[r][j][k] * m2);
+          if (gres) {  // the second consumer's gradient of x (dual-output LN): dx += gres
+            float gr[8];
+            L8<XD>::ld(gres, (rb + r) * D + vi * 8, gr);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] += gr[k];
+          }
           L8<XD>::st(dx, (rb + r) * D + vi * 8, o);
         }
       }
@@ -286,10 +292,11 @@ void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w,
 
 template <int XD, int YD>
 void bwd_dispatch(int vpl, dim3 g, size_t sm, hipStream_t s, const void* dy, const void* x, const float* w,
-                  const float* mean, const float* rstd, void* dx, float* part, int64_t rows, int D, int rpb) {
+                  const float* mean, const float* rstd, void* dx, float* part, int64_t rows, int D, int rpb,
+                  const void* gres) {
 #define DK_LNB(V) \
   hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, kRows>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, \
-                     rpb)
+                     rpb, gres)
   switch (vpl) {
     case 1: DK_LNB(1); break;
     case 2: DK_LNB(2); break;
@@ -331,17 +338,17 @@ void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const flo
 
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
                  const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
-                 hipStream_t s) {
+                 hipStream_t s, const void* gres) {
   const int nblk = ln_bwd_blocks(rows);
   const int rpb = static_cast<int>((rows + nblk - 1) / nblk);
   const size_t sm = sizeof(float) * kWaves * 2 * D;
   const int vpl = vpl_for(D);
   if (xdtype == LN_BF16)
-    bwd_dispatch<LN_BF16, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
+    bwd_dispatch<LN_BF16, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres);
   else if (ydtype == LN_BF16)
-    bwd_dispatch<LN_F32, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
+    bwd_dispatch<LN_F32, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres);
   else
-    bwd_dispatch<LN_F32, LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb);
+    bwd_dispatch<LN_F32, LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres);
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, part, nblk, D, dw, db, accum ? 1 : 0);
 }
 

@@ -99,6 +99,13 @@ class Block(nn.Module):
         self._dadd = dropout_add if cfg.fused else _plain_dropout_add
 
     def forward(self, x):
+        if isinstance(self.ln_1, FusedLayerNorm):
+            # dual-output LN: the residual stream's two gradients (branch + skip)
+            # are summed inside the LN backward kernel, not by an fp32 add
+            h, x = self.ln_1.forward_dual(x)
+            x = self._dadd(self.attn(h), x, self.p, self.training)
+            h, x = self.ln_2.forward_dual(x)
+            return self._dadd(self.mlp(h), x, self.p, self.training)
         x = self._dadd(self.attn(self.ln_1(x)), x, self.p, self.training)
         return self._dadd(self.mlp(self.ln_2(x)), x, self.p, self.training)
 

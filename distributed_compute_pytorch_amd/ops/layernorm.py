@@ -22,16 +22,26 @@ _LN_ACCUM = True
 
 
 class _LNFn(torch.autograd.Function):
+    """``dual=True``: also returns an alias of x as a second output — the
+    pre-LN residual stream's other consumer — whose gradient the backward adds
+    into dx inside the LN backward kernel (no separate fp32 add of the two
+    gradients of x: 25 per GPT-2 micro-step)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, out_dtype):
+    def forward(ctx, x, weight, bias, eps, out_dtype, dual=False):
         y, mean, rstd = _C.layer_norm_fwd(x, weight, bias, eps, out_dtype)
         ctx.save_for_backward(x, weight, bias, mean, rstd)
         ctx.params = (weight, bias)
         ctx.accum = accumulating()
+        ctx.dual = dual
+        if dual:
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dres=None):
+        if dy is None:  # only the residual alias was used
+            return dres, None, None, None, None, None
         x, weight, bias, mean, rstd = ctx.saved_tensors
         acc = None
         if _LN_ACCUM and weight is not None and bias is not None and ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
@@ -42,8 +52,9 @@ class _LNFn(torch.autograd.Function):
             tw, tb = _acc_target(ctx, ctx.params[0], D), _acc_target(ctx, ctx.params[1], D)
             if tw is not None and tb is not None:
                 acc = [tw, tb]
-        dx, dw, db = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd, accumulate_into=acc)
-        return dx, dw, db, None, None
+        dx, dw, db = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd, accumulate_into=acc,
+                                       grad_residual=dres if ctx.dual else None)
+        return dx, dw, db, None, None, None
 
 
 def fused_layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
@@ -59,6 +70,26 @@ def fused_layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
     return F.layer_norm(x, normalized_shape, weight, bias, eps)
 
 
+def fused_layer_norm_dual(x, normalized_shape, weight=None, bias=None, eps=1e-5):
+    """(layer_norm(x), x) where the gradients of both outputs meet inside the
+    LN backward kernel (pre-LN transformer blocks: ``h, x = ln_dual(x)``,
+    ``x = x + f(h)``)."""
+    D = x.shape[-1]
+    if x.is_cuda and len(normalized_shape) == 1 and _C.layer_norm_supported(D) and x.dtype in (torch.float32,
+                                                                                             torch.bfloat16):
+        out_dtype = None
+        if torch.is_autocast_enabled() and x.dtype == torch.float32:
+            out_dtype = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            y, alias = _LNFn.apply(x.contiguous(), weight, bias, eps, out_dtype, True)
+        return y, alias
+    return F.layer_norm(x, normalized_shape, weight, bias, eps), x
+
+
 class FusedLayerNorm(nn.LayerNorm):
     def forward(self, x):
         return fused_layer_norm(x, self.normalized_shape, self.weight, self.bias, self.eps)
+
+    def forward_dual(self, x):
+        """(self(x), alias of x) — see :func:`fused_layer_norm_dual`."""
+        return fused_layer_norm_dual(x, self.normalized_shape, self.weight, self.bias, self.eps)

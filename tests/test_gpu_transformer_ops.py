@@ -127,6 +127,61 @@ def test_layer_norm_autocast_fp32_in_bf16_out(cuda):
     torch.testing.assert_close(x.grad, xr.grad, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layer_norm_dual_sums_both_gradients(cuda, dtype):
+    """fused_layer_norm_dual: (ln(x), alias of x); the alias's gradient is added
+    into dx inside the LN backward kernel — vs fp64 PyTorch of ln(x)·a + x·b."""
+    from distributed_compute_pytorch_amd.ops.layernorm import fused_layer_norm_dual
+
+    torch.manual_seed(0)
+    D = 768
+    w = (1 + 0.1 * torch.randn(D, device=cuda)).requires_grad_()
+    b = (0.1 * torch.randn(D, device=cuda)).requires_grad_()
+    x = torch.randn(6, 50, D, device=cuda).to(dtype).requires_grad_()
+    a, c = torch.randn(6, 50, D, device=cuda), torch.randn(6, 50, D, device=cuda)
+    y, alias = fused_layer_norm_dual(x, (D,), w, b)
+    assert alias.data_ptr() == x.data_ptr()
+    ((y.float() * a).sum() + (alias.float() * c).sum()).backward()
+    xr = x.detach().double().requires_grad_()
+    wr, br = w.detach().double().requires_grad_(), b.detach().double().requires_grad_()
+    ((torch.nn.functional.layer_norm(xr, (D,), wr, br) * a.double()).sum() + (xr * c.double()).sum()).backward()
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(x.grad.double(), xr.grad, **tol)
+    # bf16: y (hence dy) is bf16-rounded, dγ / dβ sum 300 such rows
+    ptol = dict(rtol=1e-3, atol=1e-2) if dtype == torch.float32 else dict(rtol=2e-2, atol=0.15)
+    torch.testing.assert_close(w.grad.double(), wr.grad, **ptol)
+    torch.testing.assert_close(b.grad.double(), br.grad, **ptol)
+
+
+def test_gpt2_dual_ln_matches_plain_ln(cuda):
+    """The fused GPT-2 block with dual-output LNs computes the same gradients
+    as the same block with plain LNs (same kernels, one add moved into the LN
+    backward): fp32, tight tolerance."""
+    from distributed_compute_pytorch_amd.models import gpt2 as g2
+
+    torch.manual_seed(0)
+    cfg = g2.GPT2Config(vocab_size=512, n_positions=64, n_embd=256, n_layer=2, n_head=4, dropout=0.0, fused=True)
+    m = g2.GPT2(cfg).to(cuda)
+    idx = torch.randint(0, 512, (2, 64), device=cuda)
+    m(idx, idx).backward()
+    grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad(set_to_none=True)
+    orig = g2.Block.forward
+
+    def plain(self, x):
+        x = self._dadd(self.attn(self.ln_1(x)), x, self.p, self.training)
+        return self._dadd(self.mlp(self.ln_2(x)), x, self.p, self.training)
+
+    g2.Block.forward = plain
+    try:
+        m(idx, idx).backward()
+    finally:
+        g2.Block.forward = orig
+    for n, p in m.named_parameters():
+        if p.grad is not None:
+            torch.testing.assert_close(p.grad, grads[n], rtol=1e-5, atol=1e-6, msg=n)
+
+
 def test_dropout_add_mixed_dtypes(cuda):
     from distributed_compute_pytorch_amd.ops import dropout_add
 

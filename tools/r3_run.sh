@@ -1,3 +1,3 @@
 #!/bin/bash
 set -eo pipefail
-bash tools/gpu.sh r3p tests py=tools/attn_bench.py:--iters,10 bench=--model,gpt2 bench=--model,bert bench=--steps,20,--warmup,10 smoke
+bash tools/gpu.sh r3q tests=layer_norm,or,gpt2,or,models bench=--model,gpt2 prof=--model,gpt2,--steps,4,--warmup,3
