@@ -1048,7 +1048,8 @@ std::vector<at::Tensor> layer_norm_fwd(const at::Tensor& x, const c10::optional<
 std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& weight,
                                        const c10::optional<at::Tensor>& bias, const at::Tensor& mean,
                                        const at::Tensor& rstd, const c10::optional<std::vector<at::Tensor>>& accumulate_into,
-                                       const c10::optional<at::Tensor>& grad_residual) {
+                                       const c10::optional<at::Tensor>& grad_residual,
+                                       const c10::optional<at::Tensor>& dy2) {
   c10::hip::HIPGuard guard(x.device().index());
   at::Tensor g = dy.contiguous();
   // dy arrives in y's dtype (bf16 when the forward wrote bf16 from fp32 x)
@@ -1082,10 +1083,16 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
                                                          : grad_residual->to(x.scalar_type()).contiguous();
     DK_CHECK(gr.numel() == x.numel() && gr.device() == x.device(), "layer_norm_bwd: grad_residual must match x");
   }
+  // dy2: the gradient of the output's second consumer (dual-output LN), added to dy on load
+  at::Tensor g2;
+  if (dy2.has_value() && dy2->defined()) {
+    g2 = dy2->scalar_type() == g.scalar_type() ? dy2->contiguous() : dy2->to(g.scalar_type()).contiguous();
+    DK_CHECK(g2.numel() == g.numel() && g2.device() == g.device(), "layer_norm_bwd: dy2 must match dy");
+  }
   kern::ln_backward(ln_dtype(x), ln_dtype(g), g.data_ptr(), x.data_ptr(), has_w ? w.data_ptr<float>() : nullptr,
                     mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(),
                     db.data_ptr<float>(), part.data_ptr<float>(), rows, static_cast<int>(D), accum, stream_of(x),
-                    gr.defined() ? gr.data_ptr() : nullptr);
+                    gr.defined() ? gr.data_ptr() : nullptr, g2.defined() ? g2.data_ptr() : nullptr);
   if (accum) return {dx, at::Tensor(), at::Tensor()};
   const bool has_b = bias.has_value() && bias->defined();
   return {dx, has_w ? dw.to(weight->scalar_type()) : at::Tensor(), has_b ? db.to(bias->scalar_type()) : at::Tensor()};
@@ -1339,7 +1346,8 @@ void bind(pybind11::module& m) {
         pybind11::arg("eps"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("layer_norm_bwd", &layer_norm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("weight"),
         pybind11::arg("bias"), pybind11::arg("mean"), pybind11::arg("rstd"),
-        pybind11::arg("accumulate_into") = pybind11::none(), pybind11::arg("grad_residual") = pybind11::none());
+        pybind11::arg("accumulate_into") = pybind11::none(), pybind11::arg("grad_residual") = pybind11::none(),
+        pybind11::arg("dy2") = pybind11::none());
   m.def("cross_entropy_fwd", &cross_entropy_fwd);
   m.def("log_softmax_fwd", &log_softmax_fwd, pybind11::arg("x"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("log_softmax_bwd", &log_softmax_bwd);

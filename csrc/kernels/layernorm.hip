@@ -158,7 +158,8 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
                                                     const float* __restrict__ w, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, void* __restrict__ dx,
                                                     float* __restrict__ part, int64_t rows, int D,
-                                                    int rows_per_blk, const void* __restrict__ gres) {
+                                                    int rows_per_blk, const void* __restrict__ gres,
+                                                    const void* __restrict__ dy2) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kWaves][2][D]
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -184,6 +185,12 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
         const int vi = lane + j * 64;
         if (vi < nv) {
           L8<YD>::ld(dy, row * D + vi * 8, dv[r][j]);
+          if (dy2) {  // the output's second consumer (dual-output LN): dy += dy2
+            float d2[8];
+            L8<YD>::ld(dy2, row * D + vi * 8, d2);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dv[r][j][k] += d2[k];
+          }
           L8<XD>::ld(x, row * D + vi * 8, xh[r][j]);
         }
       }
@@ -293,10 +300,10 @@ void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w,
 template <int XD, int YD>
 void bwd_dispatch(int vpl, dim3 g, size_t sm, hipStream_t s, const void* dy, const void* x, const float* w,
                   const float* mean, const float* rstd, void* dx, float* part, int64_t rows, int D, int rpb,
-                  const void* gres) {
+                  const void* gres, const void* dy2) {
 #define DK_LNB(V) \
   hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, kRows>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, \
-                     rpb, gres)
+                     rpb, gres, dy2)
   switch (vpl) {
     case 1: DK_LNB(1); break;
     case 2: DK_LNB(2); break;
@@ -338,17 +345,17 @@ void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const flo
 
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
                  const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
-                 hipStream_t s, const void* gres) {
+                 hipStream_t s, const void* gres, const void* dy2) {
   const int nblk = ln_bwd_blocks(rows);
   const int rpb = static_cast<int>((rows + nblk - 1) / nblk);
   const size_t sm = sizeof(float) * kWaves * 2 * D;
   const int vpl = vpl_for(D);
   if (xdtype == LN_BF16)
-    bwd_dispatch<LN_BF16, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres);
+    bwd_dispatch<LN_BF16, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2);
   else if (ydtype == LN_BF16)
-    bwd_dispatch<LN_F32, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres);
+    bwd_dispatch<LN_F32, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2);
   else
-    bwd_dispatch<LN_F32, LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres);
+    bwd_dispatch<LN_F32, LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2);
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, part, nblk, D, dw, db, accum ? 1 : 0);
 }
 

@@ -19,7 +19,7 @@ void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const flo
 // part: workspace [ln_bwd_blocks(rows) * 2 * D] fp32; accum: dw / db += instead of =
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
                  const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
-                 hipStream_t s, const void* gres = nullptr);
+                 hipStream_t s, const void* gres = nullptr, const void* dy2 = nullptr);
 
 // Cross-entropy over [rows, V] logits (bf16/fp32, row stride ld elements).
 // Forward: loss[row] = lse - logit[target] (0 for ignore_index), lse saved.

@@ -18,10 +18,10 @@ import torch
 from torch import nn
 from torch.nn import functional as F
 
-from ..ops.attention import attn_supported, flash_attn
+from ..ops.attention import attn_supported, flash_attn_qkv
 from ..ops.cross_entropy import fused_cross_entropy
 from ..ops.embedding import FusedEmbedding
-from ..ops.linear import FusedLinear
+from ..ops.linear import FusedLinear, packed_linear
 from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
 
@@ -63,9 +63,12 @@ class BertSelfAttention(nn.Module):
         B, T, C = x.shape
         h = self.heads
         if self.fused and mask is None:
-            q, k, v = self.query(x), self.key(x), self.value(x)
-            if attn_supported(q, h):  # MFMA flash attention, [B, T, C] in and out
-                return flash_attn(q, k, v, h, causal=False, dropout_p=self.dropout if self.training else 0.0)
+            # query / key / value as one packed GEMM (one dgrad GEMM, no
+            # per-projection gradient adds) feeding the packed MFMA flash attention
+            qkv = packed_linear(x, (self.query, self.key, self.value))
+            if attn_supported(qkv[..., :C], h):
+                return flash_attn_qkv(qkv, h, causal=False, dropout_p=self.dropout if self.training else 0.0)
+            q, k, v = qkv.split(C, dim=2)
             return F.scaled_dot_product_attention(
                 q.view(B, T, h, C // h).transpose(1, 2), k.view(B, T, h, C // h).transpose(1, 2),
                 v.view(B, T, h, C // h).transpose(1, 2),
@@ -92,13 +95,24 @@ class BertLayer(nn.Module):
         self.p = cfg.dropout
         self._dadd = dropout_add if cfg.fused else _plain_dropout_add
 
-    def forward(self, x, mask):
-        x = self.attn_ln(self._dadd(self.attn_out(self.attention(x, mask)), x, self.p, self.training))
+    def forward(self, x, mask, x_res=None, dual_out: bool = False):
+        """``x_res``: an alias of ``x`` for the residual add (the previous
+        layer's dual-output LN), ``dual_out``: return (y, alias of y). With the
+        fused LNs every post-LN output's two gradients (next sublayer + its
+        residual add) are summed inside the LN backward instead of by an add."""
+        dual = isinstance(self.attn_ln, FusedLayerNorm)
+        x_res = x if x_res is None else x_res
+        h = self._dadd(self.attn_out(self.attention(x, mask)), x_res, self.p, self.training)
+        x, xa = self.attn_ln.forward_dual_out(h) if dual else (self.attn_ln(h), None)
         if isinstance(self.intermediate, FusedLinear):
             a = self.intermediate.forward_gelu(x)  # gelu.hip, bias grad fused into the GELU backward
         else:
             a = F.gelu(self.intermediate(x))
-        return self.out_ln(self._dadd(self.output(a), x, self.p, self.training))
+        h = self._dadd(self.output(a), x if xa is None else xa, self.p, self.training)
+        if dual_out and dual:
+            return self.out_ln.forward_dual_out(h)
+        y = self.out_ln(h)
+        return (y, None) if dual_out else y
 
 
 class BertForPreTraining(nn.Module):
@@ -140,8 +154,12 @@ class BertForPreTraining(nn.Module):
         mask = None
         if attention_mask is not None:
             mask = attention_mask[:, None, None, :].to(torch.bool)
-        for layer in self.layers:
-            x = layer(x, mask)
+        xa = None
+        for i, layer in enumerate(self.layers):
+            if i + 1 < len(self.layers):
+                x, xa = layer(x, mask, xa, dual_out=True)
+            else:
+                x = layer(x, mask, xa)
         pooled = torch.tanh(self.pooler(x[:, 0]))
         nsp_logits = self.nsp(pooled)
         if mlm_labels is None:

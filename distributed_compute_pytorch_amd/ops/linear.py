@@ -108,7 +108,9 @@ def inplace_grad(p, shape, accum: bool = False):
       post-hook on it (``reducer.cpp`` register_hooks) fires exactly once,
       after the in-place add, and finds the accumulated ``.grad``.
     """
-    g = p.grad if p is not None else None
+    if p is None or not p.is_leaf:  # a packed (concatenated) weight: autograd splits its gradient
+        return None
+    g = p.grad
     if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != shape or g.requires_grad:
         return None
     if accum:
@@ -308,3 +310,22 @@ class FusedLinear(nn.Linear):
             b16 = self._bf16(self.bias, "_b16_cache") if self.bias is not None else None
             return _LinearGeluFn.apply(x, self.weight, self.bias, w16, b16, self._bf16t(w16), approximate == "tanh")
         return F.gelu(self.forward(x), approximate=approximate)
+
+
+def packed_linear(x: torch.Tensor, layers) -> torch.Tensor:
+    """``torch.cat([l(x) for l in layers], -1)`` as ONE GEMM: the layers'
+    weights / biases are concatenated (an autograd cat, so each keeps its own
+    parameter, gradient and state_dict key) and run through :class:`_LinearFn`
+    — one forward GEMM, one data-gradient GEMM whose K spans all the layers
+    (no separate adds of the per-layer input gradients) and one weight-gradient
+    GEMM. BERT's query / key / value projections: their packed output feeds
+    the packed flash-attention entry point directly."""
+    w = torch.cat([l.weight for l in layers], 0)
+    b = torch.cat([l.bias for l in layers], 0) if all(l.bias is not None for l in layers) else None
+    fast = x.is_cuda and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and (
+        x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
+                                      and torch.get_autocast_dtype("cuda") == torch.bfloat16))
+    if not fast or b is None:
+        return F.linear(x, w, b)
+    w16 = w.detach().to(torch.bfloat16)
+    return _LinearFn.apply(x, w, b, w16, b.detach().to(torch.bfloat16), w16.t().contiguous())

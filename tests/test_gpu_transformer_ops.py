@@ -128,6 +128,59 @@ def test_layer_norm_autocast_fp32_in_bf16_out(cuda):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layer_norm_dual_output_sums_both_gradients(cuda, dtype):
+    """fused_layer_norm_dual(alias_output=True): (ln(x), alias of ln(x)); both
+    outputs' gradients are summed as the LN backward loads dy — vs fp64
+    PyTorch of ln(x)·a + ln(x)·c."""
+    from distributed_compute_pytorch_amd.ops.layernorm import fused_layer_norm_dual
+
+    torch.manual_seed(1)
+    D = 768
+    w = (1 + 0.1 * torch.randn(D, device=cuda)).requires_grad_()
+    b = (0.1 * torch.randn(D, device=cuda)).requires_grad_()
+    x = torch.randn(6, 50, D, device=cuda).to(dtype).requires_grad_()
+    a, c = torch.randn(6, 50, D, device=cuda), torch.randn(6, 50, D, device=cuda)
+    y, alias = fused_layer_norm_dual(x, (D,), w, b, alias_output=True)
+    assert alias.data_ptr() == y.data_ptr()
+    ((y.float() * a).sum() + (alias.float() * c).sum()).backward()
+    xr = x.detach().double().requires_grad_()
+    wr, br = w.detach().double().requires_grad_(), b.detach().double().requires_grad_()
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br)
+    ((yr * a.double()).sum() + (yr * c.double()).sum()).backward()
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=6e-2)
+    torch.testing.assert_close(x.grad.double(), xr.grad, **tol)
+    ptol = dict(rtol=1e-3, atol=1e-2) if dtype == torch.float32 else dict(rtol=2e-2, atol=0.3)
+    torch.testing.assert_close(w.grad.double(), wr.grad, **ptol)
+    torch.testing.assert_close(b.grad.double(), br.grad, **ptol)
+
+
+def test_bert_dual_ln_matches_plain_ln(cuda):
+    """The fused BERT layers with dual-output post-LNs compute the same
+    gradients as the same layers with plain LNs (fp32, tight)."""
+    from distributed_compute_pytorch_amd.models import bert as bm
+
+    torch.manual_seed(0)
+    cfg = bm.BertConfig(vocab_size=128, hidden=256, layers=2, heads=4, intermediate=512, max_position=64,
+                        dropout=0.0, fused=True)
+    m = bm.BertForPreTraining(cfg).to(cuda)
+    ids = torch.randint(0, 128, (2, 64), device=cuda)
+    labels = torch.randint(0, 128, (2, 64), device=cuda)
+    m(ids, mlm_labels=labels).backward()
+    grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad(set_to_none=True)
+    orig = bm.FusedLayerNorm.forward_dual_out
+    # plain LN: the two consumers share one autograd output (autograd adds their gradients)
+    bm.FusedLayerNorm.forward_dual_out = lambda self, x: (lambda y: (y, y))(self(x))
+    try:
+        m(ids, mlm_labels=labels).backward()
+    finally:
+        bm.FusedLayerNorm.forward_dual_out = orig
+    for n, p in m.named_parameters():
+        if p.grad is not None:
+            torch.testing.assert_close(p.grad, grads[n], rtol=1e-5, atol=1e-6, msg=n)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_layer_norm_dual_sums_both_gradients(cuda, dtype):
     """fused_layer_norm_dual: (ln(x), alias of x); the alias's gradient is added
     into dx inside the LN backward kernel — vs fp64 PyTorch of ln(x)·a + x·b."""
