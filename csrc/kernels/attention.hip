@@ -117,20 +117,26 @@ __device__ __forceinline__ void stage_tile(const uint16_t* src, int64_t st, int 
   }
 }
 
-// ---- dropout: 16 random bits per element (q, key) from a counter hash,
-// one 32-bit hash per (q, key pair). Identical in forward and backward.
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+// ---- dropout: 16 random bits per element (q, key) from a counter hash: one
+// 32-bit hash per (query, key pair) — keys 2j and 2j+1 take its low / high
+// half. Identical in forward and backward. The counter is bit-packed
+// (q << 12 | key / 2, T ≤ 8192) and the (batch, head) index and the seed are
+// folded into a per-workgroup key, so a hash costs one murmur3 finaliser (two
+// 32-bit multiplies — quarter-rate VALU) instead of a multiply-built counter
+// plus three multiplies.
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
   x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
   x ^= x >> 16;
   return x;
 }
-__device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t bh, uint32_t T, uint32_t q,
-                                              uint32_t key) {
-  const uint32_t ctr = (bh * T + q) * (T >> 1) + (key >> 1);
-  return mix32((ctr ^ s0) * 0x9E3779B1u + s1);
+__device__ __forceinline__ uint32_t drop_key(uint32_t s0, uint32_t s1, uint32_t bh) {
+  return fmix32(s0 ^ fmix32(bh * 0x9E3779B1u + s1));
+}
+__device__ __forceinline__ uint32_t drop_hash(uint32_t kbh, uint32_t q, uint32_t key) {
+  return fmix32(((q << 12) | (key >> 1)) ^ kbh);
 }
 __device__ __forceinline__ bool drop_keep(uint32_t hsh, uint32_t key, uint32_t thr) {
   const uint32_t r16 = (key & 1) ? (hsh >> 16) : (hsh & 0xffffu);
@@ -175,7 +181,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
   const float c = P.scale * kLog2e;
   const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
   const float inv_keep = 1.f / (1.f - P.p_drop);
-  const uint32_t s0 = static_cast<uint32_t>(P.seed), s1 = static_cast<uint32_t>(P.seed >> 32);
+  const uint32_t kbh = drop_key(static_cast<uint32_t>(P.seed), static_cast<uint32_t>(P.seed >> 32), bh);
 
   float m = -INFINITY, l = 0.f;
   f32x16 oacc[2] = {zero16(), zero16()};
@@ -245,7 +251,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
 #pragma unroll
           for (int pr = 0; pr < 2; ++pr) {
             const uint32_t key = kb + 32 * kh + 8 * g + 4 * hh + 2 * pr;
-            const uint32_t hs = drop_hash(s0, s1, bh, T, qi, key);
+            const uint32_t hs = drop_hash(kbh, qi, key);
             const int r = 4 * g + 2 * pr;
             s[kh][r] = drop_keep(hs, key, thr) ? s[kh][r] * inv_keep : 0.f;
             s[kh][r + 1] = drop_keep(hs, key + 1, thr) ? s[kh][r + 1] * inv_keep : 0.f;
@@ -337,7 +343,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
   const float c = P.scale * kLog2e;
   const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
   const float inv_keep = 1.f / (1.f - P.p_drop);
-  const uint32_t s0 = static_cast<uint32_t>(P.seed), s1 = static_cast<uint32_t>(P.seed >> 32);
+  const uint32_t kbh = drop_key(static_cast<uint32_t>(P.seed), static_cast<uint32_t>(P.seed >> 32), bh);
 
   f32x16 dacc[2] = {zero16(), zero16()};
   int nkb = T / kKB;
@@ -365,6 +371,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
         s = mfma(row_rd(sK, 32 * kh + (lane & 31), 2 * ks + hh), qf[ks], s);
         dp = mfma(row_rd(sV, 32 * kh + (lane & 31), 2 * ks + hh), gf[ks], dp);
       }
+      uint32_t hs = 0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -372,7 +379,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
         if (CAUSAL) p = key > qi ? 0.f : p;
         float g = dp[r];
         if (DROP) {
-          const uint32_t hs = drop_hash(s0, s1, bh, T, qi, key);
+          if ((r & 1) == 0) hs = drop_hash(kbh, qi, key);  // key even: one hash for keys key, key + 1
           g = drop_keep(hs, key, thr) ? g * inv_keep : 0.f;
         }
         s[r] = p * (g - dlt);  // dSᵀ (without the softmax scale)
@@ -434,7 +441,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
   const float c = P.scale * kLog2e;
   const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
   const float inv_keep = 1.f / (1.f - P.p_drop);
-  const uint32_t s0 = static_cast<uint32_t>(P.seed), s1 = static_cast<uint32_t>(P.seed >> 32);
+  const uint32_t kbh = drop_key(static_cast<uint32_t>(P.seed), static_cast<uint32_t>(P.seed >> 32), bh);
   const float* L = lse + static_cast<int64_t>(bh) * T;
   const float* DL = delta + static_cast<int64_t>(bh) * T;
 
@@ -486,6 +493,22 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
           const float4 l4 = *reinterpret_cast<const float4*>(sL + rl);
           const float4 d4 = *reinterpret_cast<const float4*>(sD + rl);
           const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+          // dropout: lanes 2j and 2j+1 hold keys 2k, 2k+1, which share each
+          // row's hash — each lane hashes every other row (row e ^ its parity)
+          // and takes the partner lane's hash of the other through a DPP
+          // quad_perm [1,0,3,2] move
+          uint32_t hrow[4];
+          if (DROP) {
+#pragma unroll
+            for (int e2 = 0; e2 < 4; e2 += 2) {
+              const bool odd = (lane & 1) != 0;
+              const uint32_t mine = drop_hash(kbh, qb + rl + e2 + (odd ? 1 : 0), key);
+              const uint32_t other = static_cast<uint32_t>(
+                  __builtin_amdgcn_mov_dpp(static_cast<int>(mine), 0xB1, 0xF, 0xF, false));
+              hrow[e2] = odd ? other : mine;
+              hrow[e2 + 1] = odd ? mine : other;
+            }
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
@@ -494,7 +517,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
             if (CAUSAL) p = key > qrow ? 0.f : p;
             float gg = dp[r], pk = p;
             if (DROP) {
-              const bool kp = drop_keep(drop_hash(s0, s1, bh, T, qrow, key), key, thr);
+              const bool kp = drop_keep(hrow[e], key, thr);
               gg = kp ? gg * inv_keep : 0.f;
               pk = kp ? p * inv_keep : 0.f;
             }
@@ -533,7 +556,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
 
 }  // namespace
 
-bool attn_supported(int T, int D) { return D == kD && T > 0 && T % kKB == 0; }
+bool attn_supported(int T, int D) { return D == kD && T > 0 && T % kKB == 0 && T <= 8192; }  // 13-bit query in the dropout counter
 
 void attn_fwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, AttnOut o, float* lse,
               hipStream_t s) {

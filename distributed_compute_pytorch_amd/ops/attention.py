@@ -89,8 +89,9 @@ def flash_attn_qkv(qkv: torch.Tensor, heads: int, causal: bool = False, dropout_
 
 def dropout_keep_mask(B: int, H: int, T: int, p: float, seed: int, device=None) -> torch.Tensor:
     """The kernels' dropout keep-mask [B, H, T, T] rebuilt with integer torch
-    ops (test oracle): 16 bits of mix32((ctr ^ s0)·0x9E3779B1 + s1) per element,
-    ctr = (bh·T + q)·(T/2) + key/2, low half for even keys."""
+    ops (test oracle): 16 bits of fmix32(((q << 12) | key/2) ^ kbh) per
+    element, kbh = fmix32(s0 ^ fmix32(bh·0x9E3779B1 + s1)) (murmur3 finaliser),
+    low half for even keys."""
     M = 0xFFFFFFFF
     dev = device or "cpu"
 
@@ -98,19 +99,19 @@ def dropout_keep_mask(B: int, H: int, T: int, p: float, seed: int, device=None) 
         lo, hi = x & 0xFFFF, x >> 16
         return ((lo * c) + (((hi * c) & 0xFFFF) << 16)) & M
 
-    def mix32(x):
+    def fmix32(x):
         x = x ^ (x >> 16)
-        x = mul32(x, 0x7feb352d)
-        x = x ^ (x >> 15)
-        x = mul32(x, 0x846ca68b)
+        x = mul32(x, 0x85EBCA6B)
+        x = x ^ (x >> 13)
+        x = mul32(x, 0xC2B2AE35)
         return x ^ (x >> 16)
 
     s0, s1 = seed & M, (seed >> 32) & M
     bh = torch.arange(B * H, device=dev, dtype=torch.int64)[:, None, None]
     qq = torch.arange(T, device=dev, dtype=torch.int64)[None, :, None]
     kk = torch.arange(T, device=dev, dtype=torch.int64)[None, None, :]
-    ctr = (((bh * T + qq) & M) * (T >> 1) + (kk >> 1)) & M
-    h = mix32((mul32(ctr ^ s0, 0x9E3779B1) + s1) & M)
+    kbh = fmix32(s0 ^ fmix32((mul32(bh, 0x9E3779B1) + s1) & M))
+    h = fmix32(((qq << 12) | (kk >> 1)) ^ kbh)
     r16 = torch.where((kk & 1) == 1, h >> 16, h & 0xFFFF)
     thr = int(p * 65536.0 + 0.5)
     return (r16 >= thr).view(B, H, T, T)
