@@ -97,7 +97,7 @@ def parse():
     ap.add_argument("--emulate-channels", type=int, default=16, help="emulated RCCL channels (workgroups)")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the persistent GEMM / conv grids leave free for collectives (DCP_RESERVE_CUS)")
-    ap.add_argument("--linear-path", choices=["ours", "aten-fwd", "aten"], default="ours",
+    ap.add_argument("--linear-path", choices=["ours", "ours-unfused-mlp", "aten-fwd", "aten"], default="ours",
                     help="transformer Linear forward / data-gradient GEMMs: ours (gemm_nt + fused epilogues), "
                          "aten-fwd (forward on hipBLASLt), aten (forward and dgrad on hipBLASLt)")
     ap.add_argument("--gemm-tune", default=None,
@@ -213,8 +213,10 @@ def main():
     if a.linear_path != "ours":
         from distributed_compute_pytorch_amd.ops import linear as _lin
 
-        _lin._OUR_FWD = False
-        _lin._OUR_DGRAD = a.linear_path == "aten-fwd"
+        _lin._FUSED_MLP = False
+        if a.linear_path != "ours-unfused-mlp":
+            _lin._OUR_FWD = False
+            _lin._OUR_DGRAD = a.linear_path == "aten-fwd"
     torch.manual_seed(0)
     wl = workloads.build(a.model, dev, batch=a.batch, fused=fused, seq_len=a.seq_len, accum=a.accum,
                          channels_last=bool(a.channels_last), fused_gemm=bool(a.gemm))
@@ -326,6 +328,10 @@ def main():
                 cfg["gemm_tune"] = tune
             if a.linear_path != "ours":
                 cfg["linear_path"] = a.linear_path
+            if a.model in ("gpt2", "bert") and ours:
+                from distributed_compute_pytorch_amd.ops.linear import autotune_choices
+
+                cfg["linear_gemm_choice"] = autotune_choices()
             if ours:
                 cfg["bucket_cap_mb"] = round(info["bucket_cap_bytes"] / 2**20, 3)
                 cfg["first_bucket_mb"] = round(info["first_bucket_bytes"] / 2**20, 3)

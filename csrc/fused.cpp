@@ -230,6 +230,33 @@ std::vector<at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, co
 // the bf16 rounding), x bf16 [.., K] contiguous, w bf16 [N, K], b fp32 [N].
 // gelu = 0: returns {y}; 1 (tanh) / 2 (erf): returns {gelu(h), h} — h is the
 // pre-activation the GELU backward reads.
+// MLP backward through the second Linear: gh = (gy · W2) ⊙ gelu'(h) in ONE
+// GEMM (data-gradient epilogue EPI 10 / 11), and db1 = Σ_rows gh (fp32,
+// added into accumulate_into when given, else a fresh tensor). gy [M, N2]
+// bf16, w2t = W2ᵀ [N1, N2] bf16, h [M, N1] bf16 (the first Linear's output).
+std::vector<at::Tensor> linear_dgrad_gelu(const at::Tensor& gy, const at::Tensor& w2t, const at::Tensor& h,
+                                          bool tanh_approx, const c10::optional<at::Tensor>& accumulate_into) {
+  DK_CHECK(gy.is_cuda() && gy.scalar_type() == at::kBFloat16 && gy.is_contiguous(), "linear_dgrad_gelu: gy");
+  DK_CHECK(w2t.scalar_type() == at::kBFloat16 && w2t.is_contiguous() && w2t.dim() == 2, "linear_dgrad_gelu: w2t");
+  c10::hip::HIPGuard guard(gy.device().index());
+  const int64_t K = gy.size(-1), M = gy.numel() / K, N = w2t.size(0);
+  DK_CHECK(w2t.size(1) == K, "linear_dgrad_gelu: w2t must be [N1, N2]");
+  DK_CHECK(h.scalar_type() == at::kBFloat16 && h.is_contiguous() && h.numel() == M * N, "linear_dgrad_gelu: h");
+  DK_CHECK(kern::gemm_nt_supported(M, N, K), "linear_dgrad_gelu: unsupported shape");
+  at::Tensor db;
+  if (accumulate_into.has_value() && accumulate_into->defined()) {
+    db = *accumulate_into;
+    DK_CHECK(db.scalar_type() == at::kFloat && db.is_contiguous() && db.numel() == N, "linear_dgrad_gelu: db target");
+  } else {
+    db = at::zeros({N}, gy.options().dtype(at::kFloat));
+  }
+  std::vector<int64_t> shape(h.sizes().begin(), h.sizes().end());
+  at::Tensor gh = at::empty(shape, h.options());
+  kern::gemm_nt_gelubwd_bf16(gy.data_ptr(), w2t.data_ptr(), gh.data_ptr(), M, static_cast<int>(N),
+                             static_cast<int>(K), h.data_ptr(), db.data_ptr<float>(), tanh_approx, stream_of(gy));
+  return {gh, db};
+}
+
 std::vector<at::Tensor> linear_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, int64_t gelu) {
   DK_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "linear_fwd: contiguous bf16 input");
   DK_CHECK(gelu >= 0 && gelu <= 2, "linear_fwd: gelu must be 0, 1 (tanh) or 2 (erf)");
@@ -1342,6 +1369,8 @@ void bind(pybind11::module& m) {
         pybind11::arg("offset"), pybind11::arg("offset_dev") = pybind11::none());
   m.def("bn_supported", [](int64_t C) { return kern::bn_supported(static_cast<int>(C)); });
   m.def("layer_norm_supported", &layer_norm_supported);
+  m.def("linear_dgrad_gelu", &linear_dgrad_gelu, pybind11::arg("gy"), pybind11::arg("w2t"), pybind11::arg("h"),
+        pybind11::arg("tanh_approx"), pybind11::arg("accumulate_into") = pybind11::none());
   m.def("layer_norm_fwd", &layer_norm_fwd, pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
         pybind11::arg("eps"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("layer_norm_bwd", &layer_norm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("weight"),

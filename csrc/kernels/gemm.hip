@@ -220,6 +220,18 @@ __device__ __forceinline__ float gelu_epi(float x) {
   return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
 }
 
+// GELU derivative of the MLP-backward epilogue (gelu.hip's gelu_d forms)
+template <bool TANH>
+__device__ __forceinline__ float gelu_dx(float x) {
+  if (TANH) {
+    const float x2 = x * x;
+    const float u = 0.79788456080286536f * x * (1.f + 0.044715f * x2);
+    const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 3.f * 0.044715f * x2);
+  }
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
 // Several parity classes of a stride-2 kxk data gradient in ONE launch
 // (EPI 4): workgroup tile ids [off[c], off[c+1]) belong to class c, one tile
 // per workgroup; each class has its own row grid / taps (g), rows (M), depth
@@ -303,6 +315,13 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   constexpr bool X2 = EPI == 6;
   constexpr bool BIAS = EPI >= 7 && EPI <= 9;  // Linear forward: + bias [+ GELU into bnr.c2]
   constexpr bool GELU = EPI == 8 || EPI == 9;
+  // EPI 10 / 11 (the transformer MLP backward): the data gradient of the
+  // second Linear IS the GELU output's gradient gy; stored instead is gh =
+  // gy·gelu'(h) (tanh / erf form; h = bnr.x, the first Linear's bf16
+  // pre-activation) and Σ gh per column (the first Linear's bias gradient, of
+  // the stored bf16 values) goes to stats[N] — the separate GELU-backward pass
+  // over gy and h disappears
+  constexpr bool GB = EPI == 10 || EPI == 11;
   static_assert(!(PRO && (RED || RR)), "RED / RESRED are data-gradient epilogues");
   constexpr int kNSnt = NS > 0 ? NS : nt_stages<BK>();
   constexpr bool CA = NS > 0;  // C staging aliased into the ring
@@ -668,11 +687,11 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       // is latency-bound on these reads); per half for EPI 6 (registers)
       constexpr int NR = 32 / RPI;
       constexpr int HB = (X2 || PIPE) ? 1 : 2;  // halves loaded ahead (PIPE: registers hold the next fragments)
-      uint4 xr[(RED || RR) ? HB * NR : 1], g2r[RR ? HB * NR : 1], x2r[X2 ? HB * NR : 1];
+      uint4 xr[(RED || RR || GB) ? HB * NR : 1], g2r[RR ? HB * NR : 1], x2r[X2 ? HB * NR : 1];
       uint32_t mbr[RR ? HB * NR : 1];
 #pragma unroll
       for (int h = 0; h < FM / 2; ++h) {  // 32-row halves of the wave's rows
-        if ((RED || RR) && h % HB == 0) {
+        if ((RED || RR || GB) && h % HB == 0) {
           // (a plain loop, not a lambda: a lambda capturing the arrays by
           // reference left dead scratch stores of them in the epilogue)
           const int h0 = h;  // first half of the group loaded here
@@ -770,6 +789,18 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
             }
             *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) =
                 make_uint4(pack2(gk[0], gk[1]), pack2(gk[2], gk[3]), pack2(gk[4], gk[5]), pack2(gk[6], gk[7]));
+          } else if (m < M && GB) {
+            const uint4 xv = xr[GB ? (h % HB) * NR + it : 0];
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, x4[4] = {xv.x, xv.y, xv.z, xv.w};
+            uint32_t g4[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              g4[k] = pack2(bf_lo(w4[k]) * gelu_dx<EPI == 10>(bf_lo(x4[k])),
+                            bf_hi(w4[k]) * gelu_dx<EPI == 10>(bf_hi(x4[k])));
+              ssum[2 * k] += bf_lo(g4[k]);  // the stored (bf16-rounded) gh, as gelu_bwd_kernel sums
+              ssum[2 * k + 1] += bf_hi(g4[k]);
+            }
+            *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) = make_uint4(g4[0], g4[1], g4[2], g4[3]);
           } else if (m < M) {
             *reinterpret_cast<uint4*>(C + m * N + n0 + wn * WN + c * 8) = v;
             if constexpr (GELU) {
@@ -815,7 +846,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       cv += P;
     }
   }
-  if (STATS || RED || RR) {
+  if (STATS || RED || RR || GB) {
     // lanes with the same channel set: lane ^ LPR, ^2LPR, ... ; then over wm via LDS
 #pragma unroll
     for (int e = 0; e < 8; ++e)
@@ -847,7 +878,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
         if (X2) d += red[2 * WM * BN + w * BN + t];
       }
       atomicAdd(stats + n0 + t, a);
-      atomicAdd(stats + N + n0 + t, b);
+      if (!GB) atomicAdd(stats + N + n0 + t, b);
       if (X2) {
         atomicAdd(bnr.acc2 + n0 + t, a);
         atomicAdd(bnr.acc2 + N + n0 + t, d);
@@ -1750,7 +1781,11 @@ WgradPlan wgrad_plan(int64_t M, int N1, int N2, int taps = 1) {
   p.tiles = (N1 / p.bm) * (N2 / p.bn);
   constexpr int kStep = 64;  // chunk granularity: whole stages at BK = 64 and 32
   const int64_t ksteps = (M + kStep - 1) / kStep;
-  int64_t S = g_wg_slots / (p.tiles * taps);  // ~2 blocks per CU
+  // ~2 blocks per CU; the gathered kxk weight gradients of the 7x7 layers
+  // (few rows, 9 taps) balance better over twice as many slabs (-12 %,
+  // profiles/r3_wgrad3_slots.jsonl)
+  const int64_t slots = (g_wg_cap == 0 && taps > 1 && M <= 65536) ? 2 * g_wg_slots : g_wg_slots;
+  int64_t S = slots / (p.tiles * taps);
   // keep the slab traffic (write + read) ≤ ~wg_cap x the operand traffic
   // (wg_cap 0 = auto: 4x at M <= 64K rows — the transformer Linear shapes
   // and ResNet's 7x7 layers, 10-30 % faster — else 1x: the 14x14-56x56
@@ -2085,6 +2120,38 @@ void gemm_nt_bias_bf16(const void* A, const void* B, void* C, int64_t M, int N, 
   }
   if (N % 128 == 0) gemm_nt_bias_launch<128>(A, B, C, M, N, K, bias, c2, gelu, s);
   else gemm_nt_bias_launch<64>(A, B, C, M, N, K, bias, c2, gelu, s);
+}
+
+// MLP backward: gh = (A·Bᵀ)·gelu'(h) (EPI 10 tanh / 11 erf), db[n] += Σ_m gh;
+// 128-row tiles on the BK = 64 ring (pipelined), persistent as gemm_nt
+void gemm_nt_gelubwd_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* h, float* db,
+                          bool tanh_approx, hipStream_t s) {
+  constexpr int BM = 128, BK = 64;
+  const int BN = N % 128 == 0 ? 128 : 64;
+  const int tiles_m = static_cast<int>((M + BM - 1) / BM);
+  const int tn = N / BN;
+  const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
+  const int kRes = 2 * grid_cus();
+  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
+  if (P < tn) P = tn;
+  const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 + 4 * 32 * (BN * 2 / 2);
+  BnRedArgs r{};
+  r.x = static_cast<const uint16_t*>(h);
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  auto c = static_cast<uint16_t*>(C);
+  const dim3 grid(P), block(256);
+#define DK_GB(BN_, E)                                                                                           \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, false, E, false, BK>), grid, block, lds, s, a, b, c, M, N, K, nullptr, \
+                     nullptr, 0, db, tiles_m, tn, ConvGeo{}, r)
+  if (BN == 128) {
+    if (tanh_approx) DK_GB(128, 10);
+    else DK_GB(128, 11);
+  } else {
+    if (tanh_approx) DK_GB(64, 10);
+    else DK_GB(64, 11);
+  }
+#undef DK_GB
 }
 
 void gemm_nt_bnred_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,

@@ -37,6 +37,9 @@ void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
 // c2 [M,N] gets gelu(h) computed from the bf16 h (what the backward reads).
 void gemm_nt_bias_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* bias, void* c2,
                        int gelu, hipStream_t s);
+// MLP backward (EPI 10 / 11): C = gh = (A·Bᵀ)·gelu'(h) bf16 [M, N], db[N] += Σ_m gh (fp32 atomics)
+void gemm_nt_gelubwd_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* h, float* db,
+                          bool tanh_approx, hipStream_t s);
 
 // fp32 weight [R][Cc] → bf16 copy wb [R][Cc] and transposed bf16 wt [Cc][R]
 // (the forward GEMM's B operand and the dgrad GEMM's B operand) in one launch.

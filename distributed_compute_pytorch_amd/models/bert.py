@@ -21,7 +21,7 @@ from torch.nn import functional as F
 from ..ops.attention import attn_supported, flash_attn_qkv
 from ..ops.cross_entropy import fused_cross_entropy
 from ..ops.embedding import FusedEmbedding
-from ..ops.linear import FusedLinear, packed_linear
+from ..ops.linear import FusedLinear, fused_mlp_gelu, packed_linear
 from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
 
@@ -105,10 +105,11 @@ class BertLayer(nn.Module):
         h = self._dadd(self.attn_out(self.attention(x, mask)), x_res, self.p, self.training)
         x, xa = self.attn_ln.forward_dual_out(h) if dual else (self.attn_ln(h), None)
         if isinstance(self.intermediate, FusedLinear):
-            a = self.intermediate.forward_gelu(x)  # gelu.hip, bias grad fused into the GELU backward
+            # one node: GELU in the first GEMM's epilogue, its backward in the second's dgrad epilogue
+            o = fused_mlp_gelu(x, self.intermediate, self.output, "none")
         else:
-            a = F.gelu(self.intermediate(x))
-        h = self._dadd(self.output(a), x if xa is None else xa, self.p, self.training)
+            o = self.output(F.gelu(self.intermediate(x)))
+        h = self._dadd(o, x if xa is None else xa, self.p, self.training)
         if dual_out and dual:
             return self.out_ln.forward_dual_out(h)
         y = self.out_ln(h)

@@ -23,7 +23,7 @@ from torch.nn import functional as F
 from ..ops.attention import attn_supported, flash_attn_qkv
 from ..ops.cross_entropy import fused_cross_entropy
 from ..ops.embedding import FusedEmbedding
-from ..ops.linear import FusedLinear
+from ..ops.linear import FusedLinear, fused_mlp_gelu
 from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
 
@@ -80,7 +80,8 @@ class MLP(nn.Module):
 
     def forward(self, x):
         if isinstance(self.c_fc, FusedLinear):
-            return self.c_proj(self.c_fc.forward_gelu(x, approximate="tanh"))  # gelu.hip
+            # one node: GELU in c_fc's GEMM epilogue, its backward in c_proj's dgrad epilogue
+            return fused_mlp_gelu(x, self.c_fc, self.c_proj, "tanh")
         return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
 
 

@@ -37,6 +37,9 @@ _OUR_DGRAD = True
 # at BERT's 16,384 (profiles/r3_linear_fwd_dgrad_vs_blas.jsonl, NOTES §22).
 _AUTOTUNE = True
 _CHOICE: dict = {}
+# MLP blocks as one node with the GELU backward in the second GEMM's epilogue
+# (False: two FusedLinear nodes + the GELU-backward kernel; bench.py --linear-path ours-unfused-mlp)
+_FUSED_MLP = True
 
 
 def _time_ms(fn, iters: int = 3) -> float:
@@ -48,6 +51,11 @@ def _time_ms(fn, iters: int = 3) -> float:
     e.record()
     e.synchronize()
     return s.elapsed_time(e)
+
+
+def autotune_choices() -> dict:
+    """{"fwd|fwd_gelu|dgrad M K N": "ours" | "hipblaslt"} measured so far."""
+    return {" ".join(str(k) for k in key): ("ours" if v else "hipblaslt") for key, v in _CHOICE.items()}
 
 
 def _prefer_ours(key, ours, aten) -> bool:
@@ -177,7 +185,7 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
     dx = dw = None
     if ctx.needs_input_grad[0]:
         if (_OUR_DGRAD and wt is not None and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096 and wt.shape[0] % 64 == 0
-                and _prefer_ours(("dgrad", g2.shape[0], g2.shape[1], wt.shape[1]), lambda: _C.conv1x1_dgrad(g2, wt),
+                and _prefer_ours(("dgrad", g2.shape[0], g2.shape[1], wt.shape[0]), lambda: _C.conv1x1_dgrad(g2, wt),
                                  lambda: g2 @ w)):
             dx = _C.conv1x1_dgrad(g2, wt).view(x.shape)
         else:
@@ -329,3 +337,114 @@ def packed_linear(x: torch.Tensor, layers) -> torch.Tensor:
         return F.linear(x, w, b)
     w16 = w.detach().to(torch.bfloat16)
     return _LinearFn.apply(x, w, b, w16, b.detach().to(torch.bfloat16), w16.t().contiguous())
+
+
+class _Sub:
+    """The per-Linear slice of an autograd ctx that _linear_backward reads."""
+
+    def __init__(self, needs, params, wdtype, bdtype, accum):
+        self.needs_input_grad, self.params, self.wdtype, self.bdtype, self.accum = needs, params, wdtype, bdtype, accum
+
+
+class _MLPFn(torch.autograd.Function):
+    """proj(gelu(fc(x))) as one node. Forward: fc with the bias + GELU
+    epilogue (h and gelu(h) out of one GEMM), proj with the bias epilogue.
+    Backward: proj's data gradient IS gelu(h)'s gradient, so its GEMM stores
+    gh = (gy·W2)·gelu'(h) directly and sums fc's bias gradient in the same
+    epilogue (``_C.linear_dgrad_gelu``, gemm.hip EPI 10/11): the separate
+    GELU-backward pass over gy and h (50-100 MB per GPT-2 / BERT layer) is gone."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w1_16, b1_16, w2_16, w1t, w2t, tanh):
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        mode = 1 if tanh else 2
+        x2 = x.reshape(-1, x.shape[-1])
+        b1_32, b2_32 = _bias32(b1), _bias32(b2)
+        y1, h = _C.linear_fwd(x, w1_16, b1_32, mode)
+        y1_2 = y1.reshape(-1, y1.shape[-1])
+        if _prefer_ours(("fwd", y1_2.shape[0], w2_16.shape[1], w2_16.shape[0]),
+                        lambda: _C.linear_fwd(y1_2, w2_16, b2_32, 0), lambda: F.linear(y1_2, w2_16, b2_16_of(b2))):
+            out = _C.linear_fwd(y1, w2_16, b2_32, 0)[0]
+        else:
+            out = F.linear(y1, w2_16, b2_16_of(b2))
+        ctx.save_for_backward(x, h, y1, w1_16, w2_16, w1t, w2t)
+        ctx.tanh = tanh
+        ctx.accum = accumulating()
+        ctx.wdtypes = (w1.dtype, w2.dtype)
+        ctx.bdtypes = (b1.dtype, b2.dtype)
+        ctx.params = (w1, b1, w2, b2)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, h, y1, w1_16, w2_16, w1t, w2t = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        gout = gout.contiguous()
+        if gout.dtype != torch.bfloat16:
+            gout = gout.to(torch.bfloat16)
+        g2 = gout.view(-1, gout.shape[-1])
+        n = ctx.needs_input_grad
+        # proj: weight / bias gradients as a plain Linear (no data gradient here)
+        sub2 = _Sub((False, n[3], n[4]), (w2, b2), ctx.wdtypes[1], ctx.bdtypes[1], ctx.accum)
+        _, dw2, db2 = _linear_backward(sub2, g2, y1, w2_16)
+        # proj's data gradient with the GELU backward and fc's bias sum fused in
+        tgt = _acc_target(ctx, b1, torch.Size((h.shape[-1],))) if n[2] else None
+        gh, db1 = _C.linear_dgrad_gelu(g2, w2t, h.view(-1, h.shape[-1]), ctx.tanh, accumulate_into=tgt)
+        if tgt is not None or not n[2]:
+            db1 = None
+        elif db1.dtype != ctx.bdtypes[0]:
+            db1 = db1.to(ctx.bdtypes[0])
+        sub1 = _Sub((n[0], n[1], n[2]), (w1, b1), ctx.wdtypes[0], ctx.bdtypes[0], ctx.accum)
+        dx, dw1, _ = _linear_backward(sub1, gh, x, w1_16, db=db1, db_done=True, wt=w1t)
+        return dx, dw1, db1, dw2, db2, None, None, None, None, None, None
+
+
+def _mlp_prefers_ours(x, w1_16, b1, b1_16, w2_16, w2t, tanh) -> bool:
+    M, K = x.numel() // x.shape[-1], x.shape[-1]
+    N1, N2 = w1_16.shape[0], w2_16.shape[0]
+    key_f, key_d = ("fwd_gelu", M, K, N1), ("dgrad", M, N2, N1)
+    if key_f in _CHOICE and key_d in _CHOICE:
+        return _CHOICE[key_f] and _CHOICE[key_d]
+    if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        return True
+    mode = 1 if tanh else 2
+    with torch.no_grad():
+        x2 = x.detach().reshape(M, K).to(torch.bfloat16)
+        b32 = _bias32(b1)
+        f = _prefer_ours(key_f, lambda: _C.linear_fwd(x2, w1_16, b32, mode),
+                         lambda: _C.gelu_fwd(F.linear(x2, w1_16, b1_16), tanh))
+        g2 = torch.empty(M, N2, device=x.device, dtype=torch.bfloat16).normal_()
+        d = _prefer_ours(key_d, lambda: _C.conv1x1_dgrad(g2, w2t), lambda: g2 @ w2_16)
+    return f and d
+
+
+def b2_16_of(b):
+    return b.detach().to(torch.bfloat16) if b is not None else None
+
+
+def fused_mlp_gelu(x: torch.Tensor, fc: "FusedLinear", proj: "FusedLinear", approximate: str = "none"):
+    """``proj(F.gelu(fc(x), approximate))`` — one autograd node (:class:`_MLPFn`)
+    on the fast path (bf16 GPU, GEMM-able shapes), else the two modules."""
+    if approximate not in ("none", "tanh"):
+        raise ValueError(f"approximate must be 'none' or 'tanh', got {approximate!r}")
+    ok = (_FUSED_MLP and _FUSED_GELU and _OUR_FWD and _OUR_DGRAD and isinstance(fc, FusedLinear) and isinstance(proj, FusedLinear)
+          and fc._fast(x) and x.is_contiguous() and fc.bias is not None and proj.bias is not None
+          and fc.out_features % 64 == 0 and fc.in_features % 64 == 0 and proj.out_features % 64 == 0
+          and fc.in_features <= 4096 and proj.in_features <= 4096 and proj.out_features <= 4096
+          and proj.in_features == fc.out_features)
+    if ok:
+        w1_16 = fc._bf16(fc.weight, "_w16_cache")
+        w1_16 = w1_16 if w1_16 is not None else fc.weight.detach().to(torch.bfloat16)
+        w2_16 = proj._bf16(proj.weight, "_w16_cache")
+        w2_16 = w2_16 if w2_16 is not None else proj.weight.detach().to(torch.bfloat16)
+        b1_16 = fc._bf16(fc.bias, "_b16_cache")
+        # the fused node runs both its GEMMs on our kernel: take it only where
+        # the per-shape autotune prefers our kernel for both (at BERT's 16,384
+        # rows hipBLASLt wins them and the unfused path measured 1.7 % faster)
+        ok = _mlp_prefers_ours(x, w1_16, fc.bias, b1_16, w2_16, proj._bf16t(w2_16), approximate == "tanh")
+    if not ok:
+        return proj(fc.forward_gelu(x, approximate) if isinstance(fc, FusedLinear) else
+                    F.gelu(fc(x), approximate=approximate))
+    return _MLPFn.apply(x, fc.weight, fc.bias, proj.weight, proj.bias, w1_16, b1_16, w2_16, fc._bf16t(w1_16),
+                        proj._bf16t(w2_16), approximate == "tanh")

@@ -517,3 +517,59 @@ def test_linear_fwd_epilogues_match_fp32(cuda, gelu, rows, fin, fout, lin_big):
     if gelu:
         y_ref = F.gelu(h.float(), approximate="tanh" if gelu == 1 else "none")  # GELU of the stored h
         torch.testing.assert_close(out[0].float(), y_ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("tanh", [True, False])
+@pytest.mark.parametrize("rows,n1,n2", [(1000, 512, 256), (4096, 3072, 768), (333, 128, 64)])
+def test_linear_dgrad_gelu_matches_fp32(cuda, tanh, rows, n1, n2):
+    """gemm.hip EPI 10/11: gh = (gy·W2)·gelu'(h) and db = Σ gh, vs fp32
+    PyTorch on the same bf16 operands (gh of the bf16-rounded gy·W2)."""
+    from distributed_compute_pytorch_amd._ext import C
+
+    g = torch.Generator().manual_seed(5)
+    gy = torch.randn(rows, n2, generator=g).to(torch.bfloat16).to(cuda)
+    w2 = (torch.randn(n2, n1, generator=g) / n1 ** 0.5).to(torch.bfloat16).to(cuda)
+    h = torch.randn(rows, n1, generator=g).to(torch.bfloat16).to(cuda)
+    gh, db = C.linear_dgrad_gelu(gy, w2.t().contiguous(), h, tanh)
+    dy = (gy.float() @ w2.float()).to(torch.bfloat16).float()
+    hr = h.float().requires_grad_()
+    torch.nn.functional.gelu(hr, approximate="tanh" if tanh else "none").backward(dy)
+    torch.testing.assert_close(gh.float(), hr.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(db, gh.float().sum(0), rtol=1e-4, atol=1e-3)
+    acc = torch.ones(n1, device=cuda)
+    C.linear_dgrad_gelu(gy, w2.t().contiguous(), h, tanh, accumulate_into=acc)
+    torch.testing.assert_close(acc, 1 + gh.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("approx", ["tanh", "none"])
+def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch):
+    """ops.linear.fused_mlp_gelu (one node: GELU forward in fc's epilogue,
+    GELU backward + fc's bias sum in proj's dgrad epilogue) vs fp32 PyTorch of
+    proj(gelu(fc(x))) on the same bf16-rounded parameters and input. The
+    per-shape autotune is off so the fused node itself runs."""
+    from distributed_compute_pytorch_amd.ops import linear as lin
+    from distributed_compute_pytorch_amd.ops.linear import FusedLinear, fused_mlp_gelu
+
+    monkeypatch.setattr(lin, "_AUTOTUNE", False)
+    monkeypatch.setattr(lin, "_CHOICE", {})
+
+    torch.manual_seed(0)
+    fc, proj = FusedLinear(256, 1024).to(cuda), FusedLinear(1024, 256).to(cuda)
+    with torch.no_grad():
+        for p in (*fc.parameters(), *proj.parameters()):
+            p.copy_(p.to(torch.bfloat16).float())
+    x = torch.randn(8, 128, 256, device=cuda).to(torch.bfloat16).float().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = fused_mlp_gelu(x, fc, proj, approx)
+    g = torch.randn_like(y, dtype=torch.float32)
+    y.float().backward(g)
+    ref = [t.detach().clone().requires_grad_() for t in (x, fc.weight, fc.bias, proj.weight, proj.bias)]
+    yr = torch.nn.functional.linear(torch.nn.functional.gelu(torch.nn.functional.linear(ref[0], ref[1], ref[2]),
+                                                             approximate=approx), ref[3], ref[4])
+    yr.backward(g)
+    assert (y.float() - yr).norm() / yr.norm() < 1e-2
+    for got, want, name in ((x.grad, ref[0].grad, "x"), (fc.weight.grad, ref[1].grad, "w1"),
+                            (fc.bias.grad, ref[2].grad, "b1"), (proj.weight.grad, ref[3].grad, "w2"),
+                            (proj.bias.grad, ref[4].grad, "b2")):
+        rel = float((got.float() - want).norm() / want.norm())
+        assert rel < 2e-2, (name, rel)

@@ -67,10 +67,36 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--wgrad-only", action="store_true")
+    ap.add_argument("--wgrad3", action="store_true", help="ResNet-50 3x3 weight gradients under each --tune entry")
     ap.add_argument("--tune", nargs="*", default=["lin_big=0", "lin_big=1", "lin_big=2"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     bf = torch.bfloat16
+    if a.wgrad3:
+        for hw, c in [(28, 128), (14, 256), (7, 512)]:
+            n = 512
+            xi = torch.randn(n, c, hw, hw, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
+            gi = torch.randn(n, c, hw, hw, device=dev).to(bf).contiguous(memory_format=torch.channels_last)
+            fl = 2 * n * hw * hw * c * 9 * c
+            rec = {"model": f"resnet3x3_{hw}", "C": c, "op": "wgrad3"}
+            ref = None
+            for kv in a.tune:
+                olds = {}
+                for e in kv.split("+"):
+                    k, v = e.split("=")
+                    olds[k] = _C.gemm_tune_get(k)
+                    _C.gemm_tune(k, int(v))
+                out = _C.conv_wgrad(gi, xi, 3, 3, 1, 1)
+                if ref is None:
+                    ref = out
+                else:
+                    rec[kv + "_maxrel"] = float((out - ref).abs().max() / ref.abs().max())
+                us = timeit(lambda: _C.conv_wgrad(gi, xi, 3, 3, 1, 1), a.iters)
+                for k, v in olds.items():
+                    _C.gemm_tune(k, v)
+                rec[kv], rec[kv + "_TF"] = round(us, 1), round(fl / us / 1e6, 1)
+            print(json.dumps(rec), flush=True)
+        return
     if a.wgrad_only:
         for hw, ci, co in [(56, 64, 256), (56, 256, 64), (28, 128, 512), (28, 512, 128), (14, 256, 1024),
                            (14, 1024, 256), (7, 512, 2048), (7, 2048, 512)]:

@@ -1,3 +1,3 @@
 #!/bin/bash
 set -eo pipefail
-bash tools/gpu.sh r3u tests=attention,or,attn,or,gpt2,or,bert,or,models py=tools/attn_bench.py:--iters,10 bench=--model,gpt2 bench=--model,bert
+bash tools/gpu.sh r3y tests=fused_mlp,or,linear,or,gpt2,or,bert bench=--model,bert bench=--model,bert,--linear-path,ours-unfused-mlp bench=--model,gpt2 bench=--model,gpt2,--linear-path,ours-unfused-mlp
