@@ -1,9 +1,8 @@
 #!/bin/bash
-# round-3 final-tree evidence on one box: GPU suite, smoke, ours vs stock (same box, back to back), ResNet profile
+# bench.py's N > 1 contract on one GPU: two ranks under torch.distributed.run sharing the GPU
+# through the host-staged backend (RCCL needs one GPU per rank)
 set -eo pipefail
-bash tools/gpu.sh r3z tests smoke \
-  bench=--steps,30,--warmup,10 bench=--impl,torch,--steps,30,--warmup,10 \
-  bench=--model,gpt2 bench=--model,gpt2,--impl,torch \
-  bench=--model,bert bench=--model,bert,--impl,torch \
-  bench=--model,convnet,--steps,200,--warmup,30 bench=--model,convnet,--impl,torch,--steps,200,--warmup,30 \
-  prof=--steps,8,--warmup,5
+mkdir -p gpurun_out
+timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29611 bench.py --gpus 2 --steps 3 --warmup 2 --backend gloo --batch 64 > gpurun_out/r3mr_bench.log 2>&1
+grep '^{' gpurun_out/r3mr_bench.log
