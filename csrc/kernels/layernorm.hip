@@ -174,7 +174,10 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_blk;
   const int64_t r1 = min(rows, r0 + rows_per_blk);
   for (int64_t rb = r0 + wid * R; rb < r1; rb += kWaves * R) {
-    float dv[R][VPL][8], xh[R][VPL][8], mu[R], rs[R];
+    // gres rows ride with the row's other loads (not behind its reductions)
+    // while the registers allow: D <= 2048
+    constexpr bool kHoist = VPL <= 4;
+    float dv[R][VPL][8], xh[R][VPL][8], gr[kHoist ? R : 1][kHoist ? VPL : 1][8], mu[R], rs[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t row = rb + r < r1 ? rb + r : r1 - 1;  // tail: recompute a valid row, store nothing
@@ -192,6 +195,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
             for (int k = 0; k < 8; ++k) dv[r][j][k] += d2[k];
           }
           L8<XD>::ld(x, row * D + vi * 8, xh[r][j]);
+          if (kHoist && gres) L8<XD>::ld(gres, row * D + vi * 8, gr[kHoist ? r : 0][kHoist ? j : 0]);
         }
       }
     }
@@ -226,10 +230,9 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] = rs[r] * (dv[r][j][k] - m1 - xh[r][j][k] * m2);
           if (gres) {  // the second consumer's gradient of x (dual-output LN): dx += gres
-            float gr[8];
-            L8<XD>::ld(gres, (rb + r) * D + vi * 8, gr);
+            if (!kHoist) L8<XD>::ld(gres, (rb + r) * D + vi * 8, gr[0][0]);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) o[k] += gr[k];
+            for (int k = 0; k < 8; ++k) o[k] += gr[kHoist ? r : 0][kHoist ? j : 0][k];
           }
           L8<XD>::st(dx, (rb + r) * D + vi * 8, o);
         }
@@ -256,6 +259,28 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
     for (int q = 0; q < kWaves; ++q) s += smem[(q * 2 + which) * D + col];
     part[(static_cast<int64_t>(blockIdx.x) * 2 + which) * D + col] = s;
   }
+}
+
+// First level of the column reduction for many workgroup partials: workgroup
+// (x, z) sums partial rows [64z, 64z + 64) of flattened columns [64x, 64x + 64)
+// (each wave 16 rows, one coalesced 256-B load per row, all 16 in flight),
+// then the 4 waves through LDS, into out[z][col]. Fixed order: deterministic.
+__global__ void __launch_bounds__(256) ln_bwd_colsum_kernel(const float* __restrict__ part, int nblk, int cols,
+                                                            float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int b0 = blockIdx.y * 64 + w * 16;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    v[i] = (c < cols && b0 + i < nblk) ? part[static_cast<int64_t>(b0 + i) * cols + c] : 0.f;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += v[i];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < cols) out[static_cast<int64_t>(blockIdx.y) * cols + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
 // accum != 0: add into dw / db (fp32 .grad under DistributedDataParallel.no_sync)
@@ -323,15 +348,25 @@ inline int vpl_for(int D) {
 
 bool ln_supported(int D) { return D % 8 == 0 && D <= 4096; }
 
-int ln_bwd_blocks(int64_t rows) {
-  // each workgroup writes one [2][D] partial row that ln_bwd_finalize_kernel
-  // re-reads column-strided: 1024 workgroups made that 6 MB pass (17 µs at
-  // BERT's 16384 x 768) cost more than the backward's own occupancy gain
-  constexpr int64_t cap = 256;
+namespace {
+// Backward workgroups: up to 1,024 (4 per CU: a memory-bound pass needs the
+// bytes in flight — at 256 workgroups, one per CU, BERT's 16,384 x 768 bf16
+// backward moved 1.5-2.3 TB/s). Each writes one [2][D] partial row; more than
+// 16 of them are first summed 64 at a time by ln_bwd_colsum_kernel (coalesced
+// rows, 16 loads in flight per lane) instead of column-strided by the finalize.
+int ln_bwd_grid(int64_t rows) {
+  constexpr int64_t cap = 1024;
   int64_t nb = (rows + 15) / 16;  // >= 16 rows (4 per wave) per workgroup
   if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
   return static_cast<int>(nb);
+}
+int ln_colsum_groups(int nblk) { return nblk > 16 ? (nblk + 63) / 64 : 0; }
+}  // namespace
+
+int ln_bwd_blocks(int64_t rows) {  // workspace rows: the partials + the colsum level
+  const int nb = ln_bwd_grid(rows);
+  return nb + ln_colsum_groups(nb);
 }
 
 void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const float* b, void* y, float* mean,
@@ -346,7 +381,7 @@ void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const flo
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
                  const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
                  hipStream_t s, const void* gres, const void* dy2) {
-  const int nblk = ln_bwd_blocks(rows);
+  const int nblk = ln_bwd_grid(rows);
   const int rpb = static_cast<int>((rows + nblk - 1) / nblk);
   const size_t sm = sizeof(float) * kWaves * 2 * D;
   const int vpl = vpl_for(D);
@@ -356,6 +391,14 @@ void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const fl
     bwd_dispatch<LN_F32, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2);
   else
     bwd_dispatch<LN_F32, LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2);
+  const int z = ln_colsum_groups(nblk);
+  if (z > 0) {
+    float* part2 = part + static_cast<int64_t>(nblk) * 2 * D;
+    hipLaunchKernelGGL(ln_bwd_colsum_kernel, dim3((2 * D + 63) / 64, z), dim3(256), 0, s, part, nblk, 2 * D, part2);
+    hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, part2, z, D, dw, db,
+                       accum ? 1 : 0);
+    return;
+  }
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, part, nblk, D, dw, db, accum ? 1 : 0);
 }
 

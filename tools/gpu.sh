@@ -40,7 +40,9 @@ for step in "$@"; do
         python3 "$R/bench.py" $(args "$val") > "$O/${TAG}_prof.log" 2>&1) || { tail -30 "$O/${TAG}_prof.log"; exit 1; }
       grep '^{' "$O/${TAG}_prof.log" || true
       # keep the per-kernel summary, drop the (large) trace database
-      python3 "$R/tools/kernel_stats.py" "$O/${TAG}_prof/prof_results.db" --top 60 > "$O/${TAG}_kernel_stats.txt" 2>&1 || true
+      ks="$O/${TAG}_kernel_stats.txt"; n=2
+      while [[ -e "$ks" ]]; do ks="$O/${TAG}_kernel_stats_$n.txt"; n=$((n + 1)); done
+      python3 "$R/tools/kernel_stats.py" "$O/${TAG}_prof/prof_results.db" --top 60 > "$ks" 2>&1 || true
       rm -rf "$O/${TAG}_prof" ;;
     pmc)
       ctr=${val%%:*}; rest=""; [[ "$val" == *:* ]] && rest=${val#*:}

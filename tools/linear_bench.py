@@ -43,7 +43,7 @@ def wgrad(model, M, K, N, x, gy, a):
     fl = 2 * M * N * K
     rec = {"model": model, "M": M, "K": K, "N": N, "op": "wgrad"}
     ref = None
-    for kv in WG_VARIANTS:
+    for kv in a.wg_variants:
         olds = {}
         for e in kv.split("+"):
             k, v = e.split("=")
@@ -67,6 +67,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--wgrad-only", action="store_true")
+    ap.add_argument("--wg-variants", nargs="*", default=WG_VARIANTS, help="gemm_tune settings of the wgrad A/B")
     ap.add_argument("--wgrad3", action="store_true", help="ResNet-50 3x3 weight gradients under each --tune entry")
     ap.add_argument("--tune", nargs="*", default=["lin_big=0", "lin_big=1", "lin_big=2"])
     a = ap.parse_args()
