@@ -106,4 +106,4 @@ def _fingerprint(rank, world):
 
 
 def test_debug_fingerprint_catches_mismatch():
-    run_world(_fingerprint, 2, backend=None, timeout=120)
+    run_world(_fingerprint, 2, backend=None, timeout=300)
