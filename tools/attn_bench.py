@@ -17,7 +17,10 @@ from distributed_compute_pytorch_amd.ops.attention import flash_attn  # noqa: E4
 
 
 def timeit(fn, iters):
-    fn()
+    # three warm-up calls: the process's first two backward passes carry the
+    # autograd engine's one-time start-up (0.7 s + 70 ms, tools/attn_diag.py)
+    for _ in range(3):
+        fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
@@ -31,10 +34,13 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--cases", nargs="*", default=None, help="subset of bert gpt2 bert-nodrop gpt2-nodrop")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for name, B, T, H, causal, p in [("bert", 32, 512, 12, False, 0.1), ("gpt2", 8, 1024, 12, True, 0.1),
                                      ("bert-nodrop", 32, 512, 12, False, 0.0), ("gpt2-nodrop", 8, 1024, 12, True, 0.0)]:
+        if a.cases and name not in a.cases:
+            continue
         C = H * 64
         q, k, v, do = (torch.randn(B, T, C, device=dev, dtype=torch.bfloat16) for _ in range(4))
         qs, ks, vs = (t.view(B, T, H, 64).transpose(1, 2) for t in (q, k, v))
