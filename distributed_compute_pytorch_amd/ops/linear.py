@@ -42,15 +42,29 @@ _CHOICE: dict = {}
 _FUSED_MLP = True
 
 
-def _time_ms(fn, iters: int = 3) -> float:
+_TIMES: dict = {}  # key -> (ours ms, hipBLASLt ms) of the autotune measurement
+
+
+def _time_ms(fn, iters: int = 5) -> float:
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fn()
     s.record()
     for _ in range(iters):
         fn()
     e.record()
     e.synchronize()
-    return s.elapsed_time(e)
+    return s.elapsed_time(e) / iters
+
+
+def _measure(ours, aten, rounds: int = 3):
+    """Best-of-``rounds`` per-call time of each side, the sides interleaved
+    (a single back-to-back pair flipped choices between runs on close shapes)."""
+    ours()
+    aten()
+    to, ta = [], []
+    for _ in range(rounds):
+        to.append(_time_ms(ours))
+        ta.append(_time_ms(aten))
+    return min(to), min(ta)
 
 
 def autotune_choices() -> dict:
@@ -65,8 +79,15 @@ def _prefer_ours(key, ours, aten) -> bool:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return True
         with torch.no_grad():
-            c = _CHOICE[key] = _time_ms(ours) <= _time_ms(aten)
+            to, ta = _measure(ours, aten)
+        _TIMES[key] = (to, ta)
+        c = _CHOICE[key] = to <= ta
     return c
+
+
+def autotune_times() -> dict:
+    """{"fwd|fwd_gelu|dgrad M K N": [ours µs, hipBLASLt µs]} of the autotune measurements."""
+    return {" ".join(str(k) for k in key): [round(a * 1e3, 1), round(b * 1e3, 1)] for key, (a, b) in _TIMES.items()}
 # let the fused Adam/AdamW write the bf16 weight copies the forward GEMMs read
 # (False: one cast launch per weight per forward; NOTES §15)
 _SHADOWS = True
