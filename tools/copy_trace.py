@@ -1,0 +1,70 @@
+"""Where do a transformer step's ATen copy / elementwise kernels come from?
+One profiled optimizer step (torch.profiler, CPU stacks) of the bench workload
+under our DDP (one rank, hop-less), aggregated by Python call site.
+
+    python tools/copy_trace.py [--model bert|gpt2]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import distributed_compute_pytorch_amd as dcp  # noqa: E402
+from distributed_compute_pytorch_amd import workloads  # noqa: E402
+from distributed_compute_pytorch_amd.distributed.launch import free_port  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="bert")
+    a = ap.parse_args()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+    dcp.distributed.init_process_group("rccl", device_id=0)
+    dev = torch.device("cuda", 0)
+    wl = workloads.build(a.model, dev)
+    ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[0], gradient_as_bucket_view=True)
+    opt = wl.make_optimizer(ddp.parameters())
+    step = workloads.make_step(wl, ddp, opt)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    from torch.profiler import ProfilerActivity, profile
+
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+                 record_shapes=True) as prof:
+        step()
+        torch.cuda.synchronize()
+    names = ("aten::copy_", "aten::add", "aten::add_", "aten::fill_", "aten::zero_", "aten::contiguous", "aten::to",
+             "aten::_to_copy", "aten::clone", "aten::cat", "aten::mul", "aten::sum")
+    tab = prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=25, max_name_column_width=40,
+                                                      max_src_column_width=140)
+    print(tab)
+    print("--- ATen data-movement ops by parent-op chain (GPU time > 4 us per call) ---")
+    agg = {}
+    for ev in prof.events():
+        if ev.name in names and ev.device_time_total > 4.0:
+            chain, p = [], ev.cpu_parent
+            while p is not None and len(chain) < 5:
+                chain.append(p.name)
+                p = p.cpu_parent
+            k = (ev.name, " <- ".join(chain))
+            c = agg.setdefault(k, [0, 0.0, set()])
+            c[0] += 1
+            c[1] += ev.device_time_total
+            c[2].add(str(ev.input_shapes)[:120])
+    for (n, ch), (cnt, us, shp) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"{us:9.1f} us {cnt:4d}x {n} <- {ch}   shapes {sorted(shp)[:2]}")
+    print("--- ATen data-movement ops by call stack ---")
+    for ev in sorted(prof.key_averages(group_by_stack_n=6), key=lambda e: -e.self_device_time_total):
+        if ev.key in names and ev.self_device_time_total > 0:
+            print(f"{ev.key:22s} calls={ev.count:5d} gpu_us={ev.self_device_time_total:9.1f}")
+            for fr in ev.stack[:6]:
+                print("      ", fr)
+    dcp.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
