@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--gemm", type=int, default=1, help="ResNet 1x1 convs as our MFMA GEMMs fused with BN")
     ap.add_argument("--bucket-cap-mb", type=float, default=None)
     ap.add_argument("--first-bucket-mb", type=float, default=None)
+    ap.add_argument("--tail-bucket-mb", type=float, default=None,
+                    help="size of the ready-last tail bucket split off the plan (0 = no split)")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--grad-as-view", type=int, default=1)
     ap.add_argument("--benchmark-cudnn", type=int, default=1)
@@ -256,6 +258,8 @@ def main():
             kw = {**dcp.parallel.XGMI_BUCKETS, **kw}
             if a.first_bucket_mb is not None:
                 kw["first_bucket_mb"] = a.first_bucket_mb
+            if a.tail_bucket_mb is not None:
+                kw["tail_bucket_mb"] = a.tail_bucket_mb
             if a.comm_dtype == "bf16":
                 kw["comm_dtype"] = torch.bfloat16
             with stream_ctx():
@@ -336,6 +340,7 @@ def main():
             if ours:
                 cfg["bucket_cap_mb"] = round(info["bucket_cap_bytes"] / 2**20, 3)
                 cfg["first_bucket_mb"] = round(info["first_bucket_bytes"] / 2**20, 3)
+                cfg["tail_bucket_mb"] = round(ddp.tail_bucket_bytes / 2**20, 3)
                 cfg["buckets_mb"] = [round(b / 2**20, 2) for b in info["bucket_sizes"]]
             elif cap_mb is not None:
                 cfg["bucket_cap_mb"] = cap_mb

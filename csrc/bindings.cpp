@@ -105,6 +105,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("backend", &Communicator::backend)
       .def_property_readonly("stream_handle", &Communicator::stream_handle)
       .def("all_reduce", &Communicator::all_reduce, py::call_guard<py::gil_scoped_release>())
+      .def("all_reduce_into", &Communicator::all_reduce_into, py::arg("wire"), py::arg("out"), py::arg("op"),
+           py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &Communicator::broadcast, py::call_guard<py::gil_scoped_release>())
       .def("all_gather", &Communicator::all_gather, py::call_guard<py::gil_scoped_release>())
       .def("reduce_scatter", &Communicator::reduce_scatter, py::call_guard<py::gil_scoped_release>())

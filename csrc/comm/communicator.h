@@ -50,6 +50,17 @@ class Communicator {
   virtual std::string backend() const = 0;
 
   virtual WorkPtr all_reduce(at::Tensor& t, ReduceOp op) = 0;
+  // All-reduce `wire` in place, then write the result into `out` (same numel,
+  // any float dtype: the cast back of a compressed collective), ordered before
+  // the Work's completion — a compression comm hook returns this Work instead
+  // of waiting inside the hook (which would order the compute stream behind
+  // every bucket's collective mid-backward). Default: reduce, wait, copy.
+  virtual WorkPtr all_reduce_into(at::Tensor& wire, at::Tensor& out, ReduceOp op) {
+    auto w = all_reduce(wire, op);
+    w->wait();
+    out.view(-1).copy_(wire.view(-1));
+    return w;
+  }
   virtual WorkPtr broadcast(at::Tensor& t, int root) = 0;
   // out: contiguous [size * in.numel()] (any shape with that numel).
   virtual WorkPtr all_gather(at::Tensor& out, const at::Tensor& in) = 0;

@@ -1,6 +1,8 @@
 // RCCL communicator over xGMI: one process per GPU, collectives on a dedicated
-// high-priority HIP stream, ordered against the caller's stream with events, no
-// host synchronisation on the hot path.
+// HIP stream (normal priority by default: a high-priority queue pre-empted the
+// backward's compute kernels, NOTES §22; DCP_COMM_STREAM_PRIORITY=high opts in),
+// ordered against the caller's stream with events, no host synchronisation on
+// the hot path.
 //
 // Parity: the reference's collectives (main.py:50 init, main.py:65 loss
 // all-reduce, main.py:90-91 metric all-reduces) went through gloo, staging GPU
@@ -158,6 +160,21 @@ class RcclCommunicator : public Communicator {
       if (size_ == 1 && !single_rank_hop_) return;  // identity for every op on one rank (in place)
       NCCL_OK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
                             to_nccl(op, t.scalar_type()), comm_, s));
+    });
+  }
+
+  WorkPtr all_reduce_into(at::Tensor& wire, at::Tensor& out, ReduceOp op) override {
+    check_tensor(wire);
+    check_tensor(out);
+    DK_CHECK(wire.numel() == out.numel(), "all_reduce_into: wire and out sizes differ");
+    account("all_reduce", wire, static_cast<int>(op));
+    return launch({wire, out}, [&](hipStream_t s) {
+      if (size_ > 1 || single_rank_hop_)
+        NCCL_OK(ncclAllReduce(wire.data_ptr(), wire.data_ptr(), wire.numel(), to_nccl(wire.scalar_type()),
+                              to_nccl(op, wire.scalar_type()), comm_, s));
+      // the cast back runs on the collective's stream, before the Work's end event
+      c10::hip::HIPStreamGuard g(c10::hip::getStreamFromExternal(s, static_cast<c10::DeviceIndex>(device_)));
+      out.view(-1).copy_(wire.view(-1));
     });
   }
 

@@ -412,13 +412,14 @@ void Reducer::finalize() {
       const double seen = b.wire.to(at::kDouble).sum().item<double>();
       const at::Tensor cs = b.check_sum.to(at::kDouble).cpu();
       const double want = cs[0].item<double>(), mag = cs[1].item<double>();
-      // rounding of the reduction itself scales with the wire dtype's epsilon
-      // times the magnitude summed (a near-zero Σx of large terms is not an
-      // ordering error): bf16 wire ~8e-3, fp32 ~1e-7 per add, ~world adds
+      // rounding of the reduction itself: each of the ~world adds of a ring
+      // (plus a hook's cast to its wire dtype) rounds by at most half an ulp,
+      // eps/2 of the magnitude summed (a near-zero Σx of large terms is not an
+      // ordering error) — bf16 wire eps 7.8e-3, fp32 1.2e-7
       const at::ScalarType wdt =
           comm_hook_ && hook_wire_ != at::ScalarType::Undefined ? hook_wire_ : b.wire.scalar_type();
       const double eps = wdt == at::kBFloat16 ? 7.8125e-3 : wdt == at::kHalf ? 9.77e-4 : 1.19e-7;
-      const double tol = (comm_->size() + 2) * eps * mag + 1e-6 * std::max(1.0, std::fabs(want)) +
+      const double tol = (comm_->size() + 1) * 0.5 * eps * mag + 1e-6 * std::max(1.0, std::fabs(want)) +
                          1e-6 * static_cast<double>(b.wire.numel());
       b.check_work.reset();
       if (!(std::fabs(seen - want) <= tol)) {

@@ -118,6 +118,49 @@ def _header_digest():
     return h.hexdigest()
 
 
+DIGEST_SYMBOL = "dcp_source_digest"
+
+
+def source_digest() -> str:
+    """Content digest of everything the extension is built from: every source
+    and header (relative path + bytes) and the compile / link flags with the
+    checkout's location masked out (the GPU box runs the same tree from a
+    different path). Embedded into ``_C`` at link time (``DIGEST_SYMBOL``) and
+    checked by ``_ext.load()`` before the extension is imported, so a stale
+    binary is rebuilt or refused instead of tested silently."""
+    h = hashlib.sha1()
+    files = _sources() + sorted(list(CSRC.rglob("*.h")) + list(CSRC.rglob("*.cuh")) + list(CSRC.rglob("*.inc")))
+    for p in sorted(files):
+        h.update(str(p.relative_to(CSRC)).encode() + b"\0")
+        h.update(p.read_bytes())
+    cxx, hip = _flags()
+    h.update(" ".join(cxx + hip).replace(str(CSRC), "<csrc>").encode())
+    return h.hexdigest()
+
+
+def embedded_digest(so: Path) -> str | None:
+    """The source digest linked into ``so`` (None if it carries none)."""
+    import ctypes
+
+    try:
+        lib = ctypes.CDLL(str(so))
+        return (ctypes.c_char * 41).in_dll(lib, DIGEST_SYMBOL).value.decode()
+    except (OSError, ValueError):
+        return None
+
+
+def _digest_obj(cxx, digest: str) -> Path:
+    src = BUILD / f"digest.{digest[:16]}.cpp"
+    obj = BUILD / f"digest.{digest[:16]}.o"
+    if not obj.exists():
+        src.write_text(f'extern "C" __attribute__((visibility("default"))) const char {DIGEST_SYMBOL}[41] = '
+                       f'"{digest}";\n')
+        r = subprocess.run(cxx + ["-c", str(src), "-o", str(obj)], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
 def _obj_for(src: Path, cmd, hdr):
     rel = src.relative_to(CSRC)
     key = hashlib.sha1((" ".join(cmd) + hdr).encode() + src.read_bytes()).hexdigest()[:16]
@@ -154,6 +197,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
         with ThreadPoolExecutor(max_workers=n) as ex:
             for src in ex.map(compile_one, tasks):
                 print(f"[dcp build] compiled {src.relative_to(REPO)}", flush=True)
+    objs.append(_digest_obj(cxx, source_digest()))
     out = ext_path()
     newest_obj = max(o.stat().st_mtime for o in objs)
     if force or tasks or not out.exists() or out.stat().st_mtime < newest_obj:
@@ -168,6 +212,9 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     for o in BUILD.glob("*.o"):
         if o.name not in keep:
             o.unlink()
+    for c in BUILD.glob("digest.*.cpp"):
+        if c.with_suffix(".o").name not in keep:
+            c.unlink()
     return out
 
 

@@ -22,24 +22,42 @@ def _try_import():
     return importlib.import_module("distributed_compute_pytorch_amd._C")
 
 
+def _stale() -> str | None:
+    """Why the in-tree ``_C`` does not match ``csrc/`` (None if it does, or if
+    there is no source tree to compare against)."""
+    so = _build.ext_path()
+    if not so.exists() or not _build.CSRC.is_dir():
+        return None
+    want, have = _build.source_digest(), _build.embedded_digest(so)
+    if have != want:
+        return f"{so.name} was built from other sources (embedded digest {have}, csrc/ digest {want})"
+    return None
+
+
 def load():
     global _C
     if _C is not None:
         return _C
-    try:
-        _C = _try_import()
-        return _C
-    except ImportError as e:
-        if os.environ.get("DCP_NO_AUTOBUILD") == "1":
-            raise ImportError(
-                "distributed_compute_pytorch_amd native extension _C is not built; run "
-                "`python -m distributed_compute_pytorch_amd._build`"
-            ) from e
+    why = _stale()
+    if why is None:
+        try:
+            _C = _try_import()
+            return _C
+        except ImportError as e:
+            why = f"import failed: {e}"
+    if os.environ.get("DCP_NO_AUTOBUILD") == "1":
+        raise ImportError(
+            f"distributed_compute_pytorch_amd native extension _C is missing or stale ({why}); run "
+            "`python -m distributed_compute_pytorch_amd._build`"
+        )
+    print(f"[dcp] rebuilding the native extension: {why}", flush=True)
     lock_path = _build.REPO / "build" / ".build.lock"
     lock_path.parent.mkdir(parents=True, exist_ok=True)
     with open(lock_path, "w") as fh:
         fcntl.flock(fh, fcntl.LOCK_EX)
         try:
+            if _stale() is not None:
+                raise ImportError("stale")
             _C = _try_import()
         except ImportError:
             _build.build()

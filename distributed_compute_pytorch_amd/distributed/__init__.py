@@ -100,6 +100,7 @@ class ProcessGroup:
         self._host = None
         self._rccl = None
         self._debug_fp = os.environ.get("DCP_DEBUG_COLLECTIVES") == "1"
+        self._obj_seq = 0  # object-collective calls on this group (store key sequence)
 
     def rank(self) -> int:
         return self._rank
@@ -437,28 +438,44 @@ def barrier(group=None, async_op=False, device_ids=None):
 
 
 # Object collectives ride on the store (rank-local pickles of this program's
-# own objects; nothing external is ever unpickled).
-_obj_seq = {"n": 0}
+# own objects; nothing external is ever unpickled). The call sequence number is
+# per group: only the group's members call its object collectives, so a world
+# counter would drift between members and non-members after a sub-group call
+# and the next world-level call would read different keys on different ranks.
+# Every rank counts its reads done; the last reader deletes the call's keys.
+
+
+def _obj_key(pg, kind):
+    n = pg._obj_seq
+    pg._obj_seq += 1
+    return f"{pg.prefix}/obj/{kind}/{n}"
+
+
+def _obj_release(pg, keys, base):
+    if pg.store.add(f"{base}/done", 1) == pg.size():
+        for k in (*keys, f"{base}/done"):
+            pg.store.delete_key(k)
 
 
 def broadcast_object_list(object_list, src=0, group=None, device=None):
     pg = _group(group)
-    key = f"{pg.prefix}/obj/bcast/{_obj_seq['n']}"
-    _obj_seq["n"] += 1
+    key = _obj_key(pg, "bcast")
     if pg.global_ranks[pg.rank()] == src:
         pg.store.set(key, pickle.dumps(list(object_list)))
     data = pickle.loads(pg.store.get(key))
     for i, o in enumerate(data):
         object_list[i] = o
+    _obj_release(pg, [key], key)
 
 
 def all_gather_object(object_list, obj, group=None):
     pg = _group(group)
-    base = f"{pg.prefix}/obj/gather/{_obj_seq['n']}"
-    _obj_seq["n"] += 1
+    base = _obj_key(pg, "gather")
     pg.store.set(f"{base}/{pg.rank()}", pickle.dumps(obj))
-    for r in range(pg.size()):
-        object_list[r] = pickle.loads(pg.store.get(f"{base}/{r}"))
+    keys = [f"{base}/{r}" for r in range(pg.size())]
+    for r, k in enumerate(keys):
+        object_list[r] = pickle.loads(pg.store.get(k))
+    _obj_release(pg, keys, base)
 
 
 from . import launch  # noqa: E402,F401  (spawn / launch_env / free_port)

@@ -18,6 +18,7 @@ inputs) fall back to ATen for the forward / data gradient.
 """
 from __future__ import annotations
 
+import os
 
 import torch
 from torch import nn
@@ -72,8 +73,28 @@ def autotune_choices() -> dict:
     return {" ".join(str(k) for k in key): ("ours" if v else "hipblaslt") for key, v in _CHOICE.items()}
 
 
+def _agree(key, mine: bool) -> bool:
+    """Every rank of the default group takes rank 0's choice for ``key`` (each
+    rank times on its own GPU and close shapes can time either way: ranks, and
+    through ``fused_mlp_gelu`` even their autograd graphs, would otherwise
+    differ). Through the rendezvous store, not a device collective: the first
+    call of a shape may sit inside a backward whose bucket collectives are in
+    flight."""
+    from .. import distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return mine
+    pg = dist.get_default_group()
+    k = "dcp/linear_autotune/" + " ".join(str(x) for x in key)
+    if pg.rank() == 0:
+        pg.store.set(k, b"1" if mine else b"0")
+    return bytes(pg.store.get(k)) == b"1"
+
+
 def _prefer_ours(key, ours, aten) -> bool:
-    """True when our GEMM is (measured) at least as fast as ATen's for ``key``."""
+    """True when our GEMM is (measured) at least as fast as ATen's for ``key``
+    (rank 0's measurement when a process group is up; a pinned table from
+    ``DCP_LINEAR_CHOICES`` / :func:`load_choices` wins over measuring)."""
     c = _CHOICE.get(key)
     if c is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
@@ -81,8 +102,35 @@ def _prefer_ours(key, ours, aten) -> bool:
         with torch.no_grad():
             to, ta = _measure(ours, aten)
         _TIMES[key] = (to, ta)
-        c = _CHOICE[key] = to <= ta
+        c = _CHOICE[key] = _agree(key, to <= ta)
     return c
+
+
+def save_choices(path: str) -> None:
+    """Write the per-shape choices made so far (JSON, :func:`autotune_choices`
+    form) so a later run can pin them and be reproduced kernel for kernel."""
+    import json
+
+    with open(path, "w") as f:
+        json.dump(autotune_choices(), f, indent=1, sort_keys=True)
+
+
+def load_choices(path: str) -> None:
+    """Pin per-shape choices from a :func:`save_choices` table; shapes it does
+    not list are still measured."""
+    import json
+
+    with open(path) as f:
+        table = json.load(f)
+    for k, v in table.items():
+        kind, *dims = k.split()
+        if v not in ("ours", "hipblaslt"):
+            raise ValueError(f"{path}: {k!r} -> {v!r} (want 'ours' or 'hipblaslt')")
+        _CHOICE[(kind, *(int(d) for d in dims))] = v == "ours"
+
+
+if os.environ.get("DCP_LINEAR_CHOICES"):
+    load_choices(os.environ["DCP_LINEAR_CHOICES"])
 
 
 def autotune_times() -> dict:
@@ -121,11 +169,29 @@ def accumulating() -> bool:
     return _ACCUM_IN_PLACE[0] > 0
 
 
+def _engine_accumulates(p) -> bool:
+    """True when the running backward will execute ``p``'s AccumulateGrad node,
+    i.e. this graph task writes ``p.grad`` at all: ``loss.backward()`` does;
+    ``torch.autograd.grad(loss, x)`` and ``backward(inputs=[x])`` without
+    ``p`` do not (they must leave ``p.grad`` untouched and, for
+    ``autograd.grad(loss, params)``, receive the gradient as a return value)."""
+    from torch.autograd.graph import get_gradient_edge
+
+    try:
+        return bool(torch._C._will_engine_execute_node(get_gradient_edge(p).node))
+    except RuntimeError:  # autograd.grad() with leaf inputs: gradients are returned, not accumulated
+        return False
+
+
 def inplace_grad(p, shape, accum: bool = False):
     """``p.grad`` when a backward may add its fp32 contribution straight into
     it and return None instead (skipping autograd's separate AccumulateGrad
     add — one elementwise launch per parameter per micro-step, 2.37 ms of a
     GPT-2 accum-4 step: profiles/r2_gpt2_kernel_stats_final.txt:11), else None.
+
+    Only when the running graph task accumulates into ``p.grad`` anyway
+    (``_engine_accumulates``: not under ``autograd.grad`` / ``backward(inputs=)``
+    that exclude ``p``), and then
 
     * under ``no_sync`` (``accum``): whenever ``.grad`` holds a compatible
       fp32 buffer (DDP ignores the hooks of these micro-steps);
@@ -142,9 +208,9 @@ def inplace_grad(p, shape, accum: bool = False):
     g = p.grad
     if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != shape or g.requires_grad:
         return None
-    if accum:
-        return g
-    if torch.is_grad_enabled() or p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None):
+    if not accum and (torch.is_grad_enabled() or p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None)):
+        return None
+    if not _engine_accumulates(p):
         return None
     return g
 
@@ -156,7 +222,7 @@ def _acc_target(ctx, p, shape):
 def _gemm_ok(x: torch.Tensor, w: torch.Tensor, bias) -> bool:
     """Shapes our gemm_nt takes (in/out features multiples of 64, ≤ 4096 in)."""
     return (_OUR_FWD and bias is not None and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and w.shape[1] <= 4096
-            and x.is_contiguous())
+            and x.is_contiguous() and x.numel() > 0)
 
 
 def _bias32(bias: torch.Tensor) -> torch.Tensor:
@@ -205,7 +271,7 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
     x2 = x.reshape(-1, x.shape[-1])
     dx = dw = None
     if ctx.needs_input_grad[0]:
-        if (_OUR_DGRAD and wt is not None and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096 and wt.shape[0] % 64 == 0
+        if (_OUR_DGRAD and wt is not None and g2.shape[0] > 0 and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096 and wt.shape[0] % 64 == 0
                 and _prefer_ours(("dgrad", g2.shape[0], g2.shape[1], wt.shape[0]), lambda: _C.conv1x1_dgrad(g2, wt),
                                  lambda: g2 @ w)):
             dx = _C.conv1x1_dgrad(g2, wt).view(x.shape)
@@ -213,7 +279,7 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
             dx = (g2 @ w).view(x.shape)
     weight, bias = ctx.params
     if ctx.needs_input_grad[1]:
-        if g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
+        if g2.shape[0] > 0 and g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
             # our split-M MFMA wgrad GEMM (gemm.hip): faster than hipBLASLt at
             # every BERT / GPT-2 shape (profiles/r1_linear_wgrad_bench.log)
             tgt = _acc_target(ctx, weight, torch.Size((g2.shape[1], x2.shape[1])))
@@ -226,9 +292,12 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
             dw = dw.to(ctx.wdtype)
     if not db_done and ctx.bdtype is not None and ctx.needs_input_grad[2]:
         tgt = _acc_target(ctx, bias, torch.Size((g2.shape[1],)))
-        db = _C.colsum(g2, accumulate_into=tgt)
-        if tgt is not None:
-            db = None
+        if g2.shape[0] == 0:  # empty batch: a zero bias gradient (no column-sum launch)
+            db = torch.zeros(g2.shape[1], device=g2.device, dtype=torch.float32)
+        else:
+            db = _C.colsum(g2, accumulate_into=tgt)
+            if tgt is not None:
+                db = None
     if db is not None and db.dtype != ctx.bdtype:
         db = db.to(ctx.bdtype)
     return dx, dw, db
@@ -435,7 +504,10 @@ def _mlp_prefers_ours(x, w1_16, b1, b1_16, w2_16, w2t, tanh) -> bool:
         b32 = _bias32(b1)
         f = _prefer_ours(key_f, lambda: _C.linear_fwd(x2, w1_16, b32, mode),
                          lambda: _C.gelu_fwd(F.linear(x2, w1_16, b1_16), tanh))
-        g2 = torch.empty(M, N2, device=x.device, dtype=torch.bfloat16).normal_()
+        # a private generator: the stand-in gradient must not move the global
+        # RNG stream that dropout / init draw from
+        gen = torch.Generator(device=x.device).manual_seed(0)
+        g2 = torch.empty(M, N2, device=x.device, dtype=torch.bfloat16).normal_(generator=gen)
         d = _prefer_ours(key_d, lambda: _C.conv1x1_dgrad(g2, w2t), lambda: g2 @ w2_16)
     return f and d
 
@@ -450,7 +522,7 @@ def fused_mlp_gelu(x: torch.Tensor, fc: "FusedLinear", proj: "FusedLinear", appr
     if approximate not in ("none", "tanh"):
         raise ValueError(f"approximate must be 'none' or 'tanh', got {approximate!r}")
     ok = (_FUSED_MLP and _FUSED_GELU and _OUR_FWD and _OUR_DGRAD and isinstance(fc, FusedLinear) and isinstance(proj, FusedLinear)
-          and fc._fast(x) and x.is_contiguous() and fc.bias is not None and proj.bias is not None
+          and fc._fast(x) and x.is_contiguous() and x.numel() > 0 and fc.bias is not None and proj.bias is not None
           and fc.out_features % 64 == 0 and fc.in_features % 64 == 0 and proj.out_features % 64 == 0
           and fc.in_features <= 4096 and proj.in_features <= 4096 and proj.out_features <= 4096
           and proj.in_features == fc.out_features)

@@ -21,13 +21,14 @@ def allreduce_hook(process_group, bucket):
 
 def _compress_hook(dtype):
     def hook(process_group, bucket):
+        # cast to the wire dtype on the compute stream (the pack), average in
+        # that dtype, cast back into the bucket on the collective's stream: the
+        # returned Work completes after the cast back, and nothing waits here
+        # (the Reducer's finalize orders the consumers after it)
         pg = process_group if process_group is not None else dist.get_default_group()
         buf = bucket.buffer()
         wire = buf.to(dtype)
-        w = pg.comm_for(wire).all_reduce(wire, dist.ReduceOp.AVG)
-        w.wait()
-        buf.copy_(wire)
-        return None
+        return pg.comm_for(wire).all_reduce_into(wire, buf, dist.ReduceOp.AVG)
 
     hook.wire_dtype = dtype
     return hook

@@ -41,17 +41,21 @@ DEFAULT_BUCKET_CAP_MB = 25.0
 DEFAULT_FIRST_BUCKET_MB = 1.0
 DEFAULT_TAIL_BUCKET_MB = 0.0
 
-# xGMI-tuned plan for 8x MI355X (NOTES.md §18), opted into by bench.py /
-# train.py / workloads via ``DistributedDataParallel(..., **XGMI_BUCKETS)``:
-# * first bucket 1 MiB: the first all-reduce starts as early as possible;
-# * cap 50 MiB: every bucket but the last overlaps backward, so what matters
-#   is the per-collective latency (~tens of µs) and RCCL reaching its
-#   multi-channel bandwidth on 7 point-to-point links, which needs tens of MB
-#   — fewer, larger collectives (and pack launches) than 25 MiB;
-# * tail 2 MiB: the last bucket's all-reduce is the only one nothing can hide,
-#   so the ready-last parameters get a bucket of their own that a latency-bound
-#   all-reduce finishes in ~α instead of α + (25 MiB remainder) / bandwidth.
-XGMI_BUCKETS = {"bucket_cap_mb": 50.0, "first_bucket_mb": 1.0, "tail_bucket_mb": 2.0}
+# xGMI-tuned plan for 8x MI355X, opted into by bench.py / train.py /
+# workloads via ``DistributedDataParallel(..., **XGMI_BUCKETS)``. Chosen from
+# the one-GPU contention-emulated sweep of an 8-rank ring all-reduce at
+# 300 GB/s bus bandwidth (NOTES §25, profiles/r4_bucket_sweep_emulated.jsonl;
+# cap 4-100 MiB x first bucket 0.25 / 1 / 4 MiB x tail 0 / 2 / 8 MiB, ResNet-50,
+# BERT-base, GPT-2):
+# * cap 16 MiB: the lowest or equal-lowest step time of all three models and
+#   exposed (un-overlapped) comm ResNet-50 0.05 ms, BERT 1.27, GPT-2 2.31 ms
+#   vs 0.055 / 1.58 / 2.89 at 50 MiB — smaller buckets start reducing earlier
+#   and leave less queued behind the ready-last ones; below 16 MiB the pack
+#   launches and per-collective latency cost ResNet-50 0.06-0.09 ms exposed;
+# * first bucket 1 MiB: 0.25 / 1 / 4 MiB measured the same (within 0.01 ms);
+# * tail 2 MiB: the ready-last parameters in a latency-bound bucket of their
+#   own — without it ResNet-50 exposes 0.11 (cap 25) / 0.38 ms (cap 50).
+XGMI_BUCKETS = {"bucket_cap_mb": 16.0, "first_bucket_mb": 1.0, "tail_bucket_mb": 2.0}
 
 
 _DTYPE_IDS = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3, torch.int64: 4,

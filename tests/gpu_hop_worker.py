@@ -57,6 +57,19 @@ def main():
         torch.cuda.synchronize()
         ok = ok and bool((consumed == 2.0 * (trial + 1)).all())
     res["ordering_ok"] = ok
+    # all_reduce_into (compression hooks): the cast back is ordered before the Work
+    ok = True
+    for trial in range(3):
+        wire = torch.zeros(1 << 20, device=dev, dtype=torch.bfloat16)
+        out = torch.full((1 << 20,), -1.0, device=dev)
+        torch.cuda._sleep(50_000_000)
+        wire.fill_(float(trial + 1))
+        w = comm.all_reduce_into(wire, out, dcp.distributed.ReduceOp.AVG)
+        w.wait()
+        consumed = out * 2
+        torch.cuda.synchronize()
+        ok = ok and bool((consumed == 2.0 * (trial + 1)).all())
+    res["reduce_into_ok"] = ok
 
     # ---- every collective (identity on one rank)
     t = torch.arange(16, dtype=torch.float32, device=dev)
@@ -82,12 +95,16 @@ def main():
     results = {}
     for name, kw in (("fp32", {}), ("bf16_wire", {"comm_dtype": torch.bfloat16}),
                      ("grad_view", {"gradient_as_bucket_view": True}),
-                     ("registered", {"gradient_as_bucket_view": True, "register_buckets": True})):
+                     ("registered", {"gradient_as_bucket_view": True, "register_buckets": True}),
+                     ("bf16_hook", {"hook": dcp.parallel.comm_hooks.bf16_compress_hook})):
+        hook = kw.pop("hook", None)
         local = ConvNet().to(dev)
         local.load_state_dict(base.state_dict())
         mine = ConvNet().to(dev)
         mine.load_state_dict(base.state_dict())
         ddp = dcp.parallel.DistributedDataParallel(mine, device_ids=[0], bucket_cap_mb=1, **kw)
+        if hook is not None:
+            ddp.register_comm_hook(None, hook)
         local.eval(), mine.eval()
         o1 = torch.optim.SGD(local.parameters(), lr=0.05, momentum=0.9)
         o2 = dcp.optim.SGD(ddp.parameters(), lr=0.05, momentum=0.9)

@@ -81,3 +81,31 @@ def test_fused_embedding_inplace_accumulation_sees_complete_grad():
             F.linear(m(idx), m.weight).square().mean().backward()
     h.remove()
     torch.testing.assert_close(ours.weight.grad, ref.weight.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_autograd_grad_leaves_populated_grad_untouched():
+    """a backward that does not accumulate into the
+    parameter (autograd.grad w.r.t. the input only, backward(inputs=...)
+    without it, autograd.grad w.r.t. the parameter) must neither add into an
+    already populated .grad nor return None for the parameter."""
+    torch.manual_seed(3)
+    emb = FusedEmbedding(40, 6)
+    idx = torch.randint(0, 40, (3, 5))
+    emb.weight.grad = torch.ones_like(emb.weight)  # e.g. zero_grad(set_to_none=False) + mid-accumulation
+    before = emb.weight.grad.clone()
+    x = emb(idx)
+    h = x * torch.linspace(0.5, 1.5, 6)
+    # gradient w.r.t. the embedding OUTPUT only (input-saliency style)
+    (gx,) = torch.autograd.grad(h.square().sum(), x, retain_graph=True)
+    assert gx.shape == x.shape
+    torch.testing.assert_close(emb.weight.grad, before)
+    # gradient w.r.t. the parameter: returned, .grad untouched
+    (gw,) = torch.autograd.grad(h.square().sum(), emb.weight, retain_graph=True)
+    ref = nn.Embedding(40, 6)
+    ref.load_state_dict(emb.state_dict())
+    (gref,) = torch.autograd.grad((ref(idx) * torch.linspace(0.5, 1.5, 6)).square().sum(), ref.weight)
+    torch.testing.assert_close(gw, gref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(emb.weight.grad, before)
+    # a real backward still accumulates (in place) into the populated .grad
+    h.square().sum().backward()
+    torch.testing.assert_close(emb.weight.grad, before + gref, rtol=1e-5, atol=1e-5)

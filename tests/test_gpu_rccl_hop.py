@@ -28,12 +28,14 @@ def test_single_rank_hop_real_rccl(cuda):
     print(res)
     assert res["comm_stream"] and res["comm_stream_differs"]
     assert res["ordering_ok"]
+    assert res["reduce_into_ok"]
     assert res["collectives_ok"]
     assert res["ops_issued"] >= 8
     errs = res["ddp_max_abs_err"]
     assert errs["fp32"] < 1e-5, errs
     assert errs["grad_view"] < 1e-5, errs
     assert errs["bf16_wire"] < 5e-2, errs  # bf16 gradients on the wire
+    assert errs["bf16_hook"] < 5e-2, errs  # the same through bf16_compress_hook (async cast back)
     assert errs["fp32_buckets"] >= 2
     assert errs["registered"] < 1e-5, errs  # bucket buffers registered with ncclCommRegister
     assert res["register_handle"] > 0 and res["registered_allreduce_ok"]

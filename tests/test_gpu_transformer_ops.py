@@ -288,10 +288,15 @@ def test_colsum_matches_torch(cuda, shape):
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3)
 
 
-def test_fused_linear_matches_fp32(cuda):
+def test_fused_linear_matches_fp32(cuda, monkeypatch):
     from torch import nn
 
+    from distributed_compute_pytorch_amd.ops import linear as lin_mod
     from distributed_compute_pytorch_amd.ops.linear import FusedLinear
+
+    # our gemm_nt is what must be validated: no per-shape autotune to hipBLASLt
+    monkeypatch.setattr(lin_mod, "_AUTOTUNE", False)
+    monkeypatch.setattr(lin_mod, "_CHOICE", {})
 
     torch.manual_seed(0)
     lin = FusedLinear(256, 384).to(cuda)
@@ -322,12 +327,16 @@ def test_fused_linear_matches_fp32(cuda):
 
 @pytest.mark.parametrize("approximate", ["none", "tanh"])
 @pytest.mark.parametrize("rows,fin,fout", [(4 * 64, 256, 1024), (37, 128, 520), (8192, 768, 3072)])
-def test_fused_linear_gelu_matches_fp32(cuda, approximate, rows, fin, fout):
+def test_fused_linear_gelu_matches_fp32(cuda, approximate, rows, fin, fout, monkeypatch):
     """FusedLinear.forward_gelu (GEMM + gelu.hip forward; GELU backward with the
     bias column sums fused) vs an fp32 PyTorch reference on the same bf16 inputs."""
     from torch import nn
 
+    from distributed_compute_pytorch_amd.ops import linear as lin_mod
     from distributed_compute_pytorch_amd.ops.linear import FusedLinear
+
+    monkeypatch.setattr(lin_mod, "_AUTOTUNE", False)
+    monkeypatch.setattr(lin_mod, "_CHOICE", {})
 
     torch.manual_seed(0)
     lin = FusedLinear(fin, fout).to(cuda)
@@ -573,3 +582,28 @@ def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch):
                             (proj.bias.grad, ref[4].grad, "b2")):
         rel = float((got.float() - want).norm() / want.norm())
         assert rel < 2e-2, (name, rel)
+
+
+def test_fused_linear_autograd_grad_leaves_populated_grad(cuda):
+    """torch.autograd.grad(loss, x) with a populated .grad
+    (set_to_none=False / mid-accumulation) must not add the weight gradient
+    into .grad; autograd.grad w.r.t. the weight must return it."""
+    from distributed_compute_pytorch_amd.ops.linear import FusedLinear
+
+    torch.manual_seed(0)
+    lin = FusedLinear(256, 384).to(cuda)
+    lin.weight.grad = torch.ones_like(lin.weight)
+    lin.bias.grad = torch.ones_like(lin.bias)
+    w0, b0 = lin.weight.grad.clone(), lin.bias.grad.clone()
+    x = torch.randn(2, 64, 256, device=cuda, requires_grad=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = lin(x).float().square().mean()
+    (gx,) = torch.autograd.grad(loss, x, retain_graph=True)
+    assert gx.shape == x.shape and torch.isfinite(gx).all()
+    assert torch.equal(lin.weight.grad, w0) and torch.equal(lin.bias.grad, b0)
+    gw, gb = torch.autograd.grad(loss, [lin.weight, lin.bias], retain_graph=True)
+    assert gw is not None and gb is not None and gw.abs().sum() > 0
+    assert torch.equal(lin.weight.grad, w0) and torch.equal(lin.bias.grad, b0)
+    loss.backward()
+    torch.testing.assert_close(lin.weight.grad, w0 + gw, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(lin.bias.grad, b0 + gb, rtol=1e-4, atol=1e-5)

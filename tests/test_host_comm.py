@@ -84,6 +84,35 @@ def test_subgroups():
     run_world(_subgroups, 3)
 
 
+def _subgroup_objects(rank, world):
+    import distributed_compute_pytorch_amd.distributed as dist
+
+    g = dist.new_group([0, 2])
+    if rank in (0, 2):  # members only: their group's object sequence advances
+        objs = [None, None]
+        dist.all_gather_object(objs, ("sub", rank), group=g)
+        assert objs == [("sub", 0), ("sub", 2)]
+        ol = [rank * 7]
+        dist.broadcast_object_list(ol, src=2, group=g)
+        assert ol == [14]
+    # the world-level object collectives afterwards must agree on their keys
+    objs = [None] * world
+    dist.all_gather_object(objs, rank)
+    assert objs == list(range(world))
+    ol = ["x"] if rank == 1 else [None]
+    dist.broadcast_object_list(ol, src=1)
+    assert ol == ["x"]
+    dist.barrier()
+    # every call's keys were deleted by its last reader (rank 0 hosts the store)
+    pg = dist.get_default_group()
+    assert not pg.store.check([f"pg0/obj/gather/0/{r}" for r in range(world)])
+    assert not pg.store.check([f"{g.prefix}/obj/gather/0/0"]) if rank in (0, 2) else True
+
+
+def test_subgroup_object_collectives_then_world():
+    run_world(_subgroup_objects, 3)
+
+
 def _fingerprint(rank, world):
     import datetime
 
