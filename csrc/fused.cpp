@@ -278,6 +278,34 @@ std::vector<at::Tensor> linear_fwd(const at::Tensor& x, const at::Tensor& w, con
   return {y};
 }
 
+// C = x·wᵀ (+ bias) (+ c2 = gelu(C)) on the 8-wave ping-pong 256 x 256 GEMM
+// (gemm_pp.hip). x [..., K] bf16, w [N, K] bf16; returns [C] or [gelu(C), C].
+std::vector<at::Tensor> gemm_pp(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                                int64_t gelu) {
+  DK_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "gemm_pp: contiguous bf16 input");
+  DK_CHECK(gelu >= 0 && gelu <= 2 && (gelu == 0 || b.has_value()), "gemm_pp: gelu 0 / 1 (tanh) / 2 (erf), with a bias");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t K = x.size(-1);
+  const int64_t M = x.numel() / K;
+  DK_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 && w.size(1) == K,
+           "gemm_pp: weight must be contiguous bf16 [N, K]");
+  const int64_t N = w.size(0);
+  DK_CHECK(kern::gemm_pp_supported(M, N, K), "gemm_pp: unsupported shape (N % 8, K % 64)");
+  const float* bp = nullptr;
+  if (b.has_value()) {
+    DK_CHECK(b->scalar_type() == at::kFloat && b->is_contiguous() && b->numel() == N, "gemm_pp: bias must be fp32 [N]");
+    bp = b->data_ptr<float>();
+  }
+  std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end());
+  shape.back() = N;
+  at::Tensor y = at::empty(shape, x.options());
+  at::Tensor g = gelu ? at::empty(shape, x.options()) : at::Tensor();
+  kern::gemm_pp_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, static_cast<int>(N), static_cast<int>(K), N, bp,
+                     gelu ? g.data_ptr() : nullptr, static_cast<int>(gelu), stream_of(x));
+  if (gelu) return {g, y};
+  return {y};
+}
+
 // (w_bf16 [R, C], w_bf16^T [C, R]) from an fp32 (or bf16) weight viewed as [R, C]
 std::vector<at::Tensor> weight_bf16_t(const at::Tensor& w) {
   DK_CHECK(w.is_cuda() && w.dim() >= 2, "weight_bf16_t: device weight required");
@@ -1395,6 +1423,8 @@ void bind(pybind11::module& m) {
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("scale") = pybind11::none(),
         pybind11::arg("shift") = pybind11::none(), pybind11::arg("relu") = false, pybind11::arg("stats") = false);
   m.def("conv1x1_dgrad", &conv1x1_dgrad, pybind11::arg("gy"), pybind11::arg("wt"));
+  m.def("gemm_pp", &gemm_pp, "x·wᵀ (+bias) (+gelu) on the 8-wave ping-pong 256x256 MFMA GEMM", py::arg("x"),
+        py::arg("w"), py::arg("bias") = py::none(), py::arg("gelu") = 0);
   m.def("linear_fwd", &linear_fwd, "Linear forward on the MFMA GEMM: bias (+ GELU tanh/erf) in the epilogue",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("gelu") = 0);
   m.def("attn_ok", &attn_ok);

@@ -41,6 +41,14 @@ void gemm_nt_bias_bf16(const void* A, const void* B, void* C, int64_t M, int N, 
 void gemm_nt_gelubwd_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* h, float* db,
                           bool tanh_approx, hipStream_t s);
 
+// 256 x 256 x 64 8-wave ping-pong GEMM (gemm_pp.hip): C[M, N] (bf16, row
+// stride ldc) = A[M, K]·B[N, K]ᵀ (bf16, K-contiguous), + bias (fp32 [N]) when
+// bias != nullptr; gelu = 1 (tanh) / 2 (erf) also stores c2 = gelu(C) (same
+// ldc). N % 8 == 0 (columns past N are neither read nor written), K % 64 == 0.
+bool gemm_pp_supported(int64_t M, int64_t N, int64_t K);
+void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
+                  void* c2, int gelu, hipStream_t s);
+
 // fp32 weight [R][Cc] → bf16 copy wb [R][Cc] and transposed bf16 wt [Cc][R]
 // (the forward GEMM's B operand and the dgrad GEMM's B operand) in one launch.
 void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s, int taps = 1);

@@ -1,0 +1,333 @@
+// 256 x 256 x 64 bf16 MFMA GEMM with an 8-wave ping-pong schedule (gfx950).
+//
+//   C[M, N] (bf16, ldc) = A[M, K] (bf16, lda = K) · B[N, K]ᵀ (bf16, ldb = K)
+//   [+ bias[N] (fp32) before the rounding] [c2 = gelu(C) from the bf16 C]
+//
+// Why another GEMM: the 128 x 128 ring of gemm.hip runs one barrier per stage
+// with every wave doing the same thing at the same time — PMC showed MFMA busy
+// 34-36 % and SQ_WAIT_ANY 25-31 % on the layer-3 shapes (NOTES §22). Here each
+// SIMD hosts two waves of DIFFERENT wave groups and the groups are staggered
+// by one barrier: while group X (waves 0-3, tile rows 0-127) runs a 16-MFMA
+// segment, group Y (waves 4-7, rows 128-255) issues its LDS fragment reads and
+// its share of the global→LDS DMA, and vice versa — the matrix pipe of every
+// SIMD alternates between its two waves instead of idling through a barrier.
+//
+// Workgroup: 512 threads = 8 waves, wave (wr, wc) = (w / 4, w % 4) owns rows
+// [128 wr, +128) x columns [64 wc, +64) of the tile: 4 quadrants (m-sub mq x
+// n-sub nq) of 64 x 32 = 16 MFMA (16x16x32) per 64-deep K-tile each.
+//
+// LDS: 2 K-tile slots of four 16 KB half-tiles, named by the phase of first
+// use: h0 = A rows m-sub 0 of both groups, h1 = B columns n-sub 0 of the four
+// wave columns, h2 = B n-sub 1, h3 = A m-sub 1; each is a [128][64] bf16 image
+// (128-B rows, 16-B chunks XOR (row >> 1) & 7: the conflict-free ds_read_b128
+// pattern of gemm.hip's BK = 64 ring) filled by global_load_lds_dwordx4 —
+// lane-linear destination, the swizzle is applied to the per-lane SOURCE.
+//
+// K-tile t, four phases p, each { ds_read fragments | issue 2 DMA per wave |
+// counted vmcnt } barrier { 16 MFMA } barrier:
+//   p0: read A(m0), B(n0); DMA h2(t+1); vmcnt(8)   MFMA (m0, n0)
+//   p1: read B(n1);        DMA h3(t+1); vmcnt(8)   MFMA (m0, n1)
+//   p2: read A(m1);        DMA h0(t+2)             MFMA (m1, n1)
+//   p3: —                  DMA h1(t+2); vmcnt(8)   MFMA (m1, n0)
+// With the one-barrier stagger (group Y passes one extra barrier first), in
+// global phase order a half-tile needed at phase s must be retired by every
+// wave's vmcnt in phase ≤ s-1 and a region read in phase q may be re-filled by
+// DMA issued in phase ≥ q+2; the schedule keeps 4 half-tiles (8 DMA per wave)
+// in flight, issued 5 phases (~2,500 cycles) before their first read. DMA for
+// K-tiles past the end go to a 2 KB sink so the vmcnt counts stay uniform.
+//
+// Parity: the Linear / 1x1-conv GEMMs of the BASELINE transformer and ResNet
+// configs (SURVEY §2f K8/K16/K18 and the N9 "MFMA GEMM with fused bias /
+// activation epilogue" stretch item).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gemm_kernels.h"
+
+namespace dcp {
+namespace kern {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kPT = 512;                   // threads
+constexpr int kHT = 16384;                 // half-tile bytes: 128 rows x 128 B
+constexpr int kSlot = 4 * kHT;             // one 64-deep K-tile
+constexpr int kSink = 2 * kSlot;           // 2 KB sink for the DMA of K-tiles past the end
+constexpr int kPPLds = 2 * kSlot + 2048;   // 133,120 B: one workgroup per CU
+
+__device__ __forceinline__ float pp_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float pp_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint32_t pp_pack(float a, float b) {
+  const bf16x2 v = {static_cast<__bf16>(a), static_cast<__bf16>(b)};
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ int pp_swz(int r) { return (r >> 1) & 7; }
+
+__device__ __forceinline__ void pp_glds(const uint16_t* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+// a barrier nothing is scheduled across (neither memory ops nor MFMAs: the
+// ping-pong needs each group's MFMA segment exactly between its two barriers)
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void pp_vm8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+
+template <bool TANH>
+__device__ __forceinline__ float pp_gelu(float x) {
+  if (TANH) {
+    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
+    const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
+    return 0.5f * x * (1.f + t);
+  }
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+
+// EPI: 0 = C = A·Bᵀ; 1 = + bias; 2 / 3 = + bias, c2 = gelu(C) (tanh / erf)
+template <int EPI>
+__global__ void __launch_bounds__(kPT, 1)
+    gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
+                   int64_t M, int N, int K, int64_t ldc, int tiles_n, const float* __restrict__ bias,
+                   uint16_t* __restrict__ c2) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 2, wc = w & 3;
+
+  // bijective XCD remap: the workgroups of one XCD take a contiguous tile range
+  // (the N-tiles of an M-tile share A through that XCD's L2)
+  const int P = static_cast<int>(gridDim.x);
+  const int wid = static_cast<int>(blockIdx.x);
+  const int xcd = wid & 7, q8 = P >> 3, r8 = P & 7;
+  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
+  const int64_t m0 = static_cast<int64_t>(v / tiles_n) * 256;
+  const int n0 = (v % tiles_n) * 256;
+  const int KT = K >> 6;
+
+  // per-lane source element offsets (k = 0) of this wave's two DMA per
+  // half-tile: image row i = 16 w + 8 q + lane / 8, physical chunk lane % 8
+  uint32_t off[4][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = w * 16 + q * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ pp_swz(i);
+    const int arow = i + (i >= 64 ? 64 : 0);          // h0: rows 0-63 | 128-191
+    const int bcol = (i >> 5) * 64 + (i & 31);         // h1: n-sub 0 of wave column i / 32
+    int64_t ra0 = m0 + arow, ra3 = m0 + arow + 64;
+    ra0 = ra0 < M ? ra0 : M - 1;
+    ra3 = ra3 < M ? ra3 : M - 1;
+    int rb1 = n0 + bcol, rb2 = n0 + bcol + 32;
+    rb1 = rb1 < N ? rb1 : N - 1;
+    rb2 = rb2 < N ? rb2 : N - 1;
+    off[0][q] = static_cast<uint32_t>(ra0 * K + lc * 8);
+    off[1][q] = static_cast<uint32_t>(static_cast<int64_t>(rb1) * K + lc * 8);
+    off[2][q] = static_cast<uint32_t>(static_cast<int64_t>(rb2) * K + lc * 8);
+    off[3][q] = static_cast<uint32_t>(ra3 * K + lc * 8);
+  }
+  // DMA of half-tile h of K-tile kt (kt ≥ KT: into the sink, from K-tile 0)
+  auto issue = [&](int h, int kt) {
+    const bool real = kt < KT;
+    const uint16_t* base = (h == 0 || h == 3) ? A : B;
+    const int k0 = real ? kt * 64 : 0;
+    char* dst = real ? lds + (kt & 1) * kSlot + h * kHT + w * 2048 : lds + kSink;
+    pp_glds(base + off[h][0] + k0, dst);
+    pp_glds(base + off[h][1] + k0, dst + 1024);
+  };
+
+  f32x4 acc[2][2][2][4];  // [mq][nq][i: 16-col frag][j: 16-row frag]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];  // [frag][k half]
+  const int lr = lane & 15, lq = lane >> 4;
+  auto read_a = [&](const char* img) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const int r = wr * 64 + j * 16 + lr;
+        af[j][kh] = *reinterpret_cast<const bf16x8*>(img + r * 128 + 16 * ((4 * kh + lq) ^ pp_swz(r)));
+      }
+  };
+  auto read_b = [&](const char* img, bf16x8 (&bf)[2][2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const int r = wc * 32 + i * 16 + lr;
+        bf[i][kh] = *reinterpret_cast<const bf16x8*>(img + r * 128 + 16 * ((4 * kh + lq) ^ pp_swz(r)));
+      }
+  };
+  // the swapped operand order (B fragment as the MFMA's A) gives each lane 4
+  // consecutive output columns of one row: 8-B packed epilogue writes
+  auto mfma = [&](f32x4 (&c)[2][4], const bf16x8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[i][kh], af[j][kh], c[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: h0..h3 of K-tile 0, h0, h1 of K-tile 1; K-tile 0's h0 / h1 retired
+  issue(0, 0);
+  issue(1, 0);
+  issue(2, 0);
+  issue(3, 0);
+  issue(0, 1);
+  issue(1, 1);
+  pp_vm8();
+  pp_barrier();
+  if (wr == 1) pp_barrier();  // the stagger: group Y runs one barrier behind
+
+  for (int kt = 0; kt < KT; ++kt) {
+    const char* s = lds + (kt & 1) * kSlot;
+    // p0
+    read_a(s);
+    read_b(s + kHT, bf0);
+    issue(2, kt + 1);
+    pp_vm8();
+    pp_barrier();
+    mfma(acc[0][0], bf0);
+    pp_barrier();
+    // p1
+    read_b(s + 2 * kHT, bf1);
+    issue(3, kt + 1);
+    pp_vm8();
+    pp_barrier();
+    mfma(acc[0][1], bf1);
+    pp_barrier();
+    // p2
+    read_a(s + 3 * kHT);
+    issue(0, kt + 2);
+    pp_barrier();
+    mfma(acc[1][1], bf1);
+    pp_barrier();
+    // p3
+    issue(1, kt + 2);
+    pp_vm8();
+    pp_barrier();
+    mfma(acc[1][0], bf0);
+    pp_barrier();
+  }
+  if (wr == 0) pp_barrier();  // both groups at the same barrier count; all ring reads done
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (only sink DMA can be outstanding)
+
+  // epilogue: each wave stages its 128 x 64 output (bf16, 128-B rows, 16-B
+  // chunks XOR row & 7) in its own 16 KB of the ring, then stores whole rows
+  char* cst = lds + w * 16384;
+  float bcol[2][2][4];
+  if constexpr (EPI >= 1) {
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = n0 + wc * 64 + nq * 32 + i * 16 + lq * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bcol[nq][i][r] = c + r < N ? bias[c + r] : 0.f;
+      }
+  }
+#pragma unroll
+  for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 a = acc[mq][nq][i][j];
+          if constexpr (EPI >= 1) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[r] += bcol[nq][i][r];
+          }
+          const int row = mq * 64 + j * 16 + lr;
+          const int col = nq * 32 + i * 16 + lq * 4;
+          *reinterpret_cast<uint2*>(cst + row * 128 + 16 * ((col >> 3) ^ (row & 7)) + (col & 7) * 2) =
+              make_uint2(pp_pack(a[0], a[1]), pp_pack(a[2], a[3]));
+        }
+  const int64_t rbase = m0 + wr * 128;
+  const int cb = n0 + wc * 64 + (lane & 7) * 8;  // this lane's 8 output columns
+  // rows (it * 8 + lane / 8) of the staged tile, read 8 at a time ahead of
+  // their guarded stores (a read under the row guard became a branch + full
+  // LDS round trip per row)
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    uint4 val[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = (half * 8 + it) * 8 + (lane >> 3);
+      val[it] = *reinterpret_cast<const uint4*>(cst + row * 128 + 16 * ((lane & 7) ^ (row & 7)));
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it)  // materialise all 8 reads before the guarded stores
+      asm volatile("" ::"v"(val[it].x), "v"(val[it].y), "v"(val[it].z), "v"(val[it].w));
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int64_t m = rbase + (half * 8 + it) * 8 + (lane >> 3);
+      if (m < M && cb < N) {
+        *reinterpret_cast<uint4*>(C + m * ldc + cb) = val[it];
+        if constexpr (EPI >= 2) {
+          const uint32_t v4[4] = {val[it].x, val[it].y, val[it].z, val[it].w};
+          uint32_t g4[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            g4[k] = pp_pack(pp_gelu<EPI == 2>(pp_lo(v4[k])), pp_gelu<EPI == 2>(pp_hi(v4[k])));
+          *reinterpret_cast<uint4*>(c2 + m * ldc + cb) = make_uint4(g4[0], g4[1], g4[2], g4[3]);
+        }
+      }
+    }
+  }
+}
+
+template <int EPI>
+void gemm_pp_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
+                    void* c2, hipStream_t s) {
+  static const bool attr = [] {  // > 64 KB of dynamic LDS
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_pp_kernel<EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPPLds);
+    return true;
+  }();
+  (void)attr;
+  const int tiles_m = static_cast<int>((M + 255) / 256);
+  const int tiles_n = (N + 255) / 256;
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI>), dim3(tiles_m * tiles_n), dim3(kPT), kPPLds, s,
+                     static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
+                     N, K, ldc, tiles_n, bias, static_cast<uint16_t*>(c2));
+}
+}  // namespace
+
+bool gemm_pp_supported(int64_t M, int64_t N, int64_t K) {
+  // 32-bit per-lane source offsets; 16-B output chunks
+  return M >= 1 && N >= 8 && N % 8 == 0 && K >= 64 && K % 64 == 0 && M * K < (int64_t(1) << 31) &&
+         N * K < (int64_t(1) << 31) && (M + 255) / 256 * ((N + 255) / 256) < (int64_t(1) << 31);
+}
+
+void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
+                  void* c2, int gelu, hipStream_t s) {
+  if (bias == nullptr) gemm_pp_launch<0>(A, B, C, M, N, K, ldc, nullptr, nullptr, s);
+  else if (gelu == 1) gemm_pp_launch<2>(A, B, C, M, N, K, ldc, bias, c2, s);
+  else if (gelu == 2) gemm_pp_launch<3>(A, B, C, M, N, K, ldc, bias, c2, s);
+  else gemm_pp_launch<1>(A, B, C, M, N, K, ldc, bias, nullptr, s);
+}
+
+}  // namespace kern
+}  // namespace dcp

@@ -1,0 +1,78 @@
+"""Ping-pong 256x256 GEMM (gemm_pp) vs our 128x128 ring (linear_fwd / conv1x1
+forward) vs hipBLASLt (torch.mm) on the transformer Linear and ResNet-50 1x1
+shapes, random operands, interleaved rounds in one process (median us, TF/s).
+
+    python tools/gemm_pp_bench.py [--rounds 5] [--iters 20] [--json out.jsonl]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_compute_pytorch_amd._ext import C  # noqa: E402
+
+SHAPES = [  # (name, M, N, K)
+    ("bert qkv/o 768->768", 16384, 768, 768), ("bert fc1 768->3072", 16384, 3072, 768),
+    ("bert fc2 3072->768", 16384, 768, 3072), ("bert dgrad fc1 3072->768", 16384, 768, 3072),
+    ("gpt2 c_attn 768->2304", 8192, 2304, 768), ("gpt2 fc 768->3072", 8192, 3072, 768),
+    ("gpt2 proj 3072->768", 8192, 768, 3072), ("gpt2 lmhead 768->50304", 8192, 50304, 768),
+    ("square 4096", 4096, 4096, 4096), ("square 8192", 8192, 8192, 8192),
+    ("rn50 56x56 64->256", 512 * 56 * 56, 256, 64), ("rn50 28x28 512->128", 512 * 28 * 28, 128, 512),
+    ("rn50 14x14 256->1024", 512 * 14 * 14, 1024, 256), ("rn50 14x14 1024->256", 512 * 14 * 14, 256, 1024),
+    ("rn50 7x7 512->2048", 512 * 7 * 7, 2048, 512), ("rn50 7x7 2048->512", 512 * 7 * 7, 512, 2048),
+]
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    out = open(a.json, "a") if a.json else None
+    for name, M, N, K in SHAPES:
+        g = torch.Generator(device=dev).manual_seed(0)
+        x = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        b = torch.zeros(N, device=dev)
+        ops = {"pp": lambda: C.gemm_pp(x, w), "pp_bias": lambda: C.gemm_pp(x, w, b),
+               "blas": lambda: torch.mm(x, w.t())}
+        if N % 64 == 0 and K <= 4096:
+            ops["ring128"] = lambda: C.linear_fwd(x, w, b, 0)
+        y = C.gemm_pp(x, w)[0]
+        ref = torch.mm(x, w.t())
+        rel = float((y.float() - ref.float()).norm() / ref.float().norm())
+        ts = {k: [] for k in ops}
+        for r in range(a.rounds):
+            for k in (list(ops)[r % len(ops):] + list(ops)[:r % len(ops)]):
+                ts[k].append(timeit(ops[k], a.iters))
+        fl = 2.0 * M * N * K
+        rec = {"shape": name, "M": M, "N": N, "K": K, "rel_err_vs_blas": round(rel, 5)}
+        for k, v in ts.items():
+            med = statistics.median(v)
+            rec[k + "_us"] = round(med, 1)
+            rec[k + "_TF"] = round(fl / med / 1e6, 1)
+        print(json.dumps(rec), flush=True)
+        if out:
+            out.write(json.dumps(rec) + "\n")
+        del x, w, y, ref
+
+
+if __name__ == "__main__":
+    main()
