@@ -336,7 +336,7 @@ def main():
                 from distributed_compute_pytorch_amd.ops.linear import autotune_choices, autotune_times
 
                 cfg["linear_gemm_choice"] = autotune_choices()
-                cfg["linear_gemm_us_ours_vs_hipblaslt"] = autotune_times()
+                cfg["linear_gemm_us_by_candidate"] = autotune_times()
             if ours:
                 cfg["bucket_cap_mb"] = round(info["bucket_cap_bytes"] / 2**20, 3)
                 cfg["first_bucket_mb"] = round(info["first_bucket_bytes"] / 2**20, 3)

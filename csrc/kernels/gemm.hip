@@ -1863,6 +1863,7 @@ void gemm_tune(const char* key, int value) {
   if (k == "wg_slots") g_wg_slots = value < 64 ? 64 : value;
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
+  if (k.rfind("pp_", 0) == 0) gemm_pp_tune(key, value);
 }
 int gemm_tune_get(const char* key) {
   const std::string k(key);
@@ -1872,6 +1873,7 @@ int gemm_tune_get(const char* key) {
   if (k == "wg_slots") return g_wg_slots;
   if (k == "wg_cap") return g_wg_cap;
   if (k == "reserve_cus") return g_reserve_cus;
+  if (k.rfind("pp_", 0) == 0) return gemm_pp_tune_get(key);
   return -1;
 }
 

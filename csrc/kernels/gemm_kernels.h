@@ -44,8 +44,12 @@ void gemm_nt_gelubwd_bf16(const void* A, const void* B, void* C, int64_t M, int 
 // 256 x 256 x 64 8-wave ping-pong GEMM (gemm_pp.hip): C[M, N] (bf16, row
 // stride ldc) = A[M, K]·B[N, K]ᵀ (bf16, K-contiguous), + bias (fp32 [N]) when
 // bias != nullptr; gelu = 1 (tanh) / 2 (erf) also stores c2 = gelu(C) (same
-// ldc). N % 8 == 0 (columns past N are neither read nor written), K % 64 == 0.
+// ldc). N % 4 == 0 (columns past N are neither read nor written), K % 64 == 0.
+// One tile per workgroup when N % 8 == 0 (gemm_tune "pp_v1" = 1, default),
+// else persistent over min(tiles, "pp_cus" = 256) workgroups (bias: N <= 7,168).
 bool gemm_pp_supported(int64_t M, int64_t N, int64_t K);
+void gemm_pp_tune(const char* key, int value);
+int gemm_pp_tune_get(const char* key);
 void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
                   void* c2, int gelu, hipStream_t s);
 

@@ -36,12 +36,21 @@
 // in flight, issued 5 phases (~2,500 cycles) before their first read. DMA for
 // K-tiles past the end go to a 2 KB sink so the vmcnt counts stay uniform.
 //
+// Persistent: a workgroup streams its tiles' K-tiles as one sequence, so the
+// next tile's first K-tiles are loading while the current tile finishes; the
+// epilogue stores straight from the accumulators (no LDS: the ring is busy)
+// and is counted in the next K-tile's vmcnt waits. A bias is staged in LDS
+// once (an ordinary global load in the loop would make hipcc drain vmcnt).
+//
 // Parity: the Linear / 1x1-conv GEMMs of the BASELINE transformer and ResNet
 // configs (SURVEY §2f K8/K16/K18 and the N9 "MFMA GEMM with fused bias /
 // activation epilogue" stretch item).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
 
 #include "gemm_kernels.h"
 
@@ -57,7 +66,10 @@ constexpr int kPT = 512;                   // threads
 constexpr int kHT = 16384;                 // half-tile bytes: 128 rows x 128 B
 constexpr int kSlot = 4 * kHT;             // one 64-deep K-tile
 constexpr int kSink = 2 * kSlot;           // 2 KB sink for the DMA of K-tiles past the end
-constexpr int kPPLds = 2 * kSlot + 2048;   // 133,120 B: one workgroup per CU
+constexpr int kPPLds = 2 * kSlot + 2048;   // 133,120 B (+ 4 N B of bias): one workgroup per CU
+int g_pp_cus = 256;                        // persistent grid size (gemm_tune "pp_cus")
+int g_pp_stage = 1;                        // LDS-staged epilogue for the last tile (gemm_tune "pp_stage")
+int g_pp_v1 = 1;                           // one tile per workgroup (gemm_tune "pp_v1"; 0: persistent)
 
 __device__ __forceinline__ float pp_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float pp_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -81,6 +93,16 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 __device__ __forceinline__ void pp_vm8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+// 16-B LDS read hidden from hipcc's waitcnt pass: a plain LDS read issued while
+// global_load_lds DMA is in flight makes it wait vmcnt(0) first (it cannot
+// tell the bias area from the DMA's destination), which drains the ring
+__device__ __forceinline__ f32x4 pp_lds_f4(const float* p) {
+  f32x4 v;
+  const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p));
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  __builtin_amdgcn_sched_barrier(0);  // nothing may use v before the wait (rule: hipcc hoists past asm waits)
+  return v;
+}
 
 template <bool TANH>
 __device__ __forceinline__ float pp_gelu(float x) {
@@ -92,10 +114,13 @@ __device__ __forceinline__ float pp_gelu(float x) {
   return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
 }
 
+// One tile per workgroup (the first version, kept for grids of at most one
+// tile per CU, where it measured faster than the persistent kernel: no cursor
+// bookkeeping, bias from registers, the whole epilogue staged in LDS).
 // EPI: 0 = C = A·Bᵀ; 1 = + bias; 2 / 3 = + bias, c2 = gelu(C) (tanh / erf)
 template <int EPI>
 __global__ void __launch_bounds__(kPT, 1)
-    gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
+    gemm_pp1_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                    int64_t M, int N, int K, int64_t ldc, int tiles_n, const float* __restrict__ bias,
                    uint16_t* __restrict__ c2) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -298,31 +323,448 @@ __global__ void __launch_bounds__(kPT, 1)
   }
 }
 
+// The tile's rows of A (h0 / h3) and columns of B (h1 / h2) this lane's two
+// DMA per half-tile fetch: image row i = 16 w + 8 q + lane / 8, physical chunk
+// lane % 8 (logical chunk lc = that ^ swz(i)). Element offsets at k = 0.
+struct PPCur {
+  int g;               // global K-tile index of this workgroup's stream
+  int kt;              // K-tile within the tile
+  int v;               // tile id
+  int64_t m0;          // tile origin (rows of A / C)
+  int n0;              // tile origin (rows of B, columns of C)
+  int remm;            // last valid tile row / column (255 on full tiles)
+  int remn;
+  const uint16_t* pa;  // A at (m0, 64 kt): the K-tile's DMA source bases (uniform)
+  const uint16_t* pb;  // B at (n0, 64 kt)
+  int dsto;            // LDS destination of the wave's DMA: slot + 2 KB x wave, or the sink
+  int hstep;           // per half-tile LDS step (0 into the sink)
+};
+
+// EPI: 0 = C = A·Bᵀ; 1 = + bias; 2 / 3 = + bias, c2 = gelu(C) (tanh / erf).
+// Persistent: workgroup wg streams tiles wg, wg + P, ... as one continuous
+// sequence of K-tiles (the DMA of the next tile's first K-tiles is in flight
+// while this tile's last ones are multiplied and its epilogue is stored).
+// The last tile's epilogue stages through the (then idle) LDS ring and stores
+// whole 128-B rows (stage_last); earlier tiles store 8 B per lane from the
+// accumulators.
+template <int EPI>
+__global__ void __launch_bounds__(kPT, 1)
+    gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
+                   int64_t M, int N, int K, int64_t ldc, int tiles_m, int tiles_n, const float* __restrict__ bias,
+                   uint16_t* __restrict__ C2, int stage_last) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int lr = lane & 15, lq = lane >> 4;
+
+  // bijective XCD remap of the P workgroups: one XCD's workgroups take
+  // consecutive tile ids (the N-tiles of an M-tile share A in that XCD's L2)
+  const int P = static_cast<int>(gridDim.x);
+  const int wid = static_cast<int>(blockIdx.x);
+  const int xcd = wid & 7, q8 = P >> 3, r8 = P & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
+  const int tiles = tiles_m * tiles_n;
+  const int KT = K >> 6;
+  const int G = ((tiles - wg + P - 1) / P) * KT;  // K-tiles this workgroup streams
+
+  float* bl = reinterpret_cast<float*>(lds + kPPLds);  // EPI >= 1: bias [N] in LDS
+  if constexpr (EPI >= 1) {
+    for (int i = t; i < N; i += kPT) bl[i] = bias[i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  // per-lane constants of the DMA images: image row i = 16 w + 8 q + lane / 8
+  // → tile row of A (h0; h3 = +64) / tile column of B (h1; h2 = +32), and the
+  // logical 16-B chunk of physical chunk lane % 8
+  int arow[2], bcol[2], lc8[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = w * 16 + q * 8 + (lane >> 3);
+    arow[q] = i + (i >= 64 ? 64 : 0);
+    bcol[q] = (i >> 5) * 64 + (i & 31);
+    lc8[q] = ((lane & 7) ^ pp_swz(i)) * 8;
+  }
+  auto set_dst = [&](PPCur& c) {
+    const bool real = c.g < G;  // past the stream's end: into the sink (every wave's vmcnt sequence unchanged)
+    c.dsto = real ? (c.g & 1) * kSlot + w * 2048 : kSink;
+    c.hstep = real ? kHT : 0;
+  };
+  auto set_tile = [&](PPCur& c) {
+    const int vv = c.v < tiles ? c.v : 0;  // past the end: a valid tile (its DMA goes to the sink)
+    c.m0 = static_cast<int64_t>(vv / tiles_n) * 256;
+    c.n0 = (vv % tiles_n) * 256;
+    const int64_t rm = M - 1 - c.m0;
+    c.remm = rm < 255 ? static_cast<int>(rm) : 255;
+    c.remn = N - 1 - c.n0 < 255 ? N - 1 - c.n0 : 255;
+    c.pa = A + c.m0 * K;
+    c.pb = B + static_cast<int64_t>(c.n0) * K;
+  };
+  // next K-tile; true when it starts a tile (the per-lane offsets change)
+  auto advance = [&](PPCur& c) -> bool {
+    ++c.g;
+    bool nt = false;
+    if (++c.kt == KT) {
+      c.kt = 0;
+      c.v += P;
+      set_tile(c);
+      nt = true;
+    } else {
+      c.pa += 64;
+      c.pb += 64;
+    }
+    set_dst(c);
+    return nt;
+  };
+  // tile-relative element offsets (k = 0) of this lane's DMA q of half-tile h
+  // (rows / columns past the edge clamp to the last valid one)
+  auto rel = [&](int h, int q, const PPCur& c) -> uint32_t {
+    int r;
+    if (h == 0 || h == 3) r = min(arow[q] + (h == 3 ? 64 : 0), c.remm);
+    else r = min(bcol[q] + (h == 2 ? 32 : 0), c.remn);
+    return static_cast<uint32_t>(r * K + lc8[q]);
+  };
+  // DMA of half-tile h of cursor c's K-tile: uniform base pointer + per-lane
+  // 32-bit offset, every address precomputed when the cursor advanced
+  auto issue = [&](int h, const PPCur& c, const uint32_t (&o)[2]) {
+    const uint16_t* base = (h == 0 || h == 3) ? c.pa : c.pb;
+    char* dst = lds + c.dsto + h * c.hstep;
+    pp_glds(base + o[0], dst);
+    pp_glds(base + o[1], dst + 1024);
+  };
+
+  f32x4 acc[2][2][2][4];  // [mq][nq][i: 16-col frag][j: 16-row frag]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];  // [frag][k half]
+  auto read_a = [&](const char* img) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const int r = wr * 64 + j * 16 + lr;
+        af[j][kh] = *reinterpret_cast<const bf16x8*>(img + r * 128 + 16 * ((4 * kh + lq) ^ pp_swz(r)));
+      }
+  };
+  auto read_b = [&](const char* img, bf16x8 (&bf)[2][2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const int r = wc * 32 + i * 16 + lr;
+        bf[i][kh] = *reinterpret_cast<const bf16x8*>(img + r * 128 + 16 * ((4 * kh + lq) ^ pp_swz(r)));
+      }
+  };
+  // the swapped operand order (B fragment as the MFMA's A) gives each lane 4
+  // consecutive output columns of one row
+  auto mfma = [&](f32x4 (&c)[2][4], const bf16x8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[i][kh], af[j][kh], c[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // vmcnt before the barrier of a phase: 4 half-tiles of DMA stay in flight;
+  // after a tile's epilogue its ES stores were issued after the awaited DMA too
+  constexpr int ES = EPI >= 2 ? 32 : 16;
+  // 4 bf16 of one row from the accumulator (+ bias), packed
+  auto pack4 = [&](const f32x4& a, const f32x4& bv, uint32_t& p01, uint32_t& p23) {
+    p01 = pp_pack(a[0] + bv[0], a[1] + bv[1]);
+    p23 = pp_pack(a[2] + bv[2], a[3] + bv[3]);
+  };
+  auto gelu2 = [&](uint32_t p) {
+    return pp_pack(pp_gelu<EPI == 2>(pp_lo(p)), pp_gelu<EPI == 2>(pp_hi(p)));
+  };
+  auto bias4 = [&](int col) {
+    f32x4 bv = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI >= 1) bv = pp_lds_f4(bl + (col < N ? col : 0));
+    return bv;
+  };
+
+  // cursors: c0 = the K-tile being multiplied, c1 = the next one (its h2 / h3
+  // are issued in phases 0 / 1), c2 = the one after that (h0 / h1, phases 2 / 3)
+  PPCur c0{};
+  c0.v = wg;
+  set_tile(c0);
+  set_dst(c0);
+  PPCur c1 = c0;
+  advance(c1);
+  PPCur c2 = c1;
+  advance(c2);
+  uint32_t o0[2], o1[2], o2[2], o3[2];  // c2: h0, h1; c1: h2, h3
+  {
+    uint32_t t0[2], t1[2], t2[2], t3[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      t0[q] = rel(0, q, c0);
+      t1[q] = rel(1, q, c0);
+      t2[q] = rel(2, q, c0);
+      t3[q] = rel(3, q, c0);
+      o0[q] = rel(0, q, c1);
+      o1[q] = rel(1, q, c1);
+    }
+    // prologue: h0..h3 of K-tile 0, h0 / h1 of K-tile 1; K-tile 0's h0 / h1 retired
+    issue(0, c0, t0);
+    issue(1, c0, t1);
+    issue(2, c0, t2);
+    issue(3, c0, t3);
+    issue(0, c1, o0);
+    issue(1, c1, o1);
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    o2[q] = rel(2, q, c1);
+    o3[q] = rel(3, q, c1);
+    o0[q] = rel(0, q, c2);
+    o1[q] = rel(1, q, c2);
+  }
+  pp_vm8();
+  pp_barrier();
+  if (wr == 1) pp_barrier();  // the stagger: group Y runs one barrier behind
+
+  // The first K-tile of every tile waits with ES more ops in flight (the
+  // previous tile's epilogue stores were issued after its awaited DMA); the
+  // stream's first tile has no epilogue before it, so ES one-byte DMA into the
+  // sink stand in for those stores and every tile runs the same code.
+  for (int e = 0; e < ES; ++e)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(A + lane),
+                                     (__attribute__((address_space(3))) void*)(lds + kSink), 1, 0, 0);
+
+  // one 64-deep K-tile (4 phases); FIRST = the first K-tile of a tile
+  auto ktile = [&](int g, auto first) {
+    constexpr bool FIRST = decltype(first)::value;
+    auto wait = [&]() {
+      if constexpr (FIRST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + ES) : "memory");
+      else pp_vm8();
+    };
+    const char* s = lds + (g & 1) * kSlot;
+    // p0
+    read_a(s);
+    read_b(s + kHT, bf0);
+    issue(2, c1, o2);
+    wait();
+    pp_barrier();
+    mfma(acc[0][0], bf0);
+    pp_barrier();
+    // p1
+    read_b(s + 2 * kHT, bf1);
+    issue(3, c1, o3);
+    wait();
+    pp_barrier();
+    mfma(acc[0][1], bf1);
+    pp_barrier();
+    // p2
+    read_a(s + 3 * kHT);
+    issue(0, c2, o0);
+    pp_barrier();
+    mfma(acc[1][1], bf1);
+    pp_barrier();
+    // p3 (no fragment reads: the cursors advance here, c0 ← c1 ← c2 ← next;
+    // the per-lane offsets only change with the tile)
+    issue(1, c2, o1);
+    c0 = c1;
+    c1 = c2;
+    if (c1.kt == 0) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        o2[q] = rel(2, q, c1);
+        o3[q] = rel(3, q, c1);
+      }
+    }
+    if (advance(c2)) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        o0[q] = rel(0, q, c2);
+        o1[q] = rel(1, q, c2);
+      }
+    }
+    wait();
+    pp_barrier();
+    mfma(acc[1][0], bf0);
+    pp_barrier();
+  };
+
+  int g = 0;
+  while (g < G) {
+    const PPCur cur = c0;  // this tile
+    ktile(g++, std::true_type{});
+    for (int k = 1; k < KT; ++k) ktile(g++, std::false_type{});
+    if (stage_last && g == G) break;  // the last tile: staged through the idle ring below
+    // epilogue straight from the accumulators. A lane holds 4 consecutive
+    // columns (lq) of row lr of each 16 x 16 fragment; v_permlane16_swap
+    // between the fragments of rows j0 = 2jj and j1 = 2jj + 1 gives lanes
+    // with even lq 8 columns of row j0 and lanes with odd lq 8 columns of
+    // row j1: one 16-B store per lane per fragment pair (half the store
+    // instructions of 8-B stores; the tail is store-issue bound). Exactly ES
+    // stores per wave (guards only mask lanes).
+    const bool full = cur.remm == 255 && cur.remn == 255;
+    const int rrow = wr * 128 + lr + (lq & 1) * 16, rcol = wc * 64 + (lq >> 1) * 8;  // tile-relative
+    uint16_t* cp = C + (cur.m0 + rrow) * ldc + cur.n0 + rcol;
+    uint16_t* gp = EPI >= 2 ? C2 + (cp - C) : nullptr;
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int dc = nq * 32 + i * 16;
+        const f32x4 bv = bias4(cur.n0 + wc * 64 + lq * 4 + dc);
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            uint32_t x01, x23, y01, y23;
+            pack4(acc[mq][nq][i][2 * jj], bv, x01, x23);
+            pack4(acc[mq][nq][i][2 * jj + 1], bv, y01, y23);
+            const auto r0 = __builtin_amdgcn_permlane16_swap(x01, y01, false, false);
+            const auto r1 = __builtin_amdgcn_permlane16_swap(x23, y23, false, false);
+            const uint4 v = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+            const int dr = mq * 64 + jj * 32;
+            const int64_t o = dr * ldc + dc;
+            if (full || (rrow + dr <= cur.remm && rcol + dc + 7 <= cur.remn)) {
+              *reinterpret_cast<uint4*>(cp + o) = v;
+              if constexpr (EPI >= 2)
+                *reinterpret_cast<uint4*>(gp + o) = make_uint4(gelu2(v.x), gelu2(v.y), gelu2(v.z), gelu2(v.w));
+            } else if (rrow + dr <= cur.remm && rcol + dc + 3 <= cur.remn) {  // N % 8 == 4: the last 4 columns
+              *reinterpret_cast<uint2*>(cp + o) = make_uint2(v.x, v.y);
+              if constexpr (EPI >= 2) *reinterpret_cast<uint2*>(gp + o) = make_uint2(gelu2(v.x), gelu2(v.y));
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[mq][nq][i][2 * jj + j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+  }
+  if (wr == 0) pp_barrier();  // both groups at the same barrier count; every ring read done
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sink DMA / stores drained
+  if (!stage_last || G == 0) return;
+
+  // the last tile (c0 has moved past it: recompute its origin): each wave stages
+  // its 128 x 64 output (bf16, 128-B rows, 16-B chunks XOR row & 7) in its own
+  // 16 KB of the idle ring and stores whole rows
+  PPCur cl{};
+  cl.v = wg + ((G / KT) - 1) * P;
+  set_tile(cl);
+  char* cst = lds + w * 16384;
+#pragma unroll
+  for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int col = nq * 32 + i * 16 + lq * 4;
+      const f32x4 bv = bias4(cl.n0 + wc * 64 + col);
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = mq * 64 + j * 16 + lr;
+          uint32_t p01, p23;
+          pack4(acc[mq][nq][i][j], bv, p01, p23);
+          *reinterpret_cast<uint2*>(cst + row * 128 + 16 * ((col >> 3) ^ (row & 7)) + (col & 7) * 2) =
+              make_uint2(p01, p23);
+        }
+    }
+  const int64_t rbase = cl.m0 + wr * 128;
+  const int cb = cl.n0 + wc * 64 + (lane & 7) * 8;  // this lane's 8 output columns
+  // rows (it * 8 + lane / 8) of the staged tile, read 8 at a time ahead of
+  // their guarded stores (a read under the row guard became a branch + full
+  // LDS round trip per row)
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    uint4 val[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = (half * 8 + it) * 8 + (lane >> 3);
+      val[it] = *reinterpret_cast<const uint4*>(cst + row * 128 + 16 * ((lane & 7) ^ (row & 7)));
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it)  // materialise all 8 reads before the guarded stores
+      asm volatile("" ::"v"(val[it].x), "v"(val[it].y), "v"(val[it].z), "v"(val[it].w));
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int64_t m = rbase + (half * 8 + it) * 8 + (lane >> 3);
+      if (m < M && cb < N) {
+        if (cb + 8 <= N) {
+          *reinterpret_cast<uint4*>(C + m * ldc + cb) = val[it];
+        } else {  // N % 8 == 4: the last 4 columns
+          *reinterpret_cast<uint2*>(C + m * ldc + cb) = make_uint2(val[it].x, val[it].y);
+        }
+        if constexpr (EPI >= 2) {
+          const uint32_t g4[4] = {gelu2(val[it].x), gelu2(val[it].y), gelu2(val[it].z), gelu2(val[it].w)};
+          if (cb + 8 <= N)
+            *reinterpret_cast<uint4*>(C2 + m * ldc + cb) = make_uint4(g4[0], g4[1], g4[2], g4[3]);
+          else
+            *reinterpret_cast<uint2*>(C2 + m * ldc + cb) = make_uint2(g4[0], g4[1]);
+        }
+      }
+    }
+  }
+}
+
 template <int EPI>
 void gemm_pp_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
                     void* c2, hipStream_t s) {
   static const bool attr = [] {  // > 64 KB of dynamic LDS
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_pp_kernel<EPI>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kPPLds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)attr;
   const int tiles_m = static_cast<int>((M + 255) / 256);
   const int tiles_n = (N + 255) / 256;
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI>), dim3(tiles_m * tiles_n), dim3(kPT), kPPLds, s,
-                     static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
-                     N, K, ldc, tiles_n, bias, static_cast<uint16_t*>(c2));
+  const int tiles = tiles_m * tiles_n;
+  const int P = tiles < g_pp_cus ? tiles : g_pp_cus;
+  if (g_pp_v1 && N % 8 == 0) {  // one tile per workgroup (measured faster than the persistent loop, NOTES §25)
+    static const bool attr1 = [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_pp1_kernel<EPI>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kPPLds);
+      return true;
+    }();
+    (void)attr1;
+    hipLaunchKernelGGL((gemm_pp1_kernel<EPI>), dim3(tiles), dim3(kPT), kPPLds, s, static_cast<const uint16_t*>(A),
+                       static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N, K, ldc, tiles_n, bias,
+                       static_cast<uint16_t*>(c2));
+    return;
+  }
+  const size_t lds = kPPLds + (EPI >= 1 ? static_cast<size_t>(N) * 4 : 0);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI>), dim3(P), dim3(kPT), lds, s, static_cast<const uint16_t*>(A),
+                     static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N, K, ldc, tiles_m, tiles_n,
+                     bias, static_cast<uint16_t*>(c2), g_pp_stage);
 }
 }  // namespace
 
+void gemm_pp_tune(const char* key, int value) {
+  const std::string k(key);
+  if (k == "pp_cus") g_pp_cus = value < 8 ? 8 : (value > 256 ? 256 : value);
+  if (k == "pp_stage") g_pp_stage = value != 0;
+  if (k == "pp_v1") g_pp_v1 = value != 0;
+}
+int gemm_pp_tune_get(const char* key) {
+  const std::string k(key);
+  if (k == "pp_cus") return g_pp_cus;
+  if (k == "pp_stage") return g_pp_stage;
+  if (k == "pp_v1") return g_pp_v1;
+  return -1;
+}
+
 bool gemm_pp_supported(int64_t M, int64_t N, int64_t K) {
-  // 32-bit per-lane source offsets; 16-B output chunks
-  return M >= 1 && N >= 8 && N % 8 == 0 && K >= 64 && K % 64 == 0 && M * K < (int64_t(1) << 31) &&
+  // 32-bit per-lane source offsets; 8-B output chunks
+  return M >= 1 && N >= 4 && N % 4 == 0 && K >= 64 && K % 64 == 0 && M * K < (int64_t(1) << 31) &&
          N * K < (int64_t(1) << 31) && (M + 255) / 256 * ((N + 255) / 256) < (int64_t(1) << 31);
 }
 
 void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
                   void* c2, int gelu, hipStream_t s) {
+  if (bias != nullptr && !(g_pp_v1 && N % 8 == 0) && static_cast<size_t>(N) * 4 + kPPLds > 160 * 1024)
+    throw std::runtime_error("gemm_pp: the persistent kernel's bias epilogue needs N <= 7,168");
   if (bias == nullptr) gemm_pp_launch<0>(A, B, C, M, N, K, ldc, nullptr, nullptr, s);
   else if (gelu == 1) gemm_pp_launch<2>(A, B, C, M, N, K, ldc, bias, c2, s);
   else if (gelu == 2) gemm_pp_launch<3>(A, B, C, M, N, K, ldc, bias, c2, s);

@@ -32,18 +32,22 @@ _FUSED_GELU = True
 # bench.py --linear-path, for same-box A/Bs)
 _OUR_FWD = True
 _OUR_DGRAD = True
-# per GEMM shape, the first call (eager, not under HIP-graph capture) times our
-# kernel against hipBLASLt and keeps the faster one — as cudnn.benchmark does
-# for convolutions. Ours wins at GPT-2's 8,192 rows, hipBLASLt's 256-wide tiles
-# at BERT's 16,384 (profiles/r3_linear_fwd_dgrad_vs_blas.jsonl, NOTES §22).
+# per GEMM shape, the first call (eager, not under HIP-graph capture) times the
+# candidate kernels and keeps the fastest — as cudnn.benchmark does for
+# convolutions: "pp" = the 256 x 256 8-wave ping-pong GEMM (gemm_pp.hip),
+# "ring" = the 128 x 128 ring (gemm.hip gemm_nt), "hipblaslt" = ATen.
+# (profiles/r4_gemm_pp_bench_variants.jsonl, NOTES §25)
 _AUTOTUNE = True
 _CHOICE: dict = {}
+# our kernel when nothing is measured (autotune off, or under graph capture)
+_DEFAULT_OURS = "pp"
 # MLP blocks as one node with the GELU backward in the second GEMM's epilogue
 # (False: two FusedLinear nodes + the GELU-backward kernel; bench.py --linear-path ours-unfused-mlp)
 _FUSED_MLP = True
+_CANDIDATES = ("pp", "ring", "hipblaslt")
 
 
-_TIMES: dict = {}  # key -> (ours ms, hipBLASLt ms) of the autotune measurement
+_TIMES: dict = {}  # key -> {candidate: ms} of the autotune measurement
 
 
 def _time_ms(fn, iters: int = 5) -> float:
@@ -56,24 +60,25 @@ def _time_ms(fn, iters: int = 5) -> float:
     return s.elapsed_time(e) / iters
 
 
-def _measure(ours, aten, rounds: int = 3):
-    """Best-of-``rounds`` per-call time of each side, the sides interleaved
-    (a single back-to-back pair flipped choices between runs on close shapes)."""
-    ours()
-    aten()
-    to, ta = [], []
+def _measure(cands: dict, rounds: int = 3) -> dict:
+    """Best-of-``rounds`` per-call time of each candidate, the candidates
+    interleaved (a single back-to-back pair flipped choices between runs on
+    close shapes)."""
+    for fn in cands.values():
+        fn()
+    ts = {k: [] for k in cands}
     for _ in range(rounds):
-        to.append(_time_ms(ours))
-        ta.append(_time_ms(aten))
-    return min(to), min(ta)
+        for k, fn in cands.items():
+            ts[k].append(_time_ms(fn))
+    return {k: min(v) for k, v in ts.items()}
 
 
 def autotune_choices() -> dict:
-    """{"fwd|fwd_gelu|dgrad M K N": "ours" | "hipblaslt"} measured so far."""
-    return {" ".join(str(k) for k in key): ("ours" if v else "hipblaslt") for key, v in _CHOICE.items()}
+    """{"fwd|fwd_gelu|dgrad M K N": "pp" | "ring" | "hipblaslt"} chosen so far."""
+    return {" ".join(str(k) for k in key): v for key, v in _CHOICE.items()}
 
 
-def _agree(key, mine: bool) -> bool:
+def _agree(key, mine: str) -> str:
     """Every rank of the default group takes rank 0's choice for ``key`` (each
     rank times on its own GPU and close shapes can time either way: ranks, and
     through ``fused_mlp_gelu`` even their autograd graphs, would otherwise
@@ -87,22 +92,24 @@ def _agree(key, mine: bool) -> bool:
     pg = dist.get_default_group()
     k = "dcp/linear_autotune/" + " ".join(str(x) for x in key)
     if pg.rank() == 0:
-        pg.store.set(k, b"1" if mine else b"0")
-    return bytes(pg.store.get(k)) == b"1"
+        pg.store.set(k, mine.encode())
+    return bytes(pg.store.get(k)).decode()
 
 
-def _prefer_ours(key, ours, aten) -> bool:
-    """True when our GEMM is (measured) at least as fast as ATen's for ``key``
-    (rank 0's measurement when a process group is up; a pinned table from
-    ``DCP_LINEAR_CHOICES`` / :func:`load_choices` wins over measuring)."""
+def _pick(key, cands: dict) -> str:
+    """The kernel to run for ``key`` among ``cands`` (name -> zero-argument
+    launch): the measured fastest (rank 0's measurement when a process group is
+    up; a pinned table from ``DCP_LINEAR_CHOICES`` / :func:`load_choices` wins
+    over measuring); ``_DEFAULT_OURS`` (else "ring") with autotune off."""
     c = _CHOICE.get(key)
-    if c is None:
-        if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
-            return True
-        with torch.no_grad():
-            to, ta = _measure(ours, aten)
-        _TIMES[key] = (to, ta)
-        c = _CHOICE[key] = _agree(key, to <= ta)
+    if c is not None and c in cands:
+        return c
+    if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        return _DEFAULT_OURS if _DEFAULT_OURS in cands else ("ring" if "ring" in cands else next(iter(cands)))
+    with torch.no_grad():
+        ts = _measure(cands)
+    _TIMES[key] = ts
+    c = _CHOICE[key] = _agree(key, min(ts, key=ts.get))
     return c
 
 
@@ -116,17 +123,18 @@ def save_choices(path: str) -> None:
 
 
 def load_choices(path: str) -> None:
-    """Pin per-shape choices from a :func:`save_choices` table; shapes it does
-    not list are still measured."""
+    """Pin per-shape choices from a :func:`save_choices` table ("ours" is read
+    as "ring", the round-3 name); shapes it does not list are still measured."""
     import json
 
     with open(path) as f:
         table = json.load(f)
     for k, v in table.items():
         kind, *dims = k.split()
-        if v not in ("ours", "hipblaslt"):
-            raise ValueError(f"{path}: {k!r} -> {v!r} (want 'ours' or 'hipblaslt')")
-        _CHOICE[(kind, *(int(d) for d in dims))] = v == "ours"
+        v = "ring" if v == "ours" else v
+        if v not in _CANDIDATES:
+            raise ValueError(f"{path}: {k!r} -> {v!r} (want one of {_CANDIDATES})")
+        _CHOICE[(kind, *(int(d) for d in dims))] = v
 
 
 if os.environ.get("DCP_LINEAR_CHOICES"):
@@ -134,8 +142,15 @@ if os.environ.get("DCP_LINEAR_CHOICES"):
 
 
 def autotune_times() -> dict:
-    """{"fwd|fwd_gelu|dgrad M K N": [ours µs, hipBLASLt µs]} of the autotune measurements."""
-    return {" ".join(str(k) for k in key): [round(a * 1e3, 1), round(b * 1e3, 1)] for key, (a, b) in _TIMES.items()}
+    """{"fwd|fwd_gelu|dgrad M K N": {candidate: µs}} of the autotune measurements."""
+    return {" ".join(str(k) for k in key): {n: round(t * 1e3, 1) for n, t in v.items()} for key, v in _TIMES.items()}
+
+
+def _pp_ok(M: int, N: int, K: int) -> bool:
+    """Shapes the ping-pong GEMM takes (K % 64, N % 8; 32-bit operand offsets)."""
+    return K % 64 == 0 and N % 8 == 0 and M > 0 and M * K < 2**31 and N * K < 2**31
+
+
 # let the fused Adam/AdamW write the bf16 weight copies the forward GEMMs read
 # (False: one cast launch per weight per forward; NOTES §15)
 _SHADOWS = True
@@ -225,6 +240,20 @@ def _gemm_ok(x: torch.Tensor, w: torch.Tensor, bias) -> bool:
             and x.is_contiguous() and x.numel() > 0)
 
 
+def _fwd_cands(x2, w, b, b32, mode: int) -> dict:
+    """Forward candidates (Linear + bias [+ GELU: mode 1 tanh / 2 erf])."""
+    M, K, N = x2.shape[0], w.shape[1], w.shape[0]
+    c = {}
+    if _pp_ok(M, N, K):
+        c["pp"] = lambda: _C.gemm_pp(x2, w, b32, mode)
+    c["ring"] = lambda: _C.linear_fwd(x2, w, b32, mode)
+    if mode:
+        c["hipblaslt"] = lambda: _C.gelu_fwd(F.linear(x2, w, b), mode == 1)
+    else:
+        c["hipblaslt"] = lambda: F.linear(x2, w, b)
+    return c
+
+
 def _bias32(bias: torch.Tensor) -> torch.Tensor:
     b = bias.detach()
     return b if b.dtype == torch.float32 and b.is_contiguous() else b.float().contiguous()
@@ -237,8 +266,11 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, w16t)
         if _gemm_ok(x, w, bias):
             x2, b32 = x.reshape(-1, x.shape[-1]), _bias32(bias)
-            if _prefer_ours(("fwd", x2.shape[0], w.shape[1], w.shape[0]), lambda: _C.linear_fwd(x2, w, b32, 0),
-                            lambda: F.linear(x2, w, b)):
+            M, K, N = x2.shape[0], w.shape[1], w.shape[0]
+            c = _pick(("fwd", M, K, N), _fwd_cands(x2, w, b, b32, 0))
+            if c == "pp":
+                return _C.gemm_pp(x, w, b32, 0)[0]
+            if c == "ring":
                 return _C.linear_fwd(x, w, b32, 0)[0]
         return F.linear(x, w, b)
 
@@ -263,6 +295,16 @@ def _setup(ctx, x, weight, bias, w16, b16):
     return x, w, b
 
 
+def _dgrad_cands(g2, w, wt) -> dict:
+    """Data-gradient candidates: dX = dY·W, as dY·(Wᵀ)ᵀ on our NT GEMMs."""
+    c = {}
+    if _pp_ok(g2.shape[0], wt.shape[0], g2.shape[1]):
+        c["pp"] = lambda: _C.gemm_pp(g2, wt)
+    c["ring"] = lambda: _C.conv1x1_dgrad(g2, wt)
+    c["hipblaslt"] = lambda: g2 @ w
+    return c
+
+
 def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
     """(dx, dW, db) of y = x Wᵀ + b from the bf16 [M, N] output gradient g2.
     ``db_done``: the bias gradient was already produced by the caller (``db``,
@@ -271,9 +313,13 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
     x2 = x.reshape(-1, x.shape[-1])
     dx = dw = None
     if ctx.needs_input_grad[0]:
-        if (_OUR_DGRAD and wt is not None and g2.shape[0] > 0 and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096 and wt.shape[0] % 64 == 0
-                and _prefer_ours(("dgrad", g2.shape[0], g2.shape[1], wt.shape[0]), lambda: _C.conv1x1_dgrad(g2, wt),
-                                 lambda: g2 @ w)):
+        c = "hipblaslt"
+        if (_OUR_DGRAD and wt is not None and g2.shape[0] > 0 and g2.shape[1] % 64 == 0 and g2.shape[1] <= 4096
+                and wt.shape[0] % 64 == 0):
+            c = _pick(("dgrad", g2.shape[0], g2.shape[1], wt.shape[0]), _dgrad_cands(g2, w, wt))
+        if c == "pp":
+            dx = _C.gemm_pp(g2, wt)[0].view(x.shape)
+        elif c == "ring":
             dx = _C.conv1x1_dgrad(g2, wt).view(x.shape)
         else:
             dx = (g2 @ w).view(x.shape)
@@ -315,10 +361,14 @@ class _LinearGeluFn(torch.autograd.Function):
         ctx.tanh = tanh_approx
         mode = 1 if tanh_approx else 2
         x2 = x.reshape(-1, x.shape[-1])
-        if _gemm_ok(x, w, bias) and _prefer_ours(
-                ("fwd_gelu", x2.shape[0], w.shape[1], w.shape[0]), lambda: _C.linear_fwd(x2, w, _bias32(bias), mode),
-                lambda: _C.gelu_fwd(F.linear(x2, w, b), tanh_approx)):
-            y, h = _C.linear_fwd(x, w, _bias32(bias), mode)  # h and gelu(h) from one GEMM epilogue
+        c = "hipblaslt"
+        if _gemm_ok(x, w, bias):
+            b32 = _bias32(bias)
+            c = _pick(("fwd_gelu", x2.shape[0], w.shape[1], w.shape[0]), _fwd_cands(x2, w, b, b32, mode))
+        if c == "pp":
+            y, h = _C.gemm_pp(x, w, b32, mode)  # h and gelu(h) from one GEMM epilogue
+        elif c == "ring":
+            y, h = _C.linear_fwd(x, w, b32, mode)
         else:
             h = F.linear(x, w, b)
             y = _C.gelu_fwd(h, tanh_approx)
@@ -451,10 +501,17 @@ class _MLPFn(torch.autograd.Function):
         mode = 1 if tanh else 2
         x2 = x.reshape(-1, x.shape[-1])
         b1_32, b2_32 = _bias32(b1), _bias32(b2)
-        y1, h = _C.linear_fwd(x, w1_16, b1_32, mode)
+        c1 = _CHOICE.get(("fwd_gelu", x2.shape[0], w1_16.shape[1], w1_16.shape[0]), _DEFAULT_OURS)
+        if c1 == "pp" and _pp_ok(x2.shape[0], w1_16.shape[0], w1_16.shape[1]):
+            y1, h = _C.gemm_pp(x, w1_16, b1_32, mode)
+        else:
+            y1, h = _C.linear_fwd(x, w1_16, b1_32, mode)
         y1_2 = y1.reshape(-1, y1.shape[-1])
-        if _prefer_ours(("fwd", y1_2.shape[0], w2_16.shape[1], w2_16.shape[0]),
-                        lambda: _C.linear_fwd(y1_2, w2_16, b2_32, 0), lambda: F.linear(y1_2, w2_16, b2_16_of(b2))):
+        c2 = _pick(("fwd", y1_2.shape[0], w2_16.shape[1], w2_16.shape[0]),
+                   _fwd_cands(y1_2, w2_16, b2_16_of(b2), b2_32, 0))
+        if c2 == "pp":
+            out = _C.gemm_pp(y1, w2_16, b2_32, 0)[0]
+        elif c2 == "ring":
             out = _C.linear_fwd(y1, w2_16, b2_32, 0)[0]
         else:
             out = F.linear(y1, w2_16, b2_16_of(b2))
@@ -491,25 +548,27 @@ class _MLPFn(torch.autograd.Function):
 
 
 def _mlp_prefers_ours(x, w1_16, b1, b1_16, w2_16, w2t, tanh) -> bool:
+    """The fused MLP node runs fc on our kernel (pp or ring, with the GELU
+    epilogue) and proj's data gradient on the ring's GELU-backward epilogue:
+    take it where the per-shape picks are ours for fc's forward and the ring
+    for proj's plain data gradient (where pp or hipBLASLt wins that GEMM, the
+    unfused path runs it there plus the separate GELU-backward pass)."""
     M, K = x.numel() // x.shape[-1], x.shape[-1]
     N1, N2 = w1_16.shape[0], w2_16.shape[0]
     key_f, key_d = ("fwd_gelu", M, K, N1), ("dgrad", M, N2, N1)
-    if key_f in _CHOICE and key_d in _CHOICE:
-        return _CHOICE[key_f] and _CHOICE[key_d]
-    if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
-        return True
-    mode = 1 if tanh else 2
-    with torch.no_grad():
-        x2 = x.detach().reshape(M, K).to(torch.bfloat16)
-        b32 = _bias32(b1)
-        f = _prefer_ours(key_f, lambda: _C.linear_fwd(x2, w1_16, b32, mode),
-                         lambda: _C.gelu_fwd(F.linear(x2, w1_16, b1_16), tanh))
-        # a private generator: the stand-in gradient must not move the global
-        # RNG stream that dropout / init draw from
-        gen = torch.Generator(device=x.device).manual_seed(0)
-        g2 = torch.empty(M, N2, device=x.device, dtype=torch.bfloat16).normal_(generator=gen)
-        d = _prefer_ours(key_d, lambda: _C.conv1x1_dgrad(g2, w2t), lambda: g2 @ w2_16)
-    return f and d
+    if not (key_f in _CHOICE and key_d in _CHOICE):
+        if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
+            return True
+        mode = 1 if tanh else 2
+        with torch.no_grad():
+            x2 = x.detach().reshape(M, K).to(torch.bfloat16)
+            _pick(key_f, _fwd_cands(x2, w1_16, b1_16, _bias32(b1), mode))
+            # a private generator: the stand-in gradient must not move the global
+            # RNG stream that dropout / init draw from
+            gen = torch.Generator(device=x.device).manual_seed(0)
+            g2 = torch.empty(M, N2, device=x.device, dtype=torch.bfloat16).normal_(generator=gen)
+            _pick(key_d, _dgrad_cands(g2, w2_16, w2t))
+    return _CHOICE[key_f] != "hipblaslt" and _CHOICE[key_d] == "ring"
 
 
 def b2_16_of(b):

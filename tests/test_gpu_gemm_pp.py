@@ -20,19 +20,38 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
 
 
+# persistent grid: ≤ 256 workgroups stream several tiles each once tiles > 256
+# (K = 64 / 128: one / two K-tiles per tile, so the DMA runs 1-2 tiles ahead
+# across tile boundaries; N % 4 tails; M tails)
 SHAPES = [(256, 256, 64), (512, 768, 768), (1000, 264, 128), (37, 520, 192), (4096, 3072, 768),
-          (777, 2304, 3072), (256, 4096, 640), (16384, 768, 3072)]
+          (777, 2304, 3072), (256, 4096, 640), (16384, 768, 3072), (8192, 2304, 768), (9000, 2052, 128),
+          (262144, 256, 64), (100352, 1024, 256), (3001, 4100, 320)]
+
+
+@pytest.fixture(params=["default", "persistent", "persistent_regepi"])
+def pp_variant(request):
+    """default: single-tile kernel for grids of <= 256 tiles, else persistent
+    with the last tile staged through LDS; persistent: the persistent kernel
+    for every grid; _regepi: every tile's epilogue from the registers."""
+    from distributed_compute_pytorch_amd._ext import C
+
+    v1, stage = {"default": (1, 1), "persistent": (0, 1), "persistent_regepi": (0, 0)}[request.param]
+    C.gemm_tune("pp_v1", v1)
+    C.gemm_tune("pp_stage", stage)
+    yield request.param
+    C.gemm_tune("pp_v1", 1)
+    C.gemm_tune("pp_stage", 1)
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("mode", ["plain", "bias", "gelu_tanh", "gelu_erf"])
-def test_gemm_pp_matches_fp32(cuda, M, N, K, mode):
+def test_gemm_pp_matches_fp32(cuda, M, N, K, mode, pp_variant):
     from distributed_compute_pytorch_amd._ext import C
 
-    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
-    x = (torch.rand(M, K, generator=g) * 2 - 1).to(cuda).to(torch.bfloat16)
-    w = ((torch.rand(N, K, generator=g) * 2 - 1) / K ** 0.5).to(cuda).to(torch.bfloat16)
-    b = (torch.rand(N, generator=g) - 0.5).to(cuda) if mode != "plain" else None
+    gd = torch.Generator(device=cuda).manual_seed(M * 7 + N * 3 + K)
+    x = (torch.rand(M, K, device=cuda, generator=gd) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=cuda, generator=gd) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+    b = (torch.rand(N, device=cuda, generator=gd) - 0.5) if mode != "plain" else None
     gelu = {"plain": 0, "bias": 0, "gelu_tanh": 1, "gelu_erf": 2}[mode]
     out = C.gemm_pp(x, w, b, gelu)
     ref = _ref(x, w, b)

@@ -288,15 +288,18 @@ def test_colsum_matches_torch(cuda, shape):
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3)
 
 
-def test_fused_linear_matches_fp32(cuda, monkeypatch):
+@pytest.mark.parametrize("ours", ["pp", "ring"])
+def test_fused_linear_matches_fp32(cuda, monkeypatch, ours):
     from torch import nn
 
     from distributed_compute_pytorch_amd.ops import linear as lin_mod
     from distributed_compute_pytorch_amd.ops.linear import FusedLinear
 
-    # our gemm_nt is what must be validated: no per-shape autotune to hipBLASLt
+    # our GEMM (ping-pong or ring) is what must be validated: no per-shape
+    # autotune to hipBLASLt
     monkeypatch.setattr(lin_mod, "_AUTOTUNE", False)
     monkeypatch.setattr(lin_mod, "_CHOICE", {})
+    monkeypatch.setattr(lin_mod, "_DEFAULT_OURS", ours)
 
     torch.manual_seed(0)
     lin = FusedLinear(256, 384).to(cuda)
@@ -325,9 +328,10 @@ def test_fused_linear_matches_fp32(cuda, monkeypatch):
     assert lin.bias.grad.dtype == torch.float32 and rel(lin.bias.grad, br.grad) < 1e-3
 
 
+@pytest.mark.parametrize("ours", ["pp", "ring"])
 @pytest.mark.parametrize("approximate", ["none", "tanh"])
 @pytest.mark.parametrize("rows,fin,fout", [(4 * 64, 256, 1024), (37, 128, 520), (8192, 768, 3072)])
-def test_fused_linear_gelu_matches_fp32(cuda, approximate, rows, fin, fout, monkeypatch):
+def test_fused_linear_gelu_matches_fp32(cuda, approximate, rows, fin, fout, monkeypatch, ours):
     """FusedLinear.forward_gelu (GEMM + gelu.hip forward; GELU backward with the
     bias column sums fused) vs an fp32 PyTorch reference on the same bf16 inputs."""
     from torch import nn
@@ -337,6 +341,7 @@ def test_fused_linear_gelu_matches_fp32(cuda, approximate, rows, fin, fout, monk
 
     monkeypatch.setattr(lin_mod, "_AUTOTUNE", False)
     monkeypatch.setattr(lin_mod, "_CHOICE", {})
+    monkeypatch.setattr(lin_mod, "_DEFAULT_OURS", ours)
 
     torch.manual_seed(0)
     lin = FusedLinear(fin, fout).to(cuda)
@@ -550,8 +555,9 @@ def test_linear_dgrad_gelu_matches_fp32(cuda, tanh, rows, n1, n2):
     torch.testing.assert_close(acc, 1 + gh.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("ours", ["pp", "ring"])
 @pytest.mark.parametrize("approx", ["tanh", "none"])
-def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch):
+def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch, ours):
     """ops.linear.fused_mlp_gelu (one node: GELU forward in fc's epilogue,
     GELU backward + fc's bias sum in proj's dgrad epilogue) vs fp32 PyTorch of
     proj(gelu(fc(x))) on the same bf16-rounded parameters and input. The
@@ -561,6 +567,7 @@ def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch):
 
     monkeypatch.setattr(lin, "_AUTOTUNE", False)
     monkeypatch.setattr(lin, "_CHOICE", {})
+    monkeypatch.setattr(lin, "_DEFAULT_OURS", ours)
 
     torch.manual_seed(0)
     fc, proj = FusedLinear(256, 1024).to(cuda), FusedLinear(1024, 256).to(cuda)

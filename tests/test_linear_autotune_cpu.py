@@ -1,0 +1,44 @@
+"""Linear GEMM selection (ops/linear.py): pinned choices round-trip through a
+JSON table and win over measuring; with autotune off the default kernel runs
+(what the GPU numerics tests rely on to validate our kernels, not hipBLASLt)."""
+import json
+
+from distributed_compute_pytorch_amd.ops import linear as lin
+
+
+def _cands(log):
+    return {n: (lambda n=n: log.append(n)) for n in ("pp", "ring", "hipblaslt")}
+
+
+def test_default_when_autotune_off(monkeypatch):
+    monkeypatch.setattr(lin, "_AUTOTUNE", False)
+    monkeypatch.setattr(lin, "_CHOICE", {})
+    for d in ("pp", "ring"):
+        monkeypatch.setattr(lin, "_DEFAULT_OURS", d)
+        assert lin._pick(("fwd", 8, 64, 64), _cands([])) == d
+    # a shape the ping-pong GEMM does not take falls back to the ring
+    monkeypatch.setattr(lin, "_DEFAULT_OURS", "pp")
+    c = _cands([])
+    del c["pp"]
+    assert lin._pick(("fwd", 8, 64, 60), c) == "ring"
+    assert lin._CHOICE == {}  # nothing measured, nothing recorded
+
+
+def test_pinned_choices_roundtrip(monkeypatch, tmp_path):
+    monkeypatch.setattr(lin, "_CHOICE", {("fwd", 8192, 768, 2304): "pp", ("dgrad", 8192, 2304, 768): "hipblaslt"})
+    path = tmp_path / "choices.json"
+    lin.save_choices(str(path))
+    table = json.loads(path.read_text())
+    assert table == {"fwd 8192 768 2304": "pp", "dgrad 8192 2304 768": "hipblaslt"}
+    table["fwd_gelu 16 64 128"] = "ours"  # round-3 tables name the ring "ours"
+    path.write_text(json.dumps(table))
+    monkeypatch.setattr(lin, "_CHOICE", {})
+    lin.load_choices(str(path))
+    assert lin._CHOICE[("fwd_gelu", 16, 64, 128)] == "ring"
+    # pinned choices win over measuring (which would need a GPU here)
+    monkeypatch.setattr(lin, "_AUTOTUNE", True)
+    assert lin._pick(("dgrad", 8192, 2304, 768), _cands([])) == "hipblaslt"
+
+
+def test_agree_single_process_keeps_local_choice():
+    assert lin._agree(("fwd", 1, 2, 3), "ring") == "ring"

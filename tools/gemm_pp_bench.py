@@ -51,13 +51,22 @@ def main():
         x = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
         w = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
         b = torch.zeros(N, device=dev)
-        ops = {"pp": lambda: C.gemm_pp(x, w), "pp_bias": lambda: C.gemm_pp(x, w, b),
+        def pp(stage, v1=1, bias=None):
+            C.gemm_tune("pp_stage", stage)
+            C.gemm_tune("pp_v1", v1)
+            return C.gemm_pp(x, w, bias)
+
+        ops = {"pp": lambda: pp(1), "pp_persist": lambda: pp(1, 0), "pp_persist_regepi": lambda: pp(0, 0),
                "blas": lambda: torch.mm(x, w.t())}
+        if N <= 7168:
+            ops["pp_bias"] = lambda: pp(1, 1, b)
         if N % 64 == 0 and K <= 4096:
             ops["ring128"] = lambda: C.linear_fwd(x, w, b, 0)
-        y = C.gemm_pp(x, w)[0]
         ref = torch.mm(x, w.t())
-        rel = float((y.float() - ref.float()).norm() / ref.float().norm())
+        rel = 0.0
+        for v in (ops["pp"], ops["pp_persist"], ops["pp_persist_regepi"]):
+            y = v()[0]
+            rel = max(rel, float((y.float() - ref.float()).norm() / ref.float().norm()))
         ts = {k: [] for k in ops}
         for r in range(a.rounds):
             for k in (list(ops)[r % len(ops):] + list(ops)[:r % len(ops)]):
