@@ -79,9 +79,15 @@ def parse():
     ap.add_argument("--tail-bucket-mb", type=float, default=None,
                     help="size of the ready-last tail bucket split off the plan (0 = no split)")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--overlap-optimizer", type=int, default=-1,
+                    help="DDP overlap_optimizer: the fused optimizer updates each bucket's parameters as soon as "
+                         "its reduction lands (-1: on for the transformers, whose ready-last embedding bucket "
+                         "is 90-150 MB)")
     ap.add_argument("--grad-as-view", type=int, default=1)
     ap.add_argument("--benchmark-cudnn", type=int, default=1)
-    ap.add_argument("--graph", type=int, default=0, help="capture the whole step in a HIP graph")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the whole step in a HIP graph (-1: per model — on for the launch-bound "
+                         "reference ConvNet / MLP, whose eager step is host-issue bound, off otherwise)")
     ap.add_argument("--backend", choices=["rccl", "gloo"], default="rccl",
                     help="gloo: the reference's literal backend (main.py:50) — GPU tensors staged through the "
                          "host; ours = the C++ host communicator, stock = torch's gloo")
@@ -175,6 +181,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.graph < 0:
+        a.graph = 1 if a.model in ("convnet", "mlp") and a.impl == "ours" and a.backend == "rccl" else 0
     if world != a.gpus:
         log(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if a.comm_timing:
@@ -262,6 +270,9 @@ def main():
                 kw["tail_bucket_mb"] = a.tail_bucket_mb
             if a.comm_dtype == "bf16":
                 kw["comm_dtype"] = torch.bfloat16
+            ov = a.overlap_optimizer if a.overlap_optimizer >= 0 else int(a.model in ("gpt2", "bert"))
+            if ov and a.grad_as_view:
+                kw["overlap_optimizer"] = True
             with stream_ctx():
                 ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[local],
                                                            gradient_as_bucket_view=bool(a.grad_as_view), **kw)
@@ -341,6 +352,7 @@ def main():
                 cfg["bucket_cap_mb"] = round(info["bucket_cap_bytes"] / 2**20, 3)
                 cfg["first_bucket_mb"] = round(info["first_bucket_bytes"] / 2**20, 3)
                 cfg["tail_bucket_mb"] = round(ddp.tail_bucket_bytes / 2**20, 3)
+                cfg["overlap_optimizer"] = bool(ddp.overlap_optimizer)
                 cfg["buckets_mb"] = [round(b / 2**20, 2) for b in info["bucket_sizes"]]
             elif cap_mb is not None:
                 cfg["bucket_cap_mb"] = cap_mb

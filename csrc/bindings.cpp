@@ -153,7 +153,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("comm_dtype", &ReducerOptions::comm_dtype)
       .def_readwrite("average", &ReducerOptions::average)
       .def_readwrite("register_buckets", &ReducerOptions::register_buckets)
-      .def_readwrite("check_streams", &ReducerOptions::check_streams);
+      .def_readwrite("check_streams", &ReducerOptions::check_streams)
+      .def_readwrite("defer_grad_wait", &ReducerOptions::defer_grad_wait);
 
   m.def("trace_enabled", &trace::enabled);
   m.def("trace_push", [](const std::string& n) { trace::push(n.c_str()); });
@@ -197,6 +198,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("bucket_buffers", &Reducer::bucket_buffers)
       .def("ready_order", &Reducer::ready_order)
       .def("wait_all", &Reducer::wait_all, py::call_guard<py::gil_scoped_release>())
+      .def("deferred_buckets", &Reducer::deferred_buckets)
+      .def("sync_bucket", &Reducer::sync_bucket, py::call_guard<py::gil_scoped_release>())
+      .def("sync_all", &Reducer::sync_all, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("num_iterations", &Reducer::num_iterations)
       .def_property_readonly("num_rebuilds", &Reducer::num_rebuilds);
 

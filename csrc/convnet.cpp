@@ -90,9 +90,58 @@ at::Tensor bwd(const at::Tensor& g_in, const at::Tensor& mask, const at::Tensor&
   return grads;
 }
 
+// y [M, N] = x [M, K] · w [N, K]ᵀ (+ b): the head's Linear forward, fp32 MFMA
+at::Tensor fc32_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b) {
+  DK_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 2, "fc32_fwd: x [M, K] fp32");
+  DK_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.dim() == 2 && w.size(1) == x.size(1),
+           "fc32_fwd: w [N, K] fp32");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int M = static_cast<int>(x.size(0)), K = static_cast<int>(x.size(1)), N = static_cast<int>(w.size(0));
+  const float* bp = nullptr;
+  if (b.has_value()) {
+    DK_CHECK(b->scalar_type() == at::kFloat && b->is_contiguous() && b->numel() == N, "fc32_fwd: b [N] fp32");
+    bp = b->data_ptr<float>();
+  }
+  at::Tensor y = at::empty({M, N}, x.options());
+  const int64_t wsn = kern::fc32_workspace(M, N, K);
+  at::Tensor ws = wsn ? at::empty({wsn}, x.options()) : at::Tensor();
+  kern::fc32_gemm(x.data_ptr<float>(), K, 1, w.data_ptr<float>(), K, 1, y.data_ptr<float>(), N, M, N, K, bp, nullptr,
+                  wsn ? ws.data_ptr<float>() : nullptr, stream_of(x));
+  return y;
+}
+
+// (dx [M, K] or undefined, dw [N, K], db [N]) of y = x·wᵀ + b from g [M, N]
+std::vector<at::Tensor> fc32_bwd(const at::Tensor& g, const at::Tensor& x, const at::Tensor& w, bool need_dx) {
+  DK_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.is_contiguous() && g.dim() == 2, "fc32_bwd: g [M, N] fp32");
+  DK_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 2 && x.size(0) == g.size(0),
+           "fc32_bwd: x [M, K] fp32");
+  DK_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.size(0) == g.size(1) && w.size(1) == x.size(1),
+           "fc32_bwd: w [N, K] fp32");
+  c10::hip::HIPGuard guard(g.device().index());
+  const int M = static_cast<int>(g.size(0)), N = static_cast<int>(g.size(1)), K = static_cast<int>(x.size(1));
+  at::Tensor dx;
+  if (need_dx) {  // dx[m][k] = Σ_n g[m][n] · w[n][k]
+    dx = at::empty({M, K}, g.options());
+    const int64_t wsn = kern::fc32_workspace(M, K, N);
+    at::Tensor ws = wsn ? at::empty({wsn}, g.options()) : at::Tensor();
+    kern::fc32_gemm(g.data_ptr<float>(), N, 1, w.data_ptr<float>(), 1, K, dx.data_ptr<float>(), K, M, K, N, nullptr,
+                    nullptr, wsn ? ws.data_ptr<float>() : nullptr, stream_of(g));
+  }
+  // dw[n][k] = Σ_m g[m][n] · x[m][k], db[n] = Σ_m g[m][n]
+  at::Tensor dw = at::empty({N, K}, g.options());
+  at::Tensor db = at::empty({N}, g.options());
+  kern::fc32_gemm(g.data_ptr<float>(), 1, N, x.data_ptr<float>(), 1, K, dw.data_ptr<float>(), K, N, K, M, nullptr,
+                  db.data_ptr<float>(), nullptr, stream_of(g));
+  return {dx, dw, db};
+}
+
 void bind(pybind11::module& m) {
   namespace py = pybind11;
   m.def("convnet_supported", &supported, py::arg("x"));
+  m.def("fc32_fwd", &fc32_fwd, "fp32 MFMA Linear forward (the ConvNet head)", py::arg("x"), py::arg("w"),
+        py::arg("b") = py::none());
+  m.def("fc32_bwd", &fc32_bwd, "fp32 MFMA Linear backward: (dx, dw, db)", py::arg("g"), py::arg("x"), py::arg("w"),
+        py::arg("need_dx") = true);
   m.def("convnet_features_fwd", &fwd, py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("drop_p") = 0.0, py::arg("seed") = 0, py::arg("offset_dev") = py::none());
   m.def("convnet_features_bwd", &bwd, py::arg("g"), py::arg("mask"), py::arg("x"), py::arg("w1"), py::arg("b1"),

@@ -37,5 +37,14 @@ int64_t convnet_bwd_workspace(int B);
 void convnet_bwd(const float* g, const uint8_t* mask, const float* x, const float* w1, const float* b1,
                  const float* w2, float scale, float* ws, float* grads, int B, bool accumulate, hipStream_t s);
 
+// fp32 MFMA GEMM of the fully connected head (fc32.hip):
+//   C[i][j] (ldc) = Σ_k A[i·sai + k·sak] · B[j·sbj + k·sbk] (+ bias[j])
+// db != nullptr: also db[i] = Σ_k A(i, k) (no K split then). ws: fp32
+// workspace of fc32_workspace(M, N, K) floats (the K-split partial slabs).
+int fc32_splits(int M, int N, int K);
+int64_t fc32_workspace(int M, int N, int K);
+void fc32_gemm(const float* A, int64_t sai, int64_t sak, const float* B, int64_t sbj, int64_t sbk, float* C,
+               int64_t ldc, int M, int N, int K, const float* bias, float* db, float* ws, hipStream_t s);
+
 }  // namespace kern
 }  // namespace dcp

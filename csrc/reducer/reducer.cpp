@@ -107,26 +107,80 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
   timing_ = t && std::strcmp(t, "1") == 0 && !params_.empty() && params_[0].is_cuda();
   const char* ds = std::getenv("DCP_DEBUG_STREAMS");
   check_ = opts_.check_streams || (ds && std::strcmp(ds, "1") == 0);
-  if (timing_) {
-    DK_CHECK(hipEventCreate(&ev_bwd_end_) == hipSuccess && hipEventCreate(&ev_final_) == hipSuccess,
-              "Reducer: event creation failed");
-  }
 }
 
 double Reducer::exposed_comm_ms() {
   std::lock_guard<std::mutex> g(mu_);
   if (!timing_ || !ev_recorded_) return -1.0;
-  if (hipEventSynchronize(ev_final_) != hipSuccess) return -1.0;
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, ev_bwd_end_, ev_final_) != hipSuccess) return -1.0;
-  return ms;
+  double total = 0.0;
+  for (auto& b : buckets_) {
+    if (!b.stall_recorded) continue;
+    if (hipEventSynchronize(b.stall1) != hipSuccess) return -1.0;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, b.stall0, b.stall1) != hipSuccess) return -1.0;
+    total += ms;
+  }
+  return total;
+}
+
+void Reducer::wait_bucket(Bucket& b, hipStream_t cur, bool timed) {
+  if (timed) {
+    if (!b.stall0) {
+      DK_CHECK(hipEventCreate(&b.stall0) == hipSuccess && hipEventCreate(&b.stall1) == hipSuccess,
+               "Reducer: event creation failed");
+    }
+    (void)hipEventRecord(b.stall0, cur);
+  }
+  b.work->wait();
+  if (timed) {
+    (void)hipEventRecord(b.stall1, cur);
+    b.stall_recorded = true;
+    ev_recorded_ = true;
+  }
+}
+
+void Reducer::sync_locked(Bucket& b) {
+  if (!b.deferred) return;
+  hipStream_t cur = nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (b.flat.is_cuda()) {
+    cur = c10::hip::getCurrentHIPStream(b.flat.device().index()).stream();
+    (void)hipStreamIsCapturing(cur, &cap);
+  }
+  const bool timed = timing_ && cap == hipStreamCaptureStatusNone;
+  wait_bucket(b, cur, timed);
+  if (timed) b.timed_work = b.work;
+  if (!b.wire.is_same(b.flat)) ops::mt_copy({b.wire}, {b.flat}, 1.0);
+  b.work.reset();
+  b.deferred = false;
+}
+
+std::vector<int64_t> Reducer::deferred_buckets() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<int64_t> r;
+  for (size_t k = 0; k < buckets_.size(); ++k)
+    if (buckets_[k].deferred) r.push_back(static_cast<int64_t>(k));
+  return r;
+}
+
+void Reducer::sync_bucket(int64_t k) {
+  std::lock_guard<std::mutex> g(mu_);
+  DK_CHECK(k >= 0 && k < static_cast<int64_t>(buckets_.size()), "Reducer::sync_bucket: bad bucket ", k);
+  sync_locked(buckets_[k]);
+}
+
+void Reducer::sync_all() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& b : buckets_) sync_locked(b);
 }
 
 Reducer::~Reducer() {
+  for (auto& b : buckets_) {
+    if (b.stall0) (void)hipEventDestroy(b.stall0);
+    if (b.stall1) (void)hipEventDestroy(b.stall1);
+  }
   release_registrations();
   if (used_ev_) (void)hipEventDestroy(used_ev_);
-  if (ev_bwd_end_) (void)hipEventDestroy(ev_bwd_end_);
-  if (ev_final_) (void)hipEventDestroy(ev_final_);
   for (size_t i = 0; i < grad_accs_.size() && i < hook_handles_.size(); ++i)
     grad_accs_[i]->del_post_hook(hook_handles_[i]);
 }
@@ -169,6 +223,10 @@ void Reducer::build_buckets(const std::vector<std::vector<int64_t>>& assignment)
   }
   for (size_t i = 0; i < params_.size(); ++i) DK_CHECK(seen[i], "Reducer: parameter ", i, " not in any bucket");
   release_registrations();
+  for (auto& b : buckets_) {
+    if (b.stall0) (void)hipEventDestroy(b.stall0);
+    if (b.stall1) (void)hipEventDestroy(b.stall1);
+  }
   buckets_ = std::move(out);
   next_bucket_ = 0;
   if (opts_.register_buckets && comm_)
@@ -208,6 +266,9 @@ void Reducer::set_expect_backward(bool v) {
 void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs, bool require_sync) {
   std::lock_guard<std::mutex> g(mu_);
   DK_CHECK(!finalize_queued_, "Reducer: forward called while a backward reduction is still in progress");
+  // a deferred bucket's buffer is still being reduced: order the compute
+  // stream (which accumulates the next gradients into it) behind it first
+  for (auto& b : buckets_) sync_locked(b);
   expect_hooks_ = require_sync;
   if (!require_sync) return;
   unused_list_.clear();
@@ -314,6 +375,7 @@ bool capturing(const at::Tensor& t) {
 }  // namespace
 
 void Reducer::launch(Bucket& b) {
+  sync_locked(b);  // (a deferred previous reduction must land before this pack)
   // Pack: one multi-tensor launch for every gradient not already in place.
   const bool compressed = !b.wire.is_same(b.flat);
   std::vector<at::Tensor> src, dst;
@@ -399,10 +461,27 @@ void Reducer::finalize() {
   if (timing_) {
     cur = c10::hip::getCurrentHIPStream(params_[0].device().index()).stream();
     (void)hipStreamIsCapturing(cur, &cap);
-    if (cap == hipStreamCaptureStatusNone) (void)hipEventRecord(ev_bwd_end_, cur);
   }
+  // defer_grad_wait: grads are pointed at their bucket views now (host
+  // only), the compute-stream waits are left to the consumer (sync_bucket).
+  // Not in an iteration that rebuilds the buckets (the buffers are replaced).
+  const bool defer = opts_.defer_grad_wait && opts_.gradient_as_bucket_view && global_used.empty() && !check_ &&
+                     !(record_order_ && opts_.rebuild_buckets);
+  for (auto& b : buckets_) b.stall_recorded = false;
   for (auto& b : buckets_) {
-    b.work->wait();
+    if (defer) {
+      // every .grad becomes its bucket view (host-only pointer swap, as the
+      // waiting path below does): the reduced values land there
+      for (size_t s = 0; s < b.params.size(); ++s) {
+        at::Tensor& grad = params_[b.params[s]].mutable_grad();
+        if (!grad.defined() || grad.data_ptr() != b.views[s].data_ptr()) grad = b.views[s];
+      }
+      b.deferred = true;
+      b.launched = false;
+      b.pending = static_cast<int>(b.params.size());
+      continue;
+    }
+    wait_bucket(b, cur, timing_ && cap == hipStreamCaptureStatusNone);
     // the collective may still be running (wait() only orders the compute
     // stream): keep the Work, bucket_stats() resolves its events when read
     if (timing_ && cap == hipStreamCaptureStatusNone) b.timed_work = b.work;
@@ -458,10 +537,6 @@ void Reducer::finalize() {
     b.work.reset();
     b.launched = false;
     b.pending = static_cast<int>(b.params.size());
-  }
-  if (timing_ && cap == hipStreamCaptureStatusNone) {
-    (void)hipEventRecord(ev_final_, cur);
-    ev_recorded_ = true;
   }
   std::fill(ready_.begin(), ready_.end(), 0);
   next_bucket_ = 0;
@@ -596,8 +671,10 @@ void Reducer::rebuild_from_ready_order() {
 
 void Reducer::wait_all() {
   std::lock_guard<std::mutex> g(mu_);
-  for (auto& b : buckets_)
+  for (auto& b : buckets_) {
+    sync_locked(b);
     if (b.work) b.work->synchronize();
+  }
 }
 
 std::vector<std::vector<int64_t>> Reducer::bucket_indices() const {

@@ -70,6 +70,15 @@ struct ReducerOptions {
   // (or a comm hook that returns before its result is in the buffer) shows up
   // as a mismatch, raised from finalize. Host-syncs once per bucket: debug only.
   bool check_streams = false;
+  // Optimizer overlap (gradient_as_bucket_view, no find_unused_parameters):
+  // finalize points every .grad at its bucket view but does NOT order the
+  // compute stream behind the bucket collectives; the consumer (the fused
+  // optimizers, optim/fused.py) calls sync_bucket(k) in launch order right
+  // before it updates bucket k's parameters, so the update of the early
+  // buckets runs while the last ones are still being reduced. Anything
+  // still deferred is synced before the next backward's first pack, by
+  // prepare_for_backward and by wait_gradients().
+  bool defer_grad_wait = false;
 };
 
 struct BucketStats {
@@ -108,10 +117,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<std::vector<int64_t>> bucket_indices() const;
   std::vector<int64_t> bucket_sizes_bytes() const;
   std::vector<BucketStats> bucket_stats();
-  // DCP_COMM_TIMING=1 on a GPU: device time between the end of the backward
-  // compute and the point where every bucket's reduction has landed in the
-  // last finished iteration = communication NOT hidden behind backward.
-  // -1 when unavailable (timing off, CPU, still in flight).
+  // DCP_COMM_TIMING=1 on a GPU: communication NOT hidden behind compute in
+  // the last finished iteration = the device time the compute stream stood
+  // at its waits on the bucket collectives (summed over buckets; with
+  // defer_grad_wait the waits sit between the optimizer's per-bucket
+  // updates). -1 when unavailable (timing off, CPU, still in flight).
   double exposed_comm_ms();
   std::vector<int64_t> ready_order() const { return ready_order_; }
   int64_t num_iterations() const { return iterations_; }
@@ -121,6 +131,12 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<at::Tensor> bucket_buffers() const;
   // Wait for in-flight reductions (used by no_sync exit / destructor paths).
   void wait_all();
+  // defer_grad_wait: bucket indices (launch order) whose collective the
+  // compute stream has not been ordered behind yet; sync_bucket orders it
+  // (and unpacks a compressed wire buffer); sync_all syncs every one.
+  std::vector<int64_t> deferred_buckets();
+  void sync_bucket(int64_t k);
+  void sync_all();
 
  private:
   struct Bucket {
@@ -137,6 +153,9 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     BucketStats stats;
     at::Tensor check_sum;  // check_streams: fp64 [1] checksum of the packed buffer (all-reduced)
     WorkPtr check_work;
+    bool deferred = false;  // defer_grad_wait: work kept, compute stream not yet ordered behind it
+    hipEvent_t stall0 = nullptr, stall1 = nullptr;  // timing: compute-stream wait on this bucket
+    bool stall_recorded = false;
   };
 
   void build_buckets(const std::vector<std::vector<int64_t>>& assignment);
@@ -150,6 +169,9 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void launch_used_map_reduce();
   std::vector<char> collect_global_used();
   void reset_iteration_state();
+  // compute stream waits on b's collective (timed when DCP_COMM_TIMING)
+  void wait_bucket(Bucket& b, hipStream_t cur, bool timed);
+  void sync_locked(Bucket& b);
 
   std::vector<at::Tensor> params_;
   std::shared_ptr<Communicator> comm_;
@@ -181,8 +203,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   double backward_t0_ms_ = 0;
   bool timing_ = false;
   bool check_ = false;  // ReducerOptions::check_streams / DCP_DEBUG_STREAMS=1
-  hipEvent_t ev_bwd_end_ = nullptr, ev_final_ = nullptr;
-  bool ev_recorded_ = false;
+  bool ev_recorded_ = false;  // timing: some bucket's stall events were recorded
   // find_unused_parameters: per-parameter used flags. Host staging (pinned on
   // GPU) -> device -> async MAX all-reduce issued at the first hook ->
   // async copy back on the comm stream; finalize waits only on that small

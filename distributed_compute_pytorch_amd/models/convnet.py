@@ -14,9 +14,11 @@ used for ``dropout2`` so behaviour is the same without the 2.x warning.
 ``fused=True`` (GPU) runs the MI355X path with identical parameters and
 state_dict: conv1 → ReLU → conv2 → ReLU → max-pool → Dropout2d → flatten as
 ONE fp32-MFMA kernel forward and one (+ reduce) backward
-(``ops/convnet.py``, ``csrc/kernels/convnet.hip``), fc1 → [BatchNorm1d +
-ReLU] on the fused BN kernels, Philox dropout, and a wave-per-row
-log-softmax.
+(``ops/convnet.py``, ``csrc/kernels/convnet.hip``), fc1 / fc2 on fp32-MFMA
+GEMMs (``csrc/kernels/fc32.hip``: K-split forward, data gradient, weight
+gradient with the bias gradient in the same launch), [BatchNorm1d + ReLU] on
+the fused BN kernels, Philox dropout, and a wave-per-row log-softmax
+(SURVEY §2f K1-K6, K8-K13, K16-K24).
 """
 from __future__ import annotations
 
@@ -55,9 +57,9 @@ class ConvNet(nn.Module):
         return F.log_softmax(x, dim=1)
 
     def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
-        from ..ops import convnet_features, fused_dropout, fused_log_softmax
+        from ..ops import convnet_features, fc32, fused_dropout, fused_log_softmax
 
         x = convnet_features(x, self.conv1, self.conv2, self.dropout1.p, self.training)
-        x = self.batchnorm(self.fc1(x))  # BN1d + ReLU
+        x = self.batchnorm(fc32(x, self.fc1))  # fp32-MFMA fc1, then BN1d + ReLU
         x = fused_dropout(x, self.dropout2.p, self.training)
-        return fused_log_softmax(self.fc2(x), 1)
+        return fused_log_softmax(fc32(x, self.fc2), 1)

@@ -6,9 +6,9 @@ from .metrics import EvalMetrics
 from .pool import FusedMaxPool2d, fused_max_pool2d, relu_max_pool2d_dropout
 from .dropout import FusedDropout, FusedDropout2d, dropout_add, fused_dropout, fused_feature_dropout
 from .softmax import fused_log_softmax
-from .convnet import convnet_features
+from .convnet import convnet_features, fc32
 
 __all__ = ["BatchNormAct1d", "BatchNormAct2d", "bn_act", "FusedLayerNorm", "fused_layer_norm", "fused_cross_entropy",
            "FusedDropout", "FusedDropout2d", "dropout_add", "fused_dropout", "fused_feature_dropout",
            "FusedMaxPool2d", "fused_max_pool2d", "relu_max_pool2d_dropout", "fused_log_softmax", "EvalMetrics",
-           "convnet_features"]
+           "convnet_features", "fc32"]

@@ -31,6 +31,35 @@ class _FeaturesFn(torch.autograd.Function):
         return None, dw1.view(32, 1, 3, 3), db1, dw2.view(64, 32, 3, 3), db2, None, None
 
 
+class _FC32Fn(torch.autograd.Function):
+    """y = x·Wᵀ + b in fp32 on the MFMA (csrc/kernels/fc32.hip): forward with
+    a K-split + deterministic reduce, backward = data gradient + weight
+    gradient with the bias gradient summed in the same launch. The reference
+    ConvNet's fc1 / fc2 (main.py:27-28, 39, 43)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return _C.fc32_fwd(x, w.detach(), None if b is None else b.detach())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        dx, dw, db = _C.fc32_bwd(g.contiguous(), x, w.detach(), bool(ctx.needs_input_grad[0]))
+        return (dx if ctx.needs_input_grad[0] else None), dw, (db if ctx.has_b else None)
+
+
+def fc32(x: torch.Tensor, linear) -> torch.Tensor:
+    """``linear(x)`` for an fp32 ``nn.Linear`` on the fp32 MFMA kernels (2-D
+    contiguous fp32 device input), else the module itself."""
+    w, b = linear.weight, linear.bias
+    if (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and w.dtype == torch.float32 and w.is_contiguous()
+            and (b is None or (b.dtype == torch.float32 and b.is_contiguous()))):
+        return _FC32Fn.apply(x.contiguous(), w, b)
+    return linear(x)
+
+
 def _fits(x, conv1, conv2) -> bool:
     ps = (conv1.weight, conv1.bias, conv2.weight, conv2.bias)
     return (_C.convnet_supported(x) and not x.requires_grad and all(

@@ -56,6 +56,52 @@ def fresh_bf16_shadow(p: torch.Tensor) -> Optional[torch.Tensor]:
     return None
 
 
+def _overlap_chunks(opt):
+    """Optimizer overlap (``DistributedDataParallel(overlap_optimizer=True)``):
+    when a DDP left bucket reductions deferred, the step runs in chunks —
+    first every parameter outside those buckets, then bucket by bucket in
+    launch order, each right after the compute stream is ordered behind that
+    bucket's collective (``sync``) — so the updates of the early buckets run
+    while the last ones are still being reduced. None when nothing is deferred."""
+    from ..parallel import ddp as _ddp
+
+    chunks, covered = [], set()
+    for d in list(_ddp._OVERLAP):
+        plan = None
+        for k in d.reducer.deferred_buckets():
+            if plan is None:
+                plan = d.reducer.bucket_indices()
+            ids = {id(d._params[i]) for i in plan[k]}
+            chunks.append((lambda d=d, k=k: d.reducer.sync_bucket(k), ids))
+            covered |= ids
+    if not chunks:
+        return None
+    mine = {id(p) for g in opt.param_groups for p in g["params"]}
+    return [(None, mine - covered)] + [(sync, ids & mine) for sync, ids in chunks]
+
+
+def _run_chunks(opt, impl, grad_scale) -> list:
+    """``impl(ids, grad_scale)`` over the overlap chunks (one call with ids =
+    None when nothing is deferred); the list of its results."""
+    out = []
+    for sync, ids in _overlap_chunks(opt) or [(None, None)]:
+        if sync is not None:
+            sync()
+        if ids is None or ids:
+            out.append(impl(ids, grad_scale))
+    return out
+
+
+def sync_deferred_gradients() -> None:
+    """Order the current stream behind every deferred bucket reduction of every
+    overlap-mode DDP (anything that reads .grad outside the fused optimizers'
+    step — e.g. gradient clipping — must call this first)."""
+    from ..parallel import ddp as _ddp
+
+    for d in list(_ddp._OVERLAP):
+        d.reducer.sync_all()
+
+
 def _grads_ok(p: torch.Tensor) -> bool:
     if p.grad is None:
         return False
@@ -94,12 +140,18 @@ class SGD(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        _run_chunks(self, self._step, grad_scale)
+        _PARAM_EPOCH[0] += 1
+        return loss
+
+    def _step(self, ids, grad_scale):
+        """Update the parameters whose id is in ``ids`` (None: all)."""
         for group in self.param_groups:
             mom = group["momentum"]
             buckets = defaultdict(lambda: ([], [], []))
             capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
             for p in group["params"]:
-                if not _grads_ok(p):
+                if (ids is not None and id(p) not in ids) or not _grads_ok(p):
                     continue
                 st = self.state[p]
                 first = False
@@ -124,8 +176,6 @@ class SGD(Optimizer):
             for (dev, dt, first), (P, G, B) in buckets.items():
                 _C.fused_sgd(P, G, B, group["lr"], mom, group["dampening"], group["weight_decay"],
                              group["nesterov"], group["maximize"], first, grad_scale)
-        _PARAM_EPOCH[0] += 1
-        return loss
 
 
 class Adam(Optimizer):
@@ -162,7 +212,18 @@ class Adam(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        shadowed = [p for sh in _run_chunks(self, self._step, grad_scale) for p in sh]
+        _PARAM_EPOCH[0] += 1
+        for p in shadowed:  # rewritten by the kernel: valid for the new epoch
+            e = _BF16_SHADOWS[p]
+            e[1], e[2] = _PARAM_EPOCH[0], p._version
+        return loss
+
+    def _step(self, ids, grad_scale):
+        """Update the parameters whose id is in ``ids`` (None: all); returns the
+        parameters whose bf16 shadow the kernel rewrote."""
         capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        shadowed = []
         for group in self.param_groups:
             b1, b2 = group["betas"]
             ams = group["amsgrad"]
@@ -173,9 +234,8 @@ class Adam(Optimizer):
                                    "optimizer with capturable=True (or set group['capturable'] = True before the "
                                    "eager warmup steps).")
             buckets = defaultdict(lambda: ([], [], [], [], [], [], []))
-            shadowed = []
             for p in group["params"]:
-                if not _grads_ok(p):
+                if (ids is not None and id(p) not in ids) or not _grads_ok(p):
                     continue
                 st = self.state[p]
                 dev_step = cap_mode and p.is_cuda
@@ -217,11 +277,7 @@ class Adam(Optimizer):
                 _C.fused_adam(P, G, M, V, VM, group["lr"], b1, b2, group["eps"], group["weight_decay"],
                               step if step is not None else 0.0, ams, group["decoupled_weight_decay"],
                               group["maximize"], grad_scale, S, ST)
-        _PARAM_EPOCH[0] += 1
-        for p in shadowed:  # rewritten by the kernel: valid for the new epoch
-            e = _BF16_SHADOWS[p]
-            e[1], e[2] = _PARAM_EPOCH[0], p._version
-        return loss
+        return shadowed
 
 
 class AdamW(Adam):
@@ -247,10 +303,15 @@ class Adadelta(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        _run_chunks(self, self._step, grad_scale)
+        _PARAM_EPOCH[0] += 1
+        return loss
+
+    def _step(self, ids, grad_scale):
         for group in self.param_groups:
             buckets = defaultdict(lambda: ([], [], [], []))
             for p in group["params"]:
-                if not _grads_ok(p):
+                if (ids is not None and id(p) not in ids) or not _grads_ok(p):
                     continue
                 st = self.state[p]
                 if len(st) == 0:
@@ -266,14 +327,13 @@ class Adadelta(Optimizer):
             for _, (P, G, S, A) in buckets.items():
                 _C.fused_adadelta(P, G, S, A, group["lr"], group["rho"], group["eps"], group["weight_decay"],
                                   group["maximize"], grad_scale)
-        _PARAM_EPOCH[0] += 1
-        return loss
 
 
 @torch.no_grad()
 def clip_grad_norm_(parameters: Iterable[torch.Tensor], max_norm: float, eps: float = 1e-6) -> torch.Tensor:
     """Total-L2-norm gradient clipping without a host sync: one sum-of-squares
     launch + one scale launch (the scale factor stays on device)."""
+    sync_deferred_gradients()
     grads: List[torch.Tensor] = [p.grad for p in parameters if p.grad is not None]
     if not grads:
         return torch.tensor(0.0)

@@ -58,6 +58,13 @@ DEFAULT_TAIL_BUCKET_MB = 0.0
 XGMI_BUCKETS = {"bucket_cap_mb": 16.0, "first_bucket_mb": 1.0, "tail_bucket_mb": 2.0}
 
 
+# overlap-mode DDP instances (optim/fused.py syncs their deferred buckets
+# chunk by chunk inside the optimizer step)
+import weakref as _weakref
+
+_OVERLAP = _weakref.WeakSet()
+
+
 _DTYPE_IDS = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3, torch.int64: 4,
               torch.int32: 5, torch.uint8: 6, torch.int8: 7, torch.bool: 8, torch.complex64: 9}
 
@@ -97,7 +104,7 @@ class DistributedDataParallel(nn.Module):
                  gradient_as_bucket_view: bool = False, static_graph: bool = False,
                  first_bucket_mb: Optional[float] = None, comm_dtype: Optional[torch.dtype] = None,
                  rebuild_buckets: bool = True, init_sync: bool = True, tail_bucket_mb: Optional[float] = None,
-                 register_buckets: bool = False):
+                 register_buckets: bool = False, overlap_optimizer: bool = False):
         super().__init__()
         self.module = module
         self.process_group = process_group if process_group is not None else dist.get_default_group()
@@ -158,9 +165,21 @@ class DistributedDataParallel(nn.Module):
         # (ncclCommRegister) once per bucket plan — zero-copy user-buffer paths
         # where RCCL has them; a no-op on one rank and on gloo
         opts.register_buckets = bool(register_buckets)
+        # overlap_optimizer: the backward leaves the last bucket reductions in
+        # flight; this package's fused optimizers (optim/fused.py) order the
+        # compute stream behind each bucket right before updating its
+        # parameters, so the update of the early buckets overlaps the
+        # reduction of the last ones (the ready-last embeddings of BERT /
+        # GPT-2 are single 90-150 MB buckets). Needs gradient_as_bucket_view
+        # (the gradients ARE the bucket buffers); anything else reading .grad
+        # between backward and step must call wait_gradients() first.
+        self.overlap_optimizer = bool(overlap_optimizer) and gradient_as_bucket_view and not find_unused_parameters
+        opts.defer_grad_wait = self.overlap_optimizer
         self._comm = pg.comm_for(params[0])
         self.reducer = _C.Reducer(params, plan, self._comm, opts)
         self._comm_hook = None
+        if self.overlap_optimizer:
+            _OVERLAP.add(self)
 
     @staticmethod
     def _key(p):
@@ -218,6 +237,12 @@ class DistributedDataParallel(nn.Module):
         # a compression hook declares its wire precision (``hook.wire_dtype``):
         # the debug stream-ordering check then tolerates that rounding
         self.reducer.set_comm_hook(_call, getattr(hook, "wire_dtype", None))
+
+    def wait_gradients(self) -> None:
+        """overlap_optimizer: order the current stream behind every bucket
+        reduction still in flight (before reading .grad outside the fused
+        optimizers' step)."""
+        self.reducer.sync_all()
 
     # ------------------------------------------------------------------
     def bucket_sizes(self) -> List[int]:

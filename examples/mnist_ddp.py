@@ -79,7 +79,10 @@ def proc(rank, world_size, opt, use_cuda):
     test_sampler = DistributedSampler(test_ds, num_replicas=world_size, rank=rank, shuffle=False)
     train_loader = DataLoader(train_ds, batch_size=opt.batch_size, sampler=train_sampler, pin_memory=use_cuda)
     test_loader = DataLoader(test_ds, batch_size=opt.batch_size, sampler=test_sampler, pin_memory=use_cuda)
-    model = dcp.parallel.DistributedDataParallel(ConvNet().to(device),
+    # fused=True on a GPU: the fp32-MFMA feature extractor (convnet.hip), fused
+    # BN1d + ReLU, Philox dropout and log-softmax kernels; identical parameters
+    # and state_dict keys (models/convnet.py), so checkpoints load either way
+    model = dcp.parallel.DistributedDataParallel(ConvNet(fused=use_cuda).to(device),
                                                  device_ids=[rank] if use_cuda else None)
     optimizer = dcp.optim.Adadelta(model.parameters(), lr=opt.lr)
     scheduler = dcp.optim.StepLR(optimizer, step_size=1, gamma=opt.gamma)

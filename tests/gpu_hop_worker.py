@@ -96,7 +96,8 @@ def main():
     for name, kw in (("fp32", {}), ("bf16_wire", {"comm_dtype": torch.bfloat16}),
                      ("grad_view", {"gradient_as_bucket_view": True}),
                      ("registered", {"gradient_as_bucket_view": True, "register_buckets": True}),
-                     ("bf16_hook", {"hook": dcp.parallel.comm_hooks.bf16_compress_hook})):
+                     ("bf16_hook", {"hook": dcp.parallel.comm_hooks.bf16_compress_hook}),
+                     ("overlap", {"gradient_as_bucket_view": True, "overlap_optimizer": True})):
         hook = kw.pop("hook", None)
         local = ConvNet().to(dev)
         local.load_state_dict(base.state_dict())

@@ -218,3 +218,27 @@ def test_convnet_features_dropout(cuda):
     _, ref = _ref_grads(x, m, g, names, scale)
     for n, a, b in zip(names, ours, ref):
         assert float((a - b).norm() / b.norm()) < 1e-5, n
+
+
+@pytest.mark.parametrize("M,K,N", [(128, 9216, 128), (128, 128, 10), (37, 300, 20), (256, 9216, 128), (5, 16, 3)])
+def test_fc32_matches_fp64(cuda, M, K, N):
+    """The head's fp32-MFMA Linear (csrc/kernels/fc32.hip): forward (K-split +
+    reduce for fc1's K = 9216), data gradient, weight gradient and bias
+    gradient vs an fp64 reference; exact fp32 products (no xf32), so only
+    summation order differs."""
+    from distributed_compute_pytorch_amd.ops.convnet import fc32
+
+    g = torch.Generator().manual_seed(M + K + N)
+    lin = torch.nn.Linear(K, N).to(cuda)
+    x = torch.randn(M, K, generator=g).to(cuda).requires_grad_(True)
+    gy = torch.randn(M, N, generator=g).to(cuda)
+    y = fc32(x, lin)
+    y.backward(gy)
+    xd, wd, bd = x.detach().double(), lin.weight.detach().double(), lin.bias.detach().double()
+    yr = xd @ wd.t() + bd
+    torch.testing.assert_close(y.double(), yr, rtol=2e-5, atol=2e-5 * K ** 0.5)
+    torch.testing.assert_close(x.grad.double(), gy.double() @ wd, rtol=2e-5, atol=2e-5 * N ** 0.5)
+    torch.testing.assert_close(lin.weight.grad.double(), gy.double().t() @ xd, rtol=2e-5, atol=2e-5 * M ** 0.5)
+    torch.testing.assert_close(lin.bias.grad.double(), gy.double().sum(0), rtol=2e-5, atol=2e-5 * M ** 0.5)
+    # deterministic: the K-split partials are summed in a fixed order
+    assert torch.equal(fc32(x.detach(), lin), y.detach())
