@@ -342,40 +342,94 @@ std::vector<at::Tensor> conv_weight_bf16(const at::Tensor& w) {
 // flipped transpose: dgrad operand), and a device descriptor table. Pointers
 // are baked in: rebuild when a weight's storage changes.
 std::tuple<at::Tensor, int64_t, std::vector<at::Tensor>, std::vector<at::Tensor>> weight_prep_plan(
-    const std::vector<at::Tensor>& ws) {
+    const std::vector<at::Tensor>& ws, const std::vector<int64_t>& groups, const std::vector<int64_t>& pad_rows) {
   DK_CHECK(!ws.empty(), "weight_prep_plan: no weights");
   c10::hip::HIPGuard guard(ws[0].device().index());
+  // groups: consecutive weights packed along their rows into one operand
+  // (BERT's query / key / value); empty = one group per weight
+  std::vector<int64_t> gs = groups.empty() ? std::vector<int64_t>(ws.size(), 1) : groups;
+  int64_t ng = 0;
+  for (int64_t g : gs) {
+    DK_CHECK(g >= 1, "weight_prep_plan: empty group");
+    ng += g;
+  }
+  DK_CHECK(ng == static_cast<int64_t>(ws.size()), "weight_prep_plan: groups must cover every weight once");
+  // pad_rows[g] > 0: group g's operands hold that many rows, the rows past the
+  // weights' own zero (a vocabulary padded to a GEMM-friendly multiple)
+  DK_CHECK(pad_rows.empty() || pad_rows.size() == gs.size(), "weight_prep_plan: one pad_rows entry per group");
   int64_t E = 0;
+  {
+    size_t wi = 0;
+    for (size_t gi = 0; gi < gs.size(); ++gi) {
+      int64_t Rg = 0;
+      for (int64_t j = 0; j < gs[gi]; ++j) Rg += ws[wi + j].size(0);
+      const int64_t pr = pad_rows.empty() ? 0 : pad_rows[gi];
+      DK_CHECK(pr == 0 || (pr >= Rg && ws[wi].dim() == 2), "weight_prep_plan: pad_rows below the group's rows, "
+               "or on a conv weight");
+      if (pr > Rg) E += (pr - Rg) * ws[wi].size(1);
+      wi += static_cast<size_t>(gs[gi]);
+    }
+  }
+  const bool padded = E > 0;
   for (auto& w : ws) {
-    DK_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.device() == ws[0].device(),
-              "weight_prep_plan: fp32 4-D device conv weights on one device required");
-    DK_CHECK(w.permute({0, 2, 3, 1}).is_contiguous(),
-              "weight_prep_plan: weights must be channels_last ([Cout][kh][kw][Cin] memory)");
+    DK_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && (w.dim() == 4 || w.dim() == 2) &&
+                 w.device() == ws[0].device(),
+             "weight_prep_plan: fp32 2-D (Linear) or 4-D (conv) device weights on one device required");
+    DK_CHECK(w.dim() == 2 ? w.is_contiguous() : w.permute({0, 2, 3, 1}).is_contiguous(),
+             "weight_prep_plan: Linear weights contiguous, conv weights channels_last ([Cout][kh][kw][Cin] memory)");
     E += w.numel();
   }
-  at::Tensor flat = at::empty({2 * E}, ws[0].options().dtype(at::kBFloat16));
+  // padding rows are zeroed once here and never written by the launch
+  at::Tensor flat = padded ? at::zeros({2 * E}, ws[0].options().dtype(at::kBFloat16))
+                           : at::empty({2 * E}, ws[0].options().dtype(at::kBFloat16));
   std::vector<at::Tensor> wbs, wts;
   std::vector<kern::WPrepDesc> descs;
   int64_t off = 0, tiles = 0;
-  for (auto& w : ws) {
-    const int64_t R = w.size(0), Ci = w.size(1), kh = w.size(2), kw = w.size(3), n = w.numel();
-    at::Tensor wb = flat.narrow(0, off, n).view({R, kh, kw, Ci});
-    at::Tensor wt = flat.narrow(0, E + off, n).view({Ci, kh, kw, R});
-    kern::WPrepDesc d{};
-    d.w = w.data_ptr<float>();
-    d.wb = static_cast<uint16_t*>(wb.data_ptr());
-    d.wt = static_cast<uint16_t*>(wt.data_ptr());
-    d.R = static_cast<int>(R);
-    d.Cc = static_cast<int>(Ci);
-    d.T = static_cast<int>(kh * kw);
-    d.tiles_c = static_cast<int>((Ci + 31) / 32);
-    d.tiles_r = static_cast<int>((R + 31) / 32);
-    d.tile0 = tiles;
-    tiles += static_cast<int64_t>(d.T) * d.tiles_c * d.tiles_r;
-    descs.push_back(d);
-    wbs.push_back(wb);
-    wts.push_back(wt);
+  size_t wi = 0;
+  for (size_t gi = 0; gi < gs.size(); ++gi) {
+    const int64_t g = gs[gi];
+    int64_t Rg = 0, n = 0;
+    const int64_t Cg = ws[wi].size(1);
+    for (int64_t j = 0; j < g; ++j) {
+      const at::Tensor& w = ws[wi + j];
+      DK_CHECK(g == 1 || (w.dim() == 2 && w.size(1) == Cg), "weight_prep_plan: a packed group holds 2-D weights "
+               "with equal input features");
+      Rg += w.size(0);
+      n += w.numel();
+    }
+    const int64_t Rp = pad_rows.empty() || pad_rows[gi] == 0 ? Rg : pad_rows[gi];
+    n += (Rp - Rg) * Cg;
+    int64_t r_off = 0;
+    for (int64_t j = 0; j < g; ++j) {
+      const at::Tensor& w = ws[wi + j];
+      const int64_t R = w.size(0), Ci = w.size(1);
+      const int64_t kh = w.dim() == 4 ? w.size(2) : 1, kw = w.dim() == 4 ? w.size(3) : 1;
+      kern::WPrepDesc d{};
+      d.w = w.data_ptr<float>();
+      d.wb = static_cast<uint16_t*>(flat.data_ptr()) + off + r_off * Ci;
+      d.wt = static_cast<uint16_t*>(flat.data_ptr()) + E + off + r_off;
+      d.R = static_cast<int>(R);
+      d.Cc = static_cast<int>(Ci);
+      d.T = static_cast<int>(kh * kw);
+      d.pad = g > 1 || Rp > Rg ? static_cast<int>(Rp) : 0;
+      d.tiles_c = static_cast<int>((Ci + 31) / 32);
+      d.tiles_r = static_cast<int>((R + 31) / 32);
+      d.tile0 = tiles;
+      tiles += static_cast<int64_t>(d.T) * d.tiles_c * d.tiles_r;
+      descs.push_back(d);
+      r_off += R;
+    }
+    const at::Tensor& w0 = ws[wi];
+    if (w0.dim() == 4) {
+      const int64_t R = w0.size(0), Ci = w0.size(1), kh = w0.size(2), kw = w0.size(3);
+      wbs.push_back(flat.narrow(0, off, n).view({R, kh, kw, Ci}));
+      wts.push_back(flat.narrow(0, E + off, n).view({Ci, kh, kw, R}));
+    } else {
+      wbs.push_back(flat.narrow(0, off, n).view({Rp, Cg}));
+      wts.push_back(flat.narrow(0, E + off, n).view({Cg, Rp}));
+    }
     off += n;
+    wi += static_cast<size_t>(g);
   }
   const int64_t bytes = static_cast<int64_t>(descs.size() * sizeof(kern::WPrepDesc));
   at::Tensor host = at::empty({bytes}, at::TensorOptions().dtype(at::kByte));
@@ -410,7 +464,7 @@ at::Tensor conv1x1_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
 // dw[Cout, Cin] (fp32) = Σ_m gy[m, :]^T ⊗ f(x)[m, :]
 at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::optional<at::Tensor>& scale,
                          const c10::optional<at::Tensor>& shift, bool relu,
-                         const c10::optional<at::Tensor>& accumulate_into) {
+                         const c10::optional<at::Tensor>& accumulate_into, int64_t out_rows) {
   check_gemm_act(gy, "conv1x1_wgrad");
   check_gemm_act(x, "conv1x1_wgrad");
   c10::hip::HIPGuard guard(gy.device().index());
@@ -418,6 +472,10 @@ at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::o
   const int64_t M = gy.numel() / N1;
   DK_CHECK(x.numel() / N2 == M, "conv1x1_wgrad: row mismatch");
   DK_CHECK(N1 % 64 == 0 && N2 % 64 == 0, "conv1x1_wgrad: channels must be multiples of 64");
+  // out_rows: dW keeps only its first out_rows rows (gy's columns past them are
+  // padding, e.g. a vocabulary padded to a multiple of 64)
+  DK_CHECK(out_rows < 0 || (out_rows <= N1 && (out_rows * N2) % 4 == 0), "conv1x1_wgrad: out_rows");
+  const int64_t R1 = out_rows < 0 ? N1 : out_rows;
   const float* sc = vec_or_null(scale, N2, "conv1x1_wgrad");
   const float* sf = vec_or_null(shift, N2, "conv1x1_wgrad");
   // accumulate_into: an existing fp32 [N1, N2] gradient that receives += dW in
@@ -425,13 +483,14 @@ at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::o
   const bool acc = accumulate_into.has_value() && accumulate_into->defined();
   if (acc)
     DK_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
-                  accumulate_into->numel() == N1 * N2 && accumulate_into->device() == gy.device(),
+                  accumulate_into->numel() == R1 * N2 && accumulate_into->device() == gy.device(),
               "conv1x1_wgrad: accumulate_into must be a contiguous fp32 [N1, N2] tensor on the same device");
-  at::Tensor dw = acc ? *accumulate_into : at::empty({N1, N2}, gy.options().dtype(at::kFloat));
+  at::Tensor dw = acc ? *accumulate_into : at::empty({R1, N2}, gy.options().dtype(at::kFloat));
   at::Tensor ws = at::empty({kern::gemm_wgrad_workspace(M, static_cast<int>(N1), static_cast<int>(N2))},
                             gy.options().dtype(at::kFloat));
   kern::gemm_wgrad_bf16(gy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), M, static_cast<int>(N1),
-                        static_cast<int>(N2), sc, sf, relu, ws.data_ptr<float>(), stream_of(gy), acc);
+                        static_cast<int>(N2), sc, sf, relu, ws.data_ptr<float>(), stream_of(gy), acc,
+                        static_cast<int>(out_rows));
   return dw;
 }
 
@@ -1155,34 +1214,51 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
 
 // ------------------------------------------------------- cross-entropy ---
 // logits [rows, V] (row stride may exceed V), target [rows] int64.
+// n_valid > 0: only the first n_valid columns are the vocabulary (the rest pad
+// the GEMM's N to a multiple of 64 and are ignored).
 std::vector<at::Tensor> cross_entropy_fwd(const at::Tensor& logits, const at::Tensor& target, int64_t ignore_index,
-                                          double label_smoothing) {
+                                          double label_smoothing, int64_t n_valid) {
   DK_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "cross_entropy_fwd: [rows, V] row-major");
   DK_CHECK(target.scalar_type() == at::kLong, "cross_entropy_fwd: int64 targets");
+  DK_CHECK(n_valid <= logits.size(1), "cross_entropy_fwd: n_valid exceeds the columns");
   c10::hip::HIPGuard guard(logits.device().index());
   const int64_t rows = logits.size(0);
+  const int64_t V = n_valid > 0 ? n_valid : logits.size(1);
   at::Tensor tg = target.contiguous();
   auto fopt = logits.options().dtype(at::kFloat);
   at::Tensor loss = at::empty({rows}, fopt), lse = at::empty({rows}, fopt);
   kern::xent_forward(ln_dtype(logits), logits.data_ptr(), logits.stride(0), tg.data_ptr<int64_t>(), rows,
-                     static_cast<int>(logits.size(1)), ignore_index, static_cast<float>(label_smoothing),
-                     loss.data_ptr<float>(), lse.data_ptr<float>(), stream_of(logits));
+                     static_cast<int>(V), ignore_index, static_cast<float>(label_smoothing), loss.data_ptr<float>(),
+                     lse.data_ptr<float>(), stream_of(logits));
   return {loss, lse};
 }
 
 // dloss: [rows] fp32 or a 1-element fp32 tensor broadcast to every row.
+// inplace: the gradient overwrites logits (which must then be contiguous) and
+// columns n_valid.. are zeroed; else a fresh [rows, n_valid] tensor.
 at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& target, const at::Tensor& lse,
-                             const at::Tensor& dloss, int64_t ignore_index, double label_smoothing) {
+                             const at::Tensor& dloss, int64_t ignore_index, double label_smoothing, int64_t n_valid,
+                             bool inplace) {
   c10::hip::HIPGuard guard(logits.device().index());
   const int64_t rows = logits.size(0);
+  const int64_t V = n_valid > 0 ? n_valid : logits.size(1);
+  DK_CHECK(V <= logits.size(1), "cross_entropy_bwd: n_valid exceeds the columns");
   at::Tensor tg = target.contiguous();
   at::Tensor dl = dloss.to(at::kFloat).contiguous();
   const int stride = dl.numel() == 1 ? 0 : 1;
   DK_CHECK(stride == 0 || dl.numel() == rows, "cross_entropy_bwd: dloss must be [rows] or scalar");
-  at::Tensor d = at::empty({rows, logits.size(1)}, logits.options());
+  at::Tensor d;
+  int Vpad = static_cast<int>(V);
+  if (inplace) {
+    DK_CHECK(logits.is_contiguous(), "cross_entropy_bwd: in place needs contiguous logits");
+    d = logits;
+    Vpad = static_cast<int>(logits.size(1));
+  } else {
+    d = at::empty({rows, V}, logits.options());
+  }
   kern::xent_backward(ln_dtype(logits), logits.data_ptr(), logits.stride(0), tg.data_ptr<int64_t>(),
-                      lse.data_ptr<float>(), dl.data_ptr<float>(), stride, rows, static_cast<int>(logits.size(1)),
-                      ignore_index, static_cast<float>(label_smoothing), d.data_ptr(), d.stride(0), stream_of(logits));
+                      lse.data_ptr<float>(), dl.data_ptr<float>(), stride, rows, static_cast<int>(V), ignore_index,
+                      static_cast<float>(label_smoothing), d.data_ptr(), d.stride(0), stream_of(logits), Vpad);
   return d;
 }
 
@@ -1405,10 +1481,13 @@ void bind(pybind11::module& m) {
         pybind11::arg("bias"), pybind11::arg("mean"), pybind11::arg("rstd"),
         pybind11::arg("accumulate_into") = pybind11::none(), pybind11::arg("grad_residual") = pybind11::none(),
         pybind11::arg("dy2") = pybind11::none());
-  m.def("cross_entropy_fwd", &cross_entropy_fwd);
+  m.def("cross_entropy_fwd", &cross_entropy_fwd, pybind11::arg("logits"), pybind11::arg("target"),
+        pybind11::arg("ignore_index"), pybind11::arg("label_smoothing"), pybind11::arg("n_valid") = -1);
   m.def("log_softmax_fwd", &log_softmax_fwd, pybind11::arg("x"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("log_softmax_bwd", &log_softmax_bwd);
-  m.def("cross_entropy_bwd", &cross_entropy_bwd);
+  m.def("cross_entropy_bwd", &cross_entropy_bwd, pybind11::arg("logits"), pybind11::arg("target"),
+        pybind11::arg("lse"), pybind11::arg("dloss"), pybind11::arg("ignore_index"), pybind11::arg("label_smoothing"),
+        pybind11::arg("n_valid") = -1, pybind11::arg("inplace") = false);
   m.def("bn_act_fwd", &bn_act_fwd, "fused NHWC BatchNorm(+residual)(+ReLU) forward", pybind11::arg("x"),
         pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"), pybind11::arg("running_var"),
         pybind11::arg("residual"), pybind11::arg("training"), pybind11::arg("momentum"), pybind11::arg("eps"),
@@ -1463,11 +1542,15 @@ void bind(pybind11::module& m) {
         pybind11::arg("pad"));
   m.def("weight_bf16_t", &weight_bf16_t, "fp32 weight -> (bf16 [R,C], bf16 transposed [C,R]) in one launch");
   m.def("conv_weight_bf16", &conv_weight_bf16, "kxk weight -> (bf16 fwd [Co][kh][kw][Ci], bf16 flipped [Ci][kh][kw][Co])");
-  m.def("weight_prep_plan", &weight_prep_plan, "conv weights -> (device table, tiles, bf16 fwd views, bf16 dgrad views)");
+  m.def("weight_prep_plan", &weight_prep_plan,
+        "conv / Linear weights -> (device table, tiles, bf16 fwd views, bf16 dgrad views), one view pair per group "
+        "(a group of Linear weights is packed along its rows)",
+        py::arg("weights"), py::arg("groups") = std::vector<int64_t>{}, py::arg("pad_rows") = std::vector<int64_t>{});
   m.def("weight_prep_run", &weight_prep_run, py::arg("table"), py::arg("tiles"));
   m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("gy"), pybind11::arg("x"),
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
-        pybind11::arg("relu") = false, pybind11::arg("accumulate_into") = pybind11::none());
+        pybind11::arg("relu") = false, pybind11::arg("accumulate_into") = pybind11::none(),
+        pybind11::arg("out_rows") = -1);
   m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward", pybind11::arg("gy"),
         pybind11::arg("gy2"), pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
         pybind11::arg("mean"), pybind11::arg("invstd"), pybind11::arg("y"), pybind11::arg("act"),

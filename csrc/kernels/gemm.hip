@@ -1220,8 +1220,10 @@ __global__ void __launch_bounds__(kT, 2) gemm_wgrad_kernel(const uint16_t* __res
 // per-thread loop over all S slabs: P[y][v] = Σ_{z∈[16y,16y+16)} ws[z][v],
 // then D[v] = Σ_y P[y][v]. Deterministic (fixed order).
 constexpr int kSlabGroup = 16;
+// n4: float4s reduced (a prefix of each slab: the wgrad's first output rows),
+// ld4: slab stride in float4s (also the stride of the partial slabs written).
 __global__ void __launch_bounds__(kT) slab_partial_kernel(const float4* __restrict__ ws, float4* __restrict__ out,
-                                                          int64_t n4, int S, int acc) {
+                                                          int64_t n4, int64_t ld4, int S, int acc) {
   const int64_t v = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   if (v >= n4) return;
   const int z0 = blockIdx.y * kSlabGroup;
@@ -1229,7 +1231,7 @@ __global__ void __launch_bounds__(kT) slab_partial_kernel(const float4* __restri
 #pragma unroll
   for (int k = 0; k < kSlabGroup; ++k) {  // clamped index, masked after the load: no branch per load
     const int z = min(z0 + k, S - 1);
-    a[k] = ws[static_cast<int64_t>(z) * n4 + v];
+    a[k] = ws[static_cast<int64_t>(z) * ld4 + v];
   }
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -1247,7 +1249,7 @@ __global__ void __launch_bounds__(kT) slab_partial_kernel(const float4* __restri
     s.z += o.z;
     s.w += o.w;
   }
-  out[static_cast<int64_t>(blockIdx.y) * n4 + v] = s;
+  out[static_cast<int64_t>(blockIdx.y) * ld4 + v] = s;
 }
 
 // fp32 [R][Cc] weight → bf16 w [R][Cc] and w^T [Cc][R] (RNE), one launch
@@ -1297,6 +1299,7 @@ __global__ void __launch_bounds__(kT) weight_prep_kernel(const WPrepDesc* __rest
   const int tap = local / per_tap, rem = local % per_tap;
   const int c0 = (rem % e.tiles_c) * 32, r0 = (rem / e.tiles_c) * 32;
   const int R = e.R, Cc = e.Cc, T = e.T;
+  const int ldt = e.pad > 0 ? e.pad : R;  // wt row length (> R: this weight is a row block of a packed one)
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
 #pragma unroll
   for (int k = 0; k < 32; k += 8) {
@@ -1312,7 +1315,7 @@ __global__ void __launch_bounds__(kT) weight_prep_kernel(const WPrepDesc* __rest
 #pragma unroll
   for (int k = 0; k < 32; k += 8) {
     const int c = c0 + ty + k, r = r0 + tx;
-    if (r < R && c < Cc) e.wt[(static_cast<int64_t>(c) * T + (T - 1 - tap)) * R + r] = tile[tx][ty + k];
+    if (r < R && c < Cc) e.wt[(static_cast<int64_t>(c) * T + (T - 1 - tap)) * ldt + r] = tile[tx][ty + k];
   }
 }
 
@@ -2405,12 +2408,12 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
 }
 
 namespace {
-void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc = false);
+void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc = false, int64_t out4 = -1);
 
 template <bool GATHER>
 void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
                   const float* shift, bool relu, float* ws, int taps, const ConvGeo& geo, hipStream_t s,
-                  bool acc = false) {
+                  bool acc = false, int rows_out = -1) {
   const int order = wgrad_order();
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
@@ -2456,14 +2459,15 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   else DK_GWG2(64, 64);
 #undef DK_GWG2
 #undef DK_GWG
-  slab_reduce(ws, D, static_cast<int64_t>(N1) * taps * N2 / 4, p.S, s, acc);
+  slab_reduce(ws, D, static_cast<int64_t>(N1) * taps * N2 / 4, p.S, s, acc,
+              rows_out >= 0 ? static_cast<int64_t>(rows_out) * taps * N2 / 4 : -1);
 }
 }  // namespace
 
 void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
-                     const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate) {
+                     const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate, int rows_out) {
   ConvGeo geo{};
-  wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s, accumulate);
+  wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s, accumulate, rows_out);
 }
 
 void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int W, int Cout, float* ws,
@@ -2532,17 +2536,20 @@ void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int 
 }
 
 namespace {
-void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc) {
+void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc, int64_t out4) {
+  // out4 ≥ 0: only the first out4 float4s of every slab reach D (D holds that many)
+  const int64_t n = out4 >= 0 ? out4 : n4;
   const WgradPlan p{0, 0, 0, S, 0};
-  const int gx = static_cast<int>((n4 + kT - 1) / kT);
+  const int gx = static_cast<int>((n + kT - 1) / kT);
   const int groups = (p.S + kSlabGroup - 1) / kSlabGroup;
   auto w4 = reinterpret_cast<const float4*>(ws);
   const int a = acc ? 1 : 0;
   if (groups == 1) {
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, w4, reinterpret_cast<float4*>(D), n4, p.S, a);
+    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, w4, reinterpret_cast<float4*>(D), n, n4, p.S,
+                       a);
   } else {
     float4* part = reinterpret_cast<float4*>(ws + static_cast<int64_t>(p.S) * n4 * 4);
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, groups), dim3(kT), 0, s, w4, part, n4, p.S, 0);
+    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, groups), dim3(kT), 0, s, w4, part, n, n4, p.S, 0);
     // groups ≤ 32 (S ≤ 512): ≤ 2 more levels
     int S2 = groups;
     const float4* src = part;
@@ -2550,11 +2557,11 @@ void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc
     if (S2 > kSlabGroup) {  // one intermediate level back into the head of ws
       const int g2 = (S2 + kSlabGroup - 1) / kSlabGroup;
       float4* mid = reinterpret_cast<float4*>(ws);
-      hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, g2), dim3(kT), 0, s, src, mid, n4, S2, 0);
+      hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, g2), dim3(kT), 0, s, src, mid, n, n4, S2, 0);
       src = mid;
       S2 = g2;
     }
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, src, dst, n4, S2, a);
+    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, src, dst, n, n4, S2, a);
   }
 }
 }  // namespace

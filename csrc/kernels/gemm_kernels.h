@@ -58,8 +58,10 @@ void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
 void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_t s, int taps = 1);
 
 // One entry per weight of weight_prep: fp32 w [R][T][Cc] -> bf16 wb (same
-// layout) and tap-flipped transpose wt [Cc][T][R]; tile0 = prefix of
-// T * ceil(R/32) * ceil(Cc/32) tiles over the table.
+// layout) and tap-flipped transpose wt [Cc][T][ldt] (ldt = pad when > 0, else
+// R: a weight that is a row block of a packed one writes its columns of the
+// packed transpose); tile0 = prefix of T * ceil(R/32) * ceil(Cc/32) tiles over
+// the table.
 struct WPrepDesc {
   const float* w;
   uint16_t* wb;
@@ -80,9 +82,11 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps = 1);
 
 // D[N1,N2] (fp32) = Σ_m A[m, :N1] (bf16, lda=N1) ⊗ f(B)[m, :N2] (bf16, ldb=N2)
 // (f = optional per-column scale/shift/relu). Deterministic: split over M
-// into fp32 slabs in `ws`, then one reduction launch.
+// into fp32 slabs in `ws`, then one reduction launch. rows_out ≥ 0: D holds
+// only the first rows_out rows (the rest of A's columns are padding).
 void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
-                     const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate = false);
+                     const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate = false,
+                     int rows_out = -1);
 
 // Weight gradient of a kh×kw NHWC convolution (implicit GEMM, one tap per
 // grid.z): D[Cout][kh][kw][Cin] (fp32; = a channels_last OIHW tensor) =

@@ -29,7 +29,7 @@ void xent_forward(int dtype, const void* logits, int64_t ld, const int64_t* targ
 // (dloss_stride 0 = one device scalar for every row, e.g. grad/count for 'mean').
 void xent_backward(int dtype, const void* logits, int64_t ld, const int64_t* target, const float* lse,
                    const float* dloss, int dloss_stride, int64_t rows, int V, int64_t ignore_index,
-                   float label_smoothing, void* dlogits, int64_t ld_out, hipStream_t s);
+                   float label_smoothing, void* dlogits, int64_t ld_out, hipStream_t s, int Vpad = 0);
 
 // Row log-softmax over contiguous [rows, D] (any D; tuned for small class
 // counts). y may be a wider dtype than x (bf16 logits -> fp32 log-probs).

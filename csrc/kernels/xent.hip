@@ -128,12 +128,16 @@ __global__ void __launch_bounds__(kT) xent_fwd_kernel(const void* __restrict__ l
   }
 }
 
+// dlogits may be logits itself (in place: every element is read, then written,
+// by the same thread; hence no __restrict__ on the two). Columns [V, Vpad) of
+// the output rows are written as zeros (the padded vocabulary of the LM head,
+// whose gradient then feeds the GEMMs with K / rows = Vpad).
 template <int DT>
-__global__ void __launch_bounds__(kT) xent_bwd_kernel(const void* __restrict__ logits, int64_t ld,
+__global__ void __launch_bounds__(kT) xent_bwd_kernel(const void* logits, int64_t ld,
                                                       const int64_t* __restrict__ target,
                                                       const float* __restrict__ lse, const float* __restrict__ dloss,
                                                       int dstride, int V, int64_t ignore, float eps_ls,
-                                                      void* __restrict__ dlogits, int64_t ld_out) {
+                                                      void* dlogits, int64_t ld_out, int Vpad) {
   const int64_t r = blockIdx.x;
   constexpr int es = DT == LN_BF16 ? 2 : 4;
   const char* row = static_cast<const char*>(logits) + r * ld * es;
@@ -182,6 +186,7 @@ __global__ void __launch_bounds__(kT) xent_bwd_kernel(const void* __restrict__ l
   }
   const int tail0 = head >= V ? 0 : head + nvec * vec;
   for (int j = tail0 + threadIdx.x; j < V; j += kT) st1(j, grad(j, ldx(row, j, DT)));
+  for (int j = V + threadIdx.x; j < Vpad; j += kT) st1(j, 0.f);
 }
 
 
@@ -272,14 +277,15 @@ void xent_forward(int dtype, const void* logits, int64_t ld, const int64_t* targ
 
 void xent_backward(int dtype, const void* logits, int64_t ld, const int64_t* target, const float* lse,
                    const float* dloss, int dloss_stride, int64_t rows, int V, int64_t ignore_index,
-                   float label_smoothing, void* dlogits, int64_t ld_out, hipStream_t s) {
+                   float label_smoothing, void* dlogits, int64_t ld_out, hipStream_t s, int Vpad) {
   if (rows <= 0) return;
+  if (Vpad < V) Vpad = V;
   if (dtype == LN_BF16)
     hipLaunchKernelGGL(xent_bwd_kernel<LN_BF16>, dim3(rows), dim3(kT), 0, s, logits, ld, target, lse, dloss,
-                       dloss_stride, V, ignore_index, label_smoothing, dlogits, ld_out);
+                       dloss_stride, V, ignore_index, label_smoothing, dlogits, ld_out, Vpad);
   else
     hipLaunchKernelGGL(xent_bwd_kernel<LN_F32>, dim3(rows), dim3(kT), 0, s, logits, ld, target, lse, dloss,
-                       dloss_stride, V, ignore_index, label_smoothing, dlogits, ld_out);
+                       dloss_stride, V, ignore_index, label_smoothing, dlogits, ld_out, Vpad);
 }
 
 }  // namespace kern

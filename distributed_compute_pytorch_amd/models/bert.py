@@ -19,9 +19,9 @@ from torch import nn
 from torch.nn import functional as F
 
 from ..ops.attention import attn_supported, flash_attn_qkv
-from ..ops.cross_entropy import fused_cross_entropy
 from ..ops.embedding import FusedEmbedding
-from ..ops.linear import FusedLinear, fused_mlp_gelu, packed_linear
+from ..ops.linear import FusedLinear, LinearWeightPrep, fused_mlp_gelu, packed_linear
+from ..ops.lm_head import lm_head_cross_entropy, padded_vocab
 from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
 
@@ -146,6 +146,12 @@ class BertForPreTraining(nn.Module):
         ``mlm_positions`` [B, P] (fixed predictions per sequence, no host sync) —
         the [B, P] label ids of those positions."""
         B, T = input_ids.shape
+        if self.cfg.fused and input_ids.is_cuda:
+            # bf16 W / Wᵀ of every Linear, packed QKV and the padded MLM head: one launch per optimizer step
+            LinearWeightPrep.attach(
+                self, packed=[(l.attention.query.weight, l.attention.key.weight, l.attention.value.weight)
+                              for l in self.layers],
+                heads={self.word_embeddings.weight: padded_vocab(self.cfg.vocab_size)})
         pos = torch.arange(T, device=input_ids.device)
         if token_type_ids is None:
             token_type_ids = torch.zeros_like(input_ids)
@@ -178,11 +184,10 @@ class BertForPreTraining(nn.Module):
             h = self.mlm_ln(self.mlm_transform.forward_gelu(h))
         else:
             h = self.mlm_ln(F.gelu(self.mlm_transform(h)))
-        logits = F.linear(h, self.word_embeddings.weight, self.mlm_bias)
         if self.cfg.fused:
-            mlm = fused_cross_entropy(logits, tgt)
+            mlm = lm_head_cross_entropy(h, self.word_embeddings.weight, self.mlm_bias, tgt)
         else:
-            mlm = F.cross_entropy(logits.float(), tgt)
+            mlm = F.cross_entropy(F.linear(h, self.word_embeddings.weight, self.mlm_bias).float(), tgt)
         loss = mlm
         if nsp_labels is not None:
             loss = loss + F.cross_entropy(nsp_logits.float(), nsp_labels)

@@ -23,7 +23,8 @@ from torch.nn import functional as F
 from ..ops.attention import attn_supported, flash_attn_qkv
 from ..ops.cross_entropy import fused_cross_entropy
 from ..ops.embedding import FusedEmbedding
-from ..ops.linear import FusedLinear, fused_mlp_gelu
+from ..ops.linear import FusedLinear, LinearWeightPrep, fused_mlp_gelu
+from ..ops.lm_head import lm_head_cross_entropy, padded_vocab
 from ..ops.dropout import dropout_add
 from ..ops.layernorm import FusedLayerNorm
 
@@ -136,11 +137,17 @@ class GPT2(nn.Module):
 
     def forward(self, idx, targets=None):
         B, T = idx.shape
+        if self.cfg.fused and idx.is_cuda:
+            # bf16 W / Wᵀ of every Linear and the padded tied head: one launch per optimizer step
+            LinearWeightPrep.attach(self, heads={self.wte.weight: padded_vocab(self.cfg.vocab_size)})
         pos = torch.arange(T, device=idx.device)
         x = self.drop(self.wte(idx) + self.wpe(pos))
         for blk in self.h:
             x = blk(x)
         x = self.ln_f(x)
+        if targets is not None and self.cfg.fused:
+            # tied head + cross-entropy as one node on our GEMMs (no logits returned)
+            return lm_head_cross_entropy(x, self.wte.weight, None, targets)
         logits = F.linear(x, self.wte.weight)  # tied head
         if targets is None:
             return logits

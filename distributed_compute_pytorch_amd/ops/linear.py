@@ -23,6 +23,7 @@ import os
 import torch
 from torch import nn
 from torch.nn import functional as F
+from torch.utils.weak import WeakIdKeyDictionary
 
 from .._ext import C as _C
 
@@ -248,10 +249,16 @@ def _fwd_cands(x2, w, b, b32, mode: int) -> dict:
         c["pp"] = lambda: _C.gemm_pp(x2, w, b32, mode)
     c["ring"] = lambda: _C.linear_fwd(x2, w, b32, mode)
     if mode:
-        c["hipblaslt"] = lambda: _C.gelu_fwd(F.linear(x2, w, b), mode == 1)
+        c["hipblaslt"] = lambda: _C.gelu_fwd(F.linear(x2, w, _lb(b)), mode == 1)
     else:
-        c["hipblaslt"] = lambda: F.linear(x2, w, b)
+        c["hipblaslt"] = lambda: F.linear(x2, w, _lb(b))
     return c
+
+
+def _lb(b):
+    """The bias as the bf16 ATen GEMMs take it, cast only where one runs (our
+    kernels read the fp32 bias in their epilogue)."""
+    return b if b is None or b.dtype == torch.bfloat16 else b.detach().to(torch.bfloat16)
 
 
 def _bias32(bias: torch.Tensor) -> torch.Tensor:
@@ -259,20 +266,26 @@ def _bias32(bias: torch.Tensor) -> torch.Tensor:
     return b if b.dtype == torch.float32 and b.is_contiguous() else b.float().contiguous()
 
 
+def _linear_fwd(x, w, b, bias):
+    """x·wᵀ + b on the kernel the per-shape autotune picked (bf16 x, w; ``b``
+    the bias as given, ``bias`` its fp32 parameter for our epilogues)."""
+    if _gemm_ok(x, w, bias):
+        x2, b32 = x.reshape(-1, x.shape[-1]), _bias32(bias)
+        M, K, N = x2.shape[0], w.shape[1], w.shape[0]
+        c = _pick(("fwd", M, K, N), _fwd_cands(x2, w, b, b32, 0))
+        if c == "pp":
+            return _C.gemm_pp(x, w, b32, 0)[0]
+        if c == "ring":
+            return _C.linear_fwd(x, w, b32, 0)[0]
+    return F.linear(x, w, _lb(b))
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, w16, b16, w16t):
         x, w, b = _setup(ctx, x, weight, bias, w16, b16)
         ctx.save_for_backward(x, w, w16t)
-        if _gemm_ok(x, w, bias):
-            x2, b32 = x.reshape(-1, x.shape[-1]), _bias32(bias)
-            M, K, N = x2.shape[0], w.shape[1], w.shape[0]
-            c = _pick(("fwd", M, K, N), _fwd_cands(x2, w, b, b32, 0))
-            if c == "pp":
-                return _C.gemm_pp(x, w, b32, 0)[0]
-            if c == "ring":
-                return _C.linear_fwd(x, w, b32, 0)[0]
-        return F.linear(x, w, b)
+        return _linear_fwd(x, w, b, bias)
 
     @staticmethod
     def backward(ctx, gy):
@@ -285,7 +298,7 @@ class _LinearFn(torch.autograd.Function):
 
 def _setup(ctx, x, weight, bias, w16, b16):
     w = w16 if w16 is not None else weight.to(torch.bfloat16)
-    b = (b16 if b16 is not None else bias.to(torch.bfloat16)) if bias is not None else None
+    b = (b16 if b16 is not None else bias.detach()) if bias is not None else None  # cast by _lb where ATen runs
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
     ctx.wdtype = weight.dtype
@@ -370,7 +383,7 @@ class _LinearGeluFn(torch.autograd.Function):
         elif c == "ring":
             y, h = _C.linear_fwd(x, w, b32, mode)
         else:
-            h = F.linear(x, w, b)
+            h = F.linear(x, w, _lb(b))
             y = _C.gelu_fwd(h, tanh_approx)
         ctx.save_for_backward(x, w, h, w16t)
         return y
@@ -437,13 +450,22 @@ class FusedLinear(nn.Linear):
             x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
                                           and torch.get_autocast_dtype("cuda") == torch.bfloat16))
 
+    def _w16_pair(self):
+        """(bf16 W, bf16 Wᵀ): the model's LinearWeightPrep views when they are
+        current, else the cached casts."""
+        v = prepped_linear((self.weight,))
+        if v is not None:
+            return v
+        w16 = self._bf16(self.weight, "_w16_cache")
+        if w16 is None:
+            w16 = self.weight.detach().to(torch.bfloat16)
+        return w16, self._bf16t(w16)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self._fast(x):
-            w16 = self._bf16(self.weight, "_w16_cache")
-            if w16 is None:
-                w16 = self.weight.detach().to(torch.bfloat16)
+            w16, w16t = self._w16_pair()
             b16 = self._bf16(self.bias, "_b16_cache") if self.bias is not None else None
-            return _LinearFn.apply(x, self.weight, self.bias, w16, b16, self._bf16t(w16))
+            return _LinearFn.apply(x, self.weight, self.bias, w16, b16, w16t)
         return super().forward(x)
 
     def forward_gelu(self, x: torch.Tensor, approximate: str = "none") -> torch.Tensor:
@@ -452,31 +474,205 @@ class FusedLinear(nn.Linear):
         if approximate not in ("none", "tanh"):
             raise ValueError(f"approximate must be 'none' or 'tanh', got {approximate!r}")
         if _FUSED_GELU and self._fast(x):
-            w16 = self._bf16(self.weight, "_w16_cache")
-            if w16 is None:
-                w16 = self.weight.detach().to(torch.bfloat16)
+            w16, w16t = self._w16_pair()
             b16 = self._bf16(self.bias, "_b16_cache") if self.bias is not None else None
-            return _LinearGeluFn.apply(x, self.weight, self.bias, w16, b16, self._bf16t(w16), approximate == "tanh")
+            return _LinearGeluFn.apply(x, self.weight, self.bias, w16, b16, w16t, approximate == "tanh")
         return F.gelu(self.forward(x), approximate=approximate)
 
 
 def packed_linear(x: torch.Tensor, layers) -> torch.Tensor:
-    """``torch.cat([l(x) for l in layers], -1)`` as ONE GEMM: the layers'
-    weights / biases are concatenated (an autograd cat, so each keeps its own
-    parameter, gradient and state_dict key) and run through :class:`_LinearFn`
-    — one forward GEMM, one data-gradient GEMM whose K spans all the layers
-    (no separate adds of the per-layer input gradients) and one weight-gradient
-    GEMM. BERT's query / key / value projections: their packed output feeds
-    the packed flash-attention entry point directly."""
-    w = torch.cat([l.weight for l in layers], 0)
-    b = torch.cat([l.bias for l in layers], 0) if all(l.bias is not None for l in layers) else None
-    fast = x.is_cuda and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and (
+    """``torch.cat([l(x) for l in layers], -1)`` as ONE GEMM: one forward GEMM,
+    one data-gradient GEMM whose K spans all the layers (no separate adds of
+    the per-layer input gradients) and one weight-gradient GEMM; each layer
+    keeps its own parameter, gradient and state_dict key. BERT's query / key /
+    value projections: their packed output feeds the packed flash-attention
+    entry point directly. With the model's :class:`LinearWeightPrep` current,
+    the packed bf16 weight and its transpose come from its one launch per
+    optimizer step (:class:`_PackedLinearFn`: no fp32 weight concatenation,
+    cast or transpose per call); else the weights are concatenated here."""
+    fast = x.is_cuda and all(l.in_features % 8 == 0 and l.out_features % 8 == 0 for l in layers) and (
         x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
                                       and torch.get_autocast_dtype("cuda") == torch.bfloat16))
+    if fast and all(l.bias is not None for l in layers):
+        v = prepped_linear(tuple(l.weight for l in layers))
+        if v is not None:
+            b = torch.cat([l.bias for l in layers], 0)
+            return _PackedLinearFn.apply(x, b, v[0], v[1], *(l.weight for l in layers))
+    w = torch.cat([l.weight for l in layers], 0)
+    b = torch.cat([l.bias for l in layers], 0) if all(l.bias is not None for l in layers) else None
     if not fast or b is None:
         return F.linear(x, w, b)
     w16 = w.detach().to(torch.bfloat16)
-    return _LinearFn.apply(x, w, b, w16, b.detach().to(torch.bfloat16), w16.t().contiguous())
+    return _LinearFn.apply(x, w, b, w16, None, w16.t().contiguous())
+
+
+class _PackedLinearFn(torch.autograd.Function):
+    """y = x·[W₁; W₂; …]ᵀ + b over the row-packed bf16 weight (and its
+    transpose) of a :class:`LinearWeightPrep` group; the packed fp32 weight
+    gradient goes back to each member as its row slice."""
+
+    @staticmethod
+    def forward(ctx, x, bias, w16, w16t, *weights):
+        x, w, b = _setup(ctx, x, weights[0], bias, w16, None)
+        ctx.params = (None, bias)  # no in-place .grad add: the packed gradient is split by rows
+        ctx.rows = [wt.shape[0] for wt in weights]
+        ctx.save_for_backward(x, w, w16t)
+        return _linear_fwd(x, w, b, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, wt = ctx.saved_tensors
+        gy = gy.contiguous()
+        if gy.dtype != torch.bfloat16:
+            gy = gy.to(torch.bfloat16)
+        n = ctx.needs_input_grad
+        sub = _Sub((n[0], any(n[4:]), n[1]), ctx.params, ctx.wdtype, ctx.bdtype, ctx.accum)
+        dx, dw, db = _linear_backward(sub, gy.view(-1, gy.shape[-1]), x, w, wt=wt)
+        dws = dw.split(ctx.rows, 0) if dw is not None else (None,) * len(ctx.rows)
+        return (dx, db, None, None, *dws)
+
+
+# weight -> (LinearWeightPrep, group index) for every weight a prep writes
+_PREP_OF = WeakIdKeyDictionary()
+
+
+def prepped_linear(weights: tuple):
+    """(bf16 W, bf16 Wᵀ) of a weight — or of a row-packed group of weights —
+    from the :class:`LinearWeightPrep` that owns it, when its buffer holds the
+    weights' current values; else None."""
+    e = _PREP_OF.get(weights[0])
+    if e is None:
+        return None
+    return e[0].views(e[1], weights)
+
+
+class LinearWeightPrep:
+    """bf16 GEMM operands of a model's Linear weights, ALL written by ONE
+    kernel launch per optimizer step (``weight_prep_kernel``, gemm.hip) into
+    one persistent buffer: per weight — or per row-packed group (BERT's
+    query / key / value) — the bf16 W [N, K] the forward GEMM reads and the
+    bf16 Wᵀ [K, N] of the data gradient, through an LDS-tiled transpose. A
+    group may be padded to ``pad_rows`` rows (zeros): the tied LM head's
+    vocabulary is padded to a multiple of 64 so it runs on our GEMMs
+    (:func:`lm_head_cross_entropy`).
+
+    Replaces, per step, one cast launch per weight (or the fused optimizer's
+    bf16 shadow write) plus one ATen strided-copy transpose per weight
+    (0.59 ms of a GPT-2 step, profiles/r3_gpt2_copy_trace.log) and
+    packed_linear's per-call fp32 concatenation, cast and transpose.
+
+    :meth:`refresh` — called at the top of the model's forward — relaunches
+    only when a weight changed (fused-optimizer epoch, autograd version) or
+    while a HIP graph is being captured (the launch is then part of every
+    replay; the buffer's addresses are fixed), and replans when a weight's
+    storage moved. Readers (:func:`prepped_linear`) get the views only while
+    they are current; otherwise they cast themselves. The backward keeps
+    references to the buffer (saved tensors); the next rewrite happens after
+    the optimizer step, i.e. after that backward.
+    Reference parity: the ``nn.Linear`` layers of the BASELINE transformer
+    configs."""
+
+    def __init__(self, groups, pad_rows=None):
+        self.groups = [tuple(g) for g in groups]
+        self.pad_rows = [int(r) for r in pad_rows] if pad_rows is not None else [0] * len(self.groups)
+        if len(self.pad_rows) != len(self.groups):
+            raise ValueError("LinearWeightPrep: one pad_rows entry per group")
+        for g in self.groups:
+            for w in g:
+                if not self.eligible(w):
+                    raise ValueError("LinearWeightPrep: contiguous fp32 2-D CUDA weights with "
+                                     f"multiples of 8 rows / columns required, got {tuple(w.shape)} {w.dtype}")
+        self._ptrs = None
+        self._epoch = None
+        self._versions = None
+        self._first = []  # group -> index of its first weight in the flat weight list
+        k = 0
+        for i, g in enumerate(self.groups):
+            _PREP_OF[g[0]] = (self, i)
+            self._first.append(k)
+            k += len(g)
+
+    @staticmethod
+    def eligible(w: torch.Tensor) -> bool:
+        return (w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.is_contiguous()
+                and w.shape[1] % 8 == 0)
+
+    @classmethod
+    def for_model(cls, model: nn.Module, packed=(), heads=None) -> "LinearWeightPrep":
+        """A prep over every eligible :class:`FusedLinear` of ``model`` (members
+        of ``packed`` groups only as their group) plus ``heads`` ({weight:
+        padded rows}: tied LM heads)."""
+        packed = [tuple(g) for g in packed if all(cls.eligible(w) and w.shape[0] % 8 == 0 for w in g)
+                  and len({w.shape[1] for w in g}) == 1]
+        heads = {w: r for w, r in (heads or {}).items() if cls.eligible(w)}
+        in_group = {id(w) for g in packed for w in g}
+        groups, pads = [], []
+        for m in model.modules():
+            if isinstance(m, FusedLinear) and id(m.weight) not in in_group and cls.eligible(m.weight) \
+                    and m.weight.shape[0] % 8 == 0:
+                groups.append((m.weight,))
+                pads.append(0)
+        for g in packed:
+            groups.append(g)
+            pads.append(0)
+        for w, rows in heads.items():
+            groups.append((w,))
+            pads.append(rows)
+        return cls(groups, pads)
+
+    @classmethod
+    def attach(cls, model: nn.Module, packed=(), heads=None):
+        """The model's prep, refreshed (a no-op while the weights are
+        unchanged): built on the first call with the model on the GPU and
+        rebuilt when a weight Parameter was replaced; None on the CPU."""
+        p = model.__dict__.get("_linear_prep")
+        if p is None or p._stale_params(model, packed, heads):
+            if not any(m.weight.is_cuda for m in model.modules() if isinstance(m, FusedLinear)):
+                return None
+            p = cls.for_model(model, packed, heads)
+            p._sig = cls._signature(model, packed, heads)
+            model.__dict__["_linear_prep"] = p
+        p.refresh()
+        return p
+
+    @staticmethod
+    def _signature(model, packed, heads):
+        return tuple(id(m.weight) for m in model.modules() if isinstance(m, FusedLinear)) + tuple(
+            id(w) for g in packed for w in g) + tuple(id(w) for w in (heads or {}))
+
+    def _stale_params(self, model, packed, heads) -> bool:
+        return getattr(self, "_sig", None) != self._signature(model, packed, heads)
+
+    def refresh(self) -> None:
+        from ..optim.fused import param_epoch
+
+        ws = [w for g in self.groups for w in g]
+        ptrs = tuple(w.data_ptr() for w in ws)
+        if ptrs != self._ptrs:
+            self.table, self.tiles, self.wb, self.wt = _C.weight_prep_plan(
+                [w.detach() for w in ws], [len(g) for g in self.groups], self.pad_rows)
+            self._ptrs, self._epoch = ptrs, None
+        capturing = torch.cuda.is_current_stream_capturing()
+        versions = [w._version for w in ws]
+        epoch = param_epoch()
+        if capturing or epoch != self._epoch or versions != self._versions:
+            _C.weight_prep_run(self.table, self.tiles)
+            self._epoch, self._versions = epoch, versions
+
+    def views(self, i: int, weights: tuple):
+        """(wb, wt) of group ``i`` if it is ``weights`` and current, else None."""
+        from ..optim.fused import param_epoch
+
+        g = self.groups[i]
+        if self._epoch is None or len(g) != len(weights) or any(a is not b for a, b in zip(g, weights)):
+            return None
+        if param_epoch() != self._epoch or self._ptrs is None:
+            return None
+        k = self._first[i]
+        for j, w in enumerate(g):
+            if w._version != self._versions[k + j] or w.data_ptr() != self._ptrs[k + j]:
+                return None
+        return self.wb[i], self.wt[i]
 
 
 class _Sub:
@@ -507,14 +703,13 @@ class _MLPFn(torch.autograd.Function):
         else:
             y1, h = _C.linear_fwd(x, w1_16, b1_32, mode)
         y1_2 = y1.reshape(-1, y1.shape[-1])
-        c2 = _pick(("fwd", y1_2.shape[0], w2_16.shape[1], w2_16.shape[0]),
-                   _fwd_cands(y1_2, w2_16, b2_16_of(b2), b2_32, 0))
+        c2 = _pick(("fwd", y1_2.shape[0], w2_16.shape[1], w2_16.shape[0]), _fwd_cands(y1_2, w2_16, b2, b2_32, 0))
         if c2 == "pp":
             out = _C.gemm_pp(y1, w2_16, b2_32, 0)[0]
         elif c2 == "ring":
             out = _C.linear_fwd(y1, w2_16, b2_32, 0)[0]
         else:
-            out = F.linear(y1, w2_16, b2_16_of(b2))
+            out = F.linear(y1, w2_16, _lb(b2))
         ctx.save_for_backward(x, h, y1, w1_16, w2_16, w1t, w2t)
         ctx.tanh = tanh
         ctx.accum = accumulating()
@@ -571,10 +766,6 @@ def _mlp_prefers_ours(x, w1_16, b1, b1_16, w2_16, w2t, tanh) -> bool:
     return _CHOICE[key_f] != "hipblaslt" and _CHOICE[key_d] == "ring"
 
 
-def b2_16_of(b):
-    return b.detach().to(torch.bfloat16) if b is not None else None
-
-
 def fused_mlp_gelu(x: torch.Tensor, fc: "FusedLinear", proj: "FusedLinear", approximate: str = "none"):
     """``proj(F.gelu(fc(x), approximate))`` — one autograd node (:class:`_MLPFn`)
     on the fast path (bf16 GPU, GEMM-able shapes), else the two modules."""
@@ -586,17 +777,15 @@ def fused_mlp_gelu(x: torch.Tensor, fc: "FusedLinear", proj: "FusedLinear", appr
           and fc.in_features <= 4096 and proj.in_features <= 4096 and proj.out_features <= 4096
           and proj.in_features == fc.out_features)
     if ok:
-        w1_16 = fc._bf16(fc.weight, "_w16_cache")
-        w1_16 = w1_16 if w1_16 is not None else fc.weight.detach().to(torch.bfloat16)
-        w2_16 = proj._bf16(proj.weight, "_w16_cache")
-        w2_16 = w2_16 if w2_16 is not None else proj.weight.detach().to(torch.bfloat16)
+        w1_16, w1t = fc._w16_pair()
+        w2_16, w2t = proj._w16_pair()
         b1_16 = fc._bf16(fc.bias, "_b16_cache")
         # the fused node runs both its GEMMs on our kernel: take it only where
         # the per-shape autotune prefers our kernel for both (at BERT's 16,384
         # rows hipBLASLt wins them and the unfused path measured 1.7 % faster)
-        ok = _mlp_prefers_ours(x, w1_16, fc.bias, b1_16, w2_16, proj._bf16t(w2_16), approximate == "tanh")
+        ok = _mlp_prefers_ours(x, w1_16, fc.bias, b1_16, w2_16, w2t, approximate == "tanh")
     if not ok:
         return proj(fc.forward_gelu(x, approximate) if isinstance(fc, FusedLinear) else
                     F.gelu(fc(x), approximate=approximate))
-    return _MLPFn.apply(x, fc.weight, fc.bias, proj.weight, proj.bias, w1_16, b1_16, w2_16, fc._bf16t(w1_16),
-                        proj._bf16t(w2_16), approximate == "tanh")
+    return _MLPFn.apply(x, fc.weight, fc.bias, proj.weight, proj.bias, w1_16, b1_16, w2_16, w1t, w2t,
+                        approximate == "tanh")

@@ -1,0 +1,134 @@
+"""Tied LM head + softmax cross-entropy on our kernels.
+
+``loss = F.cross_entropy(x @ Wᵀ + b, target)`` for a vocabulary-sized W (GPT-2's
+tied ``wte`` [50257, 768], BERT's MLM head over the word embeddings [30522,
+768]) as one autograd node:
+
+* the bf16 weight and its transpose come from the model's
+  :class:`~.linear.LinearWeightPrep`, padded with zero rows to ``Vp`` — the
+  next multiple of 64 — so the vocabulary GEMMs take our kernels' shapes (no
+  per-micro-step fp32→bf16 cast of the 38.6 M-parameter embedding);
+* forward: logits [M, Vp] on the autotuned GEMM (256×256 ping-pong / 128×128
+  ring / hipBLASLt), then the one-pass cross-entropy over the first V columns
+  (``xent.hip``; the pad columns are never read);
+* backward: the cross-entropy gradient is written IN PLACE over the logits,
+  pad columns zeroed (no second [M, Vp] buffer), the data gradient is dL·W on
+  the autotuned GEMM with K = Vp, and the fp32 weight gradient comes from our
+  split-M wgrad GEMM straight into ``W.grad`` (only its first V rows; no bf16
+  dW, no cast, no separate AccumulateGrad add — the tied embedding's two
+  gradient contributions meet in one fp32 buffer).
+
+Reference parity: the Linear + log_softmax / NLL head of ``main.py:27-28,43-44``
+ at the BASELINE transformer configs' vocabulary size.
+"""
+from __future__ import annotations
+
+import torch
+from torch.nn import functional as F
+
+from .._ext import C as _C
+from .cross_entropy import fused_cross_entropy
+from .linear import _pick, _pp_ok, accumulating, inplace_grad, prepped_linear
+
+
+def padded_vocab(v: int) -> int:
+    """Rows of the padded head weight: the next multiple of 64."""
+    return (v + 63) // 64 * 64
+
+
+_ZERO_BIAS: dict = {}
+
+
+def _zero_bias(n: int, device) -> torch.Tensor:
+    key = (n, device)
+    z = _ZERO_BIAS.get(key)
+    if z is None:
+        z = _ZERO_BIAS[key] = torch.zeros(n, device=device, dtype=torch.float32)
+    return z
+
+
+class _LMHeadXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, target, wb, wt, ignore_index):
+        V, K = weight.shape
+        Vp = wb.shape[0]
+        x2 = x.reshape(-1, K)
+        if x2.dtype != torch.bfloat16:
+            x2 = x2.to(torch.bfloat16)
+        x2 = x2.contiguous()
+        M = x2.shape[0]
+        b32 = None
+        if bias is not None:
+            b32 = F.pad(bias.detach().float(), (0, Vp - V))
+        cands = {}
+        if _pp_ok(M, Vp, K):
+            cands["pp"] = lambda: _C.gemm_pp(x2, wb, b32, 0)[0]
+        if K <= 4096 and K % 64 == 0:
+            cands["ring"] = lambda: _C.linear_fwd(x2, wb, b32 if b32 is not None else _zero_bias(Vp, x2.device), 0)[0]
+        cands["hipblaslt"] = lambda: F.linear(x2, wb, b32.to(torch.bfloat16) if b32 is not None else None)
+        c = _pick(("head", M, K, Vp), cands)
+        logits = cands[c]()
+        tg = target.reshape(-1)
+        loss, lse = _C.cross_entropy_fwd(logits, tg, ignore_index, 0.0, V)
+        count = (tg != ignore_index).sum().clamp_min(1)
+        ctx.save_for_backward(x2, logits, lse, tg, wb, wt, count)
+        ctx.ignore_index, ctx.V, ctx.accum = ignore_index, V, accumulating()
+        ctx.params = (weight, bias)
+        ctx.xshape, ctx.xdtype = x.shape, x.dtype
+        return loss.sum() / count
+
+    @staticmethod
+    def backward(ctx, g):
+        # unpacking checks the saved logits' version: a second backward through
+        # this node (retain_graph) fails here, as the first one overwrote them
+        x2, logits, lse, tg, wb, wt, count = ctx.saved_tensors
+        weight, bias = ctx.params
+        V = ctx.V
+        M, K = x2.shape
+        Vp = wb.shape[0]
+        dl = (g.float() / count).reshape(1)
+        d = _C.cross_entropy_bwd(logits, tg, lse, dl, ctx.ignore_index, 0.0, V, True)  # [M, Vp], pad cols 0
+        dx = dw = db = None
+        n = ctx.needs_input_grad
+        if n[0]:
+            cands = {}
+            if _pp_ok(M, K, Vp):
+                cands["pp"] = lambda: _C.gemm_pp(d, wt)[0]
+            cands["hipblaslt"] = lambda: d @ wb
+            c = _pick(("head_dgrad", M, Vp, K), cands)
+            dx = cands[c]().view(ctx.xshape)
+            if dx.dtype != ctx.xdtype:
+                dx = dx.to(ctx.xdtype)
+        if n[1]:
+            tgt = inplace_grad(weight, weight.shape, ctx.accum)
+            dw = _C.conv1x1_wgrad(d, x2, accumulate_into=tgt, out_rows=V)
+            if tgt is not None:
+                dw = None  # added into weight.grad by the wgrad's reduction pass
+            elif dw.dtype != weight.dtype:
+                dw = dw.to(weight.dtype)
+        if bias is not None and n[2]:
+            db = _C.colsum(d)[:V]
+            if db.dtype != bias.dtype:
+                db = db.to(bias.dtype)
+        return dx, dw, db, None, None, None, None
+
+
+def lm_head_cross_entropy(x: torch.Tensor, weight: torch.Tensor, bias, target: torch.Tensor,
+                          ignore_index: int = -100) -> torch.Tensor:
+    """Mean cross-entropy of ``x @ weight.T (+ bias)`` against ``target``
+    (``F.cross_entropy`` semantics, ``reduction="mean"``). Runs
+    :class:`_LMHeadXentFn` for bf16 compute (bf16 ``x`` or bf16 autocast) when
+    the model's LinearWeightPrep holds a current padded bf16 copy of
+    ``weight`` (see ``padded_vocab``); otherwise the ATen GEMM +
+    ``fused_cross_entropy``."""
+    K = weight.shape[1]
+    bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
+                                         and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    v = prepped_linear((weight,)) if x.is_cuda and bf16 else None
+    if v is not None and K % 64 == 0 and x.numel() > 0 and v[0].shape[0] % 64 == 0:
+        with torch.autocast("cuda", enabled=False):
+            return _LMHeadXentFn.apply(x, weight, bias, target, v[0], v[1], ignore_index)
+    logits = F.linear(x, weight, bias)
+    flat = logits.reshape(-1, logits.shape[-1])
+    return fused_cross_entropy(flat, target.reshape(-1), ignore_index=ignore_index) if x.is_cuda else \
+        F.cross_entropy(flat.float(), target.reshape(-1), ignore_index=ignore_index)
