@@ -117,13 +117,14 @@ __device__ __forceinline__ void stage_tile(const uint16_t* src, int64_t st, int 
   }
 }
 
-// ---- dropout: 16 random bits per element (q, key) from a counter hash: one
-// 32-bit hash per (query, key pair) — keys 2j and 2j+1 take its low / high
-// half. Identical in forward and backward. The counter is bit-packed
-// (q << 12 | key / 2, T ≤ 8192) and the (batch, head) index and the seed are
+// ---- dropout: 8 random bits per element (q, key) from a counter hash: one
+// 32-bit hash per (query, aligned group of 4 keys) — key 4j + e takes byte e
+// (the FlashAttention-2 practice of byte thresholds: p is quantised to
+// multiples of 1/256 and the keep scale is 1/(1 - p_eff) with p_eff =
+// thr / 256). Identical in forward and backward. The counter is bit-packed
+// (q << 11 | key / 4, T ≤ 8192) and the (batch, head) index and the seed are
 // folded into a per-workgroup key, so a hash costs one murmur3 finaliser (two
-// 32-bit multiplies — quarter-rate VALU) instead of a multiply-built counter
-// plus three multiplies.
+// 32-bit multiplies — quarter-rate VALU), one per 4 elements.
 __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x85ebca6bu;
@@ -136,12 +137,14 @@ __device__ __forceinline__ uint32_t drop_key(uint32_t s0, uint32_t s1, uint32_t 
   return fmix32(s0 ^ fmix32(bh * 0x9E3779B1u + s1));
 }
 __device__ __forceinline__ uint32_t drop_hash(uint32_t kbh, uint32_t q, uint32_t key) {
-  return fmix32(((q << 12) | (key >> 1)) ^ kbh);
+  return fmix32(((q << 11) | (key >> 2)) ^ kbh);
 }
-__device__ __forceinline__ bool drop_keep(uint32_t hsh, uint32_t key, uint32_t thr) {
-  const uint32_t r16 = (key & 1) ? (hsh >> 16) : (hsh & 0xffffu);
-  return r16 >= thr;
+// byte e of the hash ≥ thr (e is a compile-time constant at every call)
+__device__ __forceinline__ bool drop_keep(uint32_t hsh, int e, uint32_t thr) {
+  return ((hsh >> (8 * e)) & 0xffu) >= thr;
 }
+__device__ __forceinline__ uint32_t drop_thr(float p) { return static_cast<uint32_t>(p * 256.f + 0.5f); }
+__device__ __forceinline__ float drop_scale(uint32_t thr) { return 256.f / static_cast<float>(256u - thr); }
 
 struct Ptrs {
   const uint16_t* p;
@@ -179,8 +182,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
     qf[ks] = __builtin_bit_cast(bf16x8, qok ? u : z);
   }
   const float c = P.scale * kLog2e;
-  const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
-  const float inv_keep = 1.f / (1.f - P.p_drop);
+  const uint32_t thr = drop_thr(P.p_drop);
   const uint32_t kbh = drop_key(static_cast<uint32_t>(P.seed), static_cast<uint32_t>(P.seed >> 32), bh);
 
   float m = -INFINITY, l = 0.f;
@@ -211,51 +213,55 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) s[kh] = mfma(row_rd(sK, 32 * kh + (lane & 31), 2 * ks + hh), qf[ks], s[kh]);
     }
-    // s[kh][r]: key kb + 32kh + (r&3) + 8(r>>2) + 4hh, query qi
+    // s[kh][r]: key kb + 32kh + (r&3) + 8(r>>2) + 4hh, query qi. Raw scores:
+    // the max is taken before scaling (c > 0) and the scale is folded into
+    // the exponent's fma. The causal mask only on the blocks that reach past
+    // this wave's first query (wave-uniform: the others need no compare).
+    if (CAUSAL && kb + kKB - 1 > tile * 128 + wave * 32) {
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          s[kh][r] = key > qi ? -INFINITY : s[kh][r];
+        }
+    }
     float mx = m;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float x = s[kh][r] * c;
-        if (CAUSAL) {
-          const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          x = key > qi ? -INFINITY : x;
-        }
-        s[kh][r] = x;
-        mx = fmaxf(mx, x);
-      }
+      for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(s[kh][r], s[kh][r + 1]));
     mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float alpha = __builtin_amdgcn_exp2f(m - mx);
+    // (every wave's first block holds key 0 ≤ its queries: mx is finite from there on)
+    const float alpha = __builtin_amdgcn_exp2f((m - mx) * c);
+    const float nmc = -mx * c;
     float rs = 0.f;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pp = __builtin_amdgcn_exp2f(s[kh][r] - mx);
+        const float pp = __builtin_amdgcn_exp2f(fmaf(s[kh][r], c, nmc));
         s[kh][r] = pp;
         rs += pp;
       }
     rs += __shfl_xor(rs, 32);
     l = l * alpha + rs;
     m = mx;
+    if (!__all(alpha == 1.f)) {  // the running max moved in some lane: rescale O
 #pragma unroll
-    for (int dh = 0; dh < 2; ++dh)
+      for (int dh = 0; dh < 2; ++dh)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[dh][r] *= alpha;
-    if (DROP) {
+        for (int r = 0; r < 16; ++r) oacc[dh][r] *= alpha;
+    }
+    if (DROP) {  // registers 4g … 4g+3 hold keys 4j … 4j+3: one hash each; the keep scale goes on O at the end
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t hs = drop_hash(kbh, qi, kb + 32 * kh + 8 * g + 4 * hh);
 #pragma unroll
-          for (int pr = 0; pr < 2; ++pr) {
-            const uint32_t key = kb + 32 * kh + 8 * g + 4 * hh + 2 * pr;
-            const uint32_t hs = drop_hash(kbh, qi, key);
-            const int r = 4 * g + 2 * pr;
-            s[kh][r] = drop_keep(hs, key, thr) ? s[kh][r] * inv_keep : 0.f;
-            s[kh][r + 1] = drop_keep(hs, key + 1, thr) ? s[kh][r + 1] * inv_keep : 0.f;
-          }
+          for (int e = 0; e < 4; ++e) s[kh][4 * g + e] = drop_keep(hs, e, thr) ? s[kh][4 * g + e] : 0.f;
+        }
     }
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
@@ -267,7 +273,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
       }
   }
   if (qok) {
-    const float inv = 1.f / l;
+    const float inv = (DROP ? drop_scale(thr) : 1.f) / l;
     uint16_t* O = static_cast<uint16_t*>(o.ptr) + b * o.sb + hd * kD + static_cast<int64_t>(qi) * o.st;
 #pragma unroll
     for (int dh = 0; dh < 2; ++dh)
@@ -277,7 +283,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
         *reinterpret_cast<uint2*>(O + d0) = make_uint2(pack2(oacc[dh][4 * g] * inv, oacc[dh][4 * g + 1] * inv),
                                                        pack2(oacc[dh][4 * g + 2] * inv, oacc[dh][4 * g + 3] * inv));
       }
-    if (hh == 0) lse[static_cast<int64_t>(bh) * T + qi] = m + log2f(l);
+    if (hh == 0) lse[static_cast<int64_t>(bh) * T + qi] = m * c + log2f(l);
   }
 }
 
@@ -341,8 +347,8 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
   const float lse2 = qok ? lse[static_cast<int64_t>(bh) * T + qi] : 0.f;
   const float dlt = qok ? delta[static_cast<int64_t>(bh) * T + qi] : 0.f;
   const float c = P.scale * kLog2e;
-  const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
-  const float inv_keep = 1.f / (1.f - P.p_drop);
+  const uint32_t thr = drop_thr(P.p_drop);
+  const float inv_keep = drop_scale(thr);
   const uint32_t kbh = drop_key(static_cast<uint32_t>(P.seed), static_cast<uint32_t>(P.seed >> 32), bh);
 
   f32x16 dacc[2] = {zero16(), zero16()};
@@ -372,15 +378,17 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
         dp = mfma(row_rd(sV, 32 * kh + (lane & 31), 2 * ks + hh), gf[ks], dp);
       }
       uint32_t hs = 0;
+      // causal mask only where this 32-key half reaches past the wave's first query
+      const bool diag = CAUSAL && kb + 32 * kh + 31 > tile * 128 + wave * 32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        float p = __builtin_amdgcn_exp2f(s[r] * c - lse2);
-        if (CAUSAL) p = key > qi ? 0.f : p;
+        float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lse2));
+        if (CAUSAL && diag) p = key > qi ? 0.f : p;
         float g = dp[r];
         if (DROP) {
-          if ((r & 1) == 0) hs = drop_hash(kbh, qi, key);  // key even: one hash for keys key, key + 1
-          g = drop_keep(hs, key, thr) ? g * inv_keep : 0.f;
+          if ((r & 3) == 0) hs = drop_hash(kbh, qi, key);  // key ≡ 0 mod 4: one hash for keys key … key + 3
+          g = drop_keep(hs, r & 3, thr) ? g * inv_keep : 0.f;
         }
         s[r] = p * (g - dlt);  // dSᵀ (without the softmax scale)
       }
@@ -439,8 +447,8 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
     vf[ks] = __builtin_bit_cast(bf16x8, kok ? uv : z);
   }
   const float c = P.scale * kLog2e;
-  const uint32_t thr = static_cast<uint32_t>(P.p_drop * 65536.f + 0.5f);
-  const float inv_keep = 1.f / (1.f - P.p_drop);
+  const uint32_t thr = drop_thr(P.p_drop);
+  const float inv_keep = drop_scale(thr);
   const uint32_t kbh = drop_key(static_cast<uint32_t>(P.seed), static_cast<uint32_t>(P.seed >> 32), bh);
   const float* L = lse + static_cast<int64_t>(bh) * T;
   const float* DL = delta + static_cast<int64_t>(bh) * T;
@@ -474,6 +482,8 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
 #pragma unroll 1
     for (int qs = 0; qs < 2; ++qs) {
       if (CAUSAL && qb + 32 * qs + 31 < kb0 + wave * 32) continue;  // every query precedes every key
+      // the mask only where some query of the slice precedes the wave's last key
+      const bool diag = CAUSAL && qb + 32 * qs < kb0 + wave * 32 + 31;
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -493,31 +503,26 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
           const float4 l4 = *reinterpret_cast<const float4*>(sL + rl);
           const float4 d4 = *reinterpret_cast<const float4*>(sD + rl);
           const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
-          // dropout: lanes 2j and 2j+1 hold keys 2k, 2k+1, which share each
-          // row's hash — each lane hashes every other row (row e ^ its parity)
-          // and takes the partner lane's hash of the other through a DPP
-          // quad_perm [1,0,3,2] move
+          // dropout: the 4 lanes of a quad hold keys 4j … 4j+3, which share
+          // each row's hash — lane 4j + i hashes row rl + i and every lane
+          // takes row e's hash from quad lane e (DPP quad_perm [e,e,e,e])
           uint32_t hrow[4];
           if (DROP) {
-#pragma unroll
-            for (int e2 = 0; e2 < 4; e2 += 2) {
-              const bool odd = (lane & 1) != 0;
-              const uint32_t mine = drop_hash(kbh, qb + rl + e2 + (odd ? 1 : 0), key);
-              const uint32_t other = static_cast<uint32_t>(
-                  __builtin_amdgcn_mov_dpp(static_cast<int>(mine), 0xB1, 0xF, 0xF, false));
-              hrow[e2] = odd ? other : mine;
-              hrow[e2 + 1] = odd ? mine : other;
-            }
+            const int mine = static_cast<int>(drop_hash(kbh, qb + rl + (lane & 3), key));
+            hrow[0] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(mine, 0x00, 0xF, 0xF, false));
+            hrow[1] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(mine, 0x55, 0xF, 0xF, false));
+            hrow[2] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(mine, 0xAA, 0xF, 0xF, false));
+            hrow[3] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(mine, 0xFF, 0xF, 0xF, false));
           }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
             const int qrow = qb + rl + e;
-            float p = __builtin_amdgcn_exp2f(s[r] * c - lv[e]);
-            if (CAUSAL) p = key > qrow ? 0.f : p;
+            float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lv[e]));
+            if (CAUSAL && diag) p = key > qrow ? 0.f : p;
             float gg = dp[r], pk = p;
             if (DROP) {
-              const bool kp = drop_keep(hrow[e], key, thr);
+              const bool kp = drop_keep(hrow[e], key & 3, thr);
               gg = kp ? gg * inv_keep : 0.f;
               pk = kp ? p * inv_keep : 0.f;
             }

@@ -87,11 +87,18 @@ def flash_attn_qkv(qkv: torch.Tensor, heads: int, causal: bool = False, dropout_
     return _FlashAttnQKVFn.apply(qkv, heads, causal, float(dropout_p), _seed() if seed is None else int(seed))
 
 
+def dropout_p_effective(p: float) -> float:
+    """The dropout probability the kernels apply: ``p`` rounded to a multiple
+    of 1/256 (byte thresholds, as FlashAttention-2 does); kept elements are
+    scaled by 1 / (1 - dropout_p_effective(p))."""
+    return int(p * 256.0 + 0.5) / 256.0
+
+
 def dropout_keep_mask(B: int, H: int, T: int, p: float, seed: int, device=None) -> torch.Tensor:
     """The kernels' dropout keep-mask [B, H, T, T] rebuilt with integer torch
-    ops (test oracle): 16 bits of fmix32(((q << 12) | key/2) ^ kbh) per
-    element, kbh = fmix32(s0 ^ fmix32(bh·0x9E3779B1 + s1)) (murmur3 finaliser),
-    low half for even keys."""
+    ops (test oracle): byte (key mod 4) of fmix32(((q << 11) | key/4) ^ kbh)
+    per element, kbh = fmix32(s0 ^ fmix32(bh·0x9E3779B1 + s1)) (murmur3
+    finaliser), kept when ≥ round(256·p)."""
     M = 0xFFFFFFFF
     dev = device or "cpu"
 
@@ -111,7 +118,7 @@ def dropout_keep_mask(B: int, H: int, T: int, p: float, seed: int, device=None) 
     qq = torch.arange(T, device=dev, dtype=torch.int64)[None, :, None]
     kk = torch.arange(T, device=dev, dtype=torch.int64)[None, None, :]
     kbh = fmix32(s0 ^ fmix32((mul32(bh, 0x9E3779B1) + s1) & M))
-    h = fmix32(((qq << 12) | (kk >> 1)) ^ kbh)
-    r16 = torch.where((kk & 1) == 1, h >> 16, h & 0xFFFF)
-    thr = int(p * 65536.0 + 0.5)
-    return (r16 >= thr).view(B, H, T, T)
+    h = fmix32(((qq << 11) | (kk >> 2)) ^ kbh)
+    r8 = (h >> (8 * (kk & 3))) & 0xFF
+    thr = int(p * 256.0 + 0.5)
+    return (r8 >= thr).view(B, H, T, T)

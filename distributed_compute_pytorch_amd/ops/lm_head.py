@@ -79,8 +79,10 @@ class _LMHeadXentFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        # unpacking checks the saved logits' version: a second backward through
-        # this node (retain_graph) fails here, as the first one overwrote them
+        if getattr(ctx, "consumed", False):
+            raise RuntimeError("lm_head_cross_entropy: a second backward through the same graph is not supported "
+                               "(the first one overwrote the saved logits with their gradient)")
+        ctx.consumed = True
         x2, logits, lse, tg, wb, wt, count = ctx.saved_tensors
         weight, bias = ctx.params
         V = ctx.V

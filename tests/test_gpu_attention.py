@@ -31,7 +31,9 @@ def _reference(q, k, v, H, causal, p, keep):
         s = s.masked_fill(torch.ones(T, T, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
     P = torch.softmax(s, -1)
     if p > 0:
-        P = P * keep / (1 - p)
+        from distributed_compute_pytorch_amd.ops.attention import dropout_p_effective
+
+        P = P * keep / (1 - dropout_p_effective(p))
     return (P @ heads(v)).transpose(1, 2).reshape(B, T, C)
 
 
