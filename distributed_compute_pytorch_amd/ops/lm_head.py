@@ -28,6 +28,7 @@ from torch.nn import functional as F
 
 from .._ext import C as _C
 from .cross_entropy import fused_cross_entropy
+from . import linear as _lin
 from .linear import _pick, _pp_ok, accumulating, inplace_grad, prepped_linear
 
 
@@ -103,9 +104,9 @@ class _LMHeadXentFn(torch.autograd.Function):
                 dx = dx.to(ctx.xdtype)
         if n[1]:
             tgt = inplace_grad(weight, weight.shape, ctx.accum)
-            dw = _C.conv1x1_wgrad(d, x2, accumulate_into=tgt, out_rows=V)
+            dw = _head_wgrad(d, x2, V, tgt)
             if tgt is not None:
-                dw = None  # added into weight.grad by the wgrad's reduction pass
+                dw = None  # added into weight.grad by the GEMM itself
             elif dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
         if bias is not None and n[2]:
@@ -113,6 +114,36 @@ class _LMHeadXentFn(torch.autograd.Function):
             if db.dtype != bias.dtype:
                 db = db.to(bias.dtype)
         return dx, dw, db, None, None, None, None
+
+
+def _head_wgrad(d, x2, V: int, tgt):
+    """fp32 dW [V, K] = d[:, :V]ᵀ·x2, added into ``tgt`` when given (the
+    existing W.grad) else returned: our split-M wgrad GEMM (pad rows dropped
+    in its reduction pass) or hipBLASLt with an fp32 output (beta = 1 into
+    ``tgt``), whichever the per-shape autotune measured faster — timed into a
+    scratch target, so the measurement does not touch the gradient."""
+    M, K = x2.shape
+    Vp = d.shape[1]
+    key = ("head_wgrad", M, Vp, K)
+
+    def ours(t):
+        return _C.conv1x1_wgrad(d, x2, accumulate_into=t, out_rows=V)
+
+    def blas(t):
+        if t is None:
+            return torch.mm(d[:, :V].t(), x2, out_dtype=torch.float32)
+        return torch.addmm(t, d[:, :V].t(), x2, out_dtype=torch.float32, out=t)
+
+    impl = {"ring": ours, "hipblaslt": blas}
+    c = _lin._CHOICE.get(key)
+    if c is None:
+        if _lin._AUTOTUNE and not torch.cuda.is_current_stream_capturing():
+            scratch = torch.zeros(V, K, device=d.device, dtype=torch.float32)
+            c = _pick(key, {name: (lambda f=f: f(scratch)) for name, f in impl.items()})
+            del scratch
+        else:
+            c = "ring"
+    return impl[c](tgt)
 
 
 def lm_head_cross_entropy(x: torch.Tensor, weight: torch.Tensor, bias, target: torch.Tensor,

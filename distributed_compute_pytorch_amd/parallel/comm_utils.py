@@ -92,16 +92,31 @@ def unpack(flat: torch.Tensor, tensors: Sequence[torch.Tensor]):
     _copy_list(_flat_views(flat, tensors), list(tensors))
 
 
+def _word_key(t: torch.Tensor):
+    """The group a tensor is broadcast in: contiguous tensors of 4- / 8-byte
+    dtypes travel as float32 words (a broadcast moves bits, so BatchNorm's
+    fp32 running stats and int64 ``num_batches_tracked`` share ONE collective),
+    everything else by its own dtype."""
+    if t.is_contiguous() and t.element_size() in (4, 8) and t.dtype in (torch.float32, torch.int64, torch.float64,
+                                                                          torch.int32):
+        return torch.float32, t.device
+    return t.dtype, t.device
+
+
 class CoalescedBroadcaster:
     """Broadcast a fixed list of tensors from ``src`` with one collective per
-    (dtype, device) group; flat buffers are allocated once and reused (the
-    per-forward buffer broadcast is latency-bound)."""
+    word group (``_word_key``: ResNet's BatchNorm buffers are ONE broadcast per
+    forward); flat buffers are allocated once and reused (the per-forward
+    buffer broadcast is latency-bound)."""
 
     def __init__(self, tensors: Sequence[torch.Tensor], cap_bytes: int = 250 << 20):
         self.tensors = list(tensors)
         self.cap = cap_bytes
         self.plan = []  # list of (indices, flat)
-        for (dtype, device), idx in _group_by_dtype(self.tensors).items():
+        groups: "OrderedDict[tuple, List[int]]" = OrderedDict()
+        for i, t in enumerate(self.tensors):
+            groups.setdefault(_word_key(t), []).append(i)
+        for (dtype, device), idx in groups.items():
             chunk, size = [], 0
             for i in idx:
                 nb = self.tensors[i].numel() * self.tensors[i].element_size()
@@ -114,21 +129,29 @@ class CoalescedBroadcaster:
                 self.plan.append(self._mk(chunk, dtype, device))
 
     def _mk(self, idx, dtype, device):
-        n = sum(self.tensors[i].numel() for i in idx)
+        n = sum(self.tensors[i].numel() * self.tensors[i].element_size() for i in idx) // torch.empty(
+            0, dtype=dtype).element_size()
         return idx, torch.empty(n, dtype=dtype, device=device)
+
+    def _views(self, idx, flat):
+        """The group's tensors as views of ``flat``'s dtype (bit-preserving)."""
+        out = []
+        for i in idx:
+            t = self.tensors[i]
+            out.append(t if t.dtype == flat.dtype else t.reshape(-1).view(flat.dtype))
+        return out
 
     @torch.no_grad()
     def __call__(self, pg, src: int = 0):
         works = []
         for idx, flat in self.plan:
-            ts = [self.tensors[i] for i in idx]
             if pg.rank() == src:
-                pack(ts, flat)
+                pack(self._views(idx, flat), flat)
             works.append((pg.comm_for(flat).broadcast(flat, src), idx, flat))
         for w, idx, flat in works:
             w.wait()
             if pg.rank() != src:
-                unpack(flat, [self.tensors[i] for i in idx])
+                unpack(flat, self._views(idx, flat))
 
 
 def broadcast_coalesced(pg, tensors: Sequence[torch.Tensor], src: int = 0, cap_bytes: int = 250 << 20):

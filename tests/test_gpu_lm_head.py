@@ -79,14 +79,18 @@ def test_lm_head_cross_entropy_matches_fp32(cuda, ours, bias, M, K, V):
         torch.testing.assert_close(b.grad, br.grad, rtol=2e-2, atol=2e-2 * float(br.grad.abs().max()))
 
 
-def test_lm_head_accumulates_into_existing_grad(cuda, ours):
-    """A second backward adds its weight gradient into the fp32 .grad in the
-    wgrad's reduction pass (no separate add), rows past V untouched."""
+@pytest.mark.parametrize("wgrad", ["ring", "hipblaslt"])
+def test_lm_head_accumulates_into_existing_grad(cuda, ours, wgrad):
+    """A second backward adds its weight gradient into the fp32 .grad inside
+    the GEMM (our wgrad's reduction pass, or hipBLASLt's beta = 1) — no
+    separate add; rows past V are never written."""
+    from distributed_compute_pytorch_amd.ops import linear
     from distributed_compute_pytorch_amd.ops.linear import LinearWeightPrep
     from distributed_compute_pytorch_amd.ops.lm_head import lm_head_cross_entropy
 
     torch.manual_seed(1)
     V, K, M = 1003, 128, 512
+    linear._CHOICE[("head_wgrad", M, 1024, K)] = wgrad
     w = (torch.randn(V, K, device=cuda) * 0.05).requires_grad_()
     prep = LinearWeightPrep([(w,)], [1024])
     xs = [torch.randn(M, K, device=cuda, dtype=torch.bfloat16) for _ in range(2)]
@@ -102,6 +106,10 @@ def test_lm_head_accumulates_into_existing_grad(cuda, ours):
         prep.refresh()
         lm_head_cross_entropy(x, w, None, t).backward()
     torch.testing.assert_close(w.grad, gs[0] + gs[1], rtol=1e-5, atol=1e-6)
+    # and the first pass agrees with an fp32 reference of dW
+    xr, wr = xs[0].float(), _bf(w).float().requires_grad_()
+    F.cross_entropy(F.linear(xr, wr), ts[0]).backward()
+    torch.testing.assert_close(gs[0], wr.grad, rtol=2e-2, atol=2e-2 * float(wr.grad.abs().max()))
 
 
 def test_lm_head_second_backward_fails_loudly(cuda, ours):

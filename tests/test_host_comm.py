@@ -136,3 +136,29 @@ def _fingerprint(rank, world):
 
 def test_debug_fingerprint_catches_mismatch():
     run_world(_fingerprint, 2, backend=None, timeout=300)
+
+
+def _buffer_broadcast(rank, world):
+    import distributed_compute_pytorch_amd.distributed as dist
+    from distributed_compute_pytorch_amd.parallel.comm_utils import CoalescedBroadcaster
+
+    # BatchNorm-like buffers: fp32 stats + int64 counter share one word group;
+    # bf16 and a non-contiguous fp32 view ride along
+    mean = torch.full((5,), float(rank))
+    var = torch.arange(3, dtype=torch.float32) * (rank + 1)
+    nbt = torch.tensor(7 * rank + 2**40, dtype=torch.int64)
+    half = torch.full((4,), float(rank), dtype=torch.bfloat16)
+    base = torch.arange(12, dtype=torch.float32).reshape(3, 4) + rank
+    strided = base.t()
+    bc = CoalescedBroadcaster([mean, var, nbt, half, strided])
+    assert len(bc.plan) == 2, [p[1].dtype for p in bc.plan]  # fp32 words (incl. int64) + bf16
+    bc(dist.get_default_group(), src=1)
+    assert mean.tolist() == [1.0] * 5
+    assert var.tolist() == [0.0, 2.0, 4.0]
+    assert int(nbt) == 7 + 2**40
+    assert half.tolist() == [1.0] * 4
+    assert torch.equal(strided, (torch.arange(12, dtype=torch.float32).reshape(3, 4) + 1).t())
+
+
+def test_buffer_broadcast_one_collective_per_word_group():
+    run_world(_buffer_broadcast, 2)

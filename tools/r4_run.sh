@@ -17,5 +17,10 @@ for m in $MODELS; do
   timeout -k 10 400 python -u bench.py --model "$m" --steps "$STEPS" --warmup 8 $BENCH_ARGS > "$O/${TAG}_${m}.log" 2>&1 || {
     echo "[r4_run] bench $m failed"; tail -20 "$O/${TAG}_${m}.log"; exit 1; }
   grep '^{' "$O/${TAG}_${m}.log" | tail -1 | tee -a "$O/${TAG}_bench.jsonl" | cut -c1-300
+  # the per-shape GEMM autotune table (us per candidate) of that run
+  grep '^{' "$O/${TAG}_${m}.log" | tail -1 | python3 -c "
+import json, sys
+c = json.loads(sys.stdin.read())['config'].get('linear_gemm_us_by_candidate') or {}
+for k, v in sorted(c.items()): print('  ', k, v)"
 done
 echo "[r4_run] done"
