@@ -52,7 +52,6 @@ constexpr int kT = 256;
 // wgrad slab plan (gemm_tune wg_slots / wg_cap): workgroups the split over M
 // aims for, and the slab traffic allowed relative to the operand traffic
 int g_wg_slots = 512;
-int g_wg_fuse = 1;  // gemm_tune "wg_fuse": split-M wgrad reduced by its last workgroup per tile (0: separate pass)
 int g_wg_cap = 0;
 constexpr int kBK = 32;  // k per stage
 constexpr int kNS = 4;   // LDS ring stages
@@ -247,18 +246,6 @@ struct MultiGeo {
   int64_t M[4];
   const uint16_t* B[4];
   ConvGeo g[4];
-};
-
-// Final reduction of the split-M weight gradient fused into its kernel: every
-// workgroup stores its fp32 slab, then bumps its (tile, tap) counter; the
-// workgroup that arrives last sums the S slabs of that tile in slab order
-// (deterministic whatever the arrival order) into D and re-arms the counter.
-// cnt == nullptr: the separate slab_partial_kernel pass does it instead.
-struct WgFin {
-  float* D;        // [rows_out][ldo] fp32
-  int* cnt;        // one zeroed counter per (tile, tap), self-resetting
-  int acc;         // D += Σ slabs (existing gradient) instead of D = Σ slabs
-  int rows_out;    // rows of D (≤ N1: the rest of A's columns are padding)
 };
 
 // NT ring stages: BK=32 → 3 (two stages in flight), BK=64 → 2; either way
@@ -961,8 +948,7 @@ __global__ void __launch_bounds__(kT, 2) gemm_wgrad_kernel(const uint16_t* __res
                                                         float* __restrict__ ws, int64_t M, int N1, int N2,
                                                         int64_t chunk, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int relu, int tiles_j,
-                                                        ConvGeo geo, int ntiles, int ntaps, int order, int ldo,
-                                                        WgFin fin) {
+                                                        ConvGeo geo, int ntiles, int ntaps, int order, int ldo) {
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
   // BK m-rows per stage: 64 on a 2-deep ring (half the barriers per MFMA) or
   // 32 on the 4-deep ring; both ≤ 64 KB of LDS (2 blocks per CU)
@@ -1217,24 +1203,6 @@ __global__ void __launch_bounds__(kT, 2) gemm_wgrad_kernel(const uint16_t* __res
     }
   }
   // slab `by` holds D in its final [N1][taps][N2] layout (row stride ldo = taps * N2)
-  const int S = static_cast<int>(gridDim.x) / (ntiles * ntaps);
-  if (fin.cnt != nullptr && S == 1) {  // the only slab: straight into D
-    float* out = fin.D + static_cast<int64_t>(bz) * N2;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = i0 + wi * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-          const int col = j0 + wj * (BN / 2) + j * 16 + (lane & 15);
-          if ((BMODE != 2 || col < ldo) && row < fin.rows_out) {
-            float* o = out + static_cast<int64_t>(row) * ldo + col;
-            *o = fin.acc ? *o + acc[i][j][r] : acc[i][j][r];
-          }
-        }
-    return;
-  }
   float* out = ws + static_cast<int64_t>(by) * N1 * ldo + static_cast<int64_t>(bz) * N2;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -1246,44 +1214,6 @@ __global__ void __launch_bounds__(kT, 2) gemm_wgrad_kernel(const uint16_t* __res
         const int col = j0 + wj * (BN / 2) + j * 16 + (lane & 15);
         if (BMODE != 2 || col < ldo) out[static_cast<int64_t>(row) * ldo + col] = acc[i][j][r];
       }
-  if (fin.cnt == nullptr) return;
-  // publish this slab, count it; the last of the tile's S workgroups reduces
-  __shared__ int is_last;
-  __threadfence();
-  __syncthreads();
-  const int ci = bx * ntaps + bz;
-  if (t == 0) is_last = atomicAdd(fin.cnt + ci, 1) == S - 1;
-  __syncthreads();
-  if (!is_last) return;
-  __threadfence();
-  // the tile's BM x BN block (columns bz*N2 + j0 …, clipped to ldo / rows_out),
-  // 4 floats per thread-step, slabs summed in order 0 … S-1
-  const int cols = BN / 4;
-  for (int e = t; e < BM * cols; e += kT) {
-    const int row = i0 + e / cols;
-    const int col = bz * N2 + j0 + (e % cols) * 4;
-    if (row >= fin.rows_out || (BMODE == 2 && col - bz * N2 >= ldo)) continue;
-    const int64_t o = static_cast<int64_t>(row) * ldo + col;
-    const int64_t slab = static_cast<int64_t>(N1) * ldo;
-    float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int z = 0; z < S; ++z) {
-      const float4 v = *reinterpret_cast<const float4*>(ws + z * slab + o);
-      sum.x += v.x;
-      sum.y += v.y;
-      sum.z += v.z;
-      sum.w += v.w;
-    }
-    float4* d = reinterpret_cast<float4*>(fin.D + o);
-    if (fin.acc) {
-      const float4 a = *d;
-      sum.x += a.x;
-      sum.y += a.y;
-      sum.z += a.z;
-      sum.w += a.w;
-    }
-    *d = sum;
-  }
-  if (t == 0) fin.cnt[ci] = 0;  // re-armed for the next launch (stream order)
 }
 
 // Slab reduction, two levels so ~S/16 × more loads are in flight than a
@@ -1935,7 +1865,6 @@ void gemm_tune(const char* key, int value) {
   if (k == "big_pipe") g_big_pipe = value;
   if (k == "wg_slots") g_wg_slots = value < 64 ? 64 : value;
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
-  if (k == "wg_fuse") g_wg_fuse = value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
   if (k.rfind("pp_", 0) == 0) gemm_pp_tune(key, value);
 }
@@ -1946,7 +1875,6 @@ int gemm_tune_get(const char* key) {
   if (k == "big_pipe") return g_big_pipe;
   if (k == "wg_slots") return g_wg_slots;
   if (k == "wg_cap") return g_wg_cap;
-  if (k == "wg_fuse") return g_wg_fuse;
   if (k == "reserve_cus") return g_reserve_cus;
   if (k.rfind("pp_", 0) == 0) return gemm_pp_tune_get(key);
   return -1;
@@ -2482,25 +2410,6 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
 namespace {
 void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc = false, int64_t out4 = -1);
 
-// per-device (tile, tap) counters of the fused slab reduction: allocated and
-// zeroed on first use (not while a graph is being captured: the launch then
-// takes the separate reduction pass), re-armed by the kernels themselves
-constexpr int kWgCounters = 1 << 16;
-int* wgrad_counters(hipStream_t s) {
-  static int* cnt[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (cnt[dev] == nullptr) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
-    int* p = nullptr;
-    if (hipMalloc(&p, kWgCounters * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, kWgCounters * sizeof(int)) != hipSuccess) return nullptr;
-    cnt[dev] = p;
-  }
-  return cnt[dev];
-}
-
 template <bool GATHER>
 void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
                   const float* shift, bool relu, float* ws, int taps, const ConvGeo& geo, hipStream_t s,
@@ -2509,25 +2418,18 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   const int ldo = taps * N2;
-  // fused final reduction (WgFin) when counters are available for the grid
-  auto mkfin = [&](int tiles_taps) {
-    WgFin f{D, nullptr, acc ? 1 : 0, rows_out >= 0 ? rows_out : N1};
-    if (g_wg_fuse && tiles_taps <= kWgCounters) f.cnt = wgrad_counters(s);
-    return f;
-  };
   if constexpr (GATHER) {
     if (wgrad_mtap(N2, taps)) {
       const WgradPlan p = wgrad_plan_for(M, N1, N2, taps);
       const int tj = (ldo + 127) / 128;
       const dim3 grid(p.tiles * p.S);
-      const WgFin fin = mkfin(p.tiles);
       if (p.bm == 128)
         hipLaunchKernelGGL((gemm_wgrad_kernel<128, 128, false, true, 64, 0, 2>), grid, dim3(kT), 0, s, a, b, ws, M,
-                           N1, N2, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, ldo, fin);
+                           N1, N2, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, ldo);
       else
         hipLaunchKernelGGL((gemm_wgrad_kernel<64, 128, false, true, 64, 0, 2>), grid, dim3(kT), 0, s, a, b, ws, M, N1,
-                           N2, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, ldo, fin);
-      if (fin.cnt == nullptr) slab_reduce(ws, D, static_cast<int64_t>(N1) * ldo / 4, p.S, s, acc);
+                           N2, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, ldo);
+      slab_reduce(ws, D, static_cast<int64_t>(N1) * ldo / 4, p.S, s, acc);
       return;
     }
   }
@@ -2535,13 +2437,12 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   const dim3 grid(p.tiles * p.S * taps);
   const bool pro = scale != nullptr;
   const int tj = N2 / p.bn;
-  const WgFin fin = mkfin(p.tiles * taps);
   // ring: BK = 64, 2 stages (64 KB, 2 workgroups per CU) — also for the
   // BN-prologue wgrad (+0.2 %, profiles/r2_ab_wgrad_pro_bk.jsonl); the 32-deep
   // 2- and 4-stage rings measured slower everywhere (NOTES §19)
 #define DK_GWG(BM_, BN_, P)                                                                                     \
   hipLaunchKernelGGL((gemm_wgrad_kernel<BM_, BN_, P, GATHER, 64>), grid, dim3(kT), 0, s, a, b, ws, M, N1, N2,     \
-                     p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo, fin)
+                     p.chunk, scale, shift, relu ? 1 : 0, tj, geo, p.tiles, taps, order, ldo)
 #define DK_GWG2(BM_, BN_)                      \
   do {                                          \
     if constexpr (!GATHER) {                    \
@@ -2558,9 +2459,8 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
   else DK_GWG2(64, 64);
 #undef DK_GWG2
 #undef DK_GWG
-  if (fin.cnt == nullptr)
-    slab_reduce(ws, D, static_cast<int64_t>(N1) * taps * N2 / 4, p.S, s, acc,
-                rows_out >= 0 ? static_cast<int64_t>(rows_out) * taps * N2 / 4 : -1);
+  slab_reduce(ws, D, static_cast<int64_t>(N1) * taps * N2 / 4, p.S, s, acc,
+              rows_out >= 0 ? static_cast<int64_t>(rows_out) * taps * N2 / 4 : -1);
 }
 }  // namespace
 
@@ -2583,12 +2483,10 @@ void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int
   auto b = static_cast<const uint16_t*>(xp);
   if (p.bm == 128)
     hipLaunchKernelGGL((gemm_wgrad_kernel<128, 128, false, true, 64, 0, 1>), grid, dim3(kT), 0, s, a, b, ws, M, Cout,
-                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, kStemWgradCols,
-                       WgFin{});
+                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, kStemWgradCols);
   else
     hipLaunchKernelGGL((gemm_wgrad_kernel<64, 128, false, true, 64, 0, 1>), grid, dim3(kT), 0, s, a, b, ws, M, Cout,
-                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, kStemWgradCols,
-                       WgFin{});
+                       kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, kStemWgradCols);
   slab_reduce(ws, D, static_cast<int64_t>(Cout) * kStemWgradCols / 4, p.S, s, false);
 }
 
