@@ -388,9 +388,10 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
         float g = dp[r];
         if (DROP) {
           if ((r & 3) == 0) hs = drop_hash(kbh, qi, key);  // key ≡ 0 mod 4: one hash for keys key … key + 3
-          g = drop_keep(hs, r & 3, thr) ? g * inv_keep : 0.f;
+          g = drop_keep(hs, r & 3, thr) ? g : 0.f;
         }
-        s[r] = p * (g - dlt);  // dSᵀ (without the softmax scale)
+        // dSᵀ (without the softmax scale); the keep scale rides in the fma
+        s[r] = p * (DROP ? fmaf(g, inv_keep, -dlt) : g - dlt);
       }
 #pragma unroll
       for (int sg = 0; sg < 2; ++sg) {
@@ -523,11 +524,12 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
             float gg = dp[r], pk = p;
             if (DROP) {
               const bool kp = drop_keep(hrow[e], key & 3, thr);
-              gg = kp ? gg * inv_keep : 0.f;
-              pk = kp ? p * inv_keep : 0.f;
+              gg = kp ? gg : 0.f;
+              pk = kp ? p : 0.f;  // the keep scale goes on dV at the end
             }
             pv[4 * gg2 + e] = pk;
-            dsv[4 * gg2 + e] = p * (gg - dv4[e]);  // dS (without the softmax scale)
+            // dS (without the softmax scale); the keep scale rides in the fma
+            dsv[4 * gg2 + e] = p * (DROP ? fmaf(gg, inv_keep, -dv4[e]) : gg - dv4[e]);
           }
         }
         const bf16x8 pf = __builtin_bit_cast(
@@ -546,6 +548,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
     uint16_t* DK = static_cast<uint16_t*>(dk.ptr) + b * dk.sb + hd * kD + static_cast<int64_t>(key) * dk.st;
     uint16_t* DV = static_cast<uint16_t*>(dv.ptr) + b * dv.sb + hd * kD + static_cast<int64_t>(key) * dv.st;
     const float sc = P.scale;
+    const float vk = DROP ? inv_keep : 1.f;
 #pragma unroll
     for (int dh = 0; dh < 2; ++dh)
 #pragma unroll
@@ -553,8 +556,8 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
         const int d0 = 32 * dh + 8 * g + 4 * hh;
         *reinterpret_cast<uint2*>(DK + d0) = make_uint2(pack2(dka[dh][4 * g] * sc, dka[dh][4 * g + 1] * sc),
                                                         pack2(dka[dh][4 * g + 2] * sc, dka[dh][4 * g + 3] * sc));
-        *reinterpret_cast<uint2*>(DV + d0) = make_uint2(pack2(dva[dh][4 * g], dva[dh][4 * g + 1]),
-                                                        pack2(dva[dh][4 * g + 2], dva[dh][4 * g + 3]));
+        *reinterpret_cast<uint2*>(DV + d0) = make_uint2(pack2(dva[dh][4 * g] * vk, dva[dh][4 * g + 1] * vk),
+                                                        pack2(dva[dh][4 * g + 2] * vk, dva[dh][4 * g + 3] * vk));
       }
   }
 }

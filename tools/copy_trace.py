@@ -20,6 +20,7 @@ from distributed_compute_pytorch_amd.distributed.launch import free_port  # noqa
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="bert")
+    ap.add_argument("--min-us", type=float, default=4.0, help="GPU time per call below which a copy is not listed")
     a = ap.parse_args()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
     dcp.distributed.init_process_group("rccl", device_id=0)
@@ -42,10 +43,10 @@ def main():
     tab = prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=25, max_name_column_width=40,
                                                       max_src_column_width=140)
     print(tab)
-    print("--- ATen data-movement ops by parent-op chain (GPU time > 4 us per call) ---")
+    print(f"--- ATen data-movement ops by parent-op chain (GPU time > {a.min_us} us per call) ---")
     agg = {}
     for ev in prof.events():
-        if ev.name in names and ev.device_time_total > 4.0:
+        if ev.name in names and ev.device_time_total > a.min_us:
             chain, p = [], ev.cpu_parent
             while p is not None and len(chain) < 5:
                 chain.append(p.name)
