@@ -3,6 +3,7 @@ SQLite database or kernel-trace CSV), optionally with the grid size so that
 one kernel's different shapes separate.
 
     python tools/kernel_stats.py <prof_results.db | kernel_trace.csv> [--top 30] [--grid]
+    python tools/kernel_stats.py <db> --families --steps N   # GPU us per step per kernel family
 """
 import argparse
 import csv
@@ -46,7 +47,19 @@ def main():
     ap.add_argument("path")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--grid", action="store_true")
+    ap.add_argument("--families", action="store_true", help="group by kernel name without template arguments")
+    ap.add_argument("--steps", type=int, default=1, help="divide family totals by this many steps")
     a = ap.parse_args()
+    if a.families:
+        fam = defaultdict(float)
+        for n, d in rows(a.path, False):
+            base = n.split("<")[0].split("::")[-1].strip()
+            fam[base] += d
+        tot = sum(fam.values())
+        print(f"# GPU time per step per kernel family, us (share); {tot / a.steps / 1e3:.1f} us per step")
+        for n, t in sorted(fam.items(), key=lambda kv: -kv[1])[: a.top]:
+            print(f"  {t / a.steps / 1e3:9.1f}  {100 * t / tot:4.1f}%  {n[:60]}")
+        return
     agg = defaultdict(lambda: [0, 0])
     for n, d in rows(a.path, a.grid):
         agg[n][0] += 1
