@@ -146,6 +146,34 @@ __device__ __forceinline__ bool drop_keep(uint32_t hsh, int e, uint32_t thr) {
 __device__ __forceinline__ uint32_t drop_thr(float p) { return static_cast<uint32_t>(p * 256.f + 0.5f); }
 __device__ __forceinline__ float drop_scale(uint32_t thr) { return 256.f / static_cast<float>(256u - thr); }
 
+// (batch-head, tile) of this workgroup. Causal: tiles carry unequal work
+// (query tile t of the forward / dQ sees t + 1 key tiles; key tile t of dK/dV
+// is seen by nt - t query tiles). Workgroups are dispatched breadth-first, so
+// CU c receives launch positions c, c + 256, c + 512, …; with the work items
+// sorted heaviest first, odd rounds of 256 take them in reverse (serpentine)
+// so every CU's set sums to about the mean instead of heavy + heavy + medium.
+// heavy_last: the heaviest tile is the last one (forward, dQ) or tile 0 (dK/dV).
+__device__ __forceinline__ void attn_item(bool causal, bool heavy_last, int& bh, int& tile) {
+  const int nbh = static_cast<int>(gridDim.x), nt = static_cast<int>(gridDim.y);
+  if (!causal) {
+    bh = static_cast<int>(blockIdx.x);
+    tile = static_cast<int>(blockIdx.y);
+    return;
+  }
+  const int L = static_cast<int>(blockIdx.y) * nbh + static_cast<int>(blockIdx.x);
+  const int G = nbh * nt;
+  constexpr int C = 256;
+  const int r = L / C, pos = L % C;
+  int I = L;
+  if (r & 1) {
+    const int end = min(G, (r + 1) * C);  // a partial last round reverses within itself
+    I = end - 1 - pos;
+  }
+  bh = I % nbh;
+  const int rank = I / nbh;  // 0 = heaviest
+  tile = heavy_last ? nt - 1 - rank : rank;
+}
+
 struct Ptrs {
   const uint16_t* p;
   int64_t st;
@@ -162,11 +190,10 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hh = lane >> 5;
-  // grid (B*H, tiles): heads on x, so consecutive workgroups (→ consecutive XCDs) carry
-  // every tile size; with a causal mask the heaviest query tiles launch first
-  const int bh = blockIdx.x, b = bh / P.H, hd = bh % P.H;
-  const int tile = CAUSAL ? static_cast<int>(gridDim.y) - 1 - static_cast<int>(blockIdx.y)
-                          : static_cast<int>(blockIdx.y);
+  // grid (B*H, tiles); causal: heaviest query tiles first, serpentine per CU round (attn_item)
+  int bh, tile;
+  attn_item(CAUSAL, true, bh, tile);
+  const int b = bh / P.H, hd = bh % P.H;
   const int T = P.T;
   const int qi = tile * 128 + wave * 32 + (lane & 31);  // this lane's query
   const bool qok = qi < T;
@@ -324,11 +351,10 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hh = lane >> 5;
-  // grid (B*H, tiles): heads on x, so consecutive workgroups (→ consecutive XCDs) carry
-  // every tile size; with a causal mask the heaviest query tiles launch first
-  const int bh = blockIdx.x, b = bh / P.H, hd = bh % P.H;
-  const int tile = CAUSAL ? static_cast<int>(gridDim.y) - 1 - static_cast<int>(blockIdx.y)
-                          : static_cast<int>(blockIdx.y);
+  // grid (B*H, tiles); causal: heaviest query tiles first, serpentine per CU round (attn_item)
+  int bh, tile;
+  attn_item(CAUSAL, true, bh, tile);
+  const int b = bh / P.H, hd = bh % P.H;
   const int T = P.T;
   const int qi = tile * 128 + wave * 32 + (lane & 31);
   const bool qok = qi < T;
@@ -428,9 +454,10 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hh = lane >> 5;
-  // grid (B*H, key tiles): heads on x (XCD balance); key tile 0 is the heaviest (causal)
-  const int bh = blockIdx.x, b = bh / P.H, hd = bh % P.H;
-  const int tile = static_cast<int>(blockIdx.y);
+  // grid (B*H, key tiles); causal: key tile 0 is the heaviest, serpentine order (attn_item)
+  int bh, tile;
+  attn_item(CAUSAL, false, bh, tile);
+  const int b = bh / P.H, hd = bh % P.H;
   const int T = P.T;
   const int kb0 = tile * 128;
   const int key = kb0 + wave * 32 + (lane & 31);  // this lane's key
