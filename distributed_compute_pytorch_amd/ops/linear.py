@@ -700,6 +700,9 @@ class _MLPFn(torch.autograd.Function):
         c1 = _CHOICE.get(("fwd_gelu", x2.shape[0], w1_16.shape[1], w1_16.shape[0]), _DEFAULT_OURS)
         if c1 == "pp" and _pp_ok(x2.shape[0], w1_16.shape[0], w1_16.shape[1]):
             y1, h = _C.gemm_pp(x, w1_16, b1_32, mode)
+        elif c1 == "hipblaslt":  # (the node's gain is its backward: any forward kernel will do)
+            h = F.linear(x, w1_16, _lb(b1))
+            y1 = _C.gelu_fwd(h, tanh)
         else:
             y1, h = _C.linear_fwd(x, w1_16, b1_32, mode)
         y1_2 = y1.reshape(-1, y1.shape[-1])
@@ -743,27 +746,38 @@ class _MLPFn(torch.autograd.Function):
 
 
 def _mlp_prefers_ours(x, w1_16, b1, b1_16, w2_16, w2t, tanh) -> bool:
-    """The fused MLP node runs fc on our kernel (pp or ring, with the GELU
-    epilogue) and proj's data gradient on the ring's GELU-backward epilogue:
-    take it where the per-shape picks are ours for fc's forward and the ring
-    for proj's plain data gradient (where pp or hipBLASLt wins that GEMM, the
-    unfused path runs it there plus the separate GELU-backward pass)."""
+    """Whether the MLP runs as the fused node (:class:`_MLPFn`). The node's
+    gain is in its backward: proj's data gradient with the GELU backward and
+    fc's bias-gradient sums in the ring GEMM's epilogue (``linear_dgrad_gelu``)
+    instead of the fastest plain data-gradient GEMM (pp / ring / hipBLASLt)
+    plus the separate GELU-backward pass over gy and h. Both are timed
+    (``("mlp_bwd", M, N2, N1)``: "ring" = fused, "hipblaslt" = unfused — the
+    names the autotune table already carries); its forward takes whichever
+    kernel the fc forward autotune picked."""
     M, K = x.numel() // x.shape[-1], x.shape[-1]
     N1, N2 = w1_16.shape[0], w2_16.shape[0]
-    key_f, key_d = ("fwd_gelu", M, K, N1), ("dgrad", M, N2, N1)
-    if not (key_f in _CHOICE and key_d in _CHOICE):
+    key_f, key_d, key_b = ("fwd_gelu", M, K, N1), ("dgrad", M, N2, N1), ("mlp_bwd", M, N2, N1)
+    if key_b not in _CHOICE:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return True
         mode = 1 if tanh else 2
         with torch.no_grad():
             x2 = x.detach().reshape(M, K).to(torch.bfloat16)
-            _pick(key_f, _fwd_cands(x2, w1_16, b1_16, _bias32(b1), mode))
-            # a private generator: the stand-in gradient must not move the global
-            # RNG stream that dropout / init draw from
+            if key_f not in _CHOICE:
+                _pick(key_f, _fwd_cands(x2, w1_16, b1_16, _bias32(b1), mode))
+            # private generator: the stand-in gradient / pre-activation must not
+            # move the global RNG stream that dropout / init draw from
             gen = torch.Generator(device=x.device).manual_seed(0)
             g2 = torch.empty(M, N2, device=x.device, dtype=torch.bfloat16).normal_(generator=gen)
-            _pick(key_d, _dgrad_cands(g2, w2_16, w2t))
-    return _CHOICE[key_f] != "hipblaslt" and _CHOICE[key_d] == "ring"
+            h = torch.empty(M, N1, device=x.device, dtype=torch.bfloat16).normal_(generator=gen)
+            dc = _dgrad_cands(g2, w2_16, w2t)
+            best = _pick(key_d, dc)
+
+            def unfused():
+                return _C.gelu_bwd(dc[best](), h, tanh, True)
+
+            _pick(key_b, {"ring": lambda: _C.linear_dgrad_gelu(g2, w2t, h, tanh), "hipblaslt": unfused})
+    return _CHOICE[key_b] == "ring"
 
 
 def fused_mlp_gelu(x: torch.Tensor, fc: "FusedLinear", proj: "FusedLinear", approximate: str = "none"):
@@ -780,9 +794,8 @@ def fused_mlp_gelu(x: torch.Tensor, fc: "FusedLinear", proj: "FusedLinear", appr
         w1_16, w1t = fc._w16_pair()
         w2_16, w2t = proj._w16_pair()
         b1_16 = fc._bf16(fc.bias, "_b16_cache")
-        # the fused node runs both its GEMMs on our kernel: take it only where
-        # the per-shape autotune prefers our kernel for both (at BERT's 16,384
-        # rows hipBLASLt wins them and the unfused path measured 1.7 % faster)
+        # the fused node's backward (dgrad + GELU backward in one ring GEMM)
+        # against the fastest plain dgrad + the separate GELU pass, timed
         ok = _mlp_prefers_ours(x, w1_16, fc.bias, b1_16, w2_16, w2t, approximate == "tanh")
     if not ok:
         return proj(fc.forward_gelu(x, approximate) if isinstance(fc, FusedLinear) else

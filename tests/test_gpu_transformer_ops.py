@@ -555,7 +555,7 @@ def test_linear_dgrad_gelu_matches_fp32(cuda, tanh, rows, n1, n2):
     torch.testing.assert_close(acc, 1 + gh.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("ours", ["pp", "ring"])
+@pytest.mark.parametrize("ours", ["pp", "ring", "blasfwd"])
 @pytest.mark.parametrize("approx", ["tanh", "none"])
 def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch, ours):
     """ops.linear.fused_mlp_gelu (one node: GELU forward in fc's epilogue,
@@ -567,7 +567,10 @@ def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch, ours):
 
     monkeypatch.setattr(lin, "_AUTOTUNE", False)
     monkeypatch.setattr(lin, "_CHOICE", {})
-    monkeypatch.setattr(lin, "_DEFAULT_OURS", ours)
+    monkeypatch.setattr(lin, "_DEFAULT_OURS", "ring" if ours == "blasfwd" else ours)
+    if ours == "blasfwd":  # the fused node with fc's forward on hipBLASLt + the GELU kernel
+        lin._CHOICE[("fwd_gelu", 1024, 256, 1024)] = "hipblaslt"
+        lin._CHOICE[("mlp_bwd", 1024, 256, 1024)] = "ring"
 
     torch.manual_seed(0)
     fc, proj = FusedLinear(256, 1024).to(cuda), FusedLinear(1024, 256).to(cuda)
@@ -577,6 +580,7 @@ def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch, ours):
     x = torch.randn(8, 128, 256, device=cuda).to(torch.bfloat16).float().requires_grad_()
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y = fused_mlp_gelu(x, fc, proj, approx)
+    assert "MLPFn" in type(y.grad_fn).__name__
     g = torch.randn_like(y, dtype=torch.float32)
     y.float().backward(g)
     ref = [t.detach().clone().requires_grad_() for t in (x, fc.weight, fc.bias, proj.weight, proj.bias)]
