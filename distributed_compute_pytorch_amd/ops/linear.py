@@ -774,7 +774,8 @@ def _mlp_prefers_ours(x, w1_16, b1, b1_16, w2_16, w2t, tanh) -> bool:
             best = _pick(key_d, dc)
 
             def unfused():
-                return _C.gelu_bwd(dc[best](), h, tanh, True)
+                gy = dc[best]()
+                return _C.gelu_bwd(gy[0] if isinstance(gy, (list, tuple)) else gy, h, tanh, True)
 
             _pick(key_b, {"ring": lambda: _C.linear_dgrad_gelu(g2, w2t, h, tanh), "hipblaslt": unfused})
     return _CHOICE[key_b] == "ring"
