@@ -108,6 +108,9 @@ def parse():
     ap.add_argument("--linear-path", choices=["ours", "ours-unfused-mlp", "aten-fwd", "aten"], default="ours",
                     help="transformer Linear forward / data-gradient GEMMs: ours (gemm_nt + fused epilogues), "
                          "aten-fwd (forward on hipBLASLt), aten (forward and dgrad on hipBLASLt)")
+    ap.add_argument("--res-prologue", type=int, default=0,
+                    help="ResNet identity block boundaries: BN3 + residual + ReLU as the next conv1's GEMM prologue "
+                         "(1; default 0 = separate apply pass, measured faster: ops/conv.py RES_PROLOGUE)")
     ap.add_argument("--gemm-tune", default=None,
                     help="k=v[,k=v] entries of the GEMM launcher tuning table (_C.gemm_tune, e.g. nt_big=4)")
     return ap.parse_args()
@@ -220,6 +223,10 @@ def main():
             k, v = kv.split("=")
             _C.gemm_tune(k.strip(), int(v))
             tune[k.strip()] = _C.gemm_tune_get(k.strip())
+    if a.res_prologue:
+        from distributed_compute_pytorch_amd.ops import conv as _conv_ops
+
+        _conv_ops.RES_PROLOGUE = True
     if a.linear_path != "ours":
         from distributed_compute_pytorch_amd.ops import linear as _lin
 
@@ -333,7 +340,8 @@ def main():
                 "backend": a.backend,
             }
             if a.model == "resnet50":
-                cfg.update(mfma_1x1_gemm=bool(a.gemm) and fused, image_size=224, channels_last=bool(a.channels_last))
+                cfg.update(mfma_1x1_gemm=bool(a.gemm) and fused, image_size=224, channels_last=bool(a.channels_last),
+                           res_prologue=bool(a.res_prologue) and fused)
             if a.emulate_world:
                 cfg["emulated_comm"] = {"world": a.emulate_world, "busbw_gbps": a.emulate_busbw,
                                         "channels": a.emulate_channels}

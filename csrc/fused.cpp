@@ -226,6 +226,46 @@ std::vector<at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, co
   return {y, st};
 }
 
+// Block boundary forward: y = relu(x*scale + shift + res) (x = the previous
+// block's conv3 output z3, scale / shift its BN3's folded coefficients, res
+// the residual) and z = conv1x1(y, w) in ONE GEMM launch whose A prologue
+// applies the BN; y and its ReLU mask bits (1 bit per element, the backward's
+// RESRED operand) are stored by the n-tile-0 workgroups. Returns
+// {z, Σ/Σ² of z (stats) or empty, y, bits}: y / bits as the unfused
+// bn_act_fwd would produce them (same fp32 expression, bit-identical).
+std::vector<at::Tensor> conv1x1_fwd_res(const at::Tensor& x, const at::Tensor& w, const at::Tensor& scale,
+                                        const at::Tensor& shift, const at::Tensor& res, bool stats) {
+  check_gemm_act(x, "conv1x1_fwd_res");
+  check_gemm_act(res, "conv1x1_fwd_res");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t K = x.size(1);
+  const int64_t M = x.numel() / K;
+  DK_CHECK(res.sizes() == x.sizes() && res.device() == x.device(), "conv1x1_fwd_res: residual must match x");
+  DK_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() % K == 0, "conv1x1_fwd_res: weight");
+  const int64_t N = w.numel() / K;
+  DK_CHECK(kern::gemm_nt_supported(M, N, K) && K % 64 == 0, "conv1x1_fwd_res: unsupported shape");
+  const float* sc = vec_or_null(scale, K, "conv1x1_fwd_res");
+  const float* sf = vec_or_null(shift, K, "conv1x1_fwd_res");
+  DK_CHECK(sc != nullptr && sf != nullptr, "conv1x1_fwd_res: scale and shift required");
+  at::Tensor z = x.dim() == 4 ? at::empty({x.size(0), N, x.size(2), x.size(3)},
+                                          x.options().memory_format(at::MemoryFormat::ChannelsLast))
+                              : at::empty({M, N}, x.options());
+  // y / bits rows padded to the kernel's tile height: its stores need no row guard
+  const int64_t bm = kern::gemm_nt_res_rows(M, static_cast<int>(N), static_cast<int>(K));
+  const int64_t Mp = (M + bm - 1) / bm * bm;
+  at::Tensor ybuf = at::empty({Mp * K}, x.options().memory_format(at::MemoryFormat::Contiguous));
+  at::Tensor bbuf = at::empty({Mp * K / 8}, x.options().dtype(at::kByte));
+  auto s = stream_of(x);
+  at::Tensor st = stats ? zeroed_floats(2 * N, x, s) : at::empty({0}, x.options().dtype(at::kFloat));
+  kern::gemm_nt_res_bf16(x.data_ptr(), w.data_ptr(), z.data_ptr(), M, static_cast<int>(N), static_cast<int>(K), sc,
+                         sf, stats ? st.data_ptr<float>() : nullptr, res.data_ptr(), ybuf.data_ptr(), bbuf.data_ptr(), s);
+  at::Tensor y = x.dim() == 4 ? ybuf.narrow(0, 0, M * K)
+                                    .view({x.size(0), x.size(2), x.size(3), K})
+                                    .permute({0, 3, 1, 2})
+                              : ybuf.narrow(0, 0, M * K).view({M, K});
+  return {z, st, y, bbuf.narrow(0, 0, M * K / 8)};
+}
+
 // Linear forward y = x·wᵀ + b on the MFMA GEMM (bias in the epilogue, before
 // the bf16 rounding), x bf16 [.., K] contiguous, w bf16 [N, K], b fp32 [N].
 // gelu = 0: returns {y}; 1 (tanh) / 2 (erf): returns {gelu(h), h} — h is the
@@ -1502,6 +1542,9 @@ void bind(pybind11::module& m) {
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("scale") = pybind11::none(),
         pybind11::arg("shift") = pybind11::none(), pybind11::arg("relu") = false, pybind11::arg("stats") = false);
   m.def("conv1x1_dgrad", &conv1x1_dgrad, pybind11::arg("gy"), pybind11::arg("wt"));
+  m.def("conv1x1_fwd_res", &conv1x1_fwd_res, "block boundary: conv1x1(relu(x*scale+shift+res), w) with y and its "
+        "ReLU mask stored by the GEMM's prologue", py::arg("x"), py::arg("w"), py::arg("scale"), py::arg("shift"),
+        py::arg("res"), py::arg("stats") = true);
   m.def("gemm_pp", &gemm_pp, "x·wᵀ (+bias) (+gelu) on the 8-wave ping-pong 256x256 MFMA GEMM", py::arg("x"),
         py::arg("w"), py::arg("bias") = py::none(), py::arg("gelu") = 0);
   m.def("linear_fwd", &linear_fwd, "Linear forward on the MFMA GEMM: bias (+ GELU tanh/erf) in the epilogue",

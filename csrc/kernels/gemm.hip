@@ -101,6 +101,45 @@ __device__ __forceinline__ bf16x8 bn_act_frag(bf16x8 v, const float (&sc)[8], co
   return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
 }
 
+// relu(x*sc + sf + r) on one 8 x bf16 fragment — a block boundary's BN3 +
+// residual add + ReLU (gemm_nt RES prologue; the same fp32 expression as
+// batchnorm.hip's bn_apply_kernel, so y is bit-identical) — and its ReLU mask
+typedef unsigned int res_u32x4_ __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8 bn_res_frag(bf16x8 v, res_u32x4_ r, const float (&sc)[8], const float (&sf)[8],
+                                              uint32_t& bits) {
+  uint4 u = __builtin_bit_cast(uint4, v);
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  const uint32_t q[4] = {r.x, r.y, r.z, r.w};
+  bits = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float a = fmaf(bf_lo(w[k]), sc[2 * k], sf[2 * k]);
+    float b = fmaf(bf_hi(w[k]), sc[2 * k + 1], sf[2 * k + 1]);
+    a += bf_lo(q[k]);
+    b += bf_hi(q[k]);
+    bits |= (a > 0.f ? 1u : 0u) << (2 * k);
+    bits |= (b > 0.f ? 1u : 0u) << (2 * k + 1);
+    w[k] = pack2(fmaxf(a, 0.f), fmaxf(b, 0.f));
+  }
+  return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
+}
+
+// Vector-memory ops the RES prologue issues itself (inline asm: exactly one
+// instruction each, so the stage waits can count them; the compiler neither
+// sees nor re-orders them — their results are tied to the counted wait).
+typedef unsigned int res_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ res_u32x4 res_load16(const uint16_t* p) {
+  res_u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+__device__ __forceinline__ void res_store16(uint16_t* p, res_u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v));
+}
+__device__ __forceinline__ void res_store8(uint8_t* p, uint32_t v) {
+  asm volatile("global_store_byte %0, %1, off" ::"v"(p), "v"(v));
+}
+
 // ---------------------------------------------------------------- NT ----
 // Stage image: [rows][32 k] bf16, 64-B rows (4 rows per 256-B bank row);
 // physical 16-B chunk pc of row r holds logical chunk pc ^ f(r). A fragment
@@ -207,6 +246,13 @@ struct BnRedArgs {
   // gelu(h) (tanh / erf form, from the bf16-rounded h the backward reads) to c2
   const float* bias;
   uint16_t* c2;
+  // RES prologue (the conv1 forward of a block boundary): A = z3 is applied
+  // as relu(z3*scale + shift + res) on its way into the MFMAs; the workgroups
+  // of n-tile 0 store that operand to yout (rows padded to the tile height)
+  // and its ReLU mask bits to ybits (bit k of byte (m*K + c)/8: channel c + k)
+  const uint16_t* res;
+  uint16_t* yout;
+  uint8_t* ybits;
 };
 
 // GELU of the Linear epilogues (same forms as gelu.hip: tanh through one exp)
@@ -292,7 +338,7 @@ constexpr int nt_threads() { return 64 * (BM / nt_wr<BM, BN>()) * nt_wn<BM, BN>(
 // instead of a separate region: NS - 2 stages stay in flight across every
 // barrier (counted vmcnt), where the default 2-stage BK = 64 ring drains its
 // DMA at each stage and relies on a second resident workgroup to hide it.
-template <int BM, int BN, bool PRO, int EPI, bool GATHER, int BK, int AMODE = 0, int NS = 0>
+template <int BM, int BN, bool PRO, int EPI, bool GATHER, int BK, int AMODE = 0, int NS = 0, bool RES = false>
 __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() <= 256 && NS == 0 && nt_wr<BM, BN>() == 64 ? 2 : 1)) gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                      uint16_t* __restrict__ C, int64_t M, int N, int K,
                                                      const float* __restrict__ scale,
@@ -300,6 +346,8 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
                                                      float* __restrict__ stats, int tiles_m, int tn, ConvGeo geo,
                                                      BnRedArgs bnr, MultiGeo mg = MultiGeo{}) {
   static_assert(!(PRO && GATHER), "padding taps must stay zero: no BN prologue on the gathered operand");
+  static_assert(!RES || (PRO && !GATHER && AMODE == 0 && NS == 0 && BK == 32),
+                "RES: the BN prologue's BK = 32 three-stage ring, plain A operand");
   constexpr bool STATS = EPI == 1;
   constexpr bool RED = EPI == 2;
   // EPI 3 = SCATTER2: the data gradient of a stride-2 1x1 convolution. Row m =
@@ -561,6 +609,26 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
     }
   }
 
+  // RES: this stage's (rcu) and the next stage's (rnx) residual fragments —
+  // the 8 k of row wm*WR + 16j + lane%16 this lane's A fragment covers — loaded
+  // one stage ahead by res_load16 (in the stage loop: before issue(), so the
+  // counted waits find exactly group q+1, the y / bit stores and an epilogue
+  // younger than them)
+  constexpr int YS = 2 * FM * (BK / 32);  // RES stores per wave per stage (y + bits)
+  const bool ystore = RES && n0 == 0 && wn == 0;
+  res_u32x4 rnx[RES ? FM : 1], rcu[RES ? FM : 1];
+  auto res_fetch = [&](int v, int kst) {
+    if constexpr (RES) {
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        int64_t row = static_cast<int64_t>(v / tn) * BM + wm * WR + j * 16 + (lane & 15);
+        row = row < M ? row : M - 1;
+        rnx[j] = res_load16(bnr.res + row * K + kst * BK + (lane >> 4) * 8);
+      }
+    }
+  };
+  if (RES && T > 0) res_fetch(wg, 0);
+
 #pragma unroll
   for (int q = 0; q < kNSnt - 1; ++q) issue();
 
@@ -620,7 +688,25 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
     // DMA of q+1 and the epilogue stores of a tile end at q-2 or q-1 (issued
     // after q's DMA) — counting them keeps the ring full across tile ends.
     // Stage q-d ended a tile iff kt == d-1 (KT ≥ 2 > kNSnt-2).
-    if (q + kNSnt - 2 < T) {
+    if constexpr (RES) {
+      // younger than stage q's residual loads (issued at stage q-1, just before
+      // the DMA of q+1): that DMA, this wave's y / bit stores of stage q-1 and
+      // the epilogue stores of a tile that ended at q-1 (kNSnt = 3)
+      if (q + kNSnt - 2 < T) {
+        const bool e1 = q >= 1 && kt == 0, s1 = q >= 1 && ystore;
+        if (!e1 && !s1) wait_vm<G>();
+        else if (!e1) wait_vm<G + YS>();
+        else if (!s1) wait_vm<G + FS>();
+        else wait_vm<G + YS + FS>();
+      } else {
+        wait_vm<0>();
+      }
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        asm volatile("" : "+v"(rnx[j]));  // the loads' results, after the wait
+        rcu[j] = rnx[j];
+      }
+    } else if (q + kNSnt - 2 < T) {
       int ends = 0;
 #pragma unroll
       for (int d = 1; d <= kNSnt - 1; ++d) ends += (q >= d && kt == d - 1) ? 1 : 0;
@@ -631,6 +717,12 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       wait_vm<0>();
     }
     barrier();  // stage q visible to all waves; all reads of slot (q-1)%kNSnt done
+    if constexpr (RES) {
+      if (q + 1 < T) {
+        if (kt + 1 == KT) res_fetch(cv + P, 0);
+        else res_fetch(cv, kt + 1);
+      }
+    }
     issue();
     const char* sA = lds + slot * STAGE;
     const char* sB = sA + SA;
@@ -656,8 +748,22 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
           sc[e] = pro[kk + e];
           sf[e] = pro[K + kk + e];
         }
+        if constexpr (RES) {
+          const int64_t rb = static_cast<int64_t>(cv / tn) * BM + wm * WR + (lane & 15);
 #pragma unroll
-        for (int j = 0; j < FM; ++j) xf[j] = bn_act_frag(xf[j], sc, sf, relu != 0);
+          for (int j = 0; j < FM; ++j) {
+            uint32_t mb;
+            xf[j] = bn_res_frag(xf[j], rcu[j], sc, sf, mb);
+            if (ystore) {  // rows padded to the tile height: every store in bounds
+              const int64_t o = (rb + j * 16) * K + kk;
+              res_store16(bnr.yout + o, __builtin_bit_cast(res_u32x4, xf[j]));
+              res_store8(bnr.ybits + (o >> 3), mb);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < FM; ++j) xf[j] = bn_act_frag(xf[j], sc, sf, relu != 0);
+        }
       }
 #pragma unroll
       for (int i = 0; i < FN; ++i)
@@ -1959,6 +2065,41 @@ void gemm_nt_launch_bm(const void* A, const void* B, void* C, int64_t M, int N, 
 #undef DK_GNT
 }
 
+// The conv1 forward of a block boundary with the previous block's BN3 +
+// residual + ReLU as its A prologue (RES): the BN-prologue configuration
+// (BK = 32, three-stage ring, coefficients in LDS) plus the residual operand in
+// registers and the y / mask stores of the n-tile-0 workgroups.
+template <int BM>
+void gemm_nt_res_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                        const float* shift, float* stats, const BnRedArgs& bnr, hipStream_t s) {
+  constexpr int BK = 32;
+  const int BN = N % 128 == 0 ? 128 : 64;
+  const int tiles_m = static_cast<int>((M + BM - 1) / BM);
+  const int tn = N / BN;
+  const int kRes = (BM == 128 ? 2 : 1) * grid_cus();
+  const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
+  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
+  if (P < tn) P = tn;
+  const int nw = (BM / 64) * (BN == 64 && BM == 256 ? 1 : 2);
+  const size_t lds = static_cast<size_t>(nt_stages<BK>()) * (BM + BN) * BK * 2 +
+                     static_cast<size_t>(nw) * 32 * (BN * 2 / (BM == 256 && BN == 64 ? 1 : 2)) +
+                     8 * static_cast<size_t>(K);
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  auto c = static_cast<uint16_t*>(C);
+#define DK_GNR(BN_, EPI_)                                                                                     \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN_, true, EPI_, false, BK, 0, 0, true>), dim3(P), dim3(64 * nw), lds, s, \
+                     a, b, c, M, N, K, scale, shift, 1, stats, tiles_m, tn, ConvGeo{}, bnr)
+  if (BN == 128) {
+    if (stats) DK_GNR(128, 1);
+    else DK_GNR(128, 0);
+  } else {
+    if (stats) DK_GNR(64, 1);
+    else DK_GNR(64, 0);
+  }
+#undef DK_GNR
+}
+
 // 256 x 256 tiles: 2 x 4 waves of 128 x 64, one workgroup per CU (persistent
 // beyond grid_cus() tiles), BKB-deep stages on an NSB-slot ring (BKB * NSB =
 // 128: 128 KB) with the C staging aliased into it. Used as BKB = 64 / NSB = 2
@@ -2039,6 +2180,21 @@ void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int
 void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                   const float* shift, bool relu, float* stats, hipStream_t s) {
   gemm_nt_launch<false>(A, B, C, M, N, K, scale, shift, relu, stats, ConvGeo{}, s);
+}
+
+int gemm_nt_res_rows(int64_t M, int N, int K) {
+  const int BN = N % 128 == 0 ? 128 : 64;
+  return nt_bm(M, N / BN, BN, true, K, false);
+}
+
+void gemm_nt_res_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                      const float* shift, float* stats, const void* res, void* yout, void* ybits, hipStream_t s) {
+  BnRedArgs r{};
+  r.res = static_cast<const uint16_t*>(res);
+  r.yout = static_cast<uint16_t*>(yout);
+  r.ybits = static_cast<uint8_t*>(ybits);
+  if (gemm_nt_res_rows(M, N, K) == 256) gemm_nt_res_launch<256>(A, B, C, M, N, K, scale, shift, stats, r, s);
+  else gemm_nt_res_launch<128>(A, B, C, M, N, K, scale, shift, stats, r, s);
 }
 
 namespace {

@@ -32,6 +32,14 @@ bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
 void gemm_nt_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                   const float* shift, bool relu, float* stats, hipStream_t s);
 
+// conv1 of a block boundary: C = relu(A*scale + shift + res) · Bᵀ (+ Σ, Σ² of C
+// into stats when given); the A operand as applied (yout, [tile-padded rows][K]
+// bf16) and its ReLU mask (ybits, 1 bit per element) are stored once.
+// gemm_nt_res_rows: the tile height yout's rows must be padded to.
+int gemm_nt_res_rows(int64_t M, int N, int K);
+void gemm_nt_res_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
+                      const float* shift, float* stats, const void* res, void* yout, void* ybits, hipStream_t s);
+
 // Linear forward on the same kernel: C[M,N] = A[M,K]·B[N,K]ᵀ + bias (fp32 [N],
 // added before the bf16 rounding). gelu = 1 (tanh) / 2 (erf): C holds h and
 // c2 [M,N] gets gelu(h) computed from the bf16 h (what the backward reads).

@@ -182,6 +182,14 @@ def bn_relu_conv1x1(x: torch.Tensor, bn, weight: torch.Tensor, stats: bool = Fal
 # downsample blocks: BN3's and the downsample BN's apply passes as one kernel
 # (g read once; +0.95 %, profiles/r2_ab_bn_apply2.jsonl)
 _APPLY2 = True
+# identity block boundaries: BN3 + residual + ReLU as the A prologue of the next
+# conv1 GEMM, which also stores y and its mask (gemm.hip RES) instead of a
+# separate apply pass whose output the GEMM then re-reads. Correct (bit-identical
+# y, test_gpu_fusions.py::test_res_prologue_matches_apply_pass) but measured
+# SLOWER: ResNet-50 38.7 vs 36.2 ms per step (profiles/r4_res_prologue_ab.jsonl) —
+# the prologue forces the BK = 32 BN-prologue ring on GEMMs that otherwise run
+# the pipelined BK = 64 one, which costs more than the pass it removes (NOTES §25)
+RES_PROLOGUE = False
 
 
 class _BNResActConv1x1Fn(torch.autograd.Function):
@@ -208,12 +216,22 @@ class _BNResActConv1x1Fn(torch.autograd.Function):
             y, mean, invstd, bits, mean2, invstd2 = _C.bn_resbn_act_fwd(
                 z3, gamma, beta, rm, rv, nbt, stats, x2, gamma2, beta2, rm2, rv2, nbt2, stats2, float(momentum),
                 float(eps), float(momentum2), float(eps2))
+            w, wt = _w2d(w_next)
+            z1, s1 = _C.conv1x1_fwd(y, w, None, None, False, True)
+        elif RES_PROLOGUE:
+            # BN3 + residual + ReLU applied in conv1's A prologue; y and its mask
+            # stored by the GEMM (no separate apply pass, no re-read of y)
+            mean, invstd, scale, shift = _C.bn_stats_coef(z3, gamma, beta, rm, rv, float(momentum), float(eps), nbt,
+                                                          stats)
+            w, wt = _w2d(w_next)
+            z1, s1, y, bits = _C.conv1x1_fwd_res(z3, w, scale, shift, _cl(residual), True)
+            mean2 = invstd2 = None
         else:
             y, mean, invstd, bits = _C.bn_act_fwd(z3, gamma, beta, rm, rv, residual, True, float(momentum),
                                                   float(eps), True, nbt, stats)
             mean2 = invstd2 = None
-        w, wt = _w2d(w_next)
-        z1, s1 = _C.conv1x1_fwd(y, w, None, None, False, True)
+            w, wt = _w2d(w_next)
+            z1, s1 = _C.conv1x1_fwd(y, w, None, None, False, True)
         ctx.save_for_backward(z3, gamma, mean, invstd, bits, y, wt, x2, gamma2, mean2, invstd2)
         ctx.wshape, ctx.wdtype = w_next.shape, w_next.dtype
         ctx.mark_non_differentiable(s1)

@@ -216,3 +216,51 @@ def test_resnet_step_chain_fusion_matches_unfused(cuda, monkeypatch):
     assert bool(torch.isfinite(g1).all())
     assert err < 4 * noise + 0.05, (err, noise)
     torch.testing.assert_close(b1, b2, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("C,Co,N,hw", [(256, 64, 4, 14), (512, 128, 3, 9), (1024, 256, 2, 7), (256, 64, 2, 56)])
+def test_res_prologue_matches_apply_pass(cuda, C, Co, N, hw):
+    """The identity block boundary with BN3 + residual + ReLU as conv1's GEMM
+    prologue (gemm.hip RES, ops/conv.py RES_PROLOGUE) against the separate
+    apply pass + plain GEMM: y and its ReLU mask bit-identical (same fp32
+    expression), z1 / sums / running statistics / every gradient matching.
+    Covers 64- and 128-column tiles, one and two N-tiles, 128- and 256-row
+    tiles and ragged row counts (M = N·hw²)."""
+    from distributed_compute_pytorch_amd.ops import conv as conv_ops
+    from distributed_compute_pytorch_amd.ops.batchnorm import BatchNormAct2d
+
+    torch.manual_seed(3)
+    cl = torch.channels_last
+    z3 = (torch.randn(N, C, hw, hw, device=cuda) * 1.5 + 0.2).to(torch.bfloat16).contiguous(memory_format=cl)
+    r = (torch.randn(N, C, hw, hw, device=cuda) * 0.8).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(Co, C, 1, 1, device=cuda) / C ** 0.5).contiguous(memory_format=cl)
+    gy = torch.randn(N, C, hw, hw, device=cuda).to(torch.bfloat16).contiguous(memory_format=cl)
+    gz = torch.randn(N, Co, hw, hw, device=cuda).to(torch.bfloat16).contiguous(memory_format=cl)
+    outs = {}
+    for on in (False, True):
+        conv_ops.RES_PROLOGUE = on
+        try:
+            bn = BatchNormAct2d(C, act=True, residual=True, fused=True).to(cuda)
+            with torch.no_grad():
+                bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+                bn.bias.copy_(torch.linspace(-0.5, 0.5, C))
+            za, ra = z3.clone().requires_grad_(True), r.clone().requires_grad_(True)
+            wa = w.clone().requires_grad_(True)
+            y, z1, s1 = conv_ops.bn_res_act_conv1x1(bn, za, _sums(z3), ra, wa)
+            torch.autograd.backward([y, z1], [gy, gz])
+            outs[on] = (y.detach(), z1.detach(), s1, bn.running_mean.clone(), bn.running_var.clone(), za.grad,
+                        ra.grad, wa.grad, bn.weight.grad, bn.bias.grad)
+        finally:
+            conv_ops.RES_PROLOGUE = False
+    a, b = outs[False], outs[True]
+    assert torch.equal(a[0], b[0])  # y: same expression, same rounding
+
+    def rel(x, y_):
+        return float((x.float() - y_.float()).norm() / y_.float().norm().clamp_min(1e-12))
+
+    assert rel(b[1], a[1]) < 1e-2  # z1: same operands, another k order (BK 32 vs 64)
+    torch.testing.assert_close(b[2], a[2], rtol=1e-2, atol=1e-1)
+    torch.testing.assert_close(b[3], a[3], rtol=0, atol=0)
+    torch.testing.assert_close(b[4], a[4], rtol=0, atol=0)
+    for i in range(5, 10):
+        assert rel(b[i], a[i]) < 1e-2, (i, rel(b[i], a[i]))
