@@ -9,8 +9,9 @@ O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "/tmp/${TAG}" -o run -- python3 "$R/bench.py" \
-  --steps "$STEPS" --warmup "$WARM" > "$O/${TAG}.log" 2>&1 || { tail -20 "$O/${TAG}.log"; exit 1; }
+  --steps "$STEPS" --warmup "$WARM" $BENCH_ARGS > "$O/${TAG}.log" 2>&1 || { tail -20 "$O/${TAG}.log"; exit 1; }
 python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}/run_results.db" --top 40 > "$O/${TAG}_stats.txt"
+python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}/run_results.db" --top 60 --grid > "$O/${TAG}_grid.txt"
 python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}/run_results.db" --families --steps $((STEPS + WARM)) --top 30 \
   > "$O/${TAG}_families.txt"
 cat "$O/${TAG}_families.txt"
