@@ -108,6 +108,8 @@ def parse():
     ap.add_argument("--linear-path", choices=["ours", "ours-unfused-mlp", "aten-fwd", "aten"], default="ours",
                     help="transformer Linear forward / data-gradient GEMMs: ours (gemm_nt + fused epilogues), "
                          "aten-fwd (forward on hipBLASLt), aten (forward and dgrad on hipBLASLt)")
+    ap.add_argument("--pro-max-cout", type=int, default=None,
+                    help="ResNet: BN2 + ReLU as conv3's GEMM prologue while Cout <= this (models/resnet.py PRO_MAX_COUT)")
     ap.add_argument("--res-prologue", type=int, default=0,
                     help="ResNet identity block boundaries: BN3 + residual + ReLU as the next conv1's GEMM prologue "
                          "(1; default 0 = separate apply pass, measured faster: ops/conv.py RES_PROLOGUE)")
@@ -223,6 +225,10 @@ def main():
             k, v = kv.split("=")
             _C.gemm_tune(k.strip(), int(v))
             tune[k.strip()] = _C.gemm_tune_get(k.strip())
+    if a.pro_max_cout is not None:
+        from distributed_compute_pytorch_amd.models import resnet as _resnet
+
+        _resnet.PRO_MAX_COUT = a.pro_max_cout
     if a.res_prologue:
         from distributed_compute_pytorch_amd.ops import conv as _conv_ops
 
@@ -342,6 +348,8 @@ def main():
             if a.model == "resnet50":
                 cfg.update(mfma_1x1_gemm=bool(a.gemm) and fused, image_size=224, channels_last=bool(a.channels_last),
                            res_prologue=bool(a.res_prologue) and fused)
+                if a.pro_max_cout is not None:
+                    cfg["pro_max_cout"] = a.pro_max_cout
             if a.emulate_world:
                 cfg["emulated_comm"] = {"world": a.emulate_world, "busbw_gbps": a.emulate_busbw,
                                         "channels": a.emulate_channels}
