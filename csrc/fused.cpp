@@ -1226,7 +1226,7 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
     dw = at::empty({D}, fopt);
     db = at::empty({D}, fopt);
   }
-  at::Tensor part = at::empty({static_cast<int64_t>(kern::ln_bwd_blocks(rows)) * 2 * D}, fopt);
+  at::Tensor part = at::empty({static_cast<int64_t>(kern::ln_bwd_blocks(rows, static_cast<int>(D))) * 2 * D}, fopt);
   const bool has_w = weight.has_value() && weight->defined();
   at::Tensor w = has_w ? weight->to(at::kFloat).contiguous() : at::Tensor();
   // grad_residual: the gradient of x from its other consumer (dual-output LN,

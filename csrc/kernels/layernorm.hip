@@ -71,6 +71,13 @@ __device__ __forceinline__ float wsum(float v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
+// sum over the LPR lanes that share a row (LPR = 64: the wave; 32: a half-wave)
+template <int LPR>
+__device__ __forceinline__ float rsum(float v) {
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
 
 // 8 consecutive fp32 affine values (or the identity when absent)
 __device__ __forceinline__ void ld_aff(const float* p, int c, float def, float (&o)[8]) {
@@ -90,20 +97,24 @@ __device__ __forceinline__ void ld_aff(const float* p, int c, float def, float (
 // bytes in flight of a row-at-a-time wave. XD: dtype of x (and dx), YD: dtype
 // of y (and dy) — x fp32 / y bf16 is the autocast residual-stream case: the
 // LayerNorm output feeds a bf16 GEMM directly, no separate cast pass.
-template <int XD, int YD, int VPL, int R>
+// LPR = lanes per row: 64 (a row per wave) or 32 (a row per half-wave, for D
+// whose 16-B vector count is an odd multiple of 32 — D = 768: 3 vectors on
+// every lane instead of 2 on half of them and 1 on the other half).
+template <int XD, int YD, int VPL, int R, int LPR = 64>
 __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, const float* __restrict__ w,
                                                     const float* __restrict__ b, void* __restrict__ y,
                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                     int64_t rows, int D, float eps) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * R;
+  const int lane = threadIdx.x & (LPR - 1);
+  const int sub = LPR == 64 ? 0 : (threadIdx.x >> 5) & 1;
+  const int64_t row0 = ((static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * (64 / LPR) + sub) * R;
   if (row0 >= rows) return;
   const int nv = D >> 3;
   float wv[VPL][8], bv[VPL][8];
   float v[R][VPL][8];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
-    const int vi = lane + j * 64;
+    const int vi = lane + j * LPR;
     if (vi < nv) {
 #pragma unroll
       for (int r = 0; r < R; ++r)
@@ -119,27 +130,27 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, 
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < VPL; ++j)
-      if (lane + j * 64 < nv)
+      if (lane + j * LPR < nv)
 #pragma unroll
         for (int k = 0; k < 8; ++k) s += v[r][j][k];
-    const float mean = wsum(s) / static_cast<float>(D);
+    const float mean = rsum<LPR>(s) / static_cast<float>(D);
     float q = 0.f;
 #pragma unroll
     for (int j = 0; j < VPL; ++j)
-      if (lane + j * 64 < nv)
+      if (lane + j * LPR < nv)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float d = v[r][j][k] - mean;
           q = fmaf(d, d, q);
         }
-    const float rstd = rsqrtf(wsum(q) / static_cast<float>(D) + eps);
+    const float rstd = rsqrtf(rsum<LPR>(q) / static_cast<float>(D) + eps);
     if (lane == 0) {
       mean_out[row] = mean;
       rstd_out[row] = rstd;
     }
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
-      const int vi = lane + j * 64;
+      const int vi = lane + j * LPR;
       if (vi < nv) {
         float o[8];
 #pragma unroll
@@ -153,30 +164,42 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 // partial[blk][0][D] += dy * xhat (dgamma), partial[blk][1][D] += dy (dbeta)
 // Each wave takes R rows at a time with all their loads in flight together.
-template <int XD, int YD, int VPL, int R>
-__global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy, const void* __restrict__ x,
+template <int XD, int YD, int VPL, int R, int LPR = 64>
+__global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(R == 1 && VPL <= 2 ? 4 : 1))) ln_bwd_kernel(const void* __restrict__ dy, const void* __restrict__ x,
                                                     const float* __restrict__ w, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, void* __restrict__ dx,
                                                     float* __restrict__ part, int64_t rows, int D,
                                                     int rows_per_blk, const void* __restrict__ gres,
                                                     const void* __restrict__ dy2) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kWaves][2][D]
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & (LPR - 1);
+  const int sub = LPR == 64 ? 0 : (threadIdx.x >> 5) & 1;  // half-wave (LPR = 32)
   const int wid = threadIdx.x >> 6;
   const int nv = D >> 3;
+  constexpr int RPW = 64 / LPR;  // rows a wave works on at once per r
+  // lean (R = 1): gamma re-read per row from L1 rather than held, gres loaded
+  // behind the reductions — under 128 VGPRs, 4 waves per SIMD instead of 2
+  constexpr bool kLean = R == 1 && LPR == 64;
   float accg[VPL][8], accb[VPL][8], wv[VPL][8];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) accg[j][k] = accb[j][k] = 0.f;
-    if (lane + j * 64 < nv) ld_aff(w, (lane + j * 64) * 8, 1.f, wv[j]);
+    if (!kLean && lane + j * LPR < nv) ld_aff(w, (lane + j * LPR) * 8, 1.f, wv[j]);
   }
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_blk;
   const int64_t r1 = min(rows, r0 + rows_per_blk);
-  for (int64_t rb = r0 + wid * R; rb < r1; rb += kWaves * R) {
+  for (int64_t rb = r0 + (wid * RPW + sub) * R; rb < r1; rb += kWaves * RPW * R) {
+    if (kLean) {
+      const float* wp = w;
+      asm volatile("" : "+s"(wp));  // keep the gamma loads inside the loop
+#pragma unroll
+      for (int j = 0; j < VPL; ++j)
+        if (lane + j * LPR < nv) ld_aff(wp, (lane + j * LPR) * 8, 1.f, wv[j]);
+    }
     // gres rows ride with the row's other loads (not behind its reductions)
     // while the registers allow: D <= 2048
-    constexpr bool kHoist = VPL <= 4;
+    constexpr bool kHoist = VPL <= 4 && !kLean;
     float dv[R][VPL][8], xh[R][VPL][8], gr[kHoist ? R : 1][kHoist ? VPL : 1][8], mu[R], rs[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -185,7 +208,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
       rs[r] = rstd[row];
 #pragma unroll
       for (int j = 0; j < VPL; ++j) {
-        const int vi = lane + j * 64;
+        const int vi = lane + j * LPR;
         if (vi < nv) {
           L8<YD>::ld(dy, row * D + vi * 8, dv[r][j]);
           if (dy2) {  // the output's second consumer (dual-output LN): dy += dy2
@@ -205,7 +228,7 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int j = 0; j < VPL; ++j) {
-        if (lane + j * 64 < nv) {
+        if (lane + j * LPR < nv) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             xh[r][j][k] = (xh[r][j][k] - mu[r]) * rs[r];
@@ -219,12 +242,12 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
           }
         }
       }
-      const float m1 = wsum(s1) / static_cast<float>(D);
-      const float m2 = wsum(s2) / static_cast<float>(D);
+      const float m1 = rsum<LPR>(s1) / static_cast<float>(D);
+      const float m2 = rsum<LPR>(s2) / static_cast<float>(D);
       if (!live) continue;
 #pragma unroll
       for (int j = 0; j < VPL; ++j) {
-        const int vi = lane + j * 64;
+        const int vi = lane + j * LPR;
         if (vi < nv) {
           float o[8];
 #pragma unroll
@@ -239,11 +262,21 @@ __global__ void __launch_bounds__(kT) ln_bwd_kernel(const void* __restrict__ dy,
       }
     }
   }
+  // half-waves hold the same columns for different rows: fold them first
+  if (LPR == 32) {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        accg[j][k] += __shfl_xor(accg[j][k], 32, 64);
+        accb[j][k] += __shfl_xor(accb[j][k], 32, 64);
+      }
+  }
   // reduce the 4 waves' column partials through LDS, one slab per workgroup
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
-    const int vi = lane + j * 64;
-    if (vi < nv) {
+    const int vi = lane + j * LPR;
+    if (vi < nv && sub == 0) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         smem[(wid * 2 + 0) * D + vi * 8 + k] = accg[j][k];
@@ -313,13 +346,18 @@ void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w,
                   float* rstd, int64_t rows, int D, float eps) {
 #define DK_LNF(V) \
   hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V, kRows>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps)
+#define DK_LNF_H(V)                                                                                        \
+  hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V, kRows, 32>), dim3((g.x + 1) / 2), dim3(kT), 0, s, x, w, b, y, mean, \
+                     rstd, rows, D, eps)
   switch (vpl) {
+    case 103: DK_LNF_H(3); break;
     case 1: DK_LNF(1); break;
     case 2: DK_LNF(2); break;
     case 4: DK_LNF(4); break;
     default: DK_LNF(8);
   }
 #undef DK_LNF
+#undef DK_LNF_H
 }
 
 template <int XD, int YD>
@@ -329,17 +367,32 @@ void bwd_dispatch(int vpl, dim3 g, size_t sm, hipStream_t s, const void* dy, con
 #define DK_LNB(V) \
   hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, kRows>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, \
                      rpb, gres, dy2)
+#define DK_LNB_H(V)                                                                                             \
+  hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, 1, 32>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, \
+                     D, rpb, gres, dy2)
+  if (vpl == -2) {
+    hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, 2, 1>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb,
+                       gres, dy2);
+    return;
+  }
   switch (vpl) {
+    case 103: DK_LNB_H(3); break;
     case 1: DK_LNB(1); break;
     case 2: DK_LNB(2); break;
     case 4: DK_LNB(4); break;
     default: DK_LNB(8);
   }
 #undef DK_LNB
+#undef DK_LNB_H
 }
 
+// 103: half-wave rows with 3 vectors per lane (nv = 96: D = 768). Forward
+// only — bf16 [16384, 768] 14.4 -> 12.5 us, fp32 -> bf16 [8192, 768] 9.1 ->
+// 8.7 us; the backward at 3 vectors per lane needs ~200 VGPRs and ran slower.
 inline int vpl_for(int D) {
   const int nv = D / 8;
+  static const bool full = std::getenv("DCP_LN_FULLWAVE") != nullptr;  // A/B switch
+  if (nv == 96 && !full) return 103;
   const int v = (nv + 63) / 64;
   return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : 8;
 }
@@ -354,9 +407,19 @@ namespace {
 // backward moved 1.5-2.3 TB/s). Each writes one [2][D] partial row; more than
 // 16 of them are first summed 64 at a time by ln_bwd_colsum_kernel (coalesced
 // rows, 16 loads in flight per lane) instead of column-strided by the finalize.
-int ln_bwd_grid(int64_t rows) {
+// lean backward (R = 1, 4 waves per SIMD): bf16 x with rows of 2 vectors per
+// lane. Measured (tools/kernel_bench.py): bf16 [16384, 768] 35.9 -> 29.0 us;
+// fp32 x [8192, 768] 21.4 -> 25.1 us (its rows are twice the bytes, R = 2's
+// bytes in flight win there), so fp32 x keeps R = 2.
+bool ln_bwd_lean(int D, int xdtype) {
+  static const bool off = std::getenv("DCP_LN_BWD_R2") != nullptr;  // A/B switch
+  const int v = vpl_for(D);
+  return !off && xdtype == LN_BF16 && (v == 2 || v == 103);
+}
+int ln_bwd_grid(int64_t rows, int D, int xdtype) {
   constexpr int64_t cap = 1024;
-  int64_t nb = (rows + 15) / 16;  // >= 16 rows (4 per wave) per workgroup
+  // >= 16 rows (4 per wave) per workgroup; lean: >= 8 (4 workgroups per CU)
+  int64_t nb = ln_bwd_lean(D, xdtype) ? (rows + 7) / 8 : (rows + 15) / 16;
   if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
   return static_cast<int>(nb);
@@ -364,8 +427,8 @@ int ln_bwd_grid(int64_t rows) {
 int ln_colsum_groups(int nblk) { return nblk > 16 ? (nblk + 63) / 64 : 0; }
 }  // namespace
 
-int ln_bwd_blocks(int64_t rows) {  // workspace rows: the partials + the colsum level
-  const int nb = ln_bwd_grid(rows);
+int ln_bwd_blocks(int64_t rows, int D) {  // workspace rows: the partials + the colsum level
+  const int nb = ln_bwd_grid(rows, D, LN_BF16);  // >= the fp32-x grid
   return nb + ln_colsum_groups(nb);
 }
 
@@ -381,10 +444,12 @@ void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const flo
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
                  const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
                  hipStream_t s, const void* gres, const void* dy2) {
-  const int nblk = ln_bwd_grid(rows);
+  const int nblk = ln_bwd_grid(rows, D, xdtype);
   const int rpb = static_cast<int>((rows + nblk - 1) / nblk);
   const size_t sm = sizeof(float) * kWaves * 2 * D;
-  const int vpl = vpl_for(D);
+  int vpl = vpl_for(D);
+  if (vpl == 103) vpl = 2;  // half-wave rows: forward only (measured slower backward)
+  if (ln_bwd_lean(D, xdtype)) vpl = -2;
   if (xdtype == LN_BF16)
     bwd_dispatch<LN_BF16, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2);
   else if (ydtype == LN_BF16)

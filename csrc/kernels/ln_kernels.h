@@ -12,11 +12,11 @@ namespace kern {
 enum LnDType : int { LN_F32 = 0, LN_BF16 = 1 };
 
 bool ln_supported(int D);
-int ln_bwd_blocks(int64_t rows);
+int ln_bwd_blocks(int64_t rows, int D);
 // xdtype: x / dx; ydtype: y / dy (fp32->bf16 supported; bf16 x implies bf16 y)
 void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const float* b, void* y, float* mean,
                 float* rstd, int64_t rows, int D, float eps, hipStream_t s);
-// part: workspace [ln_bwd_blocks(rows) * 2 * D] fp32; accum: dw / db += instead of =
+// part: workspace [ln_bwd_blocks(rows, D) * 2 * D] fp32; accum: dw / db += instead of =
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
                  const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
                  hipStream_t s, const void* gres = nullptr, const void* dy2 = nullptr);

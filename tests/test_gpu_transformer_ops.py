@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(4, 128, 768), (33, 1024), (7, 4096), (5, 3, 8), (1000, 512), (16, 1024, 768), (3001, 256)])
+@pytest.mark.parametrize("shape", [(4, 128, 768), (33, 1024), (7, 4096), (5, 3, 8), (1000, 512), (16, 1024, 768), (3001, 256), (5, 3, 768), (1037, 768)])
 @pytest.mark.parametrize("affine", [True, False])
 def test_layer_norm(cuda, dtype, shape, affine):
     from distributed_compute_pytorch_amd.ops import fused_layer_norm

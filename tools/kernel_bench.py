@@ -97,6 +97,14 @@ def main():
     ms = timeit(lambda: _C.layer_norm_bwd(dy, xf, lw, lb, mu, rs), a.iters)
     rec(f"layernorm bwd [{T},{D}]", ms, T * D * (2 + 4 + 4))
 
+    xb = torch.randn(2 * T, D, device=dev).to(bf)
+    ms = timeit(lambda: out.__setitem__("o", _C.layer_norm_fwd(xb, lw, lb, 1e-5, bf)), a.iters)
+    rec(f"layernorm fwd bf16 [{2 * T},{D}]", ms, 2 * T * D * (2 + 2))
+    yl, mu, rs = out["o"]
+    dyb = torch.randn(2 * T, D, device=dev).to(bf)
+    ms = timeit(lambda: _C.layer_norm_bwd(dyb, xb, lw, lb, mu, rs), a.iters)
+    rec(f"layernorm bwd bf16 [{2 * T},{D}]", ms, 2 * T * D * (2 + 2 + 2))
+
     logits = torch.randn(T, V, device=dev).to(bf)
     tgt = torch.randint(0, V, (T,), device=dev)
     out = {}
