@@ -30,6 +30,7 @@ kern::DType kdtype(at::ScalarType st) {
 // ---- device table cache --------------------------------------------------
 struct TableEntry {
   std::vector<int64_t> key;
+  uint64_t hash = 0;        // of key: the lookup compares this first
   at::Tensor dev;
   int n;
   int64_t nchunks;
@@ -39,7 +40,21 @@ struct TableEntry {
 
 std::mutex g_cache_mu;
 std::list<TableEntry> g_cache;  // MRU at front
-constexpr size_t kCacheCap = 32;
+// Large enough for every distinct table of a training step: a BERT step runs
+// ~60 multi-tensor launches (optimizer chunks, bucket packs); at 32 entries the
+// LRU thrashed on that cycle and every launch re-uploaded its table (~110
+// pinned H2D copies per step, 0.45 ms of copy kernels on the compute queue).
+constexpr size_t kCacheCap = 1024;
+
+uint64_t words_hash(const std::vector<int64_t>& w) {
+  uint64_t h = 1469598103934665603ull;
+  for (int64_t v : w) {
+    h ^= static_cast<uint64_t>(v);
+    h *= 1099511628211ull;
+    h ^= h >> 29;
+  }
+  return h;
+}
 // Evicted pinned upload buffers wait here until the copy that read them has
 // finished (raw hipMemcpyAsync: the torch host allocator does not track it).
 std::vector<std::pair<hipEvent_t, at::Tensor>> g_graveyard;
@@ -84,8 +99,9 @@ TableEntry get_table(const std::vector<const TensorList*>& lists) {
   const hipStream_t st = c10::hip::getCurrentHIPStream(dev.index()).stream();
   (void)hipStreamIsCapturing(st, &cap);
   const bool capturing = cap == hipStreamCaptureStatusActive;
+  const uint64_t h = words_hash(words);
   for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
-    if (it->key == words) {
+    if (it->hash == h && it->key == words) {
       // a captured kernel now reads this device table on every replay: it must
       // never be evicted (eviction frees it to the caching allocator, and a
       // later replay would read whatever reused the memory)
@@ -108,7 +124,7 @@ TableEntry get_table(const std::vector<const TensorList*>& lists) {
                              st) == hipSuccess,
               "table upload failed");
   }
-  TableEntry e{std::move(words), d, n, chunks, host, capturing};
+  TableEntry e{std::move(words), h, d, n, chunks, host, capturing};
   g_cache.push_front(std::move(e));
   // evict the least recently used non-persistent entry (never while capturing:
   // the deferred-free event would itself be captured)

@@ -257,8 +257,21 @@ def _fwd_cands(x2, w, b, b32, mode: int) -> dict:
 
 def _lb(b):
     """The bias as the bf16 ATen GEMMs take it, cast only where one runs (our
-    kernels read the fp32 bias in their epilogue)."""
-    return b if b is None or b.dtype == torch.bfloat16 else b.detach().to(torch.bfloat16)
+    kernels read the fp32 bias in their epilogue). A CUDA fp32 bias gets a
+    registered bf16 shadow that the fused Adam/AdamW step rewrites with the
+    update (as the weights' shadows): GPT-2's hipBLASLt MLP forward cast its
+    biases 48 times a step otherwise."""
+    if b is None or b.dtype == torch.bfloat16:
+        return b
+    if _SHADOWS and b.is_cuda and b.dtype == torch.float32 and not torch.cuda.is_current_stream_capturing():
+        from ..optim.fused import fresh_bf16_shadow, register_bf16_shadow
+
+        t = fresh_bf16_shadow(b)
+        if t is None:
+            t = b.detach().to(torch.bfloat16)
+            register_bf16_shadow(b, t)
+        return t
+    return b.detach().to(torch.bfloat16)
 
 
 def _bias32(bias: torch.Tensor) -> torch.Tensor:

@@ -15,6 +15,8 @@ for m in $MODELS; do
     --steps "$STEPS" --warmup 4 > "$O/${TAG}_$m.log" 2>&1 || { tail -20 "$O/${TAG}_$m.log"; exit 1; }
   python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}_$m/run_results.db" --top 40 > "$O/${TAG}_${m}_stats.txt" 2>&1 || {
     tail -5 "$O/${TAG}_${m}_stats.txt"; exit 1; }
+  python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}_$m/run_results.db" --families --steps $((STEPS + 4)) --top 30 \
+    > "$O/${TAG}_${m}_families.txt" 2>&1 || { tail -5 "$O/${TAG}_${m}_families.txt"; exit 1; }
   head -25 "$O/${TAG}_${m}_stats.txt"
 done
 echo "[tfm_prof] done"
