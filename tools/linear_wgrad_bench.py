@@ -17,7 +17,7 @@ import distributed_compute_pytorch_amd  # noqa: E402,F401
 from distributed_compute_pytorch_amd._ext import C as _C  # noqa: E402
 
 SHAPES = [  # (M, N1 = out features, N2 = in features)
-    (16384, 768, 768), (16384, 3072, 768), (16384, 768, 3072),
+    (16384, 768, 768), (16384, 2304, 768), (16384, 3072, 768), (16384, 768, 3072),
     (8192, 2304, 768), (8192, 768, 768), (8192, 3072, 768), (8192, 768, 3072),
 ]
 
@@ -44,7 +44,10 @@ def main():
         x = torch.randn(m, n2, device=dev).to(torch.bfloat16)
         flops = 2.0 * m * n1 * n2
         r = {"M": m, "N1": n1, "N2": n2}
+        acc = torch.zeros(n1, n2, device=dev)
         for name, fn in (("ours", lambda: _C.conv1x1_wgrad(g, x)),
+                         ("ours_acc", lambda: _C.conv1x1_wgrad(g, x, accumulate_into=acc)),
+                         ("addmm_fp32_acc", lambda: torch.addmm(acc, g.t(), x, out_dtype=torch.float32)),
                          ("mm_fp32out", lambda: torch.mm(g.t(), x, out_dtype=torch.float32)),
                          ("mm_bf16_cast", lambda: torch.mm(g.t(), x).float())):
             try:
