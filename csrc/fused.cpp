@@ -274,15 +274,21 @@ std::vector<at::Tensor> conv1x1_fwd_res(const at::Tensor& x, const at::Tensor& w
 // GEMM (data-gradient epilogue EPI 10 / 11), and db1 = Σ_rows gh (fp32,
 // added into accumulate_into when given, else a fresh tensor). gy [M, N2]
 // bf16, w2t = W2ᵀ [N1, N2] bf16, h [M, N1] bf16 (the first Linear's output).
+// pp: the ping-pong GEMM's one-tile kernel (gemm_pp.hip EPI 4 / 5) instead of
+// the 128 x 128 ring.
 std::vector<at::Tensor> linear_dgrad_gelu(const at::Tensor& gy, const at::Tensor& w2t, const at::Tensor& h,
-                                          bool tanh_approx, const c10::optional<at::Tensor>& accumulate_into) {
+                                          bool tanh_approx, const c10::optional<at::Tensor>& accumulate_into,
+                                          bool pp) {
   DK_CHECK(gy.is_cuda() && gy.scalar_type() == at::kBFloat16 && gy.is_contiguous(), "linear_dgrad_gelu: gy");
   DK_CHECK(w2t.scalar_type() == at::kBFloat16 && w2t.is_contiguous() && w2t.dim() == 2, "linear_dgrad_gelu: w2t");
   c10::hip::HIPGuard guard(gy.device().index());
   const int64_t K = gy.size(-1), M = gy.numel() / K, N = w2t.size(0);
   DK_CHECK(w2t.size(1) == K, "linear_dgrad_gelu: w2t must be [N1, N2]");
   DK_CHECK(h.scalar_type() == at::kBFloat16 && h.is_contiguous() && h.numel() == M * N, "linear_dgrad_gelu: h");
-  DK_CHECK(kern::gemm_nt_supported(M, N, K), "linear_dgrad_gelu: unsupported shape");
+  if (pp)
+    DK_CHECK(kern::gemm_pp_supported(M, N, K) && N % 8 == 0, "linear_dgrad_gelu: unsupported shape for pp");
+  else
+    DK_CHECK(kern::gemm_nt_supported(M, N, K), "linear_dgrad_gelu: unsupported shape");
   at::Tensor db;
   if (accumulate_into.has_value() && accumulate_into->defined()) {
     db = *accumulate_into;
@@ -292,8 +298,12 @@ std::vector<at::Tensor> linear_dgrad_gelu(const at::Tensor& gy, const at::Tensor
   }
   std::vector<int64_t> shape(h.sizes().begin(), h.sizes().end());
   at::Tensor gh = at::empty(shape, h.options());
-  kern::gemm_nt_gelubwd_bf16(gy.data_ptr(), w2t.data_ptr(), gh.data_ptr(), M, static_cast<int>(N),
-                             static_cast<int>(K), h.data_ptr(), db.data_ptr<float>(), tanh_approx, stream_of(gy));
+  if (pp)
+    kern::gemm_pp_gelubwd_bf16(gy.data_ptr(), w2t.data_ptr(), gh.data_ptr(), M, static_cast<int>(N),
+                               static_cast<int>(K), h.data_ptr(), db.data_ptr<float>(), tanh_approx, stream_of(gy));
+  else
+    kern::gemm_nt_gelubwd_bf16(gy.data_ptr(), w2t.data_ptr(), gh.data_ptr(), M, static_cast<int>(N),
+                               static_cast<int>(K), h.data_ptr(), db.data_ptr<float>(), tanh_approx, stream_of(gy));
   return {gh, db};
 }
 
@@ -1514,7 +1524,8 @@ void bind(pybind11::module& m) {
   m.def("bn_supported", [](int64_t C) { return kern::bn_supported(static_cast<int>(C)); });
   m.def("layer_norm_supported", &layer_norm_supported);
   m.def("linear_dgrad_gelu", &linear_dgrad_gelu, pybind11::arg("gy"), pybind11::arg("w2t"), pybind11::arg("h"),
-        pybind11::arg("tanh_approx"), pybind11::arg("accumulate_into") = pybind11::none());
+        pybind11::arg("tanh_approx"), pybind11::arg("accumulate_into") = pybind11::none(),
+        pybind11::arg("pp") = false);
   m.def("layer_norm_fwd", &layer_norm_fwd, pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
         pybind11::arg("eps"), pybind11::arg("out_dtype") = pybind11::none());
   m.def("layer_norm_bwd", &layer_norm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("weight"),

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "gelu_kernels.h"
+#include "gelu_math.h"
 
 namespace dcp {
 namespace kern {
@@ -39,26 +40,14 @@ __device__ __forceinline__ uint32_t f2bf(float f) {
 }
 __device__ __forceinline__ uint32_t pack(float a, float b) { return f2bf(a) | (f2bf(b) << 16); }
 
-// tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp, saturates cleanly
-__device__ __forceinline__ float fast_tanh(float u) { return 1.f - 2.f / (__expf(2.f * u) + 1.f); }
-
 template <bool TANH>
 __device__ __forceinline__ float gelu_f(float x) {
-  if (TANH) {
-    const float t = fast_tanh(kSqrt2OverPi * (x + kTanhC * x * x * x));
-    return 0.5f * x * (1.f + t);
-  }
-  return 0.5f * x * (1.f + erff(x * kInvSqrt2));
+  return gm::gelu<TANH>(x);
 }
 
 template <bool TANH>
 __device__ __forceinline__ float gelu_d(float x) {
-  if (TANH) {
-    const float x2 = x * x;
-    const float t = fast_tanh(kSqrt2OverPi * x * (1.f + kTanhC * x2));
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kTanhC * x2);
-  }
-  return 0.5f * (1.f + erff(x * kInvSqrt2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+  return gm::gelu_dx<TANH>(x);
 }
 
 // n8 = number of 8-element vectors; 2 vectors per thread (both loads issued first)

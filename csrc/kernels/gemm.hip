@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <string>
 
+#include "gelu_math.h"
 #include "gemm_kernels.h"
 #include "stem_kernels.h"
 
@@ -255,27 +256,15 @@ struct BnRedArgs {
   uint8_t* ybits;
 };
 
-// GELU of the Linear epilogues (same forms as gelu.hip: tanh through one exp)
+// GELU of the Linear epilogues and its derivative (gelu_math.h, shared with
+// gelu.hip and gemm_pp.hip)
 template <bool TANH>
 __device__ __forceinline__ float gelu_epi(float x) {
-  if (TANH) {
-    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-    const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
-    return 0.5f * x * (1.f + t);
-  }
-  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  return gm::gelu<TANH>(x);
 }
-
-// GELU derivative of the MLP-backward epilogue (gelu.hip's gelu_d forms)
 template <bool TANH>
 __device__ __forceinline__ float gelu_dx(float x) {
-  if (TANH) {
-    const float x2 = x * x;
-    const float u = 0.79788456080286536f * x * (1.f + 0.044715f * x2);
-    const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.79788456080286536f * (1.f + 3.f * 0.044715f * x2);
-  }
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+  return gm::gelu_dx<TANH>(x);
 }
 
 // Several parity classes of a stride-2 kxk data gradient in ONE launch

@@ -60,6 +60,10 @@ void gemm_pp_tune(const char* key, int value);
 int gemm_pp_tune_get(const char* key);
 void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
                   void* c2, int gelu, hipStream_t s);
+// MLP backward through the GELU on the ping-pong GEMM: C [M, N] = bf16(A·Bᵀ) ⊙
+// gelu'(h) (h [M, N] bf16), db[N] += column sums of C (fp32 atomics). N % 8 == 0.
+void gemm_pp_gelubwd_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* h, float* db,
+                          bool tanh_approx, hipStream_t s);
 
 // fp32 weight [R][Cc] → bf16 copy wb [R][Cc] and transposed bf16 wt [Cc][R]
 // (the forward GEMM's B operand and the dgrad GEMM's B operand) in one launch.

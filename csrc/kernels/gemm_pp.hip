@@ -52,6 +52,7 @@
 #include <string>
 #include <type_traits>
 
+#include "gelu_math.h"
 #include "gemm_kernels.h"
 
 namespace dcp {
@@ -106,23 +107,27 @@ __device__ __forceinline__ f32x4 pp_lds_f4(const float* p) {
 
 template <bool TANH>
 __device__ __forceinline__ float pp_gelu(float x) {
-  if (TANH) {
-    const float u = 0.79788456080286536f * (x + 0.044715f * x * x * x);
-    const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
-    return 0.5f * x * (1.f + t);
-  }
-  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  return gm::gelu<TANH>(x);
+}
+template <bool TANH>
+__device__ __forceinline__ float pp_gelu_dx(float x) {
+  return gm::gelu_dx<TANH>(x);
 }
 
 // One tile per workgroup (the first version, kept for grids of at most one
 // tile per CU, where it measured faster than the persistent kernel: no cursor
 // bookkeeping, bias from registers, the whole epilogue staged in LDS).
-// EPI: 0 = C = A·Bᵀ; 1 = + bias; 2 / 3 = + bias, c2 = gelu(C) (tanh / erf)
+// EPI: 0 = C = A·Bᵀ; 1 = + bias; 2 / 3 = + bias, c2 = gelu(C) (tanh / erf);
+// 4 / 5 = the MLP backward's data gradient through the GELU (tanh / erf):
+// C = bf16(A·Bᵀ) ⊙ gelu'(h) (h [M, N] bf16, ldc apart) and dbias[N] += the
+// column sums of the stored C (fp32 atomics: 2 per column per workgroup).
 template <int EPI>
 __global__ void __launch_bounds__(kPT, 1)
     gemm_pp1_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                    int64_t M, int N, int K, int64_t ldc, int tiles_n, const float* __restrict__ bias,
-                   uint16_t* __restrict__ c2) {
+                   uint16_t* __restrict__ c2, const uint16_t* __restrict__ hsrc, float* __restrict__ dbias) {
+  constexpr bool BIAS = EPI >= 1 && EPI <= 3;
+  constexpr bool GB = EPI == 4 || EPI == 5;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -260,8 +265,21 @@ __global__ void __launch_bounds__(kPT, 1)
   // epilogue: each wave stages its 128 x 64 output (bf16, 128-B rows, 16-B
   // chunks XOR row & 7) in its own 16 KB of the ring, then stores whole rows
   char* cst = lds + w * 16384;
+  const int64_t rbase = m0 + wr * 128;
+  const int cb = n0 + wc * 64 + (lane & 7) * 8;  // this lane's 8 output columns
+  // GB: the first half's h rows load while the accumulators are staged
+  uint4 hv[2][8];
+  auto load_h = [&](int half) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      int64_t m = rbase + (half * 8 + it) * 8 + (lane >> 3);
+      m = m < M ? m : M - 1;  // clamped (its store is skipped): the loads stay unconditional
+      hv[half][it] = *reinterpret_cast<const uint4*>(hsrc + m * ldc + (cb < N ? cb : 0));
+    }
+  };
+  if constexpr (GB) load_h(0);
   float bcol[2][2][4];
-  if constexpr (EPI >= 1) {
+  if constexpr (BIAS) {
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
@@ -280,7 +298,7 @@ __global__ void __launch_bounds__(kPT, 1)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           f32x4 a = acc[mq][nq][i][j];
-          if constexpr (EPI >= 1) {
+          if constexpr (BIAS) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) a[r] += bcol[nq][i][r];
           }
@@ -289,8 +307,51 @@ __global__ void __launch_bounds__(kPT, 1)
           *reinterpret_cast<uint2*>(cst + row * 128 + 16 * ((col >> 3) ^ (row & 7)) + (col & 7) * 2) =
               make_uint2(pp_pack(a[0], a[1]), pp_pack(a[2], a[3]));
         }
-  const int64_t rbase = m0 + wr * 128;
-  const int cb = n0 + wc * 64 + (lane & 7) * 8;  // this lane's 8 output columns
+  if constexpr (GB) {
+    float dsum[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dsum[k] = 0.f;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      uint4 val[8];
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int row = (half * 8 + it) * 8 + (lane >> 3);
+        val[it] = *reinterpret_cast<const uint4*>(cst + row * 128 + 16 * ((lane & 7) ^ (row & 7)));
+      }
+      if (half == 0) load_h(1);  // the second half's h rows load behind this half's math
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int64_t m = rbase + (half * 8 + it) * 8 + (lane >> 3);
+        if (m < M && cb < N) {
+          const uint32_t v4[4] = {val[it].x, val[it].y, val[it].z, val[it].w};
+          const uint32_t h4[4] = {hv[half][it].x, hv[half][it].y, hv[half][it].z, hv[half][it].w};
+          uint32_t g4[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            g4[k] = pp_pack(pp_lo(v4[k]) * pp_gelu_dx<EPI == 4>(pp_lo(h4[k])),
+                            pp_hi(v4[k]) * pp_gelu_dx<EPI == 4>(pp_hi(h4[k])));
+            dsum[2 * k] += pp_lo(g4[k]);  // the stored (bf16-rounded) gradient, as gelu_bwd sums it
+            dsum[2 * k + 1] += pp_hi(g4[k]);
+          }
+          *reinterpret_cast<uint4*>(C + m * ldc + cb) = make_uint4(g4[0], g4[1], g4[2], g4[3]);
+        }
+      }
+    }
+    // lanes l, l + 8, ..., l + 56 hold the same 8 columns: fold, then one
+    // atomic per column per wave row group
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      dsum[k] += __shfl_xor(dsum[k], 8, 64);
+      dsum[k] += __shfl_xor(dsum[k], 16, 64);
+      dsum[k] += __shfl_xor(dsum[k], 32, 64);
+    }
+    if (lane < 8 && cb < N) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) atomicAdd(dbias + cb + k, dsum[k]);
+    }
+    return;
+  }
   // rows (it * 8 + lane / 8) of the staged tile, read 8 at a time ahead of
   // their guarded stores (a read under the row guard became a branch + full
   // LDS round trip per row)
@@ -731,7 +792,7 @@ void gemm_pp_launch(const void* A, const void* B, void* C, int64_t M, int N, int
     (void)attr1;
     hipLaunchKernelGGL((gemm_pp1_kernel<EPI>), dim3(tiles), dim3(kPT), kPPLds, s, static_cast<const uint16_t*>(A),
                        static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N, K, ldc, tiles_n, bias,
-                       static_cast<uint16_t*>(c2));
+                       static_cast<uint16_t*>(c2), nullptr, nullptr);
     return;
   }
   const size_t lds = kPPLds + (EPI >= 1 ? static_cast<size_t>(N) * 4 : 0);
@@ -739,7 +800,31 @@ void gemm_pp_launch(const void* A, const void* B, void* C, int64_t M, int N, int
                      static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N, K, ldc, tiles_m, tiles_n,
                      bias, static_cast<uint16_t*>(c2), g_pp_stage);
 }
+
+// the MLP backward's GELU data gradient on the one-tile kernel (EPI 4 / 5)
+template <int EPI>
+void gemm_pp_gb_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* h, float* db,
+                       hipStream_t s) {
+  static const bool attr1 = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_pp1_kernel<EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPPLds);
+    return true;
+  }();
+  (void)attr1;
+  const int tiles_m = static_cast<int>((M + 255) / 256);
+  const int tiles_n = (N + 255) / 256;
+  hipLaunchKernelGGL((gemm_pp1_kernel<EPI>), dim3(tiles_m * tiles_n), dim3(kPT), kPPLds, s,
+                     static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N,
+                     K, static_cast<int64_t>(N), tiles_n, nullptr, nullptr, static_cast<const uint16_t*>(h), db);
+}
 }  // namespace
+
+void gemm_pp_gelubwd_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* h, float* db,
+                          bool tanh_approx, hipStream_t s) {
+  if (N % 8 != 0) throw std::runtime_error("gemm_pp_gelubwd: N must be a multiple of 8");
+  if (tanh_approx) gemm_pp_gb_launch<4>(A, B, C, M, N, K, h, db, s);
+  else gemm_pp_gb_launch<5>(A, B, C, M, N, K, h, db, s);
+}
 
 void gemm_pp_tune(const char* key, int value) {
   const std::string k(key);

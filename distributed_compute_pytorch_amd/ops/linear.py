@@ -748,7 +748,9 @@ class _MLPFn(torch.autograd.Function):
         _, dw2, db2 = _linear_backward(sub2, g2, y1, w2_16)
         # proj's data gradient with the GELU backward and fc's bias sum fused in
         tgt = _acc_target(ctx, b1, torch.Size((h.shape[-1],))) if n[2] else None
-        gh, db1 = _C.linear_dgrad_gelu(g2, w2t, h.view(-1, h.shape[-1]), ctx.tanh, accumulate_into=tgt)
+        M, N1, N2 = g2.shape[0], h.shape[-1], g2.shape[1]
+        pp = _CHOICE.get(("mlp_bwd", M, N2, N1)) == "pp" and _pp_ok(M, N1, N2) and N1 % 8 == 0
+        gh, db1 = _C.linear_dgrad_gelu(g2, w2t, h.view(-1, h.shape[-1]), ctx.tanh, accumulate_into=tgt, pp=pp)
         if tgt is not None or not n[2]:
             db1 = None
         elif db1.dtype != ctx.bdtypes[0]:
@@ -764,8 +766,9 @@ def _mlp_prefers_ours(x, w1_16, b1, b1_16, w2_16, w2t, tanh) -> bool:
     fc's bias-gradient sums in the ring GEMM's epilogue (``linear_dgrad_gelu``)
     instead of the fastest plain data-gradient GEMM (pp / ring / hipBLASLt)
     plus the separate GELU-backward pass over gy and h. Both are timed
-    (``("mlp_bwd", M, N2, N1)``: "ring" = fused, "hipblaslt" = unfused — the
-    names the autotune table already carries); its forward takes whichever
+    (``("mlp_bwd", M, N2, N1)``: "ring" / "pp" = fused on the ring / the
+    ping-pong GEMM's GELU-backward epilogue, "hipblaslt" = unfused — the names
+    the autotune table already carries); its forward takes whichever
     kernel the fc forward autotune picked."""
     M, K = x.numel() // x.shape[-1], x.shape[-1]
     N1, N2 = w1_16.shape[0], w2_16.shape[0]
@@ -790,8 +793,11 @@ def _mlp_prefers_ours(x, w1_16, b1, b1_16, w2_16, w2t, tanh) -> bool:
                 gy = dc[best]()
                 return _C.gelu_bwd(gy[0] if isinstance(gy, (list, tuple)) else gy, h, tanh, True)
 
-            _pick(key_b, {"ring": lambda: _C.linear_dgrad_gelu(g2, w2t, h, tanh), "hipblaslt": unfused})
-    return _CHOICE[key_b] == "ring"
+            cands = {"ring": lambda: _C.linear_dgrad_gelu(g2, w2t, h, tanh), "hipblaslt": unfused}
+            if _pp_ok(M, N1, N2) and N1 % 8 == 0:
+                cands["pp"] = lambda: _C.linear_dgrad_gelu(g2, w2t, h, tanh, pp=True)
+            _pick(key_b, cands)
+    return _CHOICE[key_b] != "hipblaslt"
 
 
 def fused_mlp_gelu(x: torch.Tensor, fc: "FusedLinear", proj: "FusedLinear", approximate: str = "none"):

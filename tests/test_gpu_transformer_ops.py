@@ -533,29 +533,33 @@ def test_linear_fwd_epilogues_match_fp32(cuda, gelu, rows, fin, fout, lin_big):
         torch.testing.assert_close(out[0].float(), y_ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("pp", [False, True])
 @pytest.mark.parametrize("tanh", [True, False])
-@pytest.mark.parametrize("rows,n1,n2", [(1000, 512, 256), (4096, 3072, 768), (333, 128, 64)])
-def test_linear_dgrad_gelu_matches_fp32(cuda, tanh, rows, n1, n2):
-    """gemm.hip EPI 10/11: gh = (gy·W2)·gelu'(h) and db = Σ gh, vs fp32
-    PyTorch on the same bf16 operands (gh of the bf16-rounded gy·W2)."""
+@pytest.mark.parametrize("rows,n1,n2", [(1000, 512, 256), (4096, 3072, 768), (333, 128, 64), (700, 264, 128)])
+def test_linear_dgrad_gelu_matches_fp32(cuda, tanh, rows, n1, n2, pp):
+    """gemm.hip EPI 10/11 (ring) and gemm_pp.hip EPI 4/5 (ping-pong): gh =
+    (gy·W2)·gelu'(h) and db = Σ gh, vs fp32 PyTorch on the same bf16 operands
+    (gh of the bf16-rounded gy·W2)."""
     from distributed_compute_pytorch_amd._ext import C
 
+    if not pp and n1 % 64:
+        pytest.skip("the ring takes multiples of 64 columns")
     g = torch.Generator().manual_seed(5)
     gy = torch.randn(rows, n2, generator=g).to(torch.bfloat16).to(cuda)
     w2 = (torch.randn(n2, n1, generator=g) / n1 ** 0.5).to(torch.bfloat16).to(cuda)
     h = torch.randn(rows, n1, generator=g).to(torch.bfloat16).to(cuda)
-    gh, db = C.linear_dgrad_gelu(gy, w2.t().contiguous(), h, tanh)
+    gh, db = C.linear_dgrad_gelu(gy, w2.t().contiguous(), h, tanh, pp=pp)
     dy = (gy.float() @ w2.float()).to(torch.bfloat16).float()
     hr = h.float().requires_grad_()
     torch.nn.functional.gelu(hr, approximate="tanh" if tanh else "none").backward(dy)
     torch.testing.assert_close(gh.float(), hr.grad, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(db, gh.float().sum(0), rtol=1e-4, atol=1e-3)
     acc = torch.ones(n1, device=cuda)
-    C.linear_dgrad_gelu(gy, w2.t().contiguous(), h, tanh, accumulate_into=acc)
+    C.linear_dgrad_gelu(gy, w2.t().contiguous(), h, tanh, accumulate_into=acc, pp=pp)
     torch.testing.assert_close(acc, 1 + gh.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("ours", ["pp", "ring", "blasfwd"])
+@pytest.mark.parametrize("ours", ["pp", "ring", "blasfwd", "ppbwd"])
 @pytest.mark.parametrize("approx", ["tanh", "none"])
 def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch, ours):
     """ops.linear.fused_mlp_gelu (one node: GELU forward in fc's epilogue,
@@ -567,10 +571,12 @@ def test_fused_mlp_matches_fp32(cuda, approx, monkeypatch, ours):
 
     monkeypatch.setattr(lin, "_AUTOTUNE", False)
     monkeypatch.setattr(lin, "_CHOICE", {})
-    monkeypatch.setattr(lin, "_DEFAULT_OURS", "ring" if ours == "blasfwd" else ours)
+    monkeypatch.setattr(lin, "_DEFAULT_OURS", "ring" if ours in ("blasfwd", "ppbwd") else ours)
     if ours == "blasfwd":  # the fused node with fc's forward on hipBLASLt + the GELU kernel
         lin._CHOICE[("fwd_gelu", 1024, 256, 1024)] = "hipblaslt"
         lin._CHOICE[("mlp_bwd", 1024, 256, 1024)] = "ring"
+    if ours == "ppbwd":  # the GELU backward in the ping-pong GEMM's epilogue
+        lin._CHOICE[("mlp_bwd", 1024, 256, 1024)] = "pp"
 
     torch.manual_seed(0)
     fc, proj = FusedLinear(256, 1024).to(cuda), FusedLinear(1024, 256).to(cuda)
