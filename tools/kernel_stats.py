@@ -49,7 +49,28 @@ def main():
     ap.add_argument("--grid", action="store_true")
     ap.add_argument("--families", action="store_true", help="group by kernel name without template arguments")
     ap.add_argument("--steps", type=int, default=1, help="divide family totals by this many steps")
+    ap.add_argument("--busy", type=float, default=None, metavar="SKIP",
+                    help="GPU busy fraction (union of kernel intervals / span) after skipping the first SKIP of the span")
     a = ap.parse_args()
+    if a.busy is not None:
+        con = sqlite3.connect(a.path)
+        iv = sorted(con.execute("select start, end from kernels"))
+        t0, t1 = iv[0][0], max(e for _, e in iv)
+        cut = t0 + a.busy * (t1 - t0)
+        busy, cur_s, cur_e = 0, None, None
+        for s_, e_ in iv:
+            if e_ <= cut:
+                continue
+            s_ = max(s_, cut)
+            if cur_e is None or s_ > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = s_, e_
+            else:
+                cur_e = max(cur_e, e_)
+        busy += cur_e - cur_s
+        print(f"# GPU busy {busy / (t1 - cut):.3f} of {(t1 - cut) / 1e6:.1f} ms (first {a.busy:.0%} of the trace skipped)")
+        return
     if a.families:
         fam = defaultdict(float)
         for n, d in rows(a.path, False):
