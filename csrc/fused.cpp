@@ -12,6 +12,7 @@
 #include "kernels/bn_kernels.h"
 #include "kernels/gemm_kernels.h"
 #include "kernels/attn_kernels.h"
+#include "kernels/kernels.h"
 #include "kernels/ln_kernels.h"
 #include "kernels/dropout_kernels.h"
 #include "kernels/pool_kernels.h"
@@ -305,6 +306,20 @@ std::vector<at::Tensor> linear_dgrad_gelu(const at::Tensor& gy, const at::Tensor
     kern::gemm_nt_gelubwd_bf16(gy.data_ptr(), w2t.data_ptr(), gh.data_ptr(), M, static_cast<int>(N),
                                static_cast<int>(K), h.data_ptr(), db.data_ptr<float>(), tanh_approx, stream_of(gy));
   return {gh, db};
+}
+
+// Embedding weight gradient for a table of at most 8 rows (embedding.hip):
+// gw [V, D] fp32 += the per-index sums of g [M, D] fp32 (idx int64 [M]).
+void embedding_small_bwd(const at::Tensor& idx, const at::Tensor& g, at::Tensor& gw) {
+  DK_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.is_contiguous() && g.dim() == 2, "embedding_small_bwd: g");
+  DK_CHECK(gw.scalar_type() == at::kFloat && gw.is_contiguous() && gw.dim() == 2 && gw.size(1) == g.size(1),
+           "embedding_small_bwd: gw");
+  DK_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous() && idx.numel() == g.size(0), "embedding_small_bwd: idx");
+  DK_CHECK(kern::emb_small_supported(gw.size(0), gw.size(1)), "embedding_small_bwd: V <= 8 rows, D % 4 == 0");
+  c10::hip::HIPGuard guard(g.device().index());
+  if (g.size(0) == 0) return;
+  kern::emb_small_bwd(idx.data_ptr<int64_t>(), g.data_ptr<float>(), gw.data_ptr<float>(), g.size(0),
+                      static_cast<int>(gw.size(0)), static_cast<int>(gw.size(1)), stream_of(g));
 }
 
 std::vector<at::Tensor> linear_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, int64_t gelu) {
@@ -1561,6 +1576,8 @@ void bind(pybind11::module& m) {
   m.def("linear_fwd", &linear_fwd, "Linear forward on the MFMA GEMM: bias (+ GELU tanh/erf) in the epilogue",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("gelu") = 0);
   m.def("attn_ok", &attn_ok);
+  m.def("embedding_small_bwd", &embedding_small_bwd, "gw += per-index row sums (embedding tables of <= 8 rows)",
+        pybind11::arg("idx"), pybind11::arg("g"), pybind11::arg("gw"));
   m.def("colsum", &colsum, "fp32 column sums of a bf16 [.., N] tensor (bias gradient)", pybind11::arg("x"),
         pybind11::arg("accumulate_into") = pybind11::none());
   m.def("gelu_fwd", &gelu_fwd, "bf16 GELU forward (erf or tanh form)", pybind11::arg("h"),

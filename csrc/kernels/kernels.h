@@ -46,6 +46,9 @@ void mt_adadelta(TableView t, int64_t nchunks, DType p, float lr, float rho, flo
 // Sum of squares per tensor list -> out[0] (fp32, accumulated with atomics
 // per workgroup) and non-finite flag out[1]. list 0 = tensors.
 void mt_sumsq(TableView t, int64_t nchunks, DType d, float* out, hipStream_t s);
+// embedding.hip: gw[V][D] += per-index sums of g [M][D] (fp32; V <= 8, D % 4 == 0)
+bool emb_small_supported(int64_t V, int64_t D);
+void emb_small_bwd(const int64_t* idx, const float* g, float* gw, int64_t M, int V, int D, hipStream_t s);
 
 // In-place scale of every tensor: x *= scale_dev[0] (device scalar).
 void mt_scale_by(TableView t, int64_t nchunks, DType d, const float* scale_dev, hipStream_t s);
