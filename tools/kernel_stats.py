@@ -51,12 +51,19 @@ def main():
     ap.add_argument("--steps", type=int, default=1, help="divide family totals by this many steps")
     ap.add_argument("--busy", type=float, default=None, metavar="SKIP",
                     help="GPU busy fraction (union of kernel intervals / span) after skipping the first SKIP of the span")
+    ap.add_argument("--window", default=None, metavar="NAME:N",
+                    help="with --busy: the window between the last N launches of kernel NAME (substring)")
     a = ap.parse_args()
     if a.busy is not None:
         con = sqlite3.connect(a.path)
         iv = sorted(con.execute("select start, end from kernels"))
         t0, t1 = iv[0][0], max(e for _, e in iv)
         cut = t0 + a.busy * (t1 - t0)
+        if a.window:
+            name, n = a.window.rsplit(":", 1)
+            starts = sorted(st for nm, st in con.execute("select name, start from kernels") if name in nm)[-int(n):]
+            cut, t1 = starts[0], starts[-1]
+            iv = [(max(s_, cut), min(e_, t1)) for s_, e_ in iv if e_ > cut and s_ < t1]
         busy, cur_s, cur_e = 0, None, None
         for s_, e_ in iv:
             if e_ <= cut:
@@ -69,7 +76,8 @@ def main():
             else:
                 cur_e = max(cur_e, e_)
         busy += cur_e - cur_s
-        print(f"# GPU busy {busy / (t1 - cut):.3f} of {(t1 - cut) / 1e6:.1f} ms (first {a.busy:.0%} of the trace skipped)")
+        print(f"# GPU busy {busy / (t1 - cut):.3f} of {(t1 - cut) / 1e6:.1f} ms "
+              f"({'window ' + a.window if a.window else f'first {a.busy:.0%} of the trace skipped'})")
         return
     if a.families:
         fam = defaultdict(float)

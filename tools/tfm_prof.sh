@@ -17,7 +17,7 @@ for m in $MODELS; do
     tail -5 "$O/${TAG}_${m}_stats.txt"; exit 1; }
   python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}_$m/run_results.db" --families --steps $((STEPS + 4)) --top 30 \
     > "$O/${TAG}_${m}_families.txt" 2>&1 || { tail -5 "$O/${TAG}_${m}_families.txt"; exit 1; }
-  python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}_$m/run_results.db" --busy 0.5 >> "$O/${TAG}_${m}_families.txt" 2>&1 || true
+  python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}_$m/run_results.db" --busy 0 --window "${WINDOW_KERNEL:-mt_adam}:${WINDOW_N:-20}" >> "$O/${TAG}_${m}_families.txt" 2>&1 || true
   tail -1 "$O/${TAG}_${m}_families.txt"
   head -25 "$O/${TAG}_${m}_stats.txt"
 done
