@@ -314,39 +314,16 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
   }
 }
 
-// ------------------------------------------------------ bwd: delta -------
-// delta[bh][t] = Σ_d dO·O (fp32)
-__global__ void __launch_bounds__(kT) attn_delta_kernel(AttnParams P, AttnTensor o, AttnTensor dout,
-                                                        float* __restrict__ delta) {
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;  // over B*H*T
-  const int64_t n = static_cast<int64_t>(P.B) * P.H * P.T;
-  if (row >= n) return;
-  const int t = static_cast<int>(row % P.T);
-  const int bh = static_cast<int>(row / P.T), b = bh / P.H, hd = bh % P.H;
-  const uint16_t* O = static_cast<const uint16_t*>(o.ptr) + b * o.sb + static_cast<int64_t>(t) * o.st + hd * kD;
-  const uint16_t* G = static_cast<const uint16_t*>(dout.ptr) + b * dout.sb + static_cast<int64_t>(t) * dout.st + hd * kD;
-  float acc = 0.f;
-#pragma unroll
-  for (int c8 = 0; c8 < 8; ++c8) {
-    const uint4 a = reinterpret_cast<const uint4*>(O)[c8];
-    const uint4 g = reinterpret_cast<const uint4*>(G)[c8];
-    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, gw[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      acc = fmaf(__uint_as_float(aw[e] << 16), __uint_as_float(gw[e] << 16), acc);
-      acc = fmaf(__uint_as_float(aw[e] & 0xffff0000u), __uint_as_float(gw[e] & 0xffff0000u), acc);
-    }
-  }
-  delta[row] = acc;
-}
-
 // --------------------------------------------------------- bwd: dQ -------
 // query on the lane (as the forward): Sᵀ = K·Qᵀ, dPᵀ = V·dOᵀ,
 // dSᵀ = Pᵀ∘(dPᵀ∘keep/(1-p) − δ), dQᵀ += Kᵀ·dSᵀ.
+// δ = rowsum(dO ∘ O) is computed here from the query rows' dO (already loaded)
+// and O (4 more 16-B loads per lane, behind the first K/V stage), and stored
+// for the dK/dV kernel, which runs after this one (no separate δ pass).
 template <bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTensor q, AttnTensor k, AttnTensor v,
-                                                         AttnTensor dout, const float* __restrict__ lse,
-                                                         const float* __restrict__ delta, AttnOut dq) {
+                                                         AttnTensor dout, AttnTensor o, const float* __restrict__ lse,
+                                                         float* __restrict__ delta, AttnOut dq) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kTile];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -358,8 +335,9 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
   const int T = P.T;
   const int qi = tile * 128 + wave * 32 + (lane & 31);
   const bool qok = qi < T;
-  const Ptrs Q = head(q, b, hd), K = head(k, b, hd), V = head(v, b, hd), G = head(dout, b, hd);
+  const Ptrs Q = head(q, b, hd), K = head(k, b, hd), V = head(v, b, hd), G = head(dout, b, hd), O = head(o, b, hd);
   bf16x8 qf[4], gf[4];
+  uint4 uo[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     const uint4 z = make_uint4(0, 0, 0, 0);
@@ -367,11 +345,24 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
     const int64_t qc = qok ? qi : 0;  // load (row clamped), then select
     const uint4 uq = *reinterpret_cast<const uint4*>(Q.p + qc * Q.st + off);
     const uint4 ug = *reinterpret_cast<const uint4*>(G.p + qc * G.st + off);
+    uo[ks] = *reinterpret_cast<const uint4*>(O.p + qc * O.st + off);
     qf[ks] = __builtin_bit_cast(bf16x8, qok ? uq : z);
     gf[ks] = __builtin_bit_cast(bf16x8, qok ? ug : z);
   }
   const float lse2 = qok ? lse[static_cast<int64_t>(bh) * T + qi] : 0.f;
-  const float dlt = qok ? delta[static_cast<int64_t>(bh) * T + qi] : 0.f;
+  float dpart = 0.f;  // this lane's half of the row's 64 products (lanes l, l + 32: one row)
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const uint4 g = __builtin_bit_cast(uint4, gf[ks]);
+    const uint32_t aw[4] = {uo[ks].x, uo[ks].y, uo[ks].z, uo[ks].w}, gw[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      dpart = fmaf(__uint_as_float(aw[e] << 16), __uint_as_float(gw[e] << 16), dpart);
+      dpart = fmaf(__uint_as_float(aw[e] & 0xffff0000u), __uint_as_float(gw[e] & 0xffff0000u), dpart);
+    }
+  }
+  const float dlt = dpart + __shfl_xor(dpart, 32, 64);  // 0 for rows past T (gf zeroed)
+  if (qok && hh == 0) delta[static_cast<int64_t>(bh) * T + qi] = dlt;
   const float c = P.scale * kLog2e;
   const uint32_t thr = drop_thr(P.p_drop);
   const float inv_keep = drop_scale(thr);
@@ -607,15 +598,13 @@ void attn_fwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, Att
 
 void attn_bwd(const AttnParams& p, AttnTensor q, AttnTensor k, AttnTensor v, AttnTensor o, AttnTensor dout,
               const float* lse, float* delta, AttnOut dq, AttnOut dk, AttnOut dv, hipStream_t s) {
-  const int64_t rows = static_cast<int64_t>(p.B) * p.H * p.T;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3(static_cast<int>((rows + kT - 1) / kT)), dim3(kT), 0, s, p, o, dout,
-                     delta);
+  // dQ first: it computes δ = rowsum(dO ∘ O) on the way and stores it for dK/dV
   const dim3 grid(p.B * p.H, (p.T + 127) / 128);
   const bool drop = p.p_drop > 0.f;
-#define DK_AB(C, D)                                                                                          \
-  do {                                                                                                        \
+#define DK_AB(C, D)                                                                                             \
+  do {                                                                                                           \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, dout, o, lse, delta, dq);   \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, dout, lse, delta, dk, dv); \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<C, D>), grid, dim3(kT), 0, s, p, q, k, v, dout, lse, delta, dq);   \
   } while (0)
   if (p.causal && drop) DK_AB(true, true);
   else if (p.causal) DK_AB(true, false);
