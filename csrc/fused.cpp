@@ -527,9 +527,28 @@ at::Tensor conv1x1_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
 }
 
 // dw[Cout, Cin] (fp32) = Σ_m gy[m, :]^T ⊗ f(x)[m, :]
+// slots > 0: the split-M plan's workgroup budget for this call only (gemm_tune
+// "wg_slots", default 512) — the transformer Linear wgrad picks it per row count.
+namespace {
+struct ScopedWgSlots {
+  int old = 0;
+  bool on;
+  explicit ScopedWgSlots(int64_t slots) : on(slots > 0) {
+    if (on) {
+      old = kern::gemm_tune_get("wg_slots");
+      kern::gemm_tune("wg_slots", static_cast<int>(slots));
+    }
+  }
+  ~ScopedWgSlots() {
+    if (on) kern::gemm_tune("wg_slots", old);
+  }
+};
+}  // namespace
+
 at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::optional<at::Tensor>& scale,
                          const c10::optional<at::Tensor>& shift, bool relu,
-                         const c10::optional<at::Tensor>& accumulate_into, int64_t out_rows) {
+                         const c10::optional<at::Tensor>& accumulate_into, int64_t out_rows, int64_t slots) {
+  const ScopedWgSlots scoped(slots);
   check_gemm_act(gy, "conv1x1_wgrad");
   check_gemm_act(x, "conv1x1_wgrad");
   c10::hip::HIPGuard guard(gy.device().index());
@@ -1621,7 +1640,7 @@ void bind(pybind11::module& m) {
   m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("gy"), pybind11::arg("x"),
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
         pybind11::arg("relu") = false, pybind11::arg("accumulate_into") = pybind11::none(),
-        pybind11::arg("out_rows") = -1);
+        pybind11::arg("out_rows") = -1, pybind11::arg("slots") = 0);
   m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward", pybind11::arg("gy"),
         pybind11::arg("gy2"), pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
         pybind11::arg("mean"), pybind11::arg("invstd"), pybind11::arg("y"), pybind11::arg("act"),

@@ -255,6 +255,14 @@ def _fwd_cands(x2, w, b, b32, mode: int) -> dict:
     return c
 
 
+def _wgrad_slots(M: int) -> int:
+    """Workgroup budget of the split-M wgrad plan for an M-row Linear: twice
+    the default (more, shorter M splits) from 16,384 rows — same-box A/B
+    (profiles/r4_wgslots.jsonl): BERT (16,384 rows) 1,665 → 1,685 samples/s
+    at 1,024, GPT-2 (8,192 rows) 621 → 614, so it keeps 512 (0 = default)."""
+    return 1024 if M >= 16384 else 0
+
+
 def _lb(b):
     """The bias as the bf16 ATen GEMMs take it, cast only where one runs (our
     kernels read the fp32 bias in their epilogue). A CUDA fp32 bias gets a
@@ -355,7 +363,7 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
             # our split-M MFMA wgrad GEMM (gemm.hip): faster than hipBLASLt at
             # every BERT / GPT-2 shape (profiles/r1_linear_wgrad_bench.log)
             tgt = _acc_target(ctx, weight, torch.Size((g2.shape[1], x2.shape[1])))
-            dw = _C.conv1x1_wgrad(g2, x2.contiguous(), accumulate_into=tgt)
+            dw = _C.conv1x1_wgrad(g2, x2.contiguous(), accumulate_into=tgt, slots=_wgrad_slots(g2.shape[0]))
             if tgt is not None:
                 dw = None  # added into weight.grad by the kernel
         else:
