@@ -1219,9 +1219,27 @@ bool layer_norm_supported(int64_t D) { return kern::ln_supported(static_cast<int
 
 // x: [..., D] contiguous. Returns (y, mean, rstd) with mean/rstd [rows] fp32.
 // out_dtype: y's dtype (default x's; fp32 x -> bf16 y for autocast).
+namespace {
+// the fused residual dropout of a LayerNorm (ln_kernels.h LnDropAdd): same
+// threshold / scale as dropout_fwd for p
+kern::LnDropAdd ln_drop(double p, int64_t seed, const c10::optional<at::Tensor>& offset_dev) {
+  kern::LnDropAdd da{};
+  da.thr = kern::dropout_threshold(static_cast<float>(p));
+  da.scale = p < 1.0 ? 1.f / (1.f - static_cast<float>(p)) : 0.f;
+  da.seed = static_cast<uint64_t>(seed);
+  da.offset = 0;
+  da.offset_dev = offset_dev.has_value() && offset_dev->defined() ? offset_dev->data_ptr<int64_t>() : nullptr;
+  return da;
+}
+}  // namespace
+
+// branch (bf16, x's shape): the LN input becomes x + dropout(branch, p) (the
+// Philox mask of dropout_fwd for (seed, offset_dev)), returned as a 4th output.
 std::vector<at::Tensor> layer_norm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
                                        const c10::optional<at::Tensor>& bias, double eps,
-                                       c10::optional<at::ScalarType> out_dtype) {
+                                       c10::optional<at::ScalarType> out_dtype,
+                                       const c10::optional<at::Tensor>& branch, double p, int64_t seed,
+                                       const c10::optional<at::Tensor>& offset_dev) {
   DK_CHECK(x.is_cuda() && x.is_contiguous(), "layer_norm_fwd: contiguous device tensor required");
   const int64_t D = x.size(-1);
   DK_CHECK(kern::ln_supported(static_cast<int>(D)), "layer_norm_fwd: D must be a multiple of 8 and <= 4096");
@@ -1234,9 +1252,23 @@ std::vector<at::Tensor> layer_norm_fwd(const at::Tensor& x, const c10::optional<
   at::Tensor mean = at::empty({rows}, fopt), rstd = at::empty({rows}, fopt);
   at::Tensor w = weight.has_value() && weight->defined() ? weight->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor b = bias.has_value() && bias->defined() ? bias->to(at::kFloat).contiguous() : at::Tensor();
+  const bool fused = branch.has_value() && branch->defined();
+  at::Tensor xnew;
+  kern::LnDropAdd da{};
+  if (fused) {
+    DK_CHECK(branch->scalar_type() == at::kBFloat16 && branch->is_contiguous() && branch->numel() == x.numel() &&
+                 branch->device() == x.device(),
+             "layer_norm_fwd: branch must be a contiguous bf16 tensor of x's size");
+    xnew = at::empty_like(x);
+    da = ln_drop(p, seed, offset_dev);
+    da.xb = branch->data_ptr();
+    da.out = xnew.data_ptr();
+  }
   kern::ln_forward(ln_dtype(x), ln_dtype(y), x.data_ptr(), w.defined() ? w.data_ptr<float>() : nullptr,
                    b.defined() ? b.data_ptr<float>() : nullptr, y.data_ptr(), mean.data_ptr<float>(),
-                   rstd.data_ptr<float>(), rows, static_cast<int>(D), static_cast<float>(eps), stream_of(x));
+                   rstd.data_ptr<float>(), rows, static_cast<int>(D), static_cast<float>(eps), stream_of(x),
+                   fused ? &da : nullptr);
+  if (fused) return {y, mean, rstd, xnew};
   return {y, mean, rstd};
 }
 
@@ -1247,7 +1279,8 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
                                        const c10::optional<at::Tensor>& bias, const at::Tensor& mean,
                                        const at::Tensor& rstd, const c10::optional<std::vector<at::Tensor>>& accumulate_into,
                                        const c10::optional<at::Tensor>& grad_residual,
-                                       const c10::optional<at::Tensor>& dy2) {
+                                       const c10::optional<at::Tensor>& dy2, double drop_p, int64_t drop_seed,
+                                       const c10::optional<at::Tensor>& drop_offset_dev, bool branch_grad) {
   c10::hip::HIPGuard guard(x.device().index());
   at::Tensor g = dy.contiguous();
   // dy arrives in y's dtype (bf16 when the forward wrote bf16 from fp32 x)
@@ -1287,13 +1320,24 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
     g2 = dy2->scalar_type() == g.scalar_type() ? dy2->contiguous() : dy2->to(g.scalar_type()).contiguous();
     DK_CHECK(g2.numel() == g.numel() && g2.device() == g.device(), "layer_norm_bwd: dy2 must match dy");
   }
+  // branch_grad: also the fused residual dropout's branch gradient dx · keep ·
+  // scale (bf16), the mask of the forward's (drop_p, drop_seed, drop_offset_dev)
+  at::Tensor gb;
+  kern::LnDropAdd da{};
+  if (branch_grad) {
+    gb = at::empty_like(x, x.options().dtype(at::kBFloat16));
+    da = ln_drop(drop_p, drop_seed, drop_offset_dev);
+    da.out = gb.data_ptr();
+  }
   kern::ln_backward(ln_dtype(x), ln_dtype(g), g.data_ptr(), x.data_ptr(), has_w ? w.data_ptr<float>() : nullptr,
                     mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(),
                     db.data_ptr<float>(), part.data_ptr<float>(), rows, static_cast<int>(D), accum, stream_of(x),
-                    gr.defined() ? gr.data_ptr() : nullptr, g2.defined() ? g2.data_ptr() : nullptr);
-  if (accum) return {dx, at::Tensor(), at::Tensor()};
+                    gr.defined() ? gr.data_ptr() : nullptr, g2.defined() ? g2.data_ptr() : nullptr,
+                    branch_grad ? &da : nullptr);
+  if (accum) return {dx, at::Tensor(), at::Tensor(), gb};
   const bool has_b = bias.has_value() && bias->defined();
-  return {dx, has_w ? dw.to(weight->scalar_type()) : at::Tensor(), has_b ? db.to(bias->scalar_type()) : at::Tensor()};
+  return {dx, has_w ? dw.to(weight->scalar_type()) : at::Tensor(), has_b ? db.to(bias->scalar_type()) : at::Tensor(),
+          gb};
 }
 
 // ------------------------------------------------------- cross-entropy ---
@@ -1561,11 +1605,13 @@ void bind(pybind11::module& m) {
         pybind11::arg("tanh_approx"), pybind11::arg("accumulate_into") = pybind11::none(),
         pybind11::arg("pp") = false);
   m.def("layer_norm_fwd", &layer_norm_fwd, pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
-        pybind11::arg("eps"), pybind11::arg("out_dtype") = pybind11::none());
+        pybind11::arg("eps"), pybind11::arg("out_dtype") = pybind11::none(), pybind11::arg("branch") = pybind11::none(),
+        pybind11::arg("p") = 0.0, pybind11::arg("seed") = 0, pybind11::arg("offset_dev") = pybind11::none());
   m.def("layer_norm_bwd", &layer_norm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("weight"),
         pybind11::arg("bias"), pybind11::arg("mean"), pybind11::arg("rstd"),
         pybind11::arg("accumulate_into") = pybind11::none(), pybind11::arg("grad_residual") = pybind11::none(),
-        pybind11::arg("dy2") = pybind11::none());
+        pybind11::arg("dy2") = pybind11::none(), pybind11::arg("drop_p") = 0.0, pybind11::arg("drop_seed") = 0,
+        pybind11::arg("drop_offset_dev") = pybind11::none(), pybind11::arg("branch_grad") = false);
   m.def("cross_entropy_fwd", &cross_entropy_fwd, pybind11::arg("logits"), pybind11::arg("target"),
         pybind11::arg("ignore_index"), pybind11::arg("label_smoothing"), pybind11::arg("n_valid") = -1);
   m.def("log_softmax_fwd", &log_softmax_fwd, pybind11::arg("x"), pybind11::arg("out_dtype") = pybind11::none());

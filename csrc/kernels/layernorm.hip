@@ -12,6 +12,7 @@
 #include <cstdlib>
 
 #include "ln_kernels.h"
+#include "philox.h"
 
 namespace dcp {
 namespace kern {
@@ -79,6 +80,15 @@ __device__ __forceinline__ float rsum(float v) {
   return v;
 }
 
+// keep bits of the 8 elements e0 … e0 + 7 (e0 % 8 == 0)
+__device__ __forceinline__ void drop8(const LnDropAdd& da, uint64_t off, int64_t e0, bool (&kp)[8]) {
+  const U4 a = philox(da.seed, off + static_cast<uint64_t>(e0 >> 2));
+  const U4 b = philox(da.seed, off + static_cast<uint64_t>(e0 >> 2) + 1);
+  const uint32_t r[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) kp[k] = keep(r[k], da.thr);
+}
+
 // 8 consecutive fp32 affine values (or the identity when absent)
 __device__ __forceinline__ void ld_aff(const float* p, int c, float def, float (&o)[8]) {
   if (p) {
@@ -100,11 +110,12 @@ __device__ __forceinline__ void ld_aff(const float* p, int c, float def, float (
 // LPR = lanes per row: 64 (a row per wave) or 32 (a row per half-wave, for D
 // whose 16-B vector count is an odd multiple of 32 — D = 768: 3 vectors on
 // every lane instead of 2 on half of them and 1 on the other half).
-template <int XD, int YD, int VPL, int R, int LPR = 64>
+// DADD: x = res (the x argument) + dropout(da.xb), stored to da.out.
+template <int XD, int YD, int VPL, int R, int LPR = 64, bool DADD = false>
 __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, const float* __restrict__ w,
                                                     const float* __restrict__ b, void* __restrict__ y,
                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                    int64_t rows, int D, float eps) {
+                                                    int64_t rows, int D, float eps, LnDropAdd da) {
   const int lane = threadIdx.x & (LPR - 1);
   const int sub = LPR == 64 ? 0 : (threadIdx.x >> 5) & 1;
   const int64_t row0 = ((static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * (64 / LPR) + sub) * R;
@@ -118,7 +129,24 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, 
     if (vi < nv) {
 #pragma unroll
       for (int r = 0; r < R; ++r)
-        if (row0 + r < rows) L8<XD>::ld(x, (row0 + r) * D + vi * 8, v[r][j]);
+        if (row0 + r < rows) {
+          L8<XD>::ld(x, (row0 + r) * D + vi * 8, v[r][j]);
+          if constexpr (DADD) {
+            float br[8];
+            L8<LN_BF16>::ld(da.xb, (row0 + r) * D + vi * 8, br);
+            const uint64_t off = da.offset + (da.offset_dev ? static_cast<uint64_t>(*da.offset_dev) : 0);
+            bool kp[8];
+            drop8(da, off, (row0 + r) * D + vi * 8, kp);
+            // dropout.hip's expression: res + (keep ? x · scale : 0) — same bits as the unfused pass
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              v[r][j][k] = v[r][j][k] + (kp[k] ? br[k] * da.scale : 0.f);
+              // the LN normalises x as stored (and as its backward re-reads it)
+              if (XD == LN_BF16) v[r][j][k] = __uint_as_float(static_cast<uint32_t>(f2bf(v[r][j][k])) << 16);
+            }
+            L8<XD>::st(da.out, (row0 + r) * D + vi * 8, v[r][j]);
+          }
+        }
       ld_aff(w, vi * 8, 1.f, wv[j]);
       ld_aff(b, vi * 8, 0.f, bv[j]);
     }
@@ -164,13 +192,15 @@ __global__ void __launch_bounds__(kT) ln_fwd_kernel(const void* __restrict__ x, 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 // partial[blk][0][D] += dy * xhat (dgamma), partial[blk][1][D] += dy (dbeta)
 // Each wave takes R rows at a time with all their loads in flight together.
-template <int XD, int YD, int VPL, int R, int LPR = 64>
+// DMASK: da.out (bf16) = dx · keep · scale, the gradient of a fused
+// residual-dropout branch (LnDropAdd).
+template <int XD, int YD, int VPL, int R, int LPR = 64, bool DMASK = false>
 __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(R == 1 && VPL <= 2 ? 4 : 1))) ln_bwd_kernel(const void* __restrict__ dy, const void* __restrict__ x,
                                                     const float* __restrict__ w, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, void* __restrict__ dx,
                                                     float* __restrict__ part, int64_t rows, int D,
                                                     int rows_per_blk, const void* __restrict__ gres,
-                                                    const void* __restrict__ dy2) {
+                                                    const void* __restrict__ dy2, LnDropAdd da) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kWaves][2][D]
   const int lane = threadIdx.x & (LPR - 1);
   const int sub = LPR == 64 ? 0 : (threadIdx.x >> 5) & 1;  // half-wave (LPR = 32)
@@ -201,6 +231,10 @@ __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(R == 1 
     // while the registers allow: D <= 2048
     constexpr bool kHoist = VPL <= 4 && !kLean;
     float dv[R][VPL][8], xh[R][VPL][8], gr[kHoist ? R : 1][kHoist ? VPL : 1][8], mu[R], rs[R];
+    // DMASK: keep bits drawn while the row loads are in flight (R = 2; the
+    // 128-VGPR lean R = 1 kernel spills with them live: it draws at the store)
+    constexpr bool kEarly = DMASK && R > 1;
+    uint32_t kb[kEarly ? R : 1][kEarly ? VPL : 1];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t row = rb + r < r1 ? rb + r : r1 - 1;  // tail: recompute a valid row, store nothing
@@ -221,6 +255,20 @@ __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(R == 1 
           if (kHoist && gres) L8<XD>::ld(gres, row * D + vi * 8, gr[kHoist ? r : 0][kHoist ? j : 0]);
         }
       }
+    }
+    if constexpr (kEarly) {
+      const uint64_t off = da.offset + (da.offset_dev ? static_cast<uint64_t>(*da.offset_dev) : 0);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+          bool kp[8];
+          drop8(da, off, (rb + r) * D + (lane + j * LPR) * 8, kp);
+          uint32_t bits = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) bits |= kp[k] ? (1u << k) : 0u;
+          kb[kEarly ? r : 0][kEarly ? j : 0] = bits;
+        }
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -258,6 +306,22 @@ __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(R == 1 
             for (int k = 0; k < 8; ++k) o[k] += gr[kHoist ? r : 0][kHoist ? j : 0][k];
           }
           L8<XD>::st(dx, (rb + r) * D + vi * 8, o);
+          if constexpr (DMASK) {
+            uint32_t bits;
+            if constexpr (kEarly) {
+              bits = kb[kEarly ? r : 0][kEarly ? j : 0];
+            } else {
+              const uint64_t off = da.offset + (da.offset_dev ? static_cast<uint64_t>(*da.offset_dev) : 0);
+              bool kp[8];
+              drop8(da, off, (rb + r) * D + vi * 8, kp);
+              bits = 0;
+#pragma unroll
+              for (int k = 0; k < 8; ++k) bits |= kp[k] ? (1u << k) : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] = (bits >> k) & 1u ? o[k] * da.scale : 0.f;
+            L8<LN_BF16>::st(da.out, (rb + r) * D + vi * 8, o);
+          }
         }
       }
     }
@@ -341,14 +405,15 @@ __global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk,
   }
 }
 
-template <int XD, int YD>
+template <int XD, int YD, bool DA>
 void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w, const float* b, void* y, float* mean,
-                  float* rstd, int64_t rows, int D, float eps) {
-#define DK_LNF(V) \
-  hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V, kRows>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, eps)
-#define DK_LNF_H(V)                                                                                        \
-  hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V, kRows, 32>), dim3((g.x + 1) / 2), dim3(kT), 0, s, x, w, b, y, mean, \
-                     rstd, rows, D, eps)
+                  float* rstd, int64_t rows, int D, float eps, const LnDropAdd& da) {
+#define DK_LNF(V)                                                                                                  \
+  hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V, kRows, 64, DA>), g, dim3(kT), 0, s, x, w, b, y, mean, rstd, rows, D, \
+                     eps, da)
+#define DK_LNF_H(V)                                                                                              \
+  hipLaunchKernelGGL((ln_fwd_kernel<XD, YD, V, kRows, 32, DA>), dim3((g.x + 1) / 2), dim3(kT), 0, s, x, w, b, y, \
+                     mean, rstd, rows, D, eps, da)
   switch (vpl) {
     case 103: DK_LNF_H(3); break;
     case 1: DK_LNF(1); break;
@@ -360,19 +425,19 @@ void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w,
 #undef DK_LNF_H
 }
 
-template <int XD, int YD>
+template <int XD, int YD, bool DA>
 void bwd_dispatch(int vpl, dim3 g, size_t sm, hipStream_t s, const void* dy, const void* x, const float* w,
                   const float* mean, const float* rstd, void* dx, float* part, int64_t rows, int D, int rpb,
-                  const void* gres, const void* dy2) {
-#define DK_LNB(V) \
-  hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, kRows>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, \
-                     rpb, gres, dy2)
-#define DK_LNB_H(V)                                                                                             \
-  hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, 1, 32>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, \
-                     D, rpb, gres, dy2)
+                  const void* gres, const void* dy2, const LnDropAdd& da) {
+#define DK_LNB(V)                                                                                                   \
+  hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, kRows, 64, DA>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, \
+                     rows, D, rpb, gres, dy2, da)
+#define DK_LNB_H(V)                                                                                                 \
+  hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, 1, 32, DA>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, \
+                     D, rpb, gres, dy2, da)
   if (vpl == -2) {
-    hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, 2, 1>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb,
-                       gres, dy2);
+    hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, 2, 1, 64, DA>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows,
+                       D, rpb, gres, dy2, da);
     return;
   }
   switch (vpl) {
@@ -433,29 +498,44 @@ int ln_bwd_blocks(int64_t rows, int D) {  // workspace rows: the partials + the 
 }
 
 void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const float* b, void* y, float* mean,
-                float* rstd, int64_t rows, int D, float eps, hipStream_t s) {
+                float* rstd, int64_t rows, int D, float eps, hipStream_t s, const LnDropAdd* da) {
   const dim3 g(static_cast<unsigned>((rows + kWaves * kRows - 1) / (kWaves * kRows)));
   const int vpl = vpl_for(D);
-  if (xdtype == LN_BF16) fwd_dispatch<LN_BF16, LN_BF16>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
-  else if (ydtype == LN_BF16) fwd_dispatch<LN_F32, LN_BF16>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
-  else fwd_dispatch<LN_F32, LN_F32>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps);
+  const LnDropAdd none{};
+  const LnDropAdd& a = da ? *da : none;
+#define DK_FD(X, Y)                                                                       \
+  do {                                                                                    \
+    if (da) fwd_dispatch<X, Y, true>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps, a);  \
+    else fwd_dispatch<X, Y, false>(vpl, g, s, x, w, b, y, mean, rstd, rows, D, eps, a);    \
+  } while (0)
+  if (xdtype == LN_BF16) DK_FD(LN_BF16, LN_BF16);
+  else if (ydtype == LN_BF16) DK_FD(LN_F32, LN_BF16);
+  else DK_FD(LN_F32, LN_F32);
+#undef DK_FD
 }
 
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
                  const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
-                 hipStream_t s, const void* gres, const void* dy2) {
+                 hipStream_t s, const void* gres, const void* dy2, const LnDropAdd* da) {
   const int nblk = ln_bwd_grid(rows, D, xdtype);
   const int rpb = static_cast<int>((rows + nblk - 1) / nblk);
   const size_t sm = sizeof(float) * kWaves * 2 * D;
   int vpl = vpl_for(D);
   if (vpl == 103) vpl = 2;  // half-wave rows: forward only (measured slower backward)
   if (ln_bwd_lean(D, xdtype)) vpl = -2;
-  if (xdtype == LN_BF16)
-    bwd_dispatch<LN_BF16, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2);
-  else if (ydtype == LN_BF16)
-    bwd_dispatch<LN_F32, LN_BF16>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2);
-  else
-    bwd_dispatch<LN_F32, LN_F32>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2);
+  const LnDropAdd none{};
+  const LnDropAdd& a = da ? *da : none;
+#define DK_BD(X, Y)                                                                                                 \
+  do {                                                                                                              \
+    if (da)                                                                                                         \
+      bwd_dispatch<X, Y, true>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2, a);  \
+    else                                                                                                            \
+      bwd_dispatch<X, Y, false>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2, a); \
+  } while (0)
+  if (xdtype == LN_BF16) DK_BD(LN_BF16, LN_BF16);
+  else if (ydtype == LN_BF16) DK_BD(LN_F32, LN_BF16);
+  else DK_BD(LN_F32, LN_F32);
+#undef DK_BD
   const int z = ln_colsum_groups(nblk);
   if (z > 0) {
     float* part2 = part + static_cast<int64_t>(nblk) * 2 * D;

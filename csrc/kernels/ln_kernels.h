@@ -11,15 +11,32 @@ namespace kern {
 
 enum LnDType : int { LN_F32 = 0, LN_BF16 = 1 };
 
+// Residual dropout fused into the LayerNorm (transformer blocks: x = res +
+// dropout(branch) feeding a LayerNorm). Forward: the LN input is res (the x
+// argument, x dtype) + keep · scale · xb (bf16), written to `out` (x dtype)
+// as the LN reads it. Backward: `out` (bf16) also receives dx · keep · scale,
+// the branch's gradient. keep(element e) = Philox(seed, offset + e / 4)[e % 4]
+// >= thr — the mask of dropout.hip's kernels for the same (seed, offset), so
+// the fused and unfused paths draw identical masks.
+struct LnDropAdd {
+  const void* xb;
+  void* out;
+  uint32_t thr;
+  float scale;
+  uint64_t seed;
+  uint64_t offset;
+  const int64_t* offset_dev;
+};
+
 bool ln_supported(int D);
 int ln_bwd_blocks(int64_t rows, int D);
 // xdtype: x / dx; ydtype: y / dy (fp32->bf16 supported; bf16 x implies bf16 y)
 void ln_forward(int xdtype, int ydtype, const void* x, const float* w, const float* b, void* y, float* mean,
-                float* rstd, int64_t rows, int D, float eps, hipStream_t s);
+                float* rstd, int64_t rows, int D, float eps, hipStream_t s, const LnDropAdd* da = nullptr);
 // part: workspace [ln_bwd_blocks(rows, D) * 2 * D] fp32; accum: dw / db += instead of =
 void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const float* w, const float* mean,
                  const float* rstd, void* dx, float* dw, float* db, float* part, int64_t rows, int D, bool accum,
-                 hipStream_t s, const void* gres = nullptr, const void* dy2 = nullptr);
+                 hipStream_t s, const void* gres = nullptr, const void* dy2 = nullptr, const LnDropAdd* da = nullptr);
 
 // Cross-entropy over [rows, V] logits (bf16/fp32, row stride ld elements).
 // Forward: loss[row] = lse - logit[target] (0 for ignore_index), lse saved.

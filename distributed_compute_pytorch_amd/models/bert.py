@@ -23,7 +23,8 @@ from ..ops.embedding import FusedEmbedding
 from ..ops.linear import FusedLinear, LinearWeightPrep, fused_mlp_gelu, packed_linear
 from ..ops.lm_head import lm_head_cross_entropy, padded_vocab
 from ..ops.dropout import dropout_add
-from ..ops.layernorm import FusedLayerNorm
+from ..ops import layernorm as ln_mod
+from ..ops.layernorm import FusedLayerNorm, dropout_add_layer_norm
 
 
 def _plain_dropout_add(x, residual, p, training):
@@ -102,13 +103,22 @@ class BertLayer(nn.Module):
         residual add) are summed inside the LN backward instead of by an add."""
         dual = isinstance(self.attn_ln, FusedLayerNorm)
         x_res = x if x_res is None else x_res
-        h = self._dadd(self.attn_out(self.attention(x, mask)), x_res, self.p, self.training)
-        x, xa = self.attn_ln.forward_dual_out(h) if dual else (self.attn_ln(h), None)
+        fuse = dual and ln_mod.FUSE_DADD_LN
+        if fuse:  # residual dropout-add inside the LayerNorm kernels (ops.layernorm.dropout_add_layer_norm)
+            x, xa = dropout_add_layer_norm(self.attn_out(self.attention(x, mask)), x_res, self.attn_ln, self.p,
+                                           self.training, 2)
+        else:
+            h = self._dadd(self.attn_out(self.attention(x, mask)), x_res, self.p, self.training)
+            x, xa = self.attn_ln.forward_dual_out(h) if dual else (self.attn_ln(h), None)
         if isinstance(self.intermediate, FusedLinear):
             # one node: GELU in the first GEMM's epilogue, its backward in the second's dgrad epilogue
             o = fused_mlp_gelu(x, self.intermediate, self.output, "none")
         else:
             o = self.output(F.gelu(self.intermediate(x)))
+        if fuse:
+            if dual_out:
+                return dropout_add_layer_norm(o, xa, self.out_ln, self.p, self.training, 2)
+            return dropout_add_layer_norm(o, xa, self.out_ln, self.p, self.training, 0)
         h = self._dadd(o, x if xa is None else xa, self.p, self.training)
         if dual_out and dual:
             return self.out_ln.forward_dual_out(h)

@@ -26,7 +26,8 @@ from ..ops.embedding import FusedEmbedding
 from ..ops.linear import FusedLinear, LinearWeightPrep, fused_mlp_gelu
 from ..ops.lm_head import lm_head_cross_entropy, padded_vocab
 from ..ops.dropout import dropout_add
-from ..ops.layernorm import FusedLayerNorm
+from ..ops import layernorm as ln_mod
+from ..ops.layernorm import FusedLayerNorm, dropout_add_layer_norm
 
 
 def _plain_dropout_add(x, residual, p, training):
@@ -100,6 +101,18 @@ class Block(nn.Module):
         self.p = cfg.dropout
         self._dadd = dropout_add if cfg.fused else _plain_dropout_add
 
+    def forward_pending(self, x, pending=None):
+        """The fused block: ``pending`` is the previous block's MLP output whose
+        residual dropout-add runs inside this block's first LayerNorm kernel
+        (ops.layernorm.dropout_add_layer_norm); returns (this block's MLP
+        output, the residual stream before its dropout-add)."""
+        if pending is None:
+            h, x = self.ln_1.forward_dual(x)
+        else:
+            h, x = dropout_add_layer_norm(pending, x, self.ln_1, self.p, self.training, 1)
+        h, x = dropout_add_layer_norm(self.attn(h), x, self.ln_2, self.p, self.training, 1)
+        return self.mlp(h), x
+
     def forward(self, x):
         if isinstance(self.ln_1, FusedLayerNorm):
             # dual-output LN: the residual stream's two gradients (branch + skip)
@@ -142,9 +155,15 @@ class GPT2(nn.Module):
             LinearWeightPrep.attach(self, heads={self.wte.weight: padded_vocab(self.cfg.vocab_size)})
         pos = torch.arange(T, device=idx.device)
         x = self.drop(self.wte(idx) + self.wpe(pos))
-        for blk in self.h:
-            x = blk(x)
-        x = self.ln_f(x)
+        if self.cfg.fused and ln_mod.FUSE_DADD_LN and isinstance(self.ln_f, FusedLayerNorm) and x.is_cuda:
+            pending = None
+            for blk in self.h:
+                pending, x = blk.forward_pending(x, pending)
+            x = dropout_add_layer_norm(pending, x, self.ln_f, self.cfg.dropout, self.training, 0)
+        else:
+            for blk in self.h:
+                x = blk(x)
+            x = self.ln_f(x)
         if targets is not None and self.cfg.fused:
             # tied head + cross-entropy as one node on our GEMMs (no logits returned)
             return lm_head_cross_entropy(x, self.wte.weight, None, targets)

@@ -16,6 +16,12 @@ from torch.nn import functional as F
 from .._ext import C as _C
 from .linear import _acc_target, accumulating
 
+import os
+
+# residual dropout + LayerNorm as one kernel each way in the GPT-2 / BERT
+# blocks (dropout_add_layer_norm); DCP_DADD_LN=0: separate dropout_add + LN
+FUSE_DADD_LN = os.environ.get("DCP_DADD_LN", "1") != "0"
+
 # under no_sync add dγ / dβ into the existing .grad inside the backward kernel
 # (False: leave it to autograd's AccumulateGrad; profiles/r1_ln_accum_ab74.txt)
 _LN_ACCUM = True
@@ -55,9 +61,9 @@ class _LNFn(torch.autograd.Function):
             tw, tb = _acc_target(ctx, ctx.params[0], D), _acc_target(ctx, ctx.params[1], D)
             if tw is not None and tb is not None:
                 acc = [tw, tb]
-        dx, dw, db = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd, accumulate_into=acc,
-                                       grad_residual=d2 if ctx.dual == 1 else None,
-                                       dy2=d2 if ctx.dual == 2 else None)
+        dx, dw, db, _ = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd, accumulate_into=acc,
+                                          grad_residual=d2 if ctx.dual == 1 else None,
+                                          dy2=d2 if ctx.dual == 2 else None)
         return dx, dw, db, None, None, None
 
 
@@ -103,3 +109,69 @@ class FusedLayerNorm(nn.LayerNorm):
     def forward_dual_out(self, x):
         """(self(x), alias of self(x)) — see :func:`fused_layer_norm_dual`."""
         return fused_layer_norm_dual(x, self.normalized_shape, self.weight, self.bias, self.eps, alias_output=True)
+
+
+class _DropAddLNFn(torch.autograd.Function):
+    """LayerNorm(res + dropout(branch)) in one kernel each way (LnDropAdd in
+    ``ln_kernels.h``): the forward writes the new residual stream x and the LN
+    output together; the backward writes dx (x's full gradient, the residual's
+    gradient) and the branch's gradient dx · keep / (1 - p) together. The mask
+    is dropout_add's (same Philox stream, same seed draw), so the fused and
+    unfused blocks compute the same values. ``mode`` 0: y; 1: (y, x) — pre-LN,
+    x is the next residual; 2: (y, alias of y) — post-LN."""
+
+    @staticmethod
+    def forward(ctx, branch, res, weight, bias, eps, out_dtype, p, rng, mode):
+        seed, off = rng
+        y, mean, rstd, xnew = _C.layer_norm_fwd(res, weight, bias, eps, out_dtype, branch=branch, p=p, seed=seed,
+                                                offset_dev=off)
+        ctx.save_for_backward(xnew, weight, bias, mean, rstd)
+        ctx.params = (weight, bias)
+        ctx.accum = accumulating()
+        ctx.mode, ctx.p, ctx.seed, ctx.off = mode, p, seed, off
+        if mode == 1:
+            return y, xnew
+        if mode == 2:
+            return y, y.view_as(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, d2=None):
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        acc = None
+        if _LN_ACCUM and weight is not None and bias is not None and ctx.needs_input_grad[2] and ctx.needs_input_grad[3]:
+            D = torch.Size((x.shape[-1],))
+            tw, tb = _acc_target(ctx, ctx.params[0], D), _acc_target(ctx, ctx.params[1], D)
+            if tw is not None and tb is not None:
+                acc = [tw, tb]
+        dx, dw, db, gb = _C.layer_norm_bwd(dy, x, weight, bias, mean, rstd, accumulate_into=acc,
+                                           grad_residual=d2 if ctx.mode == 1 else None,
+                                           dy2=d2 if ctx.mode == 2 else None, drop_p=ctx.p, drop_seed=ctx.seed,
+                                           drop_offset_dev=ctx.off, branch_grad=True)
+        return gb, dx, dw, db, None, None, None, None, None
+
+
+def dropout_add_layer_norm(branch, res, ln, p: float, training: bool, mode: int = 0):
+    """``ln(res + dropout(branch, p))`` — mode 0: y; 1: (y, x) with x = res +
+    dropout(branch) (pre-LN transformer blocks: x is the next residual); 2:
+    (y, alias of y) (post-LN blocks). One fused kernel each way on the GPU
+    (:class:`_DropAddLNFn`); elsewhere dropout_add then the LayerNorm."""
+    from .dropout import _take_offset, dropout_add
+
+    D = res.shape[-1]
+    if (training and p > 0.0 and isinstance(ln, FusedLayerNorm) and res.is_cuda and len(ln.normalized_shape) == 1
+            and branch.dtype == torch.bfloat16 and res.dtype in (torch.float32, torch.bfloat16)
+            and branch.shape == res.shape and _C.layer_norm_supported(D)):
+        out_dtype = None
+        if torch.is_autocast_enabled() and res.dtype == torch.float32:
+            out_dtype = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return _DropAddLNFn.apply(branch.contiguous(), res.contiguous(), ln.weight, ln.bias, ln.eps, out_dtype,
+                                      float(p), _take_offset(res.device, res.numel()), mode)
+    x = dropout_add(branch, res, p, training)
+    if mode == 0:
+        return ln(x)
+    if isinstance(ln, FusedLayerNorm):
+        return ln.forward_dual(x) if mode == 1 else ln.forward_dual_out(x)
+    y = ln(x)
+    return (y, x) if mode == 1 else (y, y)

@@ -180,6 +180,95 @@ def test_bert_dual_ln_matches_plain_ln(cuda):
             torch.testing.assert_close(p.grad, grads[n], rtol=1e-5, atol=1e-6, msg=n)
 
 
+@pytest.mark.parametrize("model", ["gpt2", "bert"])
+def test_dropout_add_ln_fusion_matches_unfused(cuda, model, monkeypatch):
+    """Residual dropout + LayerNorm as one kernel each way (LnDropAdd) vs the
+    separate dropout_add + LN kernels, with dropout on: the fused op draws the
+    same Philox masks (same seed draw per dropout), so loss and every gradient
+    agree (bf16 autocast, same rounding points)."""
+    from distributed_compute_pytorch_amd.models import bert as bm
+    from distributed_compute_pytorch_amd.models import gpt2 as g2
+    from distributed_compute_pytorch_amd.ops import layernorm as lnm
+
+    torch.manual_seed(0)
+    if model == "gpt2":
+        m = g2.GPT2(g2.GPT2Config(vocab_size=512, n_positions=128, n_embd=256, n_layer=2, n_head=4, dropout=0.2)).to(cuda)
+        ids = torch.randint(0, 512, (2, 128), device=cuda)
+        run = lambda: m(ids, ids)  # noqa: E731
+    else:
+        m = bm.BertForPreTraining(bm.BertConfig(vocab_size=128, hidden=256, layers=2, heads=4, intermediate=512,
+                                                max_position=128, dropout=0.2)).to(cuda)
+        ids = torch.randint(0, 128, (2, 128), device=cuda)
+        labels = torch.randint(0, 128, (2, 128), device=cuda)
+        run = lambda: m(ids, mlm_labels=labels)  # noqa: E731
+    m.train()
+    out = {}
+    for fuse in (False, True):
+        monkeypatch.setattr(lnm, "FUSE_DADD_LN", fuse)
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(7)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = run()
+        loss.backward()
+        out[fuse] = (loss.detach().float(), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+    torch.testing.assert_close(out[True][0], out[False][0], rtol=1e-3, atol=1e-3)
+    # (the key bias's gradient is zero in exact arithmetic — softmax ignores a
+    # per-query constant — so it is rounding noise: compared against the scale
+    # of the other gradients instead)
+    mx = max(float(g.norm()) for g in out[False][1].values())
+    for n, g in out[False][1].items():
+        d = float((out[True][1][n] - g).norm())
+        if float(g.norm()) < 1e-3 * mx:
+            assert d < 1e-3 * mx, (n, d, mx)
+        else:
+            assert d / float(g.norm()) < 2e-2, (n, d / float(g.norm()))
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("rdtype", [torch.float32, torch.bfloat16])
+def test_dropout_add_layer_norm_op(cuda, mode, rdtype):
+    """dropout_add_layer_norm vs dropout_add then the (dual) LayerNorm under
+    the same seed: outputs and the gradients of branch, residual, gamma, beta."""
+    from distributed_compute_pytorch_amd.ops.dropout import dropout_add
+    from distributed_compute_pytorch_amd.ops.layernorm import FusedLayerNorm, dropout_add_layer_norm
+
+    torch.manual_seed(3)
+    D = 768
+    ln = FusedLayerNorm(D).to(cuda)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.5, 0.5)
+    br = torch.randn(4, 37, D, device=cuda).to(torch.bfloat16)
+    res = torch.randn(4, 37, D, device=cuda).to(rdtype)
+    gy = torch.randn(4, 37, D, device=cuda)
+    g2 = torch.randn(4, 37, D, device=cuda)
+    outs = []
+    for fused in (True, False):
+        b_ = br.clone().requires_grad_()
+        r_ = res.clone().requires_grad_()
+        ln.zero_grad(set_to_none=True)
+        torch.manual_seed(11)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if fused:
+                o = dropout_add_layer_norm(b_, r_, ln, 0.3, True, mode)
+            else:
+                x = dropout_add(b_, r_, 0.3, True)
+                o = ln(x) if mode == 0 else (ln.forward_dual(x) if mode == 1 else ln.forward_dual_out(x))
+        if mode == 0:
+            (o.float() * gy).sum().backward()
+            ys = [o]
+        else:
+            ((o[0].float() * gy).sum() + (o[1].float() * g2).sum()).backward()
+            ys = list(o)
+        outs.append(([y.detach().float() for y in ys], b_.grad.float(), r_.grad.float(), ln.weight.grad.clone(),
+                     ln.bias.grad.clone()))
+    (yf, bf, rf, wf, bbf), (yu, bu, ru, wu, bbu) = outs
+    for a, b in zip(yf, yu):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)  # same kernels' math, same masks: identical
+    for a, b in ((bf, bu), (rf, ru), (wf, wu), (bbf, bbu)):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_layer_norm_dual_sums_both_gradients(cuda, dtype):
     """fused_layer_norm_dual: (ln(x), alias of x); the alias's gradient is added
@@ -226,10 +315,13 @@ def test_gpt2_dual_ln_matches_plain_ln(cuda):
         return self._dadd(self.mlp(self.ln_2(x)), x, self.p, self.training)
 
     g2.Block.forward = plain
+    fuse = g2.ln_mod.FUSE_DADD_LN
+    g2.ln_mod.FUSE_DADD_LN = False  # the per-block loop (Block.forward), not forward_pending
     try:
         m(idx, idx).backward()
     finally:
         g2.Block.forward = orig
+        g2.ln_mod.FUSE_DADD_LN = fuse
     for n, p in m.named_parameters():
         if p.grad is not None:
             torch.testing.assert_close(p.grad, grads[n], rtol=1e-5, atol=1e-6, msg=n)
