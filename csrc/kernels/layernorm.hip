@@ -200,8 +200,7 @@ __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(R == 1 
                                                     const float* __restrict__ rstd, void* __restrict__ dx,
                                                     float* __restrict__ part, int64_t rows, int D,
                                                     int rows_per_blk, const void* __restrict__ gres,
-                                                    const void* __restrict__ dy2, LnDropAdd da,
-                                                    float* __restrict__ adw, float* __restrict__ adb) {
+                                                    const void* __restrict__ dy2, LnDropAdd da) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [kWaves][2][D]
   const int lane = threadIdx.x & (LPR - 1);
   const int sub = LPR == 64 ? 0 : (threadIdx.x >> 5) & 1;  // half-wave (LPR = 32)
@@ -355,10 +354,7 @@ __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(R == 1 
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < kWaves; ++q) s += smem[(q * 2 + which) * D + col];
-    if (adw)  // atomic mode: straight into dγ / dβ (no partial rows, no reduction launches)
-      atomicAdd((which ? adb : adw) + col, s);
-    else
-      part[(static_cast<int64_t>(blockIdx.x) * 2 + which) * D + col] = s;
+    part[(static_cast<int64_t>(blockIdx.x) * 2 + which) * D + col] = s;
   }
 }
 
@@ -432,16 +428,16 @@ void fwd_dispatch(int vpl, dim3 g, hipStream_t s, const void* x, const float* w,
 template <int XD, int YD, bool DA>
 void bwd_dispatch(int vpl, dim3 g, size_t sm, hipStream_t s, const void* dy, const void* x, const float* w,
                   const float* mean, const float* rstd, void* dx, float* part, int64_t rows, int D, int rpb,
-                  const void* gres, const void* dy2, const LnDropAdd& da, float* adw, float* adb) {
+                  const void* gres, const void* dy2, const LnDropAdd& da) {
 #define DK_LNB(V)                                                                                                   \
   hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, kRows, 64, DA>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, \
-                     rows, D, rpb, gres, dy2, da, adw, adb)
+                     rows, D, rpb, gres, dy2, da)
 #define DK_LNB_H(V)                                                                                                 \
   hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, V, 1, 32, DA>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows, \
-                     D, rpb, gres, dy2, da, adw, adb)
+                     D, rpb, gres, dy2, da)
   if (vpl == -2) {
     hipLaunchKernelGGL((ln_bwd_kernel<XD, YD, 2, 1, 64, DA>), g, dim3(kT), sm, s, dy, x, w, mean, rstd, dx, part, rows,
-                       D, rpb, gres, dy2, da, adw, adb);
+                       D, rpb, gres, dy2, da);
     return;
   }
   switch (vpl) {
@@ -529,37 +525,17 @@ void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const fl
   if (ln_bwd_lean(D, xdtype)) vpl = -2;
   const LnDropAdd none{};
   const LnDropAdd& a = da ? *da : none;
-  // dγ / dβ by fp32 atomics from each workgroup instead of partial rows + the
-  // colsum / finalize launches — DCP_LN_ATOMIC=1; default: the deterministic
-  // two-level sum
-  static const bool atomic_env = [] {
-    const char* e = std::getenv("DCP_LN_ATOMIC");
-    return e != nullptr && e[0] == '1';
-  }();
-  // (not under HIP-graph capture: memset nodes are not reliably ordered before
-  // the kernels that read them on replay — the defect behind fused.cpp
-  // zeroed_floats — so captured steps keep the two-level sum)
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  (void)hipStreamIsCapturing(s, &cap);
-  const bool atomic = atomic_env && dw != nullptr && db != nullptr && cap == hipStreamCaptureStatusNone;
-  float* adw = atomic ? dw : nullptr;
-  float* adb = atomic ? db : nullptr;
-  if (atomic && !accum) {
-    (void)hipMemsetAsync(dw, 0, sizeof(float) * D, s);
-    (void)hipMemsetAsync(db, 0, sizeof(float) * D, s);
-  }
 #define DK_BD(X, Y)                                                                                                 \
   do {                                                                                                              \
     if (da)                                                                                                         \
-      bwd_dispatch<X, Y, true>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2, a, adw, adb);  \
+      bwd_dispatch<X, Y, true>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2, a);  \
     else                                                                                                            \
-      bwd_dispatch<X, Y, false>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2, a, adw, adb); \
+      bwd_dispatch<X, Y, false>(vpl, dim3(nblk), sm, s, dy, x, w, mean, rstd, dx, part, rows, D, rpb, gres, dy2, a); \
   } while (0)
   if (xdtype == LN_BF16) DK_BD(LN_BF16, LN_BF16);
   else if (ydtype == LN_BF16) DK_BD(LN_F32, LN_BF16);
   else DK_BD(LN_F32, LN_F32);
 #undef DK_BD
-  if (atomic) return;
   const int z = ln_colsum_groups(nblk);
   if (z > 0) {
     float* part2 = part + static_cast<int64_t>(nblk) * 2 * D;
