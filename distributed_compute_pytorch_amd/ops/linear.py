@@ -65,8 +65,19 @@ def _measure(cands: dict, rounds: int = 3) -> dict:
     """Best-of-``rounds`` per-call time of each candidate, the candidates
     interleaved (a single back-to-back pair flipped choices between runs on
     close shapes)."""
-    for fn in cands.values():
-        fn()
+    # a candidate the current tuning cannot run (e.g. the persistent ping-pong
+    # GEMM's bias epilogue past N = 7,168, gemm_tune "pp_v1" = 0) drops out
+    ok = {}
+    err = None
+    for k, fn in cands.items():
+        try:
+            fn()
+            ok[k] = fn
+        except RuntimeError as e:
+            err = e
+    if not ok:
+        raise err
+    cands = ok
     ts = {k: [] for k in cands}
     for _ in range(rounds):
         for k, fn in cands.items():
