@@ -16,6 +16,7 @@ from __future__ import annotations
 import argparse
 import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -138,23 +139,40 @@ def source_digest() -> str:
     return h.hexdigest()
 
 
+DIGEST_MARKER = b"DCP_SRC_DIGEST:"
+
+
 def embedded_digest(so: Path) -> str | None:
-    """The source digest linked into ``so`` (None if it carries none)."""
-    import ctypes
+    """The source digest linked into ``so`` (None if it carries none).
+
+    Read from the file's bytes (the digest object stores ``DIGEST_MARKER``
+    followed by the 40 hex digits), never by loading the library: a dlopen of
+    a stale ``_C`` here would stay mapped, and the import after a rebuild at
+    the same path would get that old mapping back from the dynamic loader."""
+    import mmap
 
     try:
-        lib = ctypes.CDLL(str(so))
-        return (ctypes.c_char * 41).in_dll(lib, DIGEST_SYMBOL).value.decode()
+        with open(so, "rb") as f, mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as m:
+            i = m.find(DIGEST_MARKER)
+            if i < 0:
+                return None
+            d = m[i + len(DIGEST_MARKER):i + len(DIGEST_MARKER) + 40]
     except (OSError, ValueError):
         return None
+    try:
+        d = d.decode("ascii")
+    except UnicodeDecodeError:
+        return None
+    return d if re.fullmatch(r"[0-9a-f]{40}", d) else None
 
 
 def _digest_obj(cxx, digest: str) -> Path:
-    src = BUILD / f"digest.{digest[:16]}.cpp"
-    obj = BUILD / f"digest.{digest[:16]}.o"
+    src = BUILD / f"digestm.{digest[:16]}.cpp"
+    obj = BUILD / f"digestm.{digest[:16]}.o"
     if not obj.exists():
-        src.write_text(f'extern "C" __attribute__((visibility("default"))) const char {DIGEST_SYMBOL}[41] = '
-                       f'"{digest}";\n')
+        marker = DIGEST_MARKER.decode()
+        src.write_text(f'extern "C" __attribute__((visibility("default"), used)) const char '
+                       f'{DIGEST_SYMBOL}[{len(marker) + 41}] = "{marker}{digest}";\n')
         r = subprocess.run(cxx + ["-c", str(src), "-o", str(obj)], capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
@@ -212,7 +230,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     for o in BUILD.glob("*.o"):
         if o.name not in keep:
             o.unlink()
-    for c in BUILD.glob("digest.*.cpp"):
+    for c in BUILD.glob("digest*.cpp"):
         if c.with_suffix(".o").name not in keep:
             c.unlink()
     return out

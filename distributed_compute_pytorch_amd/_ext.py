@@ -10,6 +10,7 @@ from __future__ import annotations
 import fcntl
 import importlib
 import os
+import sys
 
 import torch  # noqa: F401  (load torch's HIP runtime / RCCL before _C)
 
@@ -60,6 +61,12 @@ def load():
                 raise ImportError("stale")
             _C = _try_import()
         except ImportError:
+            if "distributed_compute_pytorch_amd._C" in sys.modules:
+                # a mapped library cannot be replaced in place: the loader would
+                # hand the old mapping back to the import after the rebuild
+                raise ImportError(
+                    f"distributed_compute_pytorch_amd._C is stale ({why}) and already loaded in this process; "
+                    "rebuild it (`python -m distributed_compute_pytorch_amd._build`) and restart")
             _build.build()
             importlib.invalidate_caches()
             _C = _try_import()
