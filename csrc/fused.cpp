@@ -526,6 +526,8 @@ at::Tensor conv1x1_dgrad(const at::Tensor& gy, const at::Tensor& wt) {
   return dx;
 }
 
+const at::Tensor& zero_row(const at::Tensor& like);
+
 // dw[Cout, Cin] (fp32) = Σ_m gy[m, :]^T ⊗ f(x)[m, :]
 // slots > 0: the split-M plan's workgroup budget for this call only (gemm_tune
 // "wg_slots", default 512) — the transformer Linear wgrad picks it per row count.
@@ -574,7 +576,7 @@ at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::o
                             gy.options().dtype(at::kFloat));
   kern::gemm_wgrad_bf16(gy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), M, static_cast<int>(N1),
                         static_cast<int>(N2), sc, sf, relu, ws.data_ptr<float>(), stream_of(gy), acc,
-                        static_cast<int>(out_rows));
+                        static_cast<int>(out_rows), zero_row(gy).data_ptr());
   return dw;
 }
 

@@ -1962,6 +1962,7 @@ void gemm_tune(const char* key, int value) {
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
   if (k.rfind("pp_", 0) == 0) gemm_pp_tune(key, value);
+  wgrad_pp_tune(key, value);
 }
 int gemm_tune_get(const char* key) {
   const std::string k(key);
@@ -1972,7 +1973,7 @@ int gemm_tune_get(const char* key) {
   if (k == "wg_cap") return g_wg_cap;
   if (k == "reserve_cus") return g_reserve_cus;
   if (k.rfind("pp_", 0) == 0) return gemm_pp_tune_get(key);
-  return -1;
+  return wgrad_pp_tune_get(key);
 }
 
 namespace {
@@ -2547,6 +2548,12 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
   const WgradPlan p = wgrad_plan_for(M, N1, N2, taps);
   const int64_t groups = (p.S + kSlabGroup - 1) / kSlabGroup;
   int64_t need = (static_cast<int64_t>(p.S) + (groups > 1 ? groups : 0)) * N1 * taps * N2;
+  if (wgrad_pp_supported(M, N1, N2, taps)) {  // the ping-pong kernel's slabs (+ the reduction's partial groups)
+    const WgradPPPlan q = wgrad_pp_plan(M, N1, N2, taps);
+    const int64_t g2 = (q.S + kSlabGroup - 1) / kSlabGroup;
+    const int64_t need2 = (static_cast<int64_t>(q.S) + (g2 > 1 ? g2 : 0)) * N1 * taps * N2;
+    if (need2 > need) need = need2;
+  }
   // direct 3x3 / 64-channel wgrad: ≤ 256 workgroup slabs + 16 partial groups
   if (N1 == 64 && N2 == 64 && taps == 9 && need < int64_t(272) * 64 * 576) need = int64_t(272) * 64 * 576;
   return need;
@@ -2558,11 +2565,27 @@ void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc
 template <bool GATHER>
 void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
                   const float* shift, bool relu, float* ws, int taps, const ConvGeo& geo, hipStream_t s,
-                  bool acc = false, int rows_out = -1) {
+                  bool acc = false, int rows_out = -1, const void* zero = nullptr) {
   const int order = wgrad_order();
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);
   const int ldo = taps * N2;
+  // the 8-wave ping-pong kernel (wgrad_pp.hip) where its 256 x 256 tiles fit
+  // and no BN prologue applies to B
+  if (scale == nullptr && zero != nullptr && !(GATHER && wgrad_mtap(N2, taps)) &&
+      wgrad_pp_supported(M, N1, N2, taps)) {
+    const WgradPPPlan p = wgrad_pp_plan(M, N1, N2, taps);
+    const WgradPPGeo g{geo.H, geo.W, geo.Ho, geo.Wo, geo.stride, geo.pad, geo.kw};
+    const int rows = rows_out >= 0 ? rows_out : N1;
+    if (p.S == 1) {  // one slab: straight into D (+= when accumulating), no reduction launch
+      gemm_wgrad_pp(A, B, D, M, N1, N2, taps, p, GATHER ? &g : nullptr, zero, acc, rows, s);
+      return;
+    }
+    gemm_wgrad_pp(A, B, ws, M, N1, N2, taps, p, GATHER ? &g : nullptr, zero, false, N1, s);
+    slab_reduce(ws, D, static_cast<int64_t>(N1) * ldo / 4, p.S, s, acc,
+                rows_out >= 0 ? static_cast<int64_t>(rows_out) * ldo / 4 : -1);
+    return;
+  }
   if constexpr (GATHER) {
     if (wgrad_mtap(N2, taps)) {
       const WgradPlan p = wgrad_plan_for(M, N1, N2, taps);
@@ -2610,9 +2633,10 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
 }  // namespace
 
 void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
-                     const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate, int rows_out) {
+                     const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate, int rows_out,
+                     const void* zero) {
   ConvGeo geo{};
-  wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s, accumulate, rows_out);
+  wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s, accumulate, rows_out, zero);
 }
 
 void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int W, int Cout, float* ws,
@@ -2677,7 +2701,7 @@ void conv_wgrad_bf16(const void* dY, const void* X, float* D, int N, int H, int 
   }
   ConvGeo geo{H, W, Ho, Wo, stride, pad, kw, static_cast<const uint16_t*>(zero)};
   wgrad_launch<true>(dY, X, D, static_cast<int64_t>(N) * Ho * Wo, Cout, Cin, nullptr, nullptr, false, ws, kh * kw,
-                     geo, s);
+                     geo, s, false, -1, zero);
 }
 
 namespace {

@@ -89,6 +89,26 @@ void weight_prep(const void* table, int n, int64_t tiles, hipStream_t s);
 // per block.
 void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s);
 
+// Weight gradient on the 8-wave ping-pong schedule (wgrad_pp.hip): 256 x 256
+// output tiles, split over rows m into `S` fp32 slabs of `chunk` rows (plan)
+// that gemm.hip's slab reduction sums; with S == 1 the kernel writes (acc:
+// adds into) D directly. geo != nullptr: B is the NHWC input of a kxk conv,
+// one tap per grid coordinate (zero: >= 2 KB of zero bytes, always needed).
+struct WgradPPGeo {
+  int H, W, Ho, Wo, stride, pad, kw;
+};
+struct WgradPPPlan {
+  int tiles, S;
+  int64_t chunk;
+};
+bool wgrad_pp_supported(int64_t M, int N1, int N2, int taps);
+WgradPPPlan wgrad_pp_plan(int64_t M, int N1, int N2, int taps);
+void gemm_wgrad_pp(const void* A, const void* B, float* out, int64_t M, int N1, int N2, int taps,
+                   const WgradPPPlan& p, const WgradPPGeo* geo, const void* zero, bool acc, int rows_lim,
+                   hipStream_t s);
+bool wgrad_pp_tune(const char* key, int value);  // false: not one of its keys
+int wgrad_pp_tune_get(const char* key);
+
 // Workspace (fp32 elements) gemm_wgrad_bf16 needs for this shape.
 int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps = 1);
 
@@ -96,9 +116,11 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps = 1);
 // (f = optional per-column scale/shift/relu). Deterministic: split over M
 // into fp32 slabs in `ws`, then one reduction launch. rows_out ≥ 0: D holds
 // only the first rows_out rows (the rest of A's columns are padding).
+// zero: >= 2 KB of zero bytes (the ping-pong kernel's padding rows; without
+// it the ring kernel runs).
 void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
                      const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate = false,
-                     int rows_out = -1);
+                     int rows_out = -1, const void* zero = nullptr);
 
 // Weight gradient of a kh×kw NHWC convolution (implicit GEMM, one tap per
 // grid.z): D[Cout][kh][kw][Cin] (fp32; = a channels_last OIHW tensor) =
