@@ -84,6 +84,9 @@ def parse():
                          "its reduction lands (-1: on for the transformers, whose ready-last embedding bucket "
                          "is 90-150 MB)")
     ap.add_argument("--grad-as-view", type=int, default=1)
+    ap.add_argument("--defer-wgrad", type=int, default=-1,
+                    help="DDP defer_accum_wgrad: the no_sync micro-steps' Linear weight gradients are computed by the "
+                         "synchronising micro-step in one launch over all micro-steps' rows (-1: on when grad_accum > 1)")
     ap.add_argument("--benchmark-cudnn", type=int, default=1)
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole step in a HIP graph (-1: per model — on for the launch-bound "
@@ -286,6 +289,8 @@ def main():
             ov = a.overlap_optimizer if a.overlap_optimizer >= 0 else int(a.model in ("gpt2", "bert"))
             if ov and a.grad_as_view:
                 kw["overlap_optimizer"] = True
+            if (a.defer_wgrad if a.defer_wgrad >= 0 else int(wl.accum > 1)):
+                kw["defer_accum_wgrad"] = True
             with stream_ctx():
                 ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[local],
                                                            gradient_as_bucket_view=bool(a.grad_as_view), **kw)
@@ -369,6 +374,7 @@ def main():
                 cfg["first_bucket_mb"] = round(info["first_bucket_bytes"] / 2**20, 3)
                 cfg["tail_bucket_mb"] = round(ddp.tail_bucket_bytes / 2**20, 3)
                 cfg["overlap_optimizer"] = bool(ddp.overlap_optimizer)
+                cfg["defer_accum_wgrad"] = bool(getattr(ddp, "defer_accum_wgrad", False))
                 cfg["buckets_mb"] = [round(b / 2**20, 2) for b in info["bucket_sizes"]]
             elif cap_mb is not None:
                 cfg["bucket_cap_mb"] = cap_mb

@@ -191,6 +191,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                return res.cast<WorkPtr>();
              }, wdt);
            }, py::arg("fn"), py::arg("wire_dtype") = py::none())
+      .def("set_deferred_grad_hook", [](Reducer& r, py::object fn) {
+             if (fn.is_none()) {
+               r.set_deferred_grad_hook(nullptr);
+               return;
+             }
+             auto holder = std::make_shared<py::object>(fn);
+             r.set_deferred_grad_hook([holder](int64_t k, const std::vector<at::Tensor>& views) {
+               py::gil_scoped_acquire g;
+               return (*holder)(k, views).cast<std::vector<at::Tensor>>();
+             });
+           }, py::arg("fn"))
       .def("bucket_indices", &Reducer::bucket_indices)
       .def("bucket_sizes_bytes", &Reducer::bucket_sizes_bytes)
       .def("bucket_stats", &Reducer::bucket_stats)

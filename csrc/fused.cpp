@@ -580,6 +580,45 @@ at::Tensor conv1x1_wgrad(const at::Tensor& gy, const at::Tensor& x, const c10::o
   return dw;
 }
 
+// dw = Σ_i gys[i]ᵀ · xs[i] over up to 4 row segments (the micro-steps of a
+// gradient accumulation) in one wgrad launch; same contract as conv1x1_wgrad.
+at::Tensor conv1x1_wgrad_multi(const std::vector<at::Tensor>& gys, const std::vector<at::Tensor>& xs,
+                               const c10::optional<at::Tensor>& accumulate_into, int64_t out_rows) {
+  DK_CHECK(!gys.empty() && gys.size() == xs.size() && gys.size() <= static_cast<size_t>(kern::kWgradMaxSegs),
+            "conv1x1_wgrad_multi: 1-4 (gy, x) segments");
+  const int64_t N1 = gys[0].size(-1), N2 = xs[0].size(-1);
+  DK_CHECK(N1 % 64 == 0 && N2 % 64 == 0, "conv1x1_wgrad_multi: channels must be multiples of 64");
+  c10::hip::HIPGuard guard(gys[0].device().index());
+  kern::WgradPPSegs sg{};
+  sg.n = static_cast<int>(gys.size());
+  for (size_t i = 0; i < gys.size(); ++i) {
+    check_gemm_act(gys[i], "conv1x1_wgrad_multi");
+    check_gemm_act(xs[i], "conv1x1_wgrad_multi");
+    DK_CHECK(gys[i].size(-1) == N1 && xs[i].size(-1) == N2 && gys[i].device() == gys[0].device() &&
+                  xs[i].device() == gys[0].device(),
+              "conv1x1_wgrad_multi: segments must share the channel counts and the device");
+    const int64_t M = gys[i].numel() / N1;
+    DK_CHECK(xs[i].numel() / N2 == M && M > 0, "conv1x1_wgrad_multi: row mismatch");
+    sg.A[i] = gys[i].data_ptr();
+    sg.B[i] = xs[i].data_ptr();
+    sg.M[i] = M;
+  }
+  DK_CHECK(out_rows < 0 || (out_rows <= N1 && (out_rows * N2) % 4 == 0), "conv1x1_wgrad_multi: out_rows");
+  const int64_t R1 = out_rows < 0 ? N1 : out_rows;
+  const bool acc = accumulate_into.has_value() && accumulate_into->defined();
+  if (acc)
+    DK_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
+                  accumulate_into->numel() == R1 * N2 && accumulate_into->device() == gys[0].device(),
+              "conv1x1_wgrad_multi: accumulate_into must be a contiguous fp32 [N1, N2] tensor on the same device");
+  at::Tensor dw = acc ? *accumulate_into : at::empty({R1, N2}, gys[0].options().dtype(at::kFloat));
+  at::Tensor ws = at::empty({kern::gemm_wgrad_multi_workspace(sg, static_cast<int>(N1), static_cast<int>(N2))},
+                            gys[0].options().dtype(at::kFloat));
+  kern::gemm_wgrad_multi_bf16(sg, dw.data_ptr<float>(), static_cast<int>(N1), static_cast<int>(N2),
+                              ws.data_ptr<float>(), stream_of(gys[0]), acc, static_cast<int>(out_rows),
+                              zero_row(gys[0]).data_ptr());
+  return dw;
+}
+
 // ≥ 256 zeroed bytes per device: the padding row of the gathered wgrad
 const at::Tensor& zero_row(const at::Tensor& like) {
   static std::mutex mu;
@@ -1689,6 +1728,10 @@ void bind(pybind11::module& m) {
         pybind11::arg("scale") = pybind11::none(), pybind11::arg("shift") = pybind11::none(),
         pybind11::arg("relu") = false, pybind11::arg("accumulate_into") = pybind11::none(),
         pybind11::arg("out_rows") = -1, pybind11::arg("slots") = 0);
+  m.def("conv1x1_wgrad_multi", &conv1x1_wgrad_multi,
+        "dW = sum over 1-4 (gy, x) row segments (gradient-accumulation micro-steps) in one wgrad launch",
+        pybind11::arg("gys"), pybind11::arg("xs"), pybind11::arg("accumulate_into") = pybind11::none(),
+        pybind11::arg("out_rows") = -1);
   m.def("bn_act_bwd", &bn_act_bwd, "fused NHWC BatchNorm(+residual)(+ReLU) backward", pybind11::arg("gy"),
         pybind11::arg("gy2"), pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"),
         pybind11::arg("mean"), pybind11::arg("invstd"), pybind11::arg("y"), pybind11::arg("act"),

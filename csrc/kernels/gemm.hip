@@ -2577,11 +2577,12 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
     const WgradPPPlan p = wgrad_pp_plan(M, N1, N2, taps);
     const WgradPPGeo g{geo.H, geo.W, geo.Ho, geo.Wo, geo.stride, geo.pad, geo.kw};
     const int rows = rows_out >= 0 ? rows_out : N1;
+    const WgradPPSegs sg{1, {A}, {B}, {M}};
     if (p.S == 1) {  // one slab: straight into D (+= when accumulating), no reduction launch
-      gemm_wgrad_pp(A, B, D, M, N1, N2, taps, p, GATHER ? &g : nullptr, zero, acc, rows, s);
+      gemm_wgrad_pp(sg, D, N1, N2, taps, p, GATHER ? &g : nullptr, zero, acc, rows, s);
       return;
     }
-    gemm_wgrad_pp(A, B, ws, M, N1, N2, taps, p, GATHER ? &g : nullptr, zero, false, N1, s);
+    gemm_wgrad_pp(sg, ws, N1, N2, taps, p, GATHER ? &g : nullptr, zero, false, N1, s);
     slab_reduce(ws, D, static_cast<int64_t>(N1) * ldo / 4, p.S, s, acc,
                 rows_out >= 0 ? static_cast<int64_t>(rows_out) * ldo / 4 : -1);
     return;
@@ -2637,6 +2638,38 @@ void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, 
                      const void* zero) {
   ConvGeo geo{};
   wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s, accumulate, rows_out, zero);
+}
+
+int64_t gemm_wgrad_multi_workspace(const WgradPPSegs& sg, int N1, int N2) {
+  int64_t need = gemm_wgrad_workspace(wgrad_pp_rows(sg), N1, N2, 1);
+  for (int i = 0; i < sg.n; ++i) {
+    const int64_t w = gemm_wgrad_workspace(sg.M[i], N1, N2, 1);
+    if (w > need) need = w;
+  }
+  return need;
+}
+
+void gemm_wgrad_multi_bf16(const WgradPPSegs& sg, float* D, int N1, int N2, float* ws, hipStream_t s, bool accumulate,
+                           int rows_out, const void* zero) {
+  const int64_t M = wgrad_pp_rows(sg);
+  if (sg.n == 1 || !(zero != nullptr && wgrad_pp_supported(M, N1, N2, 1))) {
+    // one launch per segment (the ring kernel, or nothing to merge); the
+    // later ones add into D
+    ConvGeo geo{};
+    for (int i = 0; i < sg.n; ++i)
+      wgrad_launch<false>(sg.A[i], sg.B[i], D, sg.M[i], N1, N2, nullptr, nullptr, false, ws, 1, geo, s,
+                          accumulate || i > 0, rows_out, zero);
+    return;
+  }
+  const WgradPPPlan p = wgrad_pp_plan(M, N1, N2, 1);
+  const int rows = rows_out >= 0 ? rows_out : N1;
+  if (p.S == 1) {
+    gemm_wgrad_pp(sg, D, N1, N2, 1, p, nullptr, zero, accumulate, rows, s);
+    return;
+  }
+  gemm_wgrad_pp(sg, ws, N1, N2, 1, p, nullptr, zero, false, N1, s);
+  slab_reduce(ws, D, static_cast<int64_t>(N1) * N2 / 4, p.S, s, accumulate,
+              rows_out >= 0 ? static_cast<int64_t>(rows_out) * N2 / 4 : -1);
 }
 
 void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int W, int Cout, float* ws,

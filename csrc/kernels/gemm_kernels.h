@@ -99,13 +99,23 @@ struct WgradPPGeo {
 };
 struct WgradPPPlan {
   int tiles, S;
-  int64_t chunk;
+  int64_t chunk;  // rows per slab (a multiple of 64)
 };
+// The rows m of one weight gradient as up to kWgradMaxSegs segments (the
+// micro-steps of a gradient accumulation, summed by ONE launch): segment i is
+// A[i] [M[i], N1] and B[i] [M[i], N2]; each is padded to whole 64-row K-tiles.
+constexpr int kWgradMaxSegs = 4;
+struct WgradPPSegs {
+  int n;
+  const void* A[kWgradMaxSegs];
+  const void* B[kWgradMaxSegs];
+  int64_t M[kWgradMaxSegs];
+};
+int64_t wgrad_pp_rows(const WgradPPSegs& sg);  // rows of the padded concatenation (the plan's M)
 bool wgrad_pp_supported(int64_t M, int N1, int N2, int taps);
 WgradPPPlan wgrad_pp_plan(int64_t M, int N1, int N2, int taps);
-void gemm_wgrad_pp(const void* A, const void* B, float* out, int64_t M, int N1, int N2, int taps,
-                   const WgradPPPlan& p, const WgradPPGeo* geo, const void* zero, bool acc, int rows_lim,
-                   hipStream_t s);
+void gemm_wgrad_pp(const WgradPPSegs& sg, float* out, int N1, int N2, int taps, const WgradPPPlan& p,
+                   const WgradPPGeo* geo, const void* zero, bool acc, int rows_lim, hipStream_t s);
 bool wgrad_pp_tune(const char* key, int value);  // false: not one of its keys
 int wgrad_pp_tune_get(const char* key);
 
@@ -121,6 +131,13 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps = 1);
 void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
                      const float* shift, bool relu, float* ws, hipStream_t s, bool accumulate = false,
                      int rows_out = -1, const void* zero = nullptr);
+
+// gemm_wgrad_bf16 over several row segments (gradient-accumulation micro-steps)
+// in one ping-pong launch (+ the slab reduction) where the shape takes it,
+// else one launch per segment; D = Σ over all segments (+= when accumulate).
+int64_t gemm_wgrad_multi_workspace(const WgradPPSegs& sg, int N1, int N2);
+void gemm_wgrad_multi_bf16(const WgradPPSegs& sg, float* D, int N1, int N2, float* ws, hipStream_t s, bool accumulate,
+                           int rows_out, const void* zero);
 
 // Weight gradient of a kh×kw NHWC convolution (implicit GEMM, one tap per
 // grid.z): D[Cout][kh][kw][Cin] (fp32; = a channels_last OIHW tensor) =

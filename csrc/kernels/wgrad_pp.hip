@@ -38,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <stdexcept>
 #include <string>
 
 #include "gemm_kernels.h"
@@ -57,6 +58,7 @@ constexpr int kHT = 16384;              // half-tile bytes: 64 rows x 256 B
 constexpr int kSlot = 4 * kHT;          // one 64-deep K-tile
 constexpr int kSink = 2 * kSlot;        // 2 KB sink for the DMA of K-tiles past the slab's end
 constexpr int kLds = 2 * kSlot + 2048;  // 133,120 B: one workgroup per CU
+constexpr int kMaxSegs = kWgradMaxSegs;
 int g_wgpp = 1;                         // gemm_tune "wg_pp": 0 = the ring kernel everywhere
 int g_wgpp_slots = 256;                 // gemm_tune "wgpp_slots": workgroups the split over m aims for
 int g_wgpp_min_kt = 8;                  // gemm_tune "wgpp_min_kt": fewest K-tiles per slab
@@ -125,9 +127,9 @@ struct WpTrk {
 // ACC (single slab only): D += the tile instead of D = the tile.
 template <int GATHER, bool ACC>
 __global__ void __launch_bounds__(kPT, 1)
-    gemm_wgrad_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, float* __restrict__ out,
-                         int64_t M, int N1, int N2, int64_t chunk, int tiles_j, int ntiles, int ntaps, int ldo,
-                         int rows_lim, WgradPPGeo geo, const uint16_t* __restrict__ zero) {
+    gemm_wgrad_pp_kernel(WgradPPSegs sg, float* __restrict__ out, int N1, int N2, int64_t chunk, int tiles_j,
+                         int ntiles, int ntaps, int ldo, int rows_lim, WgradPPGeo geo,
+                         const uint16_t* __restrict__ zero) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -147,9 +149,20 @@ __global__ void __launch_bounds__(kPT, 1)
     by = rest / ntiles;
   }
   const int i0 = (bx / tiles_j) * 256, j0 = (bx % tiles_j) * 256;
-  const int64_t mz0 = static_cast<int64_t>(by) * chunk;
-  const int64_t mz1 = min(M, mz0 + chunk);
-  const int KT = static_cast<int>((mz1 - mz0 + 63) >> 6);
+  // the rows are the concatenation of sg.n segments (gradient-accumulation
+  // micro-steps), each padded to whole 64-row K-tiles: segment s owns global
+  // K-tiles [kt0[s], kt0[s + 1]); slab `by` covers chunk / 64 of them
+  int64_t kt0[kMaxSegs + 1];
+  kt0[0] = 0;
+#pragma unroll
+  for (int i = 0; i < kMaxSegs; ++i) kt0[i + 1] = kt0[i] + (i < sg.n ? (sg.M[i] + 63) >> 6 : 0);
+  const int64_t g0 = static_cast<int64_t>(by) * (chunk >> 6);
+  const int KT = static_cast<int>(min(kt0[kMaxSegs], g0 + (chunk >> 6)) - g0);
+  // GATHER (one segment): the operands and the slab's first row
+  const uint16_t* A = static_cast<const uint16_t*>(sg.A[0]);
+  const uint16_t* B = static_cast<const uint16_t*>(sg.B[0]);
+  const int64_t M = sg.M[0];
+  const int64_t mz0 = g0 * 64;
 
   // this lane's two DMA per half-tile: image row rq = 8 w + 4 q + lane / 16,
   // physical chunk lane % 16 = logical chunk lc (channel block of 8)
@@ -184,7 +197,7 @@ __global__ void __launch_bounds__(kPT, 1)
   }
   auto trk_src = [&](const WpTrk& k, int ch) -> const uint16_t* {
     const int hi = k.ho * geo.stride + gdy, wi = k.wo * geo.stride + gdx;
-    const bool ok = k.m < mz1 && static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
+    const bool ok = k.m < M && static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
                     static_cast<unsigned>(wi) < static_cast<unsigned>(geo.W);
     return wp_sel(ok, B + (static_cast<int64_t>(k.n * geo.H + hi) * geo.W + wi) * N2 + ch, zsrc);
   };
@@ -217,21 +230,28 @@ __global__ void __launch_bounds__(kPT, 1)
       return;
     }
     char* dst = lds + (kt & 1) * kSlot + h * kHT + w * 2048;
-    const int64_t mb = mz0 + static_cast<int64_t>(kt) * 64;
-    const int left = static_cast<int>(mz1 - mb);  // valid rows of this K-tile
+    // the K-tile's segment (uniform), its first row there and the rows it has left
+    const int64_t g = g0 + kt;
+    int sgi = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxSegs; ++i) sgi += (i < sg.n && g >= kt0[i]) ? 1 : 0;
+    const uint16_t* As = static_cast<const uint16_t*>(sg.A[sgi]);
+    const uint16_t* Bs = static_cast<const uint16_t*>(sg.B[sgi]);
+    const int64_t mb = (g - kt0[sgi]) * 64;
+    const int left = static_cast<int>(min(sg.M[sgi] - mb, int64_t(64)));  // valid rows of this K-tile
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const uint16_t* src;
       if (h == 0 || h == 3) {
         const int c = min(chA[q] + (h == 3 ? 64 : 0), N1 - 8);
-        src = wp_sel(rq[q] < left, A + (mb + rq[q]) * N1 + c, zsrc);
+        src = wp_sel(rq[q] < left, As + (mb + rq[q]) * N1 + c, zsrc);
       } else {
         const int c = min(chB[q] + (h == 2 ? 32 : 0), N2 - 8);
         if constexpr (GATHER) {
           src = trk_src(tk[h - 1][q], c);
           trk_adv(tk[h - 1][q]);
         } else {
-          src = wp_sel(rq[q] < left, B + (mb + rq[q]) * N2 + c, zsrc);
+          src = wp_sel(rq[q] < left, Bs + (mb + rq[q]) * N2 + c, zsrc);
         }
       }
       wp_glds(src, wp_lds_addr(dst + q * 1024));
@@ -354,8 +374,8 @@ __global__ void __launch_bounds__(kPT, 1)
 }
 
 template <int GATHER, bool ACC>
-void wgrad_pp_go(const void* A, const void* B, float* out, const WgradPPPlan& p, int64_t M, int N1, int N2, int taps,
-                 int rows_lim, const WgradPPGeo& geo, const void* zero, hipStream_t s) {
+void wgrad_pp_go(const WgradPPSegs& sg, float* out, const WgradPPPlan& p, int N1, int N2, int taps, int rows_lim,
+                 const WgradPPGeo& geo, const void* zero, hipStream_t s) {
   static const bool attr = [] {  // > 64 KB of dynamic LDS
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_wgrad_pp_kernel<GATHER, ACC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
@@ -363,9 +383,9 @@ void wgrad_pp_go(const void* A, const void* B, float* out, const WgradPPPlan& p,
   }();
   (void)attr;
   const int tiles_j = (N2 + 255) / 256;
-  hipLaunchKernelGGL((gemm_wgrad_pp_kernel<GATHER, ACC>), dim3(p.tiles * p.S * taps), dim3(kPT), kLds, s,
-                     static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), out, M, N1, N2, p.chunk,
-                     tiles_j, p.tiles, taps, taps * N2, rows_lim, geo, static_cast<const uint16_t*>(zero));
+  hipLaunchKernelGGL((gemm_wgrad_pp_kernel<GATHER, ACC>), dim3(p.tiles * p.S * taps), dim3(kPT), kLds, s, sg, out, N1,
+                     N2, p.chunk, tiles_j, p.tiles, taps, taps * N2, rows_lim, geo,
+                     static_cast<const uint16_t*>(zero));
 }
 }  // namespace
 
@@ -391,16 +411,22 @@ WgradPPPlan wgrad_pp_plan(int64_t M, int N1, int N2, int taps) {
   return p;
 }
 
-void gemm_wgrad_pp(const void* A, const void* B, float* out, int64_t M, int N1, int N2, int taps,
-                   const WgradPPPlan& p, const WgradPPGeo* geo, const void* zero, bool acc, int rows_lim,
-                   hipStream_t s) {
+int64_t wgrad_pp_rows(const WgradPPSegs& sg) {
+  int64_t kt = 0;
+  for (int i = 0; i < sg.n; ++i) kt += (sg.M[i] + 63) / 64;
+  return kt * 64;
+}
+
+void gemm_wgrad_pp(const WgradPPSegs& sg, float* out, int N1, int N2, int taps, const WgradPPPlan& p,
+                   const WgradPPGeo* geo, const void* zero, bool acc, int rows_lim, hipStream_t s) {
   const WgradPPGeo g = geo ? *geo : WgradPPGeo{1, 1, 1, 1, 1, 0, 1};
+  if (sg.n < 1 || sg.n > kMaxSegs || (geo && sg.n != 1)) throw std::runtime_error("gemm_wgrad_pp: bad segment list");
   if (geo) {
-    if (acc) wgrad_pp_go<1, true>(A, B, out, p, M, N1, N2, taps, rows_lim, g, zero, s);
-    else wgrad_pp_go<1, false>(A, B, out, p, M, N1, N2, taps, rows_lim, g, zero, s);
+    if (acc) wgrad_pp_go<1, true>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);
+    else wgrad_pp_go<1, false>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);
   } else {
-    if (acc) wgrad_pp_go<0, true>(A, B, out, p, M, N1, N2, taps, rows_lim, g, zero, s);
-    else wgrad_pp_go<0, false>(A, B, out, p, M, N1, N2, taps, rows_lim, g, zero, s);
+    if (acc) wgrad_pp_go<0, true>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);
+    else wgrad_pp_go<0, false>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);
   }
 }
 

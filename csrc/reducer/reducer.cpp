@@ -471,10 +471,23 @@ void Reducer::finalize() {
   for (auto& b : buckets_) {
     if (defer) {
       // every .grad becomes its bucket view (host-only pointer swap, as the
-      // waiting path below does): the reduced values land there
-      for (size_t s = 0; s < b.params.size(); ++s) {
-        at::Tensor& grad = params_[b.params[s]].mutable_grad();
-        if (!grad.defined() || grad.data_ptr() != b.views[s].data_ptr()) grad = b.views[s];
+      // waiting path below does): the reduced values land there — or what
+      // the deferred-grad hook wraps each view in
+      if (deferred_grad_hook_) {
+        const int64_t k = static_cast<int64_t>(&b - buckets_.data());
+        std::vector<at::Tensor> gs = deferred_grad_hook_(k, b.views);
+        DK_CHECK(gs.size() == b.params.size(), "Reducer: deferred-grad hook returned ", gs.size(), " tensors for ",
+                 b.params.size(), " parameters");
+        for (size_t s = 0; s < b.params.size(); ++s) {
+          DK_CHECK(gs[s].data_ptr() == b.views[s].data_ptr() && gs[s].sizes() == b.views[s].sizes(),
+                   "Reducer: the deferred-grad hook must return the bucket views themselves (wrapped)");
+          params_[b.params[s]].mutable_grad() = gs[s];
+        }
+      } else {
+        for (size_t s = 0; s < b.params.size(); ++s) {
+          at::Tensor& grad = params_[b.params[s]].mutable_grad();
+          if (!grad.defined() || grad.data_ptr() != b.views[s].data_ptr()) grad = b.views[s];
+        }
       }
       b.deferred = true;
       b.launched = false;

@@ -92,6 +92,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
  public:
   // (bucket buffer, position of the bucket in this iteration's launch order)
   using CommHook = std::function<WorkPtr(at::Tensor& bucket, int64_t index)>;
+  // defer_grad_wait: what a deferred bucket's parameters get as .grad — given
+  // the bucket index and its gradient views, the tensors to install (the DDP
+  // wrapper hands out views that order every reader behind the reduction:
+  // parallel/ddp.py _PendingGrad). Unset: the plain views.
+  using DeferredGradHook = std::function<std::vector<at::Tensor>(int64_t index, const std::vector<at::Tensor>& views)>;
 
   Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t>> buckets,
           std::shared_ptr<Communicator> comm, ReducerOptions opts);
@@ -109,6 +114,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   // wire_dtype: the precision the hook's collective carries (a compression
   // hook declares bf16 / fp16; Undefined = the bucket's own dtype) — it sets
   // the rounding the debug stream-ordering check tolerates
+  void set_deferred_grad_hook(DeferredGradHook hook) { deferred_grad_hook_ = std::move(hook); }
   void set_comm_hook(CommHook hook, at::ScalarType wire_dtype = at::ScalarType::Undefined) {
     comm_hook_ = std::move(hook);
     hook_wire_ = wire_dtype;
@@ -179,6 +185,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void release_registrations();
   ReducerOptions opts_;
   CommHook comm_hook_;
+  DeferredGradHook deferred_grad_hook_;
   at::ScalarType hook_wire_ = at::ScalarType::Undefined;
 
   std::vector<Bucket> buckets_;

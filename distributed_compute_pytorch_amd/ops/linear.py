@@ -64,20 +64,10 @@ def _time_ms(fn, iters: int = 5) -> float:
 def _measure(cands: dict, rounds: int = 3) -> dict:
     """Best-of-``rounds`` per-call time of each candidate, the candidates
     interleaved (a single back-to-back pair flipped choices between runs on
-    close shapes)."""
-    # a candidate the current tuning cannot run (e.g. the persistent ping-pong
-    # GEMM's bias epilogue past N = 7,168, gemm_tune "pp_v1" = 0) drops out
-    ok = {}
-    err = None
-    for k, fn in cands.items():
-        try:
-            fn()
-            ok[k] = fn
-        except RuntimeError as e:
-            err = e
-    if not ok:
-        raise err
-    cands = ok
+    close shapes). A candidate's failure propagates: shapes a kernel cannot
+    take are left out of ``cands`` up front (``_fwd_cands`` / ``_pp_ok``)."""
+    for fn in cands.values():  # warm (first-launch setup) before timing
+        fn()
     ts = {k: [] for k in cands}
     for _ in range(rounds):
         for k, fn in cands.items():
@@ -90,13 +80,21 @@ def autotune_choices() -> dict:
     return {" ".join(str(k) for k in key): v for key, v in _CHOICE.items()}
 
 
+# how long a rank other than 0 waits for rank 0's choice of a shape
+_AGREE_WAIT_S = 5.0
+
+
 def _agree(key, mine: str) -> str:
-    """Every rank of the default group takes rank 0's choice for ``key`` (each
-    rank times on its own GPU and close shapes can time either way: ranks, and
-    through ``fused_mlp_gelu`` even their autograd graphs, would otherwise
-    differ). Through the rendezvous store, not a device collective: the first
-    call of a shape may sit inside a backward whose bucket collectives are in
-    flight."""
+    """Best-effort: every rank takes rank 0's choice for ``key`` when rank 0
+    has published it within ``_AGREE_WAIT_S`` (each rank times on its own GPU
+    and close shapes can time either way; with one choice every rank runs the
+    same kernels, the same numerics). Never blocks longer: a shape rank 0 does
+    not run, or reaches much later (uneven last batch, sequence bucketing,
+    rank-dependent code), keeps this rank's own measurement. That is safe —
+    a kernel choice only changes rounding; DDP averages the gradients, so the
+    replicas stay identical. Through the rendezvous store, not a device
+    collective: the first call of a shape may sit inside a backward whose
+    bucket collectives are in flight."""
     from .. import distributed as dist
 
     if not dist.is_initialized() or dist.get_world_size() == 1:
@@ -105,7 +103,13 @@ def _agree(key, mine: str) -> str:
     k = "dcp/linear_autotune/" + " ".join(str(x) for x in key)
     if pg.rank() == 0:
         pg.store.set(k, mine.encode())
-    return bytes(pg.store.get(k)).decode()
+        return mine
+    try:
+        pg.store.wait([k], int(_AGREE_WAIT_S * 1000))
+    except (RuntimeError, TimeoutError):  # rank 0 has no entry (yet): keep the local measurement
+        return mine
+    theirs = bytes(pg.store.get(k)).decode()
+    return theirs if theirs in _CANDIDATES else mine
 
 
 def _pick(key, cands: dict) -> str:
@@ -161,6 +165,13 @@ def autotune_times() -> dict:
 def _pp_ok(M: int, N: int, K: int) -> bool:
     """Shapes the ping-pong GEMM takes (K % 64, N % 8; 32-bit operand offsets)."""
     return K % 64 == 0 and N % 8 == 0 and M > 0 and M * K < 2**31 and N * K < 2**31
+
+
+def _pp_bias_ok(N: int) -> bool:
+    """The ping-pong GEMM's bias epilogue: the one-tile kernel (gemm_tune
+    "pp_v1" = 1, N % 8 == 0) takes any N; the persistent one stages the bias in
+    LDS next to its 133,120-B ring (≤ 160 KiB: N ≤ 7,168)."""
+    return (_C.gemm_tune_get("pp_v1") == 1 and N % 8 == 0) or N * 4 + 133120 <= 160 * 1024
 
 
 # let the fused Adam/AdamW write the bf16 weight copies the forward GEMMs read
@@ -246,6 +257,122 @@ def _acc_target(ctx, p, shape):
     return inplace_grad(p, shape, getattr(ctx, "accum", False))
 
 
+# ---- micro-step weight-gradient deferral -----------------------------------
+# DistributedDataParallel(defer_accum_wgrad=True): inside no_sync the Linear
+# weight gradients are not computed. Their operands (dY and the saved X) are
+# kept, and the synchronising micro-step computes each weight gradient over
+# the rows of ALL its micro-steps in one ping-pong wgrad launch
+# (_C.conv1x1_wgrad_multi, up to 4 row segments per launch): one split-over-rows
+# slab plan and one slab reduction per step instead of one per micro-step —
+# at GPT-2's 8,192-row micro-steps the slab writes and reduction are ~25 % of
+# each wgrad (profiles/r5_wgrad_dispatches*.txt). Costs the kept operands'
+# memory (~7 GB for GPT-2-small accum 4; the GPU has 288 GB).
+# Until then p.grad lacks the deferred contributions: flush_weight_grads()
+# adds them, and every optimizer step (a global torch.optim step pre-hook,
+# stock and fused optimizers alike) calls it first.
+_DEFER = [0]
+_PENDING: dict = {}  # id(first parameter of the group) -> _Pending
+_HOOKED = [False]
+
+
+class _Pending:
+    __slots__ = ("params", "rows", "segs")
+
+    def __init__(self, params, rows):
+        self.params, self.rows, self.segs = params, rows, []
+
+
+class defer_weight_grads:
+    """Context manager used by ``DistributedDataParallel.no_sync`` when the
+    DDP was built with ``defer_accum_wgrad=True``."""
+
+    def __enter__(self):
+        _DEFER[0] += 1
+        _install_flush_hook()
+        return self
+
+    def __exit__(self, *exc):
+        _DEFER[0] -= 1
+        return False
+
+
+def deferring() -> bool:
+    """Sampled by the forward into ``ctx.defer`` (as ``accumulating``)."""
+    return _DEFER[0] > 0
+
+
+def pending_weight_grads() -> int:
+    """Parameter groups whose gradient has deferred micro-step contributions."""
+    return len(_PENDING)
+
+
+def _install_flush_hook():
+    if not _HOOKED[0]:
+        from torch.optim.optimizer import register_optimizer_step_pre_hook
+
+        register_optimizer_step_pre_hook(lambda opt, args, kwargs: flush_weight_grads())
+        _HOOKED[0] = True
+
+
+def _wgrad_sum(segs, tgt):
+    """Σ over the (gy, x) row segments, ≤ 4 per launch, into ``tgt`` (the
+    existing fp32 gradient) when given, else a new fp32 tensor."""
+    dw = tgt
+    for i in range(0, len(segs), 4):
+        chunk = segs[i:i + 4]
+        dw = _C.conv1x1_wgrad_multi([g for g, _ in chunk], [x for _, x in chunk], accumulate_into=dw)
+    return dw
+
+
+def flush_weight_grads() -> None:
+    """Add every deferred micro-step weight gradient into its parameters'
+    ``.grad`` (creating it where None). Called by every optimizer step."""
+    while _PENDING:
+        _, e = _PENDING.popitem()
+        dw = _wgrad_sum(e.segs, None)
+        parts = dw.split(e.rows, 0) if e.rows else (dw,)
+        with torch.no_grad():
+            for p, d in zip(e.params, parts):
+                d = d.view(p.shape).to(p.dtype)
+                if p.grad is None:
+                    p.grad = d
+                else:
+                    p.grad.add_(d)
+
+
+def discard_weight_grads() -> None:
+    """Drop the deferred contributions (``zero_grad`` of this package's optimizers)."""
+    _PENDING.clear()
+
+
+def _deferred_wgrad(ctx, g2, x2):
+    """(handled, dw): stash (g2, x2) under no_sync deferral (handled, dw None),
+    or — on the synchronising micro-step — dW over the stashed segments plus
+    this one (returned, or added into the parameter's .grad: dw None)."""
+    params = getattr(ctx, "defer_params", None)
+    if params is None:
+        w = ctx.params[0]
+        params = (w,) if w is not None else None
+    if params is None or not g2.is_cuda or not all(p.is_leaf for p in params):
+        return False, None
+    key = id(params[0])
+    if getattr(ctx, "defer", False):
+        if not _engine_accumulates(params[0]):
+            return False, None
+        e = _PENDING.get(key)
+        if e is None:
+            e = _PENDING[key] = _Pending(params, getattr(ctx, "rows", None))
+        e.segs.append((g2, x2.contiguous()))
+        return True, None
+    e = _PENDING.pop(key, None)
+    if e is None:
+        return False, None
+    segs = e.segs + [(g2, x2.contiguous())]
+    tgt = _acc_target(ctx, params[0], torch.Size((g2.shape[1], x2.shape[1]))) if len(params) == 1 else None
+    dw = _wgrad_sum(segs, tgt)
+    return True, (None if tgt is not None else dw)
+
+
 def _gemm_ok(x: torch.Tensor, w: torch.Tensor, bias) -> bool:
     """Shapes our gemm_nt takes (in/out features multiples of 64, ≤ 4096 in)."""
     return (_OUR_FWD and bias is not None and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and w.shape[1] <= 4096
@@ -256,7 +383,7 @@ def _fwd_cands(x2, w, b, b32, mode: int) -> dict:
     """Forward candidates (Linear + bias [+ GELU: mode 1 tanh / 2 erf])."""
     M, K, N = x2.shape[0], w.shape[1], w.shape[0]
     c = {}
-    if _pp_ok(M, N, K):
+    if _pp_ok(M, N, K) and _pp_bias_ok(N):
         c["pp"] = lambda: _C.gemm_pp(x2, w, b32, mode)
     c["ring"] = lambda: _C.linear_fwd(x2, w, b32, mode)
     if mode:
@@ -335,6 +462,7 @@ def _setup(ctx, x, weight, bias, w16, b16):
         x = x.to(torch.bfloat16)
     ctx.wdtype = weight.dtype
     ctx.accum = accumulating()
+    ctx.defer = deferring()
     ctx.bdtype = bias.dtype if bias is not None else None
     ctx.params = (weight, bias)
     return x, w, b
@@ -370,7 +498,12 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
             dx = (g2 @ w).view(x.shape)
     weight, bias = ctx.params
     if ctx.needs_input_grad[1]:
+        done = False
         if g2.shape[0] > 0 and g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
+            done, dw = _deferred_wgrad(ctx, g2, x2)
+        if done:
+            pass
+        elif g2.shape[0] > 0 and g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
             # our split-M MFMA wgrad GEMM (gemm.hip): faster than hipBLASLt at
             # every BERT / GPT-2 shape (profiles/r1_linear_wgrad_bench.log)
             tgt = _acc_target(ctx, weight, torch.Size((g2.shape[1], x2.shape[1])))
@@ -548,6 +681,7 @@ class _PackedLinearFn(torch.autograd.Function):
         x, w, b = _setup(ctx, x, weights[0], bias, w16, None)
         ctx.params = (None, bias)  # no in-place .grad add: the packed gradient is split by rows
         ctx.rows = [wt.shape[0] for wt in weights]
+        ctx.weights = weights
         ctx.save_for_backward(x, w, w16t)
         return _linear_fwd(x, w, b, bias)
 
@@ -558,7 +692,8 @@ class _PackedLinearFn(torch.autograd.Function):
         if gy.dtype != torch.bfloat16:
             gy = gy.to(torch.bfloat16)
         n = ctx.needs_input_grad
-        sub = _Sub((n[0], any(n[4:]), n[1]), ctx.params, ctx.wdtype, ctx.bdtype, ctx.accum)
+        sub = _Sub((n[0], any(n[4:]), n[1]), ctx.params, ctx.wdtype, ctx.bdtype, ctx.accum, ctx.defer,
+                   ctx.weights, ctx.rows)
         dx, dw, db = _linear_backward(sub, gy.view(-1, gy.shape[-1]), x, w, wt=wt)
         dws = dw.split(ctx.rows, 0) if dw is not None else (None,) * len(ctx.rows)
         return (dx, db, None, None, *dws)
@@ -710,8 +845,9 @@ class LinearWeightPrep:
 class _Sub:
     """The per-Linear slice of an autograd ctx that _linear_backward reads."""
 
-    def __init__(self, needs, params, wdtype, bdtype, accum):
+    def __init__(self, needs, params, wdtype, bdtype, accum, defer=False, defer_params=None, rows=None):
         self.needs_input_grad, self.params, self.wdtype, self.bdtype, self.accum = needs, params, wdtype, bdtype, accum
+        self.defer, self.defer_params, self.rows = defer, defer_params, rows
 
 
 class _MLPFn(torch.autograd.Function):
@@ -748,6 +884,7 @@ class _MLPFn(torch.autograd.Function):
         ctx.save_for_backward(x, h, y1, w1_16, w2_16, w1t, w2t)
         ctx.tanh = tanh
         ctx.accum = accumulating()
+        ctx.defer = deferring()
         ctx.wdtypes = (w1.dtype, w2.dtype)
         ctx.bdtypes = (b1.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
@@ -763,7 +900,7 @@ class _MLPFn(torch.autograd.Function):
         g2 = gout.view(-1, gout.shape[-1])
         n = ctx.needs_input_grad
         # proj: weight / bias gradients as a plain Linear (no data gradient here)
-        sub2 = _Sub((False, n[3], n[4]), (w2, b2), ctx.wdtypes[1], ctx.bdtypes[1], ctx.accum)
+        sub2 = _Sub((False, n[3], n[4]), (w2, b2), ctx.wdtypes[1], ctx.bdtypes[1], ctx.accum, ctx.defer)
         _, dw2, db2 = _linear_backward(sub2, g2, y1, w2_16)
         # proj's data gradient with the GELU backward and fc's bias sum fused in
         tgt = _acc_target(ctx, b1, torch.Size((h.shape[-1],))) if n[2] else None
@@ -774,7 +911,7 @@ class _MLPFn(torch.autograd.Function):
             db1 = None
         elif db1.dtype != ctx.bdtypes[0]:
             db1 = db1.to(ctx.bdtypes[0])
-        sub1 = _Sub((n[0], n[1], n[2]), (w1, b1), ctx.wdtypes[0], ctx.bdtypes[0], ctx.accum)
+        sub1 = _Sub((n[0], n[1], n[2]), (w1, b1), ctx.wdtypes[0], ctx.bdtypes[0], ctx.accum, ctx.defer)
         dx, dw1, _ = _linear_backward(sub1, gh, x, w1_16, db=db1, db_done=True, wt=w1t)
         return dx, dw1, db1, dw2, db2, None, None, None, None, None, None
 

@@ -29,7 +29,7 @@ from torch.nn import functional as F
 from .._ext import C as _C
 from .cross_entropy import fused_cross_entropy
 from . import linear as _lin
-from .linear import _pick, _pp_ok, accumulating, inplace_grad, prepped_linear
+from .linear import _pick, _pp_bias_ok, _pp_ok, accumulating, inplace_grad, prepped_linear
 
 
 def padded_vocab(v: int) -> int:
@@ -62,7 +62,7 @@ class _LMHeadXentFn(torch.autograd.Function):
         if bias is not None:
             b32 = F.pad(bias.detach().float(), (0, Vp - V))
         cands = {}
-        if _pp_ok(M, Vp, K):
+        if _pp_ok(M, Vp, K) and (b32 is None or _pp_bias_ok(Vp)):
             cands["pp"] = lambda: _C.gemm_pp(x2, wb, b32, 0)[0]
         if K <= 4096 and K % 64 == 0:
             cands["ring"] = lambda: _C.linear_fwd(x2, wb, b32 if b32 is not None else _zero_bias(Vp, x2.device), 0)[0]

@@ -72,7 +72,7 @@ def _overlap_chunks(opt):
             if plan is None:
                 plan = d.reducer.bucket_indices()
             ids = {id(d._params[i]) for i in plan[k]}
-            chunks.append((lambda d=d, k=k: d.reducer.sync_bucket(k), ids))
+            chunks.append((lambda d=d, k=k: d._sync_bucket(k), ids))
             covered |= ids
     if not chunks:
         return None
@@ -99,7 +99,7 @@ def sync_deferred_gradients() -> None:
     from ..parallel import ddp as _ddp
 
     for d in list(_ddp._OVERLAP):
-        d.reducer.sync_all()
+        d.wait_gradients()
 
 
 def _grads_ok(p: torch.Tensor) -> bool:

@@ -65,6 +65,50 @@ import weakref as _weakref
 _OVERLAP = _weakref.WeakSet()
 
 
+class _PendingGrad(torch.Tensor):
+    """``.grad`` of a parameter whose bucket reduction is still in flight
+    (``overlap_optimizer=True``): the bucket view itself (same storage), but
+    any torch operation on it — a stock ``torch.optim`` step, ``torch.nn.
+    utils.clip_grad_norm_``, a GradScaler, ``zero_grad(set_to_none=False)``,
+    user code — first orders the caller behind the reduction (device-side
+    event wait on RCCL, a host wait on the host backend) and rebinds the
+    parameters' ``.grad`` to the plain views; the op then runs on the reduced
+    values. Only this package's fused optimizers read the pending views
+    without that sync: they sync bucket by bucket, in launch order, right
+    before updating each bucket's parameters (the overlap)."""
+
+    @staticmethod
+    def wrap(view: torch.Tensor, ddp, k: int) -> "_PendingGrad":
+        t = view.as_subclass(_PendingGrad)
+        t._dcp_src = (_weakref.ref(ddp), k)
+        return t
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        seen = set()
+
+        def visit(a):
+            if isinstance(a, _PendingGrad):
+                src = a.__dict__.get("_dcp_src")
+                if src is not None and (id(src[0]), src[1]) not in seen:
+                    seen.add((id(src[0]), src[1]))
+                    d = src[0]()
+                    if d is not None:
+                        d._sync_bucket(src[1])
+            elif isinstance(a, (list, tuple)):
+                for x in a:
+                    visit(x)
+            elif isinstance(a, dict):
+                for x in a.values():
+                    visit(x)
+
+        visit(args)
+        visit(kwargs)
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **kwargs)
+
+
 _DTYPE_IDS = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3, torch.int64: 4,
               torch.int32: 5, torch.uint8: 6, torch.int8: 7, torch.bool: 8, torch.complex64: 9}
 
@@ -104,7 +148,7 @@ class DistributedDataParallel(nn.Module):
                  gradient_as_bucket_view: bool = False, static_graph: bool = False,
                  first_bucket_mb: Optional[float] = None, comm_dtype: Optional[torch.dtype] = None,
                  rebuild_buckets: bool = True, init_sync: bool = True, tail_bucket_mb: Optional[float] = None,
-                 register_buckets: bool = False, overlap_optimizer: bool = False):
+                 register_buckets: bool = False, overlap_optimizer: bool = False, defer_accum_wgrad: bool = False):
         super().__init__()
         self.module = module
         self.process_group = process_group if process_group is not None else dist.get_default_group()
@@ -175,11 +219,25 @@ class DistributedDataParallel(nn.Module):
         # between backward and step must call wait_gradients() first.
         self.overlap_optimizer = bool(overlap_optimizer) and gradient_as_bucket_view and not find_unused_parameters
         opts.defer_grad_wait = self.overlap_optimizer
+        # defer_accum_wgrad: under no_sync the Linear weight gradients of the
+        # micro-steps are not computed one by one; the synchronising micro-step
+        # computes each over all micro-steps' rows in one launch (ops/linear.py
+        # "micro-step weight-gradient deferral"). p.grad of those weights lacks
+        # the no_sync contributions until that backward or an optimizer step.
+        self.defer_accum_wgrad = bool(defer_accum_wgrad)
         self._comm = pg.comm_for(params[0])
         self.reducer = _C.Reducer(params, plan, self._comm, opts)
         self._comm_hook = None
         if self.overlap_optimizer:
             _OVERLAP.add(self)
+            me = _weakref.ref(self)
+
+            def _wrap(k, views):
+                d = me()
+                return [_PendingGrad.wrap(v, d, k) for v in views] if d is not None else list(views)
+
+            self.reducer.set_deferred_grad_hook(_wrap)
+            _install_step_sync_hook()
 
     @staticmethod
     def _key(p):
@@ -210,12 +268,13 @@ class DistributedDataParallel(nn.Module):
     @contextlib.contextmanager
     def no_sync(self):
         """Accumulate gradients locally (no all-reduce) inside the context."""
-        from ..ops.linear import accumulate_grads_in_place
+        from ..ops.linear import accumulate_grads_in_place, defer_weight_grads
 
         old = self.require_backward_grad_sync
         self.require_backward_grad_sync = False
         try:
-            with accumulate_grads_in_place():
+            with accumulate_grads_in_place(), (defer_weight_grads() if self.defer_accum_wgrad
+                                               else contextlib.nullcontext()):
                 yield
         finally:
             self.require_backward_grad_sync = old
@@ -240,9 +299,28 @@ class DistributedDataParallel(nn.Module):
 
     def wait_gradients(self) -> None:
         """overlap_optimizer: order the current stream behind every bucket
-        reduction still in flight (before reading .grad outside the fused
-        optimizers' step)."""
+        reduction still in flight and hand out the plain gradient views (any
+        torch op on a pending ``.grad`` does this by itself)."""
         self.reducer.sync_all()
+        self._unwrap(range(len(self.reducer.bucket_indices())))
+
+    def _sync_bucket(self, k: int) -> None:
+        """overlap_optimizer: order the current stream behind bucket k's
+        reduction and rebind its parameters' ``.grad`` to the plain views."""
+        self.reducer.sync_bucket(k)
+        self._unwrap((k,))
+
+    def _unwrap(self, ks) -> None:
+        plan = self.reducer.bucket_indices()
+        with torch._C.DisableTorchFunctionSubclass():
+            for k in ks:
+                if k >= len(plan):
+                    continue
+                for i in plan[k]:
+                    p = self._params[i]
+                    g = p.grad
+                    if isinstance(g, _PendingGrad):
+                        p.grad = g.as_subclass(torch.Tensor)
 
     # ------------------------------------------------------------------
     def bucket_sizes(self) -> List[int]:
@@ -268,6 +346,30 @@ class DistributedDataParallel(nn.Module):
             # DCP_COMM_TIMING=1: reduction time not hidden behind backward
             "exposed_comm_ms": self.reducer.exposed_comm_ms(),
         }
+
+
+_STEP_HOOK = [False]
+
+
+def _install_step_sync_hook():
+    """Before any optimizer step that is not one of this package's fused
+    optimizers (they sync bucket by bucket themselves): sync every
+    overlap-mode DDP. (A torch op on a pending .grad syncs anyway; this also
+    covers optimizers that hand the gradients to native code directly.)"""
+    if _STEP_HOOK[0]:
+        return
+    from torch.optim.optimizer import register_optimizer_step_pre_hook
+
+    def hook(opt, args, kwargs):
+        from ..optim import fused
+
+        if isinstance(opt, (fused.SGD, fused.Adam, fused.Adadelta)):
+            return
+        for d in list(_OVERLAP):
+            d.wait_gradients()
+
+    register_optimizer_step_pre_hook(hook)
+    _STEP_HOOK[0] = True
 
 
 def _tensors_in(obj):

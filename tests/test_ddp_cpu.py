@@ -139,6 +139,51 @@ def test_overlap_optimizer_defers_and_matches():
     run_world(_overlap, 2)
 
 
+def _overlap_stock(rank, world):
+    """overlap_optimizer with STOCK consumers of .grad:
+    torch.nn.utils.clip_grad_norm_ and torch.optim.AdamW read the gradients
+    while the bucket reductions are deferred. The pending views must order
+    them behind the reductions: parameters equal the non-overlapped run bit
+    for bit, and the gradients handed out after backward are the pending
+    wrappers (nothing else reads a buffer mid-reduction)."""
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.models import ConvNet
+    from distributed_compute_pytorch_amd.parallel.ddp import _PendingGrad
+
+    torch.manual_seed(0)
+    base = ConvNet()
+    runs = {}
+    for ov in (False, True):
+        m = copy.deepcopy(base)
+        ddp = dcp.parallel.DistributedDataParallel(m, gradient_as_bucket_view=True, bucket_cap_mb=0.05,
+                                                   overlap_optimizer=ov)
+        opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3, weight_decay=0.01)
+        g = torch.Generator().manual_seed(7 + rank)
+        kinds = []
+        for it in range(4):
+            opt.zero_grad(set_to_none=True)
+            x, y = torch.randn(8, 1, 28, 28, generator=g), torch.randint(0, 10, (8,), generator=g)
+            with torch.random.fork_rng():
+                torch.manual_seed(it)
+                (F.nll_loss(ddp(x), y) * 100.0).backward()
+            kinds.append(sum(isinstance(p.grad, _PendingGrad) for p in m.parameters()))
+            torch.nn.utils.clip_grad_norm_(ddp.parameters(), 1.0)
+            assert not any(isinstance(p.grad, _PendingGrad) for p in m.parameters())
+            opt.step()
+            assert ddp.reducer.deferred_buckets() == []
+        if ov:
+            assert kinds[0] == 0 and all(k == len(list(m.parameters())) for k in kinds[1:]), kinds
+        else:
+            assert kinds == [0] * 4
+        runs[ov] = [p.detach().clone() for p in m.parameters()]
+    for a, b in zip(runs[False], runs[True]):
+        assert torch.equal(a, b)
+
+
+def test_overlap_optimizer_safe_for_stock_consumers():
+    run_world(_overlap_stock, 2)
+
+
 def test_ddp_no_sync_accumulation_matches_torch():
     run_world(_parity, 2, {}, 2, 3)
 

@@ -1,0 +1,122 @@
+"""Micro-step weight-gradient deferral (DistributedDataParallel(
+defer_accum_wgrad=True), ops/linear.py): under no_sync the Linear weight
+gradients are kept as (dY, X) row segments and the synchronising micro-step
+computes each over all micro-steps in one multi-segment wgrad launch. The
+gradients must equal the per-micro-step accumulation (fp32 summation order
+aside), and nothing may be lost when no synchronising backward follows
+(the optimizer step flushes)."""
+import contextlib
+import copy
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pg(cuda):
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.distributed.launch import free_port
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+    dcp.distributed.init_process_group("rccl", device_id=0)
+    yield
+    dcp.distributed.destroy_process_group()
+
+
+@pytest.fixture
+def no_autotune():
+    from distributed_compute_pytorch_amd.ops import linear as lin
+
+    old = lin._AUTOTUNE
+    lin._AUTOTUNE = False  # both arms on the same kernels: only the deferral differs
+    yield
+    lin._AUTOTUNE = old
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+def _model(cuda):
+    from distributed_compute_pytorch_amd import models
+
+    torch.manual_seed(0)
+    return models.gpt2_small(n_layer=2, dropout=0.0, fused=True).to(cuda)
+
+
+def _grads(base, data, defer, cuda, sync_last=True):
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.ops import linear as lin
+
+    m = copy.deepcopy(base)
+    ddp = dcp.parallel.DistributedDataParallel(m, device_ids=[0], gradient_as_bucket_view=True,
+                                               defer_accum_wgrad=defer)
+    pending = []
+    for k, seq in enumerate(data):
+        last = sync_last and k == len(data) - 1
+        with (contextlib.nullcontext() if last else ddp.no_sync()):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = ddp(seq[:, :-1], seq[:, 1:]) / len(data)
+            loss.backward()
+        pending.append(lin.pending_weight_grads())
+    torch.cuda.synchronize()
+    return m, ddp, pending
+
+
+def test_deferred_wgrad_matches_per_microstep(pg, cuda, no_autotune):
+    from distributed_compute_pytorch_amd.ops import linear as lin
+
+    base = _model(cuda)
+    data = [torch.randint(0, 50257, (2, 513), device=cuda) for _ in range(4)]  # 1,024 rows per micro-step
+    m_ref, _, p_ref = _grads(base, data, False, cuda)
+    m_def, _, p_def = _grads(base, data, True, cuda)
+    assert p_ref == [0, 0, 0, 0]
+    assert p_def[0] > 0 and p_def[1] == p_def[0] and p_def[-1] == 0  # stashed, then consumed
+    n_lin = 0
+    for (name, a), b in zip(m_ref.named_parameters(), m_def.parameters()):
+        assert b.grad is not None, name
+        assert _rel(b.grad, a.grad) < 1e-4, (name, _rel(b.grad, a.grad))
+        n_lin += a.dim() == 2 and "wte" not in name and "wpe" not in name
+    assert n_lin >= 8  # the Linear weights were covered
+    assert lin.pending_weight_grads() == 0
+
+
+def test_optimizer_step_flushes_deferred(pg, cuda, no_autotune):
+    """no_sync micro-steps only, then a stock torch.optim step: the global step
+    pre-hook adds the deferred contributions before the update."""
+    from distributed_compute_pytorch_amd.ops import linear as lin
+
+    base = _model(cuda)
+    data = [torch.randint(0, 50257, (2, 257), device=cuda) for _ in range(2)]
+    m_ref, _, _ = _grads(base, data, False, cuda, sync_last=False)
+    m_def, _, pend = _grads(base, data, True, cuda, sync_last=False)
+    assert pend[-1] > 0
+    opt = torch.optim.SGD(m_def.parameters(), lr=0.0)  # lr 0: only the flush is observed
+    opt.step()
+    assert lin.pending_weight_grads() == 0
+    for (name, a), b in zip(m_ref.named_parameters(), m_def.parameters()):
+        assert b.grad is not None, name
+        assert _rel(b.grad, a.grad) < 1e-4, (name, _rel(b.grad, a.grad))
+
+
+def test_wgrad_multi_segments_match_fp64(cuda):
+    """The multi-segment launch itself: ragged segment lengths (each padded to
+    whole K-tiles), 1-4 segments, accumulation into an existing gradient."""
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    g = torch.Generator().manual_seed(21)
+    n1, n2 = 768, 512
+    rows = [1000, 640, 2049, 64]
+    gys = [torch.randn(r, n1, generator=g).to(torch.bfloat16).to(cuda) for r in rows]
+    xs = [torch.randn(r, n2, generator=g).to(torch.bfloat16).to(cuda) for r in rows]
+    for k in range(1, 5):
+        ref = sum(a.double().t() @ b.double() for a, b in zip(gys[:k], xs[:k]))
+        dw = _C.conv1x1_wgrad_multi(gys[:k], xs[:k])
+        assert _rel(dw, ref) < 1e-5, k
+        base = torch.randn(n1, n2, generator=g).to(cuda)
+        acc = base.clone()
+        _C.conv1x1_wgrad_multi(gys[:k], xs[:k], accumulate_into=acc)
+        assert _rel(acc, ref + base.double()) < 1e-5, k

@@ -42,3 +42,27 @@ def test_pinned_choices_roundtrip(monkeypatch, tmp_path):
 
 def test_agree_single_process_keeps_local_choice():
     assert lin._agree(("fwd", 1, 2, 3), "ring") == "ring"
+
+
+def _agree_world(rank, world):
+    import time
+
+    from distributed_compute_pytorch_amd import distributed as dist
+
+    lin._AGREE_WAIT_S = 0.5
+    mine = "pp" if rank == 0 else "ring"
+    # a shape every rank runs: rank 0's measurement wins everywhere
+    assert lin._agree(("fwd", 64, 64, 64), mine) == "pp"
+    # a shape only rank 1 runs (uneven last batch, rank-dependent path): rank 1
+    # keeps its own choice after a bounded wait instead of blocking on rank 0
+    if rank == 1:
+        t0 = time.time()
+        assert lin._agree(("fwd", 63, 64, 64), "hipblaslt") == "hipblaslt"
+        assert time.time() - t0 < 10
+    dist.barrier()
+
+
+def test_agree_takes_rank0_choice_and_never_blocks():
+    from mp_util import run_world
+
+    run_world(_agree_world, 2)
