@@ -2640,10 +2640,28 @@ void gemm_wgrad_bf16(const void* A, const void* B, float* D, int64_t M, int N1, 
   wgrad_launch<false>(A, B, D, M, N1, N2, scale, shift, relu, ws, 1, geo, s, accumulate, rows_out, zero);
 }
 
+namespace {
+// the one-launch plan for these segments, or S = 0 when they take one launch each
+WgradPPPlan wgrad_multi_plan(const WgradPPSegs& sg, int N1, int N2, bool have_zero) {
+  const int64_t M = wgrad_pp_rows(sg);
+  if (sg.n > 1 && have_zero && wgrad_pp_supported(M, N1, N2, 1)) {
+    const WgradPPPlan p = wgrad_pp_plan(M, N1, N2, 1);
+    if (wgrad_pp_segs_ok(sg, p.chunk)) return p;
+  }
+  return WgradPPPlan{0, 0, 0};
+}
+}  // namespace
+
 int64_t gemm_wgrad_multi_workspace(const WgradPPSegs& sg, int N1, int N2) {
-  int64_t need = gemm_wgrad_workspace(wgrad_pp_rows(sg), N1, N2, 1);
+  int64_t need = 0;
   for (int i = 0; i < sg.n; ++i) {
     const int64_t w = gemm_wgrad_workspace(sg.M[i], N1, N2, 1);
+    if (w > need) need = w;
+  }
+  const WgradPPPlan p = wgrad_multi_plan(sg, N1, N2, true);
+  if (p.S > 0) {
+    const int64_t g2 = (p.S + kSlabGroup - 1) / kSlabGroup;
+    const int64_t w = (static_cast<int64_t>(p.S) + (g2 > 1 ? g2 : 0)) * N1 * N2;
     if (w > need) need = w;
   }
   return need;
@@ -2651,17 +2669,15 @@ int64_t gemm_wgrad_multi_workspace(const WgradPPSegs& sg, int N1, int N2) {
 
 void gemm_wgrad_multi_bf16(const WgradPPSegs& sg, float* D, int N1, int N2, float* ws, hipStream_t s, bool accumulate,
                            int rows_out, const void* zero) {
-  const int64_t M = wgrad_pp_rows(sg);
-  if (sg.n == 1 || !(zero != nullptr && wgrad_pp_supported(M, N1, N2, 1))) {
-    // one launch per segment (the ring kernel, or nothing to merge); the
-    // later ones add into D
+  const WgradPPPlan p = wgrad_multi_plan(sg, N1, N2, zero != nullptr);
+  if (p.S == 0) {
+    // one launch per segment; the later ones add into D
     ConvGeo geo{};
     for (int i = 0; i < sg.n; ++i)
       wgrad_launch<false>(sg.A[i], sg.B[i], D, sg.M[i], N1, N2, nullptr, nullptr, false, ws, 1, geo, s,
                           accumulate || i > 0, rows_out, zero);
     return;
   }
-  const WgradPPPlan p = wgrad_pp_plan(M, N1, N2, 1);
   const int rows = rows_out >= 0 ? rows_out : N1;
   if (p.S == 1) {
     gemm_wgrad_pp(sg, D, N1, N2, 1, p, nullptr, zero, accumulate, rows, s);

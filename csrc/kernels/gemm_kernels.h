@@ -112,6 +112,9 @@ struct WgradPPSegs {
   int64_t M[kWgradMaxSegs];
 };
 int64_t wgrad_pp_rows(const WgradPPSegs& sg);  // rows of the padded concatenation (the plan's M)
+// Whether the plan's slabs of `chunk` rows (a multiple of 64) each span at most
+// two segments: every segment but the first and the last is >= a chunk long.
+bool wgrad_pp_segs_ok(const WgradPPSegs& sg, int64_t chunk);
 bool wgrad_pp_supported(int64_t M, int N1, int N2, int taps);
 WgradPPPlan wgrad_pp_plan(int64_t M, int N1, int N2, int taps);
 void gemm_wgrad_pp(const WgradPPSegs& sg, float* out, int N1, int N2, int taps, const WgradPPPlan& p,

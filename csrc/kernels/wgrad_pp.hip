@@ -149,20 +149,35 @@ __global__ void __launch_bounds__(kPT, 1)
     by = rest / ntiles;
   }
   const int i0 = (bx / tiles_j) * 256, j0 = (bx % tiles_j) * 256;
-  // the rows are the concatenation of sg.n segments (gradient-accumulation
-  // micro-steps), each padded to whole 64-row K-tiles: segment s owns global
-  // K-tiles [kt0[s], kt0[s + 1]); slab `by` covers chunk / 64 of them
-  int64_t kt0[kMaxSegs + 1];
-  kt0[0] = 0;
+  // The rows are up to 4 segments (gradient-accumulation micro-steps), each
+  // padded to whole 64-row K-tiles; slab `by` covers global K-tiles [g0, g0 +
+  // KT) of their concatenation and spans at most two segments (the host keeps
+  // every middle segment at least a chunk long): piece a = the segment holding
+  // g0, piece b = the next one from slab-relative K-tile `split` on. Resolved
+  // once here into uniform scalars: a per-K-tile lookup by dynamic kernel-
+  // argument index cost the loop an s_load whose lgkmcnt(0) wait also waited
+  // for the phase's LDS reads.
+  int64_t kst[kMaxSegs + 1];
+  kst[0] = 0;
 #pragma unroll
-  for (int i = 0; i < kMaxSegs; ++i) kt0[i + 1] = kt0[i] + (i < sg.n ? (sg.M[i] + 63) >> 6 : 0);
+  for (int i = 0; i < kMaxSegs; ++i) kst[i + 1] = kst[i] + (i < sg.n ? (sg.M[i] + 63) >> 6 : 0);
   const int64_t g0 = static_cast<int64_t>(by) * (chunk >> 6);
-  const int KT = static_cast<int>(min(kt0[kMaxSegs], g0 + (chunk >> 6)) - g0);
-  // GATHER (one segment): the operands and the slab's first row
-  const uint16_t* A = static_cast<const uint16_t*>(sg.A[0]);
-  const uint16_t* B = static_cast<const uint16_t*>(sg.B[0]);
-  const int64_t M = sg.M[0];
+  const int KT = static_cast<int>(min(kst[kMaxSegs], g0 + (chunk >> 6)) - g0);
+  const int sa = (sg.n > 1 && g0 >= kst[1] ? 1 : 0) + (sg.n > 2 && g0 >= kst[2] ? 1 : 0) +
+                 (sg.n > 3 && g0 >= kst[3] ? 1 : 0);
+  const int sbx = sa + 1 < sg.n ? sa + 1 : sa;
+  const uint16_t* const Aa = static_cast<const uint16_t*>(sg.A[sa]);
+  const uint16_t* const Ba = static_cast<const uint16_t*>(sg.B[sa]);
+  const uint16_t* const Ab = static_cast<const uint16_t*>(sg.A[sbx]);
+  const uint16_t* const Bb = static_cast<const uint16_t*>(sg.B[sbx]);
+  const int64_t Ma = sg.M[sa], Mb = sg.M[sbx];
+  const int64_t ka = kst[sa], kb = kst[sbx];  // the pieces' first global K-tiles
+  const int split = sbx != sa ? static_cast<int>(min(kb - g0, static_cast<int64_t>(KT))) : KT;
+  // GATHER (one segment): the operands and the slab's row range
+  const uint16_t* const A = Aa;
+  const uint16_t* const B = Ba;
   const int64_t mz0 = g0 * 64;
+  const int64_t mz1 = min(Ma, mz0 + chunk);
 
   // this lane's two DMA per half-tile: image row rq = 8 w + 4 q + lane / 16,
   // physical chunk lane % 16 = logical chunk lc (channel block of 8)
@@ -197,7 +212,7 @@ __global__ void __launch_bounds__(kPT, 1)
   }
   auto trk_src = [&](const WpTrk& k, int ch) -> const uint16_t* {
     const int hi = k.ho * geo.stride + gdy, wi = k.wo * geo.stride + gdx;
-    const bool ok = k.m < M && static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
+    const bool ok = k.m < mz1 && static_cast<unsigned>(hi) < static_cast<unsigned>(geo.H) &&
                     static_cast<unsigned>(wi) < static_cast<unsigned>(geo.W);
     return wp_sel(ok, B + (static_cast<int64_t>(k.n * geo.H + hi) * geo.W + wi) * N2 + ch, zsrc);
   };
@@ -230,15 +245,12 @@ __global__ void __launch_bounds__(kPT, 1)
       return;
     }
     char* dst = lds + (kt & 1) * kSlot + h * kHT + w * 2048;
-    // the K-tile's segment (uniform), its first row there and the rows it has left
-    const int64_t g = g0 + kt;
-    int sgi = 0;
-#pragma unroll
-    for (int i = 1; i < kMaxSegs; ++i) sgi += (i < sg.n && g >= kt0[i]) ? 1 : 0;
-    const uint16_t* As = static_cast<const uint16_t*>(sg.A[sgi]);
-    const uint16_t* Bs = static_cast<const uint16_t*>(sg.B[sgi]);
-    const int64_t mb = (g - kt0[sgi]) * 64;
-    const int left = static_cast<int>(min(sg.M[sgi] - mb, int64_t(64)));  // valid rows of this K-tile
+    // the K-tile's piece (uniform): its operands, first row there and rows left
+    const bool pb = kt >= split;
+    const uint16_t* const As = pb ? Ab : Aa;
+    const uint16_t* const Bs = pb ? Bb : Ba;
+    const int64_t mb = (g0 + kt - (pb ? kb : ka)) * 64;
+    const int left = static_cast<int>(min((pb ? Mb : Ma) - mb, int64_t(64)));  // valid rows of this K-tile
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const uint16_t* src;
@@ -417,10 +429,19 @@ int64_t wgrad_pp_rows(const WgradPPSegs& sg) {
   return kt * 64;
 }
 
-void gemm_wgrad_pp(const WgradPPSegs& sg, float* out, int N1, int N2, int taps, const WgradPPPlan& p,
+bool wgrad_pp_segs_ok(const WgradPPSegs& sg, int64_t chunk) {
+  for (int i = 1; i + 1 < sg.n; ++i)
+    if ((sg.M[i] + 63) / 64 < chunk / 64) return false;  // a slab would span three segments
+  return sg.n >= 1 && sg.n <= kWgradMaxSegs;
+}
+
+void gemm_wgrad_pp(const WgradPPSegs& sg_in, float* out, int N1, int N2, int taps, const WgradPPPlan& p_in,
                    const WgradPPGeo* geo, const void* zero, bool acc, int rows_lim, hipStream_t s) {
   const WgradPPGeo g = geo ? *geo : WgradPPGeo{1, 1, 1, 1, 1, 0, 1};
-  if (sg.n < 1 || sg.n > kMaxSegs || (geo && sg.n != 1)) throw std::runtime_error("gemm_wgrad_pp: bad segment list");
+  if ((geo && sg_in.n != 1) || !wgrad_pp_segs_ok(sg_in, p_in.chunk) || p_in.chunk % 64 != 0)
+    throw std::runtime_error("gemm_wgrad_pp: bad segment list");
+  const WgradPPSegs& sg = sg_in;
+  const WgradPPPlan& p = p_in;
   if (geo) {
     if (acc) wgrad_pp_go<1, true>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);
     else wgrad_pp_go<1, false>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);

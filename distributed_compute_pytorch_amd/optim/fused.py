@@ -72,7 +72,7 @@ def _overlap_chunks(opt):
             if plan is None:
                 plan = d.reducer.bucket_indices()
             ids = {id(d._params[i]) for i in plan[k]}
-            chunks.append((lambda d=d, k=k: d._sync_bucket(k), ids))
+            chunks.append((lambda d=d, k=k: d.reducer.sync_bucket(k), ids))
             covered |= ids
     if not chunks:
         return None
@@ -102,10 +102,22 @@ def sync_deferred_gradients() -> None:
         d.wait_gradients()
 
 
+def _grad(p: torch.Tensor):
+    """p.grad — for an overlap-mode DDP's pending gradient (parallel/ddp.py
+    _PendingGrad) the plain bucket view behind it, without the sync a torch op
+    on the wrapper performs: the step's chunk for that bucket has just synced
+    it (_run_chunks), and only the bucket's own sync may be waited for."""
+    g = p.grad
+    if g is not None and type(g).__name__ == "_PendingGrad":
+        return g.__dict__["_dcp_plain"]
+    return g
+
+
 def _grads_ok(p: torch.Tensor) -> bool:
-    if p.grad is None:
+    g = _grad(p)
+    if g is None:
         return False
-    if p.grad.is_sparse:
+    if g.is_sparse:
         raise RuntimeError("fused optimizers do not support sparse gradients")
     return True
 
@@ -170,7 +182,7 @@ class SGD(Optimizer):
                 key = (p.device, p.dtype, first)
                 P, G, B = buckets[key]
                 P.append(p)
-                G.append(_dense_like(p.grad, p))
+                G.append(_dense_like(_grad(p), p))
                 if mom != 0:
                     B.append(st["momentum_buffer"])
             for (dev, dt, first), (P, G, B) in buckets.items():
@@ -261,7 +273,7 @@ class Adam(Optimizer):
                     key = (p.device, p.dtype, float(st["step"]), sh is not None)
                 P, G, M, V, VM, S, ST = buckets[key]
                 P.append(p)
-                G.append(_dense_like(p.grad, p))
+                G.append(_dense_like(_grad(p), p))
                 M.append(st["exp_avg"])
                 V.append(st["exp_avg_sq"])
                 if ams:
@@ -321,7 +333,7 @@ class Adadelta(Optimizer):
                 st["step"] += 1
                 P, G, S, A = buckets[(p.device, p.dtype)]
                 P.append(p)
-                G.append(_dense_like(p.grad, p))
+                G.append(_dense_like(_grad(p), p))
                 S.append(st["square_avg"])
                 A.append(st["acc_delta"])
             for _, (P, G, S, A) in buckets.items():

@@ -81,6 +81,7 @@ class _PendingGrad(torch.Tensor):
     def wrap(view: torch.Tensor, ddp, k: int) -> "_PendingGrad":
         t = view.as_subclass(_PendingGrad)
         t._dcp_src = (_weakref.ref(ddp), k)
+        t._dcp_plain = view  # the fused optimizers read this after their own per-bucket sync
         return t
 
     @classmethod
@@ -231,10 +232,17 @@ class DistributedDataParallel(nn.Module):
         if self.overlap_optimizer:
             _OVERLAP.add(self)
             me = _weakref.ref(self)
+            cache = {}  # bucket -> (view data pointers, wrappers): the views persist across iterations
 
             def _wrap(k, views):
                 d = me()
-                return [_PendingGrad.wrap(v, d, k) for v in views] if d is not None else list(views)
+                if d is None:
+                    return list(views)
+                ptrs = tuple(v.data_ptr() for v in views)
+                hit = cache.get(k)
+                if hit is None or hit[0] != ptrs:
+                    hit = cache[k] = (ptrs, [_PendingGrad.wrap(v, d, k) for v in views])
+                return hit[1]
 
             self.reducer.set_deferred_grad_hook(_wrap)
             _install_step_sync_hook()

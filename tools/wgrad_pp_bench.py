@@ -62,21 +62,43 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--names", default=None, help="comma-separated subset of the shape names")
+    ap.add_argument("--xent-data", action="store_true",
+                    help="gy as a cross-entropy logits gradient (softmax - onehot) / M instead of N(0, 1)")
+    ap.add_argument("--multi", type=int, default=0,
+                    help="also time the multi-segment launch over this many row segments of M rows each")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     pp = lambda: _C.gemm_tune("wg_pp", 1)  # noqa: E731
     ring = lambda: _C.gemm_tune("wg_pp", 0)  # noqa: E731
     if a.only in (None, "linear"):
         for name, m, n1, n2 in LINEAR:
-            g = torch.randn(m, n1, device=dev).to(torch.bfloat16)
+            if a.names and name not in a.names.split(","):
+                continue
+            if a.xent_data:
+                z = torch.randn(m, n1, device=dev) * 2.0
+                g = torch.softmax(z, 1)
+                g[torch.arange(m, device=dev), torch.randint(0, n1, (m,), device=dev)] -= 1.0
+                g = (g / m).to(torch.bfloat16)
+                del z
+            else:
+                g = torch.randn(m, n1, device=dev).to(torch.bfloat16)
             x = torch.randn(m, n2, device=dev).to(torch.bfloat16)
             acc = torch.zeros(n1, n2, device=dev)
             cands = {"pp": (pp, lambda: _C.conv1x1_wgrad(g, x)),
                      "pp_acc": (pp, lambda: _C.conv1x1_wgrad(g, x, accumulate_into=acc)),
                      "ring": (ring, lambda: _C.conv1x1_wgrad(g, x)),
                      "blas_acc": (pp, lambda: torch.addmm(acc, g.t(), x, out_dtype=torch.float32))}
+            if a.multi > 1:
+                gs = [g] + [g.clone() for _ in range(a.multi - 1)]
+                xs = [x] + [x.clone() for _ in range(a.multi - 1)]
+                gcat, xcat = torch.cat(gs), torch.cat(xs)
+                cands[f"multi{a.multi}"] = (pp, lambda: _C.conv1x1_wgrad_multi(gs, xs, accumulate_into=acc))
+                cands[f"cat{a.multi}"] = (pp, lambda: _C.conv1x1_wgrad(gcat, xcat, accumulate_into=acc))
             run(name, 2.0 * m * n1 * n2, cands, a.rounds, a.iters)
             del g, x, acc
+            if a.multi > 1:
+                del gs, xs, gcat, xcat
     if a.only in (None, "conv"):
         for name, n, h, w, ci, co, k, s, p in CONV:
             x = torch.randn(n, ci, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
