@@ -404,6 +404,7 @@ def main():
                 # device time the step waited for communication after backward
                 rec["comm"] = {
                     "bucket_ready_ms": [round(x, 3) for x in info["bucket_ready_ms"]],
+                    "bucket_ready_dev_ms": [round(x, 3) for x in info["bucket_ready_dev_ms"]],
                     "bucket_comm_ms": [round(x, 4) for x in info["bucket_comm_ms"]],
                     "exposed_comm_ms": round(info["exposed_comm_ms"], 4),
                     "comm_bytes_per_step": sum(info["bucket_sizes"]),

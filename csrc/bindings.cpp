@@ -164,6 +164,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("bytes", &BucketStats::bytes)
       .def_readonly("num_params", &BucketStats::num_params)
       .def_readonly("ready_ms", &BucketStats::ready_ms)
+      .def_readonly("ready_dev_ms", &BucketStats::ready_dev_ms)
       .def_readonly("comm_ms", &BucketStats::comm_ms);
 
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")

@@ -178,9 +178,11 @@ Reducer::~Reducer() {
   for (auto& b : buckets_) {
     if (b.stall0) (void)hipEventDestroy(b.stall0);
     if (b.stall1) (void)hipEventDestroy(b.stall1);
+    if (b.ready_ev) (void)hipEventDestroy(b.ready_ev);
   }
   release_registrations();
   if (used_ev_) (void)hipEventDestroy(used_ev_);
+  if (bwd_t0_ev_) (void)hipEventDestroy(bwd_t0_ev_);
   for (size_t i = 0; i < grad_accs_.size() && i < hook_handles_.size(); ++i)
     grad_accs_[i]->del_post_hook(hook_handles_[i]);
 }
@@ -226,6 +228,7 @@ void Reducer::build_buckets(const std::vector<std::vector<int64_t>>& assignment)
   for (auto& b : buckets_) {
     if (b.stall0) (void)hipEventDestroy(b.stall0);
     if (b.stall1) (void)hipEventDestroy(b.stall1);
+    if (b.ready_ev) (void)hipEventDestroy(b.ready_ev);
   }
   buckets_ = std::move(out);
   next_bucket_ = 0;
@@ -319,6 +322,16 @@ void Reducer::autograd_hook(int64_t index) {
   if (!finalize_queued_) {
     finalize_queued_ = true;
     backward_t0_ms_ = static_cast<double>(now_ms());
+    bwd_t0_recorded_ = false;
+    if (timing_) {
+      hipStream_t cur = c10::hip::getCurrentHIPStream(params_[0].device().index()).stream();
+      hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(cur, &cap);
+      if (cap == hipStreamCaptureStatusNone) {
+        if (!bwd_t0_ev_) DK_CHECK(hipEventCreate(&bwd_t0_ev_) == hipSuccess, "Reducer: event creation failed");
+        bwd_t0_recorded_ = hipEventRecord(bwd_t0_ev_, cur) == hipSuccess;
+      }
+    }
     std::weak_ptr<Reducer> weak = shared_from_this();
     torch::autograd::Engine::get_default_engine().queue_callback([weak] {
       if (auto self = weak.lock()) self->finalize();
@@ -407,6 +420,12 @@ void Reducer::launch(Bucket& b) {
   }
   for (auto& g : b.pending_grads) g = at::Tensor();
   b.stats.ready_ms = static_cast<double>(now_ms()) - backward_t0_ms_;
+  b.ready_recorded = false;
+  if (timing_ && bwd_t0_recorded_ && b.flat.is_cuda() && !capturing(b.wire)) {
+    if (!b.ready_ev) DK_CHECK(hipEventCreate(&b.ready_ev) == hipSuccess, "Reducer: event creation failed");
+    b.ready_recorded =
+        hipEventRecord(b.ready_ev, c10::hip::getCurrentHIPStream(b.flat.device().index()).stream()) == hipSuccess;
+  }
   trace::Range r("dcp.reducer.bucket_allreduce");
   const bool check = check_ && !capturing(b.wire);
   if (check) {
@@ -710,6 +729,12 @@ std::vector<BucketStats> Reducer::bucket_stats() {
       b.timed_work->synchronize();
       b.stats.comm_ms = b.timed_work->elapsed_ms();
       b.timed_work.reset();
+    }
+    if (b.ready_recorded && bwd_t0_ev_) {
+      float ms = 0.f;
+      (void)hipEventSynchronize(b.ready_ev);
+      if (hipEventElapsedTime(&ms, bwd_t0_ev_, b.ready_ev) == hipSuccess) b.stats.ready_dev_ms = ms;
+      b.ready_recorded = false;
     }
     r.push_back(b.stats);
   }

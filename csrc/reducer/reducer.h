@@ -85,6 +85,10 @@ struct BucketStats {
   int64_t bytes = 0;
   int64_t num_params = 0;
   double ready_ms = 0;   // host time since backward start when the bucket became ready
+  // device time (DCP_COMM_TIMING=1, GPU): from the backward's first gradient
+  // hook to the completion of the bucket's pack on the compute stream — when
+  // its gradients really exist, which is what overlap depends on (-1: none)
+  double ready_dev_ms = -1;
   double comm_ms = -1;   // device time of its collective (when timing enabled)
 };
 
@@ -161,6 +165,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     WorkPtr check_work;
     bool deferred = false;  // defer_grad_wait: work kept, compute stream not yet ordered behind it
     hipEvent_t stall0 = nullptr, stall1 = nullptr;  // timing: compute-stream wait on this bucket
+    hipEvent_t ready_ev = nullptr;                    // timing: after the bucket's pack (compute stream)
+    bool ready_recorded = false;
     bool stall_recorded = false;
   };
 
@@ -208,6 +214,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   int64_t iterations_ = 0;
   int64_t rebuilds_ = 0;
   double backward_t0_ms_ = 0;
+  hipEvent_t bwd_t0_ev_ = nullptr;  // timing: the compute stream at the backward's first gradient hook
+  bool bwd_t0_recorded_ = false;
   bool timing_ = false;
   bool check_ = false;  // ReducerOptions::check_streams / DCP_DEBUG_STREAMS=1
   bool ev_recorded_ = false;  // timing: some bucket's stall events were recorded

@@ -343,7 +343,10 @@ class DistributedDataParallel(nn.Module):
             "first_bucket_bytes": self.first_bucket_bytes,
             "tail_bucket_bytes": self.tail_bucket_bytes,
             "bucket_sizes": [s.bytes for s in st],
-            "bucket_ready_ms": [s.ready_ms for s in st],
+            "bucket_ready_ms": [s.ready_ms for s in st],  # host enqueue time (1 ms resolution)
+            # DCP_COMM_TIMING=1: device time from the backward's first gradient
+            # hook to each bucket's packed gradients (-1 without timing)
+            "bucket_ready_dev_ms": [s.ready_dev_ms for s in st],
             "bucket_comm_ms": [s.comm_ms for s in st],
             "num_buckets": len(st),
             "bucket_indices": self.reducer.bucket_indices(),

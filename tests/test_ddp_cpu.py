@@ -313,3 +313,65 @@ def _ckpt(rank, world, path):
 
 def test_checkpoint_roundtrip(tmp_path):
     run_world(_ckpt, 2, str(tmp_path / "ck.pt"))
+
+
+class _TinyLM(nn.Module):
+    """Transformer-shaped: an embedding past the 16 MiB bucket cap (one
+    parameter larger than a bucket, tied to the output head, ready last),
+    LayerNorm + MLP blocks."""
+
+    def __init__(self, vocab=70000, d=64, layers=2):
+        super().__init__()
+        self.emb = nn.Embedding(vocab, d)
+        self.blocks = nn.ModuleList(nn.Sequential(nn.LayerNorm(d), nn.Linear(d, 4 * d), nn.GELU(), nn.Linear(4 * d, d))
+                                    for _ in range(layers))
+        self.ln = nn.LayerNorm(d)
+
+    def forward(self, idx, tgt):
+        h = self.emb(idx)
+        for b in self.blocks:
+            h = h + b(h)
+        logits = self.ln(h) @ self.emb.weight.t()
+        return F.cross_entropy(logits.reshape(-1, logits.shape[-1]), tgt.reshape(-1))
+
+
+def _tiny_lm_parity(rank, world):
+    """ws=4: our DDP with the xGMI bucket plan (16 MiB cap, 1 MiB first, 2 MiB
+    tail), gradient-as-bucket-view and overlap_optimizer against torch gloo
+    DDP (same cap), both stepping torch.optim.AdamW; 2 micro-steps of
+    gradient accumulation (no_sync) per step, 3 steps."""
+    import distributed_compute_pytorch_amd as dcp
+
+    tdist = _init_torch_pg(rank, world)
+    torch.manual_seed(0)
+    m_ours = _TinyLM()
+    m_ref = copy.deepcopy(m_ours)
+    assert m_ours.emb.weight.numel() * 4 > dcp.parallel.XGMI_BUCKETS["bucket_cap_mb"] * 2**20
+    ours = dcp.parallel.DistributedDataParallel(m_ours, gradient_as_bucket_view=True, overlap_optimizer=True,
+                                                **dcp.parallel.XGMI_BUCKETS)
+    ref = nn.parallel.DistributedDataParallel(m_ref, gradient_as_bucket_view=True, bucket_cap_mb=16)
+    o1 = torch.optim.AdamW(ours.parameters(), lr=1e-3, weight_decay=0.01)
+    o2 = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=0.01)
+    g = torch.Generator().manual_seed(50 + rank)
+    for it in range(3):
+        batches = [(torch.randint(0, 70000, (4, 16), generator=g), torch.randint(0, 70000, (4, 16), generator=g))
+                   for _ in range(2)]
+        losses = []
+        for model, opt in ((ours, o1), (ref, o2)):
+            opt.zero_grad(set_to_none=True)
+            for k, (x, y) in enumerate(batches):
+                with (model.no_sync() if k == 0 else _null()):
+                    loss = model(x, y) / 2
+                    loss.backward()
+            opt.step()
+            losses.append(loss.detach())
+        torch.testing.assert_close(losses[0], losses[1], rtol=1e-5, atol=1e-6)
+    for (n, p), q in zip(m_ref.named_parameters(), m_ours.parameters()):
+        torch.testing.assert_close(q, p, rtol=1e-5, atol=1e-6, msg=n)
+    sizes = ours.bucket_sizes()
+    assert len(sizes) >= 2 and max(sizes) > 16 * 2**20  # the over-cap embedding bucket + the rest
+    tdist.destroy_process_group()
+
+
+def test_transformer_shaped_ws4_xgmi_plan_overlap_matches_torch():
+    run_world(_tiny_lm_parity, 4, timeout=300)
