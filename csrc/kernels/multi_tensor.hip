@@ -557,8 +557,15 @@ __global__ void __launch_bounds__(kThreads) comm_emulate_kernel(const uint4* __r
                                                                int64_t n16, int64_t per_block16, uint64_t ticks) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int64_t begin = static_cast<int64_t>(blockIdx.x) * per_block16;
+  // wrap by subtraction: begin + i < 4 n16 (bytes_move ≤ 2 bytes_buf); a 64-bit
+  // modulo per element made the copy VALU-bound (~50 GB/s algorithm bandwidth
+  // on 16 channels), slower than every modelled link: the emulated time
+  // never depended on busbw (NOTES §27)
   for (int64_t i = threadIdx.x; i < per_block16; i += kThreads) {
-    const int64_t k = (begin + i) % n16;
+    int64_t k = begin + i;
+    k -= k >= n16 ? n16 : 0;
+    k -= k >= n16 ? n16 : 0;
+    k -= k >= n16 ? n16 : 0;
     dst[k] = src[k];
   }
   // hold the CU for the rest of the collective's duration

@@ -232,6 +232,25 @@ __global__ void __launch_bounds__(kPT, 1)
     k.n += q;
   };
 
+  // plain operands: each half-tile's per-lane source pointers for the next
+  // K-tile it fetches (every half fetches K-tiles 0, 1, 2, ... in order): set
+  // up at K-tile 0 and at the segment switch, else advanced by one uniform
+  // 64-row stride — the per-issue 64-bit row·stride products and clamps were
+  // ~3 VALU per MFMA, more than the partner wave's MFMA segment hides (PMC:
+  // 0.27 MFMA busy on the LM-head shape, NOTES §27)
+  const char* sp[4][2];
+  const int64_t strA = int64_t(64) * N1 * 2, strB = int64_t(64) * N2 * 2;
+  auto src_at = [&](int h, int q, int kt) -> const char* {
+    const bool pb = kt >= split;
+    const int64_t row = (g0 + kt - (pb ? kb : ka)) * 64 + rq[q];
+    if (h == 0 || h == 3) {
+      const int c = min(chA[q] + (h == 3 ? 64 : 0), N1 - 8);
+      return reinterpret_cast<const char*>((pb ? Ab : Aa) + row * N1 + c);
+    }
+    const int c = min(chB[q] + (h == 2 ? 32 : 0), N2 - 8);
+    return reinterpret_cast<const char*>((pb ? Bb : Ba) + row * N2 + c);
+  };
+
   // DMA of half-tile h of K-tile kt (kt ≥ KT: two 1 KB writes into the sink, so
   // every wave's vmcnt sequence is the same for every tile)
   auto issue = [&](int h, int kt) {
@@ -245,28 +264,43 @@ __global__ void __launch_bounds__(kPT, 1)
       return;
     }
     char* dst = lds + (kt & 1) * kSlot + h * kHT + w * 2048;
-    // the K-tile's piece (uniform): its operands, first row there and rows left
-    const bool pb = kt >= split;
-    const uint16_t* const As = pb ? Ab : Aa;
-    const uint16_t* const Bs = pb ? Bb : Ba;
-    const int64_t mb = (g0 + kt - (pb ? kb : ka)) * 64;
-    const int left = static_cast<int>(min((pb ? Mb : Ma) - mb, int64_t(64)));  // valid rows of this K-tile
+    if constexpr (GATHER) {
+      const int left = static_cast<int>(min(mz1 - (mz0 + static_cast<int64_t>(kt) * 64), int64_t(64)));
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const uint16_t* src;
-      if (h == 0 || h == 3) {
-        const int c = min(chA[q] + (h == 3 ? 64 : 0), N1 - 8);
-        src = wp_sel(rq[q] < left, As + (mb + rq[q]) * N1 + c, zsrc);
-      } else {
-        const int c = min(chB[q] + (h == 2 ? 32 : 0), N2 - 8);
-        if constexpr (GATHER) {
-          src = trk_src(tk[h - 1][q], c);
-          trk_adv(tk[h - 1][q]);
+      for (int q = 0; q < 2; ++q) {
+        const uint16_t* src;
+        if (h == 0 || h == 3) {
+          const int c = min(chA[q] + (h == 3 ? 64 : 0), N1 - 8);
+          src = wp_sel(rq[q] < left, A + (mz0 + static_cast<int64_t>(kt) * 64 + rq[q]) * N1 + c, zsrc);
         } else {
-          src = wp_sel(rq[q] < left, Bs + (mb + rq[q]) * N2 + c, zsrc);
+          src = trk_src(tk[h - 1][q], min(chB[q] + (h == 2 ? 32 : 0), N2 - 8));
+          trk_adv(tk[h - 1][q]);
         }
+        wp_glds(src, wp_lds_addr(dst + q * 1024));
       }
-      wp_glds(src, wp_lds_addr(dst + q * 1024));
+    } else {
+      // the K-tile's piece (uniform): rows it has left in its segment
+      const bool pb = kt >= split;
+      const int64_t mb = (g0 + kt - (pb ? kb : ka)) * 64;
+      const int left = static_cast<int>(min((pb ? Mb : Ma) - mb, int64_t(64)));
+      if (kt == 0 || kt == split) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) sp[h][q] = src_at(h, q, kt);
+      } else {
+        const int64_t st = (h == 0 || h == 3) ? strA : strB;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) sp[h][q] += st;
+      }
+      if (left >= 64) {  // every K-tile but a segment's ragged last one
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          wp_glds(reinterpret_cast<const uint16_t*>(sp[h][q]), wp_lds_addr(dst + q * 1024));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          wp_glds(wp_sel(rq[q] < left, reinterpret_cast<const uint16_t*>(sp[h][q]), zsrc),
+                  wp_lds_addr(dst + q * 1024));
+      }
     }
   };
 

@@ -24,6 +24,10 @@ def main():
         g = torch.randn(m, n1, device=dev).to(torch.bfloat16)
         x = torch.randn(m, n2, device=dev).to(torch.bfloat16)
         ops.append(lambda g=g, x=x: _C.conv1x1_wgrad(g, x))
+    # GPT-2 fc over 4 deferred micro-steps (one multi-segment launch)
+    gs = [torch.randn(8192, 3072, device=dev).to(torch.bfloat16) for _ in range(4)]
+    xs = [torch.randn(8192, 768, device=dev).to(torch.bfloat16) for _ in range(4)]
+    ops.append(lambda: _C.conv1x1_wgrad_multi(gs, xs))
     x = torch.randn(512, 256, 14, 14, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     gy = torch.randn(512, 256, 14, 14, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     ops.append(lambda: _C.conv_wgrad(gy, x, 3, 3, 1, 1))
