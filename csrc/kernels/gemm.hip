@@ -2548,10 +2548,8 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
   const WgradPlan p = wgrad_plan_for(M, N1, N2, taps);
   const int64_t groups = (p.S + kSlabGroup - 1) / kSlabGroup;
   int64_t need = (static_cast<int64_t>(p.S) + (groups > 1 ? groups : 0)) * N1 * taps * N2;
-  if (wgrad_pp_supported(M, N1, N2, taps)) {  // the ping-pong kernel's slabs (+ the reduction's partial groups)
-    const WgradPPPlan q = wgrad_pp_plan(M, N1, N2, taps);
-    const int64_t g2 = (q.S + kSlabGroup - 1) / kSlabGroup;
-    const int64_t need2 = (static_cast<int64_t>(q.S) + (g2 > 1 ? g2 : 0)) * N1 * taps * N2;
+  if (wgrad_pp_supported(M, N1, N2, taps)) {  // the ping-pong kernel's slabs
+    const int64_t need2 = wgrad_pp_ws(wgrad_pp_plan(M, N1, N2, taps), N1, N2, taps);
     if (need2 > need) need = need2;
   }
   // direct 3x3 / 64-channel wgrad: ≤ 256 workgroup slabs + 16 partial groups
@@ -2559,8 +2557,27 @@ int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps) {
   return need;
 }
 
+int64_t wgrad_pp_ws(const WgradPPPlan& p, int N1, int N2, int taps) {
+  if (!p.split()) return 0;
+  const int64_t g = (p.S + kSlabGroup - 1) / kSlabGroup;  // + the reduction's partial groups
+  return (static_cast<int64_t>(p.S) + (g > 1 ? g : 0)) * (N1 - wgrad_pp_tail_row0(p, N2)) * taps * N2;
+}
+
 namespace {
 void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc = false, int64_t out4 = -1);
+
+// the ping-pong wgrad of a plan: its kernel, then the reduction of its slabs
+// (rows wgrad_pp_tail_row0 .. N1 - 1 of D) in a fixed order
+void wgrad_pp_run(const WgradPPSegs& sg, float* D, float* ws, int N1, int N2, int taps, const WgradPPPlan& p,
+                  const WgradPPGeo* geo, const void* zero, bool acc, int rows_out, hipStream_t s) {
+  const int rows = rows_out >= 0 && rows_out < N1 ? rows_out : N1;
+  gemm_wgrad_pp(sg, D, ws, N1, N2, taps, p, geo, zero, acc, rows, s);
+  if (!p.split()) return;
+  const int r0 = wgrad_pp_tail_row0(p, N2);
+  if (rows <= r0) return;
+  const int64_t ldo = static_cast<int64_t>(taps) * N2;
+  slab_reduce(ws, D + r0 * ldo, (N1 - r0) * ldo / 4, p.S, s, acc, rows < N1 ? (rows - r0) * ldo / 4 : -1);
+}
 
 template <bool GATHER>
 void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int N2, const float* scale,
@@ -2576,15 +2593,8 @@ void wgrad_launch(const void* A, const void* B, float* D, int64_t M, int N1, int
       wgrad_pp_supported(M, N1, N2, taps)) {
     const WgradPPPlan p = wgrad_pp_plan(M, N1, N2, taps);
     const WgradPPGeo g{geo.H, geo.W, geo.Ho, geo.Wo, geo.stride, geo.pad, geo.kw};
-    const int rows = rows_out >= 0 ? rows_out : N1;
     const WgradPPSegs sg{1, {A}, {B}, {M}};
-    if (p.S == 1) {  // one slab: straight into D (+= when accumulating), no reduction launch
-      gemm_wgrad_pp(sg, D, N1, N2, taps, p, GATHER ? &g : nullptr, zero, acc, rows, s);
-      return;
-    }
-    gemm_wgrad_pp(sg, ws, N1, N2, taps, p, GATHER ? &g : nullptr, zero, false, N1, s);
-    slab_reduce(ws, D, static_cast<int64_t>(N1) * ldo / 4, p.S, s, acc,
-                rows_out >= 0 ? static_cast<int64_t>(rows_out) * ldo / 4 : -1);
+    wgrad_pp_run(sg, D, ws, N1, N2, taps, p, GATHER ? &g : nullptr, zero, acc, rows_out, s);
     return;
   }
   if constexpr (GATHER) {
@@ -2646,9 +2656,9 @@ WgradPPPlan wgrad_multi_plan(const WgradPPSegs& sg, int N1, int N2, bool have_ze
   const int64_t M = wgrad_pp_rows(sg);
   if (sg.n > 1 && have_zero && wgrad_pp_supported(M, N1, N2, 1)) {
     const WgradPPPlan p = wgrad_pp_plan(M, N1, N2, 1);
-    if (wgrad_pp_segs_ok(sg, p.chunk)) return p;
+    if (wgrad_pp_segs_ok(sg, p)) return p;
   }
-  return WgradPPPlan{0, 0, 0};
+  return WgradPPPlan{0, 0, 0, 0};
 }
 }  // namespace
 
@@ -2660,8 +2670,7 @@ int64_t gemm_wgrad_multi_workspace(const WgradPPSegs& sg, int N1, int N2) {
   }
   const WgradPPPlan p = wgrad_multi_plan(sg, N1, N2, true);
   if (p.S > 0) {
-    const int64_t g2 = (p.S + kSlabGroup - 1) / kSlabGroup;
-    const int64_t w = (static_cast<int64_t>(p.S) + (g2 > 1 ? g2 : 0)) * N1 * N2;
+    const int64_t w = wgrad_pp_ws(p, N1, N2, 1);
     if (w > need) need = w;
   }
   return need;
@@ -2678,14 +2687,7 @@ void gemm_wgrad_multi_bf16(const WgradPPSegs& sg, float* D, int N1, int N2, floa
                           accumulate || i > 0, rows_out, zero);
     return;
   }
-  const int rows = rows_out >= 0 ? rows_out : N1;
-  if (p.S == 1) {
-    gemm_wgrad_pp(sg, D, N1, N2, 1, p, nullptr, zero, accumulate, rows, s);
-    return;
-  }
-  gemm_wgrad_pp(sg, ws, N1, N2, 1, p, nullptr, zero, false, N1, s);
-  slab_reduce(ws, D, static_cast<int64_t>(N1) * N2 / 4, p.S, s, accumulate,
-              rows_out >= 0 ? static_cast<int64_t>(rows_out) * N2 / 4 : -1);
+  wgrad_pp_run(sg, D, ws, N1, N2, 1, p, nullptr, zero, accumulate, rows_out, s);
 }
 
 void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int W, int Cout, float* ws,

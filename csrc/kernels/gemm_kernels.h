@@ -90,17 +90,26 @@ void weight_prep(const void* table, int n, int64_t tiles, hipStream_t s);
 void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s);
 
 // Weight gradient on the 8-wave ping-pong schedule (wgrad_pp.hip): 256 x 256
-// output tiles, split over rows m into `S` fp32 slabs of `chunk` rows (plan)
-// that gemm.hip's slab reduction sums; with S == 1 the kernel writes (acc:
-// adds into) D directly. geo != nullptr: B is the NHWC input of a kxk conv,
-// one tap per grid coordinate (zero: >= 2 KB of zero bytes, always needed).
+// output tiles. The first `full` tiles (whole 256-row bands of D) are computed
+// over all rows m and written (acc: added) straight into D; the others are
+// split over rows m into `S` fp32 slabs of `chunk` rows in the workspace, which
+// gemm.hip's slab reduction sums into D's rows from wgrad_pp_tail_row0 on.
+// full == tiles: no slabs; full == 0: every tile split (tiles too few to fill
+// the chip); in between: the grid's last, partial round of whole tiles would
+// leave most CUs idle, so those tiles are split instead (a tail split — the LM
+// head's 591 tiles = 2.3 rounds of 256). geo != nullptr: B is the NHWC input of
+// a kxk conv, one tap per grid coordinate (zero: >= 2 KB of zero bytes).
 struct WgradPPGeo {
   int H, W, Ho, Wo, stride, pad, kw;
 };
 struct WgradPPPlan {
   int tiles, S;
   int64_t chunk;  // rows per slab (a multiple of 64)
+  int full;       // leading tiles written straight into D
+  bool split() const { return full < tiles; }
 };
+int wgrad_pp_tail_row0(const WgradPPPlan& p, int N2);  // first row of D the slabs cover
+int64_t wgrad_pp_ws(const WgradPPPlan& p, int N1, int N2, int taps);  // fp32 elements of the slabs
 // The rows m of one weight gradient as up to kWgradMaxSegs segments (the
 // micro-steps of a gradient accumulation, summed by ONE launch): segment i is
 // A[i] [M[i], N1] and B[i] [M[i], N2]; each is padded to whole 64-row K-tiles.
@@ -112,12 +121,15 @@ struct WgradPPSegs {
   int64_t M[kWgradMaxSegs];
 };
 int64_t wgrad_pp_rows(const WgradPPSegs& sg);  // rows of the padded concatenation (the plan's M)
-// Whether the plan's slabs of `chunk` rows (a multiple of 64) each span at most
-// two segments: every segment but the first and the last is >= a chunk long.
-bool wgrad_pp_segs_ok(const WgradPPSegs& sg, int64_t chunk);
+// Whether the plan's slabs of `chunk` rows (a multiple of 64; a whole tile's:
+// all rows) each span at most two segments: every segment but the first and
+// the last is >= a chunk long.
+bool wgrad_pp_segs_ok(const WgradPPSegs& sg, const WgradPPPlan& p);
 bool wgrad_pp_supported(int64_t M, int N1, int N2, int taps);
 WgradPPPlan wgrad_pp_plan(int64_t M, int N1, int N2, int taps);
-void gemm_wgrad_pp(const WgradPPSegs& sg, float* out, int N1, int N2, int taps, const WgradPPPlan& p,
+// D: the output (rows_lim rows of it exist); ws: the slabs (unused when
+// !p.split()); the caller reduces the slabs (gemm.hip wgrad_pp_run)
+void gemm_wgrad_pp(const WgradPPSegs& sg, float* D, float* ws, int N1, int N2, int taps, const WgradPPPlan& p,
                    const WgradPPGeo* geo, const void* zero, bool acc, int rows_lim, hipStream_t s);
 bool wgrad_pp_tune(const char* key, int value);  // false: not one of its keys
 int wgrad_pp_tune_get(const char* key);

@@ -62,6 +62,7 @@ constexpr int kMaxSegs = kWgradMaxSegs;
 int g_wgpp = 1;                         // gemm_tune "wg_pp": 0 = the ring kernel everywhere
 int g_wgpp_slots = 256;                 // gemm_tune "wgpp_slots": workgroups the split over m aims for
 int g_wgpp_min_kt = 8;                  // gemm_tune "wgpp_min_kt": fewest K-tiles per slab
+int g_wgpp_tail = 1;                    // gemm_tune "wgpp_tail": 0 = never split the last round (plan)
 
 __device__ __forceinline__ int wp_swz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
 
@@ -127,26 +128,32 @@ struct WpTrk {
 // ACC (single slab only): D += the tile instead of D = the tile.
 template <int GATHER, bool ACC>
 __global__ void __launch_bounds__(kPT, 1)
-    gemm_wgrad_pp_kernel(WgradPPSegs sg, float* __restrict__ out, int N1, int N2, int64_t chunk, int tiles_j,
-                         int ntiles, int ntaps, int ldo, int rows_lim, WgradPPGeo geo,
-                         const uint16_t* __restrict__ zero) {
+    gemm_wgrad_pp_kernel(WgradPPSegs sg, float* __restrict__ D, float* __restrict__ ws, int N1, int N2,
+                         int64_t chunk, int tiles_j, int ntiles, int nfull, int ntaps, int ldo, int rows_lim,
+                         WgradPPGeo geo, const uint16_t* __restrict__ zero) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 2, wc = w & 3;
 
+  // Two regions of the grid, dispatched in this order: the whole tiles
+  // [0, nfull) (straight into D), then the split tiles' slabs. In each, a
   // bijective XCD remap, taps fastest, then tiles, then slabs: the workgroups
   // of one XCD share the slab's rows of dY / X through that XCD's L2
   int bx, by, bz;
+  const int fw = nfull * ntaps;
+  const bool direct = static_cast<int>(blockIdx.x) < fw;
   {
-    const int P = static_cast<int>(gridDim.x), wid = static_cast<int>(blockIdx.x);
+    const int P = direct ? fw : static_cast<int>(gridDim.x) - fw;
+    const int wid = static_cast<int>(blockIdx.x) - (direct ? 0 : fw);
+    const int nt = direct ? nfull : ntiles - nfull;
     const int xcd = wid & 7, q8 = P >> 3, r8 = P & 7;
     const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
     bz = lin % ntaps;
     const int rest = lin / ntaps;
-    bx = rest % ntiles;
-    by = rest / ntiles;
+    bx = (direct ? 0 : nfull) + rest % nt;
+    by = direct ? 0 : rest / nt;
   }
   const int i0 = (bx / tiles_j) * 256, j0 = (bx % tiles_j) * 256;
   // The rows are up to 4 segments (gradient-accumulation micro-steps), each
@@ -161,8 +168,9 @@ __global__ void __launch_bounds__(kPT, 1)
   kst[0] = 0;
 #pragma unroll
   for (int i = 0; i < kMaxSegs; ++i) kst[i + 1] = kst[i] + (i < sg.n ? (sg.M[i] + 63) >> 6 : 0);
-  const int64_t g0 = static_cast<int64_t>(by) * (chunk >> 6);
-  const int KT = static_cast<int>(min(kst[kMaxSegs], g0 + (chunk >> 6)) - g0);
+  const int64_t ck = direct ? kst[kMaxSegs] : chunk >> 6;  // K-tiles per slab (a whole tile: all)
+  const int64_t g0 = static_cast<int64_t>(by) * ck;
+  const int KT = static_cast<int>(min(kst[kMaxSegs], g0 + ck) - g0);
   const int sa = (sg.n > 1 && g0 >= kst[1] ? 1 : 0) + (sg.n > 2 && g0 >= kst[2] ? 1 : 0) +
                  (sg.n > 3 && g0 >= kst[3] ? 1 : 0);
   const int sbx = sa + 1 < sg.n ? sa + 1 : sa;
@@ -177,7 +185,7 @@ __global__ void __launch_bounds__(kPT, 1)
   const uint16_t* const A = Aa;
   const uint16_t* const B = Ba;
   const int64_t mz0 = g0 * 64;
-  const int64_t mz1 = min(Ma, mz0 + chunk);
+  const int64_t mz1 = min(Ma, mz0 + ck * 64);
 
   // this lane's two DMA per half-tile: image row rq = 8 w + 4 q + lane / 16,
   // physical chunk lane % 16 = logical chunk lc (channel block of 8)
@@ -385,23 +393,27 @@ __global__ void __launch_bounds__(kPT, 1)
   if (wr == 0) wp_barrier();  // both groups at the same barrier count
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (only sink DMA can be outstanding)
 
-  // epilogue: lane holds D[i][j .. j + 3] of each fragment; slab `by` (or D
-  // itself) in the [N1][taps][N2] layout, row stride ldo
-  float* o = out + static_cast<int64_t>(by) * N1 * ldo + static_cast<int64_t>(bz) * N2;
+  // epilogue: lane holds D[i][j .. j + 3] of each fragment; D itself or slab
+  // `by` (rows row0 .. N1 - 1 of D) in the [N1][taps][N2] layout, row stride ldo
+  const int row0 = (nfull / tiles_j) * 256;
+  float* o = direct ? D + static_cast<int64_t>(bz) * N2
+                    : ws + (static_cast<int64_t>(by) * (N1 - row0) - row0) * ldo + static_cast<int64_t>(bz) * N2;
+  const int lim = direct ? rows_lim : N1;
+  const bool add = ACC && direct;
   const int lr = lane & 15, lq = lane >> 4;
 #pragma unroll
   for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq) {
       f32x4 prev[2][4];
-      if constexpr (ACC) {  // all of this quadrant's loads in flight before any add
+      if (add) {  // all of this quadrant's loads in flight before any add
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int row = i0 + wr * 128 + mq * 64 + j * 16 + lr;
             const int col = j0 + wc * 64 + nq * 32 + i * 16 + lq * 4;
-            prev[i][j] = (row < rows_lim && col < N2)
+            prev[i][j] = (row < lim && col < N2)
                              ? *reinterpret_cast<const f32x4*>(o + static_cast<int64_t>(row) * ldo + col)
                              : f32x4{0.f, 0.f, 0.f, 0.f};
           }
@@ -413,15 +425,15 @@ __global__ void __launch_bounds__(kPT, 1)
           const int row = i0 + wr * 128 + mq * 64 + j * 16 + lr;
           const int col = j0 + wc * 64 + nq * 32 + i * 16 + lq * 4;
           f32x4 v = acc[mq][nq][i][j];
-          if constexpr (ACC) v += prev[i][j];
-          if (row < rows_lim && col < N2) *reinterpret_cast<f32x4*>(o + static_cast<int64_t>(row) * ldo + col) = v;
+          if (add) v += prev[i][j];
+          if (row < lim && col < N2) *reinterpret_cast<f32x4*>(o + static_cast<int64_t>(row) * ldo + col) = v;
         }
     }
 }
 
 template <int GATHER, bool ACC>
-void wgrad_pp_go(const WgradPPSegs& sg, float* out, const WgradPPPlan& p, int N1, int N2, int taps, int rows_lim,
-                 const WgradPPGeo& geo, const void* zero, hipStream_t s) {
+void wgrad_pp_go(const WgradPPSegs& sg, float* D, float* ws, const WgradPPPlan& p, int N1, int N2, int taps,
+                 int rows_lim, const WgradPPGeo& geo, const void* zero, hipStream_t s) {
   static const bool attr = [] {  // > 64 KB of dynamic LDS
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_wgrad_pp_kernel<GATHER, ACC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
@@ -429,9 +441,9 @@ void wgrad_pp_go(const WgradPPSegs& sg, float* out, const WgradPPPlan& p, int N1
   }();
   (void)attr;
   const int tiles_j = (N2 + 255) / 256;
-  hipLaunchKernelGGL((gemm_wgrad_pp_kernel<GATHER, ACC>), dim3(p.tiles * p.S * taps), dim3(kPT), kLds, s, sg, out, N1,
-                     N2, p.chunk, tiles_j, p.tiles, taps, taps * N2, rows_lim, geo,
-                     static_cast<const uint16_t*>(zero));
+  const int wgs = (p.full + (p.tiles - p.full) * p.S) * taps;
+  hipLaunchKernelGGL((gemm_wgrad_pp_kernel<GATHER, ACC>), dim3(wgs), dim3(kPT), kLds, s, sg, D, ws, N1, N2, p.chunk,
+                     tiles_j, p.tiles, p.full, taps, taps * N2, rows_lim, geo, static_cast<const uint16_t*>(zero));
 }
 }  // namespace
 
@@ -446,16 +458,39 @@ bool wgrad_pp_supported(int64_t M, int N1, int N2, int taps) {
 
 WgradPPPlan wgrad_pp_plan(int64_t M, int N1, int N2, int taps) {
   WgradPPPlan p;
-  p.tiles = ((N1 + 255) / 256) * ((N2 + 255) / 256);
+  const int tj = (N2 + 255) / 256;
+  p.tiles = ((N1 + 255) / 256) * tj;
   const int64_t kts = (M + 63) / 64;
-  int64_t S = g_wgpp_slots / (static_cast<int64_t>(p.tiles) * taps);
   const int64_t smax = kts / g_wgpp_min_kt;
-  if (S > smax) S = smax;
+  const int64_t units = static_cast<int64_t>(p.tiles) * taps;  // workgroups of whole tiles
+  p.full = p.tiles;
+  int64_t S = 1;
+  if (units < g_wgpp_slots) {  // too few tiles for the chip: split them all
+    S = g_wgpp_slots / units;
+    if (S > smax) S = smax;
+    if (S > 1) p.full = 0;
+  } else if (g_wgpp_tail) {
+    // the last round of whole tiles is less than half full: split its tiles
+    // (whole 256-row bands of D, so the slabs are one contiguous row range)
+    // over the CUs that round would leave idle
+    const int64_t rem = units % g_wgpp_slots;
+    if (rem > 0 && 2 * rem <= g_wgpp_slots) {
+      const int64_t t = ((rem + taps - 1) / taps + tj - 1) / tj * tj;
+      int64_t st = g_wgpp_slots / (t * taps);
+      if (st > smax) st = smax;
+      if (st >= 2 && t < p.tiles) {
+        p.full = static_cast<int>(p.tiles - t);
+        S = st;
+      }
+    }
+  }
   if (S < 1) S = 1;
   p.chunk = ((kts + S - 1) / S) * 64;
   p.S = static_cast<int>((M + p.chunk - 1) / p.chunk);
   return p;
 }
+
+int wgrad_pp_tail_row0(const WgradPPPlan& p, int N2) { return (p.full / ((N2 + 255) / 256)) * 256; }
 
 int64_t wgrad_pp_rows(const WgradPPSegs& sg) {
   int64_t kt = 0;
@@ -463,25 +498,25 @@ int64_t wgrad_pp_rows(const WgradPPSegs& sg) {
   return kt * 64;
 }
 
-bool wgrad_pp_segs_ok(const WgradPPSegs& sg, int64_t chunk) {
+bool wgrad_pp_segs_ok(const WgradPPSegs& sg, const WgradPPPlan& p) {
+  // a whole tile's "slab" is all the rows
+  const int64_t chunk = p.full > 0 ? wgrad_pp_rows(sg) : p.chunk;
   for (int i = 1; i + 1 < sg.n; ++i)
     if ((sg.M[i] + 63) / 64 < chunk / 64) return false;  // a slab would span three segments
-  return sg.n >= 1 && sg.n <= kWgradMaxSegs;
+  return sg.n >= 1 && sg.n <= kWgradMaxSegs && p.chunk % 64 == 0;
 }
 
-void gemm_wgrad_pp(const WgradPPSegs& sg_in, float* out, int N1, int N2, int taps, const WgradPPPlan& p_in,
+void gemm_wgrad_pp(const WgradPPSegs& sg, float* D, float* ws, int N1, int N2, int taps, const WgradPPPlan& p,
                    const WgradPPGeo* geo, const void* zero, bool acc, int rows_lim, hipStream_t s) {
   const WgradPPGeo g = geo ? *geo : WgradPPGeo{1, 1, 1, 1, 1, 0, 1};
-  if ((geo && sg_in.n != 1) || !wgrad_pp_segs_ok(sg_in, p_in.chunk) || p_in.chunk % 64 != 0)
-    throw std::runtime_error("gemm_wgrad_pp: bad segment list");
-  const WgradPPSegs& sg = sg_in;
-  const WgradPPPlan& p = p_in;
+  if ((geo && sg.n != 1) || !wgrad_pp_segs_ok(sg, p)) throw std::runtime_error("gemm_wgrad_pp: bad segment list");
+  if (p.split() && ws == nullptr) throw std::runtime_error("gemm_wgrad_pp: the plan's slabs need a workspace");
   if (geo) {
-    if (acc) wgrad_pp_go<1, true>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);
-    else wgrad_pp_go<1, false>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);
+    if (acc) wgrad_pp_go<1, true>(sg, D, ws, p, N1, N2, taps, rows_lim, g, zero, s);
+    else wgrad_pp_go<1, false>(sg, D, ws, p, N1, N2, taps, rows_lim, g, zero, s);
   } else {
-    if (acc) wgrad_pp_go<0, true>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);
-    else wgrad_pp_go<0, false>(sg, out, p, N1, N2, taps, rows_lim, g, zero, s);
+    if (acc) wgrad_pp_go<0, true>(sg, D, ws, p, N1, N2, taps, rows_lim, g, zero, s);
+    else wgrad_pp_go<0, false>(sg, D, ws, p, N1, N2, taps, rows_lim, g, zero, s);
   }
 }
 
@@ -490,6 +525,7 @@ bool wgrad_pp_tune(const char* key, int value) {
   if (k == "wg_pp") g_wgpp = value != 0;
   else if (k == "wgpp_slots") g_wgpp_slots = value < 8 ? 8 : value;
   else if (k == "wgpp_min_kt") g_wgpp_min_kt = value < 1 ? 1 : value;
+  else if (k == "wgpp_tail") g_wgpp_tail = value != 0;
   else return false;
   return true;
 }
@@ -498,6 +534,7 @@ int wgrad_pp_tune_get(const char* key) {
   if (k == "wg_pp") return g_wgpp;
   if (k == "wgpp_slots") return g_wgpp_slots;
   if (k == "wgpp_min_kt") return g_wgpp_min_kt;
+  if (k == "wgpp_tail") return g_wgpp_tail;
   return -1;
 }
 

@@ -132,3 +132,42 @@ def test_wgrad_pp_conv_gathered(cuda, shape):
     with _tune(wg_pp=0):
         dw0 = _C.conv_wgrad(gy, x, k, k, s, p)
     assert _rel(dw0, ref) < 1e-5
+
+
+def test_wgrad_pp_tail_split(cuda):
+    """Tail split (wgrad_pp_plan): whole tiles straight into D, the last,
+    partial round's tiles split over rows into slabs that the reduction adds
+    from wgrad_pp_tail_row0 on — forced at small sizes by a small slot count.
+    Linear with the padded-vocabulary out_rows + accumulation, a gathered 3x3
+    conv (taps in the workgroup count) and a two-segment launch."""
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    g = torch.Generator().manual_seed(15)
+    # 9 x 3 = 27 tiles on 24 slots: 24 whole, the last band of 3 in 8 slabs
+    m, n1, n2, rows = 4096, 2112, 768, 2100
+    gy, x = _bf((m, n1), g, cuda), _bf((m, n2), g, cuda)
+    gy[:, rows:] = 0
+    full = (gy.double().t() @ x.double())
+    base = torch.randn(rows, n2, generator=g).to(cuda)
+    for tail in (1, 0):
+        with _tune(wg_pp=1, wgpp_slots=24, wgpp_min_kt=8, wgpp_tail=tail):
+            acc = base.clone()
+            _C.conv1x1_wgrad(gy, x, accumulate_into=acc, out_rows=rows)
+            dw = _C.conv1x1_wgrad(gy, x)
+        assert _rel(acc, base.double() + full[:rows]) < 1e-5, tail
+        assert _rel(dw, full) < 1e-5, tail
+    # 3 tiles x 9 taps = 27 workgroups on 24 slots: 2 tiles whole, 1 in 2 slabs
+    x4 = torch.randn(4, 256, 14, 14, generator=g).to(torch.bfloat16).to(cuda).contiguous(
+        memory_format=torch.channels_last)
+    gy4 = torch.randn(4, 768, 14, 14, generator=g).to(torch.bfloat16).to(cuda).contiguous(
+        memory_format=torch.channels_last)
+    with _tune(wg_pp=1, wgpp_slots=24, wgpp_min_kt=1):
+        dw = _C.conv_wgrad(gy4, x4, 3, 3, 1, 1)
+    assert _rel(dw, _conv_wgrad_ref(gy4, x4, 3, 1, 1)) < 1e-5
+    # two segments (micro-steps) in one launch under the tail plan
+    gys = [_bf((r, n1), g, cuda) for r in (2048, 2000)]
+    xs = [_bf((r, n2), g, cuda) for r in (2048, 2000)]
+    ref = sum(a.double().t() @ b.double() for a, b in zip(gys, xs))
+    with _tune(wg_pp=1, wgpp_slots=24, wgpp_min_kt=8):
+        dw = _C.conv1x1_wgrad_multi(gys, xs)
+    assert _rel(dw, ref) < 1e-5
