@@ -231,6 +231,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("table_cache_size", &ops::table_cache_size);
 
   m.def("gemm_tune", [](const std::string& k, int v) { kern::gemm_tune(k.c_str(), v); });
+  m.def("gemm_pp_splitk", [](int64_t M, int N, int K) { return kern::gemm_pp_splitk(M, N, K); },
+        "split-K count gemm_pp uses for this shape (1 = none)");
   m.def("gemm_tune_get", [](const std::string& k) { return kern::gemm_tune_get(k.c_str()); });
 
   fused::bind(m);

@@ -365,6 +365,13 @@ std::vector<at::Tensor> gemm_pp(const at::Tensor& x, const at::Tensor& w, const 
   shape.back() = N;
   at::Tensor y = at::empty(shape, x.options());
   at::Tensor g = gelu ? at::empty(shape, x.options()) : at::Tensor();
+  const int S = b.has_value() || N % 8 != 0 ? 1 : kern::gemm_pp_splitk(M, static_cast<int>(N), static_cast<int>(K));
+  if (S > 1) {  // split-K: fp32 partial slabs from the caching allocator
+    at::Tensor ws = at::empty({S * M * N}, x.options().dtype(at::kFloat));
+    kern::gemm_pp_splitk_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, static_cast<int>(N), static_cast<int>(K), N,
+                              S, ws.data_ptr<float>(), stream_of(x));
+    return {y};
+  }
   kern::gemm_pp_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, static_cast<int>(N), static_cast<int>(K), N, bp,
                      gelu ? g.data_ptr() : nullptr, static_cast<int>(gelu), stream_of(x));
   if (gelu) return {g, y};

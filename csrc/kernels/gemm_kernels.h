@@ -60,6 +60,14 @@ void gemm_pp_tune(const char* key, int value);
 int gemm_pp_tune_get(const char* key);
 void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
                   void* c2, int gelu, hipStream_t s);
+// Split-K on the same kernel for shapes whose tiles leave most CUs idle (the
+// LM-head data gradient: 96 tiles, K = 50,304): gemm_pp_splitk = the split
+// count a time model picks (1 = none; gemm_tune "pp_sk" 0 disables, "pp_sk_force"
+// pins); gemm_pp_splitk_bf16 writes S fp32 partial slabs into ws (S x M x N
+// floats) and sums them into C in a fixed order. No bias / GELU; N % 8 == 0.
+int gemm_pp_splitk(int64_t M, int N, int K);
+void gemm_pp_splitk_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, int S, float* ws,
+                         hipStream_t s);
 // MLP backward through the GELU on the ping-pong GEMM: C [M, N] = bf16(A·Bᵀ) ⊙
 // gelu'(h) (h [M, N] bf16), db[N] += column sums of C (fp32 atomics). N % 8 == 0.
 void gemm_pp_gelubwd_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* h, float* db,

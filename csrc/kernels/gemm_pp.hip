@@ -71,6 +71,8 @@ constexpr int kPPLds = 2 * kSlot + 2048;   // 133,120 B (+ 4 N B of bias): one w
 int g_pp_cus = 256;                        // persistent grid size (gemm_tune "pp_cus")
 int g_pp_stage = 1;                        // LDS-staged epilogue for the last tile (gemm_tune "pp_stage")
 int g_pp_v1 = 1;                           // one tile per workgroup (gemm_tune "pp_v1"; 0: persistent)
+int g_pp_sk = 1;                           // split-K where the tiles leave most CUs idle (gemm_tune "pp_sk")
+int g_pp_sk_force = 0;                     // gemm_tune "pp_sk_force": this split count on every shape (A/B)
 
 __device__ __forceinline__ float pp_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float pp_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -120,14 +122,18 @@ __device__ __forceinline__ float pp_gelu_dx(float x) {
 // EPI: 0 = C = A·Bᵀ; 1 = + bias; 2 / 3 = + bias, c2 = gelu(C) (tanh / erf);
 // 4 / 5 = the MLP backward's data gradient through the GELU (tanh / erf):
 // C = bf16(A·Bᵀ) ⊙ gelu'(h) (h [M, N] bf16, ldc apart) and dbias[N] += the
-// column sums of the stored C (fp32 atomics: 2 per column per workgroup).
+// column sums of the stored C (fp32 atomics: 2 per column per workgroup);
+// 6 = split-K partial: K-tiles [ks * kchunk, +kchunk) of the tile, fp32 into
+// slab ks of ws ([S][M][N]), summed in a fixed order by pp_splitk_reduce.
 template <int EPI>
 __global__ void __launch_bounds__(kPT, 1)
     gemm_pp1_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                    int64_t M, int N, int K, int64_t ldc, int tiles_n, const float* __restrict__ bias,
-                   uint16_t* __restrict__ c2, const uint16_t* __restrict__ hsrc, float* __restrict__ dbias) {
+                   uint16_t* __restrict__ c2, const uint16_t* __restrict__ hsrc, float* __restrict__ dbias,
+                   float* __restrict__ ws, int kchunk) {
   constexpr bool BIAS = EPI >= 1 && EPI <= 3;
   constexpr bool GB = EPI == 4 || EPI == 5;
+  constexpr bool SK = EPI == 6;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -135,14 +141,19 @@ __global__ void __launch_bounds__(kPT, 1)
   const int wr = w >> 2, wc = w & 3;
 
   // bijective XCD remap: the workgroups of one XCD take a contiguous tile range
-  // (the N-tiles of an M-tile share A through that XCD's L2)
+  // (the N-tiles of an M-tile share A through that XCD's L2); split-K: tiles
+  // fastest, then K-splits (one XCD's workgroups share a K range)
   const int P = static_cast<int>(gridDim.x);
   const int wid = static_cast<int>(blockIdx.x);
   const int xcd = wid & 7, q8 = P >> 3, r8 = P & 7;
-  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
+  const int vl = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (wid >> 3);
+  const int ntl = static_cast<int>((M + 255) >> 8) * tiles_n;
+  const int v = SK ? vl % ntl : vl;
+  const int ks = SK ? vl / ntl : 0;
   const int64_t m0 = static_cast<int64_t>(v / tiles_n) * 256;
   const int n0 = (v % tiles_n) * 256;
-  const int KT = K >> 6;
+  const int kt0 = ks * kchunk;  // first K-tile of this split
+  const int KT = SK ? min(kchunk, (K >> 6) - kt0) : K >> 6;
 
   // per-lane source element offsets (k = 0) of this wave's two DMA per
   // half-tile: image row i = 16 w + 8 q + lane / 8, physical chunk lane % 8
@@ -168,7 +179,7 @@ __global__ void __launch_bounds__(kPT, 1)
   auto issue = [&](int h, int kt) {
     const bool real = kt < KT;
     const uint16_t* base = (h == 0 || h == 3) ? A : B;
-    const int k0 = real ? kt * 64 : 0;
+    const int k0 = real ? (kt0 + kt) * 64 : 0;
     char* dst = real ? lds + (kt & 1) * kSlot + h * kHT + w * 2048 : lds + kSink;
     pp_glds(base + off[h][0] + k0, dst);
     pp_glds(base + off[h][1] + k0, dst + 1024);
@@ -261,6 +272,23 @@ __global__ void __launch_bounds__(kPT, 1)
   }
   if (wr == 0) pp_barrier();  // both groups at the same barrier count; all ring reads done
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (only sink DMA can be outstanding)
+
+  if constexpr (SK) {  // fp32 partial straight from the accumulators: 4 columns (16 B) per lane
+    float* o = ws + static_cast<int64_t>(ks) * M * N;
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t row = m0 + wr * 128 + mq * 64 + j * 16 + lr;
+            const int col = n0 + wc * 64 + nq * 32 + i * 16 + lq * 4;
+            if (row < M && col < N) *reinterpret_cast<f32x4*>(o + row * N + col) = acc[mq][nq][i][j];
+          }
+    return;
+  }
 
   // epilogue: each wave stages its 128 x 64 output (bf16, 128-B rows, 16-B
   // chunks XOR row & 7) in its own 16 KB of the ring, then stores whole rows
@@ -792,7 +820,7 @@ void gemm_pp_launch(const void* A, const void* B, void* C, int64_t M, int N, int
     (void)attr1;
     hipLaunchKernelGGL((gemm_pp1_kernel<EPI>), dim3(tiles), dim3(kPT), kPPLds, s, static_cast<const uint16_t*>(A),
                        static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N, K, ldc, tiles_n, bias,
-                       static_cast<uint16_t*>(c2), nullptr, nullptr);
+                       static_cast<uint16_t*>(c2), nullptr, nullptr, nullptr, 0);
     return;
   }
   const size_t lds = kPPLds + (EPI >= 1 ? static_cast<size_t>(N) * 4 : 0);
@@ -815,9 +843,74 @@ void gemm_pp_gb_launch(const void* A, const void* B, void* C, int64_t M, int N, 
   const int tiles_n = (N + 255) / 256;
   hipLaunchKernelGGL((gemm_pp1_kernel<EPI>), dim3(tiles_m * tiles_n), dim3(kPT), kPPLds, s,
                      static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N,
-                     K, static_cast<int64_t>(N), tiles_n, nullptr, nullptr, static_cast<const uint16_t*>(h), db);
+                     K, static_cast<int64_t>(N), tiles_n, nullptr, nullptr, static_cast<const uint16_t*>(h), db,
+                     nullptr, 0);
+}
+// C (bf16, row stride ldc) = Σ_s ws[s] (fp32 [S][M][N]) in slab order: one
+// float4 (4 columns) per thread, N % 4 == 0
+__global__ void __launch_bounds__(256) pp_splitk_reduce(const f32x4* __restrict__ ws, int S, int64_t n4, int n4row,
+                                                        uint16_t* __restrict__ C, int64_t ldc) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n4;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    f32x4 a = ws[i];
+    for (int s = 1; s < S; ++s) a += ws[s * n4 + i];
+    const int64_t row = i / n4row;
+    const int c = static_cast<int>(i - row * n4row) * 4;
+    *reinterpret_cast<uint2*>(C + row * ldc + c) = make_uint2(pp_pack(a[0], a[1]), pp_pack(a[2], a[3]));
+  }
 }
 }  // namespace
+
+int gemm_pp_splitk(int64_t M, int N, int K) {
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int KT = K / 64;
+  if (g_pp_sk_force > 0) return KT / g_pp_sk_force >= 1 ? g_pp_sk_force : 1;
+  if (!g_pp_sk || 2 * tiles > 256) return 1;
+  // time model in units of one K-tile of one workgroup (~1 us on a full chip):
+  // rounds of 256 workgroups x K-tiles per split, + the slabs' fp32 write and
+  // read back (at ~4 TB/s), + one launch
+  const double kt_us = 1.0, bw = 4.0e6;  // bytes per us
+  auto cost = [&](int S) {
+    const int64_t rounds = (tiles * S + 255) / 256;
+    const double slabs = S > 1 ? (S * 8.0 * M * N) / bw + 4.0 : 0.0;
+    return static_cast<double>(rounds) * ((KT + S - 1) / S) * kt_us + slabs;
+  };
+  // (ranks the LM-head data gradient's measured S = 5 < 8 < 2 ~ 4 < 1 the
+  // same way: 516 / 528 / 568 / 569 / 908 us, profiles/r5_splitk_sweep.jsonl)
+  int best = 1;
+  double bc = cost(1);
+  for (int S = 2; S <= 16 && KT / S >= 8; ++S) {
+    const double c = cost(S);
+    if (c < bc) {
+      bc = c;
+      best = S;
+    }
+  }
+  return best;
+}
+
+void gemm_pp_splitk_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, int S, float* ws,
+                         hipStream_t s) {
+  if (S < 2 || N % 8 != 0) throw std::runtime_error("gemm_pp_splitk: S >= 2 and N % 8 == 0");
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_pp1_kernel<6>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPPLds);
+    return true;
+  }();
+  (void)attr;
+  const int KT = K / 64;
+  const int kchunk = (KT + S - 1) / S;
+  S = (KT + kchunk - 1) / kchunk;  // every split non-empty
+  const int tiles_n = (N + 255) / 256;
+  const int tiles = static_cast<int>((M + 255) / 256) * tiles_n;
+  hipLaunchKernelGGL((gemm_pp1_kernel<6>), dim3(tiles * S), dim3(kPT), kPPLds, s, static_cast<const uint16_t*>(A),
+                     static_cast<const uint16_t*>(B), nullptr, M, N, K, ldc, tiles_n, nullptr, nullptr, nullptr,
+                     nullptr, ws, kchunk);
+  const int64_t n4 = M * N / 4;
+  const int64_t blocks = (n4 + 255) / 256;
+  hipLaunchKernelGGL(pp_splitk_reduce, dim3(static_cast<unsigned>(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s,
+                     reinterpret_cast<const f32x4*>(ws), S, n4, N / 4, static_cast<uint16_t*>(C), ldc);
+}
 
 void gemm_pp_gelubwd_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, const void* h, float* db,
                           bool tanh_approx, hipStream_t s) {
@@ -831,12 +924,16 @@ void gemm_pp_tune(const char* key, int value) {
   if (k == "pp_cus") g_pp_cus = value < 8 ? 8 : (value > 256 ? 256 : value);
   if (k == "pp_stage") g_pp_stage = value != 0;
   if (k == "pp_v1") g_pp_v1 = value != 0;
+  if (k == "pp_sk") g_pp_sk = value != 0;
+  if (k == "pp_sk_force") g_pp_sk_force = value < 0 ? 0 : value;
 }
 int gemm_pp_tune_get(const char* key) {
   const std::string k(key);
   if (k == "pp_cus") return g_pp_cus;
   if (k == "pp_stage") return g_pp_stage;
   if (k == "pp_v1") return g_pp_v1;
+  if (k == "pp_sk") return g_pp_sk;
+  if (k == "pp_sk_force") return g_pp_sk_force;
   return -1;
 }
 

@@ -558,15 +558,27 @@ __global__ void __launch_bounds__(kThreads) comm_emulate_kernel(const uint4* __r
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int64_t begin = static_cast<int64_t>(blockIdx.x) * per_block16;
   // wrap by subtraction: begin + i < 4 n16 (bytes_move ≤ 2 bytes_buf); a 64-bit
-  // modulo per element made the copy VALU-bound (~50 GB/s algorithm bandwidth
-  // on 16 channels), slower than every modelled link: the emulated time
-  // never depended on busbw (NOTES §27)
-  for (int64_t i = threadIdx.x; i < per_block16; i += kThreads) {
-    int64_t k = begin + i;
-    k -= k >= n16 ? n16 : 0;
-    k -= k >= n16 ? n16 : 0;
-    k -= k >= n16 ? n16 : 0;
-    dst[k] = src[k];
+  // modulo per element made the copy VALU-bound. 16 loads per lane in flight
+  // before their stores (64 KB per channel): with one, the copy was latency-
+  // bound at ~90 GB/s algorithm bandwidth on 16 channels, slower than every
+  // modelled link, so the emulated time never depended on busbw (NOTES §27)
+  constexpr int U = 16;
+  for (int64_t i0 = threadIdx.x; i0 < per_block16; i0 += static_cast<int64_t>(kThreads) * U) {
+    uint4 v[U];
+    int64_t kk[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + static_cast<int64_t>(u) * kThreads;
+      int64_t k = begin + (i < per_block16 ? i : 0);
+      k -= k >= n16 ? n16 : 0;
+      k -= k >= n16 ? n16 : 0;
+      k -= k >= n16 ? n16 : 0;
+      kk[u] = k;
+      v[u] = src[k];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + static_cast<int64_t>(u) * kThreads < per_block16) dst[kk[u]] = v[u];
   }
   // hold the CU for the rest of the collective's duration
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);

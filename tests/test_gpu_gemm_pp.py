@@ -84,3 +84,51 @@ def test_gemm_pp_repeatable_and_asymmetric(cuda):
         assert torch.equal(C.gemm_pp(x, w)[0], y0)
     eye = torch.eye(256, 1024, device=cuda, dtype=torch.bfloat16)
     assert torch.equal(C.gemm_pp(eye, w)[0], w[:, :256].t().contiguous())
+
+
+@pytest.mark.parametrize("M,N,K,S", [
+    (8192, 768, 6272, 2),        # LM-head data gradient shape (K = 50,304 cut to 98 K-tiles for test time)
+    (1000, 520, 4096, 3),        # M / N tails, ragged last split (64 K-tiles / 3)
+    (256, 256, 64 * 9, 4),       # 9 K-tiles in 4 splits (the last one short)
+    (512, 1032, 2048, 16),       # N % 256 != 0, many splits
+])
+def test_gemm_pp_splitk_matches_fp32(cuda, M, N, K, S):
+    """Split-K (EPI 6 partial slabs + the ordered reduction): forced split
+    counts against the fp32 reference, and the split result equal to the
+    unsplit kernel to fp32-summation-order rounding of the bf16 output."""
+    from distributed_compute_pytorch_amd._ext import C
+
+    g = torch.Generator(device=cuda).manual_seed(5)
+    x = (torch.rand(M, K, device=cuda, generator=g) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=cuda, generator=g) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+    ref = _ref(x, w, None)
+    old = (C.gemm_tune_get("pp_sk"), C.gemm_tune_get("pp_sk_force"))
+    try:
+        C.gemm_tune("pp_sk_force", S)
+        y = C.gemm_pp(x, w)[0]
+        C.gemm_tune("pp_sk_force", 0)
+        C.gemm_tune("pp_sk", 0)
+        y1 = C.gemm_pp(x, w)[0]
+    finally:
+        C.gemm_tune("pp_sk", old[0])
+        C.gemm_tune("pp_sk_force", old[1])
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert _rel(y, ref) < 6e-3
+    assert _rel(y, y1) < 6e-3
+    # repeatable: the reduction order is fixed
+    C.gemm_tune("pp_sk_force", S)
+    try:
+        y2 = C.gemm_pp(x, w)[0]
+    finally:
+        C.gemm_tune("pp_sk_force", old[1])
+    assert torch.equal(y, y2)
+
+
+def test_gemm_pp_splitk_plan():
+    """The split count the time model picks: the LM-head data gradient (96
+    tiles, 786 K-tiles) splits; full-chip shapes and short K do not."""
+    from distributed_compute_pytorch_amd._ext import C
+
+    assert C.gemm_pp_splitk(8192, 768, 50304) >= 2
+    assert C.gemm_pp_splitk(8192, 2304, 768) == 1
+    assert C.gemm_pp_splitk(8192, 768, 768) == 1
