@@ -36,7 +36,7 @@ class _Branchy(nn.Module):
 def _torch_pg(rank, world):
     import torch.distributed as tdist
 
-    port = int(os.environ["MASTER_PORT"]) + 1
+    port = int(os.environ["DCP_TEST_TORCH_PORT"])  # picked free by run_world
     tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
                              timeout=datetime.timedelta(seconds=60))
     return tdist
