@@ -91,13 +91,30 @@ __device__ __forceinline__ bf16x8 tr_op(const char* base, int rbase, int dcol0, 
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// LDS DMA (16 / 4 B per lane) into the wave-uniform LDS address lds_dst (+
+// lane x size). Inline asm on purpose: a compiler-visible global_load_lds is a
+// pending LDS write to hipcc, which then put s_waitcnt vmcnt(0) before the
+// first LDS read after it — in every loop iteration, so each tile waited for
+// the NEXT tile's DMA to land in the middle of its own compute (PMC r5: 0.3 of
+// wave cycles waiting, MFMA busy 0.14-0.22). Hidden, the ring is ordered by
+// the explicit wait_vm0 + barrier at the top of each iteration only. M0 is
+// compiler-reserved: set and restored in-statement.
+__device__ __forceinline__ uint32_t lds_u32(const char* p) {
+  return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
+}
 __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_u32(lds_dst))
+               : "memory");
 }
 __device__ __forceinline__ void glds4(const void* src, char* lds_dst) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_dst, 4, 0, 0);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_u32(lds_dst))
+               : "memory");
 }
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void barrier() {
@@ -386,6 +403,9 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
     const char* sV = sK + kTile;
     const int kb = it * kKB;
     if (CAUSAL && kb > tile * 128 + wave * 32 + 31) continue;
+    // one 32-key half at a time: issuing both halves' S / dP first (as dK/dV
+    // does) took the kernel from 152 to 197 registers, three waves per SIMD to
+    // two, and measured slower (GPT-2 43.1 → 45.7 µs, NOTES §28)
 #pragma unroll 1
     for (int kh = 0; kh < 2; ++kh) {
       f32x16 s = zero16(), dp = zero16();
@@ -496,19 +516,30 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
     const float* sL = reinterpret_cast<const float*>(sQ + 2 * kTile);
     const float* sD = sL + kKB;
     const int qb = (qt0 + it) * kKB;
-    // one 32-query sub-tile at a time (unrolling both doubles the live
-    // S / dP accumulators and drops the kernel to one wave per SIMD)
-#pragma unroll 1
+    // Both 32-query sub-tiles' S and dP are issued first: the second pair's 8
+    // MFMAs run in the matrix pipe while the first pair's softmax-gradient VALU
+    // work (exp, dropout, mask, packing: ~18 VALU per MFMA, PMC r5) issues;
+    // one pair at a time left the pipe idle through every VALU block (MFMA
+    // busy 0.17-0.22). 32 more live registers (VGPR-form MFMA: 2 waves / SIMD
+    // either way). Sub-tiles that precede every key of this wave skip their
+    // VALU and dV / dK MFMAs (the diagonal tiles only).
+    if (CAUSAL && qb + 63 < kb0 + wave * 32) continue;  // every query of the tile precedes every key
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      s[qs] = zero16();
+      dp[qs] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s[qs] = mfma(row_rd(sQ, 32 * qs + (lane & 31), 2 * ks + hh), kf[ks], s[qs]);
+        dp[qs] = mfma(row_rd(sG, 32 * qs + (lane & 31), 2 * ks + hh), vf[ks], dp[qs]);
+      }
+    }
+#pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
       if (CAUSAL && qb + 32 * qs + 31 < kb0 + wave * 32) continue;  // every query precedes every key
       // the mask only where some query of the slice precedes the wave's last key
       const bool diag = CAUSAL && qb + 32 * qs < kb0 + wave * 32 + 31;
-      f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s = mfma(row_rd(sQ, 32 * qs + (lane & 31), 2 * ks + hh), kf[ks], s);
-        dp = mfma(row_rd(sG, 32 * qs + (lane & 31), 2 * ks + hh), vf[ks], dp);
-      }
       // rows: query qb + 32qs + (r&3) + 8(r>>2) + 4hh; column: this lane's key.
       // One k-step (8 rows) at a time: P∘keep and dS packed to bf16 right away
       // (short fp32 live ranges).
@@ -537,9 +568,9 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
             const int qrow = qb + rl + e;
-            float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lv[e]));
+            float p = __builtin_amdgcn_exp2f(fmaf(s[qs][r], c, -lv[e]));
             if (CAUSAL && diag) p = key > qrow ? 0.f : p;
-            float gg = dp[r], pk = p;
+            float gg = dp[qs][r], pk = p;
             if (DROP) {
               const bool kp = drop_keep(hrow[e], key & 3, thr);
               gg = kp ? gg : 0.f;
