@@ -60,6 +60,15 @@ void gemm_pp_tune(const char* key, int value);
 int gemm_pp_tune_get(const char* key);
 void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
                   void* c2, int gelu, hipStream_t s);
+// 128 x 192 ping-pong tiles (gemm_pq.hip) for the shapes 256 x 256 tiles
+// under-fill (the transformer N = 768 / 2,304 / 3,072 Linears): gemm_pp_bf16
+// takes it when gemm_pq_pick says its fill wins (gemm_tune "pp_tile": 0 auto,
+// 1 = always 256 x 256, 2 = always 128 x 192 where supported). N % 8 == 0,
+// K % 64 == 0, ldc % 8 == 0.
+bool gemm_pq_supported(int64_t M, int64_t N, int64_t K, int64_t ldc);
+bool gemm_pq_pick(int64_t M, int64_t N);
+void gemm_pq_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
+                  void* c2, int gelu, hipStream_t s);
 // Split-K on the same kernel for shapes whose tiles leave most CUs idle (the
 // LM-head data gradient: 96 tiles, K = 50,304): gemm_pp_splitk = the split
 // count a time model picks (1 = none; gemm_tune "pp_sk" 0 disables, "pp_sk_force"

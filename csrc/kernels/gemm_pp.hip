@@ -71,6 +71,7 @@ constexpr int kPPLds = 2 * kSlot + 2048;   // 133,120 B (+ 4 N B of bias): one w
 int g_pp_cus = 256;                        // persistent grid size (gemm_tune "pp_cus")
 int g_pp_stage = 1;                        // LDS-staged epilogue for the last tile (gemm_tune "pp_stage")
 int g_pp_v1 = 1;                           // one tile per workgroup (gemm_tune "pp_v1"; 0: persistent)
+int g_pp_tile = 0;                         // gemm_tune "pp_tile": 0 auto, 1 = 256 x 256, 2 = 128 x 192 (gemm_pq.hip)
 int g_pp_sk = 1;                           // split-K where the tiles leave most CUs idle (gemm_tune "pp_sk")
 int g_pp_sk_force = 0;                     // gemm_tune "pp_sk_force": this split count on every shape (A/B)
 
@@ -925,6 +926,7 @@ void gemm_pp_tune(const char* key, int value) {
   if (k == "pp_stage") g_pp_stage = value != 0;
   if (k == "pp_v1") g_pp_v1 = value != 0;
   if (k == "pp_sk") g_pp_sk = value != 0;
+  if (k == "pp_tile") g_pp_tile = value < 0 ? 0 : (value > 2 ? 2 : value);
   if (k == "pp_sk_force") g_pp_sk_force = value < 0 ? 0 : value;
 }
 int gemm_pp_tune_get(const char* key) {
@@ -933,6 +935,7 @@ int gemm_pp_tune_get(const char* key) {
   if (k == "pp_stage") return g_pp_stage;
   if (k == "pp_v1") return g_pp_v1;
   if (k == "pp_sk") return g_pp_sk;
+  if (k == "pp_tile") return g_pp_tile;
   if (k == "pp_sk_force") return g_pp_sk_force;
   return -1;
 }
@@ -947,6 +950,10 @@ void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
                   void* c2, int gelu, hipStream_t s) {
   if (bias != nullptr && !(g_pp_v1 && N % 8 == 0) && static_cast<size_t>(N) * 4 + kPPLds > 160 * 1024)
     throw std::runtime_error("gemm_pp: the persistent kernel's bias epilogue needs N <= 7,168");
+  if (g_pp_tile != 1 && gemm_pq_supported(M, N, K, ldc) && (g_pp_tile == 2 || gemm_pq_pick(M, N))) {
+    gemm_pq_bf16(A, B, C, M, N, K, ldc, bias, c2, gelu, s);  // 128 x 192 tiles fill the chip better here
+    return;
+  }
   if (bias == nullptr) gemm_pp_launch<0>(A, B, C, M, N, K, ldc, nullptr, nullptr, s);
   else if (gelu == 1) gemm_pp_launch<2>(A, B, C, M, N, K, ldc, bias, c2, s);
   else if (gelu == 2) gemm_pp_launch<3>(A, B, C, M, N, K, ldc, bias, c2, s);

@@ -23,24 +23,29 @@ def _rel(a, b):
 # persistent grid: ≤ 256 workgroups stream several tiles each once tiles > 256
 # (K = 64 / 128: one / two K-tiles per tile, so the DMA runs 1-2 tiles ahead
 # across tile boundaries; N % 4 tails; M tails)
-SHAPES = [(256, 256, 64), (512, 768, 768), (1000, 264, 128), (37, 520, 192), (4096, 3072, 768),
+SHAPES = [(256, 256, 64), (512, 768, 768), (8192, 768, 768), (300, 200, 128), (1000, 264, 128), (37, 520, 192), (4096, 3072, 768),
           (777, 2304, 3072), (256, 4096, 640), (16384, 768, 3072), (8192, 2304, 768), (9000, 2052, 128),
           (262144, 256, 64), (100352, 1024, 256), (3001, 4100, 320)]
 
 
-@pytest.fixture(params=["default", "persistent", "persistent_regepi"])
+@pytest.fixture(params=["default", "tile256", "persistent", "persistent_regepi", "pq"])
 def pp_variant(request):
-    """default: single-tile kernel for grids of <= 256 tiles, else persistent
-    with the last tile staged through LDS; persistent: the persistent kernel
-    for every grid; _regepi: every tile's epilogue from the registers."""
+    """default: the automatic tile choice (gemm_pq_pick: 128 x 192 where it
+    fills the chip better, else 256 x 256); tile256: always the single-tile
+    256 x 256 kernel; persistent: the persistent 256 x 256 kernel for every
+    grid; _regepi: every tile's epilogue from the registers; pq: always the
+    128 x 192 kernel (gemm_pq.hip) where the shape is supported."""
     from distributed_compute_pytorch_amd._ext import C
 
-    v1, stage = {"default": (1, 1), "persistent": (0, 1), "persistent_regepi": (0, 0)}[request.param]
+    v1, stage, tile = {"default": (1, 1, 0), "tile256": (1, 1, 1), "persistent": (0, 1, 1),
+                       "persistent_regepi": (0, 0, 1), "pq": (1, 1, 2)}[request.param]
     C.gemm_tune("pp_v1", v1)
     C.gemm_tune("pp_stage", stage)
+    C.gemm_tune("pp_tile", tile)
     yield request.param
     C.gemm_tune("pp_v1", 1)
     C.gemm_tune("pp_stage", 1)
+    C.gemm_tune("pp_tile", 0)
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)

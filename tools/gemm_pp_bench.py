@@ -19,7 +19,8 @@ SHAPES = [  # (name, M, N, K)
     ("bert qkv/o 768->768", 16384, 768, 768), ("bert fc1 768->3072", 16384, 3072, 768),
     ("bert fc2 3072->768", 16384, 768, 3072), ("bert dgrad fc1 3072->768", 16384, 768, 3072),
     ("gpt2 c_attn 768->2304", 8192, 2304, 768), ("gpt2 fc 768->3072", 8192, 3072, 768),
-    ("gpt2 proj 3072->768", 8192, 768, 3072), ("gpt2 lmhead 768->50304", 8192, 50304, 768),
+    ("gpt2 proj 3072->768", 8192, 768, 3072), ("gpt2 attn-proj 768->768", 8192, 768, 768),
+    ("gpt2 dgrad qkv 2304->768", 8192, 768, 2304), ("gpt2 lmhead 768->50304", 8192, 50304, 768),
     ("square 4096", 4096, 4096, 4096), ("square 8192", 8192, 8192, 8192),
     ("rn50 56x56 64->256", 512 * 56 * 56, 256, 64), ("rn50 28x28 512->128", 512 * 28 * 28, 128, 512),
     ("rn50 14x14 256->1024", 512 * 14 * 14, 1024, 256), ("rn50 14x14 1024->256", 512 * 14 * 14, 256, 1024),
@@ -43,28 +44,39 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--quick", action="store_true", help="skip the persistent variants")
+    ap.add_argument("--names", default=None, help="comma-separated substrings of the shape names to run")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     out = open(a.json, "a") if a.json else None
     for name, M, N, K in SHAPES:
+        if a.names and not any(t in name for t in a.names.split(",")):
+            continue
         g = torch.Generator(device=dev).manual_seed(0)
         x = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
         w = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
         b = torch.zeros(N, device=dev)
-        def pp(stage, v1=1, bias=None):
+        def pp(stage, v1=1, bias=None, tile=1):
             C.gemm_tune("pp_stage", stage)
             C.gemm_tune("pp_v1", v1)
+            C.gemm_tune("pp_tile", tile)  # 1: 256 x 256, 2: 128 x 192 (gemm_pq.hip)
+            C.gemm_tune("pp_sk", 0)
             return C.gemm_pp(x, w, bias)
 
-        ops = {"pp": lambda: pp(1), "pp_persist": lambda: pp(1, 0), "pp_persist_regepi": lambda: pp(0, 0),
-               "blas": lambda: torch.mm(x, w.t())}
+        ops = {"pp": lambda: pp(1), "blas": lambda: torch.mm(x, w.t())}
+        if not a.quick:
+            ops["pp_persist"] = lambda: pp(1, 0)
+            ops["pp_persist_regepi"] = lambda: pp(0, 0)
+        if N % 8 == 0:
+            ops["pq"] = lambda: pp(1, tile=2)
+            ops["pq_bias"] = lambda: pp(1, 1, b, tile=2)
         if N <= 7168:
             ops["pp_bias"] = lambda: pp(1, 1, b)
         if N % 64 == 0 and K <= 4096:
             ops["ring128"] = lambda: C.linear_fwd(x, w, b, 0)
         ref = torch.mm(x, w.t())
         rel = 0.0
-        for v in (ops["pp"], ops["pp_persist"], ops["pp_persist_regepi"]):
+        for v in [f for k, f in ops.items() if k.startswith("p") and "bias" not in k]:
             y = v()[0]
             rel = max(rel, float((y.float() - ref.float()).norm() / ref.float().norm()))
         ts = {k: [] for k in ops}
