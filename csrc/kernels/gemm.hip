@@ -70,6 +70,10 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
+__device__ __forceinline__ void glds16_nt(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 2);
+}
 
 // wait until at most N vector-memory ops of this wave are outstanding
 template <int N>
@@ -226,6 +230,7 @@ struct ConvGeo {
   // EPI 4 (parity scatter): row (n, a, b) of the Ho × Wo row grid is stored at
   // pixel (n, 2a + ph, 2b + pw) of the oh × ow output
   int oh, ow, ph, pw;
+  int nt_a;  // gemm_tune "nt_a": 1 = A-operand DMA with the non-temporal policy (streamed activations)
 };
 
 // BatchNorm (training) of the tensor whose gradient a gemm_nt RED epilogue
@@ -516,9 +521,11 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
         const int r = p / CPR, lc = (p % CPR) ^ nt_swzk<BK>(r);
         int64_t gm = a_m0 + r;
         gm = gm < M ? gm : M - 1;
-        glds16(A + gm * K + lc * 8 + k0, base + (wave * NA + j) * 1024);
+        if (geo.nt_a) glds16_nt(A + gm * K + lc * 8 + k0, base + (wave * NA + j) * 1024);
+        else glds16(A + gm * K + lc * 8 + k0, base + (wave * NA + j) * 1024);
       } else {
-        glds16(asrc[j] + k0, base + (wave * NA + j) * 1024);
+        if (geo.nt_a) glds16_nt(asrc[j] + k0, base + (wave * NA + j) * 1024);
+        else glds16(asrc[j] + k0, base + (wave * NA + j) * 1024);
       }
     }
 #pragma unroll
@@ -1945,6 +1952,9 @@ int g_lin_big = 1;
 // 256 x 256 tiles on the private-staging ring with the pipelined stage loop (1)
 // instead of the C staging aliased into a ring slot (0)
 int g_big_pipe = 0;
+// A operand (the streamed activation) DMA with the non-temporal cache policy:
+// 0 default policy, 1 nt (gemm_tune "nt_a"; A/B: tools/rn_gemm_cold.py)
+int g_nt_a = 0;
 int g_reserve_cus = [] {
   const char* v = getenv("DCP_RESERVE_CUS");
   const int r = v ? atoi(v) : 0;
@@ -1958,6 +1968,7 @@ void gemm_tune(const char* key, int value) {
   if (k == "nt_big") g_nt_big = value;
   if (k == "lin_big") g_lin_big = value;
   if (k == "big_pipe") g_big_pipe = value;
+  if (k == "nt_a") g_nt_a = value != 0;
   if (k == "wg_slots") g_wg_slots = value < 64 ? 64 : value;
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
@@ -1969,6 +1980,7 @@ int gemm_tune_get(const char* key) {
   if (k == "nt_big") return g_nt_big;
   if (k == "lin_big") return g_lin_big;
   if (k == "big_pipe") return g_big_pipe;
+  if (k == "nt_a") return g_nt_a;
   if (k == "wg_slots") return g_wg_slots;
   if (k == "wg_cap") return g_wg_cap;
   if (k == "reserve_cus") return g_reserve_cus;
@@ -2161,9 +2173,11 @@ void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int
                     const BnRedArgs* red = nullptr) {
   // the BN prologue stays on BK=32: at BK=64 its per-half coefficient loads and
   // transforms no longer overlap the MFMAs (+20-40 % on the PRO GEMMs)
+  ConvGeo g = geo;
+  if (!GATHER) g.nt_a = g_nt_a;
   if (nt_bk() == 64 && scale == nullptr)
-    gemm_nt_launch_bk<GATHER, 64>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s);
-  else gemm_nt_launch_bk<GATHER, 32>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s);
+    gemm_nt_launch_bk<GATHER, 64>(A, B, C, M, N, K, scale, shift, relu, stats, g, red, s);
+  else gemm_nt_launch_bk<GATHER, 32>(A, B, C, M, N, K, scale, shift, relu, stats, g, red, s);
 }
 }  // namespace
 
