@@ -1953,7 +1953,8 @@ int g_lin_big = 1;
 // instead of the C staging aliased into a ring slot (0)
 int g_big_pipe = 0;
 // A operand (the streamed activation) DMA with the non-temporal cache policy:
-// 0 default policy, 1 nt (gemm_tune "nt_a"; A/B: tools/rn_gemm_cold.py)
+// 0 default policy, 1 nt, 2 nt past the Infinity Cache's size (gemm_tune
+// "nt_a"; A/B: tools/rn_gemm_cold.py, NOTES §28)
 int g_nt_a = 0;
 int g_reserve_cus = [] {
   const char* v = getenv("DCP_RESERVE_CUS");
@@ -1968,7 +1969,7 @@ void gemm_tune(const char* key, int value) {
   if (k == "nt_big") g_nt_big = value;
   if (k == "lin_big") g_lin_big = value;
   if (k == "big_pipe") g_big_pipe = value;
-  if (k == "nt_a") g_nt_a = value != 0;
+  if (k == "nt_a") g_nt_a = value < 0 ? 0 : (value > 2 ? 2 : value);
   if (k == "wg_slots") g_wg_slots = value < 64 ? 64 : value;
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
@@ -2174,7 +2175,11 @@ void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int
   // the BN prologue stays on BK=32: at BK=64 its per-half coefficient loads and
   // transforms no longer overlap the MFMAs (+20-40 % on the PRO GEMMs)
   ConvGeo g = geo;
-  if (!GATHER) g.nt_a = g_nt_a;
+  // nt A operand: always (1), or (2) when A + C exceed the 256 MiB Infinity
+  // Cache — the layer-1/2 shapes, whose activations are evicted by the time
+  // they are read either way
+  if (!GATHER)
+    g.nt_a = g_nt_a == 1 || (g_nt_a == 2 && (M * K + M * static_cast<int64_t>(N)) * 2 > (int64_t(256) << 20));
   if (nt_bk() == 64 && scale == nullptr)
     gemm_nt_launch_bk<GATHER, 64>(A, B, C, M, N, K, scale, shift, relu, stats, g, red, s);
   else gemm_nt_launch_bk<GATHER, 32>(A, B, C, M, N, K, scale, shift, relu, stats, g, red, s);
