@@ -380,6 +380,41 @@ __global__ void __launch_bounds__(256) ln_bwd_colsum_kernel(const float* __restr
   if (w == 0 && c < cols) out[static_cast<int64_t>(blockIdx.y) * cols + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
+// The whole dγ / dβ reduction in one launch: workgroup = 64 of the 2 D
+// partial columns, its 16 waves stride over the nblk partial rows (8 loads in
+// flight per lane), then one LDS fold and the final (accumulating) store —
+// the two-level colsum + finalize pair it replaces cost two launches and a
+// dependent boundary per LayerNorm backward (~10 µs, NOTES §28).
+__global__ void __launch_bounds__(1024) ln_bwd_reduce_kernel(const float* __restrict__ part, int nblk, int D,
+                                                             float* __restrict__ dw, float* __restrict__ db,
+                                                             int accum) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cols = 2 * D;
+  const int c = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (c < cols) {
+    int b = w;
+    for (; b + 7 * 16 < nblk; b += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = part[static_cast<int64_t>(b + i * 16) * cols + c];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[i];
+    }
+    for (; b < nblk; b += 16) s += part[static_cast<int64_t>(b) * cols + c];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    float* o = c < D ? (dw ? dw + c : nullptr) : (db ? db + (c - D) : nullptr);
+    if (o) *o = accum ? *o + t : t;
+  }
+}
+
 // accum != 0: add into dw / db (fp32 .grad under DistributedDataParallel.no_sync)
 __global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int D, float* __restrict__ dw,
                                        float* __restrict__ db, int accum) {
@@ -490,6 +525,11 @@ int ln_bwd_grid(int64_t rows, int D, int xdtype) {
   return static_cast<int>(nb);
 }
 int ln_colsum_groups(int nblk) { return nblk > 16 ? (nblk + 63) / 64 : 0; }
+// DCP_LN_TWO_LEVEL=1: the previous colsum + finalize pair (A/B switch)
+bool ln_two_level() {
+  static const bool on = std::getenv("DCP_LN_TWO_LEVEL") != nullptr;
+  return on;
+}
 }  // namespace
 
 int ln_bwd_blocks(int64_t rows, int D) {  // workspace rows: the partials + the colsum level
@@ -537,6 +577,11 @@ void ln_backward(int xdtype, int ydtype, const void* dy, const void* x, const fl
   else DK_BD(LN_F32, LN_F32);
 #undef DK_BD
   const int z = ln_colsum_groups(nblk);
+  if (z > 0 && !ln_two_level()) {
+    hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, s, part, nblk, D, dw, db,
+                       accum ? 1 : 0);
+    return;
+  }
   if (z > 0) {
     float* part2 = part + static_cast<int64_t>(nblk) * 2 * D;
     hipLaunchKernelGGL(ln_bwd_colsum_kernel, dim3((2 * D + 63) / 64, z), dim3(256), 0, s, part, nblk, 2 * D, part2);
