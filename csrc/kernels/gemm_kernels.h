@@ -67,6 +67,8 @@ void gemm_pp_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
 // K % 64 == 0, ldc % 8 == 0.
 bool gemm_pq_supported(int64_t M, int64_t N, int64_t K, int64_t ldc);
 bool gemm_pq_pick(int64_t M, int64_t N);
+void gemm_pq_tune(int ns);  // ring slots (3 or 4)
+int gemm_pq_tune_get();
 void gemm_pq_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
                   void* c2, int gelu, hipStream_t s);
 // Split-K on the same kernel for shapes whose tiles leave most CUs idle (the

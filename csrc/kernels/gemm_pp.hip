@@ -927,6 +927,7 @@ void gemm_pp_tune(const char* key, int value) {
   if (k == "pp_v1") g_pp_v1 = value != 0;
   if (k == "pp_sk") g_pp_sk = value != 0;
   if (k == "pp_tile") g_pp_tile = value < 0 ? 0 : (value > 2 ? 2 : value);
+  if (k == "pp_pq_ns") gemm_pq_tune(value);
   if (k == "pp_sk_force") g_pp_sk_force = value < 0 ? 0 : value;
 }
 int gemm_pp_tune_get(const char* key) {
@@ -936,6 +937,7 @@ int gemm_pp_tune_get(const char* key) {
   if (k == "pp_v1") return g_pp_v1;
   if (k == "pp_sk") return g_pp_sk;
   if (k == "pp_tile") return g_pp_tile;
+  if (k == "pp_pq_ns") return gemm_pq_tune_get();
   if (k == "pp_sk_force") return g_pp_sk_force;
   return -1;
 }

@@ -18,9 +18,9 @@
 // wave of each group (gemm_pp.hip's schedule):
 //   per 64-deep K-tile kt: { LDS fragment reads (8 A + 6 B, 16 B each) | DMA
 //   of K-tile kt+2 | vmcnt: K-tile kt+1 landed } barrier { 24 MFMA } barrier
-// LDS: a 3-slot ring of 40 KB K-tiles ([128 rows of A | 192 rows of B] x 64 k,
+// LDS: a 4-slot (3: gemm_tune "pp_pq_ns") ring of 40 KB K-tiles ([128 rows of A | 192 rows of B] x 64 k,
 // 128-B rows, 16-B chunk c of row r at chunk c ^ ((r >> 1) & 7)) filled by
-// global_load_lds (5 x 1 KB per wave per K-tile, issued 1.5 K-tiles ahead);
+// global_load_lds (5 x 1 KB per wave per K-tile, issued NS - 1 K-tiles ahead);
 // the epilogue stages the bf16 tile through the idle ring and stores whole
 // 384-B rows.
 //
@@ -47,11 +47,9 @@ constexpr int kBM = 128, kBN = 192;
 constexpr int kAI = kBM * 128;            // A image bytes (16 KB)
 constexpr int kBI = kBN * 128;            // B image bytes (24 KB)
 constexpr int kSlot = kAI + kBI;          // one 64-deep K-tile (40 KB)
-constexpr int kNS = 3;                    // ring slots
-constexpr int kSink = kNS * kSlot;        // 1 KB sink for the DMA of K-tiles past the end
-constexpr int kLds = kNS * kSlot + 1024;  // 123,904 B: one workgroup per CU
 constexpr int kCS = kBN * 2 + 16;         // staged C row stride (bytes; padded against bank conflicts)
-static_assert(kBM * kCS <= kNS * kSlot, "staged C must fit the idle ring");
+static_assert(kBM * kCS <= 3 * kSlot, "staged C must fit the idle ring");
+int g_pq_ns = 4;                          // gemm_tune "pp_pq_ns": ring slots, 3 or 4 (4 x 40 KB = all of the LDS)
 
 __device__ __forceinline__ int pq_swz(int r) { return (r >> 1) & 7; }
 __device__ __forceinline__ uint32_t pq_pack(float a, float b) {
@@ -81,11 +79,17 @@ __device__ __forceinline__ void pq_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
-__device__ __forceinline__ void pq_vm5() { asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); }
+// at most c K-tiles (5 DMA each) of this wave still in flight
+__device__ __forceinline__ void pq_vm(int c) {
+  if (c <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (c == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+}
 __device__ __forceinline__ void pq_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// EPI: 0 = C = A·Bᵀ; 1 = + bias; 2 / 3 = + bias, c2 = gelu(C) (tanh / erf)
-template <int EPI>
+// EPI: 0 = C = A·Bᵀ; 1 = + bias; 2 / 3 = + bias, c2 = gelu(C) (tanh / erf).
+// NS: ring slots (K-tiles NS - 1 ahead; 4 = 160 KB, the whole LDS).
+template <int EPI, int NS>
 __global__ void __launch_bounds__(kPT, 1)
     gemm_pq_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                    int64_t M, int N, int K, int64_t ldc, int tiles_n, const float* __restrict__ bias,
@@ -125,14 +129,10 @@ __global__ void __launch_bounds__(kPT, 1)
     const int gn = n0 + r < N ? n0 + r : N - 1;
     sb[q] = B + static_cast<int64_t>(gn) * K + ((lane & 7) ^ pq_swz(r)) * 8;
   }
-  // DMA of K-tile kt into ring slot `slot` (kt >= KT: five 1 KB writes into
-  // the sink, so every wave's vmcnt sequence is the same for every K-tile)
+  // DMA of K-tile kt into ring slot `slot` (none past the last K-tile: the
+  // waits below count what is really in flight)
   auto issue = [&](int kt, int slot) {
-    if (kt >= KT) {
-#pragma unroll
-      for (int q = 0; q < 5; ++q) pq_glds(sa[0], lds + kSink);
-      return;
-    }
+    if (kt >= KT) return;
     const int k0 = kt * 64;
     const char* s = lds + slot * kSlot;
     pq_glds(sa[0] + k0, s + (2 * w) * 1024);
@@ -177,34 +177,35 @@ __global__ void __launch_bounds__(kPT, 1)
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed everywhere
-  issue(0, 0);
-  issue(1, 1);
-  pq_vm5();
+  // prologue: K-tiles 0 .. NS - 2 in flight, K-tile 0 landed everywhere
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i) issue(i, i);
+  pq_vm(min(NS - 2, KT - 1));
   pq_barrier();
   if (wr == 1) pq_barrier();  // the stagger: group Y runs one barrier behind
 
-  // One phase per K-tile: { 14 fragment reads | DMA of K-tile kt + 2 into the
-  // slot K-tile kt - 1 used } barrier { 24 MFMA } barrier. K-tile kt + 1 must
-  // have landed for every wave before the barrier after which group X reads
-  // it — X's second barrier of this K-tile, Y's first — so X waits behind its
-  // MFMAs and Y before them (the same global barrier; 3-4 MFMA segments after
-  // the DMA was issued).
+  // One phase per K-tile: { 14 fragment reads | DMA of K-tile kt + NS - 1
+  // into the slot K-tile kt - 1 used } barrier { 24 MFMA } barrier. K-tile kt
+  // + 1 must have landed for every wave before the barrier after which group X
+  // reads it — X's second barrier of this K-tile, Y's first — so X waits
+  // behind its MFMAs and Y before them (the same global barrier). Allowed in
+  // flight then: the K-tiles issued after kt + 1 (NS - 2, fewer at the end).
   int slot = 0;
   for (int kt = 0; kt < KT; ++kt) {
     const char* s = lds + slot * kSlot;
     read(s);
-    issue(kt + 2, slot == 0 ? 2 : slot - 1);
-    if (wr == 1) pq_vm5();
+    issue(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
+    const int c = min(NS - 2, KT - 2 - kt);
+    if (wr == 1) pq_vm(c);
     pq_lgkm0();
     pq_barrier();
     mfma();
-    if (wr == 0) pq_vm5();
+    if (wr == 0) pq_vm(c);
     pq_barrier();
-    slot = slot == 2 ? 0 : slot + 1;
+    slot = slot == NS - 1 ? 0 : slot + 1;
   }
   if (wr == 0) pq_barrier();  // both groups at the same barrier count; every ring read done
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (only sink DMA can be outstanding)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // epilogue: stage the bf16 tile (+ bias, rounded once) in the idle ring,
   // then whole 384-B rows: thread -> 16-B chunk (row, chunk) of the tile
@@ -247,22 +248,32 @@ __global__ void __launch_bounds__(kPT, 1)
   }
 }
 
-template <int EPI>
-void gemm_pq_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
-                    void* c2, hipStream_t s) {
+template <int EPI, int NS>
+void gemm_pq_go(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
+                void* c2, hipStream_t s) {
+  constexpr int lds = NS * kSlot;
   static const bool attr = [] {  // > 64 KB of dynamic LDS
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_pq_kernel<EPI>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_pq_kernel<EPI, NS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     return true;
   }();
   (void)attr;
   const int tiles_n = (N + kBN - 1) / kBN;
   const int64_t tiles = (M + kBM - 1) / kBM * tiles_n;
-  hipLaunchKernelGGL((gemm_pq_kernel<EPI>), dim3(static_cast<unsigned>(tiles)), dim3(kPT), kLds, s,
+  hipLaunchKernelGGL((gemm_pq_kernel<EPI, NS>), dim3(static_cast<unsigned>(tiles)), dim3(kPT), lds, s,
                      static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N,
                      K, ldc, tiles_n, bias, static_cast<uint16_t*>(c2));
 }
+template <int EPI>
+void gemm_pq_launch(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, const float* bias,
+                    void* c2, hipStream_t s) {
+  if (g_pq_ns == 3) gemm_pq_go<EPI, 3>(A, B, C, M, N, K, ldc, bias, c2, s);
+  else gemm_pq_go<EPI, 4>(A, B, C, M, N, K, ldc, bias, c2, s);
+}
 }  // namespace
+
+void gemm_pq_tune(int ns) { g_pq_ns = ns == 3 ? 3 : 4; }
+int gemm_pq_tune_get() { return g_pq_ns; }
 
 bool gemm_pq_supported(int64_t M, int64_t N, int64_t K, int64_t ldc) {
   return M >= 1 && N >= 8 && N % 8 == 0 && K >= 64 && K % 64 == 0 && ldc % 8 == 0 && M * K < (int64_t(1) << 31) &&

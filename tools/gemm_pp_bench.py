@@ -56,7 +56,8 @@ def main():
         x = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
         w = ((torch.rand(N, K, device=dev, generator=g) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
         b = torch.zeros(N, device=dev)
-        def pp(stage, v1=1, bias=None, tile=1):
+        def pp(stage, v1=1, bias=None, tile=1, ns=4):
+            C.gemm_tune("pp_pq_ns", ns)
             C.gemm_tune("pp_stage", stage)
             C.gemm_tune("pp_v1", v1)
             C.gemm_tune("pp_tile", tile)  # 1: 256 x 256, 2: 128 x 192 (gemm_pq.hip)
@@ -69,6 +70,7 @@ def main():
             ops["pp_persist_regepi"] = lambda: pp(0, 0)
         if N % 8 == 0:
             ops["pq"] = lambda: pp(1, tile=2)
+            ops["pq3"] = lambda: pp(1, tile=2, ns=3)
             ops["pq_bias"] = lambda: pp(1, 1, b, tile=2)
         if N <= 7168:
             ops["pp_bias"] = lambda: pp(1, 1, b)
