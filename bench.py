@@ -286,7 +286,9 @@ def main():
                 kw["tail_bucket_mb"] = a.tail_bucket_mb
             if a.comm_dtype == "bf16":
                 kw["comm_dtype"] = torch.bfloat16
-            ov = a.overlap_optimizer if a.overlap_optimizer >= 0 else int(a.model in ("gpt2", "bert"))
+            # optimizer / all-reduce overlap: only with collectives to overlap
+            # (one rank: the chunked step is pure host overhead, NOTES §28)
+            ov = a.overlap_optimizer if a.overlap_optimizer >= 0 else int(a.model in ("gpt2", "bert") and world > 1)
             if ov and a.grad_as_view:
                 kw["overlap_optimizer"] = True
             if (a.defer_wgrad if a.defer_wgrad >= 0 else int(wl.accum > 1)):
@@ -322,13 +324,24 @@ def main():
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
+        prof = None
+        if os.environ.get("DCP_BENCH_CPROFILE"):  # host-side profile of the timed steps only (diagnostics)
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         for i in range(a.steps):
             loss = step()
+        t_host = time.perf_counter() - t0  # host time to enqueue the steps (the GPU may still be running)
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         elapsed = max_over_ranks(time.perf_counter() - t0)
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(os.environ["DCP_BENCH_CPROFILE"])
+            log(f"[bench] host enqueue time {t_host / a.steps * 1e3:.2f} ms/step vs {elapsed / a.steps * 1e3:.2f} ms/step")
         ms = elapsed / a.steps * 1000.0
         samples_per_step = wl.per_gpu_batch * wl.accum * world
         total = samples_per_step * a.steps / elapsed

@@ -970,6 +970,35 @@ at::Tensor colsum(const at::Tensor& x, const c10::optional<at::Tensor>& accumula
   return out;
 }
 
+// Σ over the rows of up to 4 bf16 [M_i, N] segments (a bias gradient over the
+// deferred micro-steps) in one launch; same contract as colsum.
+at::Tensor colsum_multi(const std::vector<at::Tensor>& xs, const c10::optional<at::Tensor>& accumulate_into) {
+  DK_CHECK(!xs.empty() && xs.size() <= 4, "colsum_multi: 1-4 segments");
+  const int64_t N = xs[0].size(-1);
+  kern::ColSegs sg{};
+  for (size_t i = 0; i < xs.size(); ++i) {
+    const at::Tensor& x = xs[i];
+    DK_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.size(-1) == N &&
+                 x.device() == xs[0].device(),
+             "colsum_multi: contiguous bf16 segments of one width on one device");
+    sg.x[i] = x.data_ptr();
+    sg.M[i] = x.numel() / N;
+  }
+  sg.n = static_cast<int>(xs.size());
+  DK_CHECK(N % 8 == 0, "colsum_multi: last dim must be a multiple of 8");
+  c10::hip::HIPGuard guard(xs[0].device().index());
+  auto s = stream_of(xs[0]);
+  const bool acc = accumulate_into.has_value() && accumulate_into->defined();
+  if (acc)
+    DK_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
+                 accumulate_into->numel() == N && accumulate_into->device() == xs[0].device(),
+             "colsum_multi: accumulate_into must be a contiguous fp32 [N] tensor on the same device");
+  at::Tensor out = acc ? *accumulate_into : at::empty({N}, xs[0].options().dtype(at::kFloat));
+  if (!acc) out.zero_();
+  kern::colsum_multi_bf16(sg, out.data_ptr<float>(), static_cast<int>(N), s);
+  return out;
+}
+
 // --------------------------------------------------------------- GELU ---
 namespace {
 void check_gelu_operand(const at::Tensor& t, const char* what) {
@@ -1692,6 +1721,8 @@ void bind(pybind11::module& m) {
   m.def("embedding_small_bwd", &embedding_small_bwd, "gw += per-index row sums (embedding tables of <= 8 rows)",
         pybind11::arg("idx"), pybind11::arg("g"), pybind11::arg("gw"));
   m.def("colsum", &colsum, "fp32 column sums of a bf16 [.., N] tensor (bias gradient)", pybind11::arg("x"),
+        pybind11::arg("accumulate_into") = pybind11::none());
+  m.def("colsum_multi", &colsum_multi, "colsum over 1-4 bf16 row segments in one launch", pybind11::arg("xs"),
         pybind11::arg("accumulate_into") = pybind11::none());
   m.def("gelu_fwd", &gelu_fwd, "bf16 GELU forward (erf or tanh form)", pybind11::arg("h"),
         pybind11::arg("tanh_approx"));

@@ -1425,8 +1425,12 @@ __global__ void __launch_bounds__(kT) weight_prep_kernel(const WPrepDesc* __rest
 // stage 1 writes one fp32 partial row per (column chunk, row slab) block,
 // stage 2 = slab_partial_kernel over the slabs. Deterministic, no atomics.
 constexpr int kColSlabs = 64;
-__global__ void __launch_bounds__(kT) colsum_partial_kernel(const uint16_t* __restrict__ x, float* __restrict__ part,
-                                                            int64_t M, int N, int64_t rows_per_slab) {
+__global__ void __launch_bounds__(kT) colsum_partial_kernel(ColSegs sg, float* __restrict__ part, int N,
+                                                            int64_t rows_per_slab) {
+  // row segment blockIdx.z (the micro-steps of a deferred bias gradient)
+  const uint16_t* __restrict__ x = static_cast<const uint16_t*>(sg.x[blockIdx.z]);
+  const int64_t M = sg.M[blockIdx.z];
+  if (static_cast<int64_t>(blockIdx.y) * rows_per_slab >= M) return;  // (uniform) past this segment's rows
   __shared__ float red[8][32 * 8];
   const int cv = threadIdx.x & 31, rg = threadIdx.x >> 5;  // 32 column vectors × 8 row groups
   const int c0 = (blockIdx.x * 32 + cv) * 8;
@@ -2546,12 +2550,22 @@ void weight_cast_t(const float* w, void* wb, void* wt, int R, int Cc, hipStream_
                      static_cast<uint16_t*>(wt), R, Cc, taps);
 }
 
-void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s) {
+void colsum_multi_bf16(const ColSegs& sg, float* out, int N, hipStream_t s) {
+  int64_t M = 0;
+  for (int i = 0; i < sg.n; ++i) M = sg.M[i] > M ? sg.M[i] : M;
   int64_t slabs = (M + 255) / 256;  // ≥ 32 rows per row group
   if (slabs > kColSlabs) slabs = kColSlabs;
   const int64_t rps = (M + slabs - 1) / slabs;
-  const dim3 g1((N + 255) / 256, static_cast<unsigned>(slabs));
-  hipLaunchKernelGGL(colsum_partial_kernel, g1, dim3(kT), 0, s, static_cast<const uint16_t*>(x), out, M, N, rps);
+  const dim3 g1((N + 255) / 256, static_cast<unsigned>(slabs), static_cast<unsigned>(sg.n));
+  hipLaunchKernelGGL(colsum_partial_kernel, g1, dim3(kT), 0, s, sg, out, N, rps);
+}
+
+void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s) {
+  ColSegs sg{};
+  sg.x[0] = x;
+  sg.M[0] = M;
+  sg.n = 1;
+  colsum_multi_bf16(sg, out, N, s);
 }
 
 namespace {

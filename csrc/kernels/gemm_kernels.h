@@ -107,6 +107,13 @@ void weight_prep(const void* table, int n, int64_t tiles, hipStream_t s);
 // one launch, ≤ 64 row slabs × N/256 column chunks, one fp32 atomic per column
 // per block.
 void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s);
+// the same over up to 4 row segments (x[i] [M[i], N]) in one launch
+struct ColSegs {
+  const void* x[4];
+  int64_t M[4];
+  int n;
+};
+void colsum_multi_bf16(const ColSegs& sg, float* out, int N, hipStream_t s);
 
 // Weight gradient on the 8-wave ping-pong schedule (wgrad_pp.hip): 256 x 256
 // output tiles. The first `full` tiles (whole 256-row bands of D) are computed

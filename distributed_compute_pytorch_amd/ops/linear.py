@@ -272,6 +272,7 @@ def _acc_target(ctx, p, shape):
 # stock and fused optimizers alike) calls it first.
 _DEFER = [0]
 _PENDING: dict = {}  # id(first parameter of the group) -> _Pending
+_PENDING_B: dict = {}  # id(bias) -> (bias, [dY segments]): bias gradients deferred the same way
 _HOOKED = [False]
 
 
@@ -302,8 +303,8 @@ def deferring() -> bool:
 
 
 def pending_weight_grads() -> int:
-    """Parameter groups whose gradient has deferred micro-step contributions."""
-    return len(_PENDING)
+    """Parameters (groups) whose gradient has deferred micro-step contributions."""
+    return len(_PENDING) + len(_PENDING_B)
 
 
 def _install_flush_hook():
@@ -324,9 +325,27 @@ def _wgrad_sum(segs, tgt):
     return dw
 
 
+def _colsum_sum(segs, tgt):
+    """Σ of the rows of the dY segments, ≤ 4 per launch, into ``tgt`` when given."""
+    db = tgt
+    for i in range(0, len(segs), 4):
+        db = _C.colsum_multi(segs[i:i + 4], accumulate_into=db)
+    return db
+
+
 def flush_weight_grads() -> None:
-    """Add every deferred micro-step weight gradient into its parameters'
-    ``.grad`` (creating it where None). Called by every optimizer step."""
+    """Add every deferred micro-step weight / bias gradient into its
+    parameters' ``.grad`` (creating it where None). Called by every optimizer
+    step."""
+    while _PENDING_B:
+        _, (b, segs) = _PENDING_B.popitem()
+        db = _colsum_sum(segs, None)
+        with torch.no_grad():
+            db = db.view(b.shape).to(b.dtype)
+            if b.grad is None:
+                b.grad = db
+            else:
+                b.grad.add_(db)
     while _PENDING:
         _, e = _PENDING.popitem()
         dw = _wgrad_sum(e.segs, None)
@@ -343,6 +362,29 @@ def flush_weight_grads() -> None:
 def discard_weight_grads() -> None:
     """Drop the deferred contributions (``zero_grad`` of this package's optimizers)."""
     _PENDING.clear()
+    _PENDING_B.clear()
+
+
+def _deferred_bias(ctx, bias, g2):
+    """(handled, db) — the bias-gradient twin of _deferred_wgrad: under no_sync
+    deferral keep dY (already kept for the weight gradient) instead of a
+    column-sum launch per micro-step; the synchronising micro-step sums the
+    rows of all of them in one launch (``_C.colsum_multi``)."""
+    if (bias is None or not bias.is_leaf or not g2.is_cuda or g2.shape[0] == 0 or g2.shape[1] % 8 != 0
+            or not g2.is_contiguous()):
+        return False, None
+    key = id(bias)
+    if getattr(ctx, "defer", False):
+        if not _engine_accumulates(bias):
+            return False, None
+        _PENDING_B.setdefault(key, (bias, []))[1].append(g2)
+        return True, None
+    e = _PENDING_B.pop(key, None)
+    if e is None:
+        return False, None
+    tgt = _acc_target(ctx, bias, torch.Size((g2.shape[1],)))
+    db = _colsum_sum(e[1] + [g2], tgt)
+    return True, (None if tgt is not None else db)
 
 
 def _deferred_wgrad(ctx, g2, x2):
@@ -515,8 +557,11 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
         if dw is not None and dw.dtype != ctx.wdtype:
             dw = dw.to(ctx.wdtype)
     if not db_done and ctx.bdtype is not None and ctx.needs_input_grad[2]:
-        tgt = _acc_target(ctx, bias, torch.Size((g2.shape[1],)))
-        if g2.shape[0] == 0:  # empty batch: a zero bias gradient (no column-sum launch)
+        done_b, db = _deferred_bias(ctx, bias, g2)
+        tgt = None if done_b else _acc_target(ctx, bias, torch.Size((g2.shape[1],)))
+        if done_b:
+            pass
+        elif g2.shape[0] == 0:  # empty batch: a zero bias gradient (no column-sum launch)
             db = torch.zeros(g2.shape[1], device=g2.device, dtype=torch.float32)
         else:
             db = _C.colsum(g2, accumulate_into=tgt)

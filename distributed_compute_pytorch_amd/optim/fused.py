@@ -17,6 +17,8 @@ from __future__ import annotations
 from collections import defaultdict
 from typing import Iterable, List, Optional
 
+import os
+
 import torch
 from torch.optim import Optimizer
 from torch.utils.weak import WeakIdKeyDictionary
@@ -250,10 +252,20 @@ class Adam(Optimizer):
 
     def _step(self, ids, grad_scale):
         """Update the parameters whose id is in ``ids`` (None: all); returns the
-        parameters whose bf16 shadow the kernel rewrote."""
+        parameters whose bf16 shadow the kernel rewrote.
+
+        Host cost: the per-parameter work (state lookup and migration, bucket
+        grouping, argument lists) is done once per chunk and cached as a plan,
+        revalidated each step from the gradients' addresses / layouts and the
+        bf16 shadows (`_adam_sig`); the host-side step counters of a plan are
+        0-dim views of one flat CPU tensor, advanced by a single add. Before,
+        the per-parameter loop and counter updates were ~1.5 ms of host time
+        per BERT step, spent while the GPU idled between the backward's last
+        kernel and the first update (NOTES §28)."""
         capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         shadowed = []
-        for group in self.param_groups:
+        plans = self.__dict__.setdefault("_dcp_plans", {})
+        for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             ams = group["amsgrad"]
             cap_mode = group.get("capturable", False)
@@ -262,60 +274,152 @@ class Adam(Optimizer):
                                    "bias corrections would be frozen at their capture-time step. Construct the "
                                    "optimizer with capturable=True (or set group['capturable'] = True before the "
                                    "eager warmup steps).")
-            buckets = defaultdict(lambda: ([], [], [], [], [], [], []))
-            entries, cpu_steps = [], []
-            for p in _chunk_params(self, group, ids):
-                if not _grads_ok(p):
-                    continue
-                st = self.state[p]
-                dev_step = cap_mode and p.is_cuda
-                if len(st) == 0:
-                    st["step"] = (torch.zeros((), dtype=torch.float32, device=p.device) if dev_step
-                                  else torch.tensor(0.0, dtype=torch.float32))
-                    st["exp_avg"] = _state_like(p)
-                    st["exp_avg_sq"] = _state_like(p)
-                    if ams:
-                        st["max_exp_avg_sq"] = _state_like(p)
-                elif dev_step and not st["step"].is_cuda:
-                    if capturing:
-                        raise RuntimeError("capturable Adam: run one eager step before capture (moves 'step' "
-                                           "to the device)")
-                    st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
-                elif not dev_step and st["step"].is_cuda:
-                    st["step"] = st["step"].cpu()
-                entries.append((p, st, dev_step))
-                if not dev_step:
-                    cpu_steps.append(st["step"])
-            # every host-side step counter advanced by ONE foreach call (a
-            # per-parameter `+= 1` on a 0-dim CPU tensor cost a dispatcher
-            # round trip each: ~0.6 ms of host time per GPT-2 step)
-            if cpu_steps:
-                torch._foreach_add_(cpu_steps, 1.0)
-            for p, st, dev_step in entries:
-                sh = _BF16_SHADOWS.get(p) if p.is_cuda else None
-                if dev_step:
-                    key = (p.device, p.dtype, None, sh is not None)
+            plist = _chunk_params(self, group, ids)
+            grads, sig = _adam_sig(plist)
+            pkey = (gi, id(group), None if ids is None else tuple(id(p) for p in plist), cap_mode, ams)
+            plan = plans.get(pkey)
+            if plan is None or plan.sig != sig or plan.state is not self.state or capturing or _NO_PLAN:
+                plan = self._adam_plan(plist, grads, cap_mode, ams, capturing)
+                plan.sig = sig
+                if plan.cacheable and not capturing:
+                    plans[pkey] = plan
                 else:
-                    key = (p.device, p.dtype, float(st["step"]), sh is not None)
-                P, G, M, V, VM, S, ST = buckets[key]
-                P.append(p)
-                G.append(_dense_like(_grad(p), p))
-                M.append(st["exp_avg"])
-                V.append(st["exp_avg_sq"])
-                if ams:
-                    VM.append(st["max_exp_avg_sq"])
-                if sh is not None:
-                    S.append(sh[0])
-                    shadowed.append(p)
-                if dev_step:
-                    ST.append(st["step"].view(1))
-            for (dev, dt, step, _), (P, G, M, V, VM, S, ST) in buckets.items():
-                if ST:
-                    torch._foreach_add_(ST, 1.0)  # one launch; the kernel reads the advanced steps
-                _C.fused_adam(P, G, M, V, VM, group["lr"], b1, b2, group["eps"], group["weight_decay"],
-                              step if step is not None else 0.0, ams, group["decoupled_weight_decay"],
-                              group["maximize"], grad_scale, S, ST)
+                    plans.pop(pkey, None)
+            vals = None
+            if plan.flat is not None:
+                plan.flat.add_(1.0)  # every host-side step counter of the plan, one op
+                vals = plan.flat.tolist()
+            for bk in plan.buckets:
+                if bk.st:
+                    torch._foreach_add_(bk.st, 1.0)  # one launch; the kernel reads the advanced steps
+                    step = 0.0
+                else:
+                    step = vals[bk.steps[0]]
+                    if any(vals[i] != step for i in bk.steps):  # a counter edited by hand: regroup next step
+                        plans.pop(pkey, None)
+                        for i in bk.steps:
+                            self._adam_one(plist, grads, i, vals[i], group, b1, b2, ams, grad_scale)
+                        shadowed.extend(bk.shadowed)
+                        continue
+                g = [grads[i] for i in bk.idx]
+                _C.fused_adam(bk.p, g, bk.m, bk.v, bk.vm, group["lr"], b1, b2, group["eps"], group["weight_decay"],
+                              step, ams, group["decoupled_weight_decay"], group["maximize"], grad_scale, bk.s, bk.st)
+                shadowed.extend(bk.shadowed)
         return shadowed
+
+    def _adam_one(self, plist, grads, i, step, group, b1, b2, ams, grad_scale):
+        p = plist[i]
+        st = self.state[p]
+        sh = _BF16_SHADOWS.get(p) if p.is_cuda else None
+        _C.fused_adam([p], [grads[i]], [st["exp_avg"]], [st["exp_avg_sq"]],
+                      [st["max_exp_avg_sq"]] if ams else [], group["lr"], b1, b2, group["eps"], group["weight_decay"],
+                      step, ams, group["decoupled_weight_decay"], group["maximize"], grad_scale,
+                      [sh[0]] if sh is not None else [], [])
+
+    def _adam_plan(self, plist, grads, cap_mode, ams, capturing):
+        """State creation / migration and the launch grouping of one chunk."""
+        plan = _AdamPlan()
+        plan.state = self.state
+        entries, cpu = [], []
+        for i, p in enumerate(plist):
+            if grads[i] is None:
+                continue
+            st = self.state[p]
+            dev_step = cap_mode and p.is_cuda
+            if len(st) == 0:
+                st["step"] = (torch.zeros((), dtype=torch.float32, device=p.device) if dev_step
+                              else torch.tensor(0.0, dtype=torch.float32))
+                st["exp_avg"] = _state_like(p)
+                st["exp_avg_sq"] = _state_like(p)
+                if ams:
+                    st["max_exp_avg_sq"] = _state_like(p)
+            elif dev_step and not st["step"].is_cuda:
+                if capturing:
+                    raise RuntimeError("capturable Adam: run one eager step before capture (moves 'step' "
+                                       "to the device)")
+                st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+            elif not dev_step and st["step"].is_cuda:
+                st["step"] = st["step"].cpu()
+            dense = _dense_like(grads[i], p)
+            if dense is not grads[i]:  # a layout copy: valid for this step only
+                grads[i] = dense
+                plan.cacheable = False
+            entries.append((i, p, st, dev_step))
+            if not dev_step:
+                cpu.append(st)
+        if cpu:
+            # the counters as 0-dim views of one flat tensor (values kept; a
+            # checkpoint still holds one 'step' tensor per parameter)
+            plan.flat = torch.tensor([float(st["step"]) for st in cpu], dtype=torch.float32)
+            for j, st in enumerate(cpu):
+                st["step"] = plan.flat[j]
+        vals = plan.flat.tolist() if cpu else []
+        buckets = {}
+        j = 0
+        for i, p, st, dev_step in entries:
+            sh = _BF16_SHADOWS.get(p) if p.is_cuda else None
+            if dev_step:
+                key = (p.device, p.dtype, None, sh is not None)
+            else:
+                key = (p.device, p.dtype, vals[j], sh is not None)
+            bk = buckets.get(key)
+            if bk is None:
+                bk = buckets[key] = _AdamBucket()
+            bk.idx.append(i)
+            bk.p.append(p)
+            bk.m.append(st["exp_avg"])
+            bk.v.append(st["exp_avg_sq"])
+            if ams:
+                bk.vm.append(st["max_exp_avg_sq"])
+            if sh is not None:
+                bk.s.append(sh[0])
+                bk.shadowed.append(p)
+            if dev_step:
+                bk.st.append(st["step"].view(1))
+            else:
+                bk.steps.append(j)
+                j += 1
+        plan.buckets = list(buckets.values())
+        return plan
+
+
+_NO_PLAN = os.environ.get("DCP_ADAM_NO_PLAN") == "1"  # A/B switch: rebuild the plan every step
+
+
+class _AdamBucket:
+    __slots__ = ("idx", "p", "m", "v", "vm", "s", "st", "steps", "shadowed")
+
+    def __init__(self):
+        self.idx, self.p, self.m, self.v, self.vm, self.s, self.st, self.steps, self.shadowed = (
+            [], [], [], [], [], [], [], [], [])
+
+
+class _AdamPlan:
+    __slots__ = ("sig", "state", "flat", "buckets", "cacheable")
+
+    def __init__(self):
+        self.sig, self.state, self.flat, self.buckets, self.cacheable = None, None, None, [], True
+
+
+def _adam_sig(plist):
+    """(grads, signature): each parameter's gradient (the plain bucket view for
+    an overlap-mode pending gradient) and what a cached plan depends on — the
+    gradient's address and layout and the bf16 shadow it updates."""
+    grads, sig = [], []
+    for p in plist:
+        g = p.grad
+        if g is None:
+            grads.append(None)
+            sig.append(None)
+            continue
+        if type(g).__name__ == "_PendingGrad":
+            g = g.__dict__["_dcp_plain"]
+        if g.is_sparse:
+            raise RuntimeError("fused optimizers do not support sparse gradients")
+        sh = _BF16_SHADOWS.get(p)
+        grads.append(g)
+        sig.append((g.data_ptr(), g.stride(), id(sh[0]) if sh is not None else 0))
+    return grads, tuple(sig)
 
 
 class AdamW(Adam):
