@@ -1000,7 +1000,9 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
 // (rows 8g+4h+{0..3}, g = 0,1) land on 8 distinct 32-B bank slots.
 template <int W>
 __device__ __forceinline__ int tr_f(int r) {
-  if (W == 128) return (r & 3) | (((r >> 3) & 1) << 2);  // 256-B rows, 8 pairs
+  // 256-B rows (8 pairs) and 512-B rows (16 pairs): both row strides are
+  // 0 mod 256 B, so the same 3-bit XOR spreads the 8 rows over the banks
+  if (W >= 128) return (r & 3) | (((r >> 3) & 1) << 2);
   return ((r >> 1) & 1) | (((r >> 3) & 1) << 1);         // 128-B rows (W = 64), 4 pairs
 }
 
@@ -1960,6 +1962,9 @@ int g_big_pipe = 0;
 // 0 default policy, 1 nt, 2 nt past the Infinity Cache's size (gemm_tune
 // "nt_a"; A/B: tools/rn_gemm_cold.py, NOTES §28)
 int g_nt_a = 0;
+// stem weight gradient on one 64 x 256 tile per workgroup (dY streamed once)
+// instead of two 64 x 128 tiles (gemm_tune "stem_wide")
+int g_stem_wide = 1;
 int g_reserve_cus = [] {
   const char* v = getenv("DCP_RESERVE_CUS");
   const int r = v ? atoi(v) : 0;
@@ -1974,6 +1979,7 @@ void gemm_tune(const char* key, int value) {
   if (k == "lin_big") g_lin_big = value;
   if (k == "big_pipe") g_big_pipe = value;
   if (k == "nt_a") g_nt_a = value < 0 ? 0 : (value > 2 ? 2 : value);
+  if (k == "stem_wide") g_stem_wide = value;
   if (k == "wg_slots") g_wg_slots = value < 64 ? 64 : value;
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
@@ -1986,6 +1992,7 @@ int gemm_tune_get(const char* key) {
   if (k == "lin_big") return g_lin_big;
   if (k == "big_pipe") return g_big_pipe;
   if (k == "nt_a") return g_nt_a;
+  if (k == "stem_wide") return g_stem_wide;
   if (k == "wg_slots") return g_wg_slots;
   if (k == "wg_cap") return g_wg_cap;
   if (k == "reserve_cus") return g_reserve_cus;
@@ -2571,6 +2578,20 @@ void colsum_bf16(const void* x, float* out, int64_t M, int N, hipStream_t s) {
 namespace {
 // the plan a launch uses: multi-tap runs over taps * N2 columns rounded up to
 // the 128-wide tile, as one "tap"
+// the stem's one-tile plan: one slab per workgroup slot (2 per CU)
+WgradPlan stem_wide_plan(int64_t M) {
+  WgradPlan p;
+  p.bm = 64;
+  p.bn = 256;
+  p.tiles = 1;
+  const int64_t ksteps = (M + 63) / 64;
+  int64_t S = g_wg_slots < ksteps ? g_wg_slots : ksteps;
+  if (S < 1) S = 1;
+  p.chunk = ((ksteps + S - 1) / S) * 64;
+  p.S = static_cast<int>((M + p.chunk - 1) / p.chunk);
+  return p;
+}
+
 WgradPlan wgrad_plan_for(int64_t M, int N1, int N2, int taps) {
   if (wgrad_mtap(N2, taps)) return wgrad_plan(M, N1, (taps * N2 + 127) / 128 * 128, 1);
   return wgrad_plan(M, N1, N2, taps);
@@ -2723,17 +2744,37 @@ void gemm_wgrad_multi_bf16(const WgradPPSegs& sg, float* D, int N1, int N2, floa
   wgrad_pp_run(sg, D, ws, N1, N2, 1, p, nullptr, zero, accumulate, rows_out, s);
 }
 
+int64_t stem_wgrad_workspace(int64_t M, int Cout) {
+  int64_t need = gemm_wgrad_workspace(M, Cout, kStemWgradCols, 1);
+  if (Cout == 64) {
+    const int S = stem_wide_plan(M).S;
+    const int64_t g = (S + kSlabGroup - 1) / kSlabGroup;
+    const int64_t need2 = (S + (g > 1 ? g : 0)) * int64_t(Cout) * kStemWgradCols;
+    if (need2 > need) need = need2;
+  }
+  return need;
+}
+
 void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int W, int Cout, float* ws,
                      hipStream_t s) {
   // D [Cout][256] fp32 = Σ_m dy[m][co] · field[m][k]; M = output pixels
   const ConvGeo geo{H + 6, W + 8, H / 2, W / 2, 2, 0, 1, nullptr, 4};
   const int64_t M = static_cast<int64_t>(N) * (H / 2) * (W / 2);
-  const WgradPlan p = wgrad_plan(M, Cout, kStemWgradCols, 1);
-  const dim3 grid(p.tiles * p.S);
   const int order = wgrad_order();
-  const int tj = kStemWgradCols / p.bn;
   auto a = static_cast<const uint16_t*>(dy);
   auto b = static_cast<const uint16_t*>(xp);
+  if (g_stem_wide && Cout == 64) {
+    // one 64 x 256 tile: each dY row is staged once, not once per 128-column
+    // half (the gathered field rows dominate the LDS fill either way)
+    const WgradPlan p = stem_wide_plan(M);
+    hipLaunchKernelGGL((gemm_wgrad_kernel<64, 256, false, true, 64, 0, 1>), dim3(p.S), dim3(kT), 0, s, a, b, ws, M,
+                       Cout, kStemWgradCols, p.chunk, nullptr, nullptr, 0, 1, geo, 1, 1, order, kStemWgradCols);
+    slab_reduce(ws, D, static_cast<int64_t>(Cout) * kStemWgradCols / 4, p.S, s, false);
+    return;
+  }
+  const WgradPlan p = wgrad_plan(M, Cout, kStemWgradCols, 1);
+  const dim3 grid(p.tiles * p.S);
+  const int tj = kStemWgradCols / p.bn;
   if (p.bm == 128)
     hipLaunchKernelGGL((gemm_wgrad_kernel<128, 128, false, true, 64, 0, 1>), grid, dim3(kT), 0, s, a, b, ws, M, Cout,
                        kStemWgradCols, p.chunk, nullptr, nullptr, 0, tj, geo, p.tiles, 1, order, kStemWgradCols);

@@ -33,10 +33,11 @@ void stem_conv_fwd(const void* xp, const void* wm, void* y, int N, int H, int W,
                    hipStream_t s);
 // Weight gradient of the stem conv: D [Cout][kStemWgradCols] fp32 =
 // Σ_pixels dy[pixel][co] · Xp receptive field (k = dy*32 + dx*4 + c, the
-// forward's K order padded to 8 tap rows). ws: gemm_wgrad_workspace(
-// N*(H/2)*(W/2), Cout, kStemWgradCols, 1) floats. Same split-M MFMA kernel as
-// the conv weight gradients (gemm.hip), deterministic.
+// forward's K order padded to 8 tap rows). ws: stem_wgrad_workspace(
+// N*(H/2)*(W/2), Cout) floats. Same split-M MFMA kernel as the conv weight
+// gradients (gemm.hip; one 64 x 256 tile per slab at Cout = 64), deterministic.
 constexpr int kStemWgradCols = 256;
+int64_t stem_wgrad_workspace(int64_t M, int Cout);  // fp32 elements of ws
 void stem_conv_wgrad(const void* dy, const void* xp, float* D, int N, int H, int W, int Cout, float* ws,
                      hipStream_t s);
 

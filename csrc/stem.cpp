@@ -94,7 +94,7 @@ at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& xp, int64_t H, int
   c10::hip::HIPGuard g(dy.device().index());
   const int64_t M = N * (H / 2) * (W / 2);
   auto fo = dy.options().dtype(at::kFloat);
-  at::Tensor ws = at::empty({kern::gemm_wgrad_workspace(M, static_cast<int>(Cout), kern::kStemWgradCols, 1)}, fo);
+  at::Tensor ws = at::empty({kern::stem_wgrad_workspace(M, static_cast<int>(Cout))}, fo);
   at::Tensor D = at::empty({Cout, kern::kStemWgradCols}, fo);
   kern::stem_conv_wgrad(dy.data_ptr(), xp.data_ptr(), D.data_ptr<float>(), static_cast<int>(N), static_cast<int>(H),
                         static_cast<int>(W), static_cast<int>(Cout), ws.data_ptr<float>(), stream_of(dy));

@@ -119,3 +119,31 @@ def test_resnet_uses_fused_stem_and_tracks_module_path(cuda, monkeypatch):
             losses.append(float(F.cross_entropy(m(x), y)))
     assert calls["n"] == 1
     assert abs(losses[0] - losses[1]) < 0.03 * max(1.0, abs(losses[1])), losses
+
+
+@pytest.mark.parametrize("wide", [1, 0])
+@pytest.mark.parametrize("shape", [(4, 64, 64), (3, 48, 80), (16, 224, 224)])
+def test_stem_conv_wgrad_matches_fp64(cuda, shape, wide):
+    """The stem weight-gradient GEMM alone (one 64 x 256 tile per slab, or the
+    two 64 x 128 tiles with wide = 0) against an fp64 conv2d weight gradient of
+    the same bf16 image and output gradient."""
+    from distributed_compute_pytorch_amd._ext import C
+
+    N, H, W = shape
+    torch.manual_seed(1)
+    x = torch.randn(N, 3, H, W, device=cuda).to(torch.bfloat16)
+    dy = torch.randn(N, 64, H // 2, W // 2, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    old = C.gemm_tune_get("stem_wide")
+    try:
+        C.gemm_tune("stem_wide", wide)
+        xp, _ = C.stem_prep(x, False)
+        dw = C.stem_conv_wgrad(dy, xp, H, W)
+        torch.cuda.synchronize()
+    finally:
+        C.gemm_tune("stem_wide", old)
+    ref = torch.nn.grad.conv2d_weight(x.double().cpu(), (64, 3, 7, 7), dy.double().cpu(), stride=2, padding=3)
+    err = (dw.double().cpu() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert dw.dtype == torch.float32 and dw.shape == (64, 3, 7, 7)
+    assert err <= 1e-4 * scale + 1e-3, (err, scale)

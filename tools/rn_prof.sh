@@ -14,6 +14,6 @@ python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}/run_results.db" --top 40 > "$O/$
 python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}/run_results.db" --top 60 --grid > "$O/${TAG}_grid.txt"
 python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}/run_results.db" --families --steps $((STEPS + WARM)) --top 30 \
   > "$O/${TAG}_families.txt"
-python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}/run_results.db" --busy 0 --window "mt_sgd:${STEPS}" >> "$O/${TAG}_families.txt" || true
+python3 "$R/tools/kernel_stats.py" "/tmp/${TAG}/run_results.db" --busy 0 --window "${WIN:-mt_sgd}:${STEPS}" >> "$O/${TAG}_families.txt" || true
 cat "$O/${TAG}_families.txt"
 echo "[rn_prof] done"
