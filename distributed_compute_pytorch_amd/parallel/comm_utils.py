@@ -113,6 +113,7 @@ class CoalescedBroadcaster:
         self.tensors = list(tensors)
         self.cap = cap_bytes
         self.plan = []  # list of (indices, flat)
+        self._pending = None  # (works, unpack?) between start() and finish()
         groups: "OrderedDict[tuple, List[int]]" = OrderedDict()
         for i, t in enumerate(self.tensors):
             groups.setdefault(_word_key(t), []).append(i)
@@ -142,16 +143,36 @@ class CoalescedBroadcaster:
         return out
 
     @torch.no_grad()
-    def __call__(self, pg, src: int = 0):
+    def start(self, pg, src: int = 0):
+        """Pack (on ``src``) and enqueue the broadcasts; :meth:`finish` waits
+        and unpacks. Between the two the collectives run on the communicator's
+        stream while the caller's stream goes on (the flat buffers are owned
+        here, so nothing the caller does touches them)."""
+        if self._pending is not None:
+            raise RuntimeError("CoalescedBroadcaster: start() while a broadcast is pending")
         works = []
         for idx, flat in self.plan:
             if pg.rank() == src:
                 pack(self._views(idx, flat), flat)
             works.append((pg.comm_for(flat).broadcast(flat, src), idx, flat))
+        self._pending = (works, pg.rank() != src)
+
+    @property
+    def pending(self) -> bool:
+        return self._pending is not None
+
+    @torch.no_grad()
+    def finish(self):
+        works, recv = self._pending
+        self._pending = None
         for w, idx, flat in works:
             w.wait()
-            if pg.rank() != src:
+            if recv:
                 unpack(flat, self._views(idx, flat))
+
+    def __call__(self, pg, src: int = 0):
+        self.start(pg, src)
+        self.finish()
 
 
 def broadcast_coalesced(pg, tensors: Sequence[torch.Tensor], src: int = 0, cap_bytes: int = 250 << 20):

@@ -9,7 +9,10 @@ SURVEY §2b F5, §3.2, §3.3. Same constructor arguments and semantics:
   Reducer (F6) that hooks every parameter's gradient accumulator;
 * forward: broadcast buffers from rank 0 when ``broadcast_buffers`` and the
   previous forward was a synced training forward (C3), run the module, arm the
-  Reducer for backward;
+  Reducer for backward. With ``overlap_buffer_sync`` (default) that broadcast
+  is started at the END of the synced forward, runs on the comm stream under
+  the backward, and the next forward only unpacks it: the same values, no
+  per-forward collective latency on the compute stream (SURVEY §7.6 H8);
 * backward: bucket all-reduces (average over the world) fire in bucket order
   while backward continues, finalize writes averaged gradients back;
 * ``no_sync()``, ``register_comm_hook``, ``find_unused_parameters``,
@@ -142,6 +145,18 @@ class GradBucket:
         self._buffer.copy_(tensor)
 
 
+_BUFFER_SYNCS = _weakref.WeakSet()  # DDPs that may hold an overlapped buffer broadcast in flight
+
+
+def finish_buffer_syncs() -> None:
+    """Complete every overlapped buffer broadcast still in flight (before a
+    HIP-graph capture: a captured forward must not wait on work enqueued
+    outside the capture)."""
+    for d in list(_BUFFER_SYNCS):
+        if d._buffer_bcast is not None and d._buffer_bcast.pending:
+            d._buffer_bcast.finish()
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids: Optional[List[Any]] = None, output_device=None, dim: int = 0,
                  broadcast_buffers: bool = True, process_group=None, bucket_cap_mb: Optional[float] = None,
@@ -149,7 +164,8 @@ class DistributedDataParallel(nn.Module):
                  gradient_as_bucket_view: bool = False, static_graph: bool = False,
                  first_bucket_mb: Optional[float] = None, comm_dtype: Optional[torch.dtype] = None,
                  rebuild_buckets: bool = True, init_sync: bool = True, tail_bucket_mb: Optional[float] = None,
-                 register_buckets: bool = False, overlap_optimizer: bool = False, defer_accum_wgrad: bool = False):
+                 register_buckets: bool = False, overlap_optimizer: bool = False, defer_accum_wgrad: bool = False,
+                 overlap_buffer_sync: bool = True):
         super().__init__()
         self.module = module
         self.process_group = process_group if process_group is not None else dist.get_default_group()
@@ -187,6 +203,15 @@ class DistributedDataParallel(nn.Module):
         if init_sync:
             broadcast_coalesced(pg, [p.detach() for p in params] + [b for b in self._buffers_list], 0)
         self._buffer_bcast = CoalescedBroadcaster(self._buffers_list) if self._buffers_list else None
+        # overlap_buffer_sync: the buffer broadcast a synchronising forward
+        # would make the NEXT forward wait for is started right after this one
+        # (rank 0's buffers as this forward left them) and runs on the
+        # communicator's stream under the backward; the next forward only
+        # unpacks it. Those are the values torch's start-of-forward broadcast
+        # would deliver, unless rank 0's buffers change between the forwards
+        # outside a forward (then call sync_buffers() first). Off: the
+        # broadcast runs at the start of the forward, as torch's does.
+        self.overlap_buffer_sync = bool(overlap_buffer_sync)
 
         # Initial plan: registration order, [first, cap] limits, then reversed so
         # the bucket holding the last-defined parameters (ready first) is bucket 0.
@@ -260,12 +285,19 @@ class DistributedDataParallel(nn.Module):
 
     def _forward(self, *inputs, **kwargs):
         grad = torch.is_grad_enabled()
-        if self.broadcast_buffers and self._buffer_bcast is not None and self.require_forward_param_sync \
-                and self.process_group.size() > 1:
-            self._buffer_bcast(self.process_group, 0)
+        bufs = self.broadcast_buffers and self._buffer_bcast is not None and self.process_group.size() > 1
+        if bufs:
+            if self._buffer_bcast.pending:  # started after the previous (synchronising) forward
+                self._buffer_bcast.finish()
+            elif self.require_forward_param_sync:
+                self._buffer_bcast(self.process_group, 0)
         out = self.module(*inputs, **kwargs)
         if grad and self.require_backward_grad_sync:
             self.require_forward_param_sync = True
+            if bufs and self.overlap_buffer_sync and not (self.device.type == "cuda"
+                                                           and torch.cuda.is_current_stream_capturing()):
+                self._buffer_bcast.start(self.process_group, 0)
+                _BUFFER_SYNCS.add(self)
             outs = _tensors_in(out) if self.find_unused_parameters else []
             self.reducer.prepare_for_backward(outs, True)
         else:
@@ -304,6 +336,15 @@ class DistributedDataParallel(nn.Module):
         # a compression hook declares its wire precision (``hook.wire_dtype``):
         # the debug stream-ordering check then tolerates that rounding
         self.reducer.set_comm_hook(_call, getattr(hook, "wire_dtype", None))
+
+    def sync_buffers(self) -> None:
+        """Broadcast the module's buffers from rank 0 now (after completing an
+        overlapped broadcast still in flight). Collective: every rank calls it."""
+        if self._buffer_bcast is None or self.process_group.size() == 1:
+            return
+        if self._buffer_bcast.pending:
+            self._buffer_bcast.finish()
+        self._buffer_bcast(self.process_group, 0)
 
     def wait_gradients(self) -> None:
         """overlap_optimizer: order the current stream behind every bucket

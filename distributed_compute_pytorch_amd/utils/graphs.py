@@ -78,6 +78,10 @@ class CapturedStep:
             for _ in range(self.warmup if warmup is None else warmup):
                 self.step_fn(*self.static_inputs)
         torch.cuda.current_stream().wait_stream(s)
+        from ..parallel.ddp import finish_buffer_syncs
+
+        with torch.cuda.stream(s):
+            finish_buffer_syncs()  # the warmup's last forward may have left one in flight
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         # thread_local: the communicator watchdog thread polls events while we

@@ -375,3 +375,61 @@ def _tiny_lm_parity(rank, world):
 
 def test_transformer_shaped_ws4_xgmi_plan_overlap_matches_torch():
     run_world(_tiny_lm_parity, 4, timeout=300)
+
+
+class _BNNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(1, 8, 3)
+        self.bn = nn.BatchNorm2d(8)
+        self.fc = nn.Linear(8, 10)
+
+    def forward(self, x):
+        return F.log_softmax(self.fc(F.relu(self.bn(self.conv(x))).mean((2, 3))), 1)
+
+
+def _buffer_sync(rank, world, overlap):
+    """BatchNorm running statistics under the per-forward buffer broadcast:
+    ours (broadcast started after each synchronising forward and completed at
+    the next one, or torch's start-of-forward broadcast) against torch DDP —
+    every rank's eval outputs and buffers after a mix of training, no_sync and
+    eval forwards."""
+    import distributed_compute_pytorch_amd as dcp
+
+    tdist = _init_torch_pg(rank, world)
+    torch.manual_seed(0)
+    m_ours = _BNNet()
+    m_ref = copy.deepcopy(m_ours)
+    ours = dcp.parallel.DistributedDataParallel(m_ours, overlap_buffer_sync=overlap)
+    ref = nn.parallel.DistributedDataParallel(m_ref)
+    o1 = dcp.optim.SGD(ours.parameters(), lr=0.1)
+    o2 = torch.optim.SGD(ref.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(50 + rank)
+    xe = torch.randn(4, 1, 12, 12, generator=torch.Generator().manual_seed(99))
+    for it in range(4):
+        x = [torch.randn(6, 1, 12, 12, generator=g) * (1 + rank) for _ in range(2)]
+        y = [torch.randint(0, 10, (6,), generator=g) for _ in range(2)]
+        for model, opt in ((ours, o1), (ref, o2)):
+            model.train()
+            opt.zero_grad()
+            if it % 2:  # an accumulation step: the no_sync forward broadcasts too (torch semantics)
+                with model.no_sync():
+                    F.nll_loss(model(x[1]), y[1]).backward()
+            F.nll_loss(model(x[0]), y[0]).backward()
+            opt.step()
+        if it >= 2:  # eval forwards: rank 0's statistics on every rank
+            outs = []
+            for model in (ours, ref):
+                model.eval()
+                with torch.no_grad():
+                    outs.append(model(xe))
+            torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-6)
+            for (n, b), c in zip(m_ref.named_buffers(), m_ours.buffers()):
+                torch.testing.assert_close(c, b, rtol=1e-5, atol=1e-6, msg=n)
+    ours.sync_buffers()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_buffer_broadcast_matches_torch(overlap):
+    run_world(_buffer_sync, 2, overlap)

@@ -37,7 +37,9 @@ def main():
 
     wl = workloads.build(a.model, dev, fused=True)
     dcp.distributed.init_process_group("rccl", device_id=0)
-    ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[0], gradient_as_bucket_view=True)
+    # the bench's DDP settings that change which ops run (bench.py)
+    kw = {"defer_accum_wgrad": True} if wl.accum > 1 else {}
+    ddp = dcp.parallel.DistributedDataParallel(wl.model, device_ids=[0], gradient_as_bucket_view=True, **kw)
     opt = wl.make_optimizer(ddp.parameters())
     step = workloads.make_step(wl, ddp, opt)
     for _ in range(6):
@@ -86,6 +88,24 @@ def main():
     print(f"# {a.model}: copy / fill ops per step by profiler parent chain")
     for (n, w), c in chains.most_common(a.top):
         print(f"{c / a.steps:8.1f}  {n:14s} {w[:150]}")
+    # every ATen op that launched a non-dcp GPU kernel, with its parent chain
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof2:
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+    launches = Counter()
+    for e in prof2.events():
+        ks = [k for k in getattr(e, "kernels", []) if not k.name.startswith("dcp::")]
+        if not ks or not e.name.startswith("aten::"):
+            continue
+        names, p = [], e.cpu_parent
+        while p is not None and len(names) < 3:
+            names.append(p.name)
+            p = p.cpu_parent
+        launches[(e.name, ks[0].name[:40], " < ".join(names))] += len(ks)
+    print(f"# {a.model}: non-dcp GPU kernels per step by launching ATen op and parent chain")
+    for (n, k, w), c in launches.most_common(a.top):
+        print(f"{c / a.steps:8.1f}  {n:22s} {k:40s} {w[:120]}")
     print(f"# {a.model}: ATen copy / fill ops per step and the first frame in the package")
     for (n, w), c in cnt.most_common(a.top):
         print(f"{c / a.steps:8.1f}  {n:28s} {w}")
