@@ -378,6 +378,35 @@ std::vector<at::Tensor> gemm_pp(const at::Tensor& x, const at::Tensor& w, const 
   return {y};
 }
 
+// LM head + cross-entropy forward in two launches (gemm_pp.hip EPI 7): logits
+// [M, N] bf16 = x·wᵀ with each row's softmax partials over the first V columns
+// from the GEMM epilogue, then (loss [M], lse [M]) merged from the partials —
+// no separate pass over the logits. x [M, K] bf16, w [N, K] bf16, target [M]
+// int64. Returns (logits, loss, lse).
+std::vector<at::Tensor> lm_head_xent_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& target,
+                                         int64_t ignore_index, int64_t V) {
+  DK_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 2,
+           "lm_head_xent_fwd: contiguous bf16 [M, K] input");
+  DK_CHECK(target.scalar_type() == at::kLong && target.numel() == x.size(0) && target.device() == x.device(),
+           "lm_head_xent_fwd: int64 target [M] on the input's device");
+  c10::hip::HIPGuard guard(x.device().index());
+  const int64_t M = x.size(0), K = x.size(1);
+  DK_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 && w.size(1) == K,
+           "lm_head_xent_fwd: weight must be contiguous bf16 [N, K]");
+  const int64_t N = w.size(0);
+  DK_CHECK(kern::gemm_pp_supported(M, N, K) && N % 8 == 0 && V >= 1 && V <= N,
+           "lm_head_xent_fwd: unsupported shape (N % 8, K % 64, 1 <= V <= N)");
+  at::Tensor tg = target.contiguous();
+  at::Tensor y = at::empty({M, N}, x.options());
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({kern::gemm_pp_xent_parts(static_cast<int>(N)) * M * 2}, fo);
+  at::Tensor loss = at::empty({M}, fo), lse = at::empty({M}, fo);
+  kern::gemm_pp_xent_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, static_cast<int>(N), static_cast<int>(K),
+                          static_cast<int>(V), part.data_ptr<float>(), tg.data_ptr<int64_t>(), ignore_index,
+                          loss.data_ptr<float>(), lse.data_ptr<float>(), stream_of(x));
+  return {y, loss, lse};
+}
+
 // (w_bf16 [R, C], w_bf16^T [C, R]) from an fp32 (or bf16) weight viewed as [R, C]
 std::vector<at::Tensor> weight_bf16_t(const at::Tensor& w) {
   DK_CHECK(w.is_cuda() && w.dim() >= 2, "weight_bf16_t: device weight required");
@@ -1713,6 +1742,9 @@ void bind(pybind11::module& m) {
   m.def("conv1x1_fwd_res", &conv1x1_fwd_res, "block boundary: conv1x1(relu(x*scale+shift+res), w) with y and its "
         "ReLU mask stored by the GEMM's prologue", py::arg("x"), py::arg("w"), py::arg("scale"), py::arg("shift"),
         py::arg("res"), py::arg("stats") = true);
+  m.def("lm_head_xent_fwd", &lm_head_xent_fwd,
+        "LM head GEMM with the cross-entropy's softmax partials in its epilogue -> (logits, loss, lse)",
+        py::arg("x"), py::arg("w"), py::arg("target"), py::arg("ignore_index"), py::arg("V"));
   m.def("gemm_pp", &gemm_pp, "x·wᵀ (+bias) (+gelu) on the 8-wave ping-pong 256x256 MFMA GEMM", py::arg("x"),
         py::arg("w"), py::arg("bias") = py::none(), py::arg("gelu") = 0);
   m.def("linear_fwd", &linear_fwd, "Linear forward on the MFMA GEMM: bias (+ GELU tanh/erf) in the epilogue",

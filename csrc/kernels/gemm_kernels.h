@@ -77,6 +77,14 @@ void gemm_pq_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K
 // pins); gemm_pp_splitk_bf16 writes S fp32 partial slabs into ws (S x M x N
 // floats) and sums them into C in a fixed order. No bias / GELU; N % 8 == 0.
 int gemm_pp_splitk(int64_t M, int N, int K);
+// LM head + cross-entropy forward: C [M, N] bf16 = A·Bᵀ (one-tile ping-pong
+// kernel) whose epilogue also writes each row's softmax partials over the
+// first V columns into part (float2 [gemm_pp_xent_parts(N)][M]); a second
+// launch merges them: lse[M], loss[M] = lse - C[row, target] (0 where target
+// == ignore or outside [0, V)). N % 8 == 0, V <= N.
+int gemm_pp_xent_parts(int N);
+void gemm_pp_xent_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int V, float* part,
+                       const int64_t* target, int64_t ignore, float* loss, float* lse, hipStream_t s);
 void gemm_pp_splitk_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int64_t ldc, int S, float* ws,
                          hipStream_t s);
 // MLP backward through the GELU on the ping-pong GEMM: C [M, N] = bf16(A·Bᵀ) ⊙

@@ -125,7 +125,12 @@ __device__ __forceinline__ float pp_gelu_dx(float x) {
 // C = bf16(A·Bᵀ) ⊙ gelu'(h) (h [M, N] bf16, ldc apart) and dbias[N] += the
 // column sums of the stored C (fp32 atomics: 2 per column per workgroup);
 // 6 = split-K partial: K-tiles [ks * kchunk, +kchunk) of the tile, fp32 into
-// slab ks of ws ([S][M][N]), summed in a fixed order by pp_splitk_reduce.
+// slab ks of ws ([S][M][N]), summed in a fixed order by pp_splitk_reduce;
+// 7 = C plus the softmax partials of its rows for a fused cross-entropy (the
+// LM head): per row and 64-column wave block, (max, Σ exp(c - max)) of the
+// stored bf16 values in columns < kchunk (the vocabulary; the pad columns are
+// skipped) into ws as float2 [tiles_n * 4][M] — xent_partials_finish merges
+// them, so the loss needs no extra pass over the [M, N] logits.
 template <int EPI>
 __global__ void __launch_bounds__(kPT, 1)
     gemm_pp1_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
@@ -135,6 +140,7 @@ __global__ void __launch_bounds__(kPT, 1)
   constexpr bool BIAS = EPI >= 1 && EPI <= 3;
   constexpr bool GB = EPI == 4 || EPI == 5;
   constexpr bool SK = EPI == 6;
+  constexpr bool XP = EPI == 7;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -395,12 +401,41 @@ __global__ void __launch_bounds__(kPT, 1)
 #pragma unroll
     for (int it = 0; it < 8; ++it)  // materialise all 8 reads before the guarded stores
       asm volatile("" ::"v"(val[it].x), "v"(val[it].y), "v"(val[it].z), "v"(val[it].w));
+    if constexpr (XP) {
+      // rows (half * 8 + it) * 8 + lane / 8: the 8 lanes of a row hold its 64
+      // columns of this wave; (max, Σexp) per lane, merged over those lanes
+      float2* part = reinterpret_cast<float2*>(ws) + static_cast<int64_t>((v % tiles_n) * 4 + wc) * M;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const uint32_t v4[4] = {val[it].x, val[it].y, val[it].z, val[it].w};
+        float x[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          x[2 * k] = cb + 2 * k < kchunk ? pp_lo(v4[k]) : -INFINITY;
+          x[2 * k + 1] = cb + 2 * k + 1 < kchunk ? pp_hi(v4[k]) : -INFINITY;
+        }
+        float mx = x[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) mx = fmaxf(mx, x[k]);
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        float sm = 0.f;
+        if (mx != -INFINITY) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) sm += __expf(x[k] - mx);  // exp(-inf) = 0 for the pad columns
+        }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) sm += __shfl_xor(sm, o, 64);
+        const int64_t m = rbase + (half * 8 + it) * 8 + (lane >> 3);
+        if ((lane & 7) == 0 && m < M) part[m] = make_float2(mx, sm);
+      }
+    }
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int64_t m = rbase + (half * 8 + it) * 8 + (lane >> 3);
       if (m < M && cb < N) {
         *reinterpret_cast<uint4*>(C + m * ldc + cb) = val[it];
-        if constexpr (EPI >= 2) {
+        if constexpr (EPI == 2 || EPI == 3) {
           const uint32_t v4[4] = {val[it].x, val[it].y, val[it].z, val[it].w};
           uint32_t g4[4];
 #pragma unroll
@@ -860,7 +895,66 @@ __global__ void __launch_bounds__(256) pp_splitk_reduce(const f32x4* __restrict_
     *reinterpret_cast<uint2*>(C + row * ldc + c) = make_uint2(pp_pack(a[0], a[1]), pp_pack(a[2], a[3]));
   }
 }
+// Cross-entropy from the LM head GEMM's softmax partials (EPI 7): per row,
+// lse = merge of the P (max, Σexp) pairs, loss = lse - logit[target] (0 for
+// ignored / out-of-range targets). Block: 64 rows x 16 partial groups.
+__global__ void __launch_bounds__(1024) xent_partials_finish(const float2* __restrict__ part, int P, int64_t M,
+                                                             const uint16_t* __restrict__ logits, int64_t ldl,
+                                                             const int64_t* __restrict__ target, int V, int64_t ignore,
+                                                             float* __restrict__ loss, float* __restrict__ lse) {
+  __shared__ float2 red[16][64];
+  const int r = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 64 + r;
+  float mx = -INFINITY, sm = 0.f;
+  if (row < M) {
+    for (int p = g; p < P; p += 16) {
+      const float2 q = part[static_cast<int64_t>(p) * M + row];
+      const float m2 = fmaxf(mx, q.x);
+      if (m2 != -INFINITY) {
+        sm = sm * __expf(mx - m2) + q.y * __expf(q.x - m2);
+        mx = m2;
+      }
+    }
+  }
+  red[g][r] = make_float2(mx, sm);
+  __syncthreads();
+  if (g == 0 && row < M) {
+    for (int k = 1; k < 16; ++k) {
+      const float2 q = red[k][r];
+      const float m2 = fmaxf(mx, q.x);
+      if (m2 != -INFINITY) {
+        sm = sm * __expf(mx - m2) + q.y * __expf(q.x - m2);
+        mx = m2;
+      }
+    }
+    const float l = mx + __logf(sm);
+    lse[row] = l;
+    const int64_t tg = target[row];
+    loss[row] = (tg == ignore || tg < 0 || tg >= V) ? 0.f : l - pp_lo(static_cast<uint32_t>(logits[row * ldl + tg]));
+  }
+}
 }  // namespace
+
+int gemm_pp_xent_parts(int N) { return (N + 255) / 256 * 4; }
+
+void gemm_pp_xent_bf16(const void* A, const void* B, void* C, int64_t M, int N, int K, int V, float* part,
+                       const int64_t* target, int64_t ignore, float* loss, float* lse, hipStream_t s) {
+  if (N % 8 != 0 || V > N) throw std::runtime_error("gemm_pp_xent: N % 8 == 0 and V <= N");
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_pp1_kernel<7>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kPPLds);
+    return true;
+  }();
+  (void)attr;
+  const int tiles_n = (N + 255) / 256;
+  const int tiles = static_cast<int>((M + 255) / 256) * tiles_n;
+  hipLaunchKernelGGL((gemm_pp1_kernel<7>), dim3(tiles), dim3(kPT), kPPLds, s, static_cast<const uint16_t*>(A),
+                     static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N, K, static_cast<int64_t>(N),
+                     tiles_n, nullptr, nullptr, nullptr, nullptr, part, V);
+  hipLaunchKernelGGL(xent_partials_finish, dim3(static_cast<unsigned>((M + 63) / 64)), dim3(1024), 0, s,
+                     reinterpret_cast<const float2*>(part), tiles_n * 4, M, static_cast<const uint16_t*>(C),
+                     static_cast<int64_t>(N), target, V, ignore, loss, lse);
+}
 
 int gemm_pp_splitk(int64_t M, int N, int K) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);

@@ -10,7 +10,10 @@ tied ``wte`` [50257, 768], BERT's MLM head over the word embeddings [30522,
   per-micro-step fp32→bf16 cast of the 38.6 M-parameter embedding);
 * forward: logits [M, Vp] on the autotuned GEMM (256×256 ping-pong / 128×128
   ring / hipBLASLt), then the one-pass cross-entropy over the first V columns
-  (``xent.hip``; the pad columns are never read);
+  (``xent.hip``; the pad columns are never read) — or, without a bias, the
+  ping-pong GEMM whose epilogue also emits each row's softmax partials
+  (``gemm_pp.hip`` EPI 7), merged by a small kernel: the loss then costs no
+  pass over the [M, Vp] logits (the autotune times GEMM + loss together);
 * backward: the cross-entropy gradient is written IN PLACE over the logits,
   pad columns zeroed (no second [M, Vp] buffer), the data gradient is dL·W on
   the autotuned GEMM with K = Vp, and the fp32 weight gradient comes from our
@@ -61,16 +64,31 @@ class _LMHeadXentFn(torch.autograd.Function):
         b32 = None
         if bias is not None:
             b32 = F.pad(bias.detach().float(), (0, Vp - V))
-        cands = {}
-        if _pp_ok(M, Vp, K) and (b32 is None or _pp_bias_ok(Vp)):
-            cands["pp"] = lambda: _C.gemm_pp(x2, wb, b32, 0)[0]
-        if K <= 4096 and K % 64 == 0:
-            cands["ring"] = lambda: _C.linear_fwd(x2, wb, b32 if b32 is not None else _zero_bias(Vp, x2.device), 0)[0]
-        cands["hipblaslt"] = lambda: F.linear(x2, wb, b32.to(torch.bfloat16) if b32 is not None else None)
-        c = _pick(("head", M, K, Vp), cands)
-        logits = cands[c]()
         tg = target.reshape(-1)
-        loss, lse = _C.cross_entropy_fwd(logits, tg, ignore_index, 0.0, V)
+        if tg.dtype != torch.int64:
+            tg = tg.long()
+
+        def then_xent(gemm):  # a logits GEMM followed by the one-pass cross-entropy kernel
+            def run():
+                lg = gemm()
+                return (lg,) + tuple(_C.cross_entropy_fwd(lg, tg, ignore_index, 0.0, V))
+            return run
+
+        # each candidate yields (logits, per-row loss, lse), so the autotune
+        # weighs the GEMM together with the loss's cost: "pp_xent" takes the
+        # softmax partials from the GEMM epilogue (no pass over the logits)
+        cands = {}
+        if b32 is None and Vp % 8 == 0 and _pp_ok(M, Vp, K):
+            cands["pp_xent"] = lambda: tuple(_C.lm_head_xent_fwd(x2, wb, tg, ignore_index, V))
+        if _pp_ok(M, Vp, K) and (b32 is None or _pp_bias_ok(Vp)):
+            cands["pp"] = then_xent(lambda: _C.gemm_pp(x2, wb, b32, 0)[0])
+        if K <= 4096 and K % 64 == 0:
+            cands["ring"] = then_xent(
+                lambda: _C.linear_fwd(x2, wb, b32 if b32 is not None else _zero_bias(Vp, x2.device), 0)[0])
+        cands["hipblaslt"] = then_xent(
+            lambda: F.linear(x2, wb, b32.to(torch.bfloat16) if b32 is not None else None))
+        c = _pick(("head_xent", M, K, Vp), cands)
+        logits, loss, lse = cands[c]()
         count = (tg != ignore_index).sum().clamp_min(1)
         ctx.save_for_backward(x2, logits, lse, tg, wb, wt, count)
         ctx.ignore_index, ctx.V, ctx.accum = ignore_index, V, accumulating()

@@ -1,7 +1,8 @@
 """LinearWeightPrep (one-launch bf16 W / Wᵀ of Linear weights, packed groups,
 padded vocabularies) and the fused LM head + cross-entropy node, against fp32
 PyTorch references. Autotune off: our kernels are what runs (``_DEFAULT_OURS``
-picks pp or the ring for the forward GEMMs)."""
+picks pp or the ring for the forward GEMMs; pp_xent = the head GEMM with the
+cross-entropy partials in its epilogue where there is no bias, else the ring)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -9,7 +10,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["pp", "ring"])
+@pytest.fixture(params=["pp", "ring", "pp_xent"])
 def ours(request, monkeypatch):
     from distributed_compute_pytorch_amd.ops import linear
 
@@ -205,3 +206,37 @@ def test_model_step_uses_prep_and_head(cuda, name):
     assert members == n_lin + 1, (members, n_lin)  # every FusedLinear (packed ones as groups) + the head
     loss.backward()
     assert all(p.grad is not None for n, p in m.named_parameters() if "pooler" not in n and "nsp" not in n)
+
+
+@pytest.mark.parametrize("M,K,N,V", [(512, 128, 1024, 1003), (1000, 192, 4160, 4097), (300, 64, 64, 64),
+                                     (8192, 768, 50304, 50257)])
+def test_lm_head_xent_fwd_partials_match_fp64(cuda, M, K, N, V):
+    """The head GEMM's softmax-partials epilogue + merge: logits equal the plain
+    ping-pong GEMM's bit for bit; lse and the per-row loss match an fp64
+    log-sum-exp over the stored bf16 logits' first V columns (ignored targets
+    give 0)."""
+    from distributed_compute_pytorch_amd._ext import C
+
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) * 0.1).to(torch.bfloat16)
+    w[V:] = 0  # the padded vocabulary rows, as LinearWeightPrep leaves them
+    t = torch.randint(0, V, (M,), device=cuda)
+    t[::5] = -100
+    logits, loss, lse = C.lm_head_xent_fwd(x, w, t, -100, V)
+    old = {k: C.gemm_tune_get(k) for k in ("pp_tile", "pp_sk")}
+    try:  # the same one-tile 256 x 256 kernel without the partials (no 128 x 192 tiles, no split-K)
+        C.gemm_tune("pp_tile", 1)
+        C.gemm_tune("pp_sk", 0)
+        ref_logits = C.gemm_pp(x, w, None, 0)[0]
+        torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            C.gemm_tune(k, v)
+    assert torch.equal(logits, ref_logits)
+    lg = logits[:, :V].double()
+    ref_lse = torch.logsumexp(lg, 1)
+    keep = t != -100
+    ref_loss = torch.where(keep, ref_lse - lg.gather(1, t.clamp_min(0)[:, None])[:, 0], torch.zeros_like(ref_lse))
+    torch.testing.assert_close(lse.double(), ref_lse, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(loss.double(), ref_loss, rtol=1e-5, atol=1e-5)
