@@ -116,6 +116,8 @@ def parse():
     ap.add_argument("--res-prologue", type=int, default=0,
                     help="ResNet identity block boundaries: BN3 + residual + ReLU as the next conv1's GEMM prologue "
                          "(1; default 0 = separate apply pass, measured faster: ops/conv.py RES_PROLOGUE)")
+    ap.add_argument("--grad-to-none", type=int, default=1,
+                    help="zero_grad(set_to_none=...) in the step: 1 (torch's default, as main.py) or 0 (zero in place)")
     ap.add_argument("--gemm-tune", default=None,
                     help="k=v[,k=v] entries of the GEMM launcher tuning table (_C.gemm_tune, e.g. nt_big=4)")
     return ap.parse_args()
@@ -314,7 +316,7 @@ def main():
 
     def timed_run(cap_mb):
         ddp, opt = build_ddp(cap_mb)
-        step = workloads.make_step(wl, ddp, opt, graph=bool(a.graph))
+        step = workloads.make_step(wl, ddp, opt, graph=bool(a.graph), set_to_none=bool(a.grad_to_none))
         t_w = time.time()
         for i in range(a.warmup):
             loss = step()
@@ -361,6 +363,7 @@ def main():
                 "optimizer": type(opt).__name__,
                 "comm_dtype": a.comm_dtype,
                 "hip_graph": bool(a.graph),
+                "grad_to_none": bool(a.grad_to_none),
                 "backend": a.backend,
             }
             if a.model == "resnet50":

@@ -359,10 +359,19 @@ def flush_weight_grads() -> None:
                     p.grad.add_(d)
 
 
-def discard_weight_grads() -> None:
-    """Drop the deferred contributions (``zero_grad`` of this package's optimizers)."""
-    _PENDING.clear()
-    _PENDING_B.clear()
+def discard_weight_grads(params=None) -> None:
+    """Drop the deferred contributions — all of them, or those of ``params``
+    (what a ``zero_grad`` of this package's optimizers clears: gradients
+    stashed by no_sync micro-steps belong to ``.grad`` and go with it)."""
+    if params is None:
+        _PENDING.clear()
+        _PENDING_B.clear()
+        return
+    ids = {id(p) for p in params}
+    for k in [k for k, e in _PENDING.items() if all(id(p) in ids for p in e.params)]:
+        del _PENDING[k]
+    for k in [k for k, (b, _) in _PENDING_B.items() if id(b) in ids]:
+        del _PENDING_B[k]
 
 
 def _deferred_bias(ctx, bias, g2):

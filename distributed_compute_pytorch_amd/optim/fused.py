@@ -152,7 +152,20 @@ def _state_like(p: torch.Tensor) -> torch.Tensor:
     return torch.zeros_like(p, memory_format=torch.preserve_format)
 
 
-class SGD(Optimizer):
+class _DropsDeferred:
+    """zero_grad also drops the micro-step weight-gradient contributions a
+    ``defer_accum_wgrad`` DDP still holds for these parameters (they are part
+    of ``.grad``, only not yet added into it: ops/linear.py)."""
+
+    def zero_grad(self, set_to_none: bool = True):
+        from ..ops import linear as _lin
+
+        if _lin.pending_weight_grads():
+            _lin.discard_weight_grads([p for g in self.param_groups for p in g["params"]])
+        super().zero_grad(set_to_none)
+
+
+class SGD(_DropsDeferred, Optimizer):
     """torch.optim.SGD semantics, fused multi-tensor update."""
 
     def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
@@ -209,7 +222,7 @@ class SGD(Optimizer):
                              group["nesterov"], group["maximize"], first, grad_scale)
 
 
-class Adam(Optimizer):
+class Adam(_DropsDeferred, Optimizer):
     """torch.optim.Adam / AdamW semantics (``decoupled_weight_decay``), fused.
 
     ``capturable=True`` (torch's flag of the same name): every parameter's
@@ -431,7 +444,7 @@ class AdamW(Adam):
                          capturable=capturable)
 
 
-class Adadelta(Optimizer):
+class Adadelta(_DropsDeferred, Optimizer):
     """torch.optim.Adadelta semantics (reference optimizer, main.py:124), fused."""
 
     def __init__(self, params, lr: float = 1.0, rho: float = 0.9, eps: float = 1e-6, weight_decay: float = 0.0,

@@ -120,14 +120,16 @@ def build(name: str, device, batch: Optional[int] = None, fused: bool = True, se
     raise ValueError(f"unknown workload {name!r}")
 
 
-def make_step(wl: Workload, ddp, opt, device_type: str = "cuda", graph: bool = False):
+def make_step(wl: Workload, ddp, opt, device_type: str = "cuda", graph: bool = False, set_to_none: bool = True):
     """One optimizer step = ``accum`` micro-batches (all but the last under
     ``no_sync``), bf16 autocast when ``wl.amp``. ``graph=True`` captures the
     whole step (fwd + bwd + reduction + optimizer) into one HIP graph and
-    replays it (see :mod:`.utils.graphs`)."""
+    replays it (see :mod:`.utils.graphs`). ``set_to_none=False`` zeroes the
+    gradients in place instead (they stay the DDP bucket views, so the
+    backward's kernels accumulate straight into them)."""
 
     def run(*flat):
-        opt.zero_grad(set_to_none=True)
+        opt.zero_grad(set_to_none=set_to_none)
         loss = None
         n = len(flat) // wl.accum
         for k in range(wl.accum):

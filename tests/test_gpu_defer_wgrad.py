@@ -140,3 +140,32 @@ def test_colsum_multi_matches_fp64(cuda):
         assert _rel(acc, ref + base.double()) < 1e-5, k
     # the single-segment colsum (same kernel) still agrees
     assert _rel(_C.colsum(segs[0]), segs[0].double().sum(0)) < 1e-5
+
+
+def test_zero_grad_drops_deferred(pg, cuda, no_autotune):
+    """zero_grad of a fused optimizer after no_sync micro-steps (a skipped
+    step): the stashed contributions go with .grad — the next accumulation
+    round's gradients equal a fresh run's."""
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.ops import linear as lin
+
+    base = _model(cuda)
+    data = [torch.randint(0, 50257, (2, 257), device=cuda) for _ in range(2)]
+    m_ref, _, _ = _grads(base, data, True, cuda)
+    m = copy.deepcopy(base)
+    ddp = dcp.parallel.DistributedDataParallel(m, device_ids=[0], gradient_as_bucket_view=True, defer_accum_wgrad=True)
+    opt = dcp.optim.SGD(m.parameters(), lr=0.0)
+    with ddp.no_sync():  # an accumulation round that is abandoned
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            ddp(data[1][:, :-1], data[1][:, 1:]).backward()
+    assert lin.pending_weight_grads() > 0
+    opt.zero_grad(set_to_none=True)
+    assert lin.pending_weight_grads() == 0
+    for k, seq in enumerate(data):
+        with (contextlib.nullcontext() if k == len(data) - 1 else ddp.no_sync()):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = ddp(seq[:, :-1], seq[:, 1:]) / len(data)
+            loss.backward()
+    torch.cuda.synchronize()
+    for (name, a), b in zip(m_ref.named_parameters(), m.parameters()):
+        assert _rel(b.grad, a.grad) < 1e-4, (name, _rel(b.grad, a.grad))
