@@ -1965,6 +1965,8 @@ int g_nt_a = 0;
 // stem weight gradient on one 64 x 256 tile per workgroup (dY streamed once)
 // instead of two 64 x 128 tiles (gemm_tune "stem_wide")
 int g_stem_wide = 1;
+// gemm_tune "nt_deep": 1x1 forwards on the 3-slot 256 x 128 ring (gemm_nt_launch_deep): 0 off, 1 at M >= 64K, 2 always
+int g_nt_deep = 0;
 int g_reserve_cus = [] {
   const char* v = getenv("DCP_RESERVE_CUS");
   const int r = v ? atoi(v) : 0;
@@ -1978,8 +1980,9 @@ void gemm_tune(const char* key, int value) {
   if (k == "nt_big") g_nt_big = value;
   if (k == "lin_big") g_lin_big = value;
   if (k == "big_pipe") g_big_pipe = value;
-  if (k == "nt_a") g_nt_a = value < 0 ? 0 : (value > 2 ? 2 : value);
+  if (k == "nt_a") g_nt_a = value < 0 ? 0 : (value > 3 ? 3 : value);
   if (k == "stem_wide") g_stem_wide = value;
+  if (k == "nt_deep") g_nt_deep = value;
   if (k == "wg_slots") g_wg_slots = value < 64 ? 64 : value;
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
@@ -1993,6 +1996,7 @@ int gemm_tune_get(const char* key) {
   if (k == "big_pipe") return g_big_pipe;
   if (k == "nt_a") return g_nt_a;
   if (k == "stem_wide") return g_stem_wide;
+  if (k == "nt_deep") return g_nt_deep;
   if (k == "wg_slots") return g_wg_slots;
   if (k == "wg_cap") return g_wg_cap;
   if (k == "reserve_cus") return g_reserve_cus;
@@ -2151,6 +2155,39 @@ void gemm_nt_launch_big(const void* A, const void* B, void* C, int64_t M, int N,
                        lds, s, a, b, c, M, N, K, nullptr, nullptr, 0, stats, tiles_m, tn, geo, BnRedArgs{});
 }
 
+// nt_deep: the plain / BN-stats 1x1 forward on 256 x 128 tiles with a 3-slot
+// BK = 64 ring (147 KB, one workgroup per CU: two K-stages of A in flight per
+// CU instead of one per workgroup) — for the in-step 1x1 GEMMs, which stream
+// their activation cold from HBM and are latency-bound (NOTES §28)
+void gemm_nt_launch_deep(const void* A, const void* B, void* C, int64_t M, int N, int K, float* stats, hipStream_t s) {
+  constexpr int BM = 256, BN = 128, NS = 3, BK = 64;
+  const int tiles_m = static_cast<int>((M + BM - 1) / BM);
+  const int tn = N / BN;
+  const int64_t tiles = static_cast<int64_t>(tiles_m) * tn;
+  const int kRes = grid_cus();
+  int P = tiles <= kRes ? static_cast<int>(tiles) : (kRes / tn) * tn;
+  if (P < tn) P = tn;
+  const size_t lds = static_cast<size_t>(NS) * (BM + BN) * BK * 2;
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<BM, BN, false, 0, false, BK, 0, NS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<BM, BN, false, 1, false, BK, 0, NS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  auto c = static_cast<uint16_t*>(C);
+  const ConvGeo geo{};
+  if (stats)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 1, false, BK, 0, NS>), dim3(P), dim3(nt_threads<BM, BN>()), lds,
+                       s, a, b, c, M, N, K, nullptr, nullptr, 0, stats, tiles_m, tn, geo, BnRedArgs{});
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, false, 0, false, BK, 0, NS>), dim3(P), dim3(nt_threads<BM, BN>()), lds,
+                       s, a, b, c, M, N, K, nullptr, nullptr, 0, stats, tiles_m, tn, geo, BnRedArgs{});
+}
+
 // nt_big = 4: the 256 x 256 tile only where it measured faster than the
 // 128 x 128 ring (profiles/r3_gemm_ab_big.jsonl, ResNet-50 b512): every shape
 // with M >= 256 K rows (56x56 / 28x28: 4-22 % faster), and at fewer rows N = 512
@@ -2164,6 +2201,11 @@ template <bool GATHER, int BK>
 void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, int K, const float* scale,
                        const float* shift, bool relu, float* stats, const ConvGeo& geo, const BnRedArgs* red,
                        hipStream_t s, bool scatter2 = false, bool parity = false) {
+  if (g_nt_deep && !GATHER && BK == 64 && N % 128 == 0 && scale == nullptr && red == nullptr && !scatter2 &&
+      !parity && (g_nt_deep == 2 || M >= 65536)) {
+    gemm_nt_launch_deep(A, B, C, M, N, K, stats, s);
+    return;
+  }
   if ((g_nt_big == 2 || g_nt_big == 4) && BK == 64 && N % 256 == 0 && scale == nullptr && red == nullptr && !scatter2 && !parity &&
       (g_nt_big != 4 || big_tile_wins(M, N, K))) {
     // (the gathered variant of the pipelined loop spills: aliased staging only)
@@ -2189,8 +2231,11 @@ void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int
   // nt A operand: always (1), or (2) when A + C exceed the 256 MiB Infinity
   // Cache — the layer-1/2 shapes, whose activations are evicted by the time
   // they are read either way
+  // — or (3) on the BN-stats forwards with K >= 1024 (the layer-3/4 conv1s,
+  // 18-22 % faster cold, profiles/r5_cold_deep.jsonl)
   if (!GATHER)
-    g.nt_a = g_nt_a == 1 || (g_nt_a == 2 && (M * K + M * static_cast<int64_t>(N)) * 2 > (int64_t(256) << 20));
+    g.nt_a = g_nt_a == 1 || (g_nt_a == 2 && (M * K + M * static_cast<int64_t>(N)) * 2 > (int64_t(256) << 20)) ||
+             (g_nt_a == 3 && stats != nullptr && scale == nullptr && red == nullptr && K >= 1024);
   if (nt_bk() == 64 && scale == nullptr)
     gemm_nt_launch_bk<GATHER, 64>(A, B, C, M, N, K, scale, shift, relu, stats, g, red, s);
   else gemm_nt_launch_bk<GATHER, 32>(A, B, C, M, N, K, scale, shift, relu, stats, g, red, s);

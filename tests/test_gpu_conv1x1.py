@@ -27,8 +27,20 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
 
 
+@pytest.fixture(params=[0, 2], ids=["ring", "deep"])
+def nt_deep(request):
+    """gemm_tune nt_deep: 2 = the 3-slot 256 x 128 ring on every plain / stats
+    1x1 forward (N % 128 == 0)."""
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    old = _C.gemm_tune_get("nt_deep")
+    _C.gemm_tune("nt_deep", request.param)
+    yield request.param
+    _C.gemm_tune("nt_deep", old)
+
+
 @pytest.mark.parametrize("shape", SHAPES)
-def test_conv1x1_fwd_stats(cuda, shape):
+def test_conv1x1_fwd_stats(cuda, shape, nt_deep):
     from distributed_compute_pytorch_amd._ext import C as _C
 
     n, h, w, ci, co = shape

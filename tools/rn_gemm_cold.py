@@ -35,14 +35,16 @@ def main():
         g = torch.Generator(device=dev).manual_seed(0)
         x = (torch.rand(M, K, device=dev, generator=g) - 0.5).to(torch.bfloat16)
         w = ((torch.rand(N, K, device=dev, generator=g) - 0.5) / K ** 0.5).to(torch.bfloat16)
-        def nt(f, v):
+        def nt(f, v, deep=0):
             def run():
                 C.gemm_tune("nt_a", v)
+                C.gemm_tune("nt_deep", deep)
                 return f()
             return run
 
         ops = {"ours_stats": nt(lambda: C.conv1x1_fwd(x, w, None, None, False, True), 0),
                "ours_stats_nt": nt(lambda: C.conv1x1_fwd(x, w, None, None, False, True), 1),
+               "ours_stats_deep": nt(lambda: C.conv1x1_fwd(x, w, None, None, False, True), 0, 2),
                "ours": nt(lambda: C.conv1x1_fwd(x, w, None, None, False, False), 0),
                "blas": lambda: torch.mm(x, w.t())}
         if N % 8 == 0:
@@ -68,6 +70,7 @@ def main():
                 warm.append(s.elapsed_time(e) * 1e3)
             rec[k + "_cold_us"] = round(statistics.median(cold), 1)
             rec[k + "_warm_us"] = round(statistics.median(warm), 1)
+        C.gemm_tune("nt_deep", 0)
         rec["cold_TBps_ours_stats"] = round(rec["MB"] / rec["ours_stats_cold_us"], 2)
         print(json.dumps(rec), flush=True)
         del x, w
