@@ -1326,20 +1326,22 @@ __global__ void __launch_bounds__(kT, 2) gemm_wgrad_kernel(const uint16_t* __res
 constexpr int kSlabGroup = 16;
 // n4: float4s reduced (a prefix of each slab: the wgrad's first output rows),
 // ld4: slab stride in float4s (also the stride of the partial slabs written).
+// G slabs per group: 16, or 32 (one level for S <= 32, two up to 1,024)
+template <int G = kSlabGroup>
 __global__ void __launch_bounds__(kT) slab_partial_kernel(const float4* __restrict__ ws, float4* __restrict__ out,
                                                           int64_t n4, int64_t ld4, int S, int acc) {
   const int64_t v = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   if (v >= n4) return;
-  const int z0 = blockIdx.y * kSlabGroup;
-  float4 a[kSlabGroup];
+  const int z0 = blockIdx.y * G;
+  float4 a[G];
 #pragma unroll
-  for (int k = 0; k < kSlabGroup; ++k) {  // clamped index, masked after the load: no branch per load
+  for (int k = 0; k < G; ++k) {  // clamped index, masked after the load: no branch per load
     const int z = min(z0 + k, S - 1);
     a[k] = ws[static_cast<int64_t>(z) * ld4 + v];
   }
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int k = 0; k < kSlabGroup; ++k) {
+  for (int k = 0; k < G; ++k) {
     const float w = (z0 + k < S) ? 1.f : 0.f;
     s.x = fmaf(a[k].x, w, s.x);
     s.y = fmaf(a[k].y, w, s.y);
@@ -1965,6 +1967,8 @@ int g_nt_a = 0;
 // stem weight gradient on one 64 x 256 tile per workgroup (dY streamed once)
 // instead of two 64 x 128 tiles (gemm_tune "stem_wide")
 int g_stem_wide = 1;
+// gemm_tune "slab32": the wgrad slab reduction in 32-slab groups (1) or 16 (0)
+int g_slab32 = 1;
 // gemm_tune "nt_deep": 1x1 forwards on the 3-slot 256 x 128 ring (gemm_nt_launch_deep): 0 off, 1 at M >= 64K, 2 always
 int g_nt_deep = 0;
 int g_reserve_cus = [] {
@@ -1982,6 +1986,7 @@ void gemm_tune(const char* key, int value) {
   if (k == "big_pipe") g_big_pipe = value;
   if (k == "nt_a") g_nt_a = value < 0 ? 0 : (value > 3 ? 3 : value);
   if (k == "stem_wide") g_stem_wide = value;
+  if (k == "slab32") g_slab32 = value;
   if (k == "nt_deep") g_nt_deep = value;
   if (k == "wg_slots") g_wg_slots = value < 64 ? 64 : value;
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
@@ -1996,6 +2001,7 @@ int gemm_tune_get(const char* key) {
   if (k == "big_pipe") return g_big_pipe;
   if (k == "nt_a") return g_nt_a;
   if (k == "stem_wide") return g_stem_wide;
+  if (k == "slab32") return g_slab32;
   if (k == "nt_deep") return g_nt_deep;
   if (k == "wg_slots") return g_wg_slots;
   if (k == "wg_cap") return g_wg_cap;
@@ -2884,11 +2890,23 @@ void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc
   auto w4 = reinterpret_cast<const float4*>(ws);
   const int a = acc ? 1 : 0;
   if (groups == 1) {
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, w4, reinterpret_cast<float4*>(D), n, n4, p.S,
-                       a);
+    hipLaunchKernelGGL(slab_partial_kernel<>, dim3(gx, 1), dim3(kT), 0, s, w4, reinterpret_cast<float4*>(D), n, n4,
+                       p.S, a);
+  } else if (g_slab32 && p.S <= 32 * 32) {
+    // 32 slabs per group: S <= 32 in one launch (no partial level), else two
+    if (p.S <= 32) {
+      hipLaunchKernelGGL(slab_partial_kernel<32>, dim3(gx, 1), dim3(kT), 0, s, w4, reinterpret_cast<float4*>(D), n, n4,
+                         p.S, a);
+    } else {
+      const int g32 = (p.S + 31) / 32;  // <= the 16-slab groups the workspace holds
+      float4* part = reinterpret_cast<float4*>(ws + static_cast<int64_t>(p.S) * n4 * 4);
+      hipLaunchKernelGGL(slab_partial_kernel<32>, dim3(gx, g32), dim3(kT), 0, s, w4, part, n, n4, p.S, 0);
+      hipLaunchKernelGGL(slab_partial_kernel<32>, dim3(gx, 1), dim3(kT), 0, s, part, reinterpret_cast<float4*>(D), n,
+                         n4, g32, a);
+    }
   } else {
     float4* part = reinterpret_cast<float4*>(ws + static_cast<int64_t>(p.S) * n4 * 4);
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, groups), dim3(kT), 0, s, w4, part, n, n4, p.S, 0);
+    hipLaunchKernelGGL(slab_partial_kernel<>, dim3(gx, groups), dim3(kT), 0, s, w4, part, n, n4, p.S, 0);
     // groups ≤ 32 (S ≤ 512): ≤ 2 more levels
     int S2 = groups;
     const float4* src = part;
@@ -2896,11 +2914,11 @@ void slab_reduce(float* ws, float* D, int64_t n4, int S, hipStream_t s, bool acc
     if (S2 > kSlabGroup) {  // one intermediate level back into the head of ws
       const int g2 = (S2 + kSlabGroup - 1) / kSlabGroup;
       float4* mid = reinterpret_cast<float4*>(ws);
-      hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, g2), dim3(kT), 0, s, src, mid, n, n4, S2, 0);
+      hipLaunchKernelGGL(slab_partial_kernel<>, dim3(gx, g2), dim3(kT), 0, s, src, mid, n, n4, S2, 0);
       src = mid;
       S2 = g2;
     }
-    hipLaunchKernelGGL(slab_partial_kernel, dim3(gx, 1), dim3(kT), 0, s, src, dst, n, n4, S2, a);
+    hipLaunchKernelGGL(slab_partial_kernel<>, dim3(gx, 1), dim3(kT), 0, s, src, dst, n, n4, S2, a);
   }
 }
 }  // namespace
