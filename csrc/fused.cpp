@@ -87,6 +87,33 @@ at::Tensor zeroed_floats(int64_t n, const at::Tensor& like, hipStream_t st) {
   return t;
 }
 
+// Zeroed fp32 vectors that outlive the call (bias gradients handed to
+// autograd as .grad): carved front to back from a zeroed slab, a new slab (one
+// fill launch) when the current one is used up — instead of one fill launch
+// per bias. A slab is never re-zeroed, so no carved view is ever overwritten;
+// its memory goes back to the caching allocator when its last view dies.
+// Under HIP-graph capture each call gets its own zeroed tensor.
+at::Tensor zeroed_vec(int64_t n, const at::Tensor& like, hipStream_t st) {
+  constexpr int64_t kSlab = int64_t(1) << 18;  // 1 MiB of fp32
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(st, &cap);
+  const int64_t need = (n + 63) / 64 * 64;  // 256-B aligned views
+  static const bool off = std::getenv("DCP_NO_GRAD_SLAB") != nullptr;  // A/B switch
+  if (off || cap != hipStreamCaptureStatusNone || need > kSlab / 4)
+    return at::zeros({n}, like.options().dtype(at::kFloat));
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<at::Tensor, int64_t>> slabs;
+  std::lock_guard<std::mutex> g(mu);
+  auto& e = slabs[{static_cast<int>(like.get_device()), st}];
+  if (!e.first.defined() || e.second + need > kSlab) {
+    e.first = at::zeros({kSlab}, like.options().dtype(at::kFloat));
+    e.second = 0;
+  }
+  at::Tensor t = e.first.narrow(0, e.second, n);
+  e.second += need;
+  return t;
+}
+
 }  // namespace
 
 // Returns (y, mean, invstd, relu_bits). Training: batch statistics (+ running-
@@ -295,7 +322,7 @@ std::vector<at::Tensor> linear_dgrad_gelu(const at::Tensor& gy, const at::Tensor
     db = *accumulate_into;
     DK_CHECK(db.scalar_type() == at::kFloat && db.is_contiguous() && db.numel() == N, "linear_dgrad_gelu: db target");
   } else {
-    db = at::zeros({N}, gy.options().dtype(at::kFloat));
+    db = zeroed_vec(N, gy, stream_of(gy));
   }
   std::vector<int64_t> shape(h.sizes().begin(), h.sizes().end());
   at::Tensor gh = at::empty(shape, h.options());
@@ -993,8 +1020,7 @@ at::Tensor colsum(const at::Tensor& x, const c10::optional<at::Tensor>& accumula
     DK_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
                   accumulate_into->numel() == N && accumulate_into->device() == x.device(),
               "colsum: accumulate_into must be a contiguous fp32 [N] tensor on the same device");
-  at::Tensor out = acc ? *accumulate_into : at::empty({N}, x.options().dtype(at::kFloat));
-  if (!acc) out.zero_();  // fill kernel: graph-capture safe (see zeroed_floats)
+  at::Tensor out = acc ? *accumulate_into : zeroed_vec(N, x, s);
   kern::colsum_bf16(x.data_ptr(), out.data_ptr<float>(), M, static_cast<int>(N), s);
   return out;
 }
@@ -1022,8 +1048,7 @@ at::Tensor colsum_multi(const std::vector<at::Tensor>& xs, const c10::optional<a
     DK_CHECK(accumulate_into->scalar_type() == at::kFloat && accumulate_into->is_contiguous() &&
                  accumulate_into->numel() == N && accumulate_into->device() == xs[0].device(),
              "colsum_multi: accumulate_into must be a contiguous fp32 [N] tensor on the same device");
-  at::Tensor out = acc ? *accumulate_into : at::empty({N}, xs[0].options().dtype(at::kFloat));
-  if (!acc) out.zero_();
+  at::Tensor out = acc ? *accumulate_into : zeroed_vec(N, xs[0], s);
   kern::colsum_multi_bf16(sg, out.data_ptr<float>(), static_cast<int>(N), s);
   return out;
 }
