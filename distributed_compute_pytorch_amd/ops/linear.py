@@ -112,6 +112,23 @@ def _agree(key, mine: str) -> str:
     return theirs if theirs in _CANDIDATES else mine
 
 
+# near-ties go to our kernels: hipBLASLt is taken only when it measured more
+# than this fraction faster than our best candidate (the two trade places
+# within ~1 % from box to box on shapes like the LM-head data gradient)
+_OURS_TIE = 0.02
+
+
+def _fastest(ts: dict) -> str:
+    c = min(ts, key=ts.get)
+    if c == "hipblaslt":
+        ours = [k for k in ts if k != "hipblaslt"]
+        if ours:
+            o = min(ours, key=ts.get)
+            if ts[o] <= ts[c] * (1.0 + _OURS_TIE):
+                return o
+    return c
+
+
 def _pick(key, cands: dict) -> str:
     """The kernel to run for ``key`` among ``cands`` (name -> zero-argument
     launch): the measured fastest (rank 0's measurement when a process group is
@@ -125,7 +142,7 @@ def _pick(key, cands: dict) -> str:
     with torch.no_grad():
         ts = _measure(cands)
     _TIMES[key] = ts
-    c = _CHOICE[key] = _agree(key, min(ts, key=ts.get))
+    c = _CHOICE[key] = _agree(key, _fastest(ts))
     return c
 
 

@@ -66,3 +66,17 @@ def test_agree_takes_rank0_choice_and_never_blocks():
     from mp_util import run_world
 
     run_world(_agree_world, 2)
+
+
+def test_near_ties_go_to_our_kernels(monkeypatch):
+    monkeypatch.setattr(lin, "_AUTOTUNE", True)
+    monkeypatch.setattr(lin, "_CHOICE", {})
+    times = {}
+    monkeypatch.setattr(lin, "_measure", lambda cands: dict(times))
+    monkeypatch.setattr(lin.torch.cuda, "is_current_stream_capturing", lambda: False)  # no GPU here
+    times.update(pp=1.01, ring=1.2, hipblaslt=1.0)  # within 2 %: ours
+    assert lin._pick(("fwd", 1, 2, 3), _cands([])) == "pp"
+    times.update(pp=1.05, ring=1.04, hipblaslt=1.0)  # 4 % slower: hipBLASLt
+    assert lin._pick(("fwd", 1, 2, 4), _cands([])) == "hipblaslt"
+    times.update(pp=0.9, ring=1.2, hipblaslt=1.0)
+    assert lin._pick(("fwd", 1, 2, 5), _cands([])) == "pp"
