@@ -316,6 +316,10 @@ def main():
 
     def timed_run(cap_mb):
         ddp, opt = build_ddp(cap_mb)
+        if ours and world > 1 and workloads.pretune_step(wl, ddp, opt):
+            # GEMM autotune outside any synchronised backward (no bucket
+            # collective in flight), one rank-0 table for all ranks
+            log(f"[bench] rank {rank}: GEMM shapes tuned in a no_sync micro-step")
         step = workloads.make_step(wl, ddp, opt, graph=bool(a.graph), set_to_none=bool(a.grad_to_none))
         t_w = time.time()
         for i in range(a.warmup):
@@ -348,6 +352,26 @@ def main():
         samples_per_step = wl.per_gpu_batch * wl.accum * world
         total = samples_per_step * a.steps / elapsed
         rec = None
+        diag = None
+        if ours and world > 1 and not a.comm_timing and not a.graph:
+            # untimed diagnostic steps with device comm timing on: whether
+            # overlap held (exposed vs per-bucket comm ms), as a multi-GPU run
+            # record must be able to explain itself; MAX over ranks
+            ddp.set_comm_timing(True)
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            info = ddp.ddp_logging_data()
+            ddp.set_comm_timing(False)
+            diag = {
+                "steps": 3,
+                "exposed_comm_ms": round(max_over_ranks(info["exposed_comm_ms"]), 4),
+                "bucket_comm_ms": [round(x, 4) for x in info["bucket_comm_ms"]],
+                "bucket_ready_dev_ms": [round(x, 3) for x in info["bucket_ready_dev_ms"]],
+                "comm_bytes_per_step": sum(info["bucket_sizes"]),
+                "rccl_ranks": ddp._comm.transport_size(),
+                "backend": info["backend"],
+            }
         if ours:
             info = ddp.ddp_logging_data()
         if rank == 0:
@@ -412,6 +436,8 @@ def main():
             if wl.seq_len:
                 rec["tokens_per_s"] = round(total * wl.seq_len, 1)
             rec["vs_baseline"] = _vs_baseline(a.model, wl, world, total)
+            if diag is not None:
+                rec["comm_diag"] = diag
             if a.ref_1gpu:
                 rec["scaling_efficiency"] = round(total / (world * a.ref_1gpu), 4)
             if ours and a.comm_timing:

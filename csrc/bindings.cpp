@@ -115,6 +115,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("recv", &Communicator::recv, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &Communicator::barrier, py::call_guard<py::gil_scoped_release>())
       .def("abort", &Communicator::abort)
+      .def("transport_size", &Communicator::transport_size)
+      .def("set_timing", &Communicator::set_timing)
       .def("stream_fence", &Communicator::stream_fence, py::call_guard<py::gil_scoped_release>())
       .def("register_buffer", &Communicator::register_buffer, py::arg("tensor"))
       .def("deregister_buffer", &Communicator::deregister_buffer, py::arg("handle"))
@@ -154,7 +156,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("average", &ReducerOptions::average)
       .def_readwrite("register_buckets", &ReducerOptions::register_buckets)
       .def_readwrite("check_streams", &ReducerOptions::check_streams)
-      .def_readwrite("defer_grad_wait", &ReducerOptions::defer_grad_wait);
+      .def_readwrite("defer_grad_wait", &ReducerOptions::defer_grad_wait)
+      .def_readwrite("static_graph", &ReducerOptions::static_graph);
 
   m.def("trace_enabled", &trace::enabled);
   m.def("trace_push", [](const std::string& n) { trace::push(n.c_str()); });
@@ -214,7 +217,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("sync_bucket", &Reducer::sync_bucket, py::call_guard<py::gil_scoped_release>())
       .def("sync_all", &Reducer::sync_all, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("num_iterations", &Reducer::num_iterations)
-      .def_property_readonly("num_rebuilds", &Reducer::num_rebuilds);
+      .def_property_readonly("num_rebuilds", &Reducer::num_rebuilds)
+      .def_property_readonly("static_frozen", &Reducer::static_frozen)
+      .def("static_unused", &Reducer::static_unused)
+      .def("note_used", &Reducer::note_used)
+      .def("set_timing", &Reducer::set_timing);
 
   // ------------------------------------------------------------- ops ---
   m.def("mt_copy", &ops::mt_copy, py::arg("src"), py::arg("dst"), py::arg("scale") = 1.0);

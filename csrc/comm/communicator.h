@@ -48,6 +48,12 @@ class Communicator {
   int rank() const { return rank_; }
   int size() const { return size_; }
   virtual std::string backend() const = 0;
+  // The rank count the transport itself reports (RCCL: ncclCommCount) — a
+  // cross-check of size() for multi-GPU run records.
+  virtual int transport_size() const { return size_; }
+  // Device-time events on every Work from now on (DCP_COMM_TIMING=1 sets it
+  // at construction); a no-op where there are no device events.
+  virtual void set_timing(bool) {}
 
   virtual WorkPtr all_reduce(at::Tensor& t, ReduceOp op) = 0;
   // All-reduce `wire` in place, then write the result into `out` (same numel,

@@ -152,6 +152,12 @@ class RcclCommunicator : public Communicator {
 
   int64_t stream_handle() const override { return reinterpret_cast<int64_t>(stream_.stream()); }
   std::string backend() const override { return "rccl"; }
+  int transport_size() const override {
+    int n = -1;
+    if (comm_ && !aborted_.load()) NCCL_OK(ncclCommCount(comm_, &n));
+    return n;
+  }
+  void set_timing(bool on) override { timing_ = on; }
 
   WorkPtr all_reduce(at::Tensor& t, ReduceOp op) override {
     check_tensor(t);

@@ -266,6 +266,20 @@ void Reducer::set_expect_backward(bool v) {
   expect_hooks_ = v;
 }
 
+void Reducer::set_timing(bool on) {
+  std::lock_guard<std::mutex> g(mu_);
+  timing_ = on && !params_.empty() && params_[0].is_cuda();
+  if (!timing_) ev_recorded_ = false;
+}
+
+void Reducer::note_used(const std::vector<int64_t>& indices) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (int64_t i : indices) {
+    DK_CHECK(i >= 0 && i < static_cast<int64_t>(params_.size()), "Reducer::note_used: bad parameter index ", i);
+    used_since_sync_[i] = 1;
+  }
+}
+
 void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs, bool require_sync) {
   std::lock_guard<std::mutex> g(mu_);
   DK_CHECK(!finalize_queued_, "Reducer: forward called while a backward reduction is still in progress");
@@ -276,7 +290,13 @@ void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs, bool 
   if (!require_sync) return;
   unused_list_.clear();
   std::fill(unused_.begin(), unused_.end(), 0);
-  if (opts_.find_unused_parameters) find_unused(outputs);
+  if (!opts_.find_unused_parameters) return;
+  if (static_frozen_) {
+    unused_list_ = static_unused_;
+    for (int64_t u : unused_list_) unused_[u] = 1;
+  } else {
+    find_unused(outputs);
+  }
 }
 
 void Reducer::find_unused(const std::vector<at::Tensor>& outputs) {
@@ -340,7 +360,8 @@ void Reducer::autograd_hook(int64_t index) {
   if (opts_.find_unused_parameters && !marked_unused_) {
     marked_unused_ = true;
     // Issued before any bucket on every rank: the collective order matches.
-    launch_used_map_reduce();
+    // A frozen static graph already knows the global map.
+    if (!static_frozen_) launch_used_map_reduce();
     for (int64_t u : unused_list_) mark_ready(u, /*unused=*/true);
   }
   mark_ready(index, /*unused=*/false);
@@ -473,7 +494,19 @@ void Reducer::finalize() {
   }
 
   std::vector<char> global_used;
-  if (opts_.find_unused_parameters) global_used = collect_global_used();
+  if (opts_.find_unused_parameters) {
+    if (static_frozen_) {
+      global_used = static_global_used_;
+    } else {
+      global_used = collect_global_used();
+      if (opts_.static_graph) {
+        static_frozen_ = true;
+        static_unused_ = unused_list_;
+        const bool all = std::all_of(global_used.begin(), global_used.end(), [](char c) { return c != 0; });
+        static_global_used_ = all ? std::vector<char>() : global_used;
+      }
+    }
+  }
 
   hipStream_t cur = nullptr;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;

@@ -79,6 +79,12 @@ struct ReducerOptions {
   // still deferred is synced before the next backward's first pack, by
   // prepare_for_backward and by wait_gradients().
   bool defer_grad_wait = false;
+  // torch's static_graph: the set of parameters that get no gradient is the
+  // same every iteration. The first synchronised backward traverses the graph
+  // and all-reduces the used map (as find_unused_parameters does); later ones
+  // reuse both results — no traversal, no used-map collective, and capturable
+  // in a HIP graph. Implies find_unused_parameters semantics.
+  bool static_graph = false;
 };
 
 struct BucketStats {
@@ -113,6 +119,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void prepare_for_backward(const std::vector<at::Tensor>& outputs, bool require_sync);
   // Called when a forward ran without a following backward being expected.
   void set_expect_backward(bool v);
+  // find_unused_parameters: these parameters got gradient contributions
+  // outside a hook this iteration (deferred no_sync segments added into .grad
+  // by the DDP wrapper): they count as used, like a no_sync hook would mark them.
+  void note_used(const std::vector<int64_t>& indices);
 
   // Custom comm hook (runs on the autograd thread with the bucket buffer).
   // wire_dtype: the precision the hook's collective carries (a compression
@@ -133,9 +143,15 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   // defer_grad_wait the waits sit between the optimizer's per-bucket
   // updates). -1 when unavailable (timing off, CPU, still in flight).
   double exposed_comm_ms();
+  // turn the DCP_COMM_TIMING instrumentation on / off from the next backward
+  // (GPU only): e.g. a few diagnostic steps after an untimed-instrumentation
+  // benchmark region
+  void set_timing(bool on);
   std::vector<int64_t> ready_order() const { return ready_order_; }
   int64_t num_iterations() const { return iterations_; }
   int64_t num_rebuilds() const { return rebuilds_; }
+  bool static_frozen() const { return static_frozen_; }
+  std::vector<int64_t> static_unused() const { return static_unused_; }
   bool has_rebuilt() const { return rebuilds_ > 0; }
   // Bucket buffers (tests / optimizers that work on flat buffers).
   std::vector<at::Tensor> bucket_buffers() const;
@@ -209,6 +225,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<char> unused_;
   std::vector<char> used_since_sync_;  // find_unused: got a gradient in a no_sync micro-step
   std::vector<int64_t> unused_list_;
+  // static_graph: frozen after the first synchronised backward
+  bool static_frozen_ = false;
+  std::vector<int64_t> static_unused_;
+  std::vector<char> static_global_used_;  // empty = every parameter used somewhere
   std::vector<int64_t> ready_order_;
   bool record_order_ = true;
   int64_t iterations_ = 0;

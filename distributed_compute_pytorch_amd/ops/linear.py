@@ -129,6 +129,57 @@ def _fastest(ts: dict) -> str:
     return c
 
 
+_PRETUNE = [0]
+_TABLE_ROUND = [0]
+
+
+class pretune:
+    """Context for a tuning micro-step run before training (e.g. under
+    ``DistributedDataParallel.no_sync``, so no bucket collective is in flight):
+    each shape first met inside is measured and chosen locally, without the
+    per-shape rank agreement; on exit rank 0's whole table is published in ONE
+    store round and every rank adopts it (:func:`agree_table`). The
+    synchronised steps then find every shape decided — no autotune, and no
+    store wait, inside a backward whose bucket reductions are running."""
+
+    def __enter__(self):
+        _PRETUNE[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _PRETUNE[0] -= 1
+        if exc[0] is None and _PRETUNE[0] == 0:
+            agree_table()
+        return False
+
+
+def agree_table(timeout_s: float = 300.0) -> int:
+    """Every rank adopts rank 0's choice for each shape rank 0 has decided
+    (one blocking store round; the table is small). Shapes only this rank
+    decided keep its own choice. Returns the number of choices changed here."""
+    import json
+
+    from .. import distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return 0
+    pg = dist.get_default_group()
+    _TABLE_ROUND[0] += 1
+    k = f"dcp/linear_autotune_table/{_TABLE_ROUND[0]}"
+    if pg.rank() == 0:
+        pg.store.set(k, json.dumps(autotune_choices()).encode())
+        return 0
+    pg.store.wait([k], int(timeout_s * 1000))
+    changed = 0
+    for name, v in json.loads(bytes(pg.store.get(k)).decode()).items():
+        kind, *dims = name.split()
+        key = (kind, *(int(d) for d in dims))
+        if v in _CANDIDATES and _CHOICE.get(key) != v:
+            _CHOICE[key] = v
+            changed += 1
+    return changed
+
+
 def _pick(key, cands: dict) -> str:
     """The kernel to run for ``key`` among ``cands`` (name -> zero-argument
     launch): the measured fastest (rank 0's measurement when a process group is
@@ -142,7 +193,7 @@ def _pick(key, cands: dict) -> str:
     with torch.no_grad():
         ts = _measure(cands)
     _TIMES[key] = ts
-    c = _CHOICE[key] = _agree(key, _fastest(ts))
+    c = _CHOICE[key] = _fastest(ts) if _PRETUNE[0] else _agree(key, _fastest(ts))
     return c
 
 
@@ -291,6 +342,21 @@ _DEFER = [0]
 _PENDING: dict = {}  # id(first parameter of the group) -> _Pending
 _PENDING_B: dict = {}  # id(bias) -> (bias, [dY segments]): bias gradients deferred the same way
 _HOOKED = [False]
+# ids of the parameters whose Linear ran in the current synchronising forward
+# (their backward consumes the pending segments); see flush_unclaimed
+_CLAIMED: set = set()
+# DDPs with defer_accum_wgrad over more than one rank: a flush at the
+# optimizer step (after the all-reduce) would add unreduced contributions
+_MULTI_RANK_DEFER = [0]
+
+
+def _claim(params) -> None:
+    """Forward of a Linear outside no_sync deferral: its backward will take
+    any pending segments of ``params`` into the synchronised gradient."""
+    if (_PENDING or _PENDING_B) and not _DEFER[0]:
+        for p in params:
+            if p is not None:
+                _CLAIMED.add(id(p))
 
 
 class _Pending:
@@ -328,7 +394,7 @@ def _install_flush_hook():
     if not _HOOKED[0]:
         from torch.optim.optimizer import register_optimizer_step_pre_hook
 
-        register_optimizer_step_pre_hook(lambda opt, args, kwargs: flush_weight_grads())
+        register_optimizer_step_pre_hook(lambda opt, args, kwargs: flush_weight_grads(_at_step=True))
         _HOOKED[0] = True
 
 
@@ -350,30 +416,70 @@ def _colsum_sum(segs, tgt):
     return db
 
 
-def flush_weight_grads() -> None:
+def _flush_bias(b, segs) -> None:
+    db = _colsum_sum(segs, None)
+    with torch.no_grad():
+        db = db.view(b.shape).to(b.dtype)
+        if b.grad is None:
+            b.grad = db
+        else:
+            b.grad.add_(db)
+
+
+def _flush_weight(e) -> None:
+    dw = _wgrad_sum(e.segs, None)
+    parts = dw.split(e.rows, 0) if e.rows else (dw,)
+    with torch.no_grad():
+        for p, d in zip(e.params, parts):
+            d = d.view(p.shape).to(p.dtype)
+            if p.grad is None:
+                p.grad = d
+            else:
+                p.grad.add_(d)
+
+
+def flush_weight_grads(_at_step: bool = False) -> None:
     """Add every deferred micro-step weight / bias gradient into its
     parameters' ``.grad`` (creating it where None). Called by every optimizer
     step."""
+    if _at_step and (_PENDING or _PENDING_B) and _MULTI_RANK_DEFER[0]:
+        import warnings
+
+        warnings.warn("deferred micro-step weight gradients flushed at the optimizer step, after the DDP "
+                      "all-reduce: these contributions are local to this rank (was a no_sync accumulation "
+                      "round not closed by a synchronised backward through the same Linears?)",
+                      RuntimeWarning, stacklevel=3)
     while _PENDING_B:
-        _, (b, segs) = _PENDING_B.popitem()
-        db = _colsum_sum(segs, None)
-        with torch.no_grad():
-            db = db.view(b.shape).to(b.dtype)
-            if b.grad is None:
-                b.grad = db
-            else:
-                b.grad.add_(db)
+        _flush_bias(*_PENDING_B.popitem()[1])
     while _PENDING:
-        _, e = _PENDING.popitem()
-        dw = _wgrad_sum(e.segs, None)
-        parts = dw.split(e.rows, 0) if e.rows else (dw,)
-        with torch.no_grad():
-            for p, d in zip(e.params, parts):
-                d = d.view(p.shape).to(p.dtype)
-                if p.grad is None:
-                    p.grad = d
-                else:
-                    p.grad.add_(d)
+        _flush_weight(_PENDING.popitem()[1])
+    _CLAIMED.clear()
+
+
+def flush_unclaimed(params=None) -> list:
+    """After a synchronising forward: add into ``.grad`` — before the
+    backward, so the bucket reductions cover them — the pending segments of
+    every Linear (among ``params``; all when None) that did NOT run in that
+    forward and so would never consume them. Torch DDP reduces the whole
+    accumulated ``.grad``; without this, such contributions would reach
+    ``.grad`` only at the optimizer step, unreduced (replicas diverge).
+    Returns the parameters whose ``.grad`` received something."""
+    done = []
+    if not (_PENDING or _PENDING_B):
+        _CLAIMED.clear()
+        return done
+    ids = None if params is None else {id(p) for p in params}
+    for k in [k for k, e in _PENDING.items()
+              if not any(id(p) in _CLAIMED for p in e.params) and (ids is None or id(e.params[0]) in ids)]:
+        e = _PENDING.pop(k)
+        _flush_weight(e)
+        done.extend(e.params)
+    for k in [k for k, (b, _) in _PENDING_B.items() if k not in _CLAIMED and (ids is None or k in ids)]:
+        b, segs = _PENDING_B.pop(k)
+        _flush_bias(b, segs)
+        done.append(b)
+    _CLAIMED.clear()
+    return done
 
 
 def discard_weight_grads(params=None) -> None:
@@ -396,12 +502,12 @@ def _deferred_bias(ctx, bias, g2):
     deferral keep dY (already kept for the weight gradient) instead of a
     column-sum launch per micro-step; the synchronising micro-step sums the
     rows of all of them in one launch (``_C.colsum_multi``)."""
-    if (bias is None or not bias.is_leaf or not g2.is_cuda or g2.shape[0] == 0 or g2.shape[1] % 8 != 0
+    if (bias is None or not bias.is_leaf or not g2.is_cuda or g2.shape[1] % 8 != 0
             or not g2.is_contiguous()):
         return False, None
     key = id(bias)
     if getattr(ctx, "defer", False):
-        if not _engine_accumulates(bias):
+        if g2.shape[0] == 0 or not _engine_accumulates(bias):
             return False, None
         _PENDING_B.setdefault(key, (bias, []))[1].append(g2)
         return True, None
@@ -409,7 +515,7 @@ def _deferred_bias(ctx, bias, g2):
     if e is None:
         return False, None
     tgt = _acc_target(ctx, bias, torch.Size((g2.shape[1],)))
-    db = _colsum_sum(e[1] + [g2], tgt)
+    db = _colsum_sum(e[1] + ([g2] if g2.shape[0] else []), tgt)
     return True, (None if tgt is not None else db)
 
 
@@ -425,7 +531,7 @@ def _deferred_wgrad(ctx, g2, x2):
         return False, None
     key = id(params[0])
     if getattr(ctx, "defer", False):
-        if not _engine_accumulates(params[0]):
+        if g2.shape[0] == 0 or not _engine_accumulates(params[0]):
             return False, None
         e = _PENDING.get(key)
         if e is None:
@@ -435,7 +541,7 @@ def _deferred_wgrad(ctx, g2, x2):
     e = _PENDING.pop(key, None)
     if e is None:
         return False, None
-    segs = e.segs + [(g2, x2.contiguous())]
+    segs = e.segs + ([(g2, x2.contiguous())] if g2.shape[0] else [])  # (an empty micro-batch adds nothing)
     tgt = _acc_target(ctx, params[0], torch.Size((g2.shape[1], x2.shape[1]))) if len(params) == 1 else None
     dw = _wgrad_sum(segs, tgt)
     return True, (None if tgt is not None else dw)
@@ -531,6 +637,7 @@ def _setup(ctx, x, weight, bias, w16, b16):
     ctx.wdtype = weight.dtype
     ctx.accum = accumulating()
     ctx.defer = deferring()
+    _claim((weight, bias))
     ctx.bdtype = bias.dtype if bias is not None else None
     ctx.params = (weight, bias)
     return x, w, b
@@ -567,7 +674,7 @@ def _linear_backward(ctx, g2, x, w, db=None, db_done=False, wt=None):
     weight, bias = ctx.params
     if ctx.needs_input_grad[1]:
         done = False
-        if g2.shape[0] > 0 and g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
+        if g2.shape[1] % 64 == 0 and x2.shape[1] % 64 == 0:
             done, dw = _deferred_wgrad(ctx, g2, x2)
         if done:
             pass
@@ -956,6 +1063,7 @@ class _MLPFn(torch.autograd.Function):
         ctx.tanh = tanh
         ctx.accum = accumulating()
         ctx.defer = deferring()
+        _claim((w1, b1, w2, b2))
         ctx.wdtypes = (w1.dtype, w2.dtype)
         ctx.bdtypes = (b1.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)

@@ -291,7 +291,8 @@ class Adam(_DropsDeferred, Optimizer):
             grads, sig = _adam_sig(plist)
             pkey = (gi, id(group), None if ids is None else tuple(id(p) for p in plist), cap_mode, ams)
             plan = plans.get(pkey)
-            if plan is None or plan.sig != sig or plan.state is not self.state or capturing or _NO_PLAN:
+            if (plan is None or plan.sig != sig or plan.state is not self.state or capturing or _NO_PLAN
+                    or not plan.counters_live()):
                 plan = self._adam_plan(plist, grads, cap_mode, ams, capturing)
                 plan.sig = sig
                 if plan.cacheable and not capturing:
@@ -366,6 +367,7 @@ class Adam(_DropsDeferred, Optimizer):
             plan.flat = torch.tensor([float(st["step"]) for st in cpu], dtype=torch.float32)
             for j, st in enumerate(cpu):
                 st["step"] = plan.flat[j]
+            plan.cpu = [(st, st["step"]) for st in cpu]
         vals = plan.flat.tolist() if cpu else []
         buckets = {}
         j = 0
@@ -408,10 +410,19 @@ class _AdamBucket:
 
 
 class _AdamPlan:
-    __slots__ = ("sig", "state", "flat", "buckets", "cacheable")
+    __slots__ = ("sig", "state", "flat", "buckets", "cacheable", "cpu")
 
     def __init__(self):
-        self.sig, self.state, self.flat, self.buckets, self.cacheable = None, None, None, [], True
+        self.sig, self.state, self.flat, self.buckets, self.cacheable, self.cpu = None, None, None, [], True, []
+
+    def counters_live(self) -> bool:
+        """True while every host-side 'step' of the plan is still its own view
+        of ``flat``. Plans over overlapping parameter sets (the whole group and
+        the overlap chunks of ``DistributedDataParallel(overlap_optimizer=True)``)
+        each re-point the counters to their own flat tensor when built; a plan
+        whose counters another plan took over is stale and must be rebuilt
+        (from the current values), or it would advance its own copy."""
+        return all(st.get("step") is v for st, v in self.cpu)
 
 
 def _adam_sig(plist):

@@ -170,6 +170,13 @@ class CoalescedBroadcaster:
             if recv:
                 unpack(flat, self._views(idx, flat))
 
+    def discard(self):
+        """Keep the pending broadcast (every rank still completes the same
+        collectives in :meth:`finish`), but do not unpack its result: no tensor
+        is overwritten with the values it carries."""
+        works, _ = self._pending
+        self._pending = (works, False)
+
     def __call__(self, pg, src: int = 0):
         self.start(pg, src)
         self.finish()

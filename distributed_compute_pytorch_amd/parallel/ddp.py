@@ -27,6 +27,7 @@ the pack launch).
 from __future__ import annotations
 
 import contextlib
+import warnings
 from typing import Any, Callable, List, Optional
 
 import torch
@@ -169,7 +170,16 @@ class DistributedDataParallel(nn.Module):
         super().__init__()
         self.module = module
         self.process_group = process_group if process_group is not None else dist.get_default_group()
+        if check_reduction:
+            # torch deprecated and ignores it; so do we, but not silently
+            warnings.warn("DistributedDataParallel: check_reduction is deprecated and has no effect (as in torch)",
+                          FutureWarning, stacklevel=2)
+        if not isinstance(dim, int) or isinstance(dim, bool):
+            raise TypeError(f"DistributedDataParallel: dim must be an int, got {dim!r}")
         self.device_ids = device_ids
+        # the input scatter dimension of torch's multi-device mode; a module
+        # lives on ONE device here (one process per GPU), where torch does not
+        # scatter either, so dim has no effect beyond this validation
         self.dim = dim
         self.broadcast_buffers = broadcast_buffers
         self.find_unused_parameters = find_unused_parameters
@@ -195,6 +205,21 @@ class DistributedDataParallel(nn.Module):
         if len(devs) != 1:
             raise ValueError(f"DistributedDataParallel expects the module on one device, found {devs}")
         self.device = next(iter(devs))
+        if device_ids is not None:
+            if len(device_ids) != 1:
+                raise ValueError("DistributedDataParallel: one process per device — device_ids must hold exactly "
+                                 f"one device, got {device_ids!r}")
+            if self.device.type != "cuda" or torch.device("cuda", _dev_index(device_ids[0])) != self.device:
+                raise ValueError(f"DistributedDataParallel: device_ids={device_ids!r} but the module's parameters "
+                                 f"are on {self.device}")
+        if output_device is not None:
+            od = torch.device("cuda", output_device) if isinstance(output_device, int) else torch.device(output_device)
+            if od.type == "cuda" and od.index is None:
+                od = torch.device("cuda", torch.cuda.current_device())
+            if od != self.device:
+                raise ValueError(f"DistributedDataParallel: output_device={output_device!r} differs from the module's "
+                                 f"device {self.device}; single-device modules return outputs where they are")
+        self.output_device = output_device
         self._params = params
         self._buffers_list = [b for b in module.buffers()]
 
@@ -212,6 +237,19 @@ class DistributedDataParallel(nn.Module):
         # outside a forward (then call sync_buffers() first). Off: the
         # broadcast runs at the start of the forward, as torch's does.
         self.overlap_buffer_sync = bool(overlap_buffer_sync)
+        if self._buffer_bcast is not None:
+            # buffers replaced by load_state_dict (e.g. on resume) must not be
+            # overwritten by the broadcast of rank 0's pre-load values still in
+            # flight: its result is dropped (the collective itself still
+            # completes on every rank, so ranks that did not load stay in step)
+            me_ = _weakref.ref(self)
+
+            def _loaded(_module, _keys):
+                d = me_()
+                if d is not None and d._buffer_bcast.pending:
+                    d._buffer_bcast.discard()
+
+            module.register_load_state_dict_post_hook(_loaded)
 
         # Initial plan: registration order, [first, cap] limits, then reversed so
         # the bucket holding the last-defined parameters (ready first) is bucket 0.
@@ -224,7 +262,13 @@ class DistributedDataParallel(nn.Module):
         plan = _C.split_tail_bucket(plan, sizes, self.tail_bucket_bytes)
         opts = _C.ReducerOptions()
         opts.gradient_as_bucket_view = gradient_as_bucket_view
-        opts.find_unused_parameters = find_unused_parameters
+        # static_graph (torch's flag): the used-parameter set of the first
+        # synchronised backward is reused every iteration — unused parameters
+        # are handled without find_unused_parameters' per-step traversal and
+        # used-map collective (reducer.cpp "static_graph"). The graph must not
+        # change between iterations (as in torch).
+        opts.find_unused_parameters = find_unused_parameters or static_graph
+        opts.static_graph = bool(static_graph)
         opts.rebuild_buckets = rebuild_buckets
         opts.first_bucket_bytes = self.first_bucket_bytes
         opts.bucket_bytes_cap = self.bucket_bytes_cap
@@ -244,6 +288,8 @@ class DistributedDataParallel(nn.Module):
         # (the gradients ARE the bucket buffers); anything else reading .grad
         # between backward and step must call wait_gradients() first.
         self.overlap_optimizer = bool(overlap_optimizer) and gradient_as_bucket_view and not find_unused_parameters
+        # (static_graph: deferred from the second iteration on, when every
+        # parameter was used somewhere in the first)
         opts.defer_grad_wait = self.overlap_optimizer
         # defer_accum_wgrad: under no_sync the Linear weight gradients of the
         # micro-steps are not computed one by one; the synchronising micro-step
@@ -251,6 +297,10 @@ class DistributedDataParallel(nn.Module):
         # "micro-step weight-gradient deferral"). p.grad of those weights lacks
         # the no_sync contributions until that backward or an optimizer step.
         self.defer_accum_wgrad = bool(defer_accum_wgrad)
+        if self.defer_accum_wgrad and self.process_group.size() > 1:
+            from ..ops import linear as _lin
+
+            _lin._MULTI_RANK_DEFER[0] += 1
         self._comm = pg.comm_for(params[0])
         self.reducer = _C.Reducer(params, plan, self._comm, opts)
         self._comm_hook = None
@@ -291,14 +341,28 @@ class DistributedDataParallel(nn.Module):
                 self._buffer_bcast.finish()
             elif self.require_forward_param_sync:
                 self._buffer_bcast(self.process_group, 0)
+        if self.device_ids is not None:
+            # torch moves the inputs to device_ids[0] (main.py passes them there already)
+            inputs, kwargs = _to_device(inputs, self.device), _to_device(kwargs, self.device)
         out = self.module(*inputs, **kwargs)
         if grad and self.require_backward_grad_sync:
+            if self.defer_accum_wgrad:
+                # pending no_sync segments this forward's Linears will not
+                # consume go into .grad now, inside the bucket reduction
+                from ..ops.linear import flush_unclaimed
+
+                flushed = flush_unclaimed(self._params)
+                if flushed and (self.find_unused_parameters or self.static_graph):
+                    # used in this accumulation round, even if not in this backward
+                    pos = self.__dict__.setdefault("_pos", {id(p): i for i, p in enumerate(self._params)})
+                    self.reducer.note_used([pos[id(p)] for p in flushed if id(p) in pos])
             self.require_forward_param_sync = True
             if bufs and self.overlap_buffer_sync and not (self.device.type == "cuda"
                                                            and torch.cuda.is_current_stream_capturing()):
                 self._buffer_bcast.start(self.process_group, 0)
                 _BUFFER_SYNCS.add(self)
-            outs = _tensors_in(out) if self.find_unused_parameters else []
+            traverse = self.find_unused_parameters or (self.static_graph and not self.reducer.static_frozen)
+            outs = _tensors_in(out) if traverse else []
             self.reducer.prepare_for_backward(outs, True)
         else:
             self.require_forward_param_sync = False
@@ -345,6 +409,14 @@ class DistributedDataParallel(nn.Module):
         if self._buffer_bcast.pending:
             self._buffer_bcast.finish()
         self._buffer_bcast(self.process_group, 0)
+
+    def set_comm_timing(self, on: bool) -> None:
+        """Device-time instrumentation of the bucket collectives (what
+        ``DCP_COMM_TIMING=1`` turns on at construction) from the next
+        backward on: ``ddp_logging_data()``'s bucket_comm_ms /
+        bucket_ready_dev_ms / exposed_comm_ms."""
+        self._comm.set_timing(bool(on))
+        self.reducer.set_timing(bool(on))
 
     def wait_gradients(self) -> None:
         """overlap_optimizer: order the current stream behind every bucket
@@ -422,6 +494,26 @@ def _install_step_sync_hook():
 
     register_optimizer_step_pre_hook(hook)
     _STEP_HOOK[0] = True
+
+
+def _dev_index(d) -> int:
+    if isinstance(d, int):
+        return d
+    d = torch.device(d)
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
+def _to_device(obj, device):
+    """``obj`` with every tensor in it (through tuples, lists and dicts) on ``device``."""
+    if isinstance(obj, torch.Tensor):
+        return obj if obj.device == device else obj.to(device, non_blocking=True)
+    if isinstance(obj, tuple) and hasattr(obj, "_fields"):  # namedtuple
+        return type(obj)(*(_to_device(o, device) for o in obj))
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_device(o, device) for o in obj)
+    if isinstance(obj, dict):
+        return type(obj)((k, _to_device(v, device)) for k, v in obj.items())
+    return obj
 
 
 def _tensors_in(obj):

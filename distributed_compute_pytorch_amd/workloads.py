@@ -163,6 +163,29 @@ def make_step(wl: Workload, ddp, opt, device_type: str = "cuda", graph: bool = F
     return lambda: captured(*next_flat())
 
 
+def pretune_step(wl: Workload, ddp, opt, device_type: str = "cuda") -> bool:
+    """One untimed micro-step under ``no_sync`` inside :class:`ops.linear.pretune`
+    (transformer workloads): every Linear / LM-head GEMM shape is autotuned
+    with no bucket collective in flight, and rank 0's table is adopted by all
+    ranks in one store round. The gradients it produced are dropped. False
+    (nothing run) when the model has no autotuned GEMMs or no ``no_sync``."""
+    from .ops import linear as _lin
+
+    if not (_lin._AUTOTUNE and hasattr(ddp, "no_sync")
+            and any(isinstance(m, _lin.FusedLinear) for m in wl.model.modules())):
+        return False
+    batch = list(next(wl.data))
+    with _lin.pretune(), ddp.no_sync():
+        with torch.autocast(device_type, dtype=torch.bfloat16, enabled=wl.amp):
+            loss = wl.loss_fn(ddp, batch)
+        loss.backward()
+    _lin.discard_weight_grads()
+    opt.zero_grad(set_to_none=True)
+    for p in wl.model.parameters():
+        p.grad = None
+    return True
+
+
 class _Null:
     def __enter__(self):
         return self

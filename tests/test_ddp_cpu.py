@@ -433,3 +433,98 @@ def _buffer_sync(rank, world, overlap):
 @pytest.mark.parametrize("overlap", [True, False])
 def test_buffer_broadcast_matches_torch(overlap):
     run_world(_buffer_sync, 2, overlap)
+
+
+def _static_graph(rank, world):
+    """static_graph=True (torch's flag): a branch unused on every iteration is
+    handled without find_unused_parameters — same gradients as torch DDP
+    (static_graph=True) over several iterations; from the second iteration on
+    the used map is reused (no graph traversal, no used-map collective)."""
+    import distributed_compute_pytorch_amd as dcp
+
+    tdist = _init_torch_pg(rank, world)
+    torch.manual_seed(0)
+    m = _Branchy()
+    m_ref = copy.deepcopy(m)
+    ours = dcp.parallel.DistributedDataParallel(m, static_graph=True)
+    ref = nn.parallel.DistributedDataParallel(m_ref, static_graph=True)
+    o1 = dcp.optim.SGD(ours.parameters(), lr=0.1)
+    o2 = torch.optim.SGD(ref.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(7 + rank)
+    ops0 = None
+    for it in range(4):
+        x = torch.randn(4, 8, generator=g)
+        for model, opt in ((ours, o1), (ref, o2)):
+            opt.zero_grad()
+            model(x, use_b=False).sum().backward()
+            opt.step()
+        assert ours.reducer.static_frozen
+        if it == 1:
+            ops0 = ours._comm.ops_issued
+        elif it == 2:
+            # frozen: one bucket collective per bucket, no used-map all-reduce
+            assert ours._comm.ops_issued - ops0 == len(ours.bucket_sizes())
+    for (n, p), q in zip(m_ref.named_parameters(), m.parameters()):
+        torch.testing.assert_close(q, p, rtol=1e-5, atol=1e-6, msg=n)
+    tdist.destroy_process_group()
+
+
+def test_static_graph_matches_torch():
+    run_world(_static_graph, 2)
+
+
+def _arg_validation(rank, world):
+    import warnings
+
+    import distributed_compute_pytorch_amd as dcp
+
+    m = _Branchy()
+    with pytest.raises(ValueError, match="device_ids"):
+        dcp.parallel.DistributedDataParallel(m, device_ids=[0])  # CPU module
+    with pytest.raises(ValueError, match="output_device"):
+        dcp.parallel.DistributedDataParallel(m, output_device="cuda:0")
+    with pytest.raises(TypeError, match="dim"):
+        dcp.parallel.DistributedDataParallel(m, dim="0")
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        dcp.parallel.DistributedDataParallel(m, check_reduction=True, find_unused_parameters=True)
+    assert any("check_reduction" in str(x.message) for x in w)
+    ddp = dcp.parallel.DistributedDataParallel(m, output_device="cpu", find_unused_parameters=True)
+    assert ddp.output_device == "cpu"
+
+
+def test_ddp_argument_validation():
+    """The constructor arguments torch accepts either act or are rejected —
+    none is silently stored and ignored."""
+    run_world(_arg_validation, 2)
+
+
+def _buffer_load(rank, world):
+    """overlap_buffer_sync: a load_state_dict between two forwards (resume) is
+    not overwritten by the broadcast of rank 0's pre-load buffers still in
+    flight; the collective count stays the same on every rank."""
+    import distributed_compute_pytorch_amd as dcp
+
+    torch.manual_seed(0)
+    m = _BNNet()
+    ddp = dcp.parallel.DistributedDataParallel(m, overlap_buffer_sync=True)
+    x = torch.randn(6, 1, 12, 12) * (1 + rank)
+    y = torch.randint(0, 10, (6,))
+    F.nll_loss(ddp(x), y).backward()
+    assert ddp._buffer_bcast.pending
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    for k in sd:
+        if k.endswith("running_mean"):
+            sd[k].fill_(3.0)  # the "checkpoint" every rank loads
+    m.load_state_dict(sd)
+    ddp.eval()
+    with torch.no_grad():
+        ddp(x)
+    for k, v in m.state_dict().items():
+        if k.endswith("running_mean"):
+            assert torch.all(v == 3.0), k
+    ddp.sync_buffers()  # still in step: one more collective on both ranks
+
+
+def test_load_state_dict_not_overwritten_by_pending_broadcast():
+    run_world(_buffer_load, 2)

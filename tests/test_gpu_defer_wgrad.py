@@ -169,3 +169,68 @@ def test_zero_grad_drops_deferred(pg, cuda, no_autotune):
     torch.cuda.synchronize()
     for (name, a), b in zip(m_ref.named_parameters(), m.parameters()):
         assert _rel(b.grad, a.grad) < 1e-4, (name, _rel(b.grad, a.grad))
+
+
+class _TwoBranch(torch.nn.Module):
+    """Linear ``a`` always runs; ``b`` only when asked (a branch the
+    synchronising micro-step may skip)."""
+
+    def __init__(self):
+        super().__init__()
+        from distributed_compute_pytorch_amd.ops.linear import FusedLinear
+
+        self.a = FusedLinear(256, 512)
+        self.b = FusedLinear(256, 512)
+
+    def forward(self, x, use_b=True):
+        y = self.a(x).float().square().sum() * 1e-4  # (sum: an empty micro-batch gives 0, not NaN)
+        if use_b:
+            y = y + self.b(x).float().square().sum() * 1e-4
+        return y
+
+
+def _two_branch_grads(base, xs, use_b, defer):
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.ops import linear as lin
+
+    m = copy.deepcopy(base)
+    ddp = dcp.parallel.DistributedDataParallel(m, device_ids=[0], gradient_as_bucket_view=True,
+                                               find_unused_parameters=True, defer_accum_wgrad=defer)
+    for k, (x, ub) in enumerate(zip(xs, use_b)):
+        with (contextlib.nullcontext() if k == len(xs) - 1 else ddp.no_sync()):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = ddp(x, ub)
+            loss.backward()
+    torch.cuda.synchronize()
+    # right after the synchronised backward (no optimizer step): nothing may
+    # be left for a post-reduction flush
+    assert lin.pending_weight_grads() == 0
+    return m
+
+
+def test_deferred_segments_of_skipped_linear_join_the_reduction(pg, cuda, no_autotune):
+    """a Linear that runs under no_sync but not in the synchronising
+    micro-step must have its stashed contributions in .grad before the bucket
+    reduction (not added unreduced at the optimizer step)."""
+    torch.manual_seed(3)
+    base = _TwoBranch().to(cuda)
+    xs = [torch.randn(512, 256, device=cuda) for _ in range(3)]
+    use_b = [True, True, False]
+    ref = _two_branch_grads(base, xs, use_b, False)
+    got = _two_branch_grads(base, xs, use_b, True)
+    for (name, a), b in zip(ref.named_parameters(), got.parameters()):
+        assert b.grad is not None, name
+        assert _rel(b.grad, a.grad) < 1e-4, (name, _rel(b.grad, a.grad))
+
+
+def test_deferred_segments_with_empty_sync_microbatch(pg, cuda, no_autotune):
+    """An empty synchronising micro-batch still consumes the stashed segments."""
+    torch.manual_seed(4)
+    base = _TwoBranch().to(cuda)
+    xs = [torch.randn(384, 256, device=cuda), torch.randn(640, 256, device=cuda), torch.randn(0, 256, device=cuda)]
+    use_b = [True, True, True]
+    ref = _two_branch_grads(base, xs, use_b, False)
+    got = _two_branch_grads(base, xs, use_b, True)
+    for (name, a), b in zip(ref.named_parameters(), got.parameters()):
+        assert b.grad is not None, name
+        assert _rel(b.grad, a.grad) < 1e-4, (name, _rel(b.grad, a.grad))

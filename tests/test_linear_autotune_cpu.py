@@ -80,3 +80,40 @@ def test_near_ties_go_to_our_kernels(monkeypatch):
     assert lin._pick(("fwd", 1, 2, 4), _cands([])) == "hipblaslt"
     times.update(pp=0.9, ring=1.2, hipblaslt=1.0)
     assert lin._pick(("fwd", 1, 2, 5), _cands([])) == "pp"
+
+
+def _pretune_world(rank, world):
+    """ops.linear.pretune: inside, every rank decides each shape from its own
+    measurement (no per-shape store key, no wait); on exit rank 0's table is
+    adopted by every rank in one store round — shapes only this rank met keep
+    the local choice."""
+    from distributed_compute_pytorch_amd import distributed as dist
+
+    lin._CHOICE.clear()
+    lin._AUTOTUNE = True
+    fastest = "pp" if rank == 0 else "ring"
+    # a fake measurement: this rank's favourite wins by 30 %
+    lin._measure = lambda cands, rounds=3: {k: (1.0 if k == fastest else 1.3) for k in cands}
+    import torch
+
+    torch.cuda.is_current_stream_capturing = lambda: False  # (no device in this process)
+    with lin.pretune():
+        assert lin._pick(("fwd", 64, 64, 64), _cands([])) == fastest
+        assert lin._pick(("dgrad", 64, 64, 64), _cands([])) == fastest
+        if rank == 1:
+            assert lin._pick(("fwd", 32, 64, 64), _cands([])) == "ring"
+    pg = dist.get_default_group()
+    assert not pg.store.check(["dcp/linear_autotune/fwd 64 64 64"])  # no per-shape agreement ran
+    assert lin._CHOICE[("fwd", 64, 64, 64)] == "pp"
+    assert lin._CHOICE[("dgrad", 64, 64, 64)] == "pp"
+    if rank == 1:
+        assert lin._CHOICE[("fwd", 32, 64, 64)] == "ring"
+    # later steps find the shapes decided: _pick returns without measuring
+    lin._measure = None
+    assert lin._pick(("fwd", 64, 64, 64), _cands([])) == "pp"
+
+
+def test_pretune_table_adopted_from_rank0():
+    from mp_util import run_world
+
+    run_world(_pretune_world, 2)

@@ -103,3 +103,36 @@ def test_fused_adam_shadow_list_cpu():
     for p, r, s in zip(ps, ref, sh):
         torch.testing.assert_close(p, r.detach(), rtol=1e-6, atol=1e-6)
         assert torch.equal(s, p.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("name", ["Adam", "AdamW"])
+def test_adam_mixed_chunked_and_full_steps(name):
+    """Overlap-mode steps (one chunk per deferred bucket: ``_step(ids)``) mixed
+    with whole-group steps (``_step(None)``) keep one step counter per
+    parameter: the cached plans of both kinds cover the same parameters, and
+    a plan whose counters the other took over is rebuilt, not reused stale."""
+    g = torch.Generator().manual_seed(1)
+    base = [torch.randn(s, generator=g) for s in SHAPES]
+    p1 = [b.clone().requires_grad_() for b in base]
+    p2 = [b.clone().requires_grad_() for b in base]
+    o1, o2 = getattr(torch.optim, name)(p1, lr=0.01), getattr(dcp.optim, name)(p2, lr=0.01)
+    ids_a = {id(p) for p in p2[:2]}
+    ids_b = {id(p) for p in p2[2:]}
+    pattern = [None, "chunks", "chunks", "chunks", None, "chunks", None, None]
+    for b in p2:  # fixed gradient addresses, as DDP's bucket views are
+        b.grad = torch.zeros_like(b)
+    for kind in pattern:
+        grads = [torch.randn(s, generator=g) for s in SHAPES]
+        for a, b, gr in zip(p1, p2, grads):
+            a.grad = gr.clone()
+            b.grad.copy_(gr)
+        o1.step()
+        with torch.no_grad():
+            if kind is None:
+                o2._step(None, 1.0)
+            else:
+                o2._step(ids_a, 1.0)
+                o2._step(ids_b, 1.0)
+    for a, b in zip(p1, p2):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+        assert float(o2.state[b]["step"]) == float(o1.state[a]["step"]) == len(pattern)
