@@ -353,7 +353,7 @@ def main():
         total = samples_per_step * a.steps / elapsed
         rec = None
         diag = None
-        if ours and world > 1 and not a.comm_timing and not a.graph:
+        if ours and (world > 1 or a.emulate_world) and not a.comm_timing and not a.graph:
             # untimed diagnostic steps with device comm timing on: whether
             # overlap held (exposed vs per-bucket comm ms), as a multi-GPU run
             # record must be able to explain itself; MAX over ranks
