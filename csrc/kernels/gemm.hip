@@ -106,6 +106,19 @@ __device__ __forceinline__ bf16x8 bn_act_frag(bf16x8 v, const float (&sc)[8], co
   return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
 }
 
+// The BN prologue on a wave's FM A fragments of one 32-k half: the lane's 8
+// channels' (scale, shift) from the LDS table (two 16-B reads each, the same
+// address for the 16 lanes of a chunk: broadcast), then bn_act_frag
+template <int FM>
+__device__ __forceinline__ void pro_frags(bf16x8 (&xf)[FM], const float* sc_p, const float* sf_p, bool relu) {
+  const float4 a0 = *reinterpret_cast<const float4*>(sc_p), a1 = *reinterpret_cast<const float4*>(sc_p + 4);
+  const float4 b0 = *reinterpret_cast<const float4*>(sf_p), b1 = *reinterpret_cast<const float4*>(sf_p + 4);
+  const float sc[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  const float sf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+  for (int j = 0; j < FM; ++j) xf[j] = bn_act_frag(xf[j], sc, sf, relu);
+}
+
 // relu(x*sc + sf + r) on one 8 x bf16 fragment — a block boundary's BN3 +
 // residual add + ReLU (gemm_nt RES prologue; the same fp32 expression as
 // batchnorm.hip's bn_apply_kernel, so y is bit-identical) — and its ReLU mask
@@ -639,7 +652,9 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
   // kNSnt-2 later stages and the epilogue stores of stages nq-kNSnt…nq-2
   // (the epilogue of stage nq-1 comes after this barrier): hist bit i = stage
   // nq-2-i ended a tile.
-  constexpr bool PIPE = NS == 0 && BK == 64 && !PRO;
+  // (PRO: the BN prologue is applied to the A fragments in registers between
+  // their LDS read and their MFMAs — gemm_tune "pro_pipe")
+  constexpr bool PIPE = NS == 0 && BK == 64 && !RES;
   uint32_t hist = 0;
   auto pipe_wait = [&](int nq) {
     if (nq + kNSnt - 2 < T) {
@@ -665,6 +680,8 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
     if constexpr (PIPE) {
       const char* sA = lds + slot * STAGE;
       nt_read_frags<FM, FN, RB, BK, WR, WN>(sA, sA + SA, 4 + ck, wm, wn, lane, px1, pw1);
+      const int pk = kt * BK + ck * 8;  // PRO: first channel of this lane's A chunk (first half)
+      if constexpr (PRO) pro_frags<FM>(px0, pro + pk, pro + K + pk, relu != 0);
       nt_mfma<FM, FN>(acc, px0, pw0);
       if (q + 1 < T) {
         // this wave's reads of slot q have landed (the DMA issued after the
@@ -678,6 +695,7 @@ __global__ void __launch_bounds__((nt_threads<BM, BN>()), (nt_threads<BM, BN>() 
       // MFMA sequence for both cases keeps the accumulators in place — two
       // branches with their own MFMAs cost a copy of every accumulator)
       const char* nA = lds + (slot + 1 == kNSnt ? 0 : slot + 1) * STAGE;
+      if constexpr (PRO) pro_frags<FM>(px1, pro + pk + 32, pro + K + pk + 32, relu != 0);
       nt_mfma_read<FM, FN, RB, BK, WR, WN>(acc, px1, pw1, nA, nA + SA, ck, wm, wn, lane, px0, pw0);
     } else {
     // vmcnt retires in issue order: the ops younger than stage q's DMA are the
@@ -1971,6 +1989,10 @@ int g_stem_wide = 1;
 int g_slab32 = 1;
 // gemm_tune "nt_deep": 1x1 forwards on the 3-slot 256 x 128 ring (gemm_nt_launch_deep): 0 off, 1 at M >= 64K, 2 always
 int g_nt_deep = 0;
+// gemm_tune "pro_pipe": the BN-prologue 1x1 GEMMs on the BK = 64 pipelined
+// stage loop (256-row tiles, one workgroup per CU; 1) instead of the BK = 32
+// three-stage ring (0)
+int g_pro_pipe = 0;
 int g_reserve_cus = [] {
   const char* v = getenv("DCP_RESERVE_CUS");
   const int r = v ? atoi(v) : 0;
@@ -1988,6 +2010,7 @@ void gemm_tune(const char* key, int value) {
   if (k == "stem_wide") g_stem_wide = value;
   if (k == "slab32") g_slab32 = value;
   if (k == "nt_deep") g_nt_deep = value;
+  if (k == "pro_pipe") g_pro_pipe = value;
   if (k == "wg_slots") g_wg_slots = value < 64 ? 64 : value;
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
@@ -2003,6 +2026,7 @@ int gemm_tune_get(const char* key) {
   if (k == "stem_wide") return g_stem_wide;
   if (k == "slab32") return g_slab32;
   if (k == "nt_deep") return g_nt_deep;
+  if (k == "pro_pipe") return g_pro_pipe;
   if (k == "wg_slots") return g_wg_slots;
   if (k == "wg_cap") return g_wg_cap;
   if (k == "reserve_cus") return g_reserve_cus;
@@ -2221,7 +2245,11 @@ void gemm_nt_launch_bk(const void* A, const void* B, void* C, int64_t M, int N, 
   }
   const int BN = N % 128 == 0 ? 128 : 64;
   const int tn = N / BN;
-  if (nt_bm(M, tn, BN, scale != nullptr, K, GATHER) == 256)
+  // the pipelined BN-prologue GEMM: 256-row tiles only (ring + staging + the
+  // coefficient table > 80 KB: one workgroup per CU, its grid sized for that)
+  if (BK == 64 && scale != nullptr && !GATHER)
+    gemm_nt_launch_bm<GATHER, BK, 256>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s, scatter2, parity);
+  else if (nt_bm(M, tn, BN, scale != nullptr, K, GATHER) == 256)
     gemm_nt_launch_bm<GATHER, BK, 256>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s, scatter2, parity);
   else
     gemm_nt_launch_bm<GATHER, BK, 128>(A, B, C, M, N, K, scale, shift, relu, stats, geo, red, s, scatter2, parity);
@@ -2242,7 +2270,7 @@ void gemm_nt_launch(const void* A, const void* B, void* C, int64_t M, int N, int
   if (!GATHER)
     g.nt_a = g_nt_a == 1 || (g_nt_a == 2 && (M * K + M * static_cast<int64_t>(N)) * 2 > (int64_t(256) << 20)) ||
              (g_nt_a == 3 && stats != nullptr && scale == nullptr && red == nullptr && K >= 1024);
-  if (nt_bk() == 64 && scale == nullptr)
+  if (nt_bk() == 64 && (scale == nullptr || (g_pro_pipe && !GATHER && K * 8 <= 24 * 1024)))
     gemm_nt_launch_bk<GATHER, 64>(A, B, C, M, N, K, scale, shift, relu, stats, g, red, s);
   else gemm_nt_launch_bk<GATHER, 32>(A, B, C, M, N, K, scale, shift, relu, stats, g, red, s);
 }

@@ -340,3 +340,43 @@ def test_conv3x3_c64_direct(cuda, n, h, w):
     wr = conv.weight.detach().clone().requires_grad_(True)
     F.conv2d(x.detach().float(), wr, None, 1, 1).backward(gy.float())
     assert conv.weight.grad.dtype == torch.float32 and _rel(conv.weight.grad, wr.grad) < 1e-3
+
+
+@pytest.fixture
+def pro_pipe():
+    """gemm_tune pro_pipe = 1: the BN-prologue GEMMs on the BK = 64 pipelined
+    stage loop (256-row tiles) instead of the BK = 32 ring."""
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    old = _C.gemm_tune_get("pro_pipe")
+    _C.gemm_tune("pro_pipe", 1)
+    yield
+    _C.gemm_tune("pro_pipe", old)
+
+
+@pytest.mark.parametrize("shape", SHAPES + [(16, 14, 14, 256, 1024), (4, 7, 7, 512, 2048)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_conv1x1_prologue_pipelined(cuda, shape, relu, pro_pipe):
+    """BN(+ReLU) prologue on the pipelined BK = 64 loop: output and the
+    Σy / Σy² epilogue against an fp32 reference of the same bf16 operand."""
+    from distributed_compute_pytorch_amd._ext import C as _C
+
+    n, h, w, ci, co = shape
+    g = torch.Generator().manual_seed(12)
+    x = _x(n, h, w, ci, cuda, g)
+    wt = (torch.randn(co, ci, generator=g) / ci ** 0.5).to(cuda).to(torch.bfloat16)
+    sc = (torch.rand(ci, generator=g) + 0.5).to(cuda)
+    sf = torch.randn(ci, generator=g).to(cuda)
+    y, st = _C.conv1x1_fwd(x, wt, sc, sf, relu, True)
+    a = x.float() * sc[None, :, None, None] + sf[None, :, None, None]
+    a = (torch.relu(a) if relu else a).to(torch.bfloat16)
+    ref = F.conv2d(a.float(), wt.float()[:, :, None, None])
+    assert _rel(y, ref) < 1e-2
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, co)
+    torch.testing.assert_close(st[:co], yf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[co:], (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
+    # bit-identical to the BK = 32 ring's prologue (same fp32 expression, same bf16 operand)
+    _C.gemm_tune("pro_pipe", 0)
+    y0, _ = _C.conv1x1_fwd(x, wt, sc, sf, relu, False)
+    _C.gemm_tune("pro_pipe", 1)
+    assert _rel(y, y0) < 1e-2

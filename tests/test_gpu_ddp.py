@@ -63,47 +63,60 @@ def test_ddp_matches_local_training(pg, cuda, grad_as_view):
 def test_resnet_grads_match_fp64_reference(pg, cuda):
     """One fp32 step: every parameter gradient through our DDP + fused BN
     against a deterministic fp64 CPU oracle of the same model, input and
-    labels. The bound is the accuracy fp32 arithmetic itself reaches on this
-    problem — the same model in fp32 on the CPU vs the oracle: the median
-    parameter within 1.25x of it, every parameter within 10x, no additive
-    slack.
-    (A random-init ResNet-50's BN gradients are sums with heavy cancellation:
-    fp32 on the CPU is ~3e-2 off the fp64 gradient at bn1 — which is why the
-    old stock-GPU-vs-ours comparison needed a noise floor: MIOpen's fp32
-    backward is not deterministic. tools/resnet_fp64_diag.py prints all three.)"""
+    labels, with the reduced-precision fp32 paths pinned off
+    (``allow_tf32 = False``).
+
+    Bounds (no additive slack): the median parameter within 1.25x of the
+    error fp32 arithmetic itself reaches on the CPU, and every parameter
+    within 5x of the worse of two fp32 references — the CPU run and stock
+    PyTorch (MIOpen convolutions + BatchNorm) on this GPU.
+    Why not a flat multiple of the CPU error (NOTES §31,
+    tools/resnet_fp64_diag.py, profiles/r6_fp64_diag_tf32*.txt): a
+    random-init ResNet-50's last-block BN gradients are sums with heavy
+    cancellation, so each fp32 run's forward rounding (1e-7 at the stem,
+    ~8e-5 at layer 4 — ours within 1.2x of stock's) is amplified 10-100x and
+    differently for every summation order: stock fp32 on this GPU is itself
+    2-4x the CPU's error there, and the run-to-run spread of both GPU runs
+    (atomic BN / MIOpen reductions) is ~2x. TF32 on or off moves none of it."""
     import copy
 
     import distributed_compute_pytorch_amd as dcp
     from distributed_compute_pytorch_amd.models import resnet50
 
-    torch.manual_seed(0)
-    cpu = resnet50(num_classes=100)
-    g = torch.Generator(device="cpu").manual_seed(0)
-    x = torch.randn(16, 3, 96, 96, generator=g)
-    y = torch.randint(0, 100, (16,), generator=g)
-    ref64 = copy.deepcopy(cpu).double()
-    l64 = F.cross_entropy(ref64(x.double()), y)
-    l64.backward()
-    ref32 = copy.deepcopy(cpu)
-    F.cross_entropy(ref32(x), y).backward()
-    model = resnet50(num_classes=100, fused_bn=True)
-    model.load_state_dict(cpu.state_dict())
-    model = model.to(cuda).to(memory_format=torch.channels_last)
-    ddp = dcp.parallel.DistributedDataParallel(model, device_ids=[0], gradient_as_bucket_view=True)
-    l2 = F.cross_entropy(ddp(x.to(cuda).contiguous(memory_format=torch.channels_last)), y.to(cuda))
-    l2.backward()
+    tf32 = torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cudnn.allow_tf32 = torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        torch.manual_seed(0)
+        cpu = resnet50(num_classes=100)
+        g = torch.Generator(device="cpu").manual_seed(0)
+        x = torch.randn(16, 3, 96, 96, generator=g)
+        y = torch.randint(0, 100, (16,), generator=g)
+        ref64 = copy.deepcopy(cpu).double()
+        l64 = F.cross_entropy(ref64(x.double()), y)
+        l64.backward()
+        ref32 = copy.deepcopy(cpu)
+        F.cross_entropy(ref32(x), y).backward()
+        xc, yc = x.to(cuda).contiguous(memory_format=torch.channels_last), y.to(cuda)
+        stock = copy.deepcopy(cpu).to(cuda).to(memory_format=torch.channels_last)
+        F.cross_entropy(stock(xc), yc).backward()
+        model = resnet50(num_classes=100, fused_bn=True)
+        model.load_state_dict(cpu.state_dict())
+        model = model.to(cuda).to(memory_format=torch.channels_last)
+        ddp = dcp.parallel.DistributedDataParallel(model, device_ids=[0], gradient_as_bucket_view=True)
+        l2 = F.cross_entropy(ddp(xc), yc)
+        l2.backward()
+    finally:
+        torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = tf32
     assert abs(float(l2) - float(l64)) < 1e-4 * abs(float(l64))
     ratios = []
-    for (n, p64), p32, q in zip(ref64.named_parameters(), ref32.parameters(), model.parameters()):
+    for (n, p64), p32, ps, q in zip(ref64.named_parameters(), ref32.parameters(), stock.parameters(),
+                                    model.parameters()):
         den = p64.grad.norm().clamp_min(1e-30)
         e32 = float((p32.grad.double() - p64.grad).norm() / den)
+        est = float((ps.grad.double().cpu() - p64.grad).norm() / den)
         ours = float((q.grad.double().cpu() - p64.grad).norm() / den)
         ratios.append(ours / max(e32, 1e-12))
-        # per parameter: within 10x of what fp32 arithmetic reaches (the GPU
-        # conv kernels run a different summation order; the last block's
-        # gradients, where fp32 itself is accurate to ~2e-3, carry the forward
-        # convolutions' rounding at ~1e-2 — NOTES §27)
-        assert ours <= 10 * e32 or ours < 1e-6, (n, ours, e32)
+        assert ours <= 5 * max(e32, est) or ours < 1e-6, (n, ours, e32, est)
     ratios.sort()
     assert ratios[len(ratios) // 2] <= 1.25, ratios[len(ratios) // 2]  # typically as accurate as fp32 on the CPU
     for (n, b64), c in zip(ref64.named_buffers(), model.buffers()):
