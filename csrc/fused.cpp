@@ -6,6 +6,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include <map>
+#include <tuple>
 #include <mutex>
 
 #include "common.h"
@@ -99,9 +100,27 @@ at::Tensor zeroed_vec(int64_t n, const at::Tensor& like, hipStream_t st) {
   (void)hipStreamIsCapturing(st, &cap);
   const int64_t need = (n + 63) / 64 * 64;  // 256-B aligned views
   static const bool off = std::getenv("DCP_NO_GRAD_SLAB") != nullptr;  // A/B switch
-  if (off || cap != hipStreamCaptureStatusNone || need > kSlab / 4)
-    return at::zeros({n}, like.options().dtype(at::kFloat));
+  if (off || need > kSlab / 4) return at::zeros({n}, like.options().dtype(at::kFloat));
   static std::mutex mu;
+  if (cap != hipStreamCaptureStatusNone) {
+    // Under capture: one slab per capture, zeroed by ONE captured fill at the
+    // first carve (every replay re-zeroes it before the step's first bias
+    // gradient) instead of one fill node per vector. The slab is held here
+    // for the graph's lifetime (a later capture starts its own).
+    unsigned long long id = 0;
+    (void)hipStreamGetCaptureInfo(st, &cap, &id);
+    static std::map<std::pair<int, hipStream_t>, std::tuple<at::Tensor, int64_t, unsigned long long>> cslabs;
+    std::lock_guard<std::mutex> g(mu);
+    auto& e = cslabs[{static_cast<int>(like.get_device()), st}];
+    if (!std::get<0>(e).defined() || std::get<2>(e) != id || std::get<1>(e) + need > kSlab) {
+      static std::vector<at::Tensor> keep;  // earlier captures' slabs: still read by their graphs
+      if (std::get<0>(e).defined()) keep.push_back(std::get<0>(e));
+      e = {at::zeros({kSlab}, like.options().dtype(at::kFloat)), 0, id};
+    }
+    at::Tensor t = std::get<0>(e).narrow(0, std::get<1>(e), n);
+    std::get<1>(e) += need;
+    return t;
+  }
   static std::map<std::pair<int, hipStream_t>, std::pair<at::Tensor, int64_t>> slabs;
   std::lock_guard<std::mutex> g(mu);
   auto& e = slabs[{static_cast<int>(like.get_device()), st}];
@@ -1713,8 +1732,20 @@ int stream_capture_status(int64_t stream_ptr) {
   return static_cast<int>(st);
 }
 
+// id of the capture a raw stream takes part in (0: not capturing)
+uint64_t stream_capture_id(int64_t stream_ptr) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  if (hipStreamGetCaptureInfo(reinterpret_cast<hipStream_t>(stream_ptr), &st, &id) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return st == hipStreamCaptureStatusActive ? static_cast<uint64_t>(id) : 0;
+}
+
 void bind(pybind11::module& m) {
   m.def("stream_capture_status", &stream_capture_status);
+  m.def("stream_capture_id", &stream_capture_id);
   m.def("abort_capture", &abort_capture, "end a dangling stream capture; true if one was open");
   m.def("eval_metrics_", &eval_metrics_);
   m.def("maxpool_supported", &maxpool_supported);

@@ -1000,7 +1000,18 @@ class LinearWeightPrep:
         capturing = torch.cuda.is_current_stream_capturing()
         versions = [w._version for w in ws]
         epoch = param_epoch()
-        if capturing or epoch != self._epoch or versions != self._versions:
+        if capturing:
+            # once per captured step: the micro-steps of a gradient-accumulation
+            # step see the same weights (the optimizer, which changes them,
+            # runs after the last one); a new capture or an optimizer step in
+            # between launches again. Each replay re-preps from the weights
+            # the previous replay's optimizer wrote.
+            ckey = (_C.stream_capture_id(torch.cuda.current_stream().cuda_stream), epoch, tuple(versions))
+            if ckey != getattr(self, "_cap_key", None):
+                _C.weight_prep_run(self.table, self.tiles)
+                self._cap_key = ckey
+            self._epoch, self._versions = epoch, versions
+        elif epoch != self._epoch or versions != self._versions:
             _C.weight_prep_run(self.table, self.tiles)
             self._epoch, self._versions = epoch, versions
 
