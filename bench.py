@@ -435,6 +435,7 @@ def main():
             }
             if wl.seq_len:
                 rec["tokens_per_s"] = round(total * wl.seq_len, 1)
+            rec["peak_mem_gib"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
             rec["vs_baseline"] = _vs_baseline(a.model, wl, world, total)
             if diag is not None:
                 rec["comm_diag"] = diag
