@@ -82,6 +82,7 @@ def autotune_choices() -> dict:
 
 # how long a rank other than 0 waits for rank 0's choice of a shape
 _AGREE_WAIT_S = 5.0
+_FELL_BACK: list = []  # shapes this rank decided alone (warned once)
 
 
 def _agree(key, mine: str) -> str:
@@ -107,6 +108,15 @@ def _agree(key, mine: str) -> str:
     try:
         pg.store.wait([k], int(_AGREE_WAIT_S * 1000))
     except (RuntimeError, TimeoutError):  # rank 0 has no entry (yet): keep the local measurement
+        if not _FELL_BACK:
+            import warnings
+
+            warnings.warn(f"rank {pg.rank()}: no rank-0 GEMM choice for {' '.join(str(x) for x in key)} within "
+                          f"{_AGREE_WAIT_S:.0f} s; using this rank's own measurement ({mine}). Ranks may now run "
+                          "different kernels for this shape (rounding differs; DDP still averages identical "
+                          "gradients). Tune before training (workloads.pretune_step / ops.linear.pretune) to "
+                          "avoid this.", RuntimeWarning, stacklevel=3)
+        _FELL_BACK.append(key)
         return mine
     theirs = bytes(pg.store.get(k)).decode()
     return theirs if theirs in _CANDIDATES else mine
