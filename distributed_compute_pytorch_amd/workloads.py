@@ -76,10 +76,15 @@ def build(name: str, device, batch: Optional[int] = None, fused: bool = True, se
 
     name = name.lower()
     if name == "resnet50":
-        # 512 per GPU: 288 GB of HBM holds it with room to spare; +6 % over 256
-        # on one MI355X and half the all-reduce bytes per sample at N > 1
-        # (tools/gpu_run79.sh, profiles/r1_resnet50_b512_pairs79.jsonl)
-        b = batch or 512
+        # 1024 per GPU (41 GiB peak of the 288 GB HBM): +4 % over 512 on one
+        # MI355X (the per-step fixed costs — optimizer, weight prep, tails of
+        # the persistent grids — amortised over twice the images, layer 3/4
+        # tiles filling more rounds; stock torch gains 3.7 %) and half the
+        # all-reduce bytes per sample at N > 1 again
+        # (profiles/r6_resnet_batch_sweep.jsonl: 512 / 768 / 1024 / 2048 =
+        # 14,033 / 14,414 / 14,629 / 15,088; round 1 chose 512 over 256,
+        # profiles/r1_resnet50_b512_pairs79.jsonl)
+        b = batch or 1024
         m = models.resnet50(fused_bn=fused, fused_gemm=fused if fused_gemm is None else (fused and fused_gemm)).to(device)
         if channels_last:
             m = m.to(memory_format=torch.channels_last)

@@ -8,7 +8,7 @@ O=$R/gpurun_out
 mkdir -p "$O"
 for b in $BATCHES; do
   for impl in $IMPLS; do
-    timeout -k 10 400 python3 -u "$R/bench.py" --impl "$impl" --batch "$b" --steps "$STEPS" --warmup 6 > "$O/${TAG}_run.log" 2>&1 || {
+    timeout -k 10 ${RUN_TIMEOUT:-400} python3 -u "$R/bench.py" --impl "$impl" --batch "$b" --steps "$STEPS" --warmup 6 > "$O/${TAG}_run.log" 2>&1 || {
       echo "[batch_sweep] b=$b $impl failed"; tail -5 "$O/${TAG}_run.log"; continue; }
     grep '^{' "$O/${TAG}_run.log" | tail -1 | python3 -c "
 import json, sys
