@@ -93,7 +93,7 @@ at::Tensor zeroed_floats(int64_t n, const at::Tensor& like, hipStream_t st) {
 // fill launch) when the current one is used up — instead of one fill launch
 // per bias. A slab is never re-zeroed, so no carved view is ever overwritten;
 // its memory goes back to the caching allocator when its last view dies.
-// Under HIP-graph capture each call gets its own zeroed tensor.
+// Under HIP-graph capture: views of a per-capture slab zeroed by one captured fill.
 at::Tensor zeroed_vec(int64_t n, const at::Tensor& like, hipStream_t st) {
   constexpr int64_t kSlab = int64_t(1) << 18;  // 1 MiB of fp32
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
