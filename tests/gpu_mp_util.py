@@ -13,7 +13,7 @@ import os
 from distributed_compute_pytorch_amd.distributed.launch import free_port, spawn
 
 
-def _entry(rank, fn, world, port, backend, torch_backend, pg_timeout_s, args):
+def _entry(rank, fn, world, port, backend, torch_backend, pg_timeout_s, args, port2=None):
     import torch
 
     ndev = torch.cuda.device_count()
@@ -30,7 +30,7 @@ def _entry(rank, fn, world, port, backend, torch_backend, pg_timeout_s, args):
         import torch.distributed as tdist
 
         kw = {"device_id": torch.device("cuda", dev)} if torch_backend == "nccl" else {}
-        tdist.init_process_group(torch_backend, init_method=f"tcp://127.0.0.1:{port + 1}", rank=rank,
+        tdist.init_process_group(torch_backend, init_method=f"tcp://127.0.0.1:{port2 or port + 1}", rank=rank,
                                  world_size=world, timeout=datetime.timedelta(seconds=120), **kw)
     try:
         fn(rank, world, torch.device("cuda", dev), *args)
@@ -42,4 +42,8 @@ def _entry(rank, fn, world, port, backend, torch_backend, pg_timeout_s, args):
 
 def run_gpu_world(fn, world, *args, backend="rccl", torch_backend=None, timeout=240, pg_timeout_s=120.0):
     port = free_port()
-    spawn(_entry, (fn, world, port, backend, torch_backend, pg_timeout_s, args), nprocs=world, timeout=timeout)
+    port2 = free_port()  # the stock torch group's own free port (port + 1 may be taken)
+    while port2 == port:
+        port2 = free_port()
+    spawn(_entry, (fn, world, port, backend, torch_backend, pg_timeout_s, args, port2), nprocs=world,
+          timeout=timeout)
