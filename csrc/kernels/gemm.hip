@@ -1970,8 +1970,11 @@ inline int nt_bm(int64_t M, int tn, int BN, bool pro, int K, bool gather) {
 // that cannot become resident because RCCL holds its CU delays its whole share
 // of tiles (NOTES §22; env DCP_RESERVE_CUS sets the initial value).
 namespace {
-// 256 x 256 tiles: 0 off, 2 on every eligible shape, 4 where they measured faster (default)
-int g_nt_big = 4;
+// 256 x 256 tiles: 0 off, 2 on every eligible shape (default since the
+// per-GPU batch of 1024: twice the M tiles per shape, +0.25-0.3 % over 4 in 4
+// interleaved pairs, profiles/r6_tune_sweep_b1024.jsonl), 4 where they measured
+// faster at batch 512
+int g_nt_big = 2;
 // Linear forward epilogues (bias / bias + GELU) on 256 x 256 tiles: 0 never,
 // 1 when the tiles fill at least two rounds of the chip, 2 whenever N % 256 == 0
 int g_lin_big = 1;
