@@ -90,7 +90,7 @@ def parse():
     ap.add_argument("--benchmark-cudnn", type=int, default=1)
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole step in a HIP graph (-1: per model — on for the launch-bound "
-                         "reference ConvNet / MLP, whose eager step is host-issue bound, off otherwise)")
+                         "reference ConvNet / MLP and for the transformers at one rank, off otherwise)")
     ap.add_argument("--backend", choices=["rccl", "gloo"], default="rccl",
                     help="gloo: the reference's literal backend (main.py:50) — GPU tensors staged through the "
                          "host; ours = the C++ host communicator, stock = torch's gloo")
@@ -192,7 +192,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.graph < 0:
-        a.graph = 1 if a.model in ("convnet", "mlp") and a.impl == "ours" and a.backend == "rccl" else 0
+        # the launch-bound reference ConvNet / MLP, and the transformers at one
+        # rank: their eager step idles the GPU between dependent kernels on a
+        # slow host (BERT 0.915 busy; captured 0.995, +4.6 % on such a box,
+        # parity on a fast one: profiles/r6_graph_ab*.jsonl, NOTES §31). At
+        # N > 1 the transformers run eager (optimizer overlap with the
+        # bucket collectives)
+        a.graph = 1 if (a.impl == "ours" and a.backend == "rccl"
+                        and (a.model in ("convnet", "mlp") or (a.model in ("gpt2", "bert") and world == 1))) else 0
     if world != a.gpus:
         log(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if a.comm_timing:

@@ -21,10 +21,37 @@ _OK = (torch.float32, torch.bfloat16)
 
 
 _COUNTER = {}
+# device index -> counters consumed so far by the step being captured inside
+# batched_offsets (None: no batching, one snapshot + advance per call)
+_BATCH = [None]
 
 
 def _capturing() -> bool:
     return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+class batched_offsets:
+    """Context wrapped around a whole captured training step
+    (``utils.graphs.CapturedStep``): the dropout calls inside read the device
+    counter itself — each call has its own host seed, frozen into the graph,
+    so calls of one replay draw independent streams — and ONE captured add at
+    the end of the step advances the counter past every counter the step
+    consumed, so the next replay draws fresh masks. Without it every call
+    snapshots and advances the counter itself: two tiny graph nodes per
+    dropout (96 per GPT-2 step, ~0.9 ms of replay time: NOTES §31)."""
+
+    def __enter__(self):
+        self._outer = _BATCH[0]
+        _BATCH[0] = {}
+        return self
+
+    def __exit__(self, *exc):
+        used, _BATCH[0] = _BATCH[0], self._outer
+        if exc[0] is None:
+            for key, n in used.items():
+                if n:
+                    _COUNTER[key].add_(n)  # captured: runs at the end of every replay
+        return False
 
 
 def _take_offset(device, n):
@@ -37,6 +64,9 @@ def _take_offset(device, n):
     base = _COUNTER.get(key)
     if base is None:
         raise RuntimeError("dropout inside a HIP-graph capture needs an eager warmup call first")
+    if _BATCH[0] is not None:
+        _BATCH[0][key] = _BATCH[0].get(key, 0) + (n + 3) // 4
+        return seed, base
     used = base.clone()
     base.add_((n + 3) // 4)
     return seed, used

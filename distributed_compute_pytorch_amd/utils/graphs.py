@@ -87,8 +87,11 @@ class CapturedStep:
         # thread_local: the communicator watchdog thread polls events while we
         # capture; in the default global mode that would invalidate the capture
         try:
+            from ..ops.dropout import batched_offsets
+
             with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
-                self.static_out = self.step_fn(*self.static_inputs)
+                with batched_offsets():  # one dropout-counter advance per replay, not two nodes per call
+                    self.static_out = self.step_fn(*self.static_inputs)
         except Exception:
             from .._ext import C as _C
 

@@ -120,6 +120,41 @@ def test_dropout_masks_fresh_per_replay(cuda):
     assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
 
 
+def test_dropout_masks_fresh_per_replay_batched(cuda):
+    """Inside ops.dropout.batched_offsets (what CapturedStep wraps a captured
+    step in): the calls read the device counter itself and one add at the end
+    advances it — every replay draws new masks, two calls of one replay draw
+    different ones, and each backward regenerates its forward's mask."""
+    from distributed_compute_pytorch_amd.ops import fused_dropout
+    from distributed_compute_pytorch_amd.ops.dropout import batched_offsets
+
+    x = torch.randn(4096, device=cuda, requires_grad=True)
+    z = torch.randn(4096, device=cuda, requires_grad=True)
+    (fused_dropout(x, 0.5).sum() + fused_dropout(z, 0.5).sum()).backward()  # eager warmup
+    x.grad = z.grad = None
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        (fused_dropout(x, 0.5).sum() + fused_dropout(z, 0.5).sum()).backward()
+    torch.cuda.current_stream().wait_stream(s)
+    x.grad = z.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        with batched_offsets():
+            y = fused_dropout(x, 0.5)
+            w = fused_dropout(z, 0.5)
+            (y.sum() + w.sum()).backward()
+    masks = []
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        m, n = y.detach() != 0, w.detach() != 0
+        assert torch.equal(x.grad != 0, m) and torch.equal(z.grad != 0, n)
+        assert not torch.equal(m, n)
+        masks.append(m.clone())
+    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+
+
 @pytest.mark.parametrize("gemm", [False, True])
 def test_captured_fwd_bwd_matches_eager(cuda, gemm):
     """Forward + backward (+ our DDP) captured in one HIP graph: loss equal to
