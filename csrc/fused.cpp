@@ -1146,6 +1146,7 @@ kern::AttnParams attn_params(const at::Tensor& q, int64_t heads, bool causal, do
   p.causal = causal;
   p.p_drop = static_cast<float>(p_drop);
   p.seed = static_cast<uint64_t>(seed);
+  p.mask = nullptr;
   return p;
 }
 void same_shape(const at::Tensor& a, const at::Tensor& b, const char* what) {
@@ -1157,30 +1158,39 @@ bool attn_ok(int64_t T, int64_t C, int64_t heads) {
   return heads > 0 && C == heads * 64 && kern::attn_supported(static_cast<int>(T), 64);
 }
 
-// o [B, T, H*64] (contiguous), lse [B*H, T] fp32 (log2 domain)
+// o [B, T, H*64] (contiguous), lse [B*H, T] fp32 (log2 domain), keep bits
+// (int32 [attn_mask_words], T²/8 bytes per head; empty without dropout)
 std::vector<at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t heads,
                                        bool causal, double p_drop, int64_t seed) {
   same_shape(q, k, "flash_attn_fwd");
   same_shape(q, v, "flash_attn_fwd");
   c10::hip::HIPGuard guard(q.device().index());
-  const kern::AttnParams p = attn_params(q, heads, causal, p_drop, seed);
+  kern::AttnParams p = attn_params(q, heads, causal, p_drop, seed);
   at::Tensor o = at::empty(q.sizes(), q.options().memory_format(at::MemoryFormat::Contiguous));
   at::Tensor lse = at::empty({q.size(0) * heads, q.size(1)}, q.options().dtype(at::kFloat));
+  at::Tensor mask = at::empty({p.p_drop > 0.f ? kern::attn_mask_words(p.B, p.H, p.T) : 0}, q.options().dtype(at::kInt));
+  if (p.p_drop > 0.f) p.mask = reinterpret_cast<uint32_t*>(mask.data_ptr<int32_t>());
   kern::attn_fwd(p, attn_view(q, "q"), attn_view(k, "k"), attn_view(v, "v"), attn_out(o, "o"), lse.data_ptr<float>(),
                  stream_of(q));
-  return {o, lse};
+  return {o, lse, mask};
 }
 
 // writes dq, dk, dv (strided views allowed, e.g. slices of one packed buffer)
 void flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-                    const at::Tensor& o, const at::Tensor& lse, int64_t heads, bool causal, double p_drop,
-                    int64_t seed, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv) {
+                    const at::Tensor& o, const at::Tensor& lse, const at::Tensor& mask, int64_t heads, bool causal,
+                    double p_drop, int64_t seed, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&k, &v, &o, &dout, &dq, &dk, &dv})
     same_shape(q, *t, "flash_attn_bwd");
   c10::hip::HIPGuard guard(q.device().index());
-  const kern::AttnParams p = attn_params(q, heads, causal, p_drop, seed);
+  kern::AttnParams p = attn_params(q, heads, causal, p_drop, seed);
   DK_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == q.size(0) * heads * q.size(1),
             "flash_attn_bwd: lse");
+  if (p.p_drop > 0.f) {  // the forward's keep bits
+    DK_CHECK(mask.is_cuda() && mask.scalar_type() == at::kInt && mask.is_contiguous() &&
+                 mask.numel() == kern::attn_mask_words(p.B, p.H, p.T),
+             "flash_attn_bwd: dropout keep bits of the forward required");
+    p.mask = reinterpret_cast<uint32_t*>(const_cast<int32_t*>(mask.data_ptr<int32_t>()));
+  }
   at::Tensor delta = at::empty_like(lse);
   kern::attn_bwd(p, attn_view(q, "q"), attn_view(k, "k"), attn_view(v, "v"), attn_view(o, "o"),
                  attn_view(dout, "dout"), lse.data_ptr<float>(), delta.data_ptr<float>(), attn_out(dq, "dq"),

@@ -1,6 +1,6 @@
 // Flash attention (head dim 64) for gfx950: forward, dK/dV and dQ kernels on
 // v_mfma_f32_32x32x16_bf16, bf16 I/O, fp32 online softmax, optional causal
-// mask and dropout on P regenerated from a counter hash in the backward.
+// mask and dropout on P (keep bits hashed in the forward, stored for the backward).
 //
 // Layout choices (CDNA4, wave64):
 //  * "swapped" products: the forward computes Sᵀ = K·Qᵀ so each lane owns one
@@ -18,6 +18,9 @@
 //  * backward = two kernels (FA2 split, no float atomics): dK/dV with the key
 //    on the lane (S and dP accumulators feed dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS
 //    directly), and dQ with the query on the lane (dQᵀ += Kᵀ·dSᵀ).
+//  * dropout: the forward hashes, and stores the keep decisions as bits (T²/8
+//    bytes per head, in a word order both backward kernels read directly);
+//    the backward hashes nothing.
 //
 // Replaces PyTorch-ROCm's scaled_dot_product_attention (aotriton Triton
 // kernels) on the BERT-base / GPT-2-small paths ("flash-style
@@ -138,10 +141,11 @@ __device__ __forceinline__ void stage_tile(const uint16_t* src, int64_t st, int 
 // 32-bit hash per (query, aligned group of 4 keys) — key 4j + e takes byte e
 // (the FlashAttention-2 practice of byte thresholds: p is quantised to
 // multiples of 1/256 and the keep scale is 1/(1 - p_eff) with p_eff =
-// thr / 256). Identical in forward and backward. The counter is bit-packed
-// (q << 11 | key / 4, T ≤ 8192) and the (batch, head) index and the seed are
-// folded into a per-workgroup key, so a hash costs one murmur3 finaliser (two
-// 32-bit multiplies — quarter-rate VALU), one per 4 elements.
+// thr / 256). The counter is bit-packed (q << 11 | key / 4, T ≤ 8192) and the
+// (batch, head) index and the seed are folded into a per-workgroup key, so a
+// hash costs one murmur3 finaliser (two 32-bit multiplies — quarter-rate
+// VALU), one per 4 elements. Only the forward hashes: it stores the keep bits
+// (below) and the backward kernels read them.
 __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x85ebca6bu;
@@ -156,12 +160,37 @@ __device__ __forceinline__ uint32_t drop_key(uint32_t s0, uint32_t s1, uint32_t 
 __device__ __forceinline__ uint32_t drop_hash(uint32_t kbh, uint32_t q, uint32_t key) {
   return fmix32(((q << 11) | (key >> 2)) ^ kbh);
 }
-// byte e of the hash ≥ thr (e is a compile-time constant at every call)
-__device__ __forceinline__ bool drop_keep(uint32_t hsh, int e, uint32_t thr) {
-  return ((hsh >> (8 * e)) & 0xffu) >= thr;
-}
 __device__ __forceinline__ uint32_t drop_thr(float p) { return static_cast<uint32_t>(p * 256.f + 0.5f); }
 __device__ __forceinline__ float drop_scale(uint32_t thr) { return 256.f / static_cast<float>(256u - thr); }
+// All four byte compares of a hash at once (SWAR): bit 7 of byte e of the
+// result = (byte e of h) >= thr. low: bit 7 of each byte = (byte & 0x7f) >=
+// (thr & 0x7f) — (b | 0x80) − t7 never borrows across bytes; the byte's own
+// bit 7 then ORs in (thr < 128: ta = ~0) or ANDs in (thr ≥ 128: ta = 0).
+// tb = (thr & 0x7f) · 0x01010101. Other bits are don't-care.
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t h, uint32_t tb, uint32_t ta) {
+  const uint32_t low = ((h & 0x7f7f7f7fu) | 0x80808080u) - tb;
+  return (low & (h | ta)) | (h & ta);
+}
+// bf16-pair masks from keep_bytes: 0xFFFF per kept element of the pair
+// (keys e = 0, 1 / 2, 3). v_perm selectors 8-11 replicate the sign bit of
+// byte 1 / 3 of src1 (= t: keys 1, 3) and of src0 (= t << 8: keys 0, 2).
+__device__ __forceinline__ uint32_t pair_mask01(uint32_t t) { return __builtin_amdgcn_perm(t << 8, t, 0x08080A0Au); }
+__device__ __forceinline__ uint32_t pair_mask23(uint32_t t) { return __builtin_amdgcn_perm(t << 8, t, 0x09090B0Bu); }
+// all-ones / zero from bit `pos` of w (v_bfe_i32)
+__device__ __forceinline__ uint32_t bit_mask(uint32_t w, uint32_t pos) {
+  return static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(w), pos, 1));
+}
+__device__ __forceinline__ float and_mask(float x, uint32_t m) { return __uint_as_float(__float_as_uint(x) & m); }
+
+// Keep-bit store: one 32-bit word per (batch-head bh, key block kb of 64,
+// hh, query q) at mask[((bh·T/64 + kb)·2 + hh)·T + q] holds the 32 keys
+// kb·64 + 32kh + 8g + 4hh + e (kh, e < 2·2, g < 4) at bit 8e + 4kh + g — the
+// 32 keys a forward / dQ lane (query q, lane half hh) holds of that block, so
+// both read one word per block; a dK/dV lane (one key) reads, through LDS,
+// one bit of 4 consecutive queries' words per 16-B read.
+__device__ __forceinline__ int64_t mask_word(int bh, int nblk, int kblk, int hh, int T, int q) {
+  return ((static_cast<int64_t>(bh) * nblk + kblk) * 2 + hh) * T + q;
+}
 
 // (batch-head, tile) of this workgroup. Causal: tiles carry unequal work
 // (query tile t of the forward / dQ sees t + 1 key tiles; key tile t of dK/dV
@@ -227,6 +256,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
   }
   const float c = P.scale * kLog2e;
   const uint32_t thr = drop_thr(P.p_drop);
+  const uint32_t tb = (thr & 0x7fu) * 0x01010101u, ta = thr < 128u ? ~0u : 0u;
   const uint32_t kbh = drop_key(static_cast<uint32_t>(P.seed), static_cast<uint32_t>(P.seed >> 32), bh);
 
   float m = -INFINITY, l = 0.f;
@@ -297,24 +327,32 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
 #pragma unroll
         for (int r = 0; r < 16; ++r) oacc[dh][r] *= alpha;
     }
-    if (DROP) {  // registers 4g … 4g+3 hold keys 4j … 4j+3: one hash each; the keep scale goes on O at the end
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const uint32_t hs = drop_hash(kbh, qi, kb + 32 * kh + 8 * g + 4 * hh);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) s[kh][4 * g + e] = drop_keep(hs, e, thr) ? s[kh][4 * g + e] : 0.f;
-        }
-    }
+    // P to bf16 operand fragments; dropout (the keep scale goes on O at the
+    // end): registers 4g … 4g+3 hold keys 4j … 4j+3, one hash each → the
+    // four keep bits (SWAR), the two bf16-pair masks ANDed onto the packed
+    // P, and this lane's keep word of the block for the backward
+    uint32_t word = 0;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int sg = 0; sg < 2; ++sg) {
-        const bf16x8 pf = acc_frag(s[kh], sg);
+        uint4 u = make_uint4(pack2(s[kh][8 * sg + 0], s[kh][8 * sg + 1]), pack2(s[kh][8 * sg + 2], s[kh][8 * sg + 3]),
+                             pack2(s[kh][8 * sg + 4], s[kh][8 * sg + 5]), pack2(s[kh][8 * sg + 6], s[kh][8 * sg + 7]));
+        if (DROP) {
+          const int g0 = 2 * sg, j0 = 4 * kh + g0;
+          const uint32_t t0 = keep_bytes(drop_hash(kbh, qi, kb + 32 * kh + 8 * g0 + 4 * hh), tb, ta);
+          const uint32_t t1 = keep_bytes(drop_hash(kbh, qi, kb + 32 * kh + 8 * g0 + 8 + 4 * hh), tb, ta);
+          word |= ((t0 >> (7 - j0)) & (0x01010101u << j0)) | ((t1 >> (6 - j0)) & (0x01010101u << (j0 + 1)));
+          u.x &= pair_mask01(t0);
+          u.y &= pair_mask23(t0);
+          u.z &= pair_mask01(t1);
+          u.w &= pair_mask23(t1);
+        }
+        const bf16x8 pf = __builtin_bit_cast(bf16x8, u);
 #pragma unroll
         for (int dh = 0; dh < 2; ++dh) oacc[dh] = mfma(tr_op(sV, 32 * kh + 16 * sg, 32 * dh, lane), pf, oacc[dh]);
       }
+    if (DROP && qok) P.mask[mask_word(bh, T / kKB, it, hh, T, qi)] = word;
   }
   if (qok) {
     const float inv = (DROP ? drop_scale(thr) : 1.f) / l;
@@ -381,13 +419,14 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
   const float dlt = dpart + __shfl_xor(dpart, 32, 64);  // 0 for rows past T (gf zeroed)
   if (qok && hh == 0) delta[static_cast<int64_t>(bh) * T + qi] = dlt;
   const float c = P.scale * kLog2e;
-  const uint32_t thr = drop_thr(P.p_drop);
-  const float inv_keep = drop_scale(thr);
-  const uint32_t kbh = drop_key(static_cast<uint32_t>(P.seed), static_cast<uint32_t>(P.seed >> 32), bh);
+  const float inv_keep = drop_scale(drop_thr(P.p_drop));
 
   f32x16 dacc[2] = {zero16(), zero16()};
   int nkb = T / kKB;
   if (CAUSAL) nkb = min(nkb, (tile * 128 + 128 + kKB - 1) / kKB);
+  // this lane's keep words (one per key block, stride 2T), one block ahead
+  const uint32_t* MW = P.mask + mask_word(bh, T / kKB, 0, hh, T, qok ? qi : 0);
+  uint32_t wnext = DROP ? MW[0] : 0u;
   auto issue = [&](int it) {
     if (it >= nkb) return;
     char* base = lds + (it & 1) * 2 * kTile;
@@ -398,7 +437,12 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
   for (int it = 0; it < nkb; ++it) {
     wait_vm0();
     barrier();
+    const uint32_t w = wnext;
+    // the word's use (hence hipcc's vmcnt wait for it) here, where nothing
+    // else is in flight — not after the next tile's DMA is issued
+    if (DROP) asm volatile("" ::"v"(w));
     issue(it + 1);
+    if (DROP) wnext = MW[static_cast<int64_t>(min(it + 1, nkb - 1)) * 2 * T];
     const char* sK = lds + (it & 1) * 2 * kTile;
     const char* sV = sK + kTile;
     const int kb = it * kKB;
@@ -414,7 +458,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
         s = mfma(row_rd(sK, 32 * kh + (lane & 31), 2 * ks + hh), qf[ks], s);
         dp = mfma(row_rd(sV, 32 * kh + (lane & 31), 2 * ks + hh), gf[ks], dp);
       }
-      uint32_t hs = 0;
+      const uint32_t wk = w >> (4 * kh);  // key 8g + 4hh + e of this half at bit 8e + g
       // causal mask only where this 32-key half reaches past the wave's first query
       const bool diag = CAUSAL && kb + 32 * kh + 31 > tile * 128 + wave * 32;
 #pragma unroll
@@ -423,10 +467,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
         float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lse2));
         if (CAUSAL && diag) p = key > qi ? 0.f : p;
         float g = dp[r];
-        if (DROP) {
-          if ((r & 3) == 0) hs = drop_hash(kbh, qi, key);  // key ≡ 0 mod 4: one hash for keys key … key + 3
-          g = drop_keep(hs, r & 3, thr) ? g : 0.f;
-        }
+        if (DROP) g = and_mask(g, bit_mask(wk, 8 * (r & 3) + (r >> 2)));
         // dSᵀ (without the softmax scale); the keep scale rides in the fma
         s[r] = p * (DROP ? fmaf(g, inv_keep, -dlt) : g - dlt);
       }
@@ -460,7 +501,8 @@ template <bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTensor q, AttnTensor k, AttnTensor v,
                                                           AttnTensor dout, const float* __restrict__ lse,
                                                           const float* __restrict__ delta, AttnOut dk, AttnOut dv) {
-  constexpr int kStage = 2 * kTile + 2 * kKB * 4;  // Q | dO | lse | delta
+  // Q | dO | lse | delta | keep words [key block kb0/64 + {0,1}][hh][64 queries]
+  constexpr int kStage = 2 * kTile + 2 * kKB * 4 + (DROP ? 4 * kKB * 4 : 0);
   __shared__ __attribute__((aligned(16))) char lds[2 * kStage];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -486,9 +528,11 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
     vf[ks] = __builtin_bit_cast(bf16x8, kok ? uv : z);
   }
   const float c = P.scale * kLog2e;
-  const uint32_t thr = drop_thr(P.p_drop);
-  const float inv_keep = drop_scale(thr);
-  const uint32_t kbh = drop_key(static_cast<uint32_t>(P.seed), static_cast<uint32_t>(P.seed >> 32), bh);
+  const float inv_keep = drop_scale(drop_thr(P.p_drop));
+  // this lane's key in the keep words: LDS segment (key block, hh) and bit
+  const int kl = lane & 31;
+  const int mseg = (wave >> 1) * 2 + ((kl >> 2) & 1);
+  const uint32_t mpos = 8 * (kl & 3) + 4 * (wave & 1) + ((kl >> 3) & 3);
   const float* L = lse + static_cast<int64_t>(bh) * T;
   const float* DL = delta + static_cast<int64_t>(bh) * T;
 
@@ -505,6 +549,15 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
       glds4(L + qb + lane, base + 2 * kTile);
       glds4(DL + qb + lane, base + 2 * kTile + kKB * 4);
     }
+    if (DROP && (wave == 1 || wave == 2)) {  // the keep words of key block kb0/64 + wave - 1 (if inside T)
+      const int kblk = kb0 / kKB + wave - 1;
+      if (kblk < nqt) {
+        const uint32_t* src = P.mask + mask_word(bh, nqt, kblk, 0, T, qb + lane);
+        char* dst = base + 2 * kTile + 2 * kKB * 4 + (wave - 1) * 2 * kKB * 4;
+        glds4(src, dst);
+        glds4(src + T, dst + kKB * 4);
+      }
+    }
   };
   issue(0);
   for (int it = 0; qt0 + it < nqt; ++it) {
@@ -515,6 +568,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
     const char* sG = sQ + kTile;
     const float* sL = reinterpret_cast<const float*>(sQ + 2 * kTile);
     const float* sD = sL + kKB;
+    const uint32_t* sM = reinterpret_cast<const uint32_t*>(sD + kKB) + mseg * kKB;
     const int qb = (qt0 + it) * kKB;
     // Both 32-query sub-tiles' S and dP are issued first: the second pair's 8
     // MFMAs run in the matrix pipe while the first pair's softmax-gradient VALU
@@ -553,16 +607,14 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
           const float4 l4 = *reinterpret_cast<const float4*>(sL + rl);
           const float4 d4 = *reinterpret_cast<const float4*>(sD + rl);
           const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
-          // dropout: the 4 lanes of a quad hold keys 4j … 4j+3, which share
-          // each row's hash — lane 4j + i hashes row rl + i and every lane
-          // takes row e's hash from quad lane e (DPP quad_perm [e,e,e,e])
-          uint32_t hrow[4];
+          // dropout: this key's bit of rows rl … rl+3's keep words (one 16-B read)
+          uint32_t km[4];
           if (DROP) {
-            const int mine = static_cast<int>(drop_hash(kbh, qb + rl + (lane & 3), key));
-            hrow[0] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(mine, 0x00, 0xF, 0xF, false));
-            hrow[1] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(mine, 0x55, 0xF, 0xF, false));
-            hrow[2] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(mine, 0xAA, 0xF, 0xF, false));
-            hrow[3] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(mine, 0xFF, 0xF, 0xF, false));
+            const uint4 w4 = *reinterpret_cast<const uint4*>(sM + rl);
+            km[0] = bit_mask(w4.x, mpos);
+            km[1] = bit_mask(w4.y, mpos);
+            km[2] = bit_mask(w4.z, mpos);
+            km[3] = bit_mask(w4.w, mpos);
           }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -572,9 +624,8 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
             if (CAUSAL && diag) p = key > qrow ? 0.f : p;
             float gg = dp[qs][r], pk = p;
             if (DROP) {
-              const bool kp = drop_keep(hrow[e], key & 3, thr);
-              gg = kp ? gg : 0.f;
-              pk = kp ? p : 0.f;  // the keep scale goes on dV at the end
+              gg = and_mask(gg, km[e]);
+              pk = and_mask(p, km[e]);  // the keep scale goes on dV at the end
             }
             pv[4 * gg2 + e] = pk;
             // dS (without the softmax scale); the keep scale rides in the fma

@@ -27,7 +27,15 @@ struct AttnParams {
   bool causal;
   float p_drop;      // dropout probability on P (0 = off)
   uint64_t seed;
+  // dropout keep bits, [B*H][T/64][2][T] uint32 (attn_mask_words): written by
+  // the forward, read by the backward; unused when p_drop == 0
+  uint32_t* mask;
 };
+
+// uint32 words of the dropout keep-bit store (T² / 32 per batch-head)
+inline int64_t attn_mask_words(int B, int H, int T) {
+  return static_cast<int64_t>(B) * H * (T / 64) * 2 * T;
+}
 
 bool attn_supported(int T, int D);
 

@@ -1,8 +1,9 @@
 """Flash attention on the hand-written MFMA kernels (``csrc/kernels/attention.hip``).
 
 Head dim 64, bf16 activations, fp32 softmax statistics, optional causal mask
-and dropout on the attention probabilities (mask regenerated in the backward
-from a counter hash: nothing is stored). Replaces
+and dropout on the attention probabilities (keep decisions hashed from a
+counter in the forward and kept as bits, T²/8 bytes per head, for the
+backward). Replaces
 ``scaled_dot_product_attention`` (PyTorch-ROCm's aotriton kernels) for
 GPT-2-small and BERT-base.
 
@@ -32,21 +33,21 @@ def attn_supported(x: torch.Tensor, heads: int) -> bool:
 class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, heads, causal, p_drop, seed):
-        o, lse = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed)
-        ctx.save_for_backward(q, k, v, o, lse)
+        o, lse, keep = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed)
+        ctx.save_for_backward(q, k, v, o, lse, keep)
         ctx.cfg = (heads, causal, p_drop, seed)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse = ctx.saved_tensors
+        q, k, v, o, lse, keep = ctx.saved_tensors
         heads, causal, p_drop, seed = ctx.cfg
         do = do.contiguous()
         if do.dtype != torch.bfloat16:
             do = do.to(torch.bfloat16)
         dq, dk, dv = torch.empty_like(q, memory_format=torch.contiguous_format), torch.empty_like(
             k, memory_format=torch.contiguous_format), torch.empty_like(v, memory_format=torch.contiguous_format)
-        _C.flash_attn_bwd(do, q, k, v, o, lse, heads, causal, p_drop, seed, dq, dk, dv)
+        _C.flash_attn_bwd(do, q, k, v, o, lse, keep, heads, causal, p_drop, seed, dq, dk, dv)
         return dq, dk, dv, None, None, None, None
 
 
@@ -55,14 +56,14 @@ class _FlashAttnQKVFn(torch.autograd.Function):
     def forward(ctx, qkv, heads, causal, p_drop, seed):
         C = qkv.shape[2] // 3
         q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
-        o, lse = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed)
-        ctx.save_for_backward(qkv, o, lse)
+        o, lse, keep = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed)
+        ctx.save_for_backward(qkv, o, lse, keep)
         ctx.cfg = (heads, causal, p_drop, seed)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse = ctx.saved_tensors
+        qkv, o, lse, keep = ctx.saved_tensors
         heads, causal, p_drop, seed = ctx.cfg
         do = do.contiguous()
         if do.dtype != torch.bfloat16:
@@ -71,7 +72,7 @@ class _FlashAttnQKVFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv, memory_format=torch.contiguous_format)
         q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
         dq, dk, dv = dqkv[..., :C], dqkv[..., C:2 * C], dqkv[..., 2 * C:]
-        _C.flash_attn_bwd(do, q, k, v, o, lse, heads, causal, p_drop, seed, dq, dk, dv)
+        _C.flash_attn_bwd(do, q, k, v, o, lse, keep, heads, causal, p_drop, seed, dq, dk, dv)
         return dqkv, None, None, None, None
 
 
@@ -92,6 +93,26 @@ def dropout_p_effective(p: float) -> float:
     of 1/256 (byte thresholds, as FlashAttention-2 does); kept elements are
     scaled by 1 / (1 - dropout_p_effective(p))."""
     return int(p * 256.0 + 0.5) / 256.0
+
+
+def flash_attn_keep_bits(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, causal: bool,
+                         dropout_p: float, seed: int) -> torch.Tensor:
+    """The dropout keep decisions the forward stored for the backward, decoded
+    to a bool [B, H, T, T] (test hook). Causal: entries above the diagonal are
+    not stored (never read) and come back as False."""
+    B, T = q.shape[0], q.shape[1]
+    _, _, words = _C.flash_attn_fwd(q, k, v, heads, causal, float(dropout_p), int(seed))
+    nblk = T // 64
+    w = words.view(B * heads, nblk, 2, T).to(torch.int64) & 0xFFFFFFFF
+    kk = torch.arange(64, device=q.device)
+    # key 32kh + 8g + 4hh + e of a 64-key block: word half hh, bit 8e + 4kh + g
+    hh, bit = (kk >> 2) & 1, 8 * (kk & 3) + 4 * ((kk >> 5) & 1) + ((kk >> 3) & 3)
+    sel = w[:, :, hh, :]                                   # [BH, nblk, 64 keys, T queries]
+    bits = (sel >> bit[None, None, :, None]) & 1
+    m = bits.permute(0, 3, 1, 2).reshape(B, heads, T, T).bool()
+    if causal:
+        m &= torch.ones(T, T, dtype=torch.bool, device=q.device).tril()
+    return m
 
 
 def dropout_keep_mask(B: int, H: int, T: int, p: float, seed: int, device=None) -> torch.Tensor:

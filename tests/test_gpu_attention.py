@@ -13,6 +13,9 @@ CASES = [  # B, H, T, causal, p
     (1, 2, 192, False, 0.1),   # T not a multiple of the 128-query block
     (2, 2, 256, True, 0.1),
     (1, 4, 512, False, 0.1),
+    (1, 2, 192, True, 0.1),    # causal, last key tile half outside T
+    (1, 2, 256, False, 0.6),   # keep threshold >= 128 (the other SWAR compare)
+    (1, 2, 128, True, 0.5),    # threshold exactly 128
 ]
 
 
@@ -77,3 +80,21 @@ def test_flash_attn_qkv_packed(cuda):
     o2.backward(do)
     assert torch.equal(o, o2)
     assert torch.equal(a.grad, torch.cat([t.grad for t in parts], dim=2))
+
+
+@pytest.mark.parametrize("case", [(2, 3, 256, False, 0.1), (1, 2, 192, True, 0.3), (1, 2, 128, False, 0.7)])
+def test_stored_keep_bits_match_oracle(cuda, case):
+    """The forward's stored keep bits (read by both backward kernels) decode
+    to exactly the hash oracle's mask (causal: on and below the diagonal)."""
+    from distributed_compute_pytorch_amd.ops.attention import dropout_keep_mask, flash_attn_keep_bits
+
+    B, H, T, causal, p = case
+    C = H * 64
+    g = torch.Generator().manual_seed(9)
+    q, k, v = (torch.randn(B, T, C, generator=g).to(cuda).to(torch.bfloat16) for _ in range(3))
+    seed = 987654321
+    got = flash_attn_keep_bits(q, k, v, H, causal, p, seed)
+    want = dropout_keep_mask(B, H, T, p, seed, cuda)
+    if causal:
+        want = want & torch.ones(T, T, dtype=torch.bool, device=cuda).tril()
+    assert torch.equal(got, want), int((got != want).sum())
