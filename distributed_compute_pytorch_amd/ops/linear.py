@@ -405,7 +405,36 @@ def _install_flush_hook():
         from torch.optim.optimizer import register_optimizer_step_pre_hook
 
         register_optimizer_step_pre_hook(lambda opt, args, kwargs: flush_weight_grads(_at_step=True))
+        _install_zero_grad_discard()
         _HOOKED[0] = True
+
+
+def _install_zero_grad_discard():
+    """The deferred contributions belong to ``.grad`` and must go with it:
+    stock ``torch.optim.Optimizer.zero_grad`` and ``torch.nn.Module.zero_grad``
+    (which have no hooks) are wrapped to drop the stash of their parameters
+    first, as this package's optimizers' zero_grad does — otherwise an
+    accumulation round abandoned by a stock zero_grad would leak its stashed
+    micro-steps into the next round's synchronised gradient.
+    Installed once, by the first deferring no_sync."""
+    import functools
+
+    opt_zg, mod_zg = torch.optim.Optimizer.zero_grad, torch.nn.Module.zero_grad
+
+    @functools.wraps(opt_zg)
+    def optimizer_zero_grad(self, *args, **kwargs):
+        if _PENDING or _PENDING_B:
+            discard_weight_grads([p for g in self.param_groups for p in g["params"]])
+        return opt_zg(self, *args, **kwargs)
+
+    @functools.wraps(mod_zg)
+    def module_zero_grad(self, *args, **kwargs):
+        if _PENDING or _PENDING_B:
+            discard_weight_grads(list(self.parameters()))
+        return mod_zg(self, *args, **kwargs)
+
+    torch.optim.Optimizer.zero_grad = optimizer_zero_grad
+    torch.nn.Module.zero_grad = module_zero_grad
 
 
 def _wgrad_sum(segs, tgt):

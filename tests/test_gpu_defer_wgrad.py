@@ -171,6 +171,38 @@ def test_zero_grad_drops_deferred(pg, cuda, no_autotune):
         assert _rel(b.grad, a.grad) < 1e-4, (name, _rel(b.grad, a.grad))
 
 
+@pytest.mark.parametrize("how", ["module", "stock_optimizer"])
+def test_stock_zero_grad_drops_deferred(pg, cuda, no_autotune, how):
+    """a stock zero_grad (torch's Module / Optimizer, no hooks of
+    their own) abandoning an accumulation round drops the stashed micro-steps
+    too — the next round's gradients equal a fresh run's."""
+    import distributed_compute_pytorch_amd as dcp
+    from distributed_compute_pytorch_amd.ops import linear as lin
+
+    base = _model(cuda)
+    data = [torch.randint(0, 50257, (2, 257), device=cuda) for _ in range(2)]
+    m_ref, _, _ = _grads(base, data, True, cuda)
+    m = copy.deepcopy(base)
+    ddp = dcp.parallel.DistributedDataParallel(m, device_ids=[0], gradient_as_bucket_view=True, defer_accum_wgrad=True)
+    with ddp.no_sync():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            ddp(data[1][:, :-1], data[1][:, 1:]).backward()
+    assert lin.pending_weight_grads() > 0
+    if how == "module":
+        ddp.zero_grad()
+    else:
+        torch.optim.SGD(m.parameters(), lr=0.0).zero_grad()
+    assert lin.pending_weight_grads() == 0
+    for k, seq in enumerate(data):
+        with (contextlib.nullcontext() if k == len(data) - 1 else ddp.no_sync()):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = ddp(seq[:, :-1], seq[:, 1:]) / len(data)
+            loss.backward()
+    torch.cuda.synchronize()
+    for (name, a), b in zip(m_ref.named_parameters(), m.parameters()):
+        assert _rel(b.grad, a.grad) < 1e-4, (name, _rel(b.grad, a.grad))
+
+
 class _TwoBranch(torch.nn.Module):
     """Linear ``a`` always runs; ``b`` only when asked (a branch the
     synchronising micro-step may skip)."""
