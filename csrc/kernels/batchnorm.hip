@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <string>
 
 #include "bn_kernels.h"
 
@@ -665,13 +666,16 @@ inline void red_geometry(int64_t M, int C, int* nblk, int64_t* rows_per_blk, int
   *nblk = static_cast<int>((M + rpb - 1) / rpb);
 }
 
+// apply grid cap (gemm_tune "bn_apply_cap"): ≤ 1024 workgroups (4 per CU)
+// by default — more streamed faster in isolation (tools/bw_probe.hip) but
+// measured -1.4 % in the ResNet-50 step at batch 256 (more coefficient
+// prologues, the trailing-edge partial waves; NOTES §19)
+int g_bn_apply_cap = 1024;
+
 // apply grid: multiple of nothing special (cv | 256 keeps thread→channel fixed),
-// ≤ 1024 workgroups (4 per CU) so the per-thread prologue stays cheap
+// ≤ g_bn_apply_cap workgroups so the per-thread prologue stays cheap
 inline int apply_grid(int64_t nvec, int cv) {
-  // ≤ 1024 workgroups (4 per CU): more streamed faster in isolation
-  // (tools/bw_probe.hip) but measured -1.4 % in the ResNet-50 step (more
-  // coefficient prologues, the trailing-edge partial waves)
-  constexpr int64_t cap = 1024;
+  const int64_t cap = g_bn_apply_cap;
   int64_t g = (nvec + kT * 2 - 1) / (kT * 2);
   if (g > cap) g = cap;
   if (g < 1) g = 1;
@@ -954,6 +958,13 @@ void bn_backward_apply(int dtype, const void* gy, const void* x, int64_t M, int 
     hipLaunchKernelGGL((bn_bwd_apply_kernel<BN_F32, true, false, true>), dim3(grid), dim3(kT), sm, s, gy, nullptr,
                        x, mean, invstd, gamma, beta, acc, dgamma, dbeta, true, dx, M, nvec, C);
 }
+
+bool bn_tune(const char* key, int value) {
+  if (std::string(key) != "bn_apply_cap") return false;
+  g_bn_apply_cap = value < 256 ? 256 : (value > 65536 ? 65536 : value);
+  return true;
+}
+int bn_tune_get(const char* key) { return std::string(key) == "bn_apply_cap" ? g_bn_apply_cap : -1; }
 
 }  // namespace kern
 }  // namespace dcp

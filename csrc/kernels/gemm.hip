@@ -2018,6 +2018,7 @@ void gemm_tune(const char* key, int value) {
   if (k == "wg_cap") g_wg_cap = value < 0 ? 0 : value;
   if (k == "reserve_cus") g_reserve_cus = value < 0 ? 0 : (value > 192 ? 192 : value);
   if (k.rfind("pp_", 0) == 0) gemm_pp_tune(key, value);
+  if (k.rfind("bn_", 0) == 0) bn_tune(key, value);
   wgrad_pp_tune(key, value);
 }
 int gemm_tune_get(const char* key) {
@@ -2034,6 +2035,7 @@ int gemm_tune_get(const char* key) {
   if (k == "wg_cap") return g_wg_cap;
   if (k == "reserve_cus") return g_reserve_cus;
   if (k.rfind("pp_", 0) == 0) return gemm_pp_tune_get(key);
+  if (k.rfind("bn_", 0) == 0) return bn_tune_get(key);
   return wgrad_pp_tune_get(key);
 }
 

@@ -167,6 +167,8 @@ void gemm_wgrad_pp(const WgradPPSegs& sg, float* D, float* ws, int N1, int N2, i
                    const WgradPPGeo* geo, const void* zero, bool acc, int rows_lim, hipStream_t s);
 bool wgrad_pp_tune(const char* key, int value);  // false: not one of its keys
 int wgrad_pp_tune_get(const char* key);
+bool bn_tune(const char* key, int value);  // batchnorm.hip: "bn_apply_cap"
+int bn_tune_get(const char* key);
 
 // Workspace (fp32 elements) gemm_wgrad_bf16 needs for this shape.
 int64_t gemm_wgrad_workspace(int64_t M, int N1, int N2, int taps = 1);
