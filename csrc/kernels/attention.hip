@@ -137,14 +137,16 @@ __device__ __forceinline__ void stage_tile(const uint16_t* src, int64_t st, int 
   }
 }
 
-// ---- dropout: 8 random bits per element (q, key) from a counter hash: one
-// 32-bit hash per (query, aligned group of 4 keys) — key 4j + e takes byte e
-// (the FlashAttention-2 practice of byte thresholds: p is quantised to
-// multiples of 1/256 and the keep scale is 1/(1 - p_eff) with p_eff =
-// thr / 256). The counter is bit-packed (q << 11 | key / 4, T ≤ 8192) and the
-// (batch, head) index and the seed are folded into a per-workgroup key, so a
-// hash costs one murmur3 finaliser (two 32-bit multiplies — quarter-rate
-// VALU), one per 4 elements. Only the forward hashes: it stores the keep bits
+// ---- dropout: 8 random bits per element (q, key) — byte thresholds, the
+// FlashAttention-2 practice: p is quantised to multiples of 1/256 and the
+// keep scale is 1/(1 - p_eff) with p_eff = thr / 256. Per (query, 64-key
+// block, lane half hh): one murmur3 finaliser of the bit-packed counter
+// (q << 8 | block << 1 | hh; T ≤ 8192) XOR a per-(batch, head, seed) key
+// gives the state x0; the block's 8 words (4 keys each, j = 4kh + g) are
+// x0, x1 = xs(x0), … (xorshift32 13/17/5) each XOR j·0x9E3779B9 (a Weyl
+// offset: distinct words even for the all-zero state) — one quarter-rate
+// multiply pair per 32 elements instead of per 4, the rest full-rate
+// shifts / XORs. Only the forward generates: it stores the keep bits
 // (below) and the backward kernels read them.
 __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
   x ^= x >> 16;
@@ -157,9 +159,16 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
 __device__ __forceinline__ uint32_t drop_key(uint32_t s0, uint32_t s1, uint32_t bh) {
   return fmix32(s0 ^ fmix32(bh * 0x9E3779B1u + s1));
 }
-__device__ __forceinline__ uint32_t drop_hash(uint32_t kbh, uint32_t q, uint32_t key) {
-  return fmix32(((q << 11) | (key >> 2)) ^ kbh);
+__device__ __forceinline__ uint32_t drop_state(uint32_t kbh, uint32_t q, uint32_t kblk, uint32_t hh) {
+  return fmix32(((q << 8) | (kblk << 1) | hh) ^ kbh);
 }
+__device__ __forceinline__ uint32_t xorshift32(uint32_t x) {
+  x ^= x << 13;
+  x ^= x >> 17;
+  x ^= x << 5;
+  return x;
+}
+__device__ __forceinline__ constexpr uint32_t drop_weyl(int j) { return static_cast<uint32_t>(j) * 0x9E3779B9u; }
 __device__ __forceinline__ uint32_t drop_thr(float p) { return static_cast<uint32_t>(p * 256.f + 0.5f); }
 __device__ __forceinline__ float drop_scale(uint32_t thr) { return 256.f / static_cast<float>(256u - thr); }
 // All four byte compares of a hash at once (SWAR): bit 7 of byte e of the
@@ -328,10 +337,11 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
         for (int r = 0; r < 16; ++r) oacc[dh][r] *= alpha;
     }
     // P to bf16 operand fragments; dropout (the keep scale goes on O at the
-    // end): registers 4g … 4g+3 hold keys 4j … 4j+3, one hash each → the
-    // four keep bits (SWAR), the two bf16-pair masks ANDed onto the packed
-    // P, and this lane's keep word of the block for the backward
+    // end): registers 4g … 4g+3 hold keys 4j … 4j+3, one random word each →
+    // the four keep bits (SWAR), the two bf16-pair masks ANDed onto the
+    // packed P, and this lane's keep word of the block for the backward
     uint32_t word = 0;
+    uint32_t xs = DROP ? drop_state(kbh, qi, it, hh) : 0u;  // word j = xs after j steps, ^ weyl(j)
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
@@ -340,8 +350,10 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
                              pack2(s[kh][8 * sg + 4], s[kh][8 * sg + 5]), pack2(s[kh][8 * sg + 6], s[kh][8 * sg + 7]));
         if (DROP) {
           const int g0 = 2 * sg, j0 = 4 * kh + g0;
-          const uint32_t t0 = keep_bytes(drop_hash(kbh, qi, kb + 32 * kh + 8 * g0 + 4 * hh), tb, ta);
-          const uint32_t t1 = keep_bytes(drop_hash(kbh, qi, kb + 32 * kh + 8 * g0 + 8 + 4 * hh), tb, ta);
+          const uint32_t t0 = keep_bytes(xs ^ drop_weyl(j0), tb, ta);
+          xs = xorshift32(xs);
+          const uint32_t t1 = keep_bytes(xs ^ drop_weyl(j0 + 1), tb, ta);
+          xs = xorshift32(xs);
           word |= ((t0 >> (7 - j0)) & (0x01010101u << j0)) | ((t1 >> (6 - j0)) & (0x01010101u << (j0 + 1)));
           u.x &= pair_mask01(t0);
           u.y &= pair_mask23(t0);

@@ -117,9 +117,12 @@ def flash_attn_keep_bits(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, head
 
 def dropout_keep_mask(B: int, H: int, T: int, p: float, seed: int, device=None) -> torch.Tensor:
     """The kernels' dropout keep-mask [B, H, T, T] rebuilt with integer torch
-    ops (test oracle): byte (key mod 4) of fmix32(((q << 11) | key/4) ^ kbh)
-    per element, kbh = fmix32(s0 ^ fmix32(bh·0x9E3779B1 + s1)) (murmur3
-    finaliser), kept when ≥ round(256·p)."""
+    ops (test oracle). Per (query q, 64-key block k, lane half hh):
+    x0 = fmix32(((q << 8) | (k << 1) | hh) ^ kbh), kbh = fmix32(s0 ^
+    fmix32(bh·0x9E3779B1 + s1)) (murmur3 finaliser); word j (j < 8) is
+    xorshift32 (13/17/5) applied j times to x0, XOR j·0x9E3779B9; key
+    64k + 32(j >> 2) + 8(j & 3) + 4hh + e takes byte e of word j and is
+    kept when that byte ≥ round(256·p)."""
     M = 0xFFFFFFFF
     dev = device or "cpu"
 
@@ -134,12 +137,31 @@ def dropout_keep_mask(B: int, H: int, T: int, p: float, seed: int, device=None) 
         x = mul32(x, 0xC2B2AE35)
         return x ^ (x >> 16)
 
+    def xorshift32(x):
+        x = x ^ ((x << 13) & M)
+        x = x ^ (x >> 17)
+        return x ^ ((x << 5) & M)
+
+    nblk = T // 64
     s0, s1 = seed & M, (seed >> 32) & M
-    bh = torch.arange(B * H, device=dev, dtype=torch.int64)[:, None, None]
-    qq = torch.arange(T, device=dev, dtype=torch.int64)[None, :, None]
-    kk = torch.arange(T, device=dev, dtype=torch.int64)[None, None, :]
+    i64 = dict(device=dev, dtype=torch.int64)
+    bh = torch.arange(B * H, **i64)[:, None, None, None]
+    qq = torch.arange(T, **i64)[None, :, None, None]
+    kb = torch.arange(nblk, **i64)[None, None, :, None]
+    hh = torch.arange(2, **i64)[None, None, None, :]
     kbh = fmix32(s0 ^ fmix32((mul32(bh, 0x9E3779B1) + s1) & M))
-    h = fmix32(((qq << 11) | (kk >> 2)) ^ kbh)
-    r8 = (h >> (8 * (kk & 3))) & 0xFF
+    x = fmix32(((qq << 8) | (kb << 1) | hh) ^ kbh)          # [BH, T, nblk, 2]
+    words = []
+    for j in range(8):
+        words.append(x ^ ((j * 0x9E3779B9) & M))
+        x = xorshift32(x)
+    w = torch.stack(words, -1)                               # [BH, T, nblk, hh, j]
+    e = torch.arange(4, **i64)
+    r8 = (w[..., None] >> (8 * e)) & 0xFF                    # [BH, T, nblk, hh, j, e]
     thr = int(p * 256.0 + 0.5)
-    return (r8 >= thr).view(B, H, T, T)
+    keep = (r8 >= thr).reshape(B * H, T, nblk, 64)           # block offsets in (hh, j, e) order
+    hv, jv, ev = torch.meshgrid(torch.arange(2), torch.arange(8), torch.arange(4), indexing="ij")
+    off = (32 * (jv >> 2) + 8 * (jv & 3) + 4 * hv + ev).reshape(-1)
+    inv = torch.empty_like(off)
+    inv[off] = torch.arange(64)
+    return keep[..., inv.to(keep.device)].reshape(B, H, T, T)

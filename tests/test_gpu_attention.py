@@ -98,3 +98,4 @@ def test_stored_keep_bits_match_oracle(cuda, case):
     if causal:
         want = want & torch.ones(T, T, dtype=torch.bool, device=cuda).tril()
     assert torch.equal(got, want), int((got != want).sum())
+
