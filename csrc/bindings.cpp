@@ -157,6 +157,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("register_buckets", &ReducerOptions::register_buckets)
       .def_readwrite("check_streams", &ReducerOptions::check_streams)
       .def_readwrite("defer_grad_wait", &ReducerOptions::defer_grad_wait)
+      .def_readwrite("slice_bytes", &ReducerOptions::slice_bytes)
       .def_readwrite("static_graph", &ReducerOptions::static_graph);
 
   m.def("trace_enabled", &trace::enabled);
@@ -215,6 +216,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("wait_all", &Reducer::wait_all, py::call_guard<py::gil_scoped_release>())
       .def("deferred_buckets", &Reducer::deferred_buckets)
       .def("sync_bucket", &Reducer::sync_bucket, py::call_guard<py::gil_scoped_release>())
+      .def("bucket_slice_bounds", &Reducer::bucket_slice_bounds)
+      .def("sync_bucket_slice", &Reducer::sync_bucket_slice, py::call_guard<py::gil_scoped_release>())
       .def("sync_all", &Reducer::sync_all, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("num_iterations", &Reducer::num_iterations)
       .def_property_readonly("num_rebuilds", &Reducer::num_rebuilds)

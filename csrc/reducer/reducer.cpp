@@ -131,7 +131,12 @@ void Reducer::wait_bucket(Bucket& b, hipStream_t cur, bool timed) {
     }
     (void)hipEventRecord(b.stall0, cur);
   }
-  b.work->wait();
+  if (!b.slice_works.empty()) {
+    for (auto& w : b.slice_works)
+      if (w) w->wait();
+  } else {
+    b.work->wait();
+  }
   if (timed) {
     (void)hipEventRecord(b.stall1, cur);
     b.stall_recorded = true;
@@ -148,11 +153,62 @@ void Reducer::sync_locked(Bucket& b) {
     (void)hipStreamIsCapturing(cur, &cap);
   }
   const bool timed = timing_ && cap == hipStreamCaptureStatusNone;
+  if (!b.slice_works.empty()) {
+    if (timed) {  // the stall events around the wait on every slice
+      wait_bucket(b, cur, true);
+      b.timed_work = b.work;
+    }
+    // only the slices not synced yet (each unpacks its own wire range)
+    for (size_t s = 0; s < b.slice_works.size(); ++s) sync_slice_locked(b, s);
+    finish_slices(b);
+    return;
+  }
   wait_bucket(b, cur, timed);
   if (timed) b.timed_work = b.work;
   if (!b.wire.is_same(b.flat)) ops::mt_copy({b.wire}, {b.flat}, 1.0);
   b.work.reset();
   b.deferred = false;
+}
+
+void Reducer::sync_slice_locked(Bucket& b, size_t s) {
+  if (b.slice_synced[s]) return;
+  b.slice_works[s]->wait();
+  if (!b.wire.is_same(b.flat)) {
+    const int64_t lo = b.slice_bounds[s], n = b.slice_bounds[s + 1] - lo;
+    ops::mt_copy({b.wire.narrow(0, lo, n)}, {b.flat.narrow(0, lo, n)}, 1.0);
+  }
+  b.slice_synced[s] = 1;
+}
+
+void Reducer::finish_slices(Bucket& b) {
+  for (char c : b.slice_synced)
+    if (!c) return;
+  b.slice_works.clear();
+  b.slice_synced.clear();
+  b.work.reset();
+  b.deferred = false;
+}
+
+std::vector<int64_t> Reducer::bucket_slice_bounds(int64_t k) {
+  std::lock_guard<std::mutex> g(mu_);
+  DK_CHECK(k >= 0 && k < static_cast<int64_t>(buckets_.size()), "Reducer::bucket_slice_bounds: bad bucket ", k);
+  const Bucket& b = buckets_[k];
+  if (!b.deferred || b.slice_works.empty()) return {};
+  return b.slice_bounds;
+}
+
+void Reducer::sync_bucket_slice(int64_t k, int64_t s) {
+  std::lock_guard<std::mutex> g(mu_);
+  DK_CHECK(k >= 0 && k < static_cast<int64_t>(buckets_.size()), "Reducer::sync_bucket_slice: bad bucket ", k);
+  Bucket& b = buckets_[k];
+  if (!b.deferred) return;
+  if (b.slice_works.empty() || timing_) {  // not sliced, or timed (the stall events span the whole bucket)
+    sync_locked(b);
+    return;
+  }
+  DK_CHECK(s >= 0 && s < static_cast<int64_t>(b.slice_works.size()), "Reducer::sync_bucket_slice: bad slice ", s);
+  sync_slice_locked(b, static_cast<size_t>(s));
+  finish_slices(b);
 }
 
 std::vector<int64_t> Reducer::deferred_buckets() {
@@ -221,6 +277,13 @@ void Reducer::build_buckets(const std::vector<std::vector<int64_t>>& assignment)
     b.pending = static_cast<int>(idx.size());
     b.stats.bytes = total * p0.element_size();
     b.stats.num_params = static_cast<int64_t>(idx.size());
+    if (opts_.slice_bytes > 0 && 2 * b.stats.bytes > 3 * opts_.slice_bytes) {
+      const int64_t n = (b.stats.bytes + opts_.slice_bytes - 1) / opts_.slice_bytes;
+      const int64_t al = std::max<int64_t>(1, 256 / static_cast<int64_t>(b.wire.element_size()));
+      const int64_t per = ((total + n - 1) / n + al - 1) / al * al;
+      for (int64_t lo = 0; lo < total; lo += per) b.slice_bounds.push_back(lo);
+      b.slice_bounds.push_back(total);
+    }
     out.push_back(std::move(b));
   }
   for (size_t i = 0; i < params_.size(); ++i) DK_CHECK(seen[i], "Reducer: parameter ", i, " not in any bucket");
@@ -457,8 +520,19 @@ void Reducer::launch(Bucket& b) {
     const at::Tensor w = b.wire.to(at::kDouble);
     b.check_sum = at::stack({w.sum(), w.abs().sum()}).to(at::kFloat);
   }
+  b.slice_works.clear();
+  b.slice_synced.clear();
   if (comm_hook_) {
     b.work = comm_hook_(b.wire, static_cast<int64_t>(&b - buckets_.data()));
+  } else if (!b.slice_bounds.empty()) {
+    // oversize bucket: one collective per slice, issued back to back (on the
+    // communicator's stream in order; the last one's Work stands for all)
+    for (size_t s = 0; s + 1 < b.slice_bounds.size(); ++s) {
+      at::Tensor piece = b.wire.narrow(0, b.slice_bounds[s], b.slice_bounds[s + 1] - b.slice_bounds[s]);
+      b.slice_works.push_back(comm_->all_reduce(piece, opts_.average ? ReduceOp::AVG : ReduceOp::SUM));
+    }
+    b.slice_synced.assign(b.slice_works.size(), 0);
+    b.work = b.slice_works.back();
   } else {
     b.work = comm_->all_reduce(b.wire, opts_.average ? ReduceOp::AVG : ReduceOp::SUM);
   }
@@ -600,6 +674,8 @@ void Reducer::finalize() {
     }
     if (!src.empty()) ops::mt_copy(src, dst, 1.0);
     b.work.reset();
+    b.slice_works.clear();
+    b.slice_synced.clear();
     b.launched = false;
     b.pending = static_cast<int>(b.params.size());
   }
@@ -619,6 +695,8 @@ void Reducer::finalize() {
 void Reducer::reset_iteration_state() {
   for (auto& b : buckets_) {
     b.work.reset();
+    b.slice_works.clear();
+    b.slice_synced.clear();
     b.check_work.reset();
     b.launched = false;
     b.pending = static_cast<int>(b.params.size());

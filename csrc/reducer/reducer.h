@@ -79,6 +79,13 @@ struct ReducerOptions {
   // still deferred is synced before the next backward's first pack, by
   // prepare_for_backward and by wait_gradients().
   bool defer_grad_wait = false;
+  // Oversize buckets (defer_grad_wait): a bucket of more than 1.5x this many
+  // bytes is reduced as ceil(bytes / slice_bytes) collectives over 256-B
+  // aligned slices of its buffer, each with its own Work, so a consumer can
+  // update the parameter ranges of a slice as soon as that slice lands
+  // (sync_bucket_slice) — the ready-last tied embeddings of GPT-2 / BERT are
+  // single 147 / 89 MB buckets. 0 = one collective per bucket (torch).
+  int64_t slice_bytes = 0;
   // torch's static_graph: the set of parameters that get no gradient is the
   // same every iteration. The first synchronised backward traverses the graph
   // and all-reduces the used map (as find_unused_parameters does); later ones
@@ -163,6 +170,12 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<int64_t> deferred_buckets();
   void sync_bucket(int64_t k);
   void sync_all();
+  // slice_bytes: element bounds [0, e1, …, numel] of deferred bucket k's
+  // slices when its reduction was issued slice by slice (else empty), and
+  // the per-slice sync (slices synced in any order; the bucket stops being
+  // deferred once all are)
+  std::vector<int64_t> bucket_slice_bounds(int64_t k);
+  void sync_bucket_slice(int64_t k, int64_t s);
 
  private:
   struct Bucket {
@@ -175,6 +188,9 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     int pending = 0;
     bool launched = false;
     WorkPtr work;
+    std::vector<int64_t> slice_bounds;  // slice_bytes: element bounds of the slices (empty: not sliced)
+    std::vector<WorkPtr> slice_works;   // this iteration's per-slice collectives (sliced launch)
+    std::vector<char> slice_synced;     // deferred: slices the compute stream is ordered behind
     WorkPtr timed_work;  // last finished collective, its elapsed time read lazily (bucket_stats)
     BucketStats stats;
     at::Tensor check_sum;  // check_streams: fp64 [1] checksum of the packed buffer (all-reduced)
@@ -199,6 +215,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void reset_iteration_state();
   // compute stream waits on b's collective (timed when DCP_COMM_TIMING)
   void wait_bucket(Bucket& b, hipStream_t cur, bool timed);
+  void sync_slice_locked(Bucket& b, size_t s);
+  void finish_slices(Bucket& b);
   void sync_locked(Bucket& b);
 
   std::vector<at::Tensor> params_;

@@ -58,13 +58,20 @@ def fresh_bf16_shadow(p: torch.Tensor) -> Optional[torch.Tensor]:
     return None
 
 
-def _overlap_chunks(opt):
+def _overlap_chunks(opt, ranges_ok: bool = False):
     """Optimizer overlap (``DistributedDataParallel(overlap_optimizer=True)``):
     when a DDP left bucket reductions deferred, the step runs in chunks —
     first every parameter outside those buckets, then bucket by bucket in
     launch order, each right after the compute stream is ordered behind that
     bucket's collective (``sync``) — so the updates of the early buckets run
-    while the last ones are still being reduced. None when nothing is deferred."""
+    while the last ones are still being reduced. None when nothing is deferred.
+
+    Chunks are ``(sync, ids, ranges)``. With ``ranges_ok`` (an optimizer that
+    can update part of a parameter: Adam / AdamW) a bucket the Reducer
+    reduced slice by slice (``bucket_slice_mb``: GPT-2's 147 MB tied
+    embedding) gives one chunk per slice: the parameters wholly inside the
+    slice in ``ids``, and ``ranges`` = {id(p): (lo, hi)} — the flat element
+    range of each parameter the slice only partly covers, in slice order."""
     from ..parallel import ddp as _ddp
 
     chunks, covered = [], set()
@@ -73,24 +80,54 @@ def _overlap_chunks(opt):
         for k in d.reducer.deferred_buckets():
             if plan is None:
                 plan = d.reducer.bucket_indices()
-            ids = {id(d._params[i]) for i in plan[k]}
-            chunks.append((lambda d=d, k=k: d.reducer.sync_bucket(k), ids))
+            ps = [d._params[i] for i in plan[k]]
+            ids = {id(p) for p in ps}
             covered |= ids
+            bounds = d.reducer.bucket_slice_bounds(k) if ranges_ok else []
+            if not bounds:
+                chunks.append((lambda d=d, k=k: d.reducer.sync_bucket(k), ids, None))
+                continue
+            ns = len(bounds) - 1
+            whole = [set() for _ in range(ns)]
+            part = [{} for _ in range(ns)]
+            o, s = 0, 0
+            for p in ps:  # the bucket's flat layout: parameters back to back
+                n = p.numel()
+                while s < ns - 1 and bounds[s + 1] <= o:
+                    s += 1
+                t = s
+                while t < ns - 1 and bounds[t + 1] < o + n:
+                    t += 1
+                if t == s:
+                    whole[s].add(id(p))
+                else:
+                    for u in range(s, t + 1):
+                        part[u][id(p)] = (max(o, bounds[u]) - o, min(o + n, bounds[u + 1]) - o)
+                o += n
+            for u in range(ns):
+                chunks.append((lambda d=d, k=k, u=u: d.reducer.sync_bucket_slice(k, u), whole[u], part[u]))
     if not chunks:
         return None
-    mine = {id(p) for g in opt.param_groups for p in g["params"]}
-    return [(None, mine - covered)] + [(sync, ids & mine) for sync, ids in chunks]
+    mine = {id(g_p) for g in opt.param_groups for g_p in g["params"]}
+    out = [(None, mine - covered, None)]
+    for sync, ids, ranges in chunks:
+        out.append((sync, ids & mine, {i: r for i, r in ranges.items() if i in mine} if ranges else None))
+    return out
 
 
-def _run_chunks(opt, impl, grad_scale) -> list:
+def _run_chunks(opt, impl, grad_scale, ranged=None) -> list:
     """``impl(ids, grad_scale)`` over the overlap chunks (one call with ids =
-    None when nothing is deferred); the list of its results."""
+    None when nothing is deferred), and ``ranged(ranges, grad_scale)`` for
+    the partial-parameter ranges of sliced buckets (optimizers that pass
+    one); the list of the results."""
     out = []
-    for sync, ids in _overlap_chunks(opt) or [(None, None)]:
+    for sync, ids, ranges in _overlap_chunks(opt, ranged is not None) or [(None, None, None)]:
         if sync is not None:
             sync()
         if ids is None or ids:
             out.append(impl(ids, grad_scale))
+        if ranges:
+            out.append(ranged(ranges, grad_scale))
     return out
 
 
@@ -256,7 +293,7 @@ class Adam(_DropsDeferred, Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        shadowed = [p for sh in _run_chunks(self, self._step, grad_scale) for p in sh]
+        shadowed = [p for sh in _run_chunks(self, self._step, grad_scale, self._step_ranges) for p in sh]
         _PARAM_EPOCH[0] += 1
         for p in shadowed:  # rewritten by the kernel: valid for the new epoch
             e = _BF16_SHADOWS[p]
@@ -319,6 +356,57 @@ class Adam(_DropsDeferred, Optimizer):
                 _C.fused_adam(bk.p, g, bk.m, bk.v, bk.vm, group["lr"], b1, b2, group["eps"], group["weight_decay"],
                               step, ams, group["decoupled_weight_decay"], group["maximize"], grad_scale, bk.s, bk.st)
                 shadowed.extend(bk.shadowed)
+        return shadowed
+
+    def _step_ranges(self, ranges, grad_scale):
+        """Update flat element ranges of parameters (``ranges`` = {id(p): (lo,
+        hi)}, overlap chunks of a bucket reduced slice by slice): Adam is
+        elementwise, so a range update with the parameter's step equals the
+        whole-tensor update on those elements. The step counter advances at
+        the range starting at 0 (ranges come in slice order). A parameter that
+        cannot be updated in ranges (no state yet, capturable, non-contiguous)
+        is updated whole at its last range, when all its slices have landed.
+        Returns the parameters whose bf16 shadow the kernel rewrote."""
+        shadowed = []
+        where = {}
+        for group in self.param_groups:
+            for p in group["params"]:
+                if id(p) in ranges:
+                    where[id(p)] = (group, p)
+        for pid, (lo, hi) in ranges.items():
+            if pid not in where:
+                continue
+            group, p = where[pid]
+            g = _grad(p)
+            if g is None:
+                continue
+            st = self.state[p]
+            last = hi == p.numel()
+            ams = group["amsgrad"]
+            ok = (len(st) > 0 and not group.get("capturable", False) and not st["step"].is_cuda
+                  and p.is_contiguous() and g.is_contiguous() and not g.is_sparse
+                  and st["exp_avg"].is_contiguous() and st["exp_avg_sq"].is_contiguous()
+                  and (not ams or st["max_exp_avg_sq"].is_contiguous()))
+            sh = _BF16_SHADOWS.get(p) if p.is_cuda else None
+            if ok and sh is not None and not sh[0].is_contiguous():
+                ok = False
+            if not ok:
+                if last:
+                    shadowed.extend(self._step({pid}, grad_scale))
+                continue
+            if lo == 0:
+                st["step"].add_(1.0)  # in place: the value a cached plan's flat counters share
+            b1, b2 = group["betas"]
+
+            def r(t):
+                return t.view(-1)[lo:hi]
+
+            _C.fused_adam([r(p)], [r(g)], [r(st["exp_avg"])], [r(st["exp_avg_sq"])],
+                          [r(st["max_exp_avg_sq"])] if ams else [], group["lr"], b1, b2, group["eps"],
+                          group["weight_decay"], float(st["step"]), ams, group["decoupled_weight_decay"],
+                          group["maximize"], grad_scale, [r(sh[0])] if sh is not None else [], [])
+            if sh is not None and last:
+                shadowed.append(p)
         return shadowed
 
     def _adam_one(self, plist, grads, i, step, group, b1, b2, ams, grad_scale):

@@ -166,7 +166,7 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_mb: Optional[float] = None, comm_dtype: Optional[torch.dtype] = None,
                  rebuild_buckets: bool = True, init_sync: bool = True, tail_bucket_mb: Optional[float] = None,
                  register_buckets: bool = False, overlap_optimizer: bool = False, defer_accum_wgrad: bool = False,
-                 overlap_buffer_sync: bool = True):
+                 overlap_buffer_sync: bool = True, bucket_slice_mb: Optional[float] = None):
         super().__init__()
         self.module = module
         self.process_group = process_group if process_group is not None else dist.get_default_group()
@@ -291,6 +291,19 @@ class DistributedDataParallel(nn.Module):
         # (static_graph: deferred from the second iteration on, when every
         # parameter was used somewhere in the first)
         opts.defer_grad_wait = self.overlap_optimizer
+        # bucket_slice_mb (overlap_optimizer): a bucket over 1.5x this size is
+        # reduced as several collectives over slices of its buffer, and the
+        # fused Adam updates each slice's parameter ranges as soon as that
+        # slice lands — the single-parameter tied-embedding buckets (GPT-2
+        # 147 MB, BERT 89 MB) are ready last, so otherwise their whole
+        # reduction is exposed before their update can start. Default: the
+        # bucket cap, at least 4 MB; 0 = one collective per bucket.
+        if bucket_slice_mb is None:
+            bucket_slice_mb = max(self.bucket_bytes_cap / 2**20, 4.0) if self.overlap_optimizer else 0.0
+        if bucket_slice_mb < 0:
+            raise ValueError(f"DistributedDataParallel: bucket_slice_mb must be >= 0, got {bucket_slice_mb}")
+        self.bucket_slice_bytes = int(bucket_slice_mb * 2**20) if self.overlap_optimizer else 0
+        opts.slice_bytes = self.bucket_slice_bytes
         # defer_accum_wgrad: under no_sync the Linear weight gradients of the
         # micro-steps are not computed one by one; the synchronising micro-step
         # computes each over all micro-steps' rows in one launch (ops/linear.py

@@ -528,3 +528,73 @@ def _buffer_load(rank, world):
 
 def test_load_state_dict_not_overwritten_by_pending_broadcast():
     run_world(_buffer_load, 2)
+
+
+class _EmbNet(nn.Module):
+    """A tied-embedding-like net: one big parameter (the embedding, its own
+    oversize bucket) and a few mid-size ones that straddle slice bounds."""
+
+    def __init__(self):
+        super().__init__()
+        self.emb = nn.Embedding(3000, 64)              # 768 KB
+        self.l1 = nn.Linear(64, 700)                   # ~179 KB + bias
+        self.l2 = nn.Linear(700, 300)                  # ~820 KB
+
+    def forward(self, idx):
+        h = self.emb(idx).mean(1)
+        h = torch.tanh(self.l1(h))
+        return F.log_softmax(self.l2(h), -1)
+
+
+def _sliced(rank, world, cap_mb, slice_mb):
+    """bucket_slice_mb: oversize buckets reduced slice by slice, fused AdamW
+    updating each slice's parameter ranges (and whole parameters) as the
+    slice lands — bit for bit the unsliced overlap run (Adam is elementwise),
+    within Adam's reduction-order sensitivity of torch DDP + torch AdamW, the
+    sliced buckets really issued as several collectives, nothing left
+    deferred after the step, every step counter advanced once per step
+    (VERDICT r5 Next 3c)."""
+    import distributed_compute_pytorch_amd as dcp
+
+    tdist = _init_torch_pg(rank, world)
+    torch.manual_seed(0)
+    base = _EmbNet()
+    runs, sliced = {}, []
+    for sm in (0.0, slice_mb, None):
+        m = copy.deepcopy(base)
+        if sm is None:
+            model = nn.parallel.DistributedDataParallel(m, bucket_cap_mb=cap_mb)
+            opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
+        else:
+            model = dcp.parallel.DistributedDataParallel(m, gradient_as_bucket_view=True, overlap_optimizer=True,
+                                                         bucket_cap_mb=cap_mb, bucket_slice_mb=sm)
+            opt = dcp.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
+        g = torch.Generator().manual_seed(11 + rank)
+        for it in range(4):
+            idx = torch.randint(0, 3000, (16, 5), generator=g)
+            y = torch.randint(0, 300, (16,), generator=g)
+            opt.zero_grad(set_to_none=True)
+            F.nll_loss(model(idx), y).backward()
+            if sm:
+                ks = model.reducer.deferred_buckets()
+                sliced.append(sum(len(model.reducer.bucket_slice_bounds(k)) > 2 for k in ks))
+            opt.step()
+            if sm is not None:
+                assert model.reducer.deferred_buckets() == []
+        if sm is not None:
+            assert all(float(opt.state[q]["step"]) == 4.0 for q in m.parameters())
+        runs[sm] = [p.detach().clone() for p in m.parameters()]
+    assert sliced[0] == 0 and all(n >= 1 for n in sliced[1:]), sliced  # the first iteration is never deferred
+    names = [n for n, _ in base.named_parameters()]
+    for n, a, b in zip(names, runs[0.0], runs[slice_mb]):
+        torch.testing.assert_close(b, a, rtol=0, atol=0, msg=n)
+    for n, a, b in zip(names, runs[None], runs[slice_mb]):
+        # Adam turns near-zero gradients into full-size steps: the reduction
+        # order (ours vs gloo) shows at ~1e-5 on a few embedding rows
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-4, msg=n)
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cap_mb,slice_mb", [(0.25, 0.25), (4.0, 0.2)])
+def test_sliced_buckets_match_torch(cap_mb, slice_mb):
+    run_world(_sliced, 2, cap_mb, slice_mb)
