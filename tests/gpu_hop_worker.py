@@ -97,8 +97,14 @@ def main():
                      ("grad_view", {"gradient_as_bucket_view": True}),
                      ("registered", {"gradient_as_bucket_view": True, "register_buckets": True}),
                      ("bf16_hook", {"hook": dcp.parallel.comm_hooks.bf16_compress_hook}),
-                     ("overlap", {"gradient_as_bucket_view": True, "overlap_optimizer": True})):
+                     ("overlap", {"gradient_as_bucket_view": True, "overlap_optimizer": True}),
+                     # fc1.weight (4.7 MB) reduced as 24 slice collectives
+                     ("overlap_sliced", {"gradient_as_bucket_view": True, "overlap_optimizer": True,
+                                         "bucket_slice_mb": 0.2}),
+                     ("overlap_sliced_adam", {"gradient_as_bucket_view": True, "overlap_optimizer": True,
+                                              "bucket_slice_mb": 0.2, "adam": True})):
         hook = kw.pop("hook", None)
+        adam = kw.pop("adam", False)
         local = ConvNet().to(dev)
         local.load_state_dict(base.state_dict())
         mine = ConvNet().to(dev)
@@ -107,8 +113,12 @@ def main():
         if hook is not None:
             ddp.register_comm_hook(None, hook)
         local.eval(), mine.eval()
-        o1 = torch.optim.SGD(local.parameters(), lr=0.05, momentum=0.9)
-        o2 = dcp.optim.SGD(ddp.parameters(), lr=0.05, momentum=0.9)
+        if adam:  # the per-slice parameter-range updates
+            o1 = torch.optim.AdamW(local.parameters(), lr=1e-3)
+            o2 = dcp.optim.AdamW(ddp.parameters(), lr=1e-3)
+        else:
+            o1 = torch.optim.SGD(local.parameters(), lr=0.05, momentum=0.9)
+            o2 = dcp.optim.SGD(ddp.parameters(), lr=0.05, momentum=0.9)
         gen = torch.Generator().manual_seed(3)
         for it in range(3):
             xs = [torch.randn(16, 1, 28, 28, generator=gen).to(dev) for _ in range(2)]

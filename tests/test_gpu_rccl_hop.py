@@ -37,6 +37,8 @@ def test_single_rank_hop_real_rccl(cuda):
     assert errs["bf16_wire"] < 5e-2, errs  # bf16 gradients on the wire
     assert errs["bf16_hook"] < 5e-2, errs  # the same through bf16_compress_hook (async cast back)
     assert errs["overlap"] < 1e-5, errs  # optimizer synced bucket by bucket (overlap_optimizer)
+    assert errs["overlap_sliced"] < 1e-5, errs  # oversize bucket as slice collectives (bucket_slice_mb)
+    assert errs["overlap_sliced_adam"] < 1e-4, errs  # fused AdamW on the slices' parameter ranges
     assert errs["fp32_buckets"] >= 2
     assert errs["registered"] < 1e-5, errs  # bucket buffers registered with ncclCommRegister
     assert res["register_handle"] > 0 and res["registered_allreduce_ok"]
