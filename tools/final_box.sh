@@ -8,7 +8,7 @@ TAG=${TAG:-r4_final_box}; MODELS=${MODELS:-"resnet50 gpt2 bert convnet"}; STEPS=
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
 mkdir -p "$O"
 for m in $MODELS; do
-  for impl in ours torch; do
+  for impl in ${IMPLS:-ours torch}; do
     timeout -k 10 ${RUN_TIMEOUT:-500} python3 -u bench.py --model "$m" --impl "$impl" --steps "$STEPS" --warmup 8 \
       > "$O/${TAG}_run.log" 2>&1 || { echo "[final_box] $m $impl failed"; tail -20 "$O/${TAG}_run.log"; exit 1; }
     grep '^{' "$O/${TAG}_run.log" | tail -1 | python3 -c "
