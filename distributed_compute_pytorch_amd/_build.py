@@ -84,6 +84,20 @@ def _flags():
     return cxx, hip
 
 
+# per-source extra compile flags (relative to csrc/)
+_FILE_FLAGS = {
+    # the attention kernels feed MFMA outputs to fmaxf: under IEEE NaN
+    # handling hipcc quiets each operand first (one v_max x, x per score —
+    # 33 of the forward's ~500 VALU instructions per key block, in a
+    # VALU-bound loop); nothing in the file depends on NaN semantics
+    "kernels/attention.hip": ["-fno-honor-nans"],
+}
+
+
+def _file_flags(src: Path) -> list:
+    return _FILE_FLAGS.get(str(src.relative_to(CSRC)), [])
+
+
 def _link_cmd(objs, out):
     _, lib = _torch_paths()
     return (
@@ -136,6 +150,7 @@ def source_digest() -> str:
         h.update(p.read_bytes())
     cxx, hip = _flags()
     h.update(" ".join(cxx + hip).replace(str(CSRC), "<csrc>").encode())
+    h.update(repr(sorted(_FILE_FLAGS.items())).encode())
     return h.hexdigest()
 
 
@@ -193,7 +208,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     tasks = []
     objs = []
     for src in _sources():
-        cmd = hip if src.suffix == ".hip" else cxx
+        cmd = (hip if src.suffix == ".hip" else cxx) + _file_flags(src)
         obj = _obj_for(src, cmd, hdr)
         objs.append(obj)
         if force or not obj.exists():
