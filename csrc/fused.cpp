@@ -1126,6 +1126,7 @@ kern::AttnTensor attn_view(const at::Tensor& t, const char* what) {
             ": bf16 [B, T, H*64] tensor with unit last stride required");
   DK_CHECK(t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
             what, ": rows must be 16-byte aligned");
+  DK_CHECK(t.stride(1) < (int64_t(1) << 24), what, ": row stride too large (32-bit DMA offsets within a 64-row slab)");
   return kern::AttnTensor{t.data_ptr(), t.stride(0), t.stride(1)};
 }
 kern::AttnOut attn_out(const at::Tensor& t, const char* what) {

@@ -101,22 +101,27 @@ __device__ __forceinline__ bf16x8 tr_op(const char* base, int rbase, int dcol0, 
 // the NEXT tile's DMA to land in the middle of its own compute (PMC r5: 0.3 of
 // wave cycles waiting, MFMA busy 0.14-0.22). Hidden, the ring is ordered by
 // the explicit wait_vm0 + barrier at the top of each iteration only. M0 is
-// compiler-reserved: set and restored in-statement.
+// compiler-reserved: set and restored in-statement. The source is a
+// wave-uniform 64-bit base in SGPRs plus a 32-bit per-lane byte offset
+// (saddr form): the per-lane part of a tile's source is
+// loop-invariant, so each DMA costs no VALU address arithmetic (the 64-bit
+// per-lane pointer form recomputed row × stride with two v_mad_u64_u32 and
+// moves per DMA, ~20 VALU per key block)
 __device__ __forceinline__ uint32_t lds_u32(const char* p) {
   return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
 }
-__device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, char* lds_dst) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(src), "s"(lds_u32(lds_dst))
+               : "v"(voff), "s"(sbase), "s"(lds_u32(lds_dst))
                : "memory");
 }
-__device__ __forceinline__ void glds4(const void* src, char* lds_dst) {
+__device__ __forceinline__ void glds4s(const void* sbase, uint32_t voff, char* lds_dst) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(src), "s"(lds_u32(lds_dst))
+               : "v"(voff), "s"(sbase), "s"(lds_u32(lds_dst))
                : "memory");
 }
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -127,14 +132,27 @@ __device__ __forceinline__ void barrier() {
 }
 
 // DMA rows [r0, r0+64) of a strided [T][64] head slice into a tile image;
-// 4 waves × 2 wave-instructions of 1 KiB (8 rows each).
-__device__ __forceinline__ void stage_tile(const uint16_t* src, int64_t st, int r0, char* dst, int wave, int lane) {
+// 4 waves × 2 wave-instructions of 1 KiB (8 rows each). TileOff: this lane's
+// byte offsets within the 64-row slab (row u / 8, swizzled chunk), computed
+// once per tensor; the slab base src + r0 · st is wave-uniform.
+struct TileOff {
+  uint32_t o[2];
+};
+__device__ __forceinline__ TileOff tile_off(int64_t st, int wave, int lane) {
+  TileOff t;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int u = (wave * 2 + j) * 64 + lane;  // 16-B unit of the image
     const int r = u >> 3, lc = (u & 7) ^ swz(u >> 3);
-    glds16(src + static_cast<int64_t>(r0 + r) * st + lc * 8, dst + (wave * 2 + j) * 1024);
+    t.o[j] = static_cast<uint32_t>((r * st + lc * 8) * 2);
   }
+  return t;
+}
+__device__ __forceinline__ void stage_tile(const uint16_t* src, int64_t st, int r0, const TileOff& to, char* dst,
+                                           int wave) {
+  const uint16_t* base = src + static_cast<int64_t>(r0) * st;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) glds16s(base, to.o[j], dst + (wave * 2 + j) * 1024);
 }
 
 // ---- dropout: 8 random bits per element (q, key) — byte thresholds, the
@@ -185,7 +203,15 @@ __device__ __forceinline__ uint32_t keep_bytes(uint32_t h, uint32_t tb, uint32_t
 // byte 1 / 3 of src1 (= t: keys 1, 3) and of src0 (= t << 8: keys 0, 2).
 __device__ __forceinline__ uint32_t pair_mask01(uint32_t t) { return __builtin_amdgcn_perm(t << 8, t, 0x08080A0Au); }
 __device__ __forceinline__ uint32_t pair_mask23(uint32_t t) { return __builtin_amdgcn_perm(t << 8, t, 0x09090B0Bu); }
-// all-ones / zero from bit `pos` of w (v_bfe_i32)
+// all-ones / zero from bit `pos` of w: one v_bfe_i32 (asm: with a constant
+// pos hipcc turned the builtin into and + compare + cndmask, three VALU per
+// element of the dQ kernel)
+template <int POS>
+__device__ __forceinline__ uint32_t bit_mask_c(uint32_t w) {
+  uint32_t r;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(w), "n"(POS));
+  return r;
+}
 __device__ __forceinline__ uint32_t bit_mask(uint32_t w, uint32_t pos) {
   return static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(w), pos, 1));
 }
@@ -273,11 +299,12 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
   int nkb = T / kKB;
   if (CAUSAL) nkb = min(nkb, (tile * 128 + 128 + kKB - 1) / kKB);
 
+  const TileOff ko = tile_off(K.st, wave, lane), vo = tile_off(V.st, wave, lane);
   auto issue = [&](int it) {
     if (it >= nkb) return;
     char* base = lds + (it & 1) * 2 * kTile;
-    stage_tile(K.p, K.st, it * kKB, base, wave, lane);
-    stage_tile(V.p, V.st, it * kKB, base + kTile, wave, lane);
+    stage_tile(K.p, K.st, it * kKB, ko, base, wave);
+    stage_tile(V.p, V.st, it * kKB, vo, base + kTile, wave);
   };
   issue(0);
   for (int it = 0; it < nkb; ++it) {
@@ -439,11 +466,12 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
   // this lane's keep words (one per key block, stride 2T), one block ahead
   const uint32_t* MW = P.mask + mask_word(bh, T / kKB, 0, hh, T, qok ? qi : 0);
   uint32_t wnext = DROP ? MW[0] : 0u;
+  const TileOff ko = tile_off(K.st, wave, lane), vo = tile_off(V.st, wave, lane);
   auto issue = [&](int it) {
     if (it >= nkb) return;
     char* base = lds + (it & 1) * 2 * kTile;
-    stage_tile(K.p, K.st, it * kKB, base, wave, lane);
-    stage_tile(V.p, V.st, it * kKB, base + kTile, wave, lane);
+    stage_tile(K.p, K.st, it * kKB, ko, base, wave);
+    stage_tile(V.p, V.st, it * kKB, vo, base + kTile, wave);
   };
   issue(0);
   for (int it = 0; it < nkb; ++it) {
@@ -479,7 +507,18 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
         float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lse2));
         if (CAUSAL && diag) p = key > qi ? 0.f : p;
         float g = dp[r];
-        if (DROP) g = and_mask(g, bit_mask(wk, 8 * (r & 3) + (r >> 2)));
+        if (DROP) {
+          uint32_t km;
+          switch (r) {  // bit 8e + g of key (r & 3) + 8(r >> 2): r = 4g + e
+#define DK_BM(R) \
+  case R: km = bit_mask_c<8 * ((R) & 3) + ((R) >> 2)>(wk); break;
+            DK_BM(0) DK_BM(1) DK_BM(2) DK_BM(3) DK_BM(4) DK_BM(5) DK_BM(6) DK_BM(7)
+            DK_BM(8) DK_BM(9) DK_BM(10) DK_BM(11) DK_BM(12) DK_BM(13) DK_BM(14) DK_BM(15)
+#undef DK_BM
+            default: km = 0;
+          }
+          g = and_mask(g, km);
+        }
         // dSᵀ (without the softmax scale); the keep scale rides in the fma
         s[r] = p * (DROP ? fmaf(g, inv_keep, -dlt) : g - dlt);
       }
@@ -551,23 +590,24 @@ __global__ void __launch_bounds__(kT) attn_bwd_dkv_kernel(AttnParams P, AttnTens
   f32x16 dka[2] = {zero16(), zero16()}, dva[2] = {zero16(), zero16()};
   const int qt0 = CAUSAL ? kb0 / kKB : 0;  // first query tile that can see these keys
   const int nqt = T / kKB;
+  const TileOff qo = tile_off(Q.st, wave, lane), go = tile_off(G.st, wave, lane);
   auto issue = [&](int it) {
     if (qt0 + it >= nqt) return;
     const int qb = (qt0 + it) * kKB;
     char* base = lds + (it & 1) * kStage;
-    stage_tile(Q.p, Q.st, qb, base, wave, lane);
-    stage_tile(G.p, G.st, qb, base + kTile, wave, lane);
+    stage_tile(Q.p, Q.st, qb, qo, base, wave);
+    stage_tile(G.p, G.st, qb, go, base + kTile, wave);
     if (wave == 0) {
-      glds4(L + qb + lane, base + 2 * kTile);
-      glds4(DL + qb + lane, base + 2 * kTile + kKB * 4);
+      glds4s(L + qb, lane * 4u, base + 2 * kTile);
+      glds4s(DL + qb, lane * 4u, base + 2 * kTile + kKB * 4);
     }
     if (DROP && (wave == 1 || wave == 2)) {  // the keep words of key block kb0/64 + wave - 1 (if inside T)
       const int kblk = kb0 / kKB + wave - 1;
       if (kblk < nqt) {
-        const uint32_t* src = P.mask + mask_word(bh, nqt, kblk, 0, T, qb + lane);
+        const uint32_t* src = P.mask + mask_word(bh, nqt, kblk, 0, T, qb);
         char* dst = base + 2 * kTile + 2 * kKB * 4 + (wave - 1) * 2 * kKB * 4;
-        glds4(src, dst);
-        glds4(src + T, dst + kKB * 4);
+        glds4s(src, lane * 4u, dst);
+        glds4s(src + T, lane * 4u, dst + kKB * 4);
       }
     }
   };
