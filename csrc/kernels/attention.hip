@@ -61,6 +61,10 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   const bf16x2 v = {static_cast<__bf16>(a), static_cast<__bf16>(b)};
   return __builtin_bit_cast(uint32_t, v);
 }
+// an all-ones bf16 operand fragment (1.0 = 0x3F80)
+__device__ __forceinline__ bf16x8 ones_frag() {
+  return __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
+}
 // registers 8s … 8s+7 of an accumulator → bf16 operand fragment of k-step s
 __device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
   const uint4 u = make_uint4(pack2(a[8 * s + 0], a[8 * s + 1]), pack2(a[8 * s + 2], a[8 * s + 3]),
@@ -345,17 +349,19 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
     // (every wave's first block holds key 0 ≤ its queries: mx is finite from there on)
     const float alpha = __builtin_amdgcn_exp2f((m - mx) * c);
     const float nmc = -mx * c;
-    float rs = 0.f;
+    float rs = 0.f;  // without dropout: the row sum on the VALU (the 16 accumulator
+                     // registers of the MFMA sum below would cost a wave per SIMD)
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pp = __builtin_amdgcn_exp2f(fmaf(s[kh][r], c, nmc));
-        s[kh][r] = pp;
-        rs += pp;
+        s[kh][r] = __builtin_amdgcn_exp2f(fmaf(s[kh][r], c, nmc));
+        if (!DROP) rs += s[kh][r];
       }
-    rs += __shfl_xor(rs, 32);
-    l = l * alpha + rs;
+    if (!DROP) {
+      rs += __shfl_xor(rs, 32);
+      l = l * alpha + rs;
+    }
     m = mx;
     if (!__all(alpha == 1.f)) {  // the running max moved in some lane: rescale O
 #pragma unroll
@@ -367,6 +373,12 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
     // end): registers 4g … 4g+3 hold keys 4j … 4j+3, one random word each →
     // the four keep bits (SWAR), the two bf16-pair masks ANDed onto the
     // packed P, and this lane's keep word of the block for the backward
+    // With dropout the row sum of P runs on the (otherwise mostly idle)
+    // matrix pipe: ones · P over each 16-key step, every output row the key
+    // sum of its query column — 4 MFMAs per block instead of 32 VALU adds and
+    // a cross-lane shuffle in this VALU-bound loop. It sums the bf16 P that
+    // P·V uses, before the dropout mask (the softmax normaliser).
+    f32x16 lsum = zero16();
     uint32_t word = 0;
     uint32_t xs = DROP ? drop_state(kbh, qi, it, hh) : 0u;  // word j = xs after j steps, ^ weyl(j)
 #pragma unroll
@@ -375,6 +387,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
       for (int sg = 0; sg < 2; ++sg) {
         uint4 u = make_uint4(pack2(s[kh][8 * sg + 0], s[kh][8 * sg + 1]), pack2(s[kh][8 * sg + 2], s[kh][8 * sg + 3]),
                              pack2(s[kh][8 * sg + 4], s[kh][8 * sg + 5]), pack2(s[kh][8 * sg + 6], s[kh][8 * sg + 7]));
+        if (DROP) lsum = mfma(ones_frag(), __builtin_bit_cast(bf16x8, u), lsum);
         if (DROP) {
           const int g0 = 2 * sg, j0 = 4 * kh + g0;
           const uint32_t t0 = keep_bytes(xs ^ drop_weyl(j0), tb, ta);
@@ -392,6 +405,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
         for (int dh = 0; dh < 2; ++dh) oacc[dh] = mfma(tr_op(sV, 32 * kh + 16 * sg, 32 * dh, lane), pf, oacc[dh]);
       }
     if (DROP && qok) P.mask[mask_word(bh, T / kKB, it, hh, T, qi)] = word;
+    if (DROP) l = l * alpha + lsum[0];
   }
   if (qok) {
     const float inv = (DROP ? drop_scale(thr) : 1.f) / l;
