@@ -546,7 +546,7 @@ class _EmbNet(nn.Module):
         return F.log_softmax(self.l2(h), -1)
 
 
-def _sliced(rank, world, cap_mb, slice_mb):
+def _sliced(rank, world, cap_mb, slice_mb, wire=None):
     """bucket_slice_mb: oversize buckets reduced slice by slice, fused AdamW
     updating each slice's parameter ranges (and whole parameters) as the
     slice lands — bit for bit the unsliced overlap run (Adam is elementwise),
@@ -567,7 +567,8 @@ def _sliced(rank, world, cap_mb, slice_mb):
             opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
         else:
             model = dcp.parallel.DistributedDataParallel(m, gradient_as_bucket_view=True, overlap_optimizer=True,
-                                                         bucket_cap_mb=cap_mb, bucket_slice_mb=sm)
+                                                         bucket_cap_mb=cap_mb, bucket_slice_mb=sm,
+                                                         **({"comm_dtype": wire} if wire is not None else {}))
             opt = dcp.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
         g = torch.Generator().manual_seed(11 + rank)
         for it in range(4):
@@ -588,13 +589,20 @@ def _sliced(rank, world, cap_mb, slice_mb):
     names = [n for n, _ in base.named_parameters()]
     for n, a, b in zip(names, runs[0.0], runs[slice_mb]):
         torch.testing.assert_close(b, a, rtol=0, atol=0, msg=n)
-    for n, a, b in zip(names, runs[None], runs[slice_mb]):
-        # Adam turns near-zero gradients into full-size steps: the reduction
-        # order (ours vs gloo) shows at ~1e-5 on a few embedding rows
-        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-4, msg=n)
+    if wire is None:
+        for n, a, b in zip(names, runs[None], runs[slice_mb]):
+            # Adam turns near-zero gradients into full-size steps: the reduction
+            # order (ours vs gloo) shows at ~1e-5 on a few embedding rows
+            torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-4, msg=n)
     tdist.destroy_process_group()
 
 
 @pytest.mark.parametrize("cap_mb,slice_mb", [(0.25, 0.25), (4.0, 0.2)])
 def test_sliced_buckets_match_torch(cap_mb, slice_mb):
     run_world(_sliced, 2, cap_mb, slice_mb)
+
+
+def test_sliced_buckets_bf16_wire():
+    """The same with a bf16 wire: each slice unpacks its own range of the
+    compressed buffer when it is synced (bit for bit the unsliced run)."""
+    run_world(_sliced, 2, 4.0, 0.2, torch.bfloat16)
