@@ -1162,15 +1162,17 @@ bool attn_ok(int64_t T, int64_t C, int64_t heads) {
 // o [B, T, H*64] (contiguous), lse [B*H, T] fp32 (log2 domain), keep bits
 // (int32 [attn_mask_words], T²/8 bytes per head; empty without dropout)
 std::vector<at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t heads,
-                                       bool causal, double p_drop, int64_t seed) {
+                                       bool causal, double p_drop, int64_t seed, bool keep_bits) {
   same_shape(q, k, "flash_attn_fwd");
   same_shape(q, v, "flash_attn_fwd");
   c10::hip::HIPGuard guard(q.device().index());
   kern::AttnParams p = attn_params(q, heads, causal, p_drop, seed);
   at::Tensor o = at::empty(q.sizes(), q.options().memory_format(at::MemoryFormat::Contiguous));
   at::Tensor lse = at::empty({q.size(0) * heads, q.size(1)}, q.options().dtype(at::kFloat));
-  at::Tensor mask = at::empty({p.p_drop > 0.f ? kern::attn_mask_words(p.B, p.H, p.T) : 0}, q.options().dtype(at::kInt));
-  if (p.p_drop > 0.f) p.mask = reinterpret_cast<uint32_t*>(mask.data_ptr<int32_t>());
+  // the keep bits only when a backward will read them (T²/8 bytes per head)
+  const bool store = p.p_drop > 0.f && keep_bits;
+  at::Tensor mask = at::empty({store ? kern::attn_mask_words(p.B, p.H, p.T) : 0}, q.options().dtype(at::kInt));
+  if (store) p.mask = reinterpret_cast<uint32_t*>(mask.data_ptr<int32_t>());
   kern::attn_fwd(p, attn_view(q, "q"), attn_view(k, "k"), attn_view(v, "v"), attn_out(o, "o"), lse.data_ptr<float>(),
                  stream_of(q));
   return {o, lse, mask};
@@ -1830,7 +1832,7 @@ void bind(pybind11::module& m) {
         pybind11::arg("accumulate_into") = pybind11::none());
   m.def("flash_attn_fwd", &flash_attn_fwd, "MFMA flash attention forward (head dim 64)", pybind11::arg("q"),
         pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("heads"), pybind11::arg("causal"),
-        pybind11::arg("p_drop"), pybind11::arg("seed"));
+        pybind11::arg("p_drop"), pybind11::arg("seed"), pybind11::arg("keep_bits") = true);
   m.def("flash_attn_bwd", &flash_attn_bwd, "MFMA flash attention backward into dq/dk/dv");
   m.def("conv_fwd", &conv_fwd, "kxk NHWC conv forward (implicit-GEMM MFMA) [+ output BN sums]", pybind11::arg("x"),
         pybind11::arg("wt"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("stride"), pybind11::arg("pad"),

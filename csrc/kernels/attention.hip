@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
 #pragma unroll
         for (int dh = 0; dh < 2; ++dh) oacc[dh] = mfma(tr_op(sV, 32 * kh + 16 * sg, 32 * dh, lane), pf, oacc[dh]);
       }
-    if (DROP && qok) P.mask[mask_word(bh, T / kKB, it, hh, T, qi)] = word;
+    if (DROP && qok && P.mask != nullptr) P.mask[mask_word(bh, T / kKB, it, hh, T, qi)] = word;
     if (DROP) l = l * alpha + lsum[0];
   }
   if (qok) {

@@ -28,7 +28,8 @@ struct AttnParams {
   float p_drop;      // dropout probability on P (0 = off)
   uint64_t seed;
   // dropout keep bits, [B*H][T/64][2][T] uint32 (attn_mask_words): written by
-  // the forward, read by the backward; unused when p_drop == 0
+  // the forward (unless null: no backward will run), read by the backward;
+  // unused when p_drop == 0
   uint32_t* mask;
 };
 

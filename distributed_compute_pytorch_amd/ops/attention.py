@@ -32,8 +32,8 @@ def attn_supported(x: torch.Tensor, heads: int) -> bool:
 
 class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, heads, causal, p_drop, seed):
-        o, lse, keep = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed)
+    def forward(ctx, q, k, v, heads, causal, p_drop, seed, keep_bits):
+        o, lse, keep = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed, keep_bits)
         ctx.save_for_backward(q, k, v, o, lse, keep)
         ctx.cfg = (heads, causal, p_drop, seed)
         return o
@@ -48,15 +48,15 @@ class _FlashAttnFn(torch.autograd.Function):
         dq, dk, dv = torch.empty_like(q, memory_format=torch.contiguous_format), torch.empty_like(
             k, memory_format=torch.contiguous_format), torch.empty_like(v, memory_format=torch.contiguous_format)
         _C.flash_attn_bwd(do, q, k, v, o, lse, keep, heads, causal, p_drop, seed, dq, dk, dv)
-        return dq, dk, dv, None, None, None, None
+        return dq, dk, dv, None, None, None, None, None
 
 
 class _FlashAttnQKVFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, heads, causal, p_drop, seed):
+    def forward(ctx, qkv, heads, causal, p_drop, seed, keep_bits):
         C = qkv.shape[2] // 3
         q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
-        o, lse, keep = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed)
+        o, lse, keep = _C.flash_attn_fwd(q, k, v, heads, causal, p_drop, seed, keep_bits)
         ctx.save_for_backward(qkv, o, lse, keep)
         ctx.cfg = (heads, causal, p_drop, seed)
         return o
@@ -73,19 +73,26 @@ class _FlashAttnQKVFn(torch.autograd.Function):
         q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
         dq, dk, dv = dqkv[..., :C], dqkv[..., C:2 * C], dqkv[..., 2 * C:]
         _C.flash_attn_bwd(do, q, k, v, o, lse, keep, heads, causal, p_drop, seed, dq, dk, dv)
-        return dqkv, None, None, None, None
+        return dqkv, None, None, None, None, None
 
 
 def flash_attn(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, causal: bool = False,
                dropout_p: float = 0.0, seed: int = None) -> torch.Tensor:
     """softmax(q kᵀ / 8 [+ causal mask]) → dropout(p) → · v, per head of 64."""
-    return _FlashAttnFn.apply(q, k, v, heads, causal, float(dropout_p),
-                              _seed() if seed is None else int(seed))
+    return _FlashAttnFn.apply(q, k, v, heads, causal, float(dropout_p), _seed() if seed is None else int(seed),
+                              _backward_will_run(q, k, v))
 
 
 def flash_attn_qkv(qkv: torch.Tensor, heads: int, causal: bool = False, dropout_p: float = 0.0,
                    seed: int = None) -> torch.Tensor:
-    return _FlashAttnQKVFn.apply(qkv, heads, causal, float(dropout_p), _seed() if seed is None else int(seed))
+    return _FlashAttnQKVFn.apply(qkv, heads, causal, float(dropout_p), _seed() if seed is None else int(seed),
+                                 _backward_will_run(qkv))
+
+
+def _backward_will_run(*ts) -> bool:
+    """Whether the forward must keep the dropout keep bits (T²/8 bytes per
+    head) for a backward: grad mode on and some input requires grad."""
+    return torch.is_grad_enabled() and any(t.requires_grad for t in ts)
 
 
 def dropout_p_effective(p: float) -> float:

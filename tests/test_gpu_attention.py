@@ -99,3 +99,21 @@ def test_stored_keep_bits_match_oracle(cuda, case):
         want = want & torch.ones(T, T, dtype=torch.bool, device=cuda).tril()
     assert torch.equal(got, want), int((got != want).sum())
 
+
+
+def test_no_grad_forward_skips_keep_bits(cuda):
+    """Without a backward to follow (no_grad) the forward stores no keep bits;
+    its output is the same as with them."""
+    from distributed_compute_pytorch_amd._ext import C as _C
+    from distributed_compute_pytorch_amd.ops.attention import flash_attn
+
+    B, H, T = 2, 2, 256
+    C = H * 64
+    g = torch.Generator().manual_seed(10)
+    q, k, v = (torch.randn(B, T, C, generator=g).to(cuda).to(torch.bfloat16) for _ in range(3))
+    with torch.no_grad():
+        o1 = flash_attn(q, k, v, H, True, 0.1, 77)
+        _, _, keep = _C.flash_attn_fwd(q, k, v, H, True, 0.1, 77, False)
+    assert keep.numel() == 0
+    o2 = flash_attn(q.clone().requires_grad_(True), k, v, H, True, 0.1, 77)
+    assert torch.equal(o1, o2.detach())
