@@ -61,18 +61,47 @@ def _time_ms(fn, iters: int = 5) -> float:
     return s.elapsed_time(e) / iters
 
 
+# interleave the candidates call by call (False: the round-5 groups of 5
+# back-to-back calls per candidate, kept for A/B: DCP_AUTOTUNE_GROUPED=1)
+_INTERLEAVE = os.environ.get("DCP_AUTOTUNE_GROUPED", "0") != "1"
+
+
 def _measure(cands: dict, rounds: int = 3) -> dict:
-    """Best-of-``rounds`` per-call time of each candidate, the candidates
-    interleaved (a single back-to-back pair flipped choices between runs on
-    close shapes). A candidate's failure propagates: shapes a kernel cannot
-    take are left out of ``cands`` up front (``_fwd_cands`` / ``_pp_ok``)."""
+    """Per-call time of each candidate (ms). Candidates alternate CALL BY
+    CALL, in a rotating order, each call timed by its own event pair; the
+    result is the median over ``4 * rounds`` calls. Inside a training step
+    the chip's clock swings with power: the same 0.7 ms kernel measured
+    588-900 µs over consecutive calls with nothing else running (rocprofv3
+    trace, profiles/r6_autotune_clock_trace.txt), so groups of back-to-back
+    calls per candidate timed whichever candidate landed in a dip as slower
+    (the LM-head weight gradient: ours 770 µs in the autotune, 600-640 µs in
+    the steady step). Alternating calls see the same clock. A candidate's
+    failure propagates: shapes a kernel cannot take are left out of
+    ``cands`` up front (``_fwd_cands`` / ``_pp_ok``)."""
     for fn in cands.values():  # warm (first-launch setup) before timing
         fn()
-    ts = {k: [] for k in cands}
-    for _ in range(rounds):
-        for k, fn in cands.items():
-            ts[k].append(_time_ms(fn))
-    return {k: min(v) for k, v in ts.items()}
+    if not _INTERLEAVE:
+        ts = {k: [] for k in cands}
+        for _ in range(rounds):
+            for k, fn in cands.items():
+                ts[k].append(_time_ms(fn))
+        return {k: min(v) for k, v in ts.items()}
+    names = list(cands)
+    ev = {k: [] for k in names}
+    for i in range(4 * rounds):
+        for j in range(len(names)):
+            k = names[(i + j) % len(names)]
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            cands[k]()
+            e.record()
+            ev[k].append((s, e))
+    torch.cuda.synchronize()
+    out = {}
+    for k, pairs in ev.items():
+        t = sorted(s.elapsed_time(e) for s, e in pairs)
+        out[k] = t[len(t) // 2]
+    return out
 
 
 def autotune_choices() -> dict:
