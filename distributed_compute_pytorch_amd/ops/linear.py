@@ -64,6 +64,22 @@ def _time_ms(fn, iters: int = 5) -> float:
 # interleave the candidates call by call (False: the round-5 groups of 5
 # back-to-back calls per candidate, kept for A/B: DCP_AUTOTUNE_GROUPED=1)
 _INTERLEAVE = os.environ.get("DCP_AUTOTUNE_GROUPED", "0") != "1"
+# µs of a one-wave spin kernel before each timed call (0: none); A/B knob
+_SPIN_US = float(os.environ.get("DCP_AUTOTUNE_SPIN_US", "0"))
+_SPIN_RATE: list = []  # spin cycles per µs, measured once
+
+
+def _spin_cycles() -> int:
+    if _SPIN_US <= 0:
+        return 0
+    if not _SPIN_RATE:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        torch.cuda._sleep(2_000_000)
+        e.record()
+        e.synchronize()
+        _SPIN_RATE.append(2_000_000 / max(s.elapsed_time(e) * 1e3, 1.0))
+    return int(_SPIN_US * _SPIN_RATE[0])
 
 
 def _measure(cands: dict, rounds: int = 3) -> dict:
@@ -88,9 +104,12 @@ def _measure(cands: dict, rounds: int = 3) -> dict:
         return {k: min(v) for k, v in ts.items()}
     names = list(cands)
     ev = {k: [] for k in names}
+    spin = _spin_cycles()
     for i in range(4 * rounds):
         for j in range(len(names)):
             k = names[(i + j) % len(names)]
+            if spin:
+                torch.cuda._sleep(spin)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             cands[k]()
