@@ -115,7 +115,9 @@ def _measure(cands: dict, rounds: int = 3) -> dict:
             cands[k]()
             e.record()
             ev[k].append((s, e))
-    torch.cuda.synchronize()
+    # the last event on this stream, not a device-wide sync: a bucket
+    # collective on the comm stream may be in flight (first synced backward)
+    e.synchronize()
     out = {}
     for k, pairs in ev.items():
         t = sorted(s.elapsed_time(e) for s, e in pairs)

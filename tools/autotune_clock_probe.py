@@ -41,7 +41,7 @@ def run(cands, calls, spin_cycles=0):
             cands[k]()
             e.record()
             ev[k].append((s, e))
-    torch.cuda.synchronize()
+    e.synchronize()
     return {k: [s.elapsed_time(e) * 1e3 for s, e in v] for k, v in ev.items()}
 
 
