@@ -111,6 +111,7 @@ def run_rank(cfg: TrainConfig, rank: int, world: int, local_rank: int):
     if mnist:
         train_loader, train_sampler, test_loader = _mnist_loaders(cfg, rank, world)
     step = None
+    losslog = _LossLog(log)
     for epoch in range(start_epoch, cfg.epochs):
         model.train()
         t0 = time.time()
@@ -140,8 +141,9 @@ def run_rank(cfg: TrainConfig, rank: int, world: int, local_rank: int):
                     dist.all_reduce(t, dist.ReduceOp.AVG if t.is_cuda else dist.ReduceOp.SUM)
                     if not t.is_cuda:
                         t /= world
-                    log.log(event="train", epoch=epoch, step=b, steps=nsteps, loss=round(t.item(), 6),
-                            lr=opt.param_groups[0]["lr"])
+                    losslog.push(t, epoch=epoch, step=b, steps=nsteps, lr=opt.param_groups[0]["lr"])
+                losslog.poll()
+        losslog.poll(wait=True)
         if prof is not None:
             prof.stop()
             path = (cfg.metrics_file or "dcp") + f".trace.rank{rank}.json"
@@ -166,6 +168,40 @@ def run_rank(cfg: TrainConfig, rank: int, world: int, local_rank: int):
     if cfg.save_model:
         save_model(model, cfg.save_model)
     dist.destroy_process_group()
+
+
+class _LossLog:
+    """The logged training loss without a host stall. The reference reads
+    ``loss.item()`` right after its all-reduce (``main.py:65-68``), which
+    drains the GPU queue at every logged step. Here the averaged loss is
+    copied into pinned host memory behind an event on the step's stream (so
+    a replayed graph's static output is read before the next replay) and the
+    record is written once the event has completed: polled every step,
+    flushed at the end of the epoch, in step order."""
+
+    def __init__(self, log):
+        self.log = log
+        self.q = []
+
+    def push(self, t: torch.Tensor, **fields):
+        if not t.is_cuda:
+            self._write(t.item(), fields)
+            return
+        h = torch.empty((), dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.q.append((h, ev, fields))
+
+    def poll(self, wait: bool = False):
+        while self.q and (wait or self.q[0][1].query()):
+            h, ev, fields = self.q.pop(0)
+            ev.synchronize()
+            self._write(h.item(), fields)
+
+    def _write(self, v: float, f: dict):
+        self.log.log(event="train", epoch=f["epoch"], step=f["step"], steps=f["steps"], loss=round(v, 6),
+                     lr=f["lr"])
 
 
 class _Null:

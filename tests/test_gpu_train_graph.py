@@ -40,6 +40,8 @@ def test_train_hip_graph_matches_eager(tmp_path, cuda):
     le = [e["loss"] for e in tr_e]
     lg = [e["loss"] for e in tr_g]
     assert len(le) == len(lg) == 12
+    # the loss records are written when their copies land (train._LossLog), in step order
+    assert [(e["epoch"], e["step"]) for e in tr_g] == [(ep, st) for ep in range(2) for st in range(6)]
     assert all(torch.isfinite(torch.tensor(lg)))
     # the LR schedule stepped (0.7x) and the second epoch ran on a re-captured graph
     assert abs(tr_g[-1]["lr"] - 1e-3 * 0.7) < 1e-12
