@@ -83,6 +83,26 @@ __device__ __forceinline__ uint32_t pp_pack(float a, float b) {
 }
 __device__ __forceinline__ int pp_swz(int r) { return (r >> 1) & 7; }
 
+constexpr float kLog2e = 1.4426950408889634f;
+// all-reduce over each aligned group of 8 lanes with DPP (VALU lane moves, no
+// LDS round trip as __shfl_xor's ds_bpermute): quad_perm [1,0,3,2] (xor 1),
+// [2,3,0,1] (xor 2), then row_half_mirror (lane i <-> 7 - i of the 8) joins
+// the two quads
+template <int CTRL>
+__device__ __forceinline__ float pp_dpp(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float max8_dpp(float x) {
+  x = fmaxf(x, pp_dpp<0xB1>(x));
+  x = fmaxf(x, pp_dpp<0x4E>(x));
+  return fmaxf(x, pp_dpp<0x141>(x));
+}
+__device__ __forceinline__ float sum8_dpp(float x) {
+  x += pp_dpp<0xB1>(x);
+  x += pp_dpp<0x4E>(x);
+  return x + pp_dpp<0x141>(x);
+}
+
 __device__ __forceinline__ void pp_glds(const uint16_t* src, char* lds_dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
@@ -405,30 +425,36 @@ __global__ void __launch_bounds__(kPT, 1)
       // rows (half * 8 + it) * 8 + lane / 8: the 8 lanes of a row hold its 64
       // columns of this wave; (max, Σexp) per lane, merged over those lanes
       float2* part = reinterpret_cast<float2*>(ws) + static_cast<int64_t>((v % tiles_n) * 4 + wc) * M;
+      // FULL: all 64 columns of this wave are vocabulary (every tile but the
+      // last column tile): no per-element pad test
+      auto partials = [&](auto full_t) {
+        constexpr bool FULL = decltype(full_t)::value;
 #pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const uint32_t v4[4] = {val[it].x, val[it].y, val[it].z, val[it].w};
-        float x[8];
+        for (int it = 0; it < 8; ++it) {
+          const uint32_t v4[4] = {val[it].x, val[it].y, val[it].z, val[it].w};
+          float x[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          x[2 * k] = cb + 2 * k < kchunk ? pp_lo(v4[k]) : -INFINITY;
-          x[2 * k + 1] = cb + 2 * k + 1 < kchunk ? pp_hi(v4[k]) : -INFINITY;
+          for (int k = 0; k < 4; ++k) {
+            x[2 * k] = FULL || cb + 2 * k < kchunk ? pp_lo(v4[k]) : -INFINITY;
+            x[2 * k + 1] = FULL || cb + 2 * k + 1 < kchunk ? pp_hi(v4[k]) : -INFINITY;
+          }
+          float mx = fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7])));
+          mx = max8_dpp(mx);
+          float sm = 0.f;
+          if (FULL || mx != -INFINITY) {
+            const float nb = -mx * kLog2e;  // exp(x - mx) = 2^(x·log2e - mx·log2e): one FMA + v_exp
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sm += __builtin_amdgcn_exp2f(fmaf(x[k], kLog2e, nb));  // pad: 2^-inf = 0
+          }
+          sm = sum8_dpp(sm);
+          const int64_t m = rbase + (half * 8 + it) * 8 + (lane >> 3);
+          if ((lane & 7) == 0 && m < M) part[m] = make_float2(mx, sm);
         }
-        float mx = x[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) mx = fmaxf(mx, x[k]);
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        float sm = 0.f;
-        if (mx != -INFINITY) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) sm += __expf(x[k] - mx);  // exp(-inf) = 0 for the pad columns
-        }
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) sm += __shfl_xor(sm, o, 64);
-        const int64_t m = rbase + (half * 8 + it) * 8 + (lane >> 3);
-        if ((lane & 7) == 0 && m < M) part[m] = make_float2(mx, sm);
-      }
+      };
+      if (n0 + wc * 64 + 64 <= kchunk)
+        partials(std::true_type{});
+      else
+        partials(std::false_type{});
     }
 #pragma unroll
     for (int it = 0; it < 8; ++it) {

@@ -91,6 +91,10 @@ _FILE_FLAGS = {
     # 33 of the forward's ~500 VALU instructions per key block, in a
     # VALU-bound loop); nothing in the file depends on NaN semantics
     "kernels/attention.hip": ["-fno-honor-nans"],
+    # the LM-head GEMM's softmax-partials epilogue (EPI 7): 9 quieting v_max
+    # per row of 8 logits per lane otherwise (the bf16 unpacks and DPP moves
+    # are not known canonical); the file tests ±inf, never NaN
+    "kernels/gemm_pp.hip": ["-fno-honor-nans"],
 }
 
 

@@ -45,7 +45,10 @@ _DEFAULT_OURS = "pp"
 # MLP blocks as one node with the GELU backward in the second GEMM's epilogue
 # (False: two FusedLinear nodes + the GELU-backward kernel; bench.py --linear-path ours-unfused-mlp)
 _FUSED_MLP = True
-_CANDIDATES = ("pp", "ring", "hipblaslt")
+# every name a _pick candidate dict can hold ("pp_xent": the LM head GEMM with
+# the loss partials in its epilogue, ops/lm_head.py) — rank agreement and
+# pinned tables accept only these
+_CANDIDATES = ("pp", "ring", "hipblaslt", "pp_xent")
 
 
 _TIMES: dict = {}  # key -> {candidate: ms} of the autotune measurement

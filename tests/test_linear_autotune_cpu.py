@@ -117,3 +117,16 @@ def test_pretune_table_adopted_from_rank0():
     from mp_util import run_world
 
     run_world(_pretune_world, 2)
+
+
+def test_pp_xent_choice_pins_and_roundtrips(monkeypatch, tmp_path):
+    """The LM head's fused GEMM + loss partials ("pp_xent") is a valid choice
+    for pinned tables (and so for the rank-0 table every rank adopts)."""
+    monkeypatch.setattr(lin, "_CHOICE", {})
+    path = tmp_path / "pin.json"
+    path.write_text(json.dumps({"head_xent 8192 768 50304": "pp_xent"}))
+    lin.load_choices(str(path))
+    assert lin._CHOICE == {("head_xent", 8192, 768, 50304): "pp_xent"}
+    log = []
+    cands = {n: (lambda n=n: log.append(n)) for n in ("pp_xent", "pp", "hipblaslt")}
+    assert lin._pick(("head_xent", 8192, 768, 50304), cands) == "pp_xent" and log == []
