@@ -231,6 +231,20 @@ __device__ __forceinline__ int64_t mask_word(int bh, int nblk, int kblk, int hh,
   return ((static_cast<int64_t>(bh) * nblk + kblk) * 2 + hh) * T + q;
 }
 
+// combine x with the lane 32 apart (lane ^ 32): gfx950's v_permlane32_swap
+// (a VALU lane exchange) instead of __shfl_xor's ds_bpermute round trip
+// through LDS on the softmax's critical path. With both operands x, the two
+// results hold x and its partner in some order in every lane; max / + are
+// symmetric, so every lane gets the same combined value
+__device__ __forceinline__ float max_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // (batch-head, tile) of this workgroup. Causal: tiles carry unequal work
 // (query tile t of the forward / dQ sees t + 1 key tiles; key tile t of dK/dV
 // is seen by nt - t query tiles). Workgroups are dispatched breadth-first, so
@@ -345,7 +359,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(s[kh][r], s[kh][r + 1]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mx = max_xor32(mx);
     // (every wave's first block holds key 0 ≤ its queries: mx is finite from there on)
     const float alpha = __builtin_amdgcn_exp2f((m - mx) * c);
     const float nmc = -mx * c;
@@ -359,7 +373,7 @@ __global__ void __launch_bounds__(kT) attn_fwd_kernel(AttnParams P, AttnTensor q
         if (!DROP) rs += s[kh][r];
       }
     if (!DROP) {
-      rs += __shfl_xor(rs, 32);
+      rs = sum_xor32(rs);
       l = l * alpha + rs;
     }
     m = mx;
@@ -469,7 +483,7 @@ __global__ void __launch_bounds__(kT) attn_bwd_dq_kernel(AttnParams P, AttnTenso
       dpart = fmaf(__uint_as_float(aw[e] & 0xffff0000u), __uint_as_float(gw[e] & 0xffff0000u), dpart);
     }
   }
-  const float dlt = dpart + __shfl_xor(dpart, 32, 64);  // 0 for rows past T (gf zeroed)
+  const float dlt = sum_xor32(dpart);  // 0 for rows past T (gf zeroed)
   if (qok && hh == 0) delta[static_cast<int64_t>(bh) * T + qi] = dlt;
   const float c = P.scale * kLog2e;
   const float inv_keep = drop_scale(drop_thr(P.p_drop));
