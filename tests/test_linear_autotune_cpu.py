@@ -74,9 +74,10 @@ def test_near_ties_go_to_our_kernels(monkeypatch):
     times = {}
     monkeypatch.setattr(lin, "_measure", lambda cands: dict(times))
     monkeypatch.setattr(lin.torch.cuda, "is_current_stream_capturing", lambda: False)  # no GPU here
-    times.update(pp=1.01, ring=1.2, hipblaslt=1.0)  # within 2 %: ours
+    assert lin._OURS_TIE == 0.12  # the default band (sustained-load bias, NOTES §33)
+    times.update(pp=1.10, ring=1.2, hipblaslt=1.0)  # within 12 %: ours
     assert lin._pick(("fwd", 1, 2, 3), _cands([])) == "pp"
-    times.update(pp=1.05, ring=1.04, hipblaslt=1.0)  # 4 % slower: hipBLASLt
+    times.update(pp=1.15, ring=1.14, hipblaslt=1.0)  # 14 % slower: hipBLASLt
     assert lin._pick(("fwd", 1, 2, 4), _cands([])) == "hipblaslt"
     times.update(pp=0.9, ring=1.2, hipblaslt=1.0)
     assert lin._pick(("fwd", 1, 2, 5), _cands([])) == "pp"
